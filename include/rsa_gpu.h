@@ -1,0 +1,188 @@
+/*
+ * rsa_gpu.h -- C-ABI boundary of the MI355X seed-and-extend path.
+ *
+ * This library (rabbitsalign_amd/lib/librsa_gpu.so, HIP/gfx950) replaces the
+ * reference's hot path behind plain C entry points (no torch types, plain
+ * pointers and sizes, int status returns, no exceptions across the boundary):
+ *
+ *   rsa_open / rsa_close  <- per-thread GASAL2 state set up lazily inside
+ *                            solve_ssw_on_gpu (src/gasal2_ssw.cpp:29-102) and
+ *                            the host-resident StrobemerIndex (src/index.hpp:37-183)
+ *   rsa_randstrobes       <- randstrobes_query        (src/randstrobes.hpp:62, .cpp:207-253)
+ *   rsa_seed              <- randstrobes_query + find_nams + find_nams_rescue as called by
+ *                            align_{PE,SE}_read_part  (src/nam.hpp:40-49, src/aln.cpp:1946-1962)
+ *   rsa_extend            <- solve_ssw_on_gpu         (src/gasal2_ssw.h:46-47) followed by the
+ *                            gasal_fail / Aligner::align fallback (src/pc.cpp:1779-1788); the
+ *                            result is exactly Aligner::align's AlignmentInfo
+ *                            (src/aligner.cpp:114-210, src/aligner.hpp:20-30)
+ *
+ * Threading: every entry point is thread-safe on one context; concurrent calls
+ * run on distinct HIP streams of the context (one stream "lane" per call).
+ * Ownership: the caller owns every input and output buffer.  Results are
+ * deterministic and independent of batch composition and job order.
+ * Errors: a negative return value; rsa_last_error() describes it.  A missing
+ * GPU or a failed HIP call is an error -- there is no CPU fallback.
+ */
+#ifndef RSA_GPU_H
+#define RSA_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSA_OK 0
+#define RSA_ERR_HIP (-1)
+#define RSA_ERR_ARG (-2)
+#define RSA_ERR_CAPACITY (-3)   /* an output buffer is too small; *_needed fields say how much */
+#define RSA_ERR_NOMEM (-4)
+
+/* RefRandstrobe exactly as stored in a .sti file (src/randstrobes.hpp:20-49) */
+typedef struct rsa_ref_randstrobe {
+    uint64_t hash;
+    uint32_t position;
+    uint32_t packed;          /* ref_index << 8 | (strobe2 - strobe1) */
+} rsa_ref_randstrobe;
+
+/* Index + reference as loaded from <ref>.r<N>.sti and the FASTA
+ * (src/index.cpp:91-132, IndexParameters src/indexparameters.hpp:73-104). */
+typedef struct rsa_index_view {
+    const rsa_ref_randstrobe* randstrobes;
+    uint64_t n_randstrobes;
+    const uint64_t* bucket_starts;     /* [2^bits + 1] */
+    int32_t bits;
+    int32_t filter_cutoff;
+    int32_t k, s, t_syncmer;           /* SyncmerParameters */
+    int32_t w_min, w_max, max_dist;    /* RandstrobeParameters */
+    uint64_t q;
+    const char* ref_seq;               /* contigs concatenated, uppercase (refs.cpp:8-16) */
+    const uint64_t* contig_offsets;    /* [n_contigs + 1] */
+    int32_t n_contigs;
+} rsa_index_view;
+
+typedef struct rsa_ctx rsa_ctx;
+
+/* Upload index + reference to `device` (replicated per GPU). NULL on error. */
+rsa_ctx* rsa_open(int device, const rsa_index_view* view, char* err, size_t err_len);
+void rsa_close(rsa_ctx* ctx);
+const char* rsa_last_error(rsa_ctx* ctx);
+/* bytes of HBM the context holds resident (index + reference) */
+uint64_t rsa_resident_bytes(const rsa_ctx* ctx);
+
+/* ---- seeding ------------------------------------------------------------ */
+
+typedef struct rsa_read_batch {
+    const char* seq;          /* read bases, concatenated */
+    const uint64_t* offsets;  /* [n_reads] start of read i in seq */
+    const uint32_t* lengths;  /* [n_reads] */
+    uint32_t n_reads;
+} rsa_read_batch;
+
+/* QueryRandstrobe (src/randstrobes.hpp:51-56) */
+typedef struct rsa_query_randstrobe {
+    uint64_t hash;
+    uint32_t start;
+    uint32_t end;
+    uint32_t is_reverse;
+    uint32_t pad_;
+} rsa_query_randstrobe;
+
+typedef struct rsa_randstrobe_batch {
+    rsa_query_randstrobe* out;   /* caller-owned */
+    uint64_t capacity;
+    uint64_t* offsets;           /* [n_reads + 1] */
+    uint64_t needed;             /* out: total count */
+} rsa_randstrobe_batch;
+
+int rsa_randstrobes(rsa_ctx* ctx, const rsa_read_batch* reads, rsa_randstrobe_batch* out);
+
+/* Nam (src/nam.hpp:11-38), field order preserved, bool widened to int32 */
+typedef struct rsa_nam {
+    int32_t nam_id;
+    int32_t query_start, query_end, query_prev_hit_startpos;
+    int32_t ref_start, ref_end, ref_prev_hit_startpos;
+    int32_t n_hits;
+    int32_t ref_id;
+    float score;
+    int32_t is_rc;
+} rsa_nam;
+
+typedef struct rsa_nam_batch {
+    rsa_nam* nams;               /* caller-owned, NAMs of read i at [offsets[i], offsets[i+1]) */
+    uint64_t capacity;
+    uint64_t* offsets;           /* [n_reads + 1] */
+    float* nonrepetitive_fraction; /* [n_reads], bit-equal to find_nams' .first */
+    uint8_t* rescued;            /* [n_reads], 1 if find_nams_rescue produced the list */
+    uint64_t needed;             /* out: total NAM count */
+} rsa_nam_batch;
+
+/* For every read: NAMs = find_nams(randstrobes_query(read)); if rescue_level > 1
+ * and (NAMs empty or nonrepetitive_fraction < 0.7) then NAMs =
+ * find_nams_rescue(..., rescue_cutoff)  (src/aln.cpp:1946-1962).  NAMs come in
+ * the reference's exact pre-sort order (robin_hood slot order per orientation). */
+int rsa_seed(rsa_ctx* ctx, const rsa_read_batch* reads, int32_t rescue_level, uint32_t rescue_cutoff,
+             rsa_nam_batch* out);
+
+/* ---- extension ---------------------------------------------------------- */
+
+/* One Smith-Waterman job: query bytes (caller buffer) vs a window of the
+ * device-resident reference (contig ref_id, [ref_start, ref_start+ref_len)). */
+typedef struct rsa_job {
+    uint64_t query_offset;
+    uint32_t query_len;
+    int32_t ref_id;
+    uint32_t ref_start;
+    uint32_t ref_len;
+} rsa_job;
+
+typedef struct rsa_job_batch {
+    const char* queries;       /* host buffer holding all query bytes */
+    uint64_t queries_len;
+    const rsa_job* jobs;
+    uint32_t n_jobs;
+    int32_t match, mismatch, gap_open, gap_extend, end_bonus;   /* -A -B -O -E -L */
+} rsa_job_batch;
+
+/* AlignmentInfo (src/aligner.hpp:20-30); CIGAR ops len<<4|op (src/cigar.hpp:11-21) */
+typedef struct rsa_aln {
+    int32_t sw_score;
+    uint32_t edit_distance;
+    uint32_t ref_start, ref_end;       /* half-open, relative to the job window */
+    uint32_t query_start, query_end;   /* half-open */
+    uint64_t cigar_offset;             /* into cigar_pool */
+    uint32_t cigar_len;
+    uint32_t pad_;
+} rsa_aln;
+
+typedef struct rsa_aln_batch {
+    rsa_aln* alns;             /* [n_jobs] */
+    uint32_t* cigar_pool;
+    uint64_t cigar_capacity;
+    uint64_t cigar_used;       /* out */
+} rsa_aln_batch;
+
+/* Aligner::align for every job.  ref_len > 2000 gives the reference's
+ * sentinel (sw_score -1000000), a failed SSW the -100000 sentinel. */
+int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jobs, rsa_aln_batch* out);
+
+/* upper bound of cigar_pool entries needed for a batch */
+uint64_t rsa_extend_cigar_bound(const rsa_job_batch* jobs);
+
+/* ---- instrumentation ------------------------------------------------------ */
+
+typedef struct rsa_kernel_stats {
+    double seed_ms, lookup_ms, nam_ms, ext_scan_ms, ext_band_ms;  /* cumulative HIP-event time */
+    uint64_t seed_calls, ext_calls;
+    uint64_t reads, query_randstrobes, lookups_found, hits, nams;     /* device counters */
+    uint64_t jobs, dp_cells;
+} rsa_kernel_stats;
+
+int rsa_get_stats(rsa_ctx* ctx, rsa_kernel_stats* out);
+void rsa_reset_stats(rsa_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

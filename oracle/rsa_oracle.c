@@ -934,14 +934,17 @@ void ora_aligner_align(const char* query, int qlen, const char* ref, int rlen, i
     cig c = {conv, 0};
     int mism = 0;
     if (s.read_begin1 > 0) cig_push_raw(&c, to_cigar_int((uint32_t)s.read_begin1, 'S'));
-    const int8_t* rp = tr + s.ref_begin1;
+    /* ref_begin1 is -1 only when nothing scored (score1 == 0): the reference
+     * then reads translated_ref[-1] (UB); we read it as an N, like banded_sw */
+    int rpos = s.ref_begin1;
     const int8_t* qp = tq + s.read_begin1;
     int in_m = 0, in_x = 0; uint32_t len_m = 0, len_x = 0;
     for (int i = 0; i < s.n_cigar; ++i) {
         uint32_t op = raw[i] & 0xf, len = raw[i] >> 4;
         if (op == 0) {
             for (uint32_t j = 0; j < len; ++j) {
-                if (*rp != *qp) {
+                int8_t rc = (rpos >= 0 && rpos < rlen) ? tr[rpos] : 4;
+                if (rc != *qp) {
                     ++mism;
                     if (in_m) cig_push_raw(&c, to_cigar_int(len_m, '='));
                     len_m = 0; ++len_x; in_m = 0; in_x = 1;
@@ -949,10 +952,10 @@ void ora_aligner_align(const char* query, int qlen, const char* ref, int rlen, i
                     if (in_x) cig_push_raw(&c, to_cigar_int(len_x, 'X'));
                     ++len_m; len_x = 0; in_m = 1; in_x = 0;
                 }
-                ++rp; ++qp;
+                ++rpos; ++qp;
             }
         } else if (op == 1 || op == 2) {
-            if (op == 1) qp += len; else rp += len;
+            if (op == 1) qp += len; else rpos += (int)len;
             mism += (int)len;
             if (in_m) cig_push_raw(&c, to_cigar_int(len_m, '='));
             else if (in_x) cig_push_raw(&c, to_cigar_int(len_x, 'X'));

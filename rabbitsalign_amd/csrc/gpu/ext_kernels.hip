@@ -1,0 +1,464 @@
+// ext_kernels.hip -- SSW-exact batched extension for gfx950.
+//
+// Replaces GASAL2's one-thread-per-alignment local kernel + get_tb
+// (GASAL2/src/kernels/local_kernel_template.h:71-519, get_tb.h:4-149) and the
+// CPU re-run through Aligner::align (src/aligner.cpp:114-210).  Results are
+// bit-identical to the reference CPU path (ext/ssw/ssw.c + ssw_cpp.cpp):
+//
+//  k_ext_scan  one 64-lane wavefront per job.  The query is split over the
+//              lanes (R consecutive rows per lane) and the reference streams
+//              through them as an anti-diagonal systolic array: at step s lane l
+//              owns column s-l; the row-above values (F, within-stripe F, H)
+//              move one lane per step with a DPP wave_shr:1.  Both SSW passes
+//              run here: forward (score1, ref_end1, read_end1) and the reverse
+//              pass that stops at the first column reaching score1.  The SSW
+//              striping artefact (cross-stripe F never feeds E, ssw.c:275-289)
+//              is reproduced with the byte (16 stripes) / word (8 stripes)
+//              layout of the reference.  Query/reference codes sit in LDS.
+//  k_ext_band  one lane per job: banded_sw (ssw.c:590-774) restated literally
+//              (its array-index quirks are observable), traceback, =/X CIGAR
+//              (ssw_cpp.cpp:126-210) and the end-bonus extension
+//              (aligner.cpp:147-207).
+//
+// Integer DP, no MFMA.  Roofline: VALU-bound (cells/s), see DESIGN.md.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <climits>
+
+#include "rsa_dev.h"
+#include "rsa_ext.h"
+
+#define SCAN_WAVES 4
+#define MAXQ_LDS 1024
+#define MAXR_LDS 2048
+
+__device__ __forceinline__ int subst(int a, int b, int match, int mismatch) {
+    return (a == b && a < 4) ? match : -mismatch;
+}
+
+struct PassOut {
+    int best, col, row;      // forward: max, first col, min row; reverse: see below
+    int tcol, trow;          // reverse: first column reaching terminate
+};
+
+// One SSW pass over `ncol` reference columns with `nrow` query rows.
+// fwd: row p -> qc[p], column c -> rc[c]
+// rev: row p -> qc[qend - p], column c -> rc[rend - c]
+template <int R, bool REV>
+__device__ PassOut sw_pass(const uint8_t* __restrict__ qc, int nrow, const uint8_t* __restrict__ rc, int ncol,
+                           int qend, int rend, int match, int mismatch, int gO, int gE, int seg,
+                           int terminate, int lane) {
+    const int lanes_used = (nrow + R - 1) / R;
+    int E[R], Hc[R], qv[R];
+    bool ss[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        E[r] = 0;
+        Hc[r] = 0;
+        const int p = lane * R + r;
+        ss[r] = (p % seg) == 0;
+        qv[r] = p < nrow ? (int)qc[REV ? (qend - p) : p] : 7;  // padded rows never score a match
+    }
+    int F_out = 0, Fw_out = 0, H_last = 0, diag_top = 0;
+    int best = 0, bcol = INT_MAX, brow = INT_MAX;
+    int tcol = INT_MAX, trow = INT_MAX;
+    const int steps = ncol + lanes_used - 1;
+    for (int s = 0; s < steps; ++s) {
+        const int F_in = wave_shr1(F_out);
+        const int Fw_in = wave_shr1(Fw_out);
+        const int Hl_in = wave_shr1(H_last);
+        const int c = s - lane;
+        if (lane < lanes_used && c >= 0 && c < ncol) {
+            const int rcode = rc[REV ? (rend - c) : c];
+            int dg = diag_top, F = F_in, Fw = Fw_in;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (ss[r]) Fw = 0;
+                int hm = max(dg + subst(qv[r], rcode, match, mismatch), 0);
+                hm = max(hm, E[r]);
+                hm = max(hm, Fw);
+                const int h = max(hm, F);
+                dg = Hc[r];
+                Hc[r] = h;
+                const int ho = max(hm - gO, 0);
+                E[r] = max(E[r] - gE, ho);
+                Fw = max(Fw - gE, ho);
+                F = max(F - gE, max(h - gO, 0));
+                const int p = lane * R + r;
+                if (p < nrow) {
+                    if (!REV) {
+                        if (h > best) { best = h; bcol = c; brow = p; }
+                    } else {
+                        if (h > best) best = h;
+                        if (h == terminate && tcol == INT_MAX) { tcol = c; trow = p; }
+                    }
+                }
+            }
+            F_out = F;
+            Fw_out = Fw;
+            H_last = Hc[R - 1];
+        }
+        diag_top = Hl_in;
+        if (REV && (s & 7) == 7) {
+            const int m = wave_min_i32(tcol);
+            if (m != INT_MAX && s >= m + lanes_used - 1) break;
+        }
+    }
+    PassOut o;
+    o.best = best; o.col = bcol; o.row = brow; o.tcol = tcol; o.trow = trow;
+    return o;
+}
+
+template <bool REV>
+__device__ PassOut sw_pass_dispatch(const uint8_t* qc, int nrow, const uint8_t* rc, int ncol, int qend, int rend,
+                                    int match, int mismatch, int gO, int gE, int seg, int terminate, int lane) {
+    const int R = (nrow + 63) / 64;
+#define RSA_PASS(N) return sw_pass<N, REV>(qc, nrow, rc, ncol, qend, rend, match, mismatch, gO, gE, seg, terminate, lane)
+    switch (R) {
+        case 0: case 1: RSA_PASS(1);
+        case 2: RSA_PASS(2);
+        case 3: RSA_PASS(3);
+        case 4: RSA_PASS(4);
+        case 5: RSA_PASS(5);
+        case 6: RSA_PASS(6);
+        case 7: RSA_PASS(7);
+        case 8: RSA_PASS(8);
+        case 9: case 10: case 11: case 12: RSA_PASS(12);
+        default: RSA_PASS(16);
+    }
+#undef RSA_PASS
+}
+
+__global__ void __launch_bounds__(64 * SCAN_WAVES)
+k_ext_scan(const ExtJobDev* __restrict__ jobs, int n_jobs, const char* __restrict__ qbuf,
+           const char* __restrict__ ref, ScanRes* __restrict__ out, int match, int mismatch, int gO, int gE) {
+    __shared__ uint8_t s_q[SCAN_WAVES][MAXQ_LDS];
+    __shared__ uint8_t s_r[SCAN_WAVES][MAXR_LDS];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int j = blockIdx.x * SCAN_WAVES + wave;
+    // every wave reaches the barrier; invalid / sentinel jobs skip the work after it
+    const bool in_range = j < n_jobs;
+    ExtJobDev jb;
+    jb.q_off = 0; jb.r_off = 0; jb.qlen = 0; jb.rlen = 0; jb.cig_off = 0;
+    if (in_range) jb = jobs[j];
+    const bool sentinel = in_range && (jb.rlen > 2000 || jb.qlen == 0 || jb.qlen > MAXQ_LDS);
+    const bool work = in_range && !sentinel;
+    ScanRes res;
+    res.score1 = 0; res.ref_end1 = -1; res.read_end1 = 0; res.ref_begin1 = -1; res.read_begin1 = 0;
+    res.flag = 0; res.word = 0; res.status = 0;
+    const int qlen = (int)jb.qlen, rlen = (int)jb.rlen;
+    uint8_t* qc = s_q[wave];
+    uint8_t* rc = s_r[wave];
+    if (work) {
+        for (int i = lane; i < qlen; i += 64) qc[i] = (uint8_t)ssw_code((unsigned char)qbuf[jb.q_off + i]);
+        for (int i = lane; i < rlen; i += 64) rc[i] = (uint8_t)ssw_code((unsigned char)ref[jb.r_off + i]);
+    }
+    __syncthreads();
+    if (!work) {
+        if (sentinel && lane == 0) { res.status = jb.qlen > MAXQ_LDS ? 2 : 1; out[j] = res; }
+        return;
+    }
+
+    // forward pass, byte layout first (sw_sse2_byte), word layout on overflow (ssw.c:838-850)
+    int word = 0;
+    PassOut f = sw_pass_dispatch<false>(qc, qlen, rc, rlen, 0, 0, match, mismatch, gO, gE, (qlen + 15) / 16, 0, lane);
+    int score1 = wave_max_i32(f.best);
+    if (score1 + mismatch >= 255) {
+        word = 1;
+        f = sw_pass_dispatch<false>(qc, qlen, rc, rlen, 0, 0, match, mismatch, gO, gE, (qlen + 7) / 8, 0, lane);
+        score1 = wave_max_i32(f.best);
+    }
+    int ref_end1, read_end1;
+    if (score1 == 0) {
+        ref_end1 = word ? 0 : -1;
+        read_end1 = 0;
+    } else {
+        ref_end1 = wave_min_i32(f.best == score1 ? f.col : INT_MAX);
+        read_end1 = wave_min_i32((f.best == score1 && f.col == ref_end1) ? f.row : INT_MAX);
+    }
+    res.score1 = score1; res.ref_end1 = ref_end1; res.read_end1 = read_end1; res.word = word;
+
+    if (score1 > 0) {
+        // reverse pass (ssw.c:877-893)
+        const int nrow = read_end1 + 1, ncol = ref_end1 + 1;
+        const int seg = word ? (nrow + 7) / 8 : (nrow + 15) / 16;
+        PassOut b = sw_pass_dispatch<true>(qc, nrow, rc, ncol, read_end1, ref_end1, match, mismatch, gO, gE, seg,
+                                           score1, lane);
+        const int tcol = wave_min_i32(b.tcol);
+        if (tcol == INT_MAX) {
+            res.flag = 2;   // reverse max < score1: "may miss a small part"
+            res.ref_begin1 = 0;
+            res.read_begin1 = 0;
+        } else {
+            const int trow = wave_min_i32(b.tcol == tcol ? b.trow : INT_MAX);
+            res.ref_begin1 = ref_end1 - tcol;
+            res.read_begin1 = read_end1 - trow;
+        }
+    } else {
+        res.ref_begin1 = word ? 0 : -1;
+        res.read_begin1 = 0;
+    }
+    if (lane == 0) out[j] = res;
+}
+
+// ---------------------------------------------------------------------------
+// banded_sw + traceback + CIGAR post-processing, one lane per job
+// ---------------------------------------------------------------------------
+#define SET_U(w, i, j) ((j) - max((i) - (w), 0) + 1)
+#define SET_D(w, i, j, p) (((j) - max((i) - (w), 0)) * 3 + (p))
+
+__device__ __forceinline__ uint32_t cig(uint32_t len, uint32_t op) { return (len << 4) | op; }
+
+struct BandScratch {
+    int* hb; int* eb; int* hc;   // arr_cap ints each
+    int8_t* dir;                 // dir_cap bytes
+    int arr_cap;
+    int64_t dir_cap;
+};
+
+// Returns #ops written to `out` (reversed order fixed), -1 traceback error, -2 scratch overflow.
+__device__ int banded_sw_dev(const char* __restrict__ refw, int ref_begin, int rlen_total, const char* __restrict__ qry,
+                             int ref_len, int read_len, int score, int gO, int gE, int band_width, int match,
+                             int mismatch, BandScratch sc, uint32_t* out) {
+    const int len = ref_len > read_len ? ref_len : read_len;
+    int s1 = 8;
+    int64_t s2 = 1024;
+    if (s1 > sc.arr_cap || s2 > sc.dir_cap) return -2;
+    for (int z = 0; z < s1; ++z) sc.hb[z] = sc.eb[z] = sc.hc[z] = 0;
+    for (int64_t z = 0; z < s2; ++z) sc.dir[z] = 0;
+    int* h_b = sc.hb; int* e_b = sc.eb; int* h_c = sc.hc;
+    int8_t* direction = sc.dir;
+    int8_t* direction_line = direction;
+    int max_v = 0, width, width_d;
+    do {
+        width = band_width * 2 + 3;
+        width_d = band_width * 2 + 1;
+        while (width >= s1) {
+            int ns = s1 + 1;
+            ns--; ns |= ns >> 1; ns |= ns >> 2; ns |= ns >> 4; ns |= ns >> 8; ns |= ns >> 16; ns++;
+            if (ns > sc.arr_cap) return -2;
+            for (int z = s1; z < ns; ++z) h_b[z] = e_b[z] = h_c[z] = 0;
+            s1 = ns;
+        }
+        while ((int64_t)width_d * read_len * 3 >= s2) {
+            int64_t ns = s2 + 1;
+            ns--; ns |= ns >> 1; ns |= ns >> 2; ns |= ns >> 4; ns |= ns >> 8; ns |= ns >> 16; ns |= ns >> 32; ns++;
+            if (ns > sc.dir_cap) return -2;
+            for (int64_t z = s2; z < ns; ++z) direction[z] = 0;
+            s2 = ns;
+        }
+        direction_line = direction;
+        for (int j = 1; j < width - 1; j++) h_b[j] = 0;
+        for (int i = 0; i < read_len; i++) {
+            int beg = max(0, i - band_width), end = min(ref_len - 1, i + band_width), u = 0;
+            const int edge = end + 1 < width - 1 ? end + 1 : width - 1;
+            int f = 0;
+            h_b[0] = e_b[0] = h_b[edge] = e_b[edge] = h_c[0] = 0;
+            direction_line = direction + (int64_t)width_d * i * 3;
+            const int rcode_i = ssw_code((unsigned char)qry[i]);
+            for (int j = beg; j <= end; j++) {
+                u = SET_U(band_width, i, j);
+                const int e = SET_U(band_width, i - 1, j);
+                const int b = SET_U(band_width, i, j - 1);
+                const int d = SET_U(band_width, i - 1, j - 1);
+                const int de = SET_D(band_width, i, j, 0), df = SET_D(band_width, i, j, 1), dh = SET_D(band_width, i, j, 2);
+                int temp1 = i == 0 ? -gO : h_b[e] - gO;
+                int temp2 = i == 0 ? -gE : e_b[e] - gE;
+                e_b[u] = temp1 > temp2 ? temp1 : temp2;
+                direction_line[de] = temp1 > temp2 ? 3 : 2;
+                temp1 = h_c[b] - gO;
+                temp2 = f - gE;
+                f = temp1 > temp2 ? temp1 : temp2;
+                direction_line[df] = temp1 > temp2 ? 5 : 4;
+                const int e1 = e_b[u] > 0 ? e_b[u] : 0;
+                const int f1 = f > 0 ? f : 0;
+                temp1 = e1 > f1 ? e1 : f1;
+                const int gj = ref_begin + j;
+                const int rcj = (gj >= 0 && gj < rlen_total) ? ssw_code((unsigned char)refw[gj]) : 4;
+                temp2 = h_b[d] + subst(rcj, rcode_i, match, mismatch);
+                h_c[u] = temp1 > temp2 ? temp1 : temp2;
+                if (h_c[u] > max_v) max_v = h_c[u];
+                if (temp1 <= temp2) direction_line[dh] = 1;
+                else direction_line[dh] = e1 > f1 ? direction_line[de] : direction_line[df];
+            }
+            for (int j = 1; j <= u; j++) h_b[j] = h_c[j];
+        }
+        band_width *= 2;
+    } while (max_v < score && band_width <= len);
+    band_width /= 2;
+
+    int i = read_len - 1, j = ref_len - 1, e = 0, l = 0, temp2 = 2;
+    uint32_t op = 0, prev_op = 0;   // 0 = M, 1 = I, 2 = D (SSW encoded_ops)
+    while (i >= 0 && j > 0) {
+        const int temp1 = SET_D(band_width, i, j, temp2);
+        const int64_t at = (direction_line - direction) + temp1;
+        if (at < 0 || at >= s2) return -1;
+        switch (direction_line[temp1]) {
+            case 1: --i; --j; temp2 = 2; direction_line -= width_d * 3; op = 0; break;
+            case 2: --i; temp2 = 0; direction_line -= width_d * 3; op = 1; break;
+            case 3: --i; temp2 = 2; direction_line -= width_d * 3; op = 1; break;
+            case 4: --j; temp2 = 1; op = 2; break;
+            case 5: --j; temp2 = 2; op = 2; break;
+            default: return -1;
+        }
+        if (op == prev_op) ++e;
+        else { ++l; out[l - 1] = cig((uint32_t)e, prev_op); prev_op = op; e = 1; }
+    }
+    if (op == 0) { ++l; out[l - 1] = cig((uint32_t)e + 1, op); }
+    else { l += 2; out[l - 2] = cig((uint32_t)e, op); out[l - 1] = cig(1, 0); }
+    for (int s = 0, t = l - 1; s < t; ++s, --t) { const uint32_t x = out[s]; out[s] = out[t]; out[t] = x; }
+    return l;
+}
+
+// Cigar::push merge rule (src/cigar.hpp:52-59)
+__device__ __forceinline__ void cpush(uint32_t* c, int& n, uint32_t op, uint32_t len) {
+    if (n == 0 || (c[n - 1] & 0xf) != op) c[n++] = (len << 4) | op;
+    else c[n - 1] += len << 4;
+}
+
+__global__ void __launch_bounds__(64)
+k_ext_band(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan, int n_jobs,
+           const int* __restrict__ idx_list, int job_base,
+           const char* __restrict__ qbuf, const char* __restrict__ ref, uint32_t* __restrict__ cig_pool,
+           rsa_aln* __restrict__ out, uint8_t* __restrict__ scratch, int64_t scr_stride, int arr_cap,
+           int64_t dir_cap, int match, int mismatch, int gO, int gE, int bonus, int* __restrict__ overflow) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_jobs) return;
+    const int j = idx_list ? idx_list[t] : job_base + t;
+    const ExtJobDev jb = jobs[j];
+    const ScanRes sr = scan[j];
+    rsa_aln a;
+    a.sw_score = 0; a.edit_distance = 0; a.ref_start = a.ref_end = a.query_start = a.query_end = 0;
+    a.cigar_offset = jb.cig_off; a.cigar_len = 0; a.pad_ = 0;
+    if (sr.status == 1) {                       // ref > 2000 (aligner.cpp:119-125)
+        a.edit_distance = 100000; a.sw_score = -1000000;
+        out[j] = a;
+        return;
+    }
+    const char* q = qbuf + jb.q_off;
+    const char* r = ref + jb.r_off;
+    const int qlen = (int)jb.qlen, rlen = (int)jb.rlen;
+    uint32_t* c = cig_pool + jb.cig_off;
+    if (sr.flag != 0) {                         // aligner.cpp:131-136
+        a.edit_distance = 100000; a.sw_score = -100000;
+        out[j] = a;
+        return;
+    }
+    // banded_sw over ref[ref_begin1..ref_end1] x read[read_begin1..read_end1] (ssw.c:899-918)
+    const int ref_l = sr.ref_end1 - sr.ref_begin1 + 1;
+    const int read_l = sr.read_end1 - sr.read_begin1 + 1;
+    const int bw = abs(ref_l - read_l) + 1;
+    uint8_t* my = scratch + (int64_t)t * scr_stride;
+    BandScratch bs;
+    bs.hb = (int*)my; bs.eb = bs.hb + arr_cap; bs.hc = bs.eb + arr_cap;
+    bs.dir = (int8_t*)(bs.hc + arr_cap);
+    bs.arr_cap = arr_cap; bs.dir_cap = dir_cap;
+    // raw banded ops live in the job's scratch, the final CIGAR is built in its slot
+    uint32_t* raw = (uint32_t*)(bs.dir + dir_cap);
+    const int nraw = banded_sw_dev(r, sr.ref_begin1, rlen, q + sr.read_begin1, ref_l, read_l, sr.score1, gO, gE, bw,
+                                   match, mismatch, bs, raw);
+    if (nraw == -2) { overflow[j] = idx_list ? 2 : 1; return; }
+    if (nraw < 0) {                             // banded_sw failed -> flag 1
+        a.edit_distance = 100000; a.sw_score = -100000;
+        out[j] = a;
+        return;
+    }
+    // ConvertAlignment + CalculateNumberMismatch (ssw_cpp.cpp:54-90, 126-210).
+    // Core ops are built after a gap of qs+2 entries (room for the left end-bonus ops).
+    const int qs0 = sr.read_begin1;
+    int base = qs0 + 2;
+    int n = 0;
+    uint32_t* core = c + base;
+    int mism = 0;
+    if (qs0 > 0) core[n++] = cig((uint32_t)qs0, 4);
+    int rp = sr.ref_begin1, qp = qs0;
+    int in_m = 0, in_x = 0;
+    uint32_t len_m = 0, len_x = 0;
+    for (int k = 0; k < nraw; ++k) {
+        const uint32_t opk = raw[k] & 0xf, lenk = raw[k] >> 4;
+        if (opk == 0) {
+            for (uint32_t z = 0; z < lenk; ++z) {
+                const int rcode = (rp >= 0 && rp < rlen) ? ssw_code((unsigned char)r[rp]) : 4;
+                const int qcode = ssw_code((unsigned char)q[qp]);
+                if (rcode != qcode) {
+                    ++mism;
+                    if (in_m) core[n++] = cig(len_m, 7);
+                    len_m = 0; ++len_x; in_m = 0; in_x = 1;
+                } else {
+                    if (in_x) core[n++] = cig(len_x, 8);
+                    ++len_m; len_x = 0; in_m = 1; in_x = 0;
+                }
+                ++rp; ++qp;
+            }
+        } else if (opk == 1 || opk == 2) {
+            const uint32_t rawk = raw[k];
+            if (opk == 1) qp += (int)lenk; else rp += (int)lenk;
+            mism += (int)lenk;
+            if (in_m) core[n++] = cig(len_m, 7);
+            else if (in_x) core[n++] = cig(len_x, 8);
+            in_m = in_x = 0; len_m = len_x = 0;
+            core[n++] = rawk;
+        }
+    }
+    if (in_m) core[n++] = cig(len_m, 7);
+    else if (in_x) core[n++] = cig(len_x, 8);
+    const int tail = qlen - sr.read_end1 - 1;
+    if (tail > 0) core[n++] = cig((uint32_t)tail, 4);
+
+    // Aligner::align end bonus (aligner.cpp:138-207)
+    uint32_t ed = (uint32_t)mism;
+    int sw = sr.score1;
+    uint32_t rs = (uint32_t)sr.ref_begin1, re = (uint32_t)sr.ref_end1 + 1;
+    uint32_t qs = (uint32_t)qs0, qe = (uint32_t)sr.read_end1 + 1;
+    int final_n;
+    {
+        uint32_t q0 = qs, r0 = rs;
+        int score = sw;
+        uint32_t edits = ed;
+        while (q0 > 0 && r0 > 0) {
+            q0--; r0--;
+            if (q[q0] == r[r0]) score += match;
+            else { score -= mismatch; edits++; }
+        }
+        if (q0 == 0 && score + bonus > sw) {
+            if (qs > 0) {
+                // front ops in left-to-right order, then core without its leading S
+                int fn = 0;
+                for (uint32_t z = 0; z < qs; ++z) {
+                    const uint32_t qq = z, rr = rs - qs + z;
+                    cpush(c, fn, q[qq] == r[rr] ? 7u : 8u, 1);
+                }
+                for (int k = 1; k < n; ++k) cpush(c, fn, core[k] & 0xf, core[k] >> 4);
+                final_n = fn;
+            } else {
+                for (int k = 0; k < n; ++k) c[k] = core[k];
+                final_n = n;
+            }
+            qs = 0; rs = r0; sw = score + bonus; ed = edits;
+        } else {
+            for (int k = 0; k < n; ++k) c[k] = core[k];
+            final_n = n;
+        }
+    }
+    {
+        uint32_t q1 = qe, r1 = re;
+        int score = sw;
+        uint32_t edits = ed;
+        while (q1 < (uint32_t)qlen && r1 < (uint32_t)rlen) {
+            if (q[q1] == r[r1]) score += match;
+            else { score -= mismatch; edits++; }
+            q1++; r1++;
+        }
+        if (q1 == (uint32_t)qlen && score + bonus > sw) {
+            if (qe < (uint32_t)qlen) {
+                final_n--;   // drop trailing soft clip
+                for (uint32_t z = 0; z < (uint32_t)qlen - qe; ++z)
+                    cpush(c, final_n, q[qe + z] == r[re + z] ? 7u : 8u, 1);
+            }
+            qe = (uint32_t)qlen; re = r1; sw = score + bonus; ed = edits;
+        }
+    }
+    a.sw_score = sw; a.edit_distance = ed; a.ref_start = rs; a.ref_end = re; a.query_start = qs; a.query_end = qe;
+    a.cigar_len = (uint32_t)final_n;
+    out[j] = a;
+}

@@ -1,0 +1,353 @@
+// rsa_ctx.hip -- the C-ABI (include/rsa_gpu.h) on top of the gfx950 kernels.
+//
+// One context per GPU holds the index (RefRandstrobe AoS + bucket table) and
+// the reference bytes resident in HBM.  Calls are served by "lanes": each lane
+// owns a HIP stream and its growable device/pinned buffers, so concurrent host
+// threads (the worker pool of the host pipeline) overlap H2D, kernels and D2H.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "rsa_ext.h"
+#include "rsa_seed.h"
+
+__global__ void k_ext_scan(const ExtJobDev* jobs, int n_jobs, const char* qbuf, const char* ref, ScanRes* out,
+                           int match, int mismatch, int gO, int gE);
+__global__ void k_ext_band(const ExtJobDev* jobs, const ScanRes* scan, int n_jobs, const int* idx_list, int job_base,
+                           const char* qbuf, const char* ref, uint32_t* cig_pool, rsa_aln* out, uint8_t* scratch,
+                           int64_t scr_stride, int arr_cap, int64_t dir_cap, int match, int mismatch, int gO,
+                           int gE, int bonus, int* overflow);
+
+#define HIPCHK(x)                                                                   \
+    do {                                                                            \
+        hipError_t e_ = (x);                                                        \
+        if (e_ != hipSuccess) {                                                     \
+            set_err(ctx, std::string(#x) + ": " + hipGetErrorString(e_));           \
+            return RSA_ERR_HIP;                                                     \
+        }                                                                           \
+    } while (0)
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        size_t n = std::max(bytes, cap + cap / 2);
+        hipError_t e = hipMalloc(&p, n);
+        if (e != hipSuccess) { p = nullptr; cap = 0; return e; }
+        cap = n;
+        return hipSuccess;
+    }
+    template <class T> T* as() const { return (T*)p; }
+    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+};
+
+struct HostBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        size_t n = std::max(bytes, cap + cap / 2);
+        hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
+        if (e != hipSuccess) { p = nullptr; cap = 0; return e; }
+        cap = n;
+        return hipSuccess;
+    }
+    template <class T> T* as() const { return (T*)p; }
+    void release() { if (p) (void)hipHostFree(p); p = nullptr; cap = 0; }
+};
+
+struct Lane {
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[8];
+    bool busy = false;
+    // extension
+    DevBuf d_q, d_jobs, d_scan, d_alns, d_cig, d_scratch, d_over, d_idx;
+    HostBuf h_q, h_jobs, h_over;
+    // seeding
+    SeedBufs sb;
+};
+
+}  // namespace
+
+struct rsa_ctx {
+    int device = 0;
+    std::string err;
+    std::mutex err_m;
+    // resident data
+    char* d_ref = nullptr;
+    uint64_t ref_bytes = 0;
+    std::vector<uint64_t> contig_off;  // host copy [n+1]
+    rsa_ref_randstrobe* d_rs = nullptr;
+    uint64_t n_rs = 0;
+    uint64_t* d_starts = nullptr;
+    SeedIndexParams ip{};
+    uint64_t resident = 0;
+    // lanes
+    std::vector<Lane*> lanes;
+    std::mutex lane_m;
+    std::condition_variable lane_cv;
+    // stats
+    std::mutex stat_m;
+    rsa_kernel_stats stats{};
+};
+
+static void set_err(rsa_ctx* ctx, const std::string& s) {
+    if (!ctx) return;
+    std::lock_guard<std::mutex> g(ctx->err_m);
+    ctx->err = s;
+}
+
+static Lane* acquire_lane(rsa_ctx* ctx) {
+    std::unique_lock<std::mutex> g(ctx->lane_m);
+    for (;;) {
+        for (Lane* l : ctx->lanes)
+            if (!l->busy) { l->busy = true; return l; }
+        if (ctx->lanes.size() < 16) {
+            Lane* l = new Lane();
+            if (hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking) != hipSuccess) { delete l; return nullptr; }
+            for (auto& e : l->ev) (void)hipEventCreate(&e);
+            l->busy = true;
+            ctx->lanes.push_back(l);
+            return l;
+        }
+        ctx->lane_cv.wait(g);
+    }
+}
+
+static void release_lane(rsa_ctx* ctx, Lane* l) {
+    {
+        std::lock_guard<std::mutex> g(ctx->lane_m);
+        l->busy = false;
+    }
+    ctx->lane_cv.notify_one();
+}
+
+struct LaneGuard {
+    rsa_ctx* ctx; Lane* l;
+    ~LaneGuard() { if (l) release_lane(ctx, l); }
+};
+
+extern "C" {
+
+rsa_ctx* rsa_open(int device, const rsa_index_view* v, char* errbuf, size_t err_len) {
+    auto fail = [&](const std::string& s) -> rsa_ctx* {
+        if (errbuf && err_len) { snprintf(errbuf, err_len, "%s", s.c_str()); }
+        return nullptr;
+    };
+    if (!v) return fail("rsa_open: null index view");
+    int n_dev = 0;
+    if (hipGetDeviceCount(&n_dev) != hipSuccess || n_dev == 0) return fail("rsa_open: no HIP device visible");
+    if (device < 0 || device >= n_dev) return fail("rsa_open: bad device ordinal");
+    if (hipSetDevice(device) != hipSuccess) return fail("rsa_open: hipSetDevice failed");
+    rsa_ctx* ctx = new rsa_ctx();
+    ctx->device = device;
+    ctx->contig_off.assign(v->contig_offsets, v->contig_offsets + v->n_contigs + 1);
+    ctx->ref_bytes = ctx->contig_off.back();
+    ctx->n_rs = v->n_randstrobes;
+    const size_t n_starts = ((size_t)1 << v->bits) + 1;
+    hipError_t e = hipMalloc(&ctx->d_ref, ctx->ref_bytes + 64);
+    if (e == hipSuccess) e = hipMemcpy(ctx->d_ref, v->ref_seq, ctx->ref_bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess && v->randstrobes && ctx->n_rs) {
+        e = hipMalloc(&ctx->d_rs, sizeof(rsa_ref_randstrobe) * (ctx->n_rs + 1));
+        if (e == hipSuccess) e = hipMemcpy(ctx->d_rs, v->randstrobes, sizeof(rsa_ref_randstrobe) * ctx->n_rs, hipMemcpyHostToDevice);
+    }
+    if (e == hipSuccess && v->bucket_starts) {
+        e = hipMalloc(&ctx->d_starts, sizeof(uint64_t) * n_starts);
+        if (e == hipSuccess) e = hipMemcpy(ctx->d_starts, v->bucket_starts, sizeof(uint64_t) * n_starts, hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess) {
+        std::string s = std::string("rsa_open upload: ") + hipGetErrorString(e);
+        rsa_close(ctx);
+        return fail(s);
+    }
+    ctx->ip.rs = ctx->d_rs;
+    ctx->ip.starts = ctx->d_starts;
+    ctx->ip.n = ctx->n_rs;
+    ctx->ip.bits = v->bits;
+    ctx->ip.filter_cutoff = (uint32_t)v->filter_cutoff;
+    ctx->ip.k = v->k; ctx->ip.s = v->s; ctx->ip.t = v->t_syncmer;
+    ctx->ip.w_min = v->w_min; ctx->ip.w_max = v->w_max; ctx->ip.max_dist = v->max_dist;
+    ctx->ip.q = v->q;
+    ctx->resident = ctx->ref_bytes + sizeof(rsa_ref_randstrobe) * ctx->n_rs + sizeof(uint64_t) * n_starts;
+    return ctx;
+}
+
+void rsa_close(rsa_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    for (Lane* l : ctx->lanes) {
+        if (l->stream) (void)hipStreamSynchronize(l->stream);
+        l->d_q.release(); l->d_jobs.release(); l->d_scan.release(); l->d_alns.release(); l->d_cig.release();
+        l->d_scratch.release(); l->d_over.release(); l->d_idx.release();
+        l->h_q.release(); l->h_jobs.release(); l->h_over.release();
+        seed_bufs_release(l->sb);
+        for (auto& e : l->ev) (void)hipEventDestroy(e);
+        if (l->stream) (void)hipStreamDestroy(l->stream);
+        delete l;
+    }
+    if (ctx->d_ref) (void)hipFree(ctx->d_ref);
+    if (ctx->d_rs) (void)hipFree(ctx->d_rs);
+    if (ctx->d_starts) (void)hipFree(ctx->d_starts);
+    delete ctx;
+}
+
+const char* rsa_last_error(rsa_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+uint64_t rsa_resident_bytes(const rsa_ctx* ctx) { return ctx ? ctx->resident : 0; }
+
+uint64_t rsa_extend_cigar_bound(const rsa_job_batch* jb) {
+    uint64_t t = 0;
+    for (uint32_t i = 0; i < jb->n_jobs; ++i) t += (uint64_t)jb->jobs[i].query_len + jb->jobs[i].ref_len + 8;
+    return t;
+}
+
+// band kernel scratch geometry (per in-flight job)
+static const int BAND_ARR_CAP = 1024;
+static const int64_t BAND_DIR_CAP = 48 * 1024;
+static const int BAND_CHUNK = 16384;
+static const int BIG_ARR_CAP = 1 << 16;
+static const int64_t BIG_DIR_CAP = 64ll << 20;
+static const int BIG_CHUNK = 8;
+
+static int64_t band_stride(int arr_cap, int64_t dir_cap) {
+    int64_t s = (int64_t)arr_cap * 3 * 4 + dir_cap + (int64_t)RSA_RAW_CAP * 4;
+    return (s + 255) & ~(int64_t)255;
+}
+
+int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
+    if (!ctx || !jb || !out) return RSA_ERR_ARG;
+    const uint32_t n = jb->n_jobs;
+    const uint64_t bound = rsa_extend_cigar_bound(jb);
+    out->cigar_used = bound;
+    if (n == 0) return RSA_OK;
+    if (out->cigar_capacity < bound) { set_err(ctx, "rsa_extend: cigar_pool too small"); return RSA_ERR_CAPACITY; }
+    HIPCHK(hipSetDevice(ctx->device));
+    Lane* L = acquire_lane(ctx);
+    if (!L) { set_err(ctx, "rsa_extend: cannot create HIP stream"); return RSA_ERR_HIP; }
+    LaneGuard guard{ctx, L};
+    // host job descriptors
+    HIPCHK(L->h_jobs.ensure(sizeof(ExtJobDev) * n));
+    ExtJobDev* hj = L->h_jobs.as<ExtJobDev>();
+    uint64_t cig_off = 0;
+    uint64_t cells = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const rsa_job& s = jb->jobs[i];
+        if (s.ref_id < 0 || s.ref_id >= (int)ctx->contig_off.size() - 1 || s.query_offset + s.query_len > jb->queries_len) {
+            set_err(ctx, "rsa_extend: job " + std::to_string(i) + " out of range");
+            return RSA_ERR_ARG;
+        }
+        const uint64_t clen = ctx->contig_off[s.ref_id + 1] - ctx->contig_off[s.ref_id];
+        if ((uint64_t)s.ref_start + s.ref_len > clen) {
+            set_err(ctx, "rsa_extend: job " + std::to_string(i) + " window exceeds contig");
+            return RSA_ERR_ARG;
+        }
+        if (s.query_len > 1024 && s.ref_len <= 2000) {
+            set_err(ctx, "rsa_extend: query longer than 1024 bp is not supported");
+            return RSA_ERR_ARG;
+        }
+        hj[i].q_off = s.query_offset;
+        hj[i].r_off = ctx->contig_off[s.ref_id] + s.ref_start;
+        hj[i].qlen = s.query_len;
+        hj[i].rlen = s.ref_len;
+        hj[i].cig_off = cig_off;
+        cig_off += (uint64_t)s.query_len + s.ref_len + 8;
+        if (s.ref_len <= 2000) cells += (uint64_t)s.query_len * s.ref_len;
+    }
+    HIPCHK(L->d_q.ensure(jb->queries_len + 16));
+    HIPCHK(L->d_jobs.ensure(sizeof(ExtJobDev) * n));
+    HIPCHK(L->d_scan.ensure(sizeof(ScanRes) * n));
+    HIPCHK(L->d_alns.ensure(sizeof(rsa_aln) * n));
+    HIPCHK(L->d_cig.ensure(sizeof(uint32_t) * (bound + 16)));
+    HIPCHK(L->d_over.ensure(sizeof(int) * n));
+    const int64_t stride = band_stride(BAND_ARR_CAP, BAND_DIR_CAP);
+    const int chunk = (int)std::min<uint32_t>(n, BAND_CHUNK);
+    HIPCHK(L->d_scratch.ensure((size_t)stride * chunk));
+    hipStream_t st = L->stream;
+    HIPCHK(hipMemcpyAsync(L->d_q.p, jb->queries, jb->queries_len, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(L->d_jobs.p, hj, sizeof(ExtJobDev) * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(L->d_over.p, 0, sizeof(int) * n, st));
+    HIPCHK(hipEventRecord(L->ev[0], st));
+    hipLaunchKernelGGL(k_ext_scan, dim3((n + 3) / 4), dim3(256), 0, st, L->d_jobs.as<ExtJobDev>(), (int)n,
+                       L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(), jb->match, jb->mismatch,
+                       jb->gap_open, jb->gap_extend);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(L->ev[1], st));
+    for (uint32_t base = 0; base < n; base += chunk) {
+        const int cnt = (int)std::min<uint32_t>(chunk, n - base);
+        hipLaunchKernelGGL(k_ext_band, dim3((cnt + 63) / 64), dim3(64), 0, st, L->d_jobs.as<ExtJobDev>(),
+                           L->d_scan.as<ScanRes>(), cnt, (const int*)nullptr, (int)base, L->d_q.as<char>(), ctx->d_ref,
+                           L->d_cig.as<uint32_t>(), L->d_alns.as<rsa_aln>(), L->d_scratch.as<uint8_t>(), stride,
+                           BAND_ARR_CAP, BAND_DIR_CAP, jb->match, jb->mismatch, jb->gap_open, jb->gap_extend,
+                           jb->end_bonus, L->d_over.as<int>());
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(L->ev[2], st));
+    HIPCHK(L->h_over.ensure(sizeof(int) * n));
+    HIPCHK(hipMemcpyAsync(L->h_over.p, L->d_over.p, sizeof(int) * n, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    // rare: jobs whose band doubled past the per-job scratch get a large scratch
+    std::vector<int> big;
+    const int* ho = L->h_over.as<int>();
+    for (uint32_t i = 0; i < n; ++i) if (ho[i]) big.push_back((int)i);
+    if (!big.empty()) {
+        const int64_t bstride = band_stride(BIG_ARR_CAP, BIG_DIR_CAP);
+        HIPCHK(L->d_scratch.ensure((size_t)std::max<int64_t>(bstride * BIG_CHUNK, stride * chunk)));
+        HIPCHK(L->d_idx.ensure(sizeof(int) * big.size()));
+        HIPCHK(hipMemcpyAsync(L->d_idx.p, big.data(), sizeof(int) * big.size(), hipMemcpyHostToDevice, st));
+        for (size_t b = 0; b < big.size(); b += BIG_CHUNK) {
+            const int cnt = (int)std::min<size_t>(BIG_CHUNK, big.size() - b);
+            hipLaunchKernelGGL(k_ext_band, dim3(1), dim3(64), 0, st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(),
+                               cnt, L->d_idx.as<int>() + b, 0, L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(),
+                               L->d_alns.as<rsa_aln>(), L->d_scratch.as<uint8_t>(), bstride, BIG_ARR_CAP, BIG_DIR_CAP,
+                               jb->match, jb->mismatch, jb->gap_open, jb->gap_extend, jb->end_bonus,
+                               L->d_over.as<int>());
+            HIPCHK(hipGetLastError());
+        }
+        HIPCHK(hipMemcpyAsync(L->h_over.p, L->d_over.p, sizeof(int) * n, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        for (int i : big)
+            if (L->h_over.as<int>()[i] > 1) { set_err(ctx, "rsa_extend: band scratch exhausted"); return RSA_ERR_NOMEM; }
+    }
+    HIPCHK(hipMemcpyAsync(out->alns, L->d_alns.p, sizeof(rsa_aln) * n, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(out->cigar_pool, L->d_cig.p, sizeof(uint32_t) * bound, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    float t_scan = 0, t_band = 0;
+    (void)hipEventElapsedTime(&t_scan, L->ev[0], L->ev[1]);
+    (void)hipEventElapsedTime(&t_band, L->ev[1], L->ev[2]);
+    {
+        std::lock_guard<std::mutex> g(ctx->stat_m);
+        ctx->stats.ext_scan_ms += t_scan;
+        ctx->stats.ext_band_ms += t_band;
+        ctx->stats.ext_calls++;
+        ctx->stats.jobs += n;
+        ctx->stats.dp_cells += cells;
+    }
+    return RSA_OK;
+}
+
+int rsa_get_stats(rsa_ctx* ctx, rsa_kernel_stats* out) {
+    if (!ctx || !out) return RSA_ERR_ARG;
+    std::lock_guard<std::mutex> g(ctx->stat_m);
+    *out = ctx->stats;
+    return RSA_OK;
+}
+
+void rsa_reset_stats(rsa_ctx* ctx) {
+    if (!ctx) return;
+    std::lock_guard<std::mutex> g(ctx->stat_m);
+    ctx->stats = rsa_kernel_stats{};
+}
+
+}  // extern "C"
