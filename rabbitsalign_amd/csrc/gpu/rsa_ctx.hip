@@ -25,6 +25,12 @@ __global__ void k_ext_band(const ExtJobDev* jobs, const ScanRes* scan, int n_job
                            int64_t scr_stride, int arr_cap, int64_t dir_cap, int match, int mismatch, int gO,
                            int gE, int bonus, int* overflow);
 
+int seed_run(SeedBufs& b, hipStream_t st, hipEvent_t* ev, const SeedIndexParams& p, const rsa_read_batch* rb,
+             int32_t rescue_level, uint32_t rescue_cutoff, rsa_nam_batch* out, std::string& err, float* ms,
+             uint64_t* counters);
+int seed_randstrobes_run(SeedBufs& b, hipStream_t st, const SeedIndexParams& p, const rsa_read_batch* rb,
+                         rsa_randstrobe_batch* out, std::string& err);
+
 #define HIPCHK(x)                                                                   \
     do {                                                                            \
         hipError_t e_ = (x);                                                        \
@@ -334,6 +340,56 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
         ctx->stats.jobs += n;
         ctx->stats.dp_cells += cells;
     }
+    return RSA_OK;
+}
+
+static int check_reads(rsa_ctx* ctx, const rsa_read_batch* rb) {
+    if (!rb) return RSA_ERR_ARG;
+    if (rb->n_reads && (!rb->seq || !rb->offsets || !rb->lengths)) { set_err(ctx, "null read buffers"); return RSA_ERR_ARG; }
+    if (!ctx->d_rs && ctx->n_rs) { set_err(ctx, "context has no index"); return RSA_ERR_ARG; }
+    return RSA_OK;
+}
+
+int rsa_randstrobes(rsa_ctx* ctx, const rsa_read_batch* rb, rsa_randstrobe_batch* out) {
+    if (!ctx || !out) return RSA_ERR_ARG;
+    int rc = check_reads(ctx, rb);
+    if (rc) return rc;
+    if (rb->n_reads == 0) { out->needed = 0; if (out->offsets) out->offsets[0] = 0; return RSA_OK; }
+    HIPCHK(hipSetDevice(ctx->device));
+    Lane* L = acquire_lane(ctx);
+    if (!L) { set_err(ctx, "cannot create HIP stream"); return RSA_ERR_HIP; }
+    LaneGuard guard{ctx, L};
+    std::string err;
+    rc = seed_randstrobes_run(L->sb, L->stream, ctx->ip, rb, out, err);
+    if (rc) set_err(ctx, err);
+    return rc;
+}
+
+int rsa_seed(rsa_ctx* ctx, const rsa_read_batch* rb, int32_t rescue_level, uint32_t rescue_cutoff, rsa_nam_batch* out) {
+    if (!ctx || !out) return RSA_ERR_ARG;
+    int rc = check_reads(ctx, rb);
+    if (rc) return rc;
+    if (rb->n_reads == 0) { out->needed = 0; if (out->offsets) out->offsets[0] = 0; return RSA_OK; }
+    if (!ctx->d_rs || !ctx->d_starts) { set_err(ctx, "rsa_seed: context opened without an index"); return RSA_ERR_ARG; }
+    HIPCHK(hipSetDevice(ctx->device));
+    Lane* L = acquire_lane(ctx);
+    if (!L) { set_err(ctx, "cannot create HIP stream"); return RSA_ERR_HIP; }
+    LaneGuard guard{ctx, L};
+    std::string err;
+    float ms[3] = {0, 0, 0};
+    uint64_t cnt[5] = {0, 0, 0, 0, 0};
+    rc = seed_run(L->sb, L->stream, L->ev, ctx->ip, rb, rescue_level, rescue_cutoff, out, err, ms, cnt);
+    if (rc) { set_err(ctx, err); return rc; }
+    std::lock_guard<std::mutex> g(ctx->stat_m);
+    ctx->stats.seed_ms += ms[0];
+    ctx->stats.lookup_ms += ms[1];
+    ctx->stats.nam_ms += ms[2];
+    ctx->stats.seed_calls++;
+    ctx->stats.reads += cnt[0];
+    ctx->stats.query_randstrobes += cnt[1];
+    ctx->stats.lookups_found += cnt[2];
+    ctx->stats.hits += cnt[3];
+    ctx->stats.nams += cnt[4];
     return RSA_OK;
 }
 

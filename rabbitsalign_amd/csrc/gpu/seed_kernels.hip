@@ -1,7 +1,975 @@
+// seed_kernels.hip -- randstrobe seeding + find_nams / find_nams_rescue on gfx950.
+//
+// Replaces the per-read CPU loop of align_{PE,SE}_read_part
+// (src/aln.cpp:1946-1962): randstrobes_query (src/randstrobes.cpp:207-253),
+// find_nams (src/nam.cpp:771-926), find_nams_rescue (src/nam.cpp:955-1012).
+// Output is the reference's exact pre-sort NAM vector (robin_hood iteration
+// order emulated, ext/robin_hood.h v3.11.1).
+//
+//  k_randstrobes  one lane per read: canonical syncmers (stateful window-min
+//                 with the reference's tie rules) and fwd/rc randstrobes.
+//  k_lookup       one wavefront per read, one lane per query randstrobe:
+//                 bucket bounds + binary search in the 16-B RefRandstrobe AoS,
+//                 the filter probe, the occurrence count and the min_diff hit
+//                 count.  These random 16-B reads are the HBM-bound part.
+//  k_find_nams    one lane per read: hits into per-read robin_hood emulations,
+//                 merge_hits_into_nams (sort=true) fwd then rc.
+//  k_rescue       one lane per flagged read: find_nams_rescue (pre_sort
+//                 branch) with merge_hits_into_nams_fast.
+//  k_compact      gathers the final per-read NAM lists.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "rsa_dev.h"
 #include "rsa_seed.h"
+
+#define END64 0xFFFFFFFFFFFFFFFFULL
+
+struct QrsInfo {            // per query randstrobe, filled by k_lookup
+    uint64_t pos;           // first index with equal hash, END64 if absent
+    uint32_t count;         // occurrences of the hash
+    uint32_t hits;          // entries passing the min_diff filter (count <= 1000), else 0
+    uint32_t flags;         // bit0 found, bit1 filtered
+    uint32_t pad;
+};
+
+struct ReadStat {
+    uint32_t found, good, hits_find, hits_all;
+};
+
+struct HitD {
+    int32_t qs, qe, rs, re;
+    int32_t list;           // map value (list id) ; orientation in bit 30
+    int32_t pad;
+};
+
+// ---------------------------------------------------------------------------
+// k_randstrobes
+// ---------------------------------------------------------------------------
+struct SyncD { uint64_t hash; uint32_t pos; uint32_t pad; };
+
+__device__ void rs_get(const SyncD* sm, int n, int i, const SeedIndexParams& p, uint64_t& h, uint32_t& a,
+                       uint32_t& b) {
+    const int w_end = i + p.w_max < n - 1 ? i + p.w_max : n - 1;
+    const uint64_t max_position = (uint64_t)sm[i].pos + (unsigned)p.max_dist;
+    uint64_t min_val = END64;
+    int best = i;
+    const uint64_t hi = sm[i].hash;
+    for (int j = i + p.w_min; j <= w_end && sm[j].pos <= max_position; ++j) {
+        const uint64_t res = (uint64_t)__popcll((hi ^ sm[j].hash) & p.q);
+        if (res < min_val) { min_val = res; best = j; }
+    }
+    h = hi + sm[best].hash;
+    a = sm[i].pos;
+    b = sm[best].pos;
+}
+
+__global__ void __launch_bounds__(64)
+k_randstrobes(const char* __restrict__ seq, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
+              const uint64_t* __restrict__ qbase, int n_reads, SeedIndexParams p, SyncD* __restrict__ sync,
+              rsa_query_randstrobe* __restrict__ qrs, uint32_t* __restrict__ qcnt) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_reads) return;
+    const int len = (int)rlen[r];
+    const char* s = seq + roff[r];
+    SyncD* sm = sync + qbase[r] / 2;
+    rsa_query_randstrobe* out = qrs + qbase[r];
+    if (len < p.w_max) { qcnt[r] = 0; return; }     // randstrobes.cpp:209
+    // SyncmerIterator::next (randstrobes.cpp:57-118)
+    const int k = p.k, sl = p.s, t = p.t;
+    const uint64_t kmask = (k == 32) ? ~0ULL : ((1ULL << (2 * k)) - 1);
+    const uint64_t smask = (1ULL << (2 * sl)) - 1;
+    const int kshift = (k - 1) * 2, sshift = (sl - 1) * 2;
+    const int W = k - sl + 1;
+    uint64_t ring[32];
+    int qn = 0, qhead = 0;
+    uint64_t min_val = END64;
+    long long min_pos = -1;
+    int l = 0, n = 0;
+    uint64_t xk0 = 0, xk1 = 0, xs0 = 0, xs1 = 0;
+    for (int i = 0; i < len; ++i) {
+        const int c = nt4_code((unsigned char)s[i]);
+        if (c < 4) {
+            xk0 = ((xk0 << 2) | (uint64_t)c) & kmask;
+            xk1 = (xk1 >> 2) | ((uint64_t)(3 - c) << kshift);
+            xs0 = ((xs0 << 2) | (uint64_t)c) & smask;
+            xs1 = (xs1 >> 2) | ((uint64_t)(3 - c) << sshift);
+            if (++l < sl) continue;
+            const uint64_t hs = xxh64_u64(xs0 < xs1 ? xs0 : xs1);
+            ring[(qhead + qn) & 31] = hs;
+            qn++;
+            if (qn < W) continue;
+            if (qn == W) {
+                for (int j = 0; j < qn; ++j) {
+                    const uint64_t v = ring[(qhead + j) & 31];
+                    if (v < min_val) { min_val = v; min_pos = (long long)i - k + j + 1; }
+                }
+            } else {
+                qhead = (qhead + 1) & 31; qn--;
+                if (min_pos == (long long)i - k) {
+                    min_val = END64;
+                    min_pos = (long long)i - sl + 1;
+                    for (int j = qn - 1; j >= 0; --j) {
+                        const uint64_t v = ring[(qhead + j) & 31];
+                        if (v < min_val) { min_val = v; min_pos = (long long)i - k + j + 1; }
+                    }
+                } else if (hs < min_val) {
+                    min_val = hs;
+                    min_pos = (long long)i - sl + 1;
+                }
+            }
+            if (min_pos == (long long)i - k + t) {
+                sm[n].hash = xxh64_u64(xk0 < xk1 ? xk0 : xk1);
+                sm[n].pos = (uint32_t)(i - k + 1);
+                n++;
+            }
+        } else {
+            min_val = END64; min_pos = -1;
+            l = 0; xs0 = xs1 = xk0 = xk1 = 0;
+            qn = 0; qhead = 0;
+        }
+    }
+    int cnt = 0;
+    if (n > 0) {
+        for (int i = 0; i + p.w_min < n; ++i) {
+            uint64_t h; uint32_t a, b;
+            rs_get(sm, n, i, p, h, a, b);
+            out[cnt].hash = h; out[cnt].start = a; out[cnt].end = b + (uint32_t)k; out[cnt].is_reverse = 0;
+            out[cnt].pad_ = 0;
+            cnt++;
+        }
+        for (int i = 0, j = n - 1; i < j; ++i, --j) { const SyncD x = sm[i]; sm[i] = sm[j]; sm[j] = x; }
+        for (int i = 0; i < n; ++i) sm[i].pos = (uint32_t)(len - (int)sm[i].pos - k);
+        for (int i = 0; i + p.w_min < n; ++i) {
+            uint64_t h; uint32_t a, b;
+            rs_get(sm, n, i, p, h, a, b);
+            out[cnt].hash = h; out[cnt].start = a; out[cnt].end = b + (uint32_t)k; out[cnt].is_reverse = 1;
+            out[cnt].pad_ = 0;
+            cnt++;
+        }
+    }
+    qcnt[r] = (uint32_t)cnt;
+}
+
+// ---------------------------------------------------------------------------
+// k_lookup: one wavefront per read
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t lower_bound_hash(const rsa_ref_randstrobe* rs, uint64_t lo, uint64_t hi,
+                                                     uint64_t key) {
+    while (lo < hi) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (rs[mid].hash < key) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ uint64_t upper_bound_hash(const rsa_ref_randstrobe* rs, uint64_t lo, uint64_t hi,
+                                                     uint64_t key) {
+    while (lo < hi) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (rs[mid].hash <= key) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(256)
+k_lookup(const rsa_query_randstrobe* __restrict__ qrs, const uint32_t* __restrict__ qcnt,
+         const uint64_t* __restrict__ qbase, int n_reads, SeedIndexParams p, QrsInfo* __restrict__ qi,
+         ReadStat* __restrict__ st) {
+    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (wave >= n_reads) return;
+    const int r = wave;
+    const int nq = (int)qcnt[r];
+    const uint64_t base = qbase[r];
+    uint32_t found = 0, good = 0, hfind = 0, hall = 0;
+    for (int i = lane; i < nq; i += 64) {
+        const rsa_query_randstrobe q = qrs[base + i];
+        QrsInfo o;
+        o.pos = END64; o.count = 0; o.hits = 0; o.flags = 0; o.pad = 0;
+        const uint64_t top = q.hash >> (64 - p.bits);
+        const uint64_t a = p.starts[top], b = p.starts[top + 1];
+        if (a != b) {
+            const uint64_t lo = lower_bound_hash(p.rs, a, b, q.hash);
+            if (lo < b && p.rs[lo].hash == q.hash) {
+                o.pos = lo;
+                o.flags = 1;
+                const uint64_t probe = lo + p.filter_cutoff;   // is_filtered (index.hpp:91-93)
+                const uint64_t h2 = probe < p.n ? p.rs[probe].hash : END64;
+                if (h2 == q.hash) o.flags |= 2;
+                const uint64_t ub = upper_bound_hash(p.rs, lo, b, q.hash);
+                o.count = (uint32_t)min<uint64_t>(ub - lo, 0xFFFFFFFFull);
+                if (o.count <= 1000) {
+                    // add_to_hits_per_ref min_diff filter (nam.cpp:68-85)
+                    int min_diff = INT_MAX;
+                    uint32_t h = 0;
+                    const int qspan = (int)q.end - (int)q.start;
+                    for (uint64_t e = lo; e < ub; ++e) {
+                        const rsa_ref_randstrobe x = p.rs[e];
+                        const int rspan = (int)(x.packed & 0xFF) + p.k;
+                        int d = qspan - rspan;
+                        d = d < 0 ? -d : d;
+                        if (d <= min_diff) { h++; min_diff = d; }
+                    }
+                    o.hits = h;
+                }
+                found++;
+                if (!(o.flags & 2)) { good++; hfind += o.hits; }
+                if (o.count <= 1000) hall += o.hits;
+            }
+        }
+        qi[base + i] = o;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        found += __shfl_xor(found, off, 64);
+        good += __shfl_xor(good, off, 64);
+        hfind += __shfl_xor(hfind, off, 64);
+        hall += __shfl_xor(hall, off, 64);
+    }
+    if (lane == 0) { ReadStat s; s.found = found; s.good = good; s.hits_find = hfind; s.hits_all = hall; st[r] = s; }
+}
+
+// ---------------------------------------------------------------------------
+// robin_hood::unordered_flat_map<unsigned, ...> slot-layout emulation
+// (robin_hood.h v3.11.1; same algorithm as oracle/rsa_oracle.c rh_*)
+// ---------------------------------------------------------------------------
+struct DMap {
+    uint8_t* info; uint32_t* keys; int32_t* vals;
+    uint8_t* info2; uint32_t* keys2; int32_t* vals2;
+    uint32_t cap;                          // slots per table
+    uint64_t mult;
+    uint32_t mask, num, max_allowed, nwb, info_inc, info_shift;
+    int overflow;
+};
+
+__device__ __forceinline__ uint32_t rh_calc_max(uint32_t n) { return (uint32_t)((uint64_t)n * 80 / 100); }
+__device__ __forceinline__ uint32_t rh_calc_nwb(uint32_t n) { uint32_t m = rh_calc_max(n); return n + (m < 255 ? m : 255); }
+
+__device__ bool rh_init_data(DMap& m, uint32_t max_elements) {
+    const uint32_t nwb = rh_calc_nwb(max_elements);
+    if (nwb + 16 > m.cap) { m.overflow = 1; return false; }
+    m.num = 0;
+    m.mask = max_elements - 1;
+    m.max_allowed = rh_calc_max(max_elements);
+    m.nwb = nwb;
+    for (uint32_t i = 0; i < nwb + 16; ++i) m.info[i] = 0;
+    m.info[nwb] = 1;
+    m.info_inc = 32;
+    m.info_shift = 0;
+    return true;
+}
+
+__device__ __forceinline__ void rh_key_to_idx(const DMap& m, uint32_t key, uint32_t& idx, uint32_t& info) {
+    uint64_t h = (uint64_t)key;
+    h ^= h >> 33; h *= 0xff51afd7ed558ccdULL; h ^= h >> 33;
+    h *= m.mult;
+    h ^= h >> 33;
+    info = m.info_inc + (uint32_t)((h & 31u) >> m.info_shift);
+    idx = (uint32_t)(h >> 5) & m.mask;
+}
+
+__device__ void rh_shift_up(DMap& m, uint32_t start, uint32_t ins) {
+    for (uint32_t i = start; i != ins; --i) { m.keys[i] = m.keys[i - 1]; m.vals[i] = m.vals[i - 1]; }
+    for (uint32_t i = start; i != ins; --i) {
+        m.info[i] = (uint8_t)(m.info[i - 1] + m.info_inc);
+        if ((uint32_t)m.info[i] + m.info_inc > 0xFF) m.max_allowed = 0;
+    }
+}
+
+__device__ bool rh_try_increase_info(DMap& m) {
+    if (m.info_inc <= 2) return false;
+    m.info_inc >>= 1;
+    m.info_shift++;
+    const uint32_t nwb = rh_calc_nwb(m.mask + 1);
+    for (uint32_t i = 0; i < nwb; i += 8)
+        for (uint32_t b = 0; b < 8; ++b) m.info[i + b] = (uint8_t)(m.info[i + b] >> 1);
+    m.info[nwb] = 1;
+    m.max_allowed = rh_calc_max(m.mask + 1);
+    return true;
+}
+
+__device__ void rh_insert_move(DMap& m, uint32_t key, int32_t val) {
+    if (m.max_allowed == 0 && !rh_try_increase_info(m)) { m.overflow = 2; return; }
+    uint32_t idx, info;
+    rh_key_to_idx(m, key, idx, info);
+    while (info <= m.info[idx]) { idx++; info += m.info_inc; }
+    const uint32_t ins = idx;
+    const uint8_t ins_info = (uint8_t)info;
+    if ((uint32_t)ins_info + m.info_inc > 0xFF) m.max_allowed = 0;
+    while (m.info[idx] != 0) { idx++; info += m.info_inc; }
+    if (idx != ins) rh_shift_up(m, idx, ins);
+    m.keys[ins] = key; m.vals[ins] = val;
+    m.info[ins] = ins_info;
+    m.num++;
+}
+
+__device__ void rh_rehash(DMap& m, uint32_t nb) {
+    if (!m.info2) { m.overflow = 1; return; }
+    uint8_t* oi = m.info; uint32_t* ok = m.keys; int32_t* ov = m.vals;
+    const uint32_t onwb = rh_calc_nwb(m.mask + 1);
+    m.info = m.info2; m.keys = m.keys2; m.vals = m.vals2;
+    m.info2 = oi; m.keys2 = ok; m.vals2 = ov;
+    if (!rh_init_data(m, nb)) return;
+    if (onwb > 1)
+        for (uint32_t i = 0; i < onwb; ++i)
+            if (oi[i] != 0) rh_insert_move(m, ok[i], ov[i]);
+}
+
+__device__ void rh_increase_size(DMap& m) {
+    const uint32_t maxa = rh_calc_max(m.mask + 1);
+    if (m.num < maxa && rh_try_increase_info(m)) return;
+    m.mult += 0xc4ceb9fe1a85ec54ULL;
+    if (m.num * 2 < rh_calc_max(m.mask + 1)) rh_rehash(m, m.mask + 1);
+    else rh_rehash(m, (m.mask + 1) * 2);
+}
+
+// default construction + reserve(100) (nam.cpp:913-914)
+__device__ void rh_new_reserved(DMap& m) {
+    m.mult = 0xc4ceb9fe1a85ec53ULL;
+    m.overflow = 0;
+    rh_init_data(m, 128);
+}
+
+// operator[]: returns the value of key, inserting new_val if absent
+__device__ int32_t rh_get_or_insert(DMap& m, uint32_t key, int32_t new_val, bool& inserted) {
+    inserted = false;
+    for (int attempt = 0; attempt < 256 && !m.overflow; ++attempt) {
+        uint32_t idx, info;
+        rh_key_to_idx(m, key, idx, info);
+        while (info < m.info[idx]) { idx++; info += m.info_inc; }
+        while (info == m.info[idx]) {
+            if (m.keys[idx] == key) return m.vals[idx];
+            idx++; info += m.info_inc;
+        }
+        if (m.num >= m.max_allowed) { rh_increase_size(m); continue; }
+        const uint32_t ins = idx, ins_info = info;
+        if (ins_info + m.info_inc > 0xFF) m.max_allowed = 0;
+        while (m.info[idx] != 0) { idx++; info += m.info_inc; }
+        if (idx != ins) rh_shift_up(m, idx, ins);
+        m.info[ins] = (uint8_t)ins_info;
+        m.keys[ins] = key; m.vals[ins] = new_val;
+        m.num++;
+        inserted = true;
+        return new_val;
+    }
+    m.overflow = 3;
+    return -1;
+}
+
+// per-read map scratch: 2 maps x 2 tables x cap slots x (1 + 4 + 4 bytes)
+__device__ __forceinline__ size_t map_stride(uint32_t cap) { return (size_t)cap * 9 * 4; }
+
+__device__ void map_bind(DMap& m, uint8_t* base, uint32_t cap, int which) {
+    uint8_t* b = base + (size_t)which * 2 * cap * 9;
+    m.cap = cap;
+    m.keys = (uint32_t*)b; m.vals = (int32_t*)(b + (size_t)cap * 4); m.info = b + (size_t)cap * 8;
+    uint8_t* b2 = b + (size_t)cap * 9;
+    m.keys2 = (uint32_t*)b2; m.vals2 = (int32_t*)(b2 + (size_t)cap * 4); m.info2 = b2 + (size_t)cap * 8;
+}
+
+// ---------------------------------------------------------------------------
+// NAM construction helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float nam_score(const rsa_nam& n) {   // nam.cpp:456-460
+    const int qspan = n.query_end - n.query_start, rspan = n.ref_end - n.ref_start;
+    const int mx = qspan > rspan ? qspan : rspan, mn = qspan < rspan ? qspan : rspan;
+    return (2 * mn - mx) > 0 ? (float)(n.n_hits * (2 * mn - mx)) : 1.0f;
+}
+
+__device__ __forceinline__ void nam_emit(rsa_nam* out, int& n_out, rsa_nam x) {
+    x.score = nam_score(x);
+    x.nam_id = n_out;
+    out[n_out++] = x;
+}
+
+__device__ __forceinline__ rsa_nam nam_from_hit(const HitD& h, int ref_id, int is_rc) {
+    rsa_nam n;
+    n.nam_id = 0;
+    n.query_start = h.qs; n.query_end = h.qe; n.ref_start = h.rs; n.ref_end = h.re;
+    n.query_prev_hit_startpos = h.qs; n.ref_prev_hit_startpos = h.rs;
+    n.n_hits = 1; n.ref_id = ref_id; n.score = 0.0f; n.is_rc = is_rc;
+    return n;
+}
+
+__device__ void flush_passed(rsa_nam* open, int& n_open, int query_start, rsa_nam* out, int& n_out) {
+    for (int i = 0; i < n_open; ++i)
+        if (open[i].query_end < query_start) nam_emit(out, n_out, open[i]);
+    int w = 0;
+    for (int i = 0; i < n_open; ++i)
+        if (!(open[i].query_end < query_start)) open[w++] = open[i];
+    n_open = w;
+}
+
+// add_to_hits_per_ref (nam.cpp:68-85): appends hits of one query randstrobe
+__device__ void add_hits(DMap& m, int orient, int qs, int qe, const SeedIndexParams& p, uint64_t pos, uint32_t count,
+                         HitD* hits, int& n_hits, int& n_lists) {
+    int min_diff = INT_MAX;
+    for (uint64_t e = pos; e < pos + count; ++e) {
+        const rsa_ref_randstrobe x = p.rs[e];
+        const int rs = (int)x.position;
+        const int re = rs + (int)(x.packed & 0xFF) + p.k;
+        int d = (qe - qs) - (re - rs);
+        d = d < 0 ? -d : d;
+        if (d <= min_diff) {
+            bool ins;
+            const int32_t lid = rh_get_or_insert(m, x.packed >> 8, n_lists, ins);
+            if (ins) n_lists++;
+            HitD h;
+            h.qs = qs; h.qe = qe; h.rs = rs; h.re = re; h.list = lid | (orient << 30); h.pad = 0;
+            hits[n_hits++] = h;
+            min_diff = d;
+        }
+    }
+}
+
+// merge_hits_into_nams (nam.cpp:370-536, sort=true), all lists of one orientation
+__device__ void merge_slow(const DMap& m, int orient, const HitD* hits, int n_hits, int k, rsa_nam* open,
+                           rsa_nam* out, int& n_out) {
+    for (uint32_t slot = 0; slot < m.nwb; ++slot) {
+        if (!m.info[slot]) continue;
+        const int32_t lid = m.vals[slot] | (orient << 30);
+        const int ref_id = (int)m.keys[slot];
+        int n_open = 0;
+        unsigned prev_q_start = 0;
+        for (int hi = 0; hi < n_hits; ++hi) {
+            const HitD x = hits[hi];
+            if (x.list != lid) continue;
+            bool added = false;
+            for (int o = 0; o < n_open; ++o) {
+                rsa_nam& on = open[o];
+                if (on.query_prev_hit_startpos < x.qs && x.qs <= on.query_end && on.ref_prev_hit_startpos < x.rs &&
+                    x.rs <= on.ref_end) {
+                    if (x.qe > on.query_end && x.re > on.ref_end) {
+                        on.query_end = x.qe; on.ref_end = x.re;
+                        on.query_prev_hit_startpos = x.qs; on.ref_prev_hit_startpos = x.rs;
+                        on.n_hits++; added = true; break;
+                    } else if (x.qe <= on.query_end && x.re <= on.ref_end) {
+                        on.query_prev_hit_startpos = x.qs; on.ref_prev_hit_startpos = x.rs;
+                        on.n_hits++; added = true; break;
+                    }
+                }
+            }
+            if (!added) open[n_open++] = nam_from_hit(x, ref_id, orient);
+            if ((unsigned)x.qs > prev_q_start + (unsigned)k) {
+                flush_passed(open, n_open, x.qs, out, n_out);
+                prev_q_start = (unsigned)x.qs;
+            }
+        }
+        for (int o = 0; o < n_open; ++o) nam_emit(out, n_out, open[o]);
+    }
+}
+
+// merge_hits_into_nams_fast (nam.cpp:117-366, sort=false)
+__device__ void merge_fast(const DMap& m, int orient, HitD* hits, int n_hits, int k, rsa_nam* open, uint8_t* added,
+                           HitD* grp, rsa_nam* out, int& n_out) {
+    for (uint32_t slot = 0; slot < m.nwb; ++slot) {
+        if (!m.info[slot]) continue;
+        const int32_t lid = m.vals[slot] | (orient << 30);
+        const int ref_id = (int)m.keys[slot];
+        int n_open = 0;
+        unsigned prev_q_start = 0;
+        int hi = 0;
+        // hits of this list, in insertion order, processed in query_start groups
+        while (true) {
+            while (hi < n_hits && hits[hi].list != lid) hi++;
+            if (hi >= n_hits) break;
+            const int qstart = hits[hi].qs;
+            int gn = 0;
+            for (int z = hi; z < n_hits; ++z) {
+                if (hits[z].list != lid) continue;
+                if (hits[z].qs != qstart) break;
+                grp[gn++] = hits[z];
+                hi = z + 1;
+            }
+            // sort group by (qs, rs): insertion sort on rs (qs equal)
+            for (int a = 1; a < gn; ++a) {
+                HitD x = grp[a]; int b = a - 1;
+                while (b >= 0 && x.rs < grp[b].rs) { grp[b + 1] = grp[b]; --b; }
+                grp[b + 1] = x;
+            }
+            for (int a = 0; a < gn; ++a) added[a] = 0;
+            int cnt_done = 0;
+            for (int o = 0; o < n_open; ++o) {
+                rsa_nam& on = open[o];
+                int lower = 0, upper = 0;
+                while (lower < gn && grp[lower].rs < on.ref_prev_hit_startpos + 1) lower++;
+                while (upper < gn && grp[upper].rs < on.ref_end + 1) upper++;
+                for (int z = lower; z < upper; ++z) {
+                    if (added[z]) continue;
+                    if (qstart <= on.query_end) {
+                        const HitD& x = grp[z];
+                        if (on.ref_prev_hit_startpos < x.rs && x.rs <= on.ref_end) {
+                            if (x.qe > on.query_end && x.re > on.ref_end) {
+                                on.query_end = x.qe; on.ref_end = x.re;
+                                on.query_prev_hit_startpos = x.qs; on.ref_prev_hit_startpos = x.rs;
+                                on.n_hits++; added[z] = 1; cnt_done++; break;
+                            } else if (x.qe <= on.query_end && x.re <= on.ref_end) {
+                                on.query_prev_hit_startpos = x.qs; on.ref_prev_hit_startpos = x.rs;
+                                on.n_hits++; added[z] = 1; cnt_done++; break;
+                            }
+                        }
+                    }
+                }
+                if (cnt_done == gn) break;
+            }
+            for (int z = 0; z < gn; ++z)
+                if (!added[z]) open[n_open++] = nam_from_hit(grp[z], ref_id, orient);
+            if ((unsigned)qstart > prev_q_start + (unsigned)k) {
+                flush_passed(open, n_open, qstart, out, n_out);
+                prev_q_start = (unsigned)qstart;
+            }
+        }
+        for (int o = 0; o < n_open; ++o) nam_emit(out, n_out, open[o]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_find_nams: one lane per read
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64)
+k_find_nams(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi, const uint32_t* __restrict__ qcnt,
+            const uint64_t* __restrict__ qbase, const ReadStat* __restrict__ st, const uint64_t* __restrict__ hoff,
+            int n_reads, const int* __restrict__ list, SeedIndexParams p, HitD* __restrict__ hits_buf,
+            rsa_nam* __restrict__ open_buf, rsa_nam* __restrict__ nam_buf, uint8_t* __restrict__ map_scratch,
+            uint32_t map_cap, uint32_t* __restrict__ ncnt, float* __restrict__ nonrep, uint32_t* __restrict__ flags) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_reads) return;
+    const int r = list ? list[t] : t;
+    const int nq = (int)qcnt[r];
+    const uint64_t base = qbase[r];
+    const ReadStat s = st[r];
+    // nonrepetitive_fraction (nam.cpp:920)
+    nonrep[r] = s.found > 0 ? (float)s.good / (float)s.found : 1.0f;
+    DMap m[2];
+    uint8_t* ms = map_scratch + (size_t)t * map_stride(map_cap);
+    map_bind(m[0], ms, map_cap, 0);
+    map_bind(m[1], ms, map_cap, 1);
+    rh_new_reserved(m[0]);
+    rh_new_reserved(m[1]);
+    HitD* hits = hits_buf + hoff[r];
+    int n_hits = 0, n_lists = 0;
+    for (int i = 0; i < nq; ++i) {
+        const QrsInfo o = qi[base + i];
+        if (!(o.flags & 1) || (o.flags & 2)) continue;
+        const rsa_query_randstrobe q = qrs[base + i];
+        const int orient = q.is_reverse ? 1 : 0;
+        add_hits(m[orient], orient, (int)q.start, (int)q.end, p, o.pos, o.count, hits, n_hits, n_lists);
+    }
+    if (m[0].overflow || m[1].overflow) { flags[r] = 2; ncnt[r] = 0; return; }
+    rsa_nam* out = nam_buf + hoff[r];
+    rsa_nam* open = open_buf + hoff[r];
+    int n_out = 0;
+    merge_slow(m[0], 0, hits, n_hits, p.k, open, out, n_out);
+    merge_slow(m[1], 1, hits, n_hits, p.k, open, out, n_out);
+    ncnt[r] = (uint32_t)n_out;
+    flags[r] = 0;
+}
+
+// ---------------------------------------------------------------------------
+// k_rescue: find_nams_rescue for listed reads (one lane per read)
+// ---------------------------------------------------------------------------
+struct RescueD { uint64_t pos; uint32_t count, qs, qe, pad; };
+
+__device__ __forceinline__ bool rcmp1(const RescueD& a, const RescueD& b) {   // nam.cpp:943-946
+    if (a.count != b.count) return a.count < b.count;
+    if (a.qs != b.qs) return a.qs < b.qs;
+    return a.qe < b.qe;
+}
+
+__global__ void __launch_bounds__(64)
+k_rescue(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi, const uint32_t* __restrict__ qcnt,
+         const uint64_t* __restrict__ qbase, const uint64_t* __restrict__ roff, int n_list, const int* __restrict__ list,
+         SeedIndexParams p, uint32_t rescue_cutoff, RescueD* __restrict__ rbuf, HitD* __restrict__ hits_buf,
+         rsa_nam* __restrict__ open_buf, rsa_nam* __restrict__ nam_buf, HitD* __restrict__ grp_buf,
+         uint8_t* __restrict__ added_buf, uint8_t* __restrict__ map_scratch, uint32_t map_cap,
+         uint32_t* __restrict__ ncnt, uint32_t* __restrict__ flags) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_list) return;
+    const int r = list[t];
+    const int nq = (int)qcnt[r];
+    const uint64_t base = qbase[r];
+    RescueD* rv = rbuf + base;        // room for nq entries (both orientations)
+    int nf = 0;
+    for (int i = 0; i < nq; ++i) {    // forward first, then rc
+        const QrsInfo o = qi[base + i];
+        if (!(o.flags & 1)) continue;
+        const rsa_query_randstrobe q = qrs[base + i];
+        if (q.is_reverse) continue;
+        RescueD x; x.pos = o.pos; x.count = o.count; x.qs = q.start; x.qe = q.end; x.pad = 0;
+        rv[nf++] = x;
+    }
+    int nr = nf;
+    for (int i = 0; i < nq; ++i) {
+        const QrsInfo o = qi[base + i];
+        if (!(o.flags & 1)) continue;
+        const rsa_query_randstrobe q = qrs[base + i];
+        if (!q.is_reverse) continue;
+        RescueD x; x.pos = o.pos; x.count = o.count; x.qs = q.start; x.qe = q.end; x.pad = 0;
+        rv[nr++] = x;
+    }
+    const int seg_a[2] = {0, nf}, seg_n[2] = {nf, nr - nf};
+    DMap m[2];
+    uint8_t* ms = map_scratch + (size_t)t * map_stride(map_cap);
+    map_bind(m[0], ms, map_cap, 0);
+    map_bind(m[1], ms, map_cap, 1);
+    rh_new_reserved(m[0]);
+    rh_new_reserved(m[1]);
+    int taken[2];
+    int n_lists = 0;
+    for (int o = 0; o < 2; ++o) {
+        RescueD* v = rv + seg_a[o];
+        const int n = seg_n[o];
+        for (int a = 1; a < n; ++a) {   // std::sort by cmp1: keys are unique
+            RescueD x = v[a]; int b = a - 1;
+            while (b >= 0 && rcmp1(x, v[b])) { v[b + 1] = v[b]; --b; }
+            v[b + 1] = x;
+        }
+        int cnt = 0;
+        for (int a = 0; a < n; ++a) {
+            if ((v[a].count > rescue_cutoff && cnt >= 5) || v[a].count > 1000) break;
+            // add_to_hits_per_ref_pre (nam.cpp:87-107): pre-insert keys
+            int min_diff = INT_MAX;
+            for (uint64_t e = v[a].pos; e < v[a].pos + v[a].count; ++e) {
+                const rsa_ref_randstrobe x = p.rs[e];
+                const int rs = (int)x.position, re = rs + (int)(x.packed & 0xFF) + p.k;
+                int d = ((int)v[a].qe - (int)v[a].qs) - (re - rs);
+                d = d < 0 ? -d : d;
+                if (d <= min_diff) {
+                    bool ins;
+                    (void)rh_get_or_insert(m[o], x.packed >> 8, n_lists, ins);
+                    if (ins) n_lists++;
+                    min_diff = d;
+                }
+            }
+            cnt++;
+        }
+        taken[o] = cnt;
+        // re-sort the taken prefix by query_start (cmp2, nam.cpp:948-952)
+        for (int a = 1; a < cnt; ++a) {
+            RescueD x = v[a]; int b = a - 1;
+            while (b >= 0 && x.qs < v[b].qs) { v[b + 1] = v[b]; --b; }
+            v[b + 1] = x;
+        }
+    }
+    HitD* hits = hits_buf + roff[r];
+    int n_hits = 0;
+    for (int o = 0; o < 2; ++o) {
+        const RescueD* v = rv + seg_a[o];
+        for (int a = 0; a < taken[o]; ++a)
+            add_hits(m[o], o, (int)v[a].qs, (int)v[a].qe, p, v[a].pos, v[a].count, hits, n_hits, n_lists);
+    }
+    if (m[0].overflow || m[1].overflow) { flags[r] |= 4; ncnt[r] = 0; return; }
+    rsa_nam* out = nam_buf + roff[r];
+    rsa_nam* open = open_buf + roff[r];
+    HitD* grp = grp_buf + roff[r];
+    uint8_t* added = added_buf + roff[r];
+    int n_out = 0;
+    merge_fast(m[0], 0, hits, n_hits, p.k, open, added, grp, out, n_out);
+    merge_fast(m[1], 1, hits, n_hits, p.k, open, added, grp, out, n_out);
+    ncnt[r] = (uint32_t)n_out;
+    flags[r] = (flags[r] & ~4u) | 8u;   // bit3: rescued result present
+}
+
+// ---------------------------------------------------------------------------
+// k_compact: final list per read = rescue list if rescued else find_nams list
+// ---------------------------------------------------------------------------
+__global__ void k_compact(int n_reads, const uint64_t* __restrict__ hoff, const uint64_t* __restrict__ roff,
+                          const uint32_t* __restrict__ ncnt1, const uint32_t* __restrict__ ncnt2,
+                          const uint32_t* __restrict__ flags, const rsa_nam* __restrict__ nam1,
+                          const rsa_nam* __restrict__ nam2, const uint64_t* __restrict__ ooff, rsa_nam* __restrict__ out) {
+    const int r = blockIdx.x;
+    if (r >= n_reads) return;
+    const bool resc = flags[r] & 8u;
+    const rsa_nam* src = resc ? nam2 + roff[r] : nam1 + hoff[r];
+    const uint32_t n = resc ? ncnt2[r] : ncnt1[r];
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) out[ooff[r] + i] = src[i];
+}
+
+// ---------------------------------------------------------------------------
+// host orchestration
+// ---------------------------------------------------------------------------
+enum {
+    B_SEQ, B_ROFF, B_RLEN, B_QBASE, B_QRS, B_QCNT, B_SYNC, B_QI, B_ST, B_HOFF, B_HITS, B_OPEN, B_NAM1, B_NCNT1,
+    B_NONREP, B_FLAGS, B_MAP, B_ROFF2, B_NAM2, B_NCNT2, B_LIST, B_RBUF, B_OUT, B_OOFF
+};
+enum { H_ST, H_HOFF, H_FLAGS, H_CNT, H_ROFF, H_LIST, H_OOFF, H_CNT2 };
+
 void seed_bufs_release(SeedBufs& b) {
     for (int i = 0; i < 24; ++i) if (b.p[i]) (void)hipFree(b.p[i]);
     for (int i = 0; i < 8; ++i) if (b.h[i]) (void)hipHostFree(b.h[i]);
+    for (int i = 0; i < 24; ++i) { b.p[i] = nullptr; b.cap[i] = 0; }
+    for (int i = 0; i < 8; ++i) { b.h[i] = nullptr; b.hcap[i] = 0; }
 }
-extern "C" int rsa_randstrobes(rsa_ctx*, const rsa_read_batch*, rsa_randstrobe_batch*) { return RSA_ERR_ARG; }
-extern "C" int rsa_seed(rsa_ctx*, const rsa_read_batch*, int32_t, uint32_t, rsa_nam_batch*) { return RSA_ERR_ARG; }
+
+static hipError_t dens(SeedBufs& b, int i, size_t bytes) {
+    bytes = std::max<size_t>(bytes, 64);
+    if (bytes <= b.cap[i]) return hipSuccess;
+    if (b.p[i]) (void)hipFree(b.p[i]);
+    size_t n = std::max(bytes, b.cap[i] + b.cap[i] / 2);
+    hipError_t e = hipMalloc(&b.p[i], n);
+    if (e != hipSuccess) { b.p[i] = nullptr; b.cap[i] = 0; return e; }
+    b.cap[i] = n;
+    return hipSuccess;
+}
+
+static hipError_t hens(SeedBufs& b, int i, size_t bytes) {
+    bytes = std::max<size_t>(bytes, 64);
+    if (bytes <= b.hcap[i]) return hipSuccess;
+    if (b.h[i]) (void)hipHostFree(b.h[i]);
+    size_t n = std::max(bytes, b.hcap[i] + b.hcap[i] / 2);
+    hipError_t e = hipHostMalloc(&b.h[i], n, hipHostMallocDefault);
+    if (e != hipSuccess) { b.h[i] = nullptr; b.hcap[i] = 0; return e; }
+    b.hcap[i] = n;
+    return hipSuccess;
+}
+
+#define SCHK(x)                                                        \
+    do {                                                               \
+        hipError_t e_ = (x);                                           \
+        if (e_ != hipSuccess) { err = std::string(#x) + ": " + hipGetErrorString(e_); return RSA_ERR_HIP; } \
+    } while (0)
+#define DP(i, T) ((T*)b.p[i])
+#define HP(i, T) ((T*)b.h[i])
+
+static const uint32_t MAP_SMALL = 256;
+static const uint32_t MAP_BIG = 65536 + 512;
+
+// Stage 1 (shared by rsa_randstrobes and rsa_seed): upload reads, run k_randstrobes.
+int seed_stage_randstrobes(SeedBufs& b, hipStream_t st, const SeedIndexParams& p, const rsa_read_batch* rb,
+                           std::vector<uint64_t>& qbase, std::string& err) {
+    const uint32_t n = rb->n_reads;
+    qbase.assign(n + 1, 0);
+    uint64_t total_len = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        qbase[i + 1] = qbase[i] + 2ull * rb->lengths[i];
+        total_len = std::max<uint64_t>(total_len, rb->offsets[i] + rb->lengths[i]);
+    }
+    SCHK(dens(b, B_SEQ, total_len + 16));
+    SCHK(dens(b, B_ROFF, 8ull * n));
+    SCHK(dens(b, B_RLEN, 4ull * n));
+    SCHK(dens(b, B_QBASE, 8ull * (n + 1)));
+    SCHK(dens(b, B_QRS, sizeof(rsa_query_randstrobe) * (qbase[n] + 1)));
+    SCHK(dens(b, B_QCNT, 4ull * n));
+    SCHK(dens(b, B_SYNC, sizeof(SyncD) * (qbase[n] / 2 + 1)));
+    SCHK(hipMemcpyAsync(b.p[B_SEQ], rb->seq, total_len, hipMemcpyHostToDevice, st));
+    SCHK(hipMemcpyAsync(b.p[B_ROFF], rb->offsets, 8ull * n, hipMemcpyHostToDevice, st));
+    SCHK(hipMemcpyAsync(b.p[B_RLEN], rb->lengths, 4ull * n, hipMemcpyHostToDevice, st));
+    SCHK(hipMemcpyAsync(b.p[B_QBASE], qbase.data(), 8ull * (n + 1), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_randstrobes, dim3((n + 63) / 64), dim3(64), 0, st, DP(B_SEQ, char), DP(B_ROFF, uint64_t),
+                       DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n, p, DP(B_SYNC, SyncD),
+                       DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
+    SCHK(hipGetLastError());
+    return RSA_OK;
+}
+
+int seed_randstrobes_run(SeedBufs& b, hipStream_t st, const SeedIndexParams& p, const rsa_read_batch* rb,
+                         rsa_randstrobe_batch* out, std::string& err) {
+    const uint32_t n = rb->n_reads;
+    std::vector<uint64_t> qbase;
+    int rc = seed_stage_randstrobes(b, st, p, rb, qbase, err);
+    if (rc) return rc;
+    std::vector<uint32_t> cnt(n);
+    SCHK(hipMemcpyAsync(cnt.data(), b.p[B_QCNT], 4ull * n, hipMemcpyDeviceToHost, st));
+    SCHK(hipStreamSynchronize(st));
+    uint64_t tot = 0;
+    for (uint32_t i = 0; i < n; ++i) { out->offsets[i] = tot; tot += cnt[i]; }
+    out->offsets[n] = tot;
+    out->needed = tot;
+    if (tot > out->capacity) { err = "rsa_randstrobes: output too small"; return RSA_ERR_CAPACITY; }
+    std::vector<rsa_query_randstrobe> all(qbase[n] + 1);
+    SCHK(hipMemcpyAsync(all.data(), b.p[B_QRS], sizeof(rsa_query_randstrobe) * qbase[n], hipMemcpyDeviceToHost, st));
+    SCHK(hipStreamSynchronize(st));
+    for (uint32_t i = 0; i < n; ++i)
+        memcpy(out->out + out->offsets[i], all.data() + qbase[i], sizeof(rsa_query_randstrobe) * cnt[i]);
+    return RSA_OK;
+}
+
+int seed_run(SeedBufs& b, hipStream_t st, hipEvent_t* ev, const SeedIndexParams& p, const rsa_read_batch* rb,
+             int32_t rescue_level, uint32_t rescue_cutoff, rsa_nam_batch* out, std::string& err, float* ms,
+             uint64_t* counters) {
+    const uint32_t n = rb->n_reads;
+    std::vector<uint64_t> qbase;
+    SCHK(hipEventRecord(ev[0], st));
+    int rc = seed_stage_randstrobes(b, st, p, rb, qbase, err);
+    if (rc) return rc;
+    SCHK(hipEventRecord(ev[1], st));
+    SCHK(dens(b, B_QI, sizeof(QrsInfo) * (qbase[n] + 1)));
+    SCHK(dens(b, B_ST, sizeof(ReadStat) * n));
+    hipLaunchKernelGGL(k_lookup, dim3((n + 3) / 4), dim3(256), 0, st, DP(B_QRS, rsa_query_randstrobe),
+                       DP(B_QCNT, uint32_t), DP(B_QBASE, uint64_t), (int)n, p, DP(B_QI, QrsInfo), DP(B_ST, ReadStat));
+    SCHK(hipGetLastError());
+    SCHK(hipEventRecord(ev[2], st));
+    SCHK(hens(b, H_ST, sizeof(ReadStat) * n));
+    SCHK(hipMemcpyAsync(b.h[H_ST], b.p[B_ST], sizeof(ReadStat) * n, hipMemcpyDeviceToHost, st));
+    SCHK(hens(b, H_CNT, 4ull * n));
+    SCHK(hipMemcpyAsync(b.h[H_CNT], b.p[B_QCNT], 4ull * n, hipMemcpyDeviceToHost, st));
+    SCHK(hipStreamSynchronize(st));
+    const ReadStat* hs = HP(H_ST, ReadStat);
+    SCHK(hens(b, H_HOFF, 8ull * (n + 1)));
+    uint64_t* hoff = HP(H_HOFF, uint64_t);
+    hoff[0] = 0;
+    uint64_t n_qrs = 0, n_found = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        hoff[i + 1] = hoff[i] + hs[i].hits_find;
+        n_qrs += HP(H_CNT, uint32_t)[i];
+        n_found += hs[i].found;
+    }
+    const uint64_t H = hoff[n];
+    SCHK(dens(b, B_HOFF, 8ull * (n + 1)));
+    SCHK(dens(b, B_HITS, sizeof(HitD) * (H + 1)));
+    SCHK(dens(b, B_OPEN, sizeof(rsa_nam) * (H + 1)));
+    SCHK(dens(b, B_NAM1, sizeof(rsa_nam) * (H + 1)));
+    SCHK(dens(b, B_NCNT1, 4ull * n));
+    SCHK(dens(b, B_NONREP, 4ull * n));
+    SCHK(dens(b, B_FLAGS, 4ull * n));
+    const size_t small_stride = (size_t)MAP_SMALL * 9 * 4;
+    const uint32_t chunk = 65536;
+    SCHK(dens(b, B_MAP, small_stride * std::min<uint32_t>(n, chunk)));
+    SCHK(hipMemcpyAsync(b.p[B_HOFF], hoff, 8ull * (n + 1), hipMemcpyHostToDevice, st));
+    for (uint32_t a = 0; a < n; a += chunk) {
+        const uint32_t cnt = std::min(chunk, n - a);
+        // reads [a, a+cnt) use map slots [0, cnt): pass a list-less launch by offsetting pointers
+        hipLaunchKernelGGL(k_find_nams, dim3((cnt + 63) / 64), dim3(64), 0, st, DP(B_QRS, rsa_query_randstrobe),
+                           DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t) + a, DP(B_QBASE, uint64_t) + a, DP(B_ST, ReadStat) + a,
+                           DP(B_HOFF, uint64_t) + a, (int)cnt, (const int*)nullptr, p, DP(B_HITS, HitD),
+                           DP(B_OPEN, rsa_nam), DP(B_NAM1, rsa_nam), DP(B_MAP, uint8_t), MAP_SMALL,
+                           DP(B_NCNT1, uint32_t) + a, DP(B_NONREP, float) + a, DP(B_FLAGS, uint32_t) + a);
+        SCHK(hipGetLastError());
+    }
+    SCHK(hens(b, H_FLAGS, 4ull * n));
+    SCHK(hipMemcpyAsync(b.h[H_FLAGS], b.p[B_FLAGS], 4ull * n, hipMemcpyDeviceToHost, st));
+    SCHK(hipMemcpyAsync(b.h[H_CNT], b.p[B_NCNT1], 4ull * n, hipMemcpyDeviceToHost, st));
+    SCHK(hipStreamSynchronize(st));
+    // rare: reads whose maps rehash past the small table -> big-map pass
+    std::vector<int> big;
+    for (uint32_t i = 0; i < n; ++i) if (HP(H_FLAGS, uint32_t)[i] & 2u) big.push_back((int)i);
+    if (!big.empty()) {
+        const size_t big_stride = (size_t)MAP_BIG * 9 * 4;
+        const uint32_t bchunk = 32;
+        SCHK(dens(b, B_MAP, std::max(big_stride * bchunk, small_stride * std::min<uint32_t>(n, chunk))));
+        SCHK(dens(b, B_LIST, 4ull * big.size()));
+        SCHK(hipMemcpyAsync(b.p[B_LIST], big.data(), 4ull * big.size(), hipMemcpyHostToDevice, st));
+        for (size_t a = 0; a < big.size(); a += bchunk) {
+            const int cnt = (int)std::min<size_t>(bchunk, big.size() - a);
+            hipLaunchKernelGGL(k_find_nams, dim3(1), dim3(64), 0, st, DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo),
+                               DP(B_QCNT, uint32_t), DP(B_QBASE, uint64_t), DP(B_ST, ReadStat), DP(B_HOFF, uint64_t), cnt,
+                               DP(B_LIST, int) + a, p, DP(B_HITS, HitD), DP(B_OPEN, rsa_nam), DP(B_NAM1, rsa_nam),
+                               DP(B_MAP, uint8_t), MAP_BIG, DP(B_NCNT1, uint32_t), DP(B_NONREP, float),
+                               DP(B_FLAGS, uint32_t));
+            SCHK(hipGetLastError());
+        }
+        SCHK(hipMemcpyAsync(b.h[H_FLAGS], b.p[B_FLAGS], 4ull * n, hipMemcpyDeviceToHost, st));
+        SCHK(hipMemcpyAsync(b.h[H_CNT], b.p[B_NCNT1], 4ull * n, hipMemcpyDeviceToHost, st));
+        SCHK(hipStreamSynchronize(st));
+        for (int i : big) if (HP(H_FLAGS, uint32_t)[i] & 2u) { err = "rsa_seed: robin_hood emulation overflow"; return RSA_ERR_NOMEM; }
+    }
+    SCHK(hipEventRecord(ev[3], st));
+    // nonrepetitive fraction to host
+    SCHK(hipMemcpyAsync(out->nonrepetitive_fraction, b.p[B_NONREP], 4ull * n, hipMemcpyDeviceToHost, st));
+    SCHK(hipStreamSynchronize(st));
+    // rescue decision (aln.cpp:1954-1962)
+    std::vector<int> resc;
+    std::vector<uint32_t> n1(HP(H_CNT, uint32_t), HP(H_CNT, uint32_t) + n);
+    SCHK(hens(b, H_ROFF, 8ull * (n + 1)));
+    uint64_t* roff = HP(H_ROFF, uint64_t);
+    roff[0] = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const bool need = rescue_level > 1 && (n1[i] == 0 || out->nonrepetitive_fraction[i] < 0.7f);
+        roff[i + 1] = roff[i] + (need ? hs[i].hits_all : 0);
+        if (need) resc.push_back((int)i);
+        out->rescued[i] = need ? 1 : 0;
+    }
+    std::vector<uint32_t> n2(n, 0);
+    if (!resc.empty()) {
+        const uint64_t R = roff[n];
+        SCHK(dens(b, B_ROFF2, 8ull * (n + 1)));
+        SCHK(dens(b, B_NAM2, sizeof(rsa_nam) * (R + 1)));
+        SCHK(dens(b, B_NCNT2, 4ull * n));
+        SCHK(dens(b, B_RBUF, sizeof(RescueD) * (qbase[n] + 1)));
+        // rescue reuses the hits/open buffers sized for max(H, R), plus group + added scratch
+        SCHK(dens(b, B_HITS, sizeof(HitD) * (std::max(H, R) + 1)));
+        SCHK(dens(b, B_OPEN, sizeof(rsa_nam) * (std::max(H, R) + 1)));
+        SCHK(dens(b, B_OUT, (sizeof(HitD) + 1) * (R + 1)));
+        SCHK(dens(b, B_LIST, 4ull * resc.size()));
+        SCHK(hipMemcpyAsync(b.p[B_ROFF2], roff, 8ull * (n + 1), hipMemcpyHostToDevice, st));
+        SCHK(hipMemcpyAsync(b.p[B_LIST], resc.data(), 4ull * resc.size(), hipMemcpyHostToDevice, st));
+        HitD* grp = DP(B_OUT, HitD);
+        uint8_t* added = (uint8_t*)(grp + (R + 1));
+        for (size_t a = 0; a < resc.size(); a += chunk) {
+            const int cnt = (int)std::min<size_t>(chunk, resc.size() - a);
+            hipLaunchKernelGGL(k_rescue, dim3((cnt + 63) / 64), dim3(64), 0, st, DP(B_QRS, rsa_query_randstrobe),
+                               DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t), DP(B_QBASE, uint64_t), DP(B_ROFF2, uint64_t), cnt,
+                               DP(B_LIST, int) + a, p, rescue_cutoff, DP(B_RBUF, RescueD), DP(B_HITS, HitD),
+                               DP(B_OPEN, rsa_nam), DP(B_NAM2, rsa_nam), grp, added, DP(B_MAP, uint8_t), MAP_SMALL,
+                               DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t));
+            SCHK(hipGetLastError());
+        }
+        SCHK(hipMemcpyAsync(b.h[H_FLAGS], b.p[B_FLAGS], 4ull * n, hipMemcpyDeviceToHost, st));
+        SCHK(hipStreamSynchronize(st));
+        std::vector<int> bigr;
+        for (int i : resc) if (HP(H_FLAGS, uint32_t)[i] & 4u) bigr.push_back(i);
+        if (!bigr.empty()) {
+            const size_t big_stride = (size_t)MAP_BIG * 9 * 4;
+            const uint32_t bchunk = 32;
+            SCHK(dens(b, B_MAP, std::max(big_stride * bchunk, b.cap[B_MAP])));
+            SCHK(dens(b, B_LIST, 4ull * std::max(bigr.size(), resc.size())));
+            SCHK(hipMemcpyAsync(b.p[B_LIST], bigr.data(), 4ull * bigr.size(), hipMemcpyHostToDevice, st));
+            for (size_t a = 0; a < bigr.size(); a += bchunk) {
+                const int cnt = (int)std::min<size_t>(bchunk, bigr.size() - a);
+                hipLaunchKernelGGL(k_rescue, dim3(1), dim3(64), 0, st, DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo),
+                                   DP(B_QCNT, uint32_t), DP(B_QBASE, uint64_t), DP(B_ROFF2, uint64_t), cnt,
+                                   DP(B_LIST, int) + a, p, rescue_cutoff, DP(B_RBUF, RescueD), DP(B_HITS, HitD),
+                                   DP(B_OPEN, rsa_nam), DP(B_NAM2, rsa_nam), grp, added, DP(B_MAP, uint8_t), MAP_BIG,
+                                   DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t));
+                SCHK(hipGetLastError());
+            }
+            SCHK(hipMemcpyAsync(b.h[H_FLAGS], b.p[B_FLAGS], 4ull * n, hipMemcpyDeviceToHost, st));
+            SCHK(hipStreamSynchronize(st));
+            for (int i : bigr) if (HP(H_FLAGS, uint32_t)[i] & 4u) { err = "rsa_seed: rescue map overflow"; return RSA_ERR_NOMEM; }
+        }
+        SCHK(hens(b, H_CNT2, 4ull * n));
+        SCHK(hipMemcpyAsync(b.h[H_CNT2], b.p[B_NCNT2], 4ull * n, hipMemcpyDeviceToHost, st));
+        SCHK(hipStreamSynchronize(st));
+        for (int i : resc) n2[i] = HP(H_CNT2, uint32_t)[i];
+    } else {
+        SCHK(dens(b, B_ROFF2, 8ull * (n + 1)));
+        SCHK(dens(b, B_NAM2, sizeof(rsa_nam)));
+        SCHK(dens(b, B_NCNT2, 4ull * n));
+        SCHK(hipMemcpyAsync(b.p[B_ROFF2], roff, 8ull * (n + 1), hipMemcpyHostToDevice, st));
+    }
+    // final offsets + compaction
+    SCHK(hens(b, H_OOFF, 8ull * (n + 1)));
+    uint64_t* ooff = HP(H_OOFF, uint64_t);
+    ooff[0] = 0;
+    for (uint32_t i = 0; i < n; ++i) ooff[i + 1] = ooff[i] + (out->rescued[i] ? n2[i] : n1[i]);
+    const uint64_t total = ooff[n];
+    for (uint32_t i = 0; i <= n; ++i) out->offsets[i] = ooff[i];
+    out->needed = total;
+    if (total > out->capacity) { err = "rsa_seed: NAM output too small"; return RSA_ERR_CAPACITY; }
+    // resc flag bit3 must be visible to k_compact for rescued reads with bit3 set on device already
+    SCHK(dens(b, B_OOFF, 8ull * (n + 1)));
+    SCHK(dens(b, B_OUT, std::max(b.cap[B_OUT], sizeof(rsa_nam) * (total + 1))));
+    SCHK(hipMemcpyAsync(b.p[B_OOFF], ooff, 8ull * (n + 1), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_compact, dim3(n), dim3(64), 0, st, (int)n, DP(B_HOFF, uint64_t), DP(B_ROFF2, uint64_t),
+                       DP(B_NCNT1, uint32_t), DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t), DP(B_NAM1, rsa_nam),
+                       DP(B_NAM2, rsa_nam), DP(B_OOFF, uint64_t), DP(B_OUT, rsa_nam));
+    SCHK(hipGetLastError());
+    SCHK(hipEventRecord(ev[4], st));
+    if (total) SCHK(hipMemcpyAsync(out->nams, b.p[B_OUT], sizeof(rsa_nam) * total, hipMemcpyDeviceToHost, st));
+    SCHK(hipStreamSynchronize(st));
+    float t01 = 0, t12 = 0, t23 = 0, t34 = 0;
+    (void)hipEventElapsedTime(&t01, ev[0], ev[1]);
+    (void)hipEventElapsedTime(&t12, ev[1], ev[2]);
+    (void)hipEventElapsedTime(&t23, ev[2], ev[3]);
+    (void)hipEventElapsedTime(&t34, ev[3], ev[4]);
+    ms[0] = t01; ms[1] = t12; ms[2] = t23 + t34;
+    counters[0] = n; counters[1] = n_qrs; counters[2] = n_found; counters[3] = H; counters[4] = total;
+    return RSA_OK;
+}

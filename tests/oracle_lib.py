@@ -72,7 +72,7 @@ def align(query: bytes, ref: bytes, match=2, mismatch=8, gap_open=12, gap_extend
                 cigar=[int(x) for x in cig[:info.n_cigar]])
 
 
-QRS_DTYPE = np.dtype([("hash", "<u8"), ("start", "<u4"), ("end", "<u4"), ("is_reverse", "<u4")])
+QRS_DTYPE = np.dtype([("hash", "<u8"), ("start", "<u4"), ("end", "<u4"), ("is_reverse", "<u4"), ("pad_", "<u4")])
 NAM_DTYPE = np.dtype([("nam_id", "<i4"), ("query_start", "<i4"), ("query_end", "<i4"),
                       ("query_prev_hit_startpos", "<i4"), ("ref_start", "<i4"), ("ref_end", "<i4"),
                       ("ref_prev_hit_startpos", "<i4"), ("n_hits", "<i4"), ("ref_id", "<i4"),
