@@ -909,8 +909,22 @@ static void cig_push(cig* c, uint32_t op, uint32_t len) {
     else c->v[c->n - 1] += len << 4;
 }
 
+typedef void (*ora_raw_fn)(const int8_t*, int, const int8_t*, int, int, int, int, int, ora_ssw_res*, uint32_t*);
+
+void ora_aligner_align_with(const char* query, int qlen, const char* ref, int rlen, int match, int mismatch,
+                            int gap_open, int gap_extend, int end_bonus, ora_aln_info* out, uint32_t* cigar,
+                            ora_raw_fn raw_fn);
+
 void ora_aligner_align(const char* query, int qlen, const char* ref, int rlen, int match, int mismatch,
                        int gap_open, int gap_extend, int end_bonus, ora_aln_info* out, uint32_t* cigar) {
+    ora_aligner_align_with(query, qlen, ref, rlen, match, mismatch, gap_open, gap_extend, end_bonus, out, cigar,
+                           ora_ssw_align);
+}
+
+/* Aligner::align with a pluggable raw ssw_align (ours, or the reference's ssw.c) */
+void ora_aligner_align_with(const char* query, int qlen, const char* ref, int rlen, int match, int mismatch,
+                            int gap_open, int gap_extend, int end_bonus, ora_aln_info* out, uint32_t* cigar,
+                            ora_raw_fn raw_fn) {
     memset(out, 0, sizeof *out);
     if (rlen > 2000) {                       /* aligner.cpp:119-125 */
         out->edit_distance = 100000; out->ref_start = 0; out->sw_score = -1000000;
@@ -922,7 +936,7 @@ void ora_aligner_align(const char* query, int qlen, const char* ref, int rlen, i
     for (int i = 0; i < rlen; ++i) tr[i] = translate((unsigned char)ref[i]);
     uint32_t* raw = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(2 * (qlen + rlen) + 16));
     ora_ssw_res s;
-    ora_ssw_align(tq, qlen, tr, rlen, match, mismatch, gap_open, gap_extend, &s, raw);
+    raw_fn(tq, qlen, tr, rlen, match, mismatch, gap_open, gap_extend, &s, raw);
     if (s.flag != 0) {                       /* aligner.cpp:131-136 */
         out->edit_distance = 100000; out->ref_start = 0; out->sw_score = -100000;
         free(tq); free(tr); free(raw);

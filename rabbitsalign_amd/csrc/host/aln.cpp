@@ -1,0 +1,960 @@
+// aln.cpp -- mapping decisions around the hot path, restated from the
+// reference's src/aln.cpp (part/last split of RabbitSAlign) and the per-job
+// string building / result storing of src/pc.cpp.  Every function keeps the
+// reference's arithmetic types (float vs double vs size_t) because they are
+// observable in the SAM output.  Compile with -ffp-contract=off.
+#include <algorithm>
+#include <cassert>
+#include <climits>
+#include <cmath>
+#include <math.h>
+#include <unordered_set>
+
+#include "rsa_host.hpp"
+
+namespace rsa {
+
+// ------------------------------------------------------------ sequences ---
+static const unsigned char* revcomp_table() {      // src/revcomp.hpp:10-27
+    static unsigned char t[256];
+    static bool init = false;
+    if (!init) {
+        for (int i = 0; i < 256; ++i) t[i] = 'N';
+        t['A'] = 'T'; t['C'] = 'G'; t['G'] = 'C'; t['T'] = 'A'; t['U'] = 'A';
+        t['a'] = 'T'; t['c'] = 'G'; t['g'] = 'C'; t['t'] = 'A'; t['u'] = 'A';
+        init = true;
+    }
+    return t;
+}
+
+std::string reverse_complement(std::string_view s) {
+    const unsigned char* t = revcomp_table();
+    std::string r(s.size(), 'N');
+    for (size_t i = 0; i < s.size(); ++i) r[i] = (char)t[(unsigned char)s[s.size() - 1 - i]];
+    return r;
+}
+
+Read::Read(const std::string& s) : seq(s), rc(reverse_complement(s)) {}
+
+void to_uppercase(std::string& s) {
+    for (auto& c : s) c = (char)((unsigned char)c & ~32);
+}
+
+// std::string::substr semantics without the copy (throws never: pos <= size holds on every call site)
+static inline std::string_view sub(std::string_view s, size_t pos, size_t len) {
+    if (pos > s.size()) pos = s.size();
+    return s.substr(pos, len);
+}
+
+// --------------------------------------------------------- estimators ---
+void InsertSizeDistribution::update(int dist) {      // aln.cpp:1880-1903
+    if (dist >= 2000) return;
+    const float e = dist - mu;
+    mu += e / sample_size;
+    SSE += e * (dist - mu);
+    if (sample_size > 1) V = SSE / (sample_size - 1.0);
+    else V = SSE;
+    sigma = std::sqrt(V);
+    sample_size = sample_size + 1.0;
+}
+
+template <typename T>
+static bool by_score(const T& a, const T& b) { return a.score > b.score; }
+
+// ------------------------------------------------------------- NAM ops ---
+// aln.cpp:60-93
+static bool reverse_nam_if_needed(Nam& nam, const Read& read, const References& refs, int k) {
+    const size_t read_len = read.size();
+    std::string_view ref = refs.seqs[nam.ref_id];
+    std::string_view ref_start_kmer = sub(ref, (size_t)nam.ref_start, (size_t)k);
+    std::string_view ref_end_kmer = sub(ref, (size_t)(nam.ref_end - k), (size_t)k);
+    std::string_view seq, seq_rc;
+    if (nam.is_rc) { seq = read.rc; seq_rc = read.seq; }
+    else { seq = read.seq; seq_rc = read.rc; }
+    std::string_view read_start_kmer = sub(seq, (size_t)nam.query_start, (size_t)k);
+    std::string_view read_end_kmer = sub(seq, (size_t)(nam.query_end - k), (size_t)k);
+    if (ref_start_kmer == read_start_kmer && ref_end_kmer == read_end_kmer) return true;
+    const int q_start_tmp = (int)read_len - nam.query_end;
+    const int q_end_tmp = (int)read_len - nam.query_start;
+    read_start_kmer = sub(seq_rc, (size_t)q_start_tmp, (size_t)k);
+    read_end_kmer = sub(seq_rc, (size_t)(q_end_tmp - k), (size_t)k);
+    if (ref_start_kmer == read_start_kmer && ref_end_kmer == read_end_kmer) {
+        nam.is_rc = !nam.is_rc;
+        nam.query_start = q_start_tmp;
+        nam.query_end = q_end_tmp;
+        return true;
+    }
+    return false;
+}
+
+static void shuffle_top_nams(std::vector<Nam>& nams, std::minstd_rand& rng) {   // aln.cpp:1910-1925
+    if (nams.empty()) return;
+    const float best = nams[0].score;
+    auto it = std::find_if(nams.begin(), nams.end(), [&](const Nam& n) { return n.score != best; });
+    if (it != nams.end()) std::shuffle(nams.begin(), it, rng);
+}
+
+static float top_dropoff(const std::vector<Nam>& nams) {   // aln.cpp:1349-1360
+    const Nam& n_max = nams[0];
+    if (n_max.n_hits <= 2) return 1.0;
+    if (nams.size() > 1) return (float)nams[1].n_hits / n_max.n_hits;
+    return 0.0;
+}
+
+static uint8_t get_mapq(const std::vector<Nam>& nams, const Nam& n_max) {   // aln.cpp:493-503
+    if (nams.size() <= 1) return 60;
+    const float s1 = n_max.score;
+    const float s2 = nams[1].score;
+    const float min_matches = std::min(n_max.n_hits / 10.0, 1.0);
+    const int uncapped_mapq = 40 * (1 - s2 / s1) * min_matches * log(s1);
+    return std::min(uncapped_mapq, 60);
+}
+
+static bool is_proper_nam_pair(const Nam& nam1, const Nam& nam2, float mu, float sigma) {   // aln.cpp:552-569
+    if (nam1.ref_id != nam2.ref_id || nam1.is_rc == nam2.is_rc) return false;
+    int a = std::max(0, nam1.ref_start - nam1.query_start);
+    int b = std::max(0, nam2.ref_start - nam2.query_start);
+    bool r1_r2 = nam2.is_rc && (a <= b) && (b - a < mu + 10 * sigma);
+    if (r1_r2) return true;
+    bool r2_r1 = nam1.is_rc && (b <= a) && (a - b < mu + 10 * sigma);
+    if (r2_r1) return true;
+    return false;
+}
+
+struct NamPair { int score; Nam nam1; Nam nam2; };
+
+// aln.cpp:583-918 (use_fast_loop3 variant)
+static std::vector<NamPair> get_best_scoring_nam_pairs(const std::vector<Nam>& nams1, const std::vector<Nam>& nams2,
+                                                       float mu, float sigma) {
+    std::vector<NamPair> joint;
+    if (nams1.empty() && nams2.empty()) return joint;
+    joint.reserve(nams1.size() + nams2.size());
+    std::unordered_set<int> added_n1, added_n2;
+    int best_joint_hits = 0;
+    std::vector<Nam> sorted2[2];
+    for (const auto& n2 : nams2) sorted2[n2.is_rc ? 1 : 0].push_back(n2);
+    for (int i = 0; i < 2; ++i)
+        std::sort(sorted2[i].begin(), sorted2[i].end(), [](const Nam& a, const Nam& b) {
+            int v1 = std::max(0, a.ref_start - a.query_start);
+            int v2 = std::max(0, b.ref_start - b.query_start);
+            return v1 < v2;
+        });
+    for (const auto& nam1 : nams1) {
+        const int nam1_val = std::max(0, nam1.ref_start - nam1.query_start);
+        if (nam1.is_rc == 1) {
+            const float L_val = nam1_val - (mu + 10 * sigma);
+            const float R_val = nam1_val;
+            const auto& v = sorted2[0];
+            int ll = 0, rr = (int)v.size() - 1, ans = (int)v.size();
+            while (ll <= rr) {
+                int mid = (ll + rr) / 2;
+                int now = std::max(0, v[mid].ref_start - v[mid].query_start);
+                if (now > L_val) { rr = mid - 1; ans = mid; }
+                else ll = mid + 1;
+            }
+            for (int id = ans; id < (int)v.size(); ++id) {
+                const Nam& nam2 = v[id];
+                int joint_hits = nam1.n_hits + nam2.n_hits;
+                if (nam1.ref_id != nam2.ref_id) continue;
+                int a = std::max(0, nam1.ref_start - nam1.query_start);
+                int b = std::max(0, nam2.ref_start - nam2.query_start);
+                if (b > R_val - 1e-6) break;
+                bool r2_r1 = (a - b >= 0) && (a - b < mu + 10 * sigma);
+                if (r2_r1) {
+                    joint.push_back(NamPair{joint_hits, nam1, nam2});
+                    added_n1.insert(nam1.nam_id);
+                    added_n2.insert(nam2.nam_id);
+                }
+            }
+        } else {
+            const float L_val = nam1_val;
+            const float R_val = nam1_val + mu + 10 * sigma;
+            const auto& v = sorted2[1];
+            int ll = 0, rr = (int)v.size() - 1, ans = (int)v.size();
+            while (ll <= rr) {
+                int mid = (ll + rr) / 2;
+                int now = std::max(0, v[mid].ref_start - v[mid].query_start);
+                if (now >= L_val) { rr = mid - 1; ans = mid; }
+                else ll = mid + 1;
+            }
+            for (int id = ans; id < (int)v.size(); ++id) {
+                const Nam& nam2 = v[id];
+                int joint_hits = nam1.n_hits + nam2.n_hits;
+                if (nam1.ref_id != nam2.ref_id) continue;
+                int a = std::max(0, nam1.ref_start - nam1.query_start);
+                int b = std::max(0, nam2.ref_start - nam2.query_start);
+                if (b >= R_val - 1e-6) break;
+                bool r1_r2 = (b - a >= 0) && (b - a < mu + 10 * sigma);
+                if (r1_r2) {
+                    joint.push_back(NamPair{joint_hits, nam1, nam2});
+                    added_n1.insert(nam1.nam_id);
+                    added_n2.insert(nam2.nam_id);
+                }
+            }
+        }
+    }
+    Nam dummy{};
+    dummy.ref_start = -1;
+    if (!nams1.empty()) {
+        int best1 = best_joint_hits > 0 ? best_joint_hits : nams1[0].n_hits;
+        for (const auto& nam1 : nams1) {
+            if (nam1.n_hits < best1 / 2) break;
+            if (added_n1.count(nam1.nam_id)) continue;
+            joint.push_back(NamPair{nam1.n_hits, nam1, dummy});
+        }
+    }
+    if (!nams2.empty()) {
+        int best2 = best_joint_hits > 0 ? best_joint_hits : nams2[0].n_hits;
+        for (const auto& nam2 : nams2) {
+            if (nam2.n_hits < best2 / 2) break;
+            if (added_n2.count(nam2.nam_id)) continue;
+            joint.push_back(NamPair{nam2.n_hits, dummy, nam2});
+        }
+    }
+    std::sort(joint.begin(), joint.end(), [](const NamPair& a, const NamPair& b) { return a.score > b.score; });
+    return joint;
+}
+
+// ------------------------------------------------------------ hamming ---
+static int hamming_distance(std::string_view s, std::string_view t) {   // aligner.hpp:54-67
+    if (s.size() != t.size()) return -1;
+    int m = 0;
+    for (size_t i = 0; i < s.size(); ++i) m += s[i] != t[i];
+    return m;
+}
+
+// aligner.cpp:219-252
+static void highest_scoring_segment(std::string_view q, std::string_view r, int match, int mismatch, int end_bonus,
+                                    size_t& bs, size_t& be, int& bsc) {
+    size_t n = q.size(), start = 0;
+    int score = end_bonus;
+    size_t best_start = 0, best_end = 0;
+    int best_score = 0;
+    for (size_t i = 0; i < n; ++i) {
+        if (q[i] == r[i]) score += match; else score -= mismatch;
+        if (score < 0) { start = i + 1; score = 0; }
+        if (score > best_score) { best_start = start; best_score = score; best_end = i + 1; }
+    }
+    if (score + end_bonus > best_score) {
+        best_score = score + end_bonus;
+        best_end = q.size();
+        best_start = start;
+    }
+    bs = best_start; be = best_end; bsc = best_score;
+}
+
+// aligner.cpp:254-302
+static AlignmentInfo hamming_align(std::string_view q, std::string_view r, int match, int mismatch, int end_bonus) {
+    AlignmentInfo aln;
+    if (q.size() != r.size()) return aln;
+    size_t s, e;
+    int score;
+    highest_scoring_segment(q, r, match, mismatch, end_bonus, s, e, score);
+    Cigar cigar;
+    if (s > 0) cigar.push(C_S, (uint32_t)s);
+    int counter = 0, mismatches = 0;
+    bool prev_is_match = false, first = true;
+    for (size_t i = s; i < e; i++) {
+        bool is_match = q[i] == r[i];
+        mismatches += is_match ? 0 : 1;
+        if (!first && is_match != prev_is_match) {
+            cigar.push(prev_is_match ? C_EQ : C_X, (uint32_t)counter);
+            counter = 0;
+        }
+        counter++;
+        prev_is_match = is_match;
+        first = false;
+    }
+    if (!first) cigar.push(prev_is_match ? C_EQ : C_X, (uint32_t)counter);
+    int soft_right = (int)q.size() - (int)e;
+    if (soft_right > 0) cigar.push(C_S, (uint32_t)soft_right);
+    aln.cigar = std::move(cigar);
+    aln.sw_score = score;
+    aln.edit_distance = (unsigned)mismatches;
+    aln.ref_start = (unsigned)s; aln.ref_end = (unsigned)e;
+    aln.query_start = (unsigned)s; aln.query_end = (unsigned)e;
+    return aln;
+}
+
+// ------------------------------------------------------------- part ---
+// extend_seed_part (aln.cpp:374-431)
+static bool extend_seed_part(AlignTmpRes& res, const AlignmentParameters& ap, const Nam& nam, const References& refs,
+                             const Read& read, bool consistent_nam) {
+    std::string_view query = nam.is_rc ? std::string_view(read.rc) : std::string_view(read.seq);
+    std::string_view ref = refs.seqs[nam.ref_id];
+    const auto projected_ref_start = std::max(0, nam.ref_start - nam.query_start);
+    const auto projected_ref_end = std::min(nam.ref_end + query.size() - nam.query_end, ref.size());
+    AlignmentInfo info;
+    int result_ref_start = 0;
+    bool gapped = true;
+    if (projected_ref_end - projected_ref_start == query.size() && consistent_nam) {
+        std::string_view segm = sub(ref, (size_t)projected_ref_start, query.size());
+        int hd = hamming_distance(query, segm);
+        if (hd >= 0 && (((float)hd / query.size()) < 0.05)) {
+            info = hamming_align(query, segm, ap.match, ap.mismatch, ap.end_bonus);
+            result_ref_start = projected_ref_start + (int)info.ref_start;
+            gapped = false;
+        }
+    }
+    res.todo_nams.push_back(nam);
+    res.is_extend_seed.push_back(true);
+    if (gapped) {
+        res.done_align.push_back(false);
+        res.align_res.push_back(Alignment());
+    } else {
+        res.done_align.push_back(true);
+        int softclipped = (int)info.query_start + ((int)query.size() - (int)info.query_end);
+        Alignment a;
+        a.cigar = std::move(info.cigar);
+        a.edit_distance = (int)info.edit_distance;
+        a.global_ed = (int)info.edit_distance + softclipped;
+        a.score = info.sw_score;
+        a.ref_start = result_ref_start;
+        a.length = info.ref_span();
+        a.is_rc = nam.is_rc;
+        a.is_unaligned = false;
+        a.ref_id = nam.ref_id;
+        a.gapped = gapped;
+        res.align_res.push_back(std::move(a));
+    }
+    return gapped;
+}
+
+// has_shared_substring (aln.cpp:1000-1013)
+static bool has_shared_substring(std::string_view read_seq, std::string_view ref_seq, int k) {
+    int sub_size = 2 * k / 3;
+    int step_size = k / 3;
+    for (size_t i = 0; i + sub_size < read_seq.size(); i += step_size) {
+        if (ref_seq.find(read_seq.substr(i, sub_size)) != std::string_view::npos) return true;
+    }
+    return false;
+}
+
+// rescue window (aln.cpp:1029-1042 / pc.cpp:255-272): the mixed int/size_t/float arithmetic is kept
+static void rescue_window(const Nam& nam, size_t read_len, float mu, float sigma, int ref_len_i, int& ref_start,
+                          int& ref_end) {
+    int a, b;
+    if (nam.is_rc) {
+        a = nam.ref_start - nam.query_start - (mu + 5 * sigma);
+        b = nam.ref_start - nam.query_start + read_len / 2;
+    } else {
+        a = nam.ref_end + (read_len - nam.query_end) - read_len / 2;
+        b = nam.ref_end + (read_len - nam.query_end) + (mu + 5 * sigma);
+    }
+    ref_start = std::max(0, std::min(a, ref_len_i));
+    ref_end = std::min(ref_len_i, std::max(0, b));
+}
+
+// rescue_mate_part (aln.cpp:1015-1076)
+static bool rescue_mate_part(AlignTmpRes& res, const Nam& nam, const References& refs, const Read& read, float mu,
+                             float sigma, int k) {
+    Alignment alignment;
+    const size_t read_len = read.size();
+    std::string_view r_tmp = nam.is_rc ? std::string_view(read.seq) : std::string_view(read.rc);
+    const int ref_len = (int)refs.seqs[nam.ref_id].size();
+    int ref_start, ref_end;
+    rescue_window(nam, read_len, mu, sigma, ref_len, ref_start, ref_end);
+    res.todo_nams.push_back(nam);
+    res.is_extend_seed.push_back(false);
+    auto unaligned = [&]() {
+        alignment.cigar = Cigar();
+        alignment.edit_distance = (int)read_len;
+        alignment.score = 0;
+        alignment.ref_start = 0;
+        alignment.is_rc = nam.is_rc;
+        alignment.ref_id = nam.ref_id;
+        alignment.is_unaligned = true;
+        res.done_align.push_back(true);
+        res.align_res.push_back(alignment);
+        return true;
+    };
+    if (ref_end < ref_start + k) return unaligned();
+    std::string_view segm = sub(refs.seqs[nam.ref_id], (size_t)ref_start, (size_t)(ref_end - ref_start));
+    if (!has_shared_substring(r_tmp, segm, k)) return unaligned();
+    res.done_align.push_back(false);
+    res.align_res.push_back(alignment);
+    return false;
+}
+
+// rescue_read_part (aln.cpp:1135-1176)
+static void rescue_read_part(int flag, AlignTmpRes& res, const Read& read2, const Read& read1, const MapContext& mc,
+                             std::vector<Nam>& nams1, Details det[2], int k, float mu, float sigma) {
+    res.type = flag;
+    const Nam n_max1 = nams1[0];
+    int tries = 0;
+    for (auto& nam : nams1) {
+        float score_dropoff1 = (float)nam.n_hits / n_max1.n_hits;
+        if (tries >= mc.mparams.max_tries || score_dropoff1 < mc.mparams.dropoff_threshold) break;
+        const bool consistent = reverse_nam_if_needed(nam, read1, mc.refs, k);
+        det[0].nam_inconsistent += !consistent;
+        res.is_read1.push_back(flag == 1);
+        bool gapped = extend_seed_part(res, mc.aparams, nam, mc.refs, read1, consistent);
+        det[0].gapped += gapped;
+        det[0].tried_alignment++;
+        res.is_read1.push_back(flag != 1);
+        (void)rescue_mate_part(res, nam, mc.refs, read2, mu, sigma, k);
+        tries++;
+    }
+}
+
+// align_PE_part (aln.cpp:1372-1580)
+static void align_PE_part(AlignTmpRes& res, const MapContext& mc, std::vector<Nam>& nams1, std::vector<Nam>& nams2,
+                          const Record& r1, const Record& r2, int k, Details det[2], InsertSizeDistribution& isize) {
+    const float mu = isize.mu, sigma = isize.sigma;
+    Read read1(r1.seq), read2(r2.seq);
+    const float dropoff = mc.mparams.dropoff_threshold;
+    const unsigned max_tries = (unsigned)mc.mparams.max_tries;
+    if (nams1.empty() && nams2.empty()) { res.type = 0; return; }
+    if (!nams1.empty() && nams2.empty()) {
+        rescue_read_part(1, res, read2, read1, mc, nams1, det, k, mu, sigma);
+        return;
+    }
+    if (nams1.empty() && !nams2.empty()) {
+        rescue_read_part(2, res, read1, read2, mc, nams2, det, k, mu, sigma);   // details unswapped (sic)
+        return;
+    }
+    if (top_dropoff(nams1) < dropoff && top_dropoff(nams2) < dropoff && is_proper_nam_pair(nams1[0], nams2[0], mu, sigma)) {
+        res.type = 3;
+        Nam n_max1 = nams1[0], n_max2 = nams2[0];
+        bool c1 = reverse_nam_if_needed(n_max1, read1, mc.refs, k);
+        det[0].nam_inconsistent += !c1;
+        bool c2 = reverse_nam_if_needed(n_max2, read2, mc.refs, k);
+        det[1].nam_inconsistent += !c2;
+        res.is_read1.push_back(true);
+        bool g1 = extend_seed_part(res, mc.aparams, n_max1, mc.refs, read1, c1);
+        det[0].tried_alignment++;
+        det[0].gapped += g1;
+        res.is_read1.push_back(false);
+        bool g2 = extend_seed_part(res, mc.aparams, n_max2, mc.refs, read2, c2);
+        det[1].tried_alignment++;
+        det[1].gapped += g2;
+        res.mapq1 = get_mapq(nams1, n_max1);
+        res.mapq2 = get_mapq(nams2, n_max2);
+        if (!g1 && !g2) {
+            const size_t n = res.align_res.size();
+            const Alignment& a1 = res.align_res[n - 2];
+            const Alignment& a2 = res.align_res[n - 1];
+            bool proper = is_proper_pair(a1, a2, mu, sigma);
+            if ((isize.sample_size < 400) && (a1.edit_distance + a2.edit_distance < 3) && proper)
+                isize.update(std::abs(a1.ref_start - a2.ref_start));
+        }
+        return;
+    }
+    res.type = 4;
+    std::vector<NamPair> joint = get_best_scoring_nam_pairs(nams1, nams2, mu, sigma);
+    std::unordered_set<int> aligned1, aligned2;
+    {
+        Nam n1 = nams1[0];
+        bool c1 = reverse_nam_if_needed(n1, read1, mc.refs, k);
+        det[0].nam_inconsistent += !c1;
+        res.is_read1.push_back(true);
+        bool g1 = extend_seed_part(res, mc.aparams, n1, mc.refs, read1, c1);
+        aligned1.insert(n1.nam_id);
+        det[0].tried_alignment++;
+        det[0].gapped += g1;
+        Nam n2 = nams2[0];
+        bool c2 = reverse_nam_if_needed(n2, read2, mc.refs, k);
+        det[1].nam_inconsistent += !c2;
+        res.is_read1.push_back(false);
+        bool g2 = extend_seed_part(res, mc.aparams, n2, mc.refs, read2, c2);
+        aligned2.insert(n2.nam_id);
+        det[1].tried_alignment++;
+        det[1].gapped += g2;
+    }
+    const int max_score = joint[0].score;
+    res.type4_loop_size = 0;
+    size_t n_high = 0;
+    for (auto& jp : joint) {
+        Nam& n1 = jp.nam1;
+        Nam& n2 = jp.nam2;
+        float score_dropoff = (float)jp.score / max_score;
+        if (n_high >= max_tries || score_dropoff < dropoff) break;
+        res.type4_nams.push_back(n1);
+        res.type4_nams.push_back(n2);
+        res.type4_loop_size++;
+        if (n1.ref_start >= 0) {
+            if (!aligned1.count(n1.nam_id)) {
+                bool c = reverse_nam_if_needed(n1, read1, mc.refs, k);
+                det[0].nam_inconsistent += !c;
+                res.is_read1.push_back(true);
+                bool g = extend_seed_part(res, mc.aparams, n1, mc.refs, read1, c);
+                aligned1.insert(n1.nam_id);
+                det[0].tried_alignment++;
+                det[0].gapped += g;
+            }
+        } else {
+            det[1].nam_inconsistent += !reverse_nam_if_needed(n2, read2, mc.refs, k);
+            res.is_read1.push_back(true);
+            (void)rescue_mate_part(res, n2, mc.refs, read1, mu, sigma, k);
+            det[0].tried_alignment++;
+        }
+        if (n2.ref_start >= 0) {
+            if (!aligned2.count(n2.nam_id)) {
+                bool c = reverse_nam_if_needed(n2, read2, mc.refs, k);
+                det[1].nam_inconsistent += !c;
+                res.is_read1.push_back(false);
+                bool g = extend_seed_part(res, mc.aparams, n2, mc.refs, read2, c);
+                aligned2.insert(n2.nam_id);
+                det[1].tried_alignment++;
+                det[1].gapped += g;
+            }
+        } else {
+            det[0].nam_inconsistent += !reverse_nam_if_needed(n1, read1, mc.refs, k);
+            res.is_read1.push_back(false);
+            (void)rescue_mate_part(res, n1, mc.refs, read2, mu, sigma, k);
+            det[1].tried_alignment++;
+        }
+        n_high++;
+    }
+}
+
+// align_PE_read_part (aln.cpp:1927-1981); the find_nams/rescue results come from the engine
+void align_PE_read_part(AlignTmpRes& res, const Record& r1, const Record& r2, std::vector<Nam> nams[2],
+                        const bool rescued[2], AlignmentStatistics& stats, InsertSizeDistribution& isize,
+                        const MapContext& mc, std::minstd_rand& rng) {
+    Details det[2];
+    for (int m = 0; m < 2; ++m) {
+        if (mc.mparams.rescue_level > 1 && rescued[m]) det[m].nam_rescue = true;
+        det[m].nams = nams[m].size();
+        std::sort(nams[m].begin(), nams[m].end(), by_score<Nam>);
+        shuffle_top_nams(nams[m], rng);
+    }
+    align_PE_part(res, mc, nams[0], nams[1], r1, r2, mc.iparams.k, det, isize);
+    stats.add(det[0]);
+    stats.add(det[1]);
+}
+
+// align_SE_part (aln.cpp:95-124)
+void align_SE_read_part(AlignTmpRes& res, const Record& r, std::vector<Nam>& nams, bool rescued,
+                        AlignmentStatistics& stats, const MapContext& mc, std::minstd_rand& rng) {
+    Details det;
+    if (mc.mparams.rescue_level > 1 && rescued) det.nam_rescue = true;
+    det.nams = nams.size();
+    std::sort(nams.begin(), nams.end(), by_score<Nam>);
+    shuffle_top_nams(nams, rng);
+    if (nams.empty()) {
+        res.type = 0;
+    } else {
+        Read read(r.seq);
+        int tries = 0;
+        const Nam n_max = nams[0];
+        res.type = 4;
+        for (auto& nam : nams) {
+            float score_dropoff = (float)nam.n_hits / n_max.n_hits;
+            if (tries >= mc.mparams.max_tries || score_dropoff < mc.mparams.dropoff_threshold) break;
+            bool consistent = reverse_nam_if_needed(nam, read, mc.refs, mc.iparams.k);
+            res.consistent_nam.push_back(consistent);
+            res.is_read1.push_back(true);
+            (void)extend_seed_part(res, mc.aparams, nam, mc.refs, read, consistent);
+            tries++;
+        }
+    }
+    stats.add(det);
+}
+
+// ------------------------------------------------------ SW job strings ---
+// part2_extend_seed_get_str (pc.cpp:214-242)
+static void extend_job(const Nam& nam, const Read& read, const References& refs, std::vector<SwJob>& jobs) {
+    std::string_view query = nam.is_rc ? std::string_view(read.rc) : std::string_view(read.seq);
+    const std::string& ref = refs.seqs[nam.ref_id];
+    const auto projected_ref_start = std::max(0, nam.ref_start - nam.query_start);
+    const int diff = std::abs((nam.ref_end - nam.ref_start) - (nam.query_end - nam.query_start));
+    const int ext_left = std::min(50, projected_ref_start);
+    const int ref_start = projected_ref_start - ext_left;
+    const int ext_right = (int)std::min(std::size_t(50), ref.size() - nam.ref_end);
+    const size_t ref_segm_size = read.size() + diff + ext_left + ext_right;
+    const size_t len = std::min(ref_segm_size, ref.size() - (size_t)ref_start);
+    jobs.push_back(SwJob{std::string(query), nam.ref_id, (uint32_t)ref_start, (uint32_t)len});
+}
+
+// part2_rescue_mate_get_str (pc.cpp:333-368)
+static void rescue_job(const Nam& nam, const Read& read, const References& refs, float mu, float sigma,
+                       std::vector<SwJob>& jobs) {
+    std::string_view r_tmp = nam.is_rc ? std::string_view(read.seq) : std::string_view(read.rc);
+    int ref_start, ref_end;
+    rescue_window(nam, read.size(), mu, sigma, (int)refs.seqs[nam.ref_id].size(), ref_start, ref_end);
+    const size_t clen = refs.seqs[nam.ref_id].size();
+    size_t start = std::min((size_t)ref_start, clen);
+    size_t len = std::min((size_t)(ref_end - ref_start), clen - start);
+    jobs.push_back(SwJob{std::string(r_tmp), nam.ref_id, (uint32_t)start, (uint32_t)len});
+}
+
+void collect_jobs_pe(AlignTmpRes& res, const Record&, const Record&, const Read& read1, const Read& read2,
+                     const MapContext& mc, float mu, float sigma, std::vector<SwJob>& jobs) {
+    const size_t n = res.todo_nams.size();
+    auto rd = [&](size_t j) -> const Read& { return res.is_read1[j] ? read1 : read2; };
+    if (res.type == 1 || res.type == 2) {
+        for (size_t j = 0; j < n; j += 2) {
+            if (!res.done_align[j]) extend_job(res.todo_nams[j], rd(j), mc.refs, jobs);
+            if (!res.done_align[j + 1]) rescue_job(res.todo_nams[j + 1], rd(j + 1), mc.refs, mu, sigma, jobs);
+        }
+    } else if (res.type == 3) {
+        if (!res.done_align[0]) extend_job(res.todo_nams[0], rd(0), mc.refs, jobs);
+        if (!res.done_align[1]) extend_job(res.todo_nams[1], rd(1), mc.refs, jobs);
+    } else if (res.type == 4) {
+        for (size_t j = 0; j < n; ++j) {
+            if (res.done_align[j]) continue;
+            if (res.is_extend_seed[j]) extend_job(res.todo_nams[j], rd(j), mc.refs, jobs);
+            else rescue_job(res.todo_nams[j], rd(j), mc.refs, mu, sigma, jobs);
+        }
+    }
+}
+
+// part2_extend_seed_store_res (pc.cpp:177-212)
+static void store_extend(AlignTmpRes& res, size_t j, const Read& read, const References& refs,
+                         const AlignmentInfo& info) {
+    const Nam& nam = res.todo_nams[j];
+    const std::string& ref = refs.seqs[nam.ref_id];
+    const size_t qsize = read.size();
+    const auto projected_ref_start = std::max(0, nam.ref_start - nam.query_start);
+    const int ext_left = std::min(50, projected_ref_start);
+    const int ref_start = projected_ref_start - ext_left;
+    (void)ref;
+    int result_ref_start = ref_start + (int)info.ref_start;
+    int softclipped = (int)info.query_start + ((int)qsize - (int)info.query_end);
+    Alignment& a = res.align_res[j];
+    a.cigar = info.cigar;
+    a.edit_distance = (int)info.edit_distance;
+    a.global_ed = (int)info.edit_distance + softclipped;
+    a.score = info.sw_score;
+    a.ref_start = result_ref_start;
+    a.length = info.ref_span();
+    a.is_rc = nam.is_rc;
+    a.is_unaligned = false;
+    a.ref_id = nam.ref_id;
+    a.gapped = true;
+}
+
+// part2_rescue_mate_store_res (pc.cpp:291-331)
+static void store_rescue(AlignTmpRes& res, size_t j, const Read& read, const References& refs, float mu, float sigma,
+                         const AlignmentInfo& info) {
+    const Nam& nam = res.todo_nams[j];
+    int ref_start, ref_end;
+    rescue_window(nam, read.size(), mu, sigma, (int)refs.seqs[nam.ref_id].size(), ref_start, ref_end);
+    Alignment& a = res.align_res[j];
+    a.cigar = info.cigar;
+    a.edit_distance = (int)info.edit_distance;
+    a.score = info.sw_score;
+    a.ref_start = ref_start + (int)info.ref_start;
+    a.is_rc = !nam.is_rc;
+    a.ref_id = nam.ref_id;
+    a.is_unaligned = info.cigar.empty();
+    a.length = info.ref_span();
+}
+
+size_t store_results_pe(AlignTmpRes& res, const Read& read1, const Read& read2, const MapContext& mc, float mu,
+                        float sigma, const std::vector<AlignmentInfo>& infos, size_t pos) {
+    const size_t n = res.todo_nams.size();
+    auto rd = [&](size_t j) -> const Read& { return res.is_read1[j] ? read1 : read2; };
+    if (res.type == 1 || res.type == 2) {
+        for (size_t j = 0; j < n; j += 2) {
+            if (!res.done_align[j]) store_extend(res, j, rd(j), mc.refs, infos[pos++]);
+            if (!res.done_align[j + 1]) store_rescue(res, j + 1, rd(j + 1), mc.refs, mu, sigma, infos[pos++]);
+        }
+    } else if (res.type == 3) {
+        if (!res.done_align[0]) store_extend(res, 0, rd(0), mc.refs, infos[pos++]);
+        if (!res.done_align[1]) store_extend(res, 1, rd(1), mc.refs, infos[pos++]);
+    } else if (res.type == 4) {
+        for (size_t j = 0; j < n; ++j) {
+            if (res.done_align[j]) continue;
+            if (res.is_extend_seed[j]) store_extend(res, j, rd(j), mc.refs, infos[pos++]);
+            else store_rescue(res, j, rd(j), mc.refs, mu, sigma, infos[pos++]);
+        }
+    }
+    return pos;
+}
+
+void collect_jobs_se(AlignTmpRes& res, const Read& read, const MapContext& mc, std::vector<SwJob>& jobs) {
+    if (res.type != 4) return;
+    for (size_t j = 0; j < res.todo_nams.size(); ++j)
+        if (!res.done_align[j] && res.is_extend_seed[j]) extend_job(res.todo_nams[j], read, mc.refs, jobs);
+}
+
+size_t store_results_se(AlignTmpRes& res, const Read& read, const MapContext& mc,
+                        const std::vector<AlignmentInfo>& infos, size_t pos) {
+    if (res.type != 4) return pos;
+    for (size_t j = 0; j < res.todo_nams.size(); ++j)
+        if (!res.done_align[j] && res.is_extend_seed[j]) store_extend(res, j, read, mc.refs, infos[pos++]);
+    return pos;
+}
+
+// -------------------------------------------------------------- last ---
+struct ScoredAlignmentPair { double score; Alignment alignment1; Alignment alignment2; };
+
+static inline float normal_pdf(float x, float mu, float sigma) {   // aln.cpp:528-533
+    static const float inv_sqrt_2pi = 0.3989422804014327;
+    const float a = (x - mu) / sigma;
+    return inv_sqrt_2pi / sigma * std::exp(-0.5f * a * a);
+}
+
+// aln.cpp:535-550
+static std::vector<ScoredAlignmentPair> get_best_scoring_pairs(const std::vector<Alignment>& al1,
+                                                               const std::vector<Alignment>& al2, float mu, float sigma) {
+    std::vector<ScoredAlignmentPair> pairs;
+    for (auto& a1 : al1) {
+        for (auto& a2 : al2) {
+            float dist = std::abs(a1.ref_start - a2.ref_start);
+            double score = a1.score + a2.score;
+            if ((a1.is_rc ^ a2.is_rc) && (dist < mu + 4 * sigma)) score += log(normal_pdf(dist, mu, sigma));
+            else score -= 10;
+            pairs.push_back(ScoredAlignmentPair{score, a1, a2});
+        }
+    }
+    return pairs;
+}
+
+static std::pair<int, int> joint_mapq_from_high_scores(const std::vector<ScoredAlignmentPair>& pairs) {  // aln.cpp:506-526
+    if (pairs.size() <= 1) return {60, 60};
+    auto score1 = pairs[0].score;
+    auto score2 = pairs[1].score;
+    if (score1 == score2) return {0, 0};
+    int mapq;
+    const int diff = score1 - score2;
+    if (score1 > 0 && score2 > 0) mapq = std::min(60, diff);
+    else if (score1 > 0 && score2 <= 0) mapq = 60;
+    else mapq = 1;
+    return {mapq, mapq};
+}
+
+static void deduplicate_scored_pairs(std::vector<ScoredAlignmentPair>& pairs) {   // aln.cpp:1082-1105
+    int p1 = pairs[0].alignment1.ref_start, p2 = pairs[0].alignment2.ref_start;
+    int i1 = pairs[0].alignment1.ref_id, i2 = pairs[0].alignment2.ref_id;
+    size_t j = 1;
+    for (size_t i = 1; i < pairs.size(); i++) {
+        int s1 = pairs[i].alignment1.ref_start, s2 = pairs[i].alignment2.ref_start;
+        int d1 = pairs[i].alignment1.ref_id, d2 = pairs[i].alignment2.ref_id;
+        if (s1 != p1 || s2 != p2 || d1 != i1 || d2 != i2) {
+            p1 = s1; p2 = s2; i1 = d1; i2 = d2;
+            pairs[j] = pairs[i];
+            j++;
+        }
+    }
+    pairs.resize(j);
+}
+
+static void pick_random_top_pair(std::vector<ScoredAlignmentPair>& hs, std::minstd_rand& rng) {   // aln.cpp:1111-1127
+    size_t i = 1;
+    for (; i < hs.size(); ++i)
+        if (hs[i].score != hs[0].score) break;
+    if (i > 1) {
+        size_t ri = std::uniform_int_distribution<>(0, i - 1)(rng);
+        if (ri != 0) std::swap(hs[0], hs[ri]);
+    }
+}
+
+// rescue_read_last (aln.cpp:1983-2081)
+static void rescue_read_last(AlignTmpRes& res, const Read& read2, const Read& read1, const MapContext& mc,
+                             Details det[2], float mu, float sigma, Sam& sam, const Record& rec1, const Record& rec2,
+                             bool swap_r1r2, std::minstd_rand& rng) {
+    std::vector<Alignment> al1, al2;
+    const size_t n = res.todo_nams.size();
+    for (size_t i = 0; i < n; i += 2) {
+        al1.push_back(res.align_res[i]);
+        al2.push_back(res.align_res[i + 1]);
+        det[1].mate_rescue += !res.align_res[i + 1].is_unaligned;
+    }
+    std::sort(al1.begin(), al1.end(), by_score<Alignment>);
+    std::sort(al2.begin(), al2.end(), by_score<Alignment>);
+    auto hs = get_best_scoring_pairs(al1, al2, mu, sigma);
+    std::sort(hs.begin(), hs.end(), by_score<ScoredAlignmentPair>);
+    deduplicate_scored_pairs(hs);
+    pick_random_top_pair(hs, rng);
+    auto [mapq1, mapq2] = joint_mapq_from_high_scores(hs);
+    const double secondary_dropoff = 2 * mc.aparams.mismatch + mc.aparams.gap_open;
+    if (mc.mparams.max_secondary == 0) {
+        const Alignment& a1 = hs[0].alignment1;
+        const Alignment& a2 = hs[0].alignment2;
+        if (swap_r1r2) sam.add_pair(a2, a1, rec2, rec1, read2.rc, read1.rc, mapq2, mapq1, is_proper_pair(a2, a1, mu, sigma), true, det);
+        else sam.add_pair(a1, a2, rec1, rec2, read1.rc, read2.rc, mapq1, mapq2, is_proper_pair(a1, a2, mu, sigma), true, det);
+    } else {
+        auto max_out = std::min(hs.size(), (size_t)mc.mparams.max_secondary);
+        bool is_primary = true;
+        auto s_max = hs[0].score;
+        for (size_t i = 0; i < max_out; ++i) {
+            if (i > 0) { is_primary = false; mapq1 = 0; mapq2 = 0; }
+            const auto& ap = hs[i];
+            if (s_max - ap.score < secondary_dropoff) {
+                if (swap_r1r2) {
+                    bool proper = is_proper_pair(ap.alignment2, ap.alignment1, mu, sigma);
+                    Details sw[2] = {det[1], det[0]};
+                    sam.add_pair(ap.alignment2, ap.alignment1, rec2, rec1, read2.rc, read1.rc, mapq2, mapq1, proper, is_primary, sw);
+                } else {
+                    bool proper = is_proper_pair(ap.alignment1, ap.alignment2, mu, sigma);
+                    sam.add_pair(ap.alignment1, ap.alignment2, rec1, rec2, read1.rc, read2.rc, mapq1, mapq2, proper, is_primary, det);
+                }
+            } else break;
+        }
+    }
+}
+
+// align_PE_read_last (aln.cpp:2083-2306)
+void align_PE_read_last(AlignTmpRes& res, const Record& rec1, const Record& rec2, Sam& sam,
+                        AlignmentStatistics& stats, const InsertSizeDistribution& isize, const MapContext& mc,
+                        std::minstd_rand& rng) {
+    Details det[2];
+    const float mu = isize.mu, sigma = isize.sigma;
+    Read read1(rec1.seq), read2(rec2.seq);
+    if (res.type == 0) {
+        sam.add_unmapped_pair(rec1, rec2);
+    } else if (res.type == 1) {
+        rescue_read_last(res, read2, read1, mc, det, mu, sigma, sam, rec1, rec2, false, rng);
+    } else if (res.type == 2) {
+        rescue_read_last(res, read1, read2, mc, det, mu, sigma, sam, rec2, rec1, true, rng);   // details unswapped (sic)
+    } else if (res.type == 3) {
+        const Alignment& a1 = res.align_res[0];
+        const Alignment& a2 = res.align_res[1];
+        bool proper = is_proper_pair(a1, a2, mu, sigma);
+        sam.add_pair(a1, a2, rec1, rec2, read1.rc, read2.rc, (uint8_t)res.mapq1, (uint8_t)res.mapq2, proper, true, det);
+    } else if (res.type == 4) {
+        size_t pos = 0;
+        std::vector<std::pair<int, Alignment>> cache1, cache2;   // nam_id -> alignment (small; linear lookup)
+        auto find_c = [](std::vector<std::pair<int, Alignment>>& c, int id) -> Alignment* {
+            for (auto& x : c) if (x.first == id) return &x.second;
+            return nullptr;
+        };
+        Alignment a1_indv_max = res.align_res[pos];
+        cache1.push_back({res.todo_nams[pos].nam_id, a1_indv_max});
+        pos++;
+        Alignment a2_indv_max = res.align_res[pos];
+        cache2.push_back({res.todo_nams[pos].nam_id, a2_indv_max});
+        pos++;
+        std::vector<ScoredAlignmentPair> hs;
+        for (int i = 0; i < res.type4_loop_size; ++i) {
+            const Nam& n1 = res.type4_nams[2 * i];
+            const Nam& n2 = res.type4_nams[2 * i + 1];
+            Alignment a1, a2;
+            if (n1.ref_start >= 0) {
+                Alignment* c = find_c(cache1, n1.nam_id);
+                if (c) a1 = *c;
+                else { a1 = res.align_res[pos]; pos++; cache1.push_back({n1.nam_id, a1}); }
+            } else {
+                a1 = res.align_res[pos]; pos++;
+                det[0].mate_rescue += !a1.is_unaligned;
+            }
+            if (a1.score > a1_indv_max.score) a1_indv_max = a1;
+            if (n2.ref_start >= 0) {
+                Alignment* c = find_c(cache2, n2.nam_id);
+                if (c) a2 = *c;
+                else { a2 = res.align_res[pos]; pos++; cache2.push_back({n2.nam_id, a2}); }
+            } else {
+                a2 = res.align_res[pos]; pos++;
+                det[1].mate_rescue += !a2.is_unaligned;
+            }
+            if (a2.score > a2_indv_max.score) a2_indv_max = a2;
+            bool r1_r2 = a2.is_rc && (a1.ref_start <= a2.ref_start) && ((a2.ref_start - a1.ref_start) < mu + 10 * sigma);
+            bool r2_r1 = a1.is_rc && (a2.ref_start <= a1.ref_start) && ((a1.ref_start - a2.ref_start) < mu + 10 * sigma);
+            double combined;
+            if (r1_r2 || r2_r1) {
+                float x = std::abs(a1.ref_start - a2.ref_start);
+                combined = (double)a1.score + (double)a2.score + std::max(-20.0f + 0.001f, log(normal_pdf(x, mu, sigma)));
+            } else {
+                combined = (double)a1.score + (double)a2.score - 20;
+            }
+            hs.push_back(ScoredAlignmentPair{combined, std::move(a1), std::move(a2)});
+        }
+        double combined = (double)a1_indv_max.score + (double)a2_indv_max.score - 20;
+        hs.push_back(ScoredAlignmentPair{combined, a1_indv_max, a2_indv_max});
+        std::sort(hs.begin(), hs.end(), by_score<ScoredAlignmentPair>);
+        deduplicate_scored_pairs(hs);
+        pick_random_top_pair(hs, rng);
+        auto [mapq1, mapq2] = joint_mapq_from_high_scores(hs);
+        const auto& best = hs[0];
+        if (mc.mparams.max_secondary == 0) {
+            bool proper = is_proper_pair(best.alignment1, best.alignment2, mu, sigma);
+            sam.add_pair(best.alignment1, best.alignment2, rec1, rec2, read1.rc, read2.rc, mapq1, mapq2, proper, true, det);
+        } else {
+            auto max_out = std::min(hs.size(), (size_t)mc.mparams.max_secondary);
+            float s_max = best.score;
+            bool is_primary = true;
+            const double sd = 2 * mc.aparams.mismatch + mc.aparams.gap_open;
+            for (size_t i = 0; i < max_out; ++i) {
+                const auto& ap = hs[i];
+                float s_score = ap.score;
+                if (i > 0) { is_primary = false; mapq1 = 255; mapq2 = 255; }
+                if (s_max - s_score < sd) {
+                    bool proper = is_proper_pair(ap.alignment1, ap.alignment2, mu, sigma);
+                    sam.add_pair(ap.alignment1, ap.alignment2, rec1, rec2, read1.rc, read2.rc, mapq1, mapq2, proper, is_primary, det);
+                } else break;
+            }
+        }
+    }
+    stats.add(det[0]);
+    stats.add(det[1]);
+}
+
+// align_SE_read_last (aln.cpp:126-238)
+void align_SE_read_last(AlignTmpRes& res, const Record& rec, Sam& sam, AlignmentStatistics& stats,
+                        const MapContext& mc, std::minstd_rand& rng) {
+    Details det;
+    if (res.type == 0) {
+        sam.add_unmapped(rec);
+        return;
+    }
+    Read read(rec.seq);
+    std::vector<Alignment> alignments;
+    int tries = 0;
+    const Nam n_max = res.todo_nams[0];
+    int best_edit_distance = INT_MAX, best_score = 0, second_best_score = 0, alignments_with_best_score = 0;
+    size_t best_index = 0;
+    Alignment best_alignment;
+    best_alignment.is_unaligned = true;
+    const int max_secondary = mc.mparams.max_secondary;
+    for (size_t i = 0; i < res.todo_nams.size(); i++) {
+        const Nam& nam = res.todo_nams[i];
+        float score_dropoff = (float)nam.n_hits / n_max.n_hits;
+        if (tries >= mc.mparams.max_tries || (tries > 1 && best_edit_distance == 0) ||
+            score_dropoff < mc.mparams.dropoff_threshold) {
+            for (size_t j = i; j < res.todo_nams.size(); j++)
+                if (!res.done_align[j]) stats.tot_aligner_calls--;
+            break;
+        }
+        bool consistent = res.consistent_nam[i];
+        det.nam_inconsistent += !consistent;
+        Alignment alignment = res.align_res[i];
+        det.tried_alignment++;
+        det.gapped += alignment.gapped;
+        if (max_secondary > 0) alignments.emplace_back(alignment);
+        if (alignment.score >= best_score) {
+            second_best_score = best_score;
+            bool update_best = false;
+            if (alignment.score > best_score) {
+                alignments_with_best_score = 1;
+                update_best = true;
+            } else {
+                alignments_with_best_score++;
+                std::uniform_int_distribution<> distrib(1, alignments_with_best_score);
+                if (distrib(rng) == 1) update_best = true;
+            }
+            if (update_best) {
+                best_score = alignment.score;
+                best_alignment = std::move(alignment);
+                best_index = (size_t)tries;
+                if (max_secondary == 0) best_edit_distance = best_alignment.global_ed;
+            }
+        } else if (alignment.score > second_best_score) {
+            second_best_score = alignment.score;
+        }
+        tries++;
+    }
+    // (60.0 * (best - second) + best - 1) / best as a double -> uint8_t (x86: via int32 truncation)
+    const double mq = (60.0 * (best_score - second_best_score) + best_score - 1) / best_score;
+    int32_t mq32 = (std::isnan(mq) || mq >= 2147483648.0 || mq < -2147483648.0) ? INT32_MIN : (int32_t)mq;
+    uint8_t mapq = (uint8_t)mq32;
+    sam.add(best_alignment, rec, read.rc, mapq, true, det);
+    if (max_secondary == 0) {
+        stats.add(det);
+        return;
+    }
+    if (alignments.size() > 1) std::swap(alignments[best_index], alignments[alignments.size() - 1]);
+    alignments.resize(alignments.size() - 1);
+    std::sort(alignments.begin(), alignments.end(), [](const Alignment& a, const Alignment& b) { return a.score > b.score; });
+    size_t n = 0;
+    for (const auto& a : alignments) {
+        if (n >= (size_t)max_secondary || a.score - best_score > 2 * mc.aparams.mismatch + mc.aparams.gap_open) break;
+        sam.add(a, rec, read.rc, mapq, false, det);
+        n++;
+    }
+    stats.add(det);
+}
+
+}  // namespace rsa

@@ -1,0 +1,607 @@
+// io.cpp -- CIGAR text, SAM records, FASTA, .sti read/write/build, FASTQ input.
+// Restated from src/cigar.cpp, src/sam.cpp, src/refs.cpp, src/index.cpp,
+// src/indexparameters.cpp and the kseq++ record semantics used by src/fastq.cpp.
+#include <zlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <stdexcept>
+#include <thread>
+
+#include "rsa_host.hpp"
+
+namespace rsa {
+
+// ----------------------------------------------------------------- CIGAR --
+Cigar Cigar::to_m() const {                        // cigar.cpp:6-18
+    Cigar c;
+    for (uint32_t x : ops) {
+        uint32_t op = x & 0xf, len = x >> 4;
+        if (op == C_EQ || op == C_X) c.push(C_M, len);
+        else c.push(op, len);
+    }
+    return c;
+}
+
+static inline void append_uint(std::string& out, uint64_t v) {
+    char buf[24];
+    int n = 0;
+    do { buf[n++] = (char)('0' + v % 10); v /= 10; } while (v);
+    while (n) out.push_back(buf[--n]);
+}
+
+static inline void append_int(std::string& out, int64_t v) {
+    if (v < 0) { out.push_back('-'); append_uint(out, (uint64_t)(-v)); }
+    else append_uint(out, (uint64_t)v);
+}
+
+void Cigar::to_string(std::string& out) const {    // cigar.cpp:45-51
+    for (uint32_t x : ops) {
+        append_uint(out, x >> 4);
+        out.push_back("MIDNSHP=X"[x & 0xf]);
+    }
+}
+
+// ------------------------------------------------------------------- SAM --
+static std::string_view strip_suffix(const std::string& name) {   // sam.cpp:29-40
+    size_t len = name.size();
+    if (len >= 2 && name[len - 2] == '/' && (name[len - 1] == '1' || name[len - 1] == '2'))
+        return std::string_view(name).substr(0, len - 2);
+    return name;
+}
+
+Sam::Sam(std::string& out, const References& refs, bool eqx, const std::string& rg_id, bool output_unmapped,
+         bool details)
+    : out_(out), refs_(refs), eqx_(eqx), output_unmapped_(output_unmapped), details_(details) {
+    tail_ = rg_id.empty() ? "\n" : "\tRG:Z:" + rg_id + "\n";
+}
+
+static void append_details(std::string& out, const Details& d, bool paired) {   // sam.cpp:46-60
+    out += "\tna:i:"; append_uint(out, d.nams);
+    out += "\tnr:i:"; append_uint(out, d.nam_rescue ? 1 : 0);
+    out += "\tal:i:"; append_uint(out, d.tried_alignment);
+    out += "\tga:i:"; append_uint(out, d.gapped);
+    if (paired) { out += "\tmr:i:"; append_uint(out, d.mate_rescue); }
+}
+
+void Sam::add_unmapped(const Record& r, uint16_t flags) {   // sam.cpp:77-92
+    if (!output_unmapped_) return;
+    out_.append(strip_suffix(r.name));
+    out_ += '\t';
+    append_uint(out_, flags);
+    out_ += "\t*\t0\t0\t*\t*\t0\t0\t";
+    out_.append(r.seq.empty() ? "*" : r.seq);
+    out_ += '\t';
+    out_.append(r.qual.empty() ? "*" : r.qual);
+    out_ += tail_;
+}
+
+void Sam::add_unmapped_mate(const Record& r, uint16_t flags, const std::string& mate_ref, uint32_t mate_pos) {
+    out_.append(strip_suffix(r.name));                       // sam.cpp:94-116
+    out_ += '\t';
+    append_uint(out_, flags);
+    out_ += '\t';
+    out_ += mate_ref;
+    out_ += '\t';
+    append_uint(out_, (uint32_t)(mate_pos + 1));
+    out_ += "\t0\t*\t=\t";
+    append_uint(out_, (uint32_t)(mate_pos + 1));
+    out_ += "\t0\t";
+    out_.append(r.seq.empty() ? "*" : r.seq);
+    out_ += '\t';
+    out_.append(r.qual.empty() ? "*" : r.qual);
+    out_ += tail_;
+}
+
+void Sam::add_unmapped_pair(const Record& r1, const Record& r2) {
+    add_unmapped(r1, 1 | 4 | 8 | 0x40);
+    add_unmapped(r2, 1 | 4 | 8 | 0x80);
+}
+
+void Sam::add(const Alignment& a, const Record& r, const std::string& rc, uint8_t mapq, bool primary,
+              const Details& d) {                               // sam.cpp:124-139
+    int flags = 0;
+    if (!a.is_unaligned && a.is_rc) flags |= 0x10;
+    if (!primary) { flags |= 0x100; mapq = 255; }
+    add_record(r.name, (uint16_t)flags, refs_.names[a.ref_id], (uint32_t)a.ref_start, mapq, a.cigar, "*",
+               (uint32_t)-1, 0, r.seq, rc, r.qual, a.edit_distance, a.score, d);
+}
+
+void Sam::add_record(const std::string& qname, uint16_t flags, const std::string& rname, uint32_t pos, uint8_t mapq,
+                     const Cigar& cigar, const std::string& mate_rname, uint32_t mate_pos, int32_t tlen,
+                     const std::string& seq, const std::string& seq_rc, const std::string& qual, int ed, int score,
+                     const Details& d) {                        // sam.cpp:141-213
+    std::string& o = out_;
+    o.append(strip_suffix(qname));
+    o += '\t';
+    append_uint(o, flags);
+    o += '\t';
+    o += rname;
+    o += '\t';
+    append_uint(o, (uint32_t)(pos + 1));
+    o += '\t';
+    append_uint(o, mapq);
+    o += '\t';
+    if (cigar.empty()) o += '*';
+    else if (eqx_) cigar.to_string(o);
+    else cigar.to_m().to_string(o);
+    o += '\t';
+    o += mate_rname;
+    o += '\t';
+    append_uint(o, (uint32_t)(mate_pos + 1));
+    o += '\t';
+    append_int(o, tlen);
+    o += '\t';
+    if (flags & 0x100) o += '*';
+    else if (flags & 0x10) o.append(seq_rc.empty() ? "*" : seq_rc);
+    else o.append(seq.empty() ? "*" : seq);
+    if (!(flags & 4)) {
+        o += '\t';
+        if (flags & 0x100) o += '*';
+        else if (flags & 0x10) {
+            if (qual.empty()) o += '*';
+            else o.append(qual.rbegin(), qual.rend());
+        } else o.append(qual.empty() ? "*" : qual);
+        o += "\tNM:i:";
+        append_int(o, ed);
+        o += "\tAS:i:";
+        append_int(o, score);
+    } else {
+        o += '\t';
+        o.append(qual.empty() ? "*" : qual);
+    }
+    if (details_) append_details(o, d, flags & 1);
+    o += tail_;
+}
+
+void Sam::add_pair(const Alignment& a1, const Alignment& a2, const Record& r1, const Record& r2, const std::string& rc1,
+                   const std::string& rc2, uint8_t mapq1, uint8_t mapq2, bool proper, bool primary,
+                   const Details d[2]) {                        // sam.cpp:215-313
+    int f1 = 1 | 0x40, f2 = 1 | 0x80;
+    if (!primary) { f1 |= 0x100; f2 |= 0x100; }
+    int tlen1 = 0;
+    bool both = !a1.is_unaligned && !a2.is_unaligned;
+    if (both && a1.ref_id == a2.ref_id) {
+        const int dist = a2.ref_start - a1.ref_start;
+        if (dist > 0) tlen1 = dist + a2.length;
+        else tlen1 = dist - a1.length;
+    }
+    if (proper) { f1 |= 2; f2 |= 2; }
+    std::string rn1, rn2;
+    int pos1 = a1.ref_start, pos2 = a2.ref_start;
+    if (a1.is_unaligned) { f1 |= 4; f2 |= 8; pos1 = -1; rn1 = "*"; }
+    else { if (a1.is_rc) { f1 |= 0x10; f2 |= 0x20; } rn1 = refs_.names[a1.ref_id]; }
+    if (a2.is_unaligned) { f2 |= 4; f1 |= 8; pos2 = -1; rn2 = "*"; }
+    else { if (a2.is_rc) { f1 |= 0x20; f2 |= 0x10; } rn2 = refs_.names[a2.ref_id]; }
+    std::string mrn1 = rn1, mrn2 = rn2;
+    if ((both && a1.ref_id == a2.ref_id) || (a1.is_unaligned != a2.is_unaligned)) { mrn1 = "="; mrn2 = "="; }
+    if (a1.is_unaligned != a2.is_unaligned) {
+        if (a1.is_unaligned) pos1 = pos2; else pos2 = pos1;
+    }
+    if (a1.is_unaligned) add_unmapped_mate(r1, (uint16_t)f1, rn2, (uint32_t)pos2);
+    else add_record(r1.name, (uint16_t)f1, rn1, (uint32_t)a1.ref_start, mapq1, a1.cigar, mrn2, (uint32_t)pos2, tlen1,
+                    r1.seq, rc1, r1.qual, a1.edit_distance, a1.score, d[0]);
+    if (a2.is_unaligned) add_unmapped_mate(r2, (uint16_t)f2, rn1, (uint32_t)pos1);
+    else add_record(r2.name, (uint16_t)f2, rn2, (uint32_t)a2.ref_start, mapq2, a2.cigar, mrn1, (uint32_t)pos1, -tlen1,
+                    r2.seq, rc2, r2.qual, a2.edit_distance, a2.score, d[1]);
+}
+
+bool is_proper_pair(const Alignment& a1, const Alignment& a2, float mu, float sigma) {   // sam.cpp:315-325
+    const int dist = a2.ref_start - a1.ref_start;
+    const bool same_reference = a1.ref_id == a2.ref_id;
+    const bool both_aligned = same_reference && !a1.is_unaligned && !a2.is_unaligned;
+    const bool r1_r2 = !a1.is_rc && a2.is_rc && dist >= 0;
+    const bool r2_r1 = !a2.is_rc && a1.is_rc && dist <= 0;
+    const bool rel_orientation_good = r1_r2 || r2_r1;
+    const bool insert_good = std::abs(dist) <= mu + 6 * sigma;
+    return both_aligned && insert_good && rel_orientation_good;
+}
+
+std::string sam_header(const References& refs, const std::string& rg_id, const std::vector<std::string>& rg,
+                       const std::string& cmd_line) {          // main.cpp:84-99
+    std::string o = "@HD\tVN:1.6\tSO:unsorted\n";
+    for (size_t i = 0; i < refs.size(); ++i) {
+        o += "@SQ\tSN:" + refs.names[i] + "\tLN:";
+        append_uint(o, (uint32_t)refs.seqs[i].size());
+        o += "\n";
+    }
+    if (!rg_id.empty()) {
+        o += "@RG\tID:" + rg_id;
+        for (const auto& f : rg) o += "\t" + f;
+        o += "\n";
+    }
+    o += "@PG\tID:rabbitsalign\tPN:rabbitsalign\tVN:0.1.0-mi355x\tCL:" + cmd_line + "\n";
+    return o;
+}
+
+// ----------------------------------------------------------------- FASTA --
+References References::from_fasta(const std::string& path) {   // refs.cpp:20-58
+    std::ifstream in(path);
+    if (!in) throw std::runtime_error("Cannot read from FASTA file " + path);
+    if (in.peek() != '>') throw std::runtime_error("FASTA file must begin with '>' character");
+    References r;
+    std::string line, seq, name;
+    bool eof = false;
+    do {
+        eof = !bool(std::getline(in, line));
+        if (eof || (!line.empty() && line[0] == '>')) {
+            if (!seq.empty()) {
+                to_uppercase(seq);
+                r.seqs.push_back(seq);
+                r.names.push_back(name);
+            }
+            if (!eof) name = line.substr(1, line.find(' ') - 1);
+            seq.clear();
+        } else {
+            seq += line;
+        }
+    } while (!eof);
+    r.offsets.assign(1, 0);
+    size_t total = 0;
+    for (auto& s : r.seqs) { total += s.size(); r.offsets.push_back(total); }
+    r.concat.reserve(total);
+    for (auto& s : r.seqs) r.concat += s;
+    return r;
+}
+
+// ------------------------------------------------------ IndexParameters --
+struct Profile { int crl, r_threshold, k, s_offset, l, u; };
+static const Profile kProfiles[] = {            // indexparameters.cpp:136-144
+    {50, 90, 20, -4, -3, 2}, {100, 110, 20, -4, -2, 2}, {125, 135, 20, -4, -1, 4}, {150, 175, 20, -4, 1, 7},
+    {250, 275, 20, -4, 4, 13}, {300, 375, 22, -4, 2, 12}, {400, INT32_MAX, 23, -6, 2, 12},
+};
+
+void IndexParameters::finalize() {
+    t = (k - s) / 2 + 1;
+    int wm = k / (k - s + 1) + l;
+    w_min = (unsigned)std::max(0, wm);
+    w_max = (unsigned)(k / (k - s + 1) + u);
+    if (k <= 7 || k > 32) throw std::runtime_error("k not in [8,32]");
+    if (s > k) throw std::runtime_error("s is larger than k");
+    if ((k - s) % 2 != 0) throw std::runtime_error("(k - s) must be an even number");
+    if (max_dist > 255) throw std::runtime_error("maximum seed length (-m) is larger than 255");
+    if (w_min > w_max) throw std::runtime_error("w_min is greater than w_max");
+}
+
+IndexParameters IndexParameters::from_read_length(int read_length, int k, int s, int l, int u, int c,
+                                                  int max_seed_len) {   // indexparameters.cpp:150-182
+    const int DEF = INT32_MIN;
+    int crl = 50;
+    for (const auto& p : kProfiles) {
+        if (read_length <= p.r_threshold) {
+            if (k == DEF) k = p.k;
+            if (s == DEF) s = k + p.s_offset;
+            if (l == DEF) l = p.l;
+            if (u == DEF) u = p.u;
+            crl = p.crl;
+            break;
+        }
+    }
+    int max_dist;
+    if (max_seed_len == DEF) {
+        max_dist = std::max(crl - 70, k);
+        max_dist = std::min(255, max_dist);
+    } else {
+        max_dist = max_seed_len - k;
+    }
+    int q = (int)std::pow(2, c == DEF ? 8 : c) - 1;
+    IndexParameters ip;
+    ip.canonical_read_length = crl; ip.k = k; ip.s = s; ip.l = l; ip.u = u; ip.q = q; ip.max_dist = max_dist;
+    ip.finalize();
+    return ip;
+}
+
+bool IndexParameters::operator==(const IndexParameters& o) const {
+    return canonical_read_length == o.canonical_read_length && k == o.k && s == o.s && t == o.t && l == o.l &&
+           u == o.u && q == o.q && max_dist == o.max_dist && w_min == o.w_min && w_max == o.w_max;
+}
+
+std::string IndexParameters::filename_extension() const {   // indexparameters.cpp:216-224
+    std::string s;
+    if (*this == from_read_length(canonical_read_length)) s = ".r" + std::to_string(canonical_read_length);
+    return s + ".sti";
+}
+
+// ------------------------------------------------------------------ .sti --
+template <class T> static void wr(std::ofstream& o, const T& v) { o.write((const char*)&v, sizeof(T)); }
+template <class T> static T rd(std::ifstream& i) { T v{}; i.read((char*)&v, sizeof(T)); return v; }
+
+void StiIndex::write(const std::string& path) const {   // index.cpp:73-89
+    std::ofstream o(path, std::ios::binary);
+    o.write("STI\1", 4);
+    wr<int32_t>(o, 2);
+    wr<uint64_t>(o, 8);
+    const char reserved[8] = {0};
+    o.write(reserved, 8);
+    wr<int32_t>(o, filter_cutoff);
+    wr<int32_t>(o, bits);
+    const int32_t prm[7] = {params.canonical_read_length, params.k, params.s, params.l, params.u, params.q,
+                            params.max_dist};
+    o.write((const char*)prm, sizeof prm);
+    wr<uint64_t>(o, randstrobes.size());
+    o.write((const char*)randstrobes.data(), (std::streamsize)(randstrobes.size() * sizeof(rsa_ref_randstrobe)));
+    wr<uint64_t>(o, bucket_starts.size());
+    o.write((const char*)bucket_starts.data(), (std::streamsize)(bucket_starts.size() * 8));
+    if (!o) throw std::runtime_error("cannot write " + path);
+}
+
+void StiIndex::read(const std::string& path) {          // index.cpp:91-132
+    std::ifstream in(path, std::ios::binary);
+    if (!in) throw std::runtime_error("cannot open index " + path);
+    char magic[4];
+    in.read(magic, 4);
+    if (memcmp(magic, "STI\1", 4) != 0) throw std::runtime_error("Index file has incorrect format (magic number mismatch)");
+    if (rd<int32_t>(in) != 2) throw std::runtime_error("Can only read index file format version 2");
+    uint64_t reserved = rd<uint64_t>(in);
+    in.seekg((std::streamoff)reserved, std::ios_base::cur);
+    filter_cutoff = rd<int32_t>(in);
+    bits = rd<int32_t>(in);
+    int32_t prm[7];
+    in.read((char*)prm, sizeof prm);
+    params.canonical_read_length = prm[0]; params.k = prm[1]; params.s = prm[2]; params.l = prm[3];
+    params.u = prm[4]; params.q = prm[5]; params.max_dist = prm[6];
+    params.finalize();
+    uint64_t n = rd<uint64_t>(in);
+    randstrobes.resize(n);
+    in.read((char*)randstrobes.data(), (std::streamsize)(n * sizeof(rsa_ref_randstrobe)));
+    uint64_t ns = rd<uint64_t>(in);
+    bucket_starts.resize(ns);
+    in.read((char*)bucket_starts.data(), (std::streamsize)(ns * 8));
+    if (!in) throw std::runtime_error("truncated index " + path);
+    if (ns != (1ull << bits) + 1) throw std::runtime_error("randstrobe_start_indices vector is of the wrong size");
+}
+
+// --- index construction (index.cpp:141-309) --------------------------------
+// Randstrobes of the forward reference (RandstrobeGenerator semantics equal the
+// query iterator's: window [i+w_min, min(i+w_max, n-1)], first min popcount).
+static uint64_t xxh64_u64(uint64_t input) {              // hash.hpp:105-118
+    const uint64_t P1 = 0x9E3779B185EBCA87ULL, P2 = 0xC2B2AE3D27D4EB4FULL, P3 = 0x165667B19E3779F9ULL,
+                   P4 = 0x85EBCA77C2B2AE63ULL, P5 = 0x27D4EB2F165667C5ULL;
+    uint64_t acc = P5 + 8, k1 = input * P2;
+    k1 = (k1 << 31) | (k1 >> 33);
+    acc ^= k1 * P1;
+    acc = ((acc << 27) | (acc >> 37)) * P1 + P4;
+    acc ^= acc >> 33; acc *= P2; acc ^= acc >> 29; acc *= P3; acc ^= acc >> 32;
+    return acc;
+}
+
+struct Syncmer { uint64_t hash; uint32_t pos; };
+
+static void syncmers_of(std::string_view seq, const IndexParameters& p, std::vector<Syncmer>& out) {
+    out.clear();
+    const int k = p.k, s = p.s, t = p.t;
+    const uint64_t kmask = (k == 32) ? ~0ULL : ((1ULL << (2 * k)) - 1), smask = (1ULL << (2 * s)) - 1;
+    const int kshift = (k - 1) * 2, sshift = (s - 1) * 2, W = k - s + 1;
+    uint64_t ring[64];
+    int qn = 0, qh = 0, l = 0;
+    uint64_t min_val = UINT64_MAX, xk0 = 0, xk1 = 0, xs0 = 0, xs1 = 0;
+    long long min_pos = -1;
+    for (size_t i = 0; i < seq.size(); ++i) {
+        int c;
+        switch (seq[i]) {
+            case 'A': case 'a': c = 0; break;
+            case 'C': case 'c': c = 1; break;
+            case 'G': case 'g': c = 2; break;
+            case 'T': case 't': case 'U': case 'u': c = 3; break;
+            default: c = 4;
+        }
+        if (c < 4) {
+            xk0 = ((xk0 << 2) | (uint64_t)c) & kmask;
+            xk1 = (xk1 >> 2) | ((uint64_t)(3 - c) << kshift);
+            xs0 = ((xs0 << 2) | (uint64_t)c) & smask;
+            xs1 = (xs1 >> 2) | ((uint64_t)(3 - c) << sshift);
+            if (++l < s) continue;
+            uint64_t hs = xxh64_u64(std::min(xs0, xs1));
+            ring[(qh + qn) & 63] = hs;
+            qn++;
+            if (qn < W) continue;
+            long long ii = (long long)i;
+            if (qn == W) {
+                for (int j = 0; j < qn; ++j) {
+                    uint64_t v = ring[(qh + j) & 63];
+                    if (v < min_val) { min_val = v; min_pos = ii - k + j + 1; }
+                }
+            } else {
+                qh = (qh + 1) & 63; qn--;
+                if (min_pos == ii - k) {
+                    min_val = UINT64_MAX; min_pos = ii - s + 1;
+                    for (int j = qn - 1; j >= 0; --j) {
+                        uint64_t v = ring[(qh + j) & 63];
+                        if (v < min_val) { min_val = v; min_pos = ii - k + j + 1; }
+                    }
+                } else if (hs < min_val) { min_val = hs; min_pos = ii - s + 1; }
+            }
+            if (min_pos == ii - k + t) out.push_back(Syncmer{xxh64_u64(std::min(xk0, xk1)), (uint32_t)(ii - k + 1)});
+        } else {
+            min_val = UINT64_MAX; min_pos = -1; l = 0; xs0 = xs1 = xk0 = xk1 = 0; qn = 0; qh = 0;
+        }
+    }
+}
+
+void StiIndex::build(const References& refs, const IndexParameters& p, int bits_override, float f, int threads) {
+    params = p;
+    size_t total = 0;
+    for (auto& s : refs.seqs) total += s.size();
+    if (bits_override >= 0) bits = bits_override;
+    else {   // pick_bits (index.cpp:135-139)
+        size_t est = total / (size_t)(p.k - p.s + 1);
+        bits = std::clamp((int)std::log2((double)est) - 1, 8, 31);
+    }
+    // per contig randstrobes (count, then assign), contigs distributed over threads
+    std::vector<std::vector<rsa_ref_randstrobe>> per(refs.size());
+    std::atomic<size_t> next{0};
+    auto worker = [&]() {
+        std::vector<Syncmer> sm;
+        for (;;) {
+            size_t j = next.fetch_add(1);
+            if (j >= refs.size()) break;
+            const std::string& seq = refs.seqs[j];
+            if (seq.size() < p.w_max) continue;
+            syncmers_of(seq, p, sm);
+            auto& v = per[j];
+            const size_t n = sm.size();
+            for (size_t i = 0; i + p.w_min < n; ++i) {
+                size_t w_end = std::min(i + p.w_max, n - 1);
+                uint64_t maxp = (uint64_t)sm[i].pos + (unsigned)p.max_dist, min_val = UINT64_MAX;
+                size_t best = i;
+                for (size_t x = i + p.w_min; x <= w_end && sm[x].pos <= maxp; ++x) {
+                    uint64_t res = (uint64_t)__builtin_popcountll((sm[i].hash ^ sm[x].hash) & (uint64_t)p.q);
+                    if (res < min_val) { min_val = res; best = x; }
+                }
+                uint32_t packed = (uint32_t)(j << 8) + (sm[best].pos - sm[i].pos);
+                v.push_back(rsa_ref_randstrobe{sm[i].hash + sm[best].hash, sm[i].pos, packed});
+            }
+        }
+    };
+    std::vector<std::thread> ws;
+    for (int t = 0; t < std::max(1, threads); ++t) ws.emplace_back(worker);
+    for (auto& w : ws) w.join();
+    size_t n = 0;
+    for (auto& v : per) n += v.size();
+    randstrobes.clear();
+    randstrobes.reserve(n);
+    for (auto& v : per) { randstrobes.insert(randstrobes.end(), v.begin(), v.end()); std::vector<rsa_ref_randstrobe>().swap(v); }
+    // RefRandstrobe::operator< orders by (hash, position); ties (equal hash and
+    // position in two contigs) are left in contig order here while the
+    // reference's pdqsort_branchless leaves them in an unspecified order.
+    auto lt = [](const rsa_ref_randstrobe& a, const rsa_ref_randstrobe& b) {
+        if (a.hash != b.hash) return a.hash < b.hash;
+        return a.position < b.position;
+    };
+    {   // parallel sort: sort slices, then pairwise merges
+        const int T = std::max(1, threads);
+        std::vector<size_t> cut(T + 1);
+        for (int t = 0; t <= T; ++t) cut[t] = n * (size_t)t / (size_t)T;
+        std::vector<std::thread> st;
+        for (int t = 0; t < T; ++t)
+            st.emplace_back([&, t]() { std::stable_sort(randstrobes.begin() + cut[t], randstrobes.begin() + cut[t + 1], lt); });
+        for (auto& x : st) x.join();
+        for (int width = 1; width < T; width *= 2) {
+            std::vector<std::thread> mt;
+            for (int t = 0; t + width < T; t += 2 * width) {
+                size_t a = cut[t], m = cut[t + width], b = cut[std::min(T, t + 2 * width)];
+                mt.emplace_back([&, a, m, b]() {
+                    std::inplace_merge(randstrobes.begin() + a, randstrobes.begin() + m, randstrobes.begin() + b, lt);
+                });
+            }
+            for (auto& x : mt) x.join();
+        }
+    }
+    // bucket table + filter cutoff (index.cpp:174-238)
+    bucket_starts.clear();
+    bucket_starts.reserve((1ull << bits) + 1);
+    uint64_t unique_mers = randstrobes.empty() ? 0 : 1;
+    uint64_t prev = randstrobes.empty() ? 0 : randstrobes[0].hash;
+    unsigned count = 0;
+    std::vector<unsigned> counts;
+    for (uint64_t pos = 0; pos < randstrobes.size(); ++pos) {
+        const uint64_t h = randstrobes[pos].hash;
+        if (h == prev) { ++count; continue; }
+        ++unique_mers;
+        if (count != 1) counts.push_back(count);
+        count = 1;
+        const uint64_t top = h >> (64 - bits);
+        while (bucket_starts.size() <= top) bucket_starts.push_back(pos);
+        prev = h;
+    }
+    if (count != 1 && !randstrobes.empty()) counts.push_back(count);
+    else if (randstrobes.empty()) { /* nothing */ }
+    while (bucket_starts.size() < (1ull << bits) + 1) bucket_starts.push_back(randstrobes.size());
+    std::sort(counts.begin(), counts.end(), std::greater<int>());
+    uint64_t index_cutoff = (uint64_t)(unique_mers * f);
+    if (!counts.empty()) {
+        unsigned fc = index_cutoff < counts.size() ? counts[index_cutoff] : counts.back();
+        fc = std::max(30U, fc);
+        fc = std::min(100U, fc);
+        filter_cutoff = (int)fc;
+    } else {
+        filter_cutoff = 30;
+    }
+}
+
+// ----------------------------------------------------------------- FASTQ --
+// kseq semantics: '@' or '>' header, name = up to the first whitespace, the
+// rest of the header line (after that whitespace) is the comment; sequence
+// lines are concatenated until '+' (FASTQ) or the next header (FASTA);
+// quality is read until it is as long as the sequence.
+struct FastxReader::Impl {
+    gzFile f = nullptr;
+    std::vector<char> buf;
+    size_t pos = 0, len = 0;
+    bool eof = false;
+    int last_char = -1;   // header char of the next record, if already read
+    int getc() {
+        if (pos >= len) {
+            if (eof) return -1;
+            int n = gzread(f, buf.data(), (unsigned)buf.size());
+            if (n <= 0) { eof = true; return -1; }
+            len = (size_t)n; pos = 0;
+        }
+        return (unsigned char)buf[pos++];
+    }
+    bool getline(std::string& s) {
+        s.clear();
+        int c;
+        bool any = false;
+        while ((c = getc()) != -1) {
+            any = true;
+            if (c == '\n') break;
+            s.push_back((char)c);
+        }
+        if (!s.empty() && s.back() == '\r') s.pop_back();
+        return any;
+    }
+};
+
+FastxReader::FastxReader(const std::string& path) : impl_(new Impl) {
+    impl_->f = gzopen(path == "-" ? "/dev/stdin" : path.c_str(), "r");
+    if (!impl_->f) throw std::runtime_error("Could not open FASTQ file: " + path);
+    impl_->buf.resize(1 << 20);
+    (void)gzbuffer(impl_->f, 1 << 20);
+}
+
+FastxReader::~FastxReader() { if (impl_->f) gzclose(impl_->f); }
+
+bool FastxReader::next(Record& r) {
+    Impl& I = *impl_;
+    int c = I.last_char;
+    if (c == -1) {
+        while ((c = I.getc()) != -1 && c != '>' && c != '@') {}
+        if (c == -1) return false;
+    }
+    std::string line;
+    I.getline(line);
+    size_t ws = line.find_first_of(" \t\v\f\r");
+    if (ws == std::string::npos) { r.name = line; r.comment.clear(); }
+    else {
+        r.name = line.substr(0, ws);
+        size_t cs = line.find_first_not_of(" \t\v\f\r", ws);
+        r.comment = cs == std::string::npos ? std::string() : line.substr(cs);
+    }
+    r.seq.clear();
+    r.qual.clear();
+    I.last_char = -1;
+    while ((c = I.getc()) != -1 && c != '>' && c != '@' && c != '+') {
+        if (c == '\n') continue;
+        std::string rest;
+        I.getline(rest);
+        r.seq.push_back((char)c);
+        r.seq += rest;
+        while (!r.seq.empty() && (r.seq.back() == ' ' || r.seq.back() == '\t')) r.seq.pop_back();
+    }
+    if (c == '>' || c == '@') { I.last_char = c; return true; }
+    if (c == -1) return true;
+    I.getline(line);   // rest of '+' line
+    while (r.qual.size() < r.seq.size()) {
+        if (!I.getline(line)) break;
+        r.qual += line;
+    }
+    if (r.qual.size() != r.seq.size()) throw std::runtime_error("FASTQ quality length differs from sequence length");
+    return true;
+}
+
+}  // namespace rsa

@@ -1,0 +1,256 @@
+// pipeline.cpp -- chunk pipeline with the reference's single-worker semantics.
+//
+// The reference (src/pc.cpp:1522-1887, perform_task_async_pe) interleaves per
+// worker: part(N-1) ... get_str(N-1) | part(N) | SW(N-1) | store(N-1), last(N-1).
+// Two pieces of state make results depend on that order:
+//  * the insert-size estimate (updated inside part() until 400 samples), read by
+//    get_str/store/last at different times (pc.cpp:1620, 1798, 1861);
+//  * minstd_rand seeded with the chunk index (pc.cpp:1583, 1750), consumed by
+//    part() (shuffle_top_nams) and then by last() (pick_random_top_pair).
+// We replay the exact single-worker timeline until the estimate is frozen; from
+// then on chunks are independent and run in parallel on the host workers, each
+// calling the GPU engine (seeding + extension) for its own chunk.
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <map>
+#include <mutex>
+#include <thread>
+
+#include "rsa_host.hpp"
+
+namespace rsa {
+
+namespace {
+
+struct OrderedSink {
+    SamSink sink;
+    void* user;
+    std::mutex m;
+    std::map<size_t, std::string> pending;
+    size_t next = 0;
+    uint64_t bytes = 0;
+    void put(size_t idx, std::string&& s) {
+        std::lock_guard<std::mutex> g(m);
+        pending.emplace(idx, std::move(s));
+        for (auto it = pending.find(next); it != pending.end(); it = pending.find(next)) {
+            bytes += it->second.size();
+            sink(user, it->second);
+            pending.erase(it);
+            next++;
+        }
+    }
+};
+
+struct PeChunk {
+    size_t index = 0, begin = 0, end = 0;
+    std::vector<Record> r1, r2;               // upper-cased copies (pc.cpp:1586-1587)
+    std::vector<AlignTmpRes> res;
+    std::minstd_rand rng;
+    AlignmentStatistics stats;
+};
+
+void pe_load(PeChunk& c, const std::vector<Record>& a, const std::vector<Record>& b, size_t idx, size_t chunk) {
+    c.index = idx;
+    c.begin = std::min(a.size(), idx * chunk);
+    c.end = std::min(a.size(), c.begin + chunk);
+    c.r1.assign(a.begin() + c.begin, a.begin() + c.end);
+    c.r2.assign(b.begin() + c.begin, b.begin() + c.end);
+    for (auto& r : c.r1) to_uppercase(r.seq);
+    for (auto& r : c.r2) to_uppercase(r.seq);
+    c.res.clear();
+    c.res.resize(c.r1.size());
+}
+
+// part() of every pair in chunk order (pc.cpp:1739-1766), seeding batched on the engine
+void pe_part(PeChunk& c, Engine& eng, const MapContext& mc, InsertSizeDistribution& isize) {
+    c.rng.seed((unsigned)c.index);
+    const size_t n = c.r1.size();
+    if (n == 0) return;
+    std::vector<const std::string*> reads;
+    reads.reserve(2 * n);
+    for (size_t i = 0; i < n; ++i) { reads.push_back(&c.r1[i].seq); reads.push_back(&c.r2[i].seq); }
+    SeedBatchOut so;
+    eng.seed(reads, mc.mparams.rescue_level, (unsigned)mc.mparams.rescue_cutoff, so);
+    for (size_t i = 0; i < n; ++i) {
+        std::vector<Nam> nams[2];
+        bool rescued[2];
+        for (int m = 0; m < 2; ++m) {
+            const size_t r = 2 * i + m;
+            nams[m].assign(so.nams.begin() + (long)so.offsets[r], so.nams.begin() + (long)so.offsets[r + 1]);
+            rescued[m] = so.rescued[r] != 0;
+        }
+        align_PE_read_part(c.res[i], c.r1[i], c.r2[i], nams, rescued, c.stats, isize, mc, c.rng);
+        c.stats.n_reads += 2;
+    }
+}
+
+void pe_get_str(PeChunk& c, const MapContext& mc, float mu, float sigma, std::vector<SwJob>& jobs) {
+    jobs.clear();
+    for (size_t i = 0; i < c.r1.size(); ++i) {
+        Read read1(c.r1[i].seq), read2(c.r2[i].seq);
+        collect_jobs_pe(c.res[i], c.r1[i], c.r2[i], read1, read2, mc, mu, sigma, jobs);
+    }
+}
+
+void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistribution& isize,
+                   const std::vector<AlignmentInfo>& infos, const std::string& rg_id, std::string& out) {
+    size_t pos = 0;
+    for (size_t i = 0; i < c.r1.size(); ++i) {
+        Read read1(c.r1[i].seq), read2(c.r2[i].seq);
+        pos = store_results_pe(c.res[i], read1, read2, mc, isize.mu, isize.sigma, infos, pos);
+    }
+    out.clear();
+    out.reserve(7 * (size_t)mc.mparams.r * c.r1.size());
+    Sam sam(out, mc.refs, mc.mparams.cigar_eqx, rg_id, mc.mparams.output_unmapped, mc.mparams.details);
+    for (size_t i = 0; i < c.r1.size(); ++i)
+        align_PE_read_last(c.res[i], c.r1[i], c.r2[i], sam, c.stats, isize, mc, c.rng);
+}
+
+}  // namespace
+
+PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<Record>& r2, Engine& eng,
+                               const MapContext& mc, const PipelineOptions& opt, SamSink sink, void* user) {
+    auto t0 = std::chrono::steady_clock::now();
+    PipelineResult result;
+    OrderedSink os{sink, user};
+    const size_t chunk = (size_t)std::max(1, opt.chunk_size);
+    const size_t n_chunks = (r1.size() + chunk - 1) / chunk;
+    InsertSizeDistribution isize;
+    std::vector<SwJob> jobs;
+    std::vector<AlignmentInfo> infos;
+    // ---- single-worker timeline until the insert-size estimate freezes ----
+    auto pre = std::make_unique<PeChunk>();
+    size_t next_chunk = 0;
+    if (n_chunks == 0) return result;
+    pe_load(*pre, r1, r2, next_chunk++, chunk);
+    pe_part(*pre, eng, mc, isize);
+    while (!isize.frozen() && next_chunk <= n_chunks) {
+        pe_get_str(*pre, mc, isize.mu, isize.sigma, jobs);
+        auto cur = std::make_unique<PeChunk>();
+        const bool have = next_chunk < n_chunks;
+        if (have) {
+            pe_load(*cur, r1, r2, next_chunk, chunk);
+            pe_part(*cur, eng, mc, isize);
+        }
+        next_chunk++;
+        eng.extend(jobs, mc.aparams, infos);
+        pre->stats.tot_aligner_calls += jobs.size();
+        std::string out;
+        pe_store_last(*pre, mc, isize, infos, opt.rg_id, out);
+        os.put(pre->index, std::move(out));
+        result.stats.add(pre->stats);
+        if (!have) { pre.reset(); break; }
+        pre = std::move(cur);
+    }
+    // ---- frozen: chunk-parallel ----
+    if (pre || next_chunk < n_chunks) {
+        const InsertSizeDistribution frozen = isize;
+        std::mutex stat_m;
+        std::atomic<size_t> next{next_chunk};
+        std::unique_ptr<PeChunk> handed = std::move(pre);   // part() already done, rng continues
+        std::mutex hand_m;
+        auto worker = [&]() {
+            std::vector<SwJob> wj;
+            std::vector<AlignmentInfo> wi;
+            AlignmentStatistics local;
+            for (;;) {
+                std::unique_ptr<PeChunk> c;
+                {
+                    std::lock_guard<std::mutex> g(hand_m);
+                    if (handed) c = std::move(handed);
+                }
+                if (!c) {
+                    size_t idx = next.fetch_add(1);
+                    if (idx >= n_chunks) break;
+                    c = std::make_unique<PeChunk>();
+                    pe_load(*c, r1, r2, idx, chunk);
+                    InsertSizeDistribution est = frozen;
+                    pe_part(*c, eng, mc, est);
+                }
+                pe_get_str(*c, mc, frozen.mu, frozen.sigma, wj);
+                eng.extend(wj, mc.aparams, wi);
+                c->stats.tot_aligner_calls += wj.size();
+                std::string out;
+                pe_store_last(*c, mc, frozen, wi, opt.rg_id, out);
+                os.put(c->index, std::move(out));
+                local.add(c->stats);
+            }
+            std::lock_guard<std::mutex> g(stat_m);
+            result.stats.add(local);
+        };
+        std::vector<std::thread> ws;
+        const int T = std::max(1, opt.threads);
+        for (int t = 0; t < T; ++t) ws.emplace_back(worker);
+        for (auto& w : ws) w.join();
+    }
+    result.map_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    result.sam_bytes = os.bytes;
+    return result;
+}
+
+// Single-end: perform_task_async_se (pc.cpp:814-1096).  No insert-size state;
+// records are NOT upper-cased on this path; chunks are independent from the start.
+PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, const MapContext& mc,
+                               const PipelineOptions& opt, SamSink sink, void* user) {
+    auto t0 = std::chrono::steady_clock::now();
+    PipelineResult result;
+    OrderedSink os{sink, user};
+    const size_t chunk = (size_t)std::max(1, opt.chunk_size);
+    const size_t n_chunks = (recs.size() + chunk - 1) / chunk;
+    std::atomic<size_t> next{0};
+    std::mutex stat_m;
+    auto worker = [&]() {
+        std::vector<SwJob> jobs;
+        std::vector<AlignmentInfo> infos;
+        AlignmentStatistics local;
+        for (;;) {
+            size_t idx = next.fetch_add(1);
+            if (idx >= n_chunks) break;
+            const size_t b = idx * chunk, e = std::min(recs.size(), b + chunk);
+            AlignmentStatistics st;
+            std::minstd_rand rng;
+            rng.seed((unsigned)idx);
+            std::vector<const std::string*> reads;
+            for (size_t i = b; i < e; ++i) reads.push_back(&recs[i].seq);
+            SeedBatchOut so;
+            eng.seed(reads, mc.mparams.rescue_level, (unsigned)mc.mparams.rescue_cutoff, so);
+            std::vector<AlignTmpRes> res(e - b);
+            for (size_t i = b; i < e; ++i) {
+                const size_t r = i - b;
+                std::vector<Nam> nams(so.nams.begin() + (long)so.offsets[r], so.nams.begin() + (long)so.offsets[r + 1]);
+                align_SE_read_part(res[r], recs[i], nams, so.rescued[r] != 0, st, mc, rng);
+                st.n_reads++;
+            }
+            jobs.clear();
+            for (size_t i = b; i < e; ++i) {
+                Read read(recs[i].seq);
+                collect_jobs_se(res[i - b], read, mc, jobs);
+            }
+            eng.extend(jobs, mc.aparams, infos);
+            st.tot_aligner_calls += jobs.size();
+            size_t pos = 0;
+            for (size_t i = b; i < e; ++i) {
+                Read read(recs[i].seq);
+                pos = store_results_se(res[i - b], read, mc, infos, pos);
+            }
+            std::string out;
+            out.reserve(7 * (size_t)mc.mparams.r * (e - b));
+            Sam sam(out, mc.refs, mc.mparams.cigar_eqx, opt.rg_id, mc.mparams.output_unmapped, mc.mparams.details);
+            for (size_t i = b; i < e; ++i) align_SE_read_last(res[i - b], recs[i], sam, st, mc, rng);
+            os.put(idx, std::move(out));
+            local.add(st);
+        }
+        std::lock_guard<std::mutex> g(stat_m);
+        result.stats.add(local);
+    };
+    std::vector<std::thread> ws;
+    for (int t = 0; t < std::max(1, opt.threads); ++t) ws.emplace_back(worker);
+    for (auto& w : ws) w.join();
+    result.map_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    result.sam_bytes = os.bytes;
+    return result;
+}
+
+}  // namespace rsa

@@ -1,0 +1,277 @@
+// rsa_host.hpp -- host side of the MI355X seed-and-extend path.
+//
+// Restates, byte-exactly, the reference's host logic around the hot path
+// (mapping decisions src/aln.cpp, chunk pipeline src/pc.cpp, SAM src/sam.cpp,
+// CIGAR src/cigar.{hpp,cpp}, FASTA src/refs.cpp, .sti src/index.cpp).  The
+// hot path itself (seeding, find_nams, SW extension) is reached only through
+// the Engine interface; the product engine is the HIP C-ABI (include/rsa_gpu.h).
+#pragma once
+#include <cstdint>
+#include <memory>
+#include <random>
+#include <string>
+#include <string_view>
+#include <vector>
+
+#include "../../../include/rsa_gpu.h"
+
+namespace rsa {
+
+// ---------------------------------------------------------------- CIGAR ---
+enum CigarOp : uint8_t { C_M = 0, C_I = 1, C_D = 2, C_N = 3, C_S = 4, C_H = 5, C_P = 6, C_EQ = 7, C_X = 8 };
+
+struct Cigar {                                  // src/cigar.hpp:23-93
+    std::vector<uint32_t> ops;
+    bool empty() const { return ops.empty(); }
+    void push(uint32_t op, uint32_t len) {
+        if (ops.empty() || (ops.back() & 0xf) != op) ops.push_back(len << 4 | op);
+        else ops.back() += len << 4;
+    }
+    void append(const Cigar& o) { for (uint32_t x : o.ops) push(x & 0xf, x >> 4); }
+    Cigar to_m() const;
+    void to_string(std::string& out) const;
+};
+
+// ---------------------------------------------------------------- types ---
+using Nam = rsa_nam;                            // src/nam.hpp:11-38
+
+struct AlignmentInfo {                          // src/aligner.hpp:20-30
+    Cigar cigar;
+    unsigned edit_distance = 0, ref_start = 0, ref_end = 0, query_start = 0, query_end = 0;
+    int sw_score = 0;
+    int ref_span() const { return (int)(ref_end - ref_start); }
+};
+
+struct Alignment {                              // src/sam.hpp:12-25
+    int ref_id = 0;
+    int ref_start = 0;
+    Cigar cigar;
+    int edit_distance = 0;
+    int global_ed = 0;
+    int score = 0;
+    int length = 0;
+    bool is_rc = false;
+    bool is_unaligned = false;
+    bool gapped = false;
+};
+
+struct AlignTmpRes {                            // src/sam.hpp:27-45
+    int type = 0;
+    int mapq1 = 0, mapq2 = 0;
+    int type4_loop_size = 0;
+    std::vector<bool> is_extend_seed, consistent_nam, is_read1;
+    std::vector<Nam> type4_nams, todo_nams;
+    std::vector<bool> done_align;
+    std::vector<Alignment> align_res;
+};
+
+struct Details {                                // src/sam.hpp:60-67
+    bool nam_rescue = false;
+    uint64_t nams = 0, nam_inconsistent = 0, mate_rescue = 0, tried_alignment = 0, gapped = 0;
+};
+
+struct AlignmentParameters { int match = 2, mismatch = 8, gap_open = 12, gap_extend = 1, end_bonus = 10; };
+
+struct MappingParameters {                      // src/aln.hpp:58-74
+    int r = 150;
+    int max_secondary = 0;
+    float dropoff_threshold = 0.5f;
+    int rescue_level = 2;
+    int max_tries = 20;
+    int rescue_cutoff = 0;
+    bool cigar_eqx = false;
+    bool output_unmapped = true;
+    bool details = false;
+};
+
+struct InsertSizeDistribution {                 // src/aln.hpp:79-90, aln.cpp:1880-1903
+    float sample_size = 1, mu = 300, sigma = 100, V = 10000, SSE = 10000;
+    void update(int dist);
+    bool frozen() const { return !(sample_size < 400); }
+};
+
+struct AlignmentStatistics {
+    uint64_t n_reads = 0, tot_aligner_calls = 0, tot_rescued = 0, tot_all_tried = 0, inconsistent_nams = 0,
+             nam_rescue = 0;
+    void add(const Details& d) {
+        nam_rescue += d.nam_rescue; tot_rescued += d.mate_rescue; tot_all_tried += d.tried_alignment;
+        inconsistent_nams += d.nam_inconsistent;
+    }
+    void add(const AlignmentStatistics& o) {
+        n_reads += o.n_reads; tot_aligner_calls += o.tot_aligner_calls; tot_rescued += o.tot_rescued;
+        tot_all_tried += o.tot_all_tried; inconsistent_nams += o.inconsistent_nams; nam_rescue += o.nam_rescue;
+    }
+};
+
+struct Record { std::string name, comment, seq, qual; };   // klibpp::KSeq fields used
+
+struct Read {                                   // src/revcomp.hpp:41-55
+    const std::string& seq;
+    std::string rc;
+    explicit Read(const std::string& s);
+    size_t size() const { return seq.size(); }
+};
+std::string reverse_complement(std::string_view s);
+void to_uppercase(std::string& s);             // refs.cpp:10-16 (c & ~32)
+
+struct References {                             // src/refs.hpp
+    std::vector<std::string> names;
+    std::vector<std::string> seqs;
+    std::vector<uint64_t> offsets;              // concatenation offsets [n+1]
+    std::string concat;                         // all contigs back to back (device upload)
+    size_t size() const { return seqs.size(); }
+    static References from_fasta(const std::string& path);
+};
+
+struct IndexParameters {                        // src/indexparameters.hpp
+    int canonical_read_length = 150, k = 20, s = 16, t = 3, l = 1, u = 7, q = 255, max_dist = 80;
+    unsigned w_min = 0, w_max = 0;
+    static IndexParameters from_read_length(int read_length, int k = INT32_MIN, int s = INT32_MIN,
+                                            int l = INT32_MIN, int u = INT32_MIN, int c = INT32_MIN,
+                                            int max_seed_len = INT32_MIN);
+    void finalize();
+    bool operator==(const IndexParameters& o) const;
+    std::string filename_extension() const;
+};
+
+struct StiIndex {                               // .sti contents (src/index.cpp:73-132)
+    IndexParameters params;
+    int filter_cutoff = 0;
+    int bits = 0;
+    std::vector<rsa_ref_randstrobe> randstrobes;
+    std::vector<uint64_t> bucket_starts;
+    void read(const std::string& path);
+    void write(const std::string& path) const;
+    void build(const References& refs, const IndexParameters& p, int bits_override, float f, int threads);
+};
+
+// --------------------------------------------------------------- engine ---
+struct SeedBatchOut {
+    std::vector<Nam> nams;
+    std::vector<uint64_t> offsets;              // [n+1]
+    std::vector<float> nonrep;
+    std::vector<uint8_t> rescued;
+};
+
+struct SwJob {                                  // query host bytes vs reference window
+    std::string query;
+    int ref_id;
+    uint32_t ref_start, ref_len;
+};
+
+class Engine {
+public:
+    virtual ~Engine() = default;
+    virtual const char* name() const = 0;
+    // NAMs (pre-sort order) for every read, as align_*_read_part computes them (aln.cpp:1946-1962)
+    virtual void seed(const std::vector<const std::string*>& reads, int rescue_level, unsigned rescue_cutoff,
+                      SeedBatchOut& out) = 0;
+    // Aligner::align for every job (aligner.cpp:114-210)
+    virtual void extend(const std::vector<SwJob>& jobs, const AlignmentParameters& p,
+                        std::vector<AlignmentInfo>& out) = 0;
+};
+
+// GPU engine over the C-ABI (engine_gpu.cpp)
+std::unique_ptr<Engine> make_gpu_engine(const References& refs, const StiIndex& index, int device);
+
+class Sam;
+
+// ------------------------------------------------------------- mapping ---
+struct MapContext {
+    const References& refs;
+    const IndexParameters& iparams;
+    const AlignmentParameters& aparams;
+    const MappingParameters& mparams;
+};
+
+// part / last split of src/aln.cpp:1927-2306 (PE) and 2372-2467 (SE).  `nams`
+// are the pre-sort NAM lists of both mates (already through find_nams/rescue).
+void align_PE_read_part(AlignTmpRes& res, const Record& r1, const Record& r2, std::vector<Nam> nams[2],
+                        const bool rescued[2], AlignmentStatistics& stats, InsertSizeDistribution& isize,
+                        const MapContext& mc, std::minstd_rand& rng);
+void align_PE_read_last(AlignTmpRes& res, const Record& r1, const Record& r2, Sam& sam,
+                        AlignmentStatistics& stats, const InsertSizeDistribution& isize, const MapContext& mc,
+                        std::minstd_rand& rng);
+void align_SE_read_part(AlignTmpRes& res, const Record& r, std::vector<Nam>& nams, bool rescued,
+                        AlignmentStatistics& stats, const MapContext& mc, std::minstd_rand& rng);
+void align_SE_read_last(AlignTmpRes& res, const Record& r, Sam& sam, AlignmentStatistics& stats,
+                        const MapContext& mc, std::minstd_rand& rng);
+
+// SW jobs of a finished part() (pc.cpp:1604-1669 get_str) and storing their results (pc.cpp:1789-1844)
+void collect_jobs_pe(AlignTmpRes& res, const Record& r1, const Record& r2, const Read& read1, const Read& read2,
+                     const MapContext& mc, float mu, float sigma, std::vector<SwJob>& jobs);
+size_t store_results_pe(AlignTmpRes& res, const Read& read1, const Read& read2, const MapContext& mc, float mu,
+                        float sigma, const std::vector<AlignmentInfo>& infos, size_t pos);
+void collect_jobs_se(AlignTmpRes& res, const Read& read, const MapContext& mc, std::vector<SwJob>& jobs);
+size_t store_results_se(AlignTmpRes& res, const Read& read, const MapContext& mc,
+                        const std::vector<AlignmentInfo>& infos, size_t pos);
+
+// --------------------------------------------------------------- SAM -----
+std::string sam_header(const References& refs, const std::string& rg_id, const std::vector<std::string>& rg,
+                       const std::string& cmd_line);
+
+class Sam {                                     // src/sam.hpp:69-120
+public:
+    Sam(std::string& out, const References& refs, bool eqx, const std::string& rg_id, bool output_unmapped,
+        bool details);
+    void add(const Alignment& a, const Record& r, const std::string& rc, uint8_t mapq, bool primary,
+             const Details& d);
+    void add_pair(const Alignment& a1, const Alignment& a2, const Record& r1, const Record& r2,
+                  const std::string& rc1, const std::string& rc2, uint8_t mapq1, uint8_t mapq2, bool proper,
+                  bool primary, const Details d[2]);
+    void add_unmapped(const Record& r, uint16_t flags = 4);
+    void add_unmapped_pair(const Record& r1, const Record& r2);
+    void add_unmapped_mate(const Record& r, uint16_t flags, const std::string& mate_ref, uint32_t mate_pos);
+
+private:
+    void add_record(const std::string& qname, uint16_t flags, const std::string& rname, uint32_t pos, uint8_t mapq,
+                    const Cigar& cigar, const std::string& mate_rname, uint32_t mate_pos, int32_t tlen,
+                    const std::string& seq, const std::string& seq_rc, const std::string& qual, int ed, int score,
+                    const Details& d);
+    std::string& out_;
+    const References& refs_;
+    bool eqx_, output_unmapped_, details_;
+    std::string tail_;
+};
+
+bool is_proper_pair(const Alignment& a1, const Alignment& a2, float mu, float sigma);
+
+// ------------------------------------------------------------- input -----
+class FastxReader {                             // kseq++ record semantics (src/fastq.cpp)
+public:
+    explicit FastxReader(const std::string& path);
+    ~FastxReader();
+    bool next(Record& r);
+private:
+    struct Impl;
+    std::unique_ptr<Impl> impl_;
+};
+
+// ------------------------------------------------------------ pipeline ---
+struct PipelineOptions {
+    int threads = 3;
+    int chunk_size = 10000;
+    bool interleaved = false;
+    std::string rg_id;
+};
+
+struct PipelineResult {
+    AlignmentStatistics stats;
+    double map_seconds = 0;
+    uint64_t sam_bytes = 0;
+};
+
+// perform_task_async_{pe,se} (src/pc.cpp:814-1096, 1522-1887) with -t 1 semantics:
+// chunks are processed strictly in the single-worker timeline until the insert
+// size estimate freezes, then chunk-parallel over `threads` host workers.
+using SamSink = void (*)(void* user, const std::string& chunk);
+PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<Record>& r2, Engine& eng,
+                               const MapContext& mc, const PipelineOptions& opt, SamSink sink, void* user);
+PipelineResult run_pipeline_se(const std::vector<Record>& r, Engine& eng, const MapContext& mc,
+                               const PipelineOptions& opt, SamSink sink, void* user);
+
+// CLI entry (main.cpp); the oracle CPU binary reuses it with its own engine factory
+using EngineFactory = std::unique_ptr<Engine> (*)(const References&, const StiIndex&, int device);
+int cli_main(int argc, char** argv, EngineFactory factory, const char* prog);
+
+}  // namespace rsa

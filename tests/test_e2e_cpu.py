@@ -1,0 +1,28 @@
+"""CPU: the host pipeline is deterministic and the C restatement engine equals the
+reference's own hot-path code (randstrobes/nam/ssw.c) end to end."""
+import os
+
+import pytest
+
+from e2e import CPU_PORT, CPU_REF, make_dataset, map_reads, sam_body
+
+
+@pytest.fixture(scope="module")
+def data(tmp_path_factory):
+    d = tmp_path_factory.mktemp("e2e_cpu")
+    return d, make_dataset(str(d), pairs=3000, ref_len=200_000)
+
+
+@pytest.mark.skipif(not os.path.exists(CPU_REF), reason="reference build absent")
+def test_port_equals_reference_hot_path(data):
+    d, (fa, reads) = data
+    map_reads(CPU_PORT, fa, reads, str(d / "port.sam"), "-t", "2", "--chunk-size", "700")
+    map_reads(CPU_REF, fa, reads, str(d / "ref.sam"), "-t", "2", "--chunk-size", "700")
+    assert sam_body(d / "port.sam") == sam_body(d / "ref.sam")
+
+
+def test_thread_and_chunk_invariance(data):
+    d, (fa, reads) = data
+    map_reads(CPU_PORT, fa, reads, str(d / "t1.sam"), "-t", "1", "--chunk-size", "500")
+    map_reads(CPU_PORT, fa, reads, str(d / "t4.sam"), "-t", "4", "--chunk-size", "500")
+    assert sam_body(d / "t1.sam") == sam_body(d / "t4.sam")
