@@ -1,0 +1,246 @@
+#!/usr/bin/env python3
+"""bench.py -- headline benchmark of the MI355X mapping path.
+
+Metric (BASELINE.json): Mreads/s aligned, paired-end 2x150 bp against a 3 Gb
+reference, SAM bit-exact with the CPU path.  One "step" maps one batch of
+synthetic pairs end to end (reads in host RAM -> seeding, NAMs, extension on
+the GPU, pairing/rescue/SAM on the host -> SAM bytes in memory), i.e. the
+reference's "consumer cost" (src/main.cpp:446,595).  Reference and index are
+built once before timing and stay resident in HBM.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload pe150_3g]
+
+N>1: one process per GPU under torch.distributed.run; every rank holds the
+replicated index and maps its own shard of pairs (no data-path collective);
+the wall time is the max over ranks and the read count the sum ("weak").
+rank 0 prints one JSON line.  The cpu_baseline leg (rank 0, N=1) maps a
+bounded sample of the same workload with oracle/_ref/librsalign_ref.so (the
+reference's own seeding + SSW code inside the same host pipeline) and checks
+that its SAM hash equals the GPU path's on that sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+WORKLOADS = {
+    # name: reference bp, contigs, read length, insert mean/sd, paired
+    "pe150_3g": dict(ref_len=3_000_000_000, n_contigs=24, read_len=150, mu=300.0, sigma=30.0, paired=True,
+                     desc="PE 2x150 vs 3 Gb synthetic reference (24 x 125 Mb contigs), 1 GPU"),
+    "pe250_3g": dict(ref_len=3_000_000_000, n_contigs=24, read_len=250, mu=500.0, sigma=50.0, paired=True,
+                     desc="PE 2x250 vs 3 Gb synthetic reference (24 x 125 Mb contigs)"),
+    "pe150_250m": dict(ref_len=250_000_000, n_contigs=1, read_len=150, mu=300.0, sigma=30.0, paired=True,
+                       desc="PE 2x150 vs 250 Mb synthetic reference (chr1)"),
+    "se100_5m": dict(ref_len=5_000_000, n_contigs=1, read_len=100, mu=300.0, sigma=30.0, paired=False,
+                     desc="SE 1x100 vs 5 Mb synthetic reference"),
+}
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
+REF_CPU_LIB = os.path.join(ROOT, "oracle", "_ref", "librsalign_ref.so")
+
+
+def log(rank, *a):
+    print(f"[bench r{rank} {time.strftime('%H:%M:%S')}]", *a, file=sys.stderr, flush=True)
+
+
+def host_cores() -> int:
+    n = len(os.sched_getaffinity(0))
+    for var in ("OMP_NUM_THREADS", "MAX_JOBS"):
+        v = os.environ.get(var)
+        if v and v.isdigit() and int(v) > 0:
+            n = min(n, int(v))
+    return max(1, n)
+
+
+def roofline(ks: dict) -> dict:
+    """Roofline object for the kernel with the largest total device time.
+
+    achieved = algorithmic bytes per launch / average launch duration, both
+    from the HIP events recorded around every launch on its own stream.
+    """
+    kern = ks["kernels"]
+    name = max(kern, key=lambda k: kern[k]["ms"])
+    k = kern[name]
+    if k["launches"] == 0 or k["ms"] <= 0:
+        return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                "traffic": None, "kernel": None}
+    per_launch_bytes = k["alg_bytes"] / k["launches"]
+    avg_ms = k["ms"] / k["launches"]
+    achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9
+    from rabbitsalign_amd.native import KERNEL_SYMBOLS
+    return {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+            "kernel": KERNEL_SYMBOLS[name], "alg_bytes_per_launch": round(per_launch_bytes, 1),
+            "avg_launch_us": round(avg_ms * 1e3, 3), "launches": k["launches"]}
+
+
+def kernel_table(ks: dict) -> dict:
+    out = {}
+    for name, k in ks["kernels"].items():
+        if k["launches"]:
+            out[name] = {"ms": round(k["ms"], 3), "launches": k["launches"],
+                         "avg_us": round(1e3 * k["ms"] / k["launches"], 3),
+                         "GBps_alg": round(k["alg_bytes"] / (k["ms"] * 1e-3) / 1e9, 3) if k["ms"] > 0 else None}
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="pe150_3g", choices=sorted(WORKLOADS))
+    ap.add_argument("--pairs", type=int, default=500_000, help="pairs (SE: reads) per step per GPU")
+    ap.add_argument("--threads", type=int, default=0, help="host pipeline threads (0: all host cores, max 32)")
+    ap.add_argument("--chunk-size", type=int, default=10000)
+    ap.add_argument("--ref-seed", type=int, default=1)
+    ap.add_argument("--read-seed", type=int, default=7)
+    ap.add_argument("--cpu-pairs", type=int, default=200_000, help="cpu_baseline sample (pairs)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ref-len", type=int, default=0, help="override reference length (testing only)")
+    ap.add_argument("--stats-out", default="", help="write per-kernel stats JSON here")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(rank, f"note: WORLD_SIZE={world} but --gpus {args.gpus}; using WORLD_SIZE")
+    wl = dict(WORKLOADS[args.workload])
+    if args.ref_len:
+        wl["ref_len"] = args.ref_len
+    cores = host_cores()
+    threads = args.threads or min(32, cores)
+
+    # torch first: its libamdhip64 (soname libamdhip64.so.7) is then the one
+    # runtime of the process and librsa_gpu.so binds to it; loading ours first
+    # would put two HIP runtimes in one process (torch needs "libamdhip64.so").
+    import torch
+    import torch.distributed as dist
+    from rabbitsalign_amd import mapper as M
+    M.load()
+
+    has_gpu = torch.cuda.is_available()
+    if not has_gpu:
+        raise SystemExit("bench.py needs a GPU (the product path has no CPU fallback)")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def allreduce(v: float, op) -> float:
+        if world == 1:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=op)
+        return float(t.item())
+
+    t = time.time()
+    log(rank, f"building {wl['ref_len']/1e9:.3f} Gb reference ({wl['n_contigs']} contigs) + index, {threads} threads")
+    m = M.Mapper.synthetic(args.ref_seed, wl["ref_len"], wl["n_contigs"], wl["read_len"], device=local_rank,
+                           threads=threads)
+    info = m.info()
+    log(rank, f"index ready in {time.time()-t:.1f} s: {info['n_randstrobes']} randstrobes, bits {info['bits']}, "
+              f"upload {info['upload_seconds']:.2f} s, engine {m.engine}")
+
+    P = args.pairs
+    total_steps = args.warmup + args.steps
+    batches = []
+    t = time.time()
+    for s in range(total_steps):
+        first = (rank * total_steps + s) * P
+        batches.append(m.synthetic_reads(args.read_seed, first, P, wl["read_len"], wl["mu"], wl["sigma"],
+                                         wl["paired"]))
+    log(rank, f"generated {total_steps} x {P} {'pairs' if wl['paired'] else 'reads'} in {time.time()-t:.1f} s")
+
+    for s in range(args.warmup):
+        st = m.map(batches[s], threads=threads, chunk_size=args.chunk_size)
+        log(rank, f"warmup {s}: {st.n_reads} reads in {st.map_seconds:.3f} s")
+    m.reset_kernel_stats()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n_reads = 0
+    hashes = []
+    for s in range(args.warmup, total_steps):
+        st = m.map(batches[s], threads=threads, chunk_size=args.chunk_size)
+        n_reads += st.n_reads
+        hashes.append(st.sam_hash)
+        log(rank, f"step {s - args.warmup}: {st.n_reads} reads in {st.map_seconds:.3f} s "
+                  f"({st.n_reads / st.map_seconds / 1e6:.4f} Mreads/s), SW {st.sw_calls}")
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    ks = m.kernel_stats()
+
+    elapsed_max = allreduce(elapsed, dist.ReduceOp.MAX if world > 1 else None)
+    reads_all = allreduce(float(n_reads), dist.ReduceOp.SUM if world > 1 else None)
+    for b in batches:
+        b.close()
+
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if os.path.exists(REF_CPU_LIB):
+            n_cpu = min(args.cpu_pairs, P)
+            sample = m.synthetic_reads(args.read_seed, 0, n_cpu, wl["read_len"], wl["mu"], wl["sigma"], wl["paired"])
+            g = m.map(sample, threads=threads, chunk_size=args.chunk_size)
+            log(rank, f"cpu_baseline: opening CPU path on the same index ({cores} cores)")
+            cm = m.like(device=0, threads=cores, lib_path=REF_CPU_LIB)
+            c = cm.map(sample, threads=cores, chunk_size=args.chunk_size)
+            cm.close()
+            cpu = {"value": round(c.n_reads / c.map_seconds / 1e6, 6), "unit": "Mreads/s", "cores": cores,
+                   "kind": "reference",
+                   "sample": f"{n_cpu} {'pairs' if wl['paired'] else 'reads'} of the same workload "
+                             f"({c.n_reads} reads, {c.map_seconds:.2f} s wall), -t {cores}, chunk {args.chunk_size}; "
+                             "reference randstrobes/nam/ssw.c objects + restated host pipeline"}
+            parity = {"sample_reads": c.n_reads, "sam_bytes": c.sam_bytes, "gpu_sam_hash": f"{g.sam_hash:016x}",
+                      "cpu_sam_hash": f"{c.sam_hash:016x}", "sam_identical": g.sam_hash == c.sam_hash
+                      and g.sam_bytes == c.sam_bytes}
+            log(rank, f"cpu_baseline {cpu['value']} Mreads/s; SAM identical on sample: {parity['sam_identical']}")
+            sample.close()
+        else:
+            log(rank, f"cpu_baseline skipped: {REF_CPU_LIB} not built")
+
+    if rank == 0:
+        value = reads_all / elapsed_max / 1e6
+        rl = roofline(ks)
+        line = {
+            "metric": "Mreads/s aligned (PE 2x150 vs 3 Gb, SAM bit-exact vs CPU)" if args.workload == "pe150_3g"
+            else f"Mreads/s aligned ({args.workload})",
+            "value": round(value, 6), "unit": "Mreads/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed_max / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32",
+            "data": "synthetic (seeded reference + reads, SURVEY.md Appendix D)",
+            "config": {"workload": wl["desc"], "reference_bp": wl["ref_len"], "contigs": wl["n_contigs"],
+                       "read_len": wl["read_len"], "paired": wl["paired"], "pairs_per_step_per_gpu": P,
+                       "host_threads": threads, "chunk_size": args.chunk_size, "index_bits": info["bits"],
+                       "randstrobes": info["n_randstrobes"], "parallelism": f"dp{world} (replicated index)"},
+            "roofline": rl,
+            "cpu_baseline": cpu,
+            "parity": parity,
+            "kernels": kernel_table(ks),
+            "device_counters": {k: v for k, v in ks.items() if k != "kernels"},
+            "sam_hashes": [f"{h:016x}" for h in hashes],
+        }
+        if args.stats_out:
+            with open(args.stats_out, "w") as f:
+                json.dump({"kernel_stats": ks, "info": info, "line": line}, f, indent=1)
+        print(json.dumps(line), flush=True)
+    m.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

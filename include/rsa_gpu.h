@@ -172,11 +172,25 @@ uint64_t rsa_extend_cigar_bound(const rsa_job_batch* jobs);
 
 /* ---- instrumentation ------------------------------------------------------ */
 
+/* kernels of the path, in stats arrays */
+enum {
+    RSA_K_RANDSTROBES = 0, /* syncmers + randstrobes per read (randstrobes.cpp:57-254) */
+    RSA_K_LOOKUP = 1,      /* bucket lookup, filter probe, min_diff count (nam.cpp:68-85,920-943) */
+    RSA_K_FIND_NAMS = 2,   /* hits_per_ref + merge_hits_into_nams (nam.cpp:87-245) */
+    RSA_K_RESCUE = 3,      /* find_nams_rescue (nam.cpp:946-1010) */
+    RSA_K_COMPACT = 4,     /* NAM output compaction */
+    RSA_K_EXT_SCAN = 5,    /* SSW forward/reverse score scans (ssw.c:121-620) */
+    RSA_K_EXT_BAND = 6,    /* banded_sw traceback + Aligner::align (ssw.c:622-790, aligner.cpp:114-210) */
+    RSA_K_COUNT = 7
+};
+
 typedef struct rsa_kernel_stats {
-    double seed_ms, lookup_ms, nam_ms, ext_scan_ms, ext_band_ms;  /* cumulative HIP-event time */
+    double kernel_ms[RSA_K_COUNT];   /* sum of per-launch HIP-event durations (launch stream) */
+    uint64_t launches[RSA_K_COUNT];
+    double alg_bytes[RSA_K_COUNT];   /* algorithmic HBM bytes (DESIGN.md "Kernels") */
     uint64_t seed_calls, ext_calls;
-    uint64_t reads, query_randstrobes, lookups_found, hits, nams;     /* device counters */
-    uint64_t jobs, dp_cells;
+    uint64_t reads, read_bases, query_randstrobes, lookups_found, filtered, hits, nams, rescued_reads;
+    uint64_t jobs, dp_cells;         /* dp_cells: sum query_len * ref_len of the forward scan */
 } rsa_kernel_stats;
 
 int rsa_get_stats(rsa_ctx* ctx, rsa_kernel_stats* out);

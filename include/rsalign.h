@@ -1,0 +1,71 @@
+/*
+ * rsalign.h -- C-ABI of the whole mapping path (host pipeline + GPU engine),
+ * librsalign.so.  It is the library form of the reference's CLI entry
+ * (run_rabbitsalign, src/main.cpp:240-617: read references, load/build the
+ * .sti index, spawn workers over read chunks, write SAM) so that a binding can
+ * drive mapping without a subprocess.  bench.py and the Python mirror
+ * (rabbitsalign_amd/mapper.py) use it through ctypes.
+ */
+#ifndef RSALIGN_H
+#define RSALIGN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "rsa_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rsam rsam;              /* reference + index (+ engine) */
+typedef struct rsam_reads rsam_reads;  /* a read set held in host memory */
+
+typedef struct rsam_stats {
+    uint64_t n_reads;         /* reads mapped (each mate counts, pc.cpp:1596) */
+    uint64_t sam_bytes;       /* SAM body bytes produced */
+    uint64_t sam_hash;        /* FNV-1a 64 of the SAM body, in output order */
+    uint64_t sw_calls, tried, nam_rescue, mate_rescue, inconsistent;
+    double map_seconds;       /* first chunk read -> last SAM byte (consumer cost, main.cpp:446,595) */
+} rsam_stats;
+
+/* Open from files: FASTA + optional .sti (NULL: build the index in memory). */
+rsam* rsam_open_files(const char* ref_fa, const char* sti, int read_len, int device, int threads, char* err,
+                      size_t err_len);
+/* Open on a synthetic reference (seeded): n_contigs equal contigs. */
+rsam* rsam_open_synthetic(uint64_t seed, uint64_t ref_len, int n_contigs, int read_len, int device, int threads,
+                          char* err, size_t err_len);
+/* Open on the host-side reference + index of another mapper (no rebuild). */
+rsam* rsam_open_like(const rsam* other, int device, int threads, char* err, size_t err_len);
+void rsam_close(rsam* m);
+
+/* index/reference shape of a mapper */
+typedef struct rsam_info {
+    uint64_t ref_bases, n_randstrobes;
+    int32_t n_contigs, bits, filter_cutoff, k, canonical_read_length;
+    double index_seconds, upload_seconds;
+    uint64_t device_resident_bytes;
+} rsam_info;
+int rsam_get_info(const rsam* m, rsam_info* out);
+
+rsam_reads* rsam_reads_load(const char* fq1, const char* fq2 /* NULL: single-end */);
+/* pairs p in [first, first + n) of the synthetic stream `seed` (paired or SE with mate 1 only) */
+rsam_reads* rsam_reads_synthetic(const rsam* m, uint64_t seed, uint64_t first, uint64_t n, int read_len,
+                                 double mu, double sigma, int paired);
+uint64_t rsam_reads_count(const rsam_reads* r);
+void rsam_reads_free(rsam_reads* r);
+
+/* Map every read; SAM to `sam_path` (header + body) or kept in memory only when NULL. */
+int rsam_map(rsam* m, const rsam_reads* reads, int threads, int chunk_size, const char* sam_path,
+             rsam_stats* out);
+
+/* GPU kernel statistics of the engine (zeros for a CPU engine). */
+int rsam_kernel_stats(rsam* m, rsa_kernel_stats* out);
+void rsam_reset_kernel_stats(rsam* m);
+const char* rsam_engine_name(const rsam* m);
+const char* rsam_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -2,7 +2,6 @@
 // aln.cpp/pc.cpp/sam.cpp) driven by the C restatement of the hot path
 // (rsa_oracle.c) instead of the GPU.  TEST INFRASTRUCTURE ONLY: it is the
 // parity reference for end-to-end SAM and bench.py's cpu_baseline leg.
-#define RSA_NO_MAIN
 #include <cstring>
 #include <stdexcept>
 
@@ -86,4 +85,13 @@ std::unique_ptr<rsa::Engine> make_cpu_engine(const rsa::References& refs, const 
 
 }  // namespace
 
+// engine of the CPU-path build of librsalign (capi.cpp)
+namespace rsa {
+std::unique_ptr<Engine> make_default_engine(const References& refs, const StiIndex& idx, int device) {
+    return make_cpu_engine(refs, idx, device);
+}
+}  // namespace rsa
+
+#ifndef RSA_ENGINE_LIB
 int main(int argc, char** argv) { return rsa::cli_main(argc, argv, make_cpu_engine, "rsalign_cpu"); }
+#endif

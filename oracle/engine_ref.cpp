@@ -7,7 +7,6 @@
 // ext/ssw/ssw_cpp.cpp and src/aligner.cpp include a CUDA header and cannot be
 // built here.  TEST INFRASTRUCTURE ONLY: end-to-end SAM parity reference and
 // bench.py's cpu_baseline leg ("kind": "reference").
-#define RSA_NO_MAIN
 #include <cstring>
 #include <stdexcept>
 
@@ -121,4 +120,13 @@ std::unique_ptr<rsa::Engine> make_ref_engine(const rsa::References& refs, const 
 
 }  // namespace
 
+// engine of the CPU-path build of librsalign (capi.cpp)
+namespace rsa {
+std::unique_ptr<Engine> make_default_engine(const References& refs, const StiIndex& idx, int device) {
+    return make_ref_engine(refs, idx, device);
+}
+}  // namespace rsa
+
+#ifndef RSA_ENGINE_LIB
 int main(int argc, char** argv) { return rsa::cli_main(argc, argv, make_ref_engine, "rsalign_ref"); }
+#endif

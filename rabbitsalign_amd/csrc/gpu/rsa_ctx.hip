@@ -17,6 +17,7 @@
 
 #include "rsa_ext.h"
 #include "rsa_seed.h"
+#include "rsa_timer.h"
 
 __global__ void k_ext_scan(const ExtJobDev* jobs, int n_jobs, const char* qbuf, const char* ref, ScanRes* out,
                            int match, int mismatch, int gO, int gE);
@@ -25,9 +26,8 @@ __global__ void k_ext_band(const ExtJobDev* jobs, const ScanRes* scan, int n_job
                            int64_t scr_stride, int arr_cap, int64_t dir_cap, int match, int mismatch, int gO,
                            int gE, int bonus, int* overflow);
 
-int seed_run(SeedBufs& b, hipStream_t st, hipEvent_t* ev, const SeedIndexParams& p, const rsa_read_batch* rb,
-             int32_t rescue_level, uint32_t rescue_cutoff, rsa_nam_batch* out, std::string& err, float* ms,
-             uint64_t* counters);
+int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, const rsa_read_batch* rb,
+             int32_t rescue_level, uint32_t rescue_cutoff, rsa_nam_batch* out, std::string& err, SeedCounters& c);
 int seed_randstrobes_run(SeedBufs& b, hipStream_t st, const SeedIndexParams& p, const rsa_read_batch* rb,
                          rsa_randstrobe_batch* out, std::string& err);
 
@@ -76,7 +76,7 @@ struct HostBuf {
 
 struct Lane {
     hipStream_t stream = nullptr;
-    hipEvent_t ev[8];
+    KTimer kt;
     bool busy = false;
     // extension
     DevBuf d_q, d_jobs, d_scan, d_alns, d_cig, d_scratch, d_over, d_idx;
@@ -123,7 +123,6 @@ static Lane* acquire_lane(rsa_ctx* ctx) {
         if (ctx->lanes.size() < 16) {
             Lane* l = new Lane();
             if (hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking) != hipSuccess) { delete l; return nullptr; }
-            for (auto& e : l->ev) (void)hipEventCreate(&e);
             l->busy = true;
             ctx->lanes.push_back(l);
             return l;
@@ -199,7 +198,7 @@ void rsa_close(rsa_ctx* ctx) {
         l->d_scratch.release(); l->d_over.release(); l->d_idx.release();
         l->h_q.release(); l->h_jobs.release(); l->h_over.release();
         seed_bufs_release(l->sb);
-        for (auto& e : l->ev) (void)hipEventDestroy(e);
+        l->kt.destroy();
         if (l->stream) (void)hipStreamDestroy(l->stream);
         delete l;
     }
@@ -284,22 +283,24 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
     HIPCHK(hipMemcpyAsync(L->d_q.p, jb->queries, jb->queries_len, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(L->d_jobs.p, hj, sizeof(ExtJobDev) * n, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemsetAsync(L->d_over.p, 0, sizeof(int) * n, st));
-    HIPCHK(hipEventRecord(L->ev[0], st));
+    L->kt.reset();
+    L->kt.begin(st, RSA_K_EXT_SCAN);
     hipLaunchKernelGGL(k_ext_scan, dim3((n + 3) / 4), dim3(256), 0, st, L->d_jobs.as<ExtJobDev>(), (int)n,
                        L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(), jb->match, jb->mismatch,
                        jb->gap_open, jb->gap_extend);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(L->ev[1], st));
+    L->kt.end(st);
     for (uint32_t base = 0; base < n; base += chunk) {
         const int cnt = (int)std::min<uint32_t>(chunk, n - base);
+        L->kt.begin(st, RSA_K_EXT_BAND);
         hipLaunchKernelGGL(k_ext_band, dim3((cnt + 63) / 64), dim3(64), 0, st, L->d_jobs.as<ExtJobDev>(),
                            L->d_scan.as<ScanRes>(), cnt, (const int*)nullptr, (int)base, L->d_q.as<char>(), ctx->d_ref,
                            L->d_cig.as<uint32_t>(), L->d_alns.as<rsa_aln>(), L->d_scratch.as<uint8_t>(), stride,
                            BAND_ARR_CAP, BAND_DIR_CAP, jb->match, jb->mismatch, jb->gap_open, jb->gap_extend,
                            jb->end_bonus, L->d_over.as<int>());
         HIPCHK(hipGetLastError());
+        L->kt.end(st);
     }
-    HIPCHK(hipEventRecord(L->ev[2], st));
     HIPCHK(L->h_over.ensure(sizeof(int) * n));
     HIPCHK(hipMemcpyAsync(L->h_over.p, L->d_over.p, sizeof(int) * n, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -314,12 +315,14 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
         HIPCHK(hipMemcpyAsync(L->d_idx.p, big.data(), sizeof(int) * big.size(), hipMemcpyHostToDevice, st));
         for (size_t b = 0; b < big.size(); b += BIG_CHUNK) {
             const int cnt = (int)std::min<size_t>(BIG_CHUNK, big.size() - b);
+            L->kt.begin(st, RSA_K_EXT_BAND);
             hipLaunchKernelGGL(k_ext_band, dim3(1), dim3(64), 0, st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(),
                                cnt, L->d_idx.as<int>() + b, 0, L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(),
                                L->d_alns.as<rsa_aln>(), L->d_scratch.as<uint8_t>(), bstride, BIG_ARR_CAP, BIG_DIR_CAP,
                                jb->match, jb->mismatch, jb->gap_open, jb->gap_extend, jb->end_bonus,
                                L->d_over.as<int>());
             HIPCHK(hipGetLastError());
+            L->kt.end(st);
         }
         HIPCHK(hipMemcpyAsync(L->h_over.p, L->d_over.p, sizeof(int) * n, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
@@ -329,13 +332,18 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
     HIPCHK(hipMemcpyAsync(out->alns, L->d_alns.p, sizeof(rsa_aln) * n, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(out->cigar_pool, L->d_cig.p, sizeof(uint32_t) * bound, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    float t_scan = 0, t_band = 0;
-    (void)hipEventElapsedTime(&t_scan, L->ev[0], L->ev[1]);
-    (void)hipEventElapsedTime(&t_band, L->ev[1], L->ev[2]);
+    uint64_t qr_bytes = 0, cig_ops = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        qr_bytes += (uint64_t)hj[i].qlen + hj[i].rlen;
+        cig_ops += out->alns[i].cigar_len;
+    }
     {
         std::lock_guard<std::mutex> g(ctx->stat_m);
-        ctx->stats.ext_scan_ms += t_scan;
-        ctx->stats.ext_band_ms += t_band;
+        L->kt.collect(ctx->stats.kernel_ms, ctx->stats.launches);
+        // scan: query + window in, ScanRes out; band: the same bytes again, ScanRes in, rsa_aln + CIGAR out
+        ctx->stats.alg_bytes[RSA_K_EXT_SCAN] += (double)qr_bytes + (double)(sizeof(ExtJobDev) + sizeof(ScanRes)) * n;
+        ctx->stats.alg_bytes[RSA_K_EXT_BAND] += (double)qr_bytes + (double)(sizeof(ExtJobDev) + sizeof(ScanRes) +
+                                                                            sizeof(rsa_aln)) * n + 4.0 * cig_ops;
         ctx->stats.ext_calls++;
         ctx->stats.jobs += n;
         ctx->stats.dp_cells += cells;
@@ -376,20 +384,22 @@ int rsa_seed(rsa_ctx* ctx, const rsa_read_batch* rb, int32_t rescue_level, uint3
     if (!L) { set_err(ctx, "cannot create HIP stream"); return RSA_ERR_HIP; }
     LaneGuard guard{ctx, L};
     std::string err;
-    float ms[3] = {0, 0, 0};
-    uint64_t cnt[5] = {0, 0, 0, 0, 0};
-    rc = seed_run(L->sb, L->stream, L->ev, ctx->ip, rb, rescue_level, rescue_cutoff, out, err, ms, cnt);
+    SeedCounters c;
+    L->kt.reset();
+    rc = seed_run(L->sb, L->stream, L->kt, ctx->ip, rb, rescue_level, rescue_cutoff, out, err, c);
     if (rc) { set_err(ctx, err); return rc; }
     std::lock_guard<std::mutex> g(ctx->stat_m);
-    ctx->stats.seed_ms += ms[0];
-    ctx->stats.lookup_ms += ms[1];
-    ctx->stats.nam_ms += ms[2];
+    L->kt.collect(ctx->stats.kernel_ms, ctx->stats.launches);
+    for (int k = 0; k < RSA_K_COUNT; ++k) ctx->stats.alg_bytes[k] += c.alg_bytes[k];
     ctx->stats.seed_calls++;
-    ctx->stats.reads += cnt[0];
-    ctx->stats.query_randstrobes += cnt[1];
-    ctx->stats.lookups_found += cnt[2];
-    ctx->stats.hits += cnt[3];
-    ctx->stats.nams += cnt[4];
+    ctx->stats.reads += c.reads;
+    ctx->stats.read_bases += c.read_bases;
+    ctx->stats.query_randstrobes += c.qrs;
+    ctx->stats.lookups_found += c.found;
+    ctx->stats.filtered += c.filtered;
+    ctx->stats.hits += c.hits;
+    ctx->stats.nams += c.nams;
+    ctx->stats.rescued_reads += c.rescued;
     return RSA_OK;
 }
 

@@ -1,0 +1,48 @@
+// rsa_timer.h -- per-launch HIP-event timing of the path's kernels.  Each lane
+// owns one KTimer; events are recorded on the lane's stream around every
+// launch and read back after the lane's final synchronisation.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "../../../include/rsa_gpu.h"
+
+struct KTimer {
+    std::vector<hipEvent_t> ev;
+    std::vector<int> kind;
+    size_t used = 0;
+
+    void reset() { used = 0; kind.clear(); }
+    hipEvent_t take() {
+        if (used == ev.size()) {
+            hipEvent_t e = nullptr;
+            (void)hipEventCreate(&e);
+            ev.push_back(e);
+        }
+        return ev[used++];
+    }
+    void begin(hipStream_t s, int k) { (void)hipEventRecord(take(), s); kind.push_back(k); }
+    void end(hipStream_t s) { (void)hipEventRecord(take(), s); }
+    // call after the stream has been synchronised
+    void collect(double* ms, uint64_t* launches) const {
+        for (size_t i = 0; i < kind.size(); ++i) {
+            float t = 0;
+            (void)hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]);
+            ms[kind[i]] += t;
+            launches[kind[i]] += 1;
+        }
+    }
+    void destroy() {
+        for (auto e : ev) (void)hipEventDestroy(e);
+        ev.clear();
+        reset();
+    }
+};
+
+// per-call counters and algorithmic bytes of the seeding kernels
+struct SeedCounters {
+    uint64_t reads = 0, read_bases = 0, qrs = 0, found = 0, filtered = 0, hits = 0, nams = 0, rescued = 0;
+    double alg_bytes[RSA_K_COUNT] = {0};
+};

@@ -29,6 +29,7 @@
 
 #include "rsa_dev.h"
 #include "rsa_seed.h"
+#include "rsa_timer.h"
 
 #define END64 0xFFFFFFFFFFFFFFFFULL
 
@@ -42,6 +43,7 @@ struct QrsInfo {            // per query randstrobe, filled by k_lookup
 
 struct ReadStat {
     uint32_t found, good, hits_find, hits_all;
+    uint32_t scan_find, scan_all;   // index entries read by the min_diff pass (instrumentation)
 };
 
 struct HitD {
@@ -189,7 +191,7 @@ k_lookup(const rsa_query_randstrobe* __restrict__ qrs, const uint32_t* __restric
     const int r = wave;
     const int nq = (int)qcnt[r];
     const uint64_t base = qbase[r];
-    uint32_t found = 0, good = 0, hfind = 0, hall = 0;
+    uint32_t found = 0, good = 0, hfind = 0, hall = 0, sfind = 0, sall = 0;
     for (int i = lane; i < nq; i += 64) {
         const rsa_query_randstrobe q = qrs[base + i];
         QrsInfo o;
@@ -221,8 +223,10 @@ k_lookup(const rsa_query_randstrobe* __restrict__ qrs, const uint32_t* __restric
                     o.hits = h;
                 }
                 found++;
-                if (!(o.flags & 2)) { good++; hfind += o.hits; }
+                const uint32_t scanned = o.count <= 1000 ? o.count : 0;
+                if (!(o.flags & 2)) { good++; hfind += o.hits; sfind += scanned; }
                 if (o.count <= 1000) hall += o.hits;
+                sall += scanned;
             }
         }
         qi[base + i] = o;
@@ -232,8 +236,14 @@ k_lookup(const rsa_query_randstrobe* __restrict__ qrs, const uint32_t* __restric
         good += __shfl_xor(good, off, 64);
         hfind += __shfl_xor(hfind, off, 64);
         hall += __shfl_xor(hall, off, 64);
+        sfind += __shfl_xor(sfind, off, 64);
+        sall += __shfl_xor(sall, off, 64);
     }
-    if (lane == 0) { ReadStat s; s.found = found; s.good = good; s.hits_find = hfind; s.hits_all = hall; st[r] = s; }
+    if (lane == 0) {
+        ReadStat s;
+        s.found = found; s.good = good; s.hits_find = hfind; s.hits_all = hall; s.scan_find = sfind; s.scan_all = sall;
+        st[r] = s;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -743,7 +753,7 @@ static const uint32_t MAP_BIG = 65536 + 512;
 
 // Stage 1 (shared by rsa_randstrobes and rsa_seed): upload reads, run k_randstrobes.
 int seed_stage_randstrobes(SeedBufs& b, hipStream_t st, const SeedIndexParams& p, const rsa_read_batch* rb,
-                           std::vector<uint64_t>& qbase, std::string& err) {
+                           std::vector<uint64_t>& qbase, std::string& err, KTimer* kt) {
     const uint32_t n = rb->n_reads;
     qbase.assign(n + 1, 0);
     uint64_t total_len = 0;
@@ -762,10 +772,12 @@ int seed_stage_randstrobes(SeedBufs& b, hipStream_t st, const SeedIndexParams& p
     SCHK(hipMemcpyAsync(b.p[B_ROFF], rb->offsets, 8ull * n, hipMemcpyHostToDevice, st));
     SCHK(hipMemcpyAsync(b.p[B_RLEN], rb->lengths, 4ull * n, hipMemcpyHostToDevice, st));
     SCHK(hipMemcpyAsync(b.p[B_QBASE], qbase.data(), 8ull * (n + 1), hipMemcpyHostToDevice, st));
+    if (kt) kt->begin(st, RSA_K_RANDSTROBES);
     hipLaunchKernelGGL(k_randstrobes, dim3((n + 63) / 64), dim3(64), 0, st, DP(B_SEQ, char), DP(B_ROFF, uint64_t),
                        DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n, p, DP(B_SYNC, SyncD),
                        DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
     SCHK(hipGetLastError());
+    if (kt) kt->end(st);
     return RSA_OK;
 }
 
@@ -773,7 +785,7 @@ int seed_randstrobes_run(SeedBufs& b, hipStream_t st, const SeedIndexParams& p, 
                          rsa_randstrobe_batch* out, std::string& err) {
     const uint32_t n = rb->n_reads;
     std::vector<uint64_t> qbase;
-    int rc = seed_stage_randstrobes(b, st, p, rb, qbase, err);
+    int rc = seed_stage_randstrobes(b, st, p, rb, qbase, err, nullptr);
     if (rc) return rc;
     std::vector<uint32_t> cnt(n);
     SCHK(hipMemcpyAsync(cnt.data(), b.p[B_QCNT], 4ull * n, hipMemcpyDeviceToHost, st));
@@ -791,21 +803,19 @@ int seed_randstrobes_run(SeedBufs& b, hipStream_t st, const SeedIndexParams& p, 
     return RSA_OK;
 }
 
-int seed_run(SeedBufs& b, hipStream_t st, hipEvent_t* ev, const SeedIndexParams& p, const rsa_read_batch* rb,
-             int32_t rescue_level, uint32_t rescue_cutoff, rsa_nam_batch* out, std::string& err, float* ms,
-             uint64_t* counters) {
+int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, const rsa_read_batch* rb,
+             int32_t rescue_level, uint32_t rescue_cutoff, rsa_nam_batch* out, std::string& err, SeedCounters& c) {
     const uint32_t n = rb->n_reads;
     std::vector<uint64_t> qbase;
-    SCHK(hipEventRecord(ev[0], st));
-    int rc = seed_stage_randstrobes(b, st, p, rb, qbase, err);
+    int rc = seed_stage_randstrobes(b, st, p, rb, qbase, err, &kt);
     if (rc) return rc;
-    SCHK(hipEventRecord(ev[1], st));
     SCHK(dens(b, B_QI, sizeof(QrsInfo) * (qbase[n] + 1)));
     SCHK(dens(b, B_ST, sizeof(ReadStat) * n));
+    kt.begin(st, RSA_K_LOOKUP);
     hipLaunchKernelGGL(k_lookup, dim3((n + 3) / 4), dim3(256), 0, st, DP(B_QRS, rsa_query_randstrobe),
                        DP(B_QCNT, uint32_t), DP(B_QBASE, uint64_t), (int)n, p, DP(B_QI, QrsInfo), DP(B_ST, ReadStat));
     SCHK(hipGetLastError());
-    SCHK(hipEventRecord(ev[2], st));
+    kt.end(st);
     SCHK(hens(b, H_ST, sizeof(ReadStat) * n));
     SCHK(hipMemcpyAsync(b.h[H_ST], b.p[B_ST], sizeof(ReadStat) * n, hipMemcpyDeviceToHost, st));
     SCHK(hens(b, H_CNT, 4ull * n));
@@ -815,11 +825,16 @@ int seed_run(SeedBufs& b, hipStream_t st, hipEvent_t* ev, const SeedIndexParams&
     SCHK(hens(b, H_HOFF, 8ull * (n + 1)));
     uint64_t* hoff = HP(H_HOFF, uint64_t);
     hoff[0] = 0;
-    uint64_t n_qrs = 0, n_found = 0;
+    uint64_t n_qrs = 0, n_found = 0, n_good = 0, scan_find = 0, scan_all = 0, bases = 0;
+    std::vector<uint32_t> qcnt(HP(H_CNT, uint32_t), HP(H_CNT, uint32_t) + n);
     for (uint32_t i = 0; i < n; ++i) {
         hoff[i + 1] = hoff[i] + hs[i].hits_find;
-        n_qrs += HP(H_CNT, uint32_t)[i];
+        n_qrs += qcnt[i];
         n_found += hs[i].found;
+        n_good += hs[i].good;
+        scan_find += hs[i].scan_find;
+        scan_all += hs[i].scan_all;
+        bases += rb->lengths[i];
     }
     const uint64_t H = hoff[n];
     SCHK(dens(b, B_HOFF, 8ull * (n + 1)));
@@ -836,12 +851,14 @@ int seed_run(SeedBufs& b, hipStream_t st, hipEvent_t* ev, const SeedIndexParams&
     for (uint32_t a = 0; a < n; a += chunk) {
         const uint32_t cnt = std::min(chunk, n - a);
         // reads [a, a+cnt) use map slots [0, cnt): pass a list-less launch by offsetting pointers
+        kt.begin(st, RSA_K_FIND_NAMS);
         hipLaunchKernelGGL(k_find_nams, dim3((cnt + 63) / 64), dim3(64), 0, st, DP(B_QRS, rsa_query_randstrobe),
                            DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t) + a, DP(B_QBASE, uint64_t) + a, DP(B_ST, ReadStat) + a,
                            DP(B_HOFF, uint64_t) + a, (int)cnt, (const int*)nullptr, p, DP(B_HITS, HitD),
                            DP(B_OPEN, rsa_nam), DP(B_NAM1, rsa_nam), DP(B_MAP, uint8_t), MAP_SMALL,
                            DP(B_NCNT1, uint32_t) + a, DP(B_NONREP, float) + a, DP(B_FLAGS, uint32_t) + a);
         SCHK(hipGetLastError());
+        kt.end(st);
     }
     SCHK(hens(b, H_FLAGS, 4ull * n));
     SCHK(hipMemcpyAsync(b.h[H_FLAGS], b.p[B_FLAGS], 4ull * n, hipMemcpyDeviceToHost, st));
@@ -858,19 +875,20 @@ int seed_run(SeedBufs& b, hipStream_t st, hipEvent_t* ev, const SeedIndexParams&
         SCHK(hipMemcpyAsync(b.p[B_LIST], big.data(), 4ull * big.size(), hipMemcpyHostToDevice, st));
         for (size_t a = 0; a < big.size(); a += bchunk) {
             const int cnt = (int)std::min<size_t>(bchunk, big.size() - a);
+            kt.begin(st, RSA_K_FIND_NAMS);
             hipLaunchKernelGGL(k_find_nams, dim3(1), dim3(64), 0, st, DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo),
                                DP(B_QCNT, uint32_t), DP(B_QBASE, uint64_t), DP(B_ST, ReadStat), DP(B_HOFF, uint64_t), cnt,
                                DP(B_LIST, int) + a, p, DP(B_HITS, HitD), DP(B_OPEN, rsa_nam), DP(B_NAM1, rsa_nam),
                                DP(B_MAP, uint8_t), MAP_BIG, DP(B_NCNT1, uint32_t), DP(B_NONREP, float),
                                DP(B_FLAGS, uint32_t));
             SCHK(hipGetLastError());
+            kt.end(st);
         }
         SCHK(hipMemcpyAsync(b.h[H_FLAGS], b.p[B_FLAGS], 4ull * n, hipMemcpyDeviceToHost, st));
         SCHK(hipMemcpyAsync(b.h[H_CNT], b.p[B_NCNT1], 4ull * n, hipMemcpyDeviceToHost, st));
         SCHK(hipStreamSynchronize(st));
         for (int i : big) if (HP(H_FLAGS, uint32_t)[i] & 2u) { err = "rsa_seed: robin_hood emulation overflow"; return RSA_ERR_NOMEM; }
     }
-    SCHK(hipEventRecord(ev[3], st));
     // nonrepetitive fraction to host
     SCHK(hipMemcpyAsync(out->nonrepetitive_fraction, b.p[B_NONREP], 4ull * n, hipMemcpyDeviceToHost, st));
     SCHK(hipStreamSynchronize(st));
@@ -904,12 +922,14 @@ int seed_run(SeedBufs& b, hipStream_t st, hipEvent_t* ev, const SeedIndexParams&
         uint8_t* added = (uint8_t*)(grp + (R + 1));
         for (size_t a = 0; a < resc.size(); a += chunk) {
             const int cnt = (int)std::min<size_t>(chunk, resc.size() - a);
+            kt.begin(st, RSA_K_RESCUE);
             hipLaunchKernelGGL(k_rescue, dim3((cnt + 63) / 64), dim3(64), 0, st, DP(B_QRS, rsa_query_randstrobe),
                                DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t), DP(B_QBASE, uint64_t), DP(B_ROFF2, uint64_t), cnt,
                                DP(B_LIST, int) + a, p, rescue_cutoff, DP(B_RBUF, RescueD), DP(B_HITS, HitD),
                                DP(B_OPEN, rsa_nam), DP(B_NAM2, rsa_nam), grp, added, DP(B_MAP, uint8_t), MAP_SMALL,
                                DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t));
             SCHK(hipGetLastError());
+            kt.end(st);
         }
         SCHK(hipMemcpyAsync(b.h[H_FLAGS], b.p[B_FLAGS], 4ull * n, hipMemcpyDeviceToHost, st));
         SCHK(hipStreamSynchronize(st));
@@ -923,12 +943,14 @@ int seed_run(SeedBufs& b, hipStream_t st, hipEvent_t* ev, const SeedIndexParams&
             SCHK(hipMemcpyAsync(b.p[B_LIST], bigr.data(), 4ull * bigr.size(), hipMemcpyHostToDevice, st));
             for (size_t a = 0; a < bigr.size(); a += bchunk) {
                 const int cnt = (int)std::min<size_t>(bchunk, bigr.size() - a);
+                kt.begin(st, RSA_K_RESCUE);
                 hipLaunchKernelGGL(k_rescue, dim3(1), dim3(64), 0, st, DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo),
                                    DP(B_QCNT, uint32_t), DP(B_QBASE, uint64_t), DP(B_ROFF2, uint64_t), cnt,
                                    DP(B_LIST, int) + a, p, rescue_cutoff, DP(B_RBUF, RescueD), DP(B_HITS, HitD),
                                    DP(B_OPEN, rsa_nam), DP(B_NAM2, rsa_nam), grp, added, DP(B_MAP, uint8_t), MAP_BIG,
                                    DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t));
                 SCHK(hipGetLastError());
+                kt.end(st);
             }
             SCHK(hipMemcpyAsync(b.h[H_FLAGS], b.p[B_FLAGS], 4ull * n, hipMemcpyDeviceToHost, st));
             SCHK(hipStreamSynchronize(st));
@@ -957,19 +979,26 @@ int seed_run(SeedBufs& b, hipStream_t st, hipEvent_t* ev, const SeedIndexParams&
     SCHK(dens(b, B_OOFF, 8ull * (n + 1)));
     SCHK(dens(b, B_OUT, std::max(b.cap[B_OUT], sizeof(rsa_nam) * (total + 1))));
     SCHK(hipMemcpyAsync(b.p[B_OOFF], ooff, 8ull * (n + 1), hipMemcpyHostToDevice, st));
+    kt.begin(st, RSA_K_COMPACT);
     hipLaunchKernelGGL(k_compact, dim3(n), dim3(64), 0, st, (int)n, DP(B_HOFF, uint64_t), DP(B_ROFF2, uint64_t),
                        DP(B_NCNT1, uint32_t), DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t), DP(B_NAM1, rsa_nam),
                        DP(B_NAM2, rsa_nam), DP(B_OOFF, uint64_t), DP(B_OUT, rsa_nam));
     SCHK(hipGetLastError());
-    SCHK(hipEventRecord(ev[4], st));
+    kt.end(st);
     if (total) SCHK(hipMemcpyAsync(out->nams, b.p[B_OUT], sizeof(rsa_nam) * total, hipMemcpyDeviceToHost, st));
     SCHK(hipStreamSynchronize(st));
-    float t01 = 0, t12 = 0, t23 = 0, t34 = 0;
-    (void)hipEventElapsedTime(&t01, ev[0], ev[1]);
-    (void)hipEventElapsedTime(&t12, ev[1], ev[2]);
-    (void)hipEventElapsedTime(&t23, ev[2], ev[3]);
-    (void)hipEventElapsedTime(&t34, ev[3], ev[4]);
-    ms[0] = t01; ms[1] = t12; ms[2] = t23 + t34;
-    counters[0] = n; counters[1] = n_qrs; counters[2] = n_found; counters[3] = H; counters[4] = total;
+    // counters and algorithmic bytes (DESIGN.md "Kernels")
+    uint64_t n1_tot = 0, n2_tot = 0, resc_q = 0, resc_scan = 0, resc_hits = 0;
+    for (uint32_t i = 0; i < n; ++i) n1_tot += n1[i];
+    for (int i : resc) { n2_tot += n2[i]; resc_q += qcnt[i]; resc_scan += hs[i].scan_all; resc_hits += hs[i].hits_all; }
+    const double QRS = sizeof(rsa_query_randstrobe), QI = sizeof(QrsInfo), RS = sizeof(rsa_ref_randstrobe),
+                 NAM = sizeof(rsa_nam), HIT = sizeof(HitD);
+    c.reads = n; c.read_bases = bases; c.qrs = n_qrs; c.found = n_found; c.filtered = n_found - n_good;
+    c.hits = H; c.nams = total; c.rescued = resc.size();
+    c.alg_bytes[RSA_K_RANDSTROBES] = (double)bases + QRS * n_qrs + 24.0 * n;
+    c.alg_bytes[RSA_K_LOOKUP] = (QRS + 16 + QI) * n_qrs + 8.0 * n_found + RS * scan_all + sizeof(ReadStat) * (double)n;
+    c.alg_bytes[RSA_K_FIND_NAMS] = (QRS + QI) * n_qrs + RS * scan_find + 2 * HIT * H + NAM * n1_tot + 16.0 * n;
+    c.alg_bytes[RSA_K_RESCUE] = (QRS + QI) * resc_q + RS * resc_scan + 2 * HIT * resc_hits + NAM * n2_tot;
+    c.alg_bytes[RSA_K_COMPACT] = 2 * NAM * total + 28.0 * n;
     return RSA_OK;
 }

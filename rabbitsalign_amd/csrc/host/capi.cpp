@@ -1,0 +1,248 @@
+// capi.cpp -- include/rsalign.h: the mapping path as a C library.
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
+
+#include "../../../include/rsalign.h"
+#include "rsa_host.hpp"
+#include "synth.hpp"
+
+namespace rsa {
+// provided by the engine translation unit linked into the library
+std::unique_ptr<Engine> make_default_engine(const References& refs, const StiIndex& idx, int device);
+}
+
+using namespace rsa;
+
+static thread_local std::string g_err;
+
+struct rsam {
+    References refs;
+    StiIndex idx;
+    std::unique_ptr<Engine> eng;
+    AlignmentParameters ap;
+    MappingParameters mp;
+    double index_seconds = 0, upload_seconds = 0;
+    int read_len = 150;
+};
+
+struct rsam_reads {
+    std::vector<Record> r1, r2;
+    bool paired = false;
+};
+
+static void finish_refs(References& r) {
+    r.offsets.assign(1, 0);
+    size_t tot = 0;
+    for (auto& s : r.seqs) { tot += s.size(); r.offsets.push_back(tot); }
+    r.concat.clear();
+    r.concat.reserve(tot);
+    for (auto& s : r.seqs) r.concat += s;
+}
+
+static void setup_params(rsam* m) {
+    m->mp.r = m->read_len;
+    m->mp.rescue_cutoff = m->mp.rescue_level < 100 ? m->mp.rescue_level * m->idx.filter_cutoff : 1000;
+}
+
+static rsam* open_common(rsam* m, int device, char* err, size_t err_len) {
+    try {
+        setup_params(m);
+        auto t = std::chrono::steady_clock::now();
+        m->eng = make_default_engine(m->refs, m->idx, device);
+        m->upload_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+        return m;
+    } catch (const std::exception& e) {
+        if (err && err_len) snprintf(err, err_len, "%s", e.what());
+        g_err = e.what();
+        delete m;
+        return nullptr;
+    }
+}
+
+extern "C" {
+
+rsam* rsam_open_files(const char* ref_fa, const char* sti, int read_len, int device, int threads, char* err,
+                      size_t err_len) {
+    rsam* m = new rsam();
+    try {
+        m->read_len = read_len;
+        m->refs = References::from_fasta(ref_fa);
+        auto t = std::chrono::steady_clock::now();
+        IndexParameters ip = IndexParameters::from_read_length(read_len);
+        if (sti && *sti) {
+            m->idx.read(sti);
+            if (!(m->idx.params == ip)) throw std::runtime_error("index parameters differ from the read length profile");
+        } else {
+            m->idx.build(m->refs, ip, -1, 0.0002f, std::max(1, threads));
+        }
+        m->index_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+    } catch (const std::exception& e) {
+        if (err && err_len) snprintf(err, err_len, "%s", e.what());
+        g_err = e.what();
+        delete m;
+        return nullptr;
+    }
+    return open_common(m, device, err, err_len);
+}
+
+rsam* rsam_open_synthetic(uint64_t seed, uint64_t ref_len, int n_contigs, int read_len, int device, int threads,
+                          char* err, size_t err_len) {
+    rsam* m = new rsam();
+    try {
+        m->read_len = read_len;
+        m->refs.seqs = synth::reference(seed, ref_len, n_contigs, std::max(1, threads));
+        for (int c = 0; c < n_contigs; ++c) m->refs.names.push_back("chr" + std::to_string(c + 1));
+        finish_refs(m->refs);
+        auto t = std::chrono::steady_clock::now();
+        m->idx.build(m->refs, IndexParameters::from_read_length(read_len), -1, 0.0002f, std::max(1, threads));
+        m->index_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+    } catch (const std::exception& e) {
+        if (err && err_len) snprintf(err, err_len, "%s", e.what());
+        g_err = e.what();
+        delete m;
+        return nullptr;
+    }
+    return open_common(m, device, err, err_len);
+}
+
+rsam* rsam_open_like(const rsam* o, int device, int threads, char* err, size_t err_len) {
+    (void)threads;
+    rsam* m = new rsam();
+    m->read_len = o->read_len;
+    m->refs = o->refs;
+    m->idx = o->idx;
+    m->index_seconds = o->index_seconds;
+    return open_common(m, device, err, err_len);
+}
+
+void rsam_close(rsam* m) { delete m; }
+
+int rsam_get_info(const rsam* m, rsam_info* out) {
+    if (!m || !out) return -1;
+    out->ref_bases = m->refs.concat.size();
+    out->n_randstrobes = m->idx.randstrobes.size();
+    out->n_contigs = (int32_t)m->refs.size();
+    out->bits = m->idx.bits;
+    out->filter_cutoff = m->idx.filter_cutoff;
+    out->k = m->idx.params.k;
+    out->canonical_read_length = m->idx.params.canonical_read_length;
+    out->index_seconds = m->index_seconds;
+    out->upload_seconds = m->upload_seconds;
+    out->device_resident_bytes = m->refs.concat.size() + m->idx.randstrobes.size() * sizeof(rsa_ref_randstrobe) +
+                                 m->idx.bucket_starts.size() * 8;
+    return 0;
+}
+
+rsam_reads* rsam_reads_load(const char* fq1, const char* fq2) {
+    try {
+        auto* r = new rsam_reads();
+        Record rec;
+        {
+            FastxReader in(fq1);
+            while (in.next(rec)) r->r1.push_back(rec);
+        }
+        if (fq2 && *fq2) {
+            FastxReader in(fq2);
+            while (in.next(rec)) r->r2.push_back(rec);
+            r->paired = true;
+            if (r->r1.size() != r->r2.size()) throw std::runtime_error("read files have different record counts");
+        }
+        return r;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return nullptr;
+    }
+}
+
+rsam_reads* rsam_reads_synthetic(const rsam* m, uint64_t seed, uint64_t first, uint64_t n, int read_len, double mu,
+                                 double sigma, int paired) {
+    auto* r = new rsam_reads();
+    r->paired = paired != 0;
+    r->r1.resize(n);
+    if (paired) r->r2.resize(n);
+    const std::string qual((size_t)read_len, 'I');
+    const int T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> ws;
+    for (int t = 0; t < T; ++t)
+        ws.emplace_back([&, t]() {
+            for (uint64_t i = (uint64_t)t; i < n; i += (uint64_t)T) {
+                const uint64_t p = first + i;
+                synth::Pair pr = synth::pair(m->refs.seqs, seed, p, read_len, mu, sigma);
+                const std::string nm = "r" + std::to_string(p);
+                r->r1[i] = Record{paired ? nm + "/1" : nm, "", pr.a, qual};
+                if (paired) r->r2[i] = Record{nm + "/2", "", pr.b, qual};
+            }
+        });
+    for (auto& w : ws) w.join();
+    return r;
+}
+
+uint64_t rsam_reads_count(const rsam_reads* r) { return r ? r->r1.size() + r->r2.size() : 0; }
+void rsam_reads_free(rsam_reads* r) { delete r; }
+
+struct SinkState {
+    FILE* f = nullptr;
+    uint64_t hash = 1469598103934665603ULL;
+};
+
+static void sink_fn(void* user, const std::string& chunk) {
+    auto* s = (SinkState*)user;
+    uint64_t h = s->hash;
+    for (unsigned char c : chunk) { h ^= c; h *= 1099511628211ULL; }
+    s->hash = h;
+    if (s->f) fwrite(chunk.data(), 1, chunk.size(), s->f);
+}
+
+int rsam_map(rsam* m, const rsam_reads* reads, int threads, int chunk_size, const char* sam_path, rsam_stats* out) {
+    if (!m || !reads) return -1;
+    try {
+        SinkState st;
+        if (sam_path && *sam_path) {
+            st.f = fopen(sam_path, "wb");
+            if (!st.f) throw std::runtime_error(std::string("cannot open ") + sam_path);
+            std::string hdr = sam_header(m->refs, "", {}, "rsalign (library)");
+            fwrite(hdr.data(), 1, hdr.size(), st.f);
+        }
+        MapContext mc{m->refs, m->idx.params, m->ap, m->mp};
+        PipelineOptions po;
+        po.threads = threads;
+        po.chunk_size = chunk_size;
+        PipelineResult res = reads->paired ? run_pipeline_pe(reads->r1, reads->r2, *m->eng, mc, po, sink_fn, &st)
+                                           : run_pipeline_se(reads->r1, *m->eng, mc, po, sink_fn, &st);
+        if (st.f) fclose(st.f);
+        if (out) {
+            out->n_reads = res.stats.n_reads;
+            out->sam_bytes = res.sam_bytes;
+            out->sam_hash = st.hash;
+            out->sw_calls = res.stats.tot_aligner_calls;
+            out->tried = res.stats.tot_all_tried;
+            out->nam_rescue = res.stats.nam_rescue;
+            out->mate_rescue = res.stats.tot_rescued;
+            out->inconsistent = res.stats.inconsistent_nams;
+            out->map_seconds = res.map_seconds;
+        }
+        return 0;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+int rsam_kernel_stats(rsam* m, rsa_kernel_stats* out) {
+    if (!m || !out) return -1;
+    memset(out, 0, sizeof *out);
+    return m->eng->kernel_stats(out) ? 0 : 1;
+}
+
+void rsam_reset_kernel_stats(rsam* m) { if (m) m->eng->reset_kernel_stats(); }
+
+const char* rsam_engine_name(const rsam* m) { return m ? m->eng->name() : ""; }
+
+const char* rsam_last_error(void) { return g_err.c_str(); }
+
+}  // extern "C"

@@ -93,6 +93,9 @@ public:
         }
     }
 
+    bool kernel_stats(rsa_kernel_stats* out) override { return rsa_get_stats(ctx_, out) == RSA_OK; }
+    void reset_kernel_stats() override { rsa_reset_stats(ctx_); }
+
 private:
     rsa_ctx* ctx_ = nullptr;
 };
@@ -101,6 +104,11 @@ private:
 
 std::unique_ptr<Engine> make_gpu_engine(const References& refs, const StiIndex& index, int device) {
     return std::unique_ptr<Engine>(new GpuEngine(refs, index, device));
+}
+
+// engine of librsalign.so (capi.cpp)
+std::unique_ptr<Engine> make_default_engine(const References& refs, const StiIndex& index, int device) {
+    return make_gpu_engine(refs, index, device);
 }
 
 }  // namespace rsa

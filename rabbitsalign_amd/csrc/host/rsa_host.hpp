@@ -169,6 +169,9 @@ public:
     // Aligner::align for every job (aligner.cpp:114-210)
     virtual void extend(const std::vector<SwJob>& jobs, const AlignmentParameters& p,
                         std::vector<AlignmentInfo>& out) = 0;
+    // device kernel timings/counters (GPU engine only)
+    virtual bool kernel_stats(rsa_kernel_stats*) { return false; }
+    virtual void reset_kernel_stats() {}
 };
 
 // GPU engine over the C-ABI (engine_gpu.cpp)

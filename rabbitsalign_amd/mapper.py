@@ -1,0 +1,177 @@
+"""Python mirror of the reference's mapping entry (run_rabbitsalign,
+src/main.cpp:240-617) over the C-ABI of include/rsalign.h (librsalign.so).
+
+    m = Mapper.synthetic(seed=1, ref_len=3_000_000_000, n_contigs=24, read_len=150)
+    reads = m.synthetic_reads(seed=7, first=0, n=1_000_000, read_len=150, mu=300, sigma=30)
+    st = m.map(reads, threads=16)          # SAM kept in memory, FNV-1a hash in st.sam_hash
+
+The product library drives the HIP engine (librsa_gpu.so); nothing here
+computes.  ``lib_path`` may name another build of the same ABI (bench.py's
+cpu_baseline leg points it at oracle/_ref/librsalign_ref.so).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+from .native import LIB_DIR, KernelStats, stats_dict
+
+PRODUCT_LIB = os.path.join(LIB_DIR, "librsalign.so")
+
+
+class _Stats(C.Structure):
+    _fields_ = [("n_reads", C.c_uint64), ("sam_bytes", C.c_uint64), ("sam_hash", C.c_uint64),
+                ("sw_calls", C.c_uint64), ("tried", C.c_uint64), ("nam_rescue", C.c_uint64),
+                ("mate_rescue", C.c_uint64), ("inconsistent", C.c_uint64), ("map_seconds", C.c_double)]
+
+
+class _Info(C.Structure):
+    _fields_ = [("ref_bases", C.c_uint64), ("n_randstrobes", C.c_uint64), ("n_contigs", C.c_int32),
+                ("bits", C.c_int32), ("filter_cutoff", C.c_int32), ("k", C.c_int32),
+                ("canonical_read_length", C.c_int32), ("index_seconds", C.c_double),
+                ("upload_seconds", C.c_double), ("device_resident_bytes", C.c_uint64)]
+
+
+EXPORTED_SYMBOLS = [
+    "rsam_open_files", "rsam_open_synthetic", "rsam_open_like", "rsam_close", "rsam_get_info",
+    "rsam_reads_load", "rsam_reads_synthetic", "rsam_reads_count", "rsam_reads_free", "rsam_map",
+    "rsam_kernel_stats", "rsam_reset_kernel_stats", "rsam_engine_name", "rsam_last_error",
+]
+
+_LIBS: dict = {}
+
+
+def load(path: str = PRODUCT_LIB) -> C.CDLL:
+    if path in _LIBS:
+        return _LIBS[path]
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is not built (run `make -C rabbitsalign_amd`); there is no fallback path")
+    lib = C.CDLL(path)
+    vp, sz, u64, i32, cp = C.c_void_p, C.c_size_t, C.c_uint64, C.c_int, C.c_char_p
+    lib.rsam_open_files.restype = vp
+    lib.rsam_open_files.argtypes = [cp, cp, i32, i32, i32, cp, sz]
+    lib.rsam_open_synthetic.restype = vp
+    lib.rsam_open_synthetic.argtypes = [u64, u64, i32, i32, i32, i32, cp, sz]
+    lib.rsam_open_like.restype = vp
+    lib.rsam_open_like.argtypes = [vp, i32, i32, cp, sz]
+    lib.rsam_close.argtypes = [vp]
+    lib.rsam_get_info.argtypes = [vp, C.POINTER(_Info)]
+    lib.rsam_reads_load.restype = vp
+    lib.rsam_reads_load.argtypes = [cp, cp]
+    lib.rsam_reads_synthetic.restype = vp
+    lib.rsam_reads_synthetic.argtypes = [vp, u64, u64, u64, i32, C.c_double, C.c_double, i32]
+    lib.rsam_reads_count.restype = u64
+    lib.rsam_reads_count.argtypes = [vp]
+    lib.rsam_reads_free.argtypes = [vp]
+    lib.rsam_map.argtypes = [vp, vp, i32, i32, cp, C.POINTER(_Stats)]
+    lib.rsam_kernel_stats.argtypes = [vp, C.POINTER(KernelStats)]
+    lib.rsam_reset_kernel_stats.argtypes = [vp]
+    lib.rsam_engine_name.restype = cp
+    lib.rsam_engine_name.argtypes = [vp]
+    lib.rsam_last_error.restype = cp
+    _LIBS[path] = lib
+    return lib
+
+
+@dataclass
+class MapStats:
+    n_reads: int
+    sam_bytes: int
+    sam_hash: int
+    sw_calls: int
+    tried: int
+    nam_rescue: int
+    mate_rescue: int
+    inconsistent: int
+    map_seconds: float
+
+
+class Reads:
+    def __init__(self, lib, handle):
+        self._lib, self._h = lib, handle
+
+    def __len__(self):
+        return int(self._lib.rsam_reads_count(self._h))
+
+    def close(self):
+        if self._h:
+            self._lib.rsam_reads_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+class Mapper:
+    """Reference + .sti index resident on one device, plus the host pipeline."""
+
+    def __init__(self, lib, handle):
+        self._lib, self._h = lib, handle
+
+    @classmethod
+    def _open(cls, lib, fn, *args):
+        err = C.create_string_buffer(1024)
+        h = fn(*args, err, len(err))
+        if not h:
+            raise RuntimeError(f"rsalign open failed: {err.value.decode(errors='replace')}")
+        return cls(lib, h)
+
+    @classmethod
+    def from_files(cls, ref_fa, sti=None, read_len=150, device=0, threads=8, lib_path=PRODUCT_LIB):
+        lib = load(lib_path)
+        return cls._open(lib, lib.rsam_open_files, str(ref_fa).encode(), (str(sti).encode() if sti else None),
+                         read_len, device, threads)
+
+    @classmethod
+    def synthetic(cls, seed, ref_len, n_contigs, read_len=150, device=0, threads=8, lib_path=PRODUCT_LIB):
+        lib = load(lib_path)
+        return cls._open(lib, lib.rsam_open_synthetic, seed, ref_len, n_contigs, read_len, device, threads)
+
+    def like(self, device=0, threads=8, lib_path=PRODUCT_LIB):
+        """Same reference + index (host copy), another engine build or device."""
+        lib = load(lib_path)
+        return Mapper._open(lib, lib.rsam_open_like, self._h, device, threads)
+
+    @property
+    def engine(self) -> str:
+        return self._lib.rsam_engine_name(self._h).decode()
+
+    def info(self) -> dict:
+        i = _Info()
+        self._lib.rsam_get_info(self._h, C.byref(i))
+        return {f: getattr(i, f) for f, _ in _Info._fields_}
+
+    def synthetic_reads(self, seed, first, n, read_len=150, mu=300.0, sigma=30.0, paired=True) -> Reads:
+        return Reads(self._lib, self._lib.rsam_reads_synthetic(self._h, seed, first, n, read_len, mu, sigma,
+                                                               1 if paired else 0))
+
+    def load_reads(self, fq1, fq2=None) -> Reads:
+        h = self._lib.rsam_reads_load(str(fq1).encode(), str(fq2).encode() if fq2 else None)
+        if not h:
+            raise RuntimeError(self._lib.rsam_last_error().decode())
+        return Reads(self._lib, h)
+
+    def map(self, reads: Reads, threads=8, chunk_size=10000, sam_path=None) -> MapStats:
+        st = _Stats()
+        rc = self._lib.rsam_map(self._h, reads._h, threads, chunk_size,
+                                str(sam_path).encode() if sam_path else None, C.byref(st))
+        if rc != 0:
+            raise RuntimeError(f"rsam_map: {self._lib.rsam_last_error().decode()}")
+        return MapStats(**{f: getattr(st, f) for f, _ in _Stats._fields_})
+
+    def kernel_stats(self) -> dict:
+        ks = KernelStats()
+        self._lib.rsam_kernel_stats(self._h, C.byref(ks))
+        return stats_dict(ks)
+
+    def reset_kernel_stats(self):
+        self._lib.rsam_reset_kernel_stats(self._h)
+
+    def close(self):
+        if self._h:
+            self._lib.rsam_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()

@@ -76,12 +76,28 @@ class AlnBatch(C.Structure):
                 ("cigar_used", C.c_uint64)]
 
 
+KERNELS = ["randstrobes", "lookup", "find_nams", "rescue", "compact", "ext_scan", "ext_band"]
+KERNEL_SYMBOLS = {"randstrobes": "k_randstrobes", "lookup": "k_lookup", "find_nams": "k_find_nams",
+                  "rescue": "k_rescue", "compact": "k_compact", "ext_scan": "k_ext_scan", "ext_band": "k_ext_band"}
+NK = len(KERNELS)
+
+
 class KernelStats(C.Structure):
-    _fields_ = [("seed_ms", C.c_double), ("lookup_ms", C.c_double), ("nam_ms", C.c_double),
-                ("ext_scan_ms", C.c_double), ("ext_band_ms", C.c_double),
+    _fields_ = [("kernel_ms", C.c_double * NK), ("launches", C.c_uint64 * NK), ("alg_bytes", C.c_double * NK),
                 ("seed_calls", C.c_uint64), ("ext_calls", C.c_uint64),
-                ("reads", C.c_uint64), ("query_randstrobes", C.c_uint64), ("lookups_found", C.c_uint64),
-                ("hits", C.c_uint64), ("nams", C.c_uint64), ("jobs", C.c_uint64), ("dp_cells", C.c_uint64)]
+                ("reads", C.c_uint64), ("read_bases", C.c_uint64), ("query_randstrobes", C.c_uint64),
+                ("lookups_found", C.c_uint64), ("filtered", C.c_uint64), ("hits", C.c_uint64),
+                ("nams", C.c_uint64), ("rescued_reads", C.c_uint64),
+                ("jobs", C.c_uint64), ("dp_cells", C.c_uint64)]
+
+
+def stats_dict(ks: "KernelStats") -> dict:
+    """Flatten a KernelStats into {"kernels": {name: {ms, launches, alg_bytes}}, counters...}."""
+    out = {"kernels": {k: {"ms": ks.kernel_ms[i], "launches": int(ks.launches[i]), "alg_bytes": ks.alg_bytes[i]}
+                       for i, k in enumerate(KERNELS)}}
+    for f, _ in KernelStats._fields_[3:]:
+        out[f] = int(getattr(ks, f))
+    return out
 
 
 EXPORTED_SYMBOLS = ["rsa_open", "rsa_close", "rsa_last_error", "rsa_resident_bytes", "rsa_randstrobes",
@@ -312,7 +328,7 @@ class GpuContext:
     def stats(self) -> dict:
         s = KernelStats()
         self._check(self.lib.rsa_get_stats(self.ctx, C.byref(s)), "rsa_get_stats")
-        return {f: getattr(s, f) for f, _ in KernelStats._fields_}
+        return stats_dict(s)
 
     def reset_stats(self):
         self.lib.rsa_reset_stats(self.ctx)
