@@ -180,8 +180,9 @@ enum {
     RSA_K_RESCUE = 3,      /* find_nams_rescue (nam.cpp:946-1010) */
     RSA_K_COMPACT = 4,     /* NAM output compaction */
     RSA_K_EXT_SCAN = 5,    /* SSW forward/reverse score scans (ssw.c:121-620) */
-    RSA_K_EXT_BAND = 6,    /* banded_sw traceback + Aligner::align (ssw.c:622-790, aligner.cpp:114-210) */
-    RSA_K_COUNT = 7
+    RSA_K_EXT_BAND = 6,    /* banded_sw + traceback + Aligner::align, 16 lanes/job (ssw.c:622-790, aligner.cpp:114-210) */
+    RSA_K_EXT_BAND_LANE = 7, /* the same, one lane per job, for jobs the 16-lane kernel defers */
+    RSA_K_COUNT = 8
 };
 
 typedef struct rsa_kernel_stats {

@@ -24,9 +24,11 @@ typedef struct rsam_reads rsam_reads;  /* a read set held in host memory */
 typedef struct rsam_stats {
     uint64_t n_reads;         /* reads mapped (each mate counts, pc.cpp:1596) */
     uint64_t sam_bytes;       /* SAM body bytes produced */
-    uint64_t sam_hash;        /* FNV-1a 64 of the SAM body, in output order */
+    uint64_t sam_hash;        /* sum_k fnv1a64(line_k) * 0x100000001b3^(N-1-k) mod 2^64 over SAM body lines */
     uint64_t sw_calls, tried, nam_rescue, mate_rescue, inconsistent;
     double map_seconds;       /* first chunk read -> last SAM byte (consumer cost, main.cpp:446,595) */
+    /* host pipeline phases, seconds summed over worker threads (PE path) */
+    double t_seed, t_extend, t_part, t_collect, t_last, t_sequential;
 } rsam_stats;
 
 /* Open from files: FASTA + optional .sti (NULL: build the index in memory). */

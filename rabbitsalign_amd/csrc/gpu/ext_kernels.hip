@@ -316,53 +316,12 @@ __device__ __forceinline__ void cpush(uint32_t* c, int& n, uint32_t op, uint32_t
     else c[n - 1] += len << 4;
 }
 
-__global__ void __launch_bounds__(64)
-k_ext_band(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan, int n_jobs,
-           const int* __restrict__ idx_list, int job_base,
-           const char* __restrict__ qbuf, const char* __restrict__ ref, uint32_t* __restrict__ cig_pool,
-           rsa_aln* __restrict__ out, uint8_t* __restrict__ scratch, int64_t scr_stride, int arr_cap,
-           int64_t dir_cap, int match, int mismatch, int gO, int gE, int bonus, int* __restrict__ overflow) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n_jobs) return;
-    const int j = idx_list ? idx_list[t] : job_base + t;
-    const ExtJobDev jb = jobs[j];
-    const ScanRes sr = scan[j];
-    rsa_aln a;
-    a.sw_score = 0; a.edit_distance = 0; a.ref_start = a.ref_end = a.query_start = a.query_end = 0;
-    a.cigar_offset = jb.cig_off; a.cigar_len = 0; a.pad_ = 0;
-    if (sr.status == 1) {                       // ref > 2000 (aligner.cpp:119-125)
-        a.edit_distance = 100000; a.sw_score = -1000000;
-        out[j] = a;
-        return;
-    }
-    const char* q = qbuf + jb.q_off;
-    const char* r = ref + jb.r_off;
+// ConvertAlignment + CalculateNumberMismatch + the end-bonus step of
+// Aligner::align, given the raw banded_sw ops of a job (shared by both band kernels).
+__device__ void ext_finish(const ExtJobDev& jb, const ScanRes& sr, const char* __restrict__ q,
+                           const char* __restrict__ r, const uint32_t* __restrict__ raw, int nraw,
+                           uint32_t* __restrict__ c, rsa_aln& a, int match, int mismatch, int bonus) {
     const int qlen = (int)jb.qlen, rlen = (int)jb.rlen;
-    uint32_t* c = cig_pool + jb.cig_off;
-    if (sr.flag != 0) {                         // aligner.cpp:131-136
-        a.edit_distance = 100000; a.sw_score = -100000;
-        out[j] = a;
-        return;
-    }
-    // banded_sw over ref[ref_begin1..ref_end1] x read[read_begin1..read_end1] (ssw.c:899-918)
-    const int ref_l = sr.ref_end1 - sr.ref_begin1 + 1;
-    const int read_l = sr.read_end1 - sr.read_begin1 + 1;
-    const int bw = abs(ref_l - read_l) + 1;
-    uint8_t* my = scratch + (int64_t)t * scr_stride;
-    BandScratch bs;
-    bs.hb = (int*)my; bs.eb = bs.hb + arr_cap; bs.hc = bs.eb + arr_cap;
-    bs.dir = (int8_t*)(bs.hc + arr_cap);
-    bs.arr_cap = arr_cap; bs.dir_cap = dir_cap;
-    // raw banded ops live in the job's scratch, the final CIGAR is built in its slot
-    uint32_t* raw = (uint32_t*)(bs.dir + dir_cap);
-    const int nraw = banded_sw_dev(r, sr.ref_begin1, rlen, q + sr.read_begin1, ref_l, read_l, sr.score1, gO, gE, bw,
-                                   match, mismatch, bs, raw);
-    if (nraw == -2) { overflow[j] = idx_list ? 2 : 1; return; }
-    if (nraw < 0) {                             // banded_sw failed -> flag 1
-        a.edit_distance = 100000; a.sw_score = -100000;
-        out[j] = a;
-        return;
-    }
     // ConvertAlignment + CalculateNumberMismatch (ssw_cpp.cpp:54-90, 126-210).
     // Core ops are built after a gap of qs+2 entries (room for the left end-bonus ops).
     const int qs0 = sr.read_begin1;
@@ -460,5 +419,237 @@ k_ext_band(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan,
     }
     a.sw_score = sw; a.edit_distance = ed; a.ref_start = rs; a.ref_end = re; a.query_start = qs; a.query_end = qe;
     a.cigar_len = (uint32_t)final_n;
+}
+
+__global__ void __launch_bounds__(64)
+k_ext_band(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan, int n_jobs,
+           const int* __restrict__ idx_list, int job_base,
+           const char* __restrict__ qbuf, const char* __restrict__ ref, uint32_t* __restrict__ cig_pool,
+           rsa_aln* __restrict__ out, uint8_t* __restrict__ scratch, int64_t scr_stride, int arr_cap,
+           int64_t dir_cap, int match, int mismatch, int gO, int gE, int bonus, int* __restrict__ overflow,
+           int over_code) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_jobs) return;
+    const int j = idx_list ? idx_list[t] : job_base + t;
+    const ExtJobDev jb = jobs[j];
+    const ScanRes sr = scan[j];
+    rsa_aln a;
+    a.sw_score = 0; a.edit_distance = 0; a.ref_start = a.ref_end = a.query_start = a.query_end = 0;
+    a.cigar_offset = jb.cig_off; a.cigar_len = 0; a.pad_ = 0;
+    if (sr.status == 1) {                       // ref > 2000 (aligner.cpp:119-125)
+        a.edit_distance = 100000; a.sw_score = -1000000;
+        out[j] = a;
+        return;
+    }
+    const char* q = qbuf + jb.q_off;
+    const char* r = ref + jb.r_off;
+    const int qlen = (int)jb.qlen, rlen = (int)jb.rlen;
+    uint32_t* c = cig_pool + jb.cig_off;
+    if (sr.flag != 0) {                         // aligner.cpp:131-136
+        a.edit_distance = 100000; a.sw_score = -100000;
+        out[j] = a;
+        return;
+    }
+    // banded_sw over ref[ref_begin1..ref_end1] x read[read_begin1..read_end1] (ssw.c:899-918)
+    const int ref_l = sr.ref_end1 - sr.ref_begin1 + 1;
+    const int read_l = sr.read_end1 - sr.read_begin1 + 1;
+    const int bw = abs(ref_l - read_l) + 1;
+    uint8_t* my = scratch + (int64_t)t * scr_stride;
+    BandScratch bs;
+    bs.hb = (int*)my; bs.eb = bs.hb + arr_cap; bs.hc = bs.eb + arr_cap;
+    bs.dir = (int8_t*)(bs.hc + arr_cap);
+    bs.arr_cap = arr_cap; bs.dir_cap = dir_cap;
+    // raw banded ops live in the job's scratch, the final CIGAR is built in its slot
+    uint32_t* raw = (uint32_t*)(bs.dir + dir_cap);
+    const int nraw = banded_sw_dev(r, sr.ref_begin1, rlen, q + sr.read_begin1, ref_l, read_l, sr.score1, gO, gE, bw,
+                                   match, mismatch, bs, raw);
+    if (nraw == -2) { overflow[j] = over_code; return; }
+    if (nraw < 0) {                             // banded_sw failed -> flag 1
+        a.edit_distance = 100000; a.sw_score = -100000;
+        out[j] = a;
+        return;
+    }
+    ext_finish(jb, sr, q, r, raw, nraw, c, a, match, mismatch, bonus);
+    out[j] = a;
+}
+
+// ---------------------------------------------------------------------------
+// k_ext_band16: banded_sw with 16 lanes per job (4 jobs per wave64).
+//
+// Same result as banded_sw_dev, computed row by row with one band cell per
+// lane.  The band arrays (h_b, e_b) and the direction matrix keep the
+// reference's exact index layout (SET_U / SET_D), in LDS, so the traceback --
+// including its out-of-band reads -- sees the same bytes.  Within a row the
+// only serial term is F (horizontal gap); with gap_open >= gap_extend
+//     F_j = max(H'_{j-1} - gO, F_{j-1} - gE),  H' = max(E+, diag)
+// equals the reference's recurrence on the full H (the F-arm of H never wins
+// the next F), so it is a max-plus prefix scan over the 16 lanes of the group
+// (DPP row_shr 1,2,4,8).  Jobs the group cannot hold (band wider than 16
+// cells, direction bytes beyond B16_DIRCAP, long segments, gO < gE, scan
+// sentinels) are flagged in `defer` for k_ext_band.
+// ---------------------------------------------------------------------------
+#define B16_GROUPS 4
+#define B16_DIRCAP 4096
+#define B16_SEGCAP 320
+#define B16_NEG (-0x20000000)
+
+template <int S>
+__device__ __forceinline__ int grp_shr(int v) {
+    // lane z of a 16-lane row receives lane z-S; z < S receives B16_NEG
+    return __builtin_amdgcn_update_dpp(B16_NEG, v, 0x110 + S, 0xf, 0xf, false);
+}
+
+__device__ __forceinline__ int grp_max(int v) {
+    for (int o = 8; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 16));
+    return v;
+}
+
+#define WSYNC() do { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); } while (0)
+
+__global__ void __launch_bounds__(64)
+k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan, int n_jobs,
+             const char* __restrict__ qbuf, const char* __restrict__ ref, uint32_t* __restrict__ cig_pool,
+             uint32_t* __restrict__ raw_pool, rsa_aln* __restrict__ out, int match, int mismatch, int gO, int gE,
+             int bonus, int* __restrict__ defer) {
+    __shared__ __attribute__((aligned(16))) int8_t s_dir[B16_GROUPS][B16_DIRCAP];
+    __shared__ int s_hb[B16_GROUPS][32];
+    __shared__ int s_eb[B16_GROUPS][32];
+    __shared__ uint8_t s_qc[B16_GROUPS][B16_SEGCAP];
+    __shared__ uint8_t s_rc[B16_GROUPS][B16_SEGCAP];
+    const int lane = threadIdx.x & 63, g = lane >> 4, z = lane & 15;
+    const int j = blockIdx.x * B16_GROUPS + g;
+    if (j >= n_jobs) return;                       // whole group leaves together
+    const ExtJobDev jb = jobs[j];
+    const ScanRes sr = scan[j];
+    if (sr.status != 0) { if (z == 0) defer[j] = 1; return; }
+    if (sr.flag != 0) {                            // aligner.cpp:131-136
+        if (z == 0) {
+            rsa_aln a;
+            a.sw_score = -100000; a.edit_distance = 100000; a.ref_start = a.ref_end = a.query_start = a.query_end = 0;
+            a.cigar_offset = jb.cig_off; a.cigar_len = 0; a.pad_ = 0;
+            out[j] = a;
+        }
+        return;
+    }
+    const char* q = qbuf + jb.q_off;
+    const char* r = ref + jb.r_off;
+    const int rlen = (int)jb.rlen;
+    const int ref_begin = sr.ref_begin1;
+    const int ref_l = sr.ref_end1 - sr.ref_begin1 + 1;
+    const int read_l = sr.read_end1 - sr.read_begin1 + 1;
+    int bw = abs(ref_l - read_l) + 1;
+    if (read_l > B16_SEGCAP || ref_l > B16_SEGCAP || read_l <= 0 || ref_l <= 0 || gO < gE || 2 * bw + 1 > 16) {
+        if (z == 0) defer[j] = 1;
+        return;
+    }
+    int8_t* dir = s_dir[g];
+    int* hb = s_hb[g];
+    int* eb = s_eb[g];
+    uint8_t* qc = s_qc[g];
+    uint8_t* rc = s_rc[g];
+    for (int x = z; x < read_l; x += 16) qc[x] = (uint8_t)ssw_code((unsigned char)q[sr.read_begin1 + x]);
+    for (int x = z; x < ref_l; x += 16) {
+        const int gj = ref_begin + x;
+        rc[x] = (uint8_t)((gj >= 0 && gj < rlen) ? ssw_code((unsigned char)r[gj]) : 4);
+    }
+    for (int x = z * 16; x < B16_DIRCAP; x += 256) *(int4*)(dir + x) = make_int4(0, 0, 0, 0);
+    hb[z] = 0; hb[z + 16] = 0; eb[z] = 0; eb[z + 16] = 0;
+    WSYNC();
+
+    const int len = ref_l > read_l ? ref_l : read_l;
+    int s2 = 1024, max_v = 0, width_d = 0;
+    bool deferred = false;
+    do {
+        const int width = bw * 2 + 3;
+        width_d = bw * 2 + 1;
+        if (width_d > 16) { deferred = true; break; }
+        while (width_d * read_l * 3 >= s2) s2 *= 2;
+        if (s2 > B16_DIRCAP) { deferred = true; break; }
+        if (z >= 1 && z <= width - 2) hb[z] = 0;
+        WSYNC();
+        int lmax = 0;
+        for (int i = 0; i < read_l; ++i) {
+            const int beg = max(0, i - bw), end = min(ref_l - 1, i + bw);
+            const int edge = end + 1 < width - 1 ? end + 1 : width - 1;
+            if (z == 0) { hb[0] = 0; eb[0] = 0; hb[edge] = 0; eb[edge] = 0; }
+            WSYNC();
+            const int jj = beg + z;
+            const bool on = jj <= end;
+            const int u = z + 1;
+            const int e = u + (i - bw >= 1 ? 1 : 0);
+            const int hb_e = hb[e], eb_e = eb[e], hb_d = hb[e - 1];
+            const int qv = qc[i];
+            const int rv = on ? rc[jj] : 4;
+            WSYNC();
+            const int t1 = i == 0 ? -gO : hb_e - gO;
+            const int t2 = i == 0 ? -gE : eb_e - gE;
+            const int E = t1 > t2 ? t1 : t2;
+            const int de = t1 > t2 ? 3 : 2;
+            const int diag = hb_d + ((rv == qv && rv < 4) ? match : -mismatch);
+            const int e1 = E > 0 ? E : 0;
+            const int hp = e1 > diag ? e1 : diag;
+            const int prev_hp = grp_shr<1>(hp);
+            const int A = z == 0 ? -gO : prev_hp - gO;
+            int X = A;
+            X = max(X, grp_shr<1>(X) - gE);
+            X = max(X, grp_shr<2>(X) - 2 * gE);
+            X = max(X, grp_shr<4>(X) - 4 * gE);
+            X = max(X, grp_shr<8>(X) - 8 * gE);
+            const int F = max(X, -(z + 1) * gE);
+            const int f_prev = z == 0 ? 0 : grp_shr<1>(F);
+            const int df = A > f_prev - gE ? 5 : 4;
+            const int f1 = F > 0 ? F : 0;
+            const int m = e1 > f1 ? e1 : f1;
+            const int H = m > diag ? m : diag;
+            const int dh = m <= diag ? 1 : (e1 > f1 ? de : df);
+            if (on) {
+                eb[u] = E;
+                int8_t* dl = dir + width_d * 3 * i + 3 * z;
+                dl[0] = (int8_t)de; dl[1] = (int8_t)df; dl[2] = (int8_t)dh;
+                if (H > lmax) lmax = H;
+            }
+            WSYNC();
+            if (on) hb[u] = H;                       // h_b[1..u] = h_c[1..u]
+            WSYNC();
+        }
+        lmax = grp_max(lmax);
+        if (lmax > max_v) max_v = lmax;
+        bw *= 2;
+    } while (max_v < sr.score1 && bw <= len);
+    if (deferred) { if (z == 0) defer[j] = 1; return; }
+    if (z != 0) return;
+    bw /= 2;
+
+    // traceback (ssw.c:748-776), leader lane
+    rsa_aln a;
+    a.sw_score = 0; a.edit_distance = 0; a.ref_start = a.ref_end = a.query_start = a.query_end = 0;
+    a.cigar_offset = jb.cig_off; a.cigar_len = 0; a.pad_ = 0;
+    uint32_t* raw = raw_pool + jb.cig_off;
+    int i = read_l - 1, jx = ref_l - 1, ecount = 0, l = 0, temp2 = 2;
+    int line = width_d * 3 * (read_l - 1);
+    uint32_t op = 0, prev_op = 0;
+    bool fail = false;
+    while (i >= 0 && jx > 0) {
+        const int at = line + (jx - max(i - bw, 0)) * 3 + temp2;
+        if (at < 0 || at >= s2) { fail = true; break; }
+        const int dv = dir[at];
+        if (dv == 1) { --i; --jx; temp2 = 2; line -= width_d * 3; op = 0; }
+        else if (dv == 2) { --i; temp2 = 0; line -= width_d * 3; op = 1; }
+        else if (dv == 3) { --i; temp2 = 2; line -= width_d * 3; op = 1; }
+        else if (dv == 4) { --jx; temp2 = 1; op = 2; }
+        else if (dv == 5) { --jx; temp2 = 2; op = 2; }
+        else { fail = true; break; }
+        if (op == prev_op) ++ecount;
+        else { ++l; raw[l - 1] = cig((uint32_t)ecount, prev_op); prev_op = op; ecount = 1; }
+    }
+    if (fail) {                                     // banded_sw failed -> flag 1 sentinel
+        a.edit_distance = 100000; a.sw_score = -100000;
+        out[j] = a;
+        return;
+    }
+    if (op == 0) { ++l; raw[l - 1] = cig((uint32_t)ecount + 1, op); }
+    else { l += 2; raw[l - 2] = cig((uint32_t)ecount, op); raw[l - 1] = cig(1, 0); }
+    for (int s = 0, t = l - 1; s < t; ++s, --t) { const uint32_t x = raw[s]; raw[s] = raw[t]; raw[t] = x; }
+    ext_finish(jb, sr, q, r, raw, l, cig_pool + jb.cig_off, a, match, mismatch, bonus);
     out[j] = a;
 }

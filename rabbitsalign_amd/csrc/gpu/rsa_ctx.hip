@@ -24,7 +24,10 @@ __global__ void k_ext_scan(const ExtJobDev* jobs, int n_jobs, const char* qbuf, 
 __global__ void k_ext_band(const ExtJobDev* jobs, const ScanRes* scan, int n_jobs, const int* idx_list, int job_base,
                            const char* qbuf, const char* ref, uint32_t* cig_pool, rsa_aln* out, uint8_t* scratch,
                            int64_t scr_stride, int arr_cap, int64_t dir_cap, int match, int mismatch, int gO,
-                           int gE, int bonus, int* overflow);
+                           int gE, int bonus, int* overflow, int over_code);
+__global__ void k_ext_band16(const ExtJobDev* jobs, const ScanRes* scan, int n_jobs, const char* qbuf, const char* ref,
+                             uint32_t* cig_pool, uint32_t* raw_pool, rsa_aln* out, int match, int mismatch, int gO,
+                             int gE, int bonus, int* defer);
 
 int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, const rsa_read_batch* rb,
              int32_t rescue_level, uint32_t rescue_cutoff, rsa_nam_batch* out, std::string& err, SeedCounters& c);
@@ -79,7 +82,7 @@ struct Lane {
     KTimer kt;
     bool busy = false;
     // extension
-    DevBuf d_q, d_jobs, d_scan, d_alns, d_cig, d_scratch, d_over, d_idx;
+    DevBuf d_q, d_jobs, d_scan, d_alns, d_cig, d_raw, d_scratch, d_over, d_defer, d_idx;
     HostBuf h_q, h_jobs, h_over;
     // seeding
     SeedBufs sb;
@@ -275,14 +278,15 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
     HIPCHK(L->d_scan.ensure(sizeof(ScanRes) * n));
     HIPCHK(L->d_alns.ensure(sizeof(rsa_aln) * n));
     HIPCHK(L->d_cig.ensure(sizeof(uint32_t) * (bound + 16)));
+    HIPCHK(L->d_raw.ensure(sizeof(uint32_t) * (bound + 16)));
     HIPCHK(L->d_over.ensure(sizeof(int) * n));
+    HIPCHK(L->d_defer.ensure(sizeof(int) * n));
     const int64_t stride = band_stride(BAND_ARR_CAP, BAND_DIR_CAP);
-    const int chunk = (int)std::min<uint32_t>(n, BAND_CHUNK);
-    HIPCHK(L->d_scratch.ensure((size_t)stride * chunk));
     hipStream_t st = L->stream;
     HIPCHK(hipMemcpyAsync(L->d_q.p, jb->queries, jb->queries_len, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(L->d_jobs.p, hj, sizeof(ExtJobDev) * n, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemsetAsync(L->d_over.p, 0, sizeof(int) * n, st));
+    HIPCHK(hipMemsetAsync(L->d_defer.p, 0, sizeof(int) * n, st));
     L->kt.reset();
     L->kt.begin(st, RSA_K_EXT_SCAN);
     hipLaunchKernelGGL(k_ext_scan, dim3((n + 3) / 4), dim3(256), 0, st, L->d_jobs.as<ExtJobDev>(), (int)n,
@@ -290,18 +294,37 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
                        jb->gap_open, jb->gap_extend);
     HIPCHK(hipGetLastError());
     L->kt.end(st);
-    for (uint32_t base = 0; base < n; base += chunk) {
-        const int cnt = (int)std::min<uint32_t>(chunk, n - base);
-        L->kt.begin(st, RSA_K_EXT_BAND);
-        hipLaunchKernelGGL(k_ext_band, dim3((cnt + 63) / 64), dim3(64), 0, st, L->d_jobs.as<ExtJobDev>(),
-                           L->d_scan.as<ScanRes>(), cnt, (const int*)nullptr, (int)base, L->d_q.as<char>(), ctx->d_ref,
-                           L->d_cig.as<uint32_t>(), L->d_alns.as<rsa_aln>(), L->d_scratch.as<uint8_t>(), stride,
-                           BAND_ARR_CAP, BAND_DIR_CAP, jb->match, jb->mismatch, jb->gap_open, jb->gap_extend,
-                           jb->end_bonus, L->d_over.as<int>());
-        HIPCHK(hipGetLastError());
-        L->kt.end(st);
-    }
+    // 16 lanes per job for the common narrow bands
+    L->kt.begin(st, RSA_K_EXT_BAND);
+    hipLaunchKernelGGL(k_ext_band16, dim3((n + 3) / 4), dim3(64), 0, st, L->d_jobs.as<ExtJobDev>(),
+                       L->d_scan.as<ScanRes>(), (int)n, L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(),
+                       L->d_raw.as<uint32_t>(), L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open,
+                       jb->gap_extend, jb->end_bonus, L->d_defer.as<int>());
+    HIPCHK(hipGetLastError());
+    L->kt.end(st);
     HIPCHK(L->h_over.ensure(sizeof(int) * n));
+    HIPCHK(hipMemcpyAsync(L->h_over.p, L->d_defer.p, sizeof(int) * n, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    // deferred jobs (wide bands, sentinels, long segments): one lane per job
+    std::vector<int> dlist;
+    for (uint32_t i = 0; i < n; ++i) if (L->h_over.as<int>()[i]) dlist.push_back((int)i);
+    if (!dlist.empty()) {
+        const int chunk = (int)std::min<size_t>(dlist.size(), BAND_CHUNK);
+        HIPCHK(L->d_scratch.ensure((size_t)stride * chunk));
+        HIPCHK(L->d_idx.ensure(sizeof(int) * dlist.size()));
+        HIPCHK(hipMemcpyAsync(L->d_idx.p, dlist.data(), sizeof(int) * dlist.size(), hipMemcpyHostToDevice, st));
+        for (size_t base = 0; base < dlist.size(); base += chunk) {
+            const int cnt = (int)std::min<size_t>(chunk, dlist.size() - base);
+            L->kt.begin(st, RSA_K_EXT_BAND_LANE);
+            hipLaunchKernelGGL(k_ext_band, dim3((cnt + 63) / 64), dim3(64), 0, st, L->d_jobs.as<ExtJobDev>(),
+                               L->d_scan.as<ScanRes>(), cnt, L->d_idx.as<int>() + base, 0, L->d_q.as<char>(),
+                               ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_alns.as<rsa_aln>(),
+                               L->d_scratch.as<uint8_t>(), stride, BAND_ARR_CAP, BAND_DIR_CAP, jb->match,
+                               jb->mismatch, jb->gap_open, jb->gap_extend, jb->end_bonus, L->d_over.as<int>(), 1);
+            HIPCHK(hipGetLastError());
+            L->kt.end(st);
+        }
+    }
     HIPCHK(hipMemcpyAsync(L->h_over.p, L->d_over.p, sizeof(int) * n, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     // rare: jobs whose band doubled past the per-job scratch get a large scratch
@@ -310,17 +333,17 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
     for (uint32_t i = 0; i < n; ++i) if (ho[i]) big.push_back((int)i);
     if (!big.empty()) {
         const int64_t bstride = band_stride(BIG_ARR_CAP, BIG_DIR_CAP);
-        HIPCHK(L->d_scratch.ensure((size_t)std::max<int64_t>(bstride * BIG_CHUNK, stride * chunk)));
+        HIPCHK(L->d_scratch.ensure((size_t)bstride * BIG_CHUNK));
         HIPCHK(L->d_idx.ensure(sizeof(int) * big.size()));
         HIPCHK(hipMemcpyAsync(L->d_idx.p, big.data(), sizeof(int) * big.size(), hipMemcpyHostToDevice, st));
         for (size_t b = 0; b < big.size(); b += BIG_CHUNK) {
             const int cnt = (int)std::min<size_t>(BIG_CHUNK, big.size() - b);
-            L->kt.begin(st, RSA_K_EXT_BAND);
+            L->kt.begin(st, RSA_K_EXT_BAND_LANE);
             hipLaunchKernelGGL(k_ext_band, dim3(1), dim3(64), 0, st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(),
                                cnt, L->d_idx.as<int>() + b, 0, L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(),
                                L->d_alns.as<rsa_aln>(), L->d_scratch.as<uint8_t>(), bstride, BIG_ARR_CAP, BIG_DIR_CAP,
                                jb->match, jb->mismatch, jb->gap_open, jb->gap_extend, jb->end_bonus,
-                               L->d_over.as<int>());
+                               L->d_over.as<int>(), 2);
             HIPCHK(hipGetLastError());
             L->kt.end(st);
         }

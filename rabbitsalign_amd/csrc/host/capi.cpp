@@ -187,14 +187,10 @@ void rsam_reads_free(rsam_reads* r) { delete r; }
 
 struct SinkState {
     FILE* f = nullptr;
-    uint64_t hash = 1469598103934665603ULL;
 };
 
 static void sink_fn(void* user, const std::string& chunk) {
     auto* s = (SinkState*)user;
-    uint64_t h = s->hash;
-    for (unsigned char c : chunk) { h ^= c; h *= 1099511628211ULL; }
-    s->hash = h;
     if (s->f) fwrite(chunk.data(), 1, chunk.size(), s->f);
 }
 
@@ -212,19 +208,27 @@ int rsam_map(rsam* m, const rsam_reads* reads, int threads, int chunk_size, cons
         PipelineOptions po;
         po.threads = threads;
         po.chunk_size = chunk_size;
-        PipelineResult res = reads->paired ? run_pipeline_pe(reads->r1, reads->r2, *m->eng, mc, po, sink_fn, &st)
-                                           : run_pipeline_se(reads->r1, *m->eng, mc, po, sink_fn, &st);
+        po.digest = true;
+        SamSink sk = st.f ? sink_fn : nullptr;
+        PipelineResult res = reads->paired ? run_pipeline_pe(reads->r1, reads->r2, *m->eng, mc, po, sk, &st)
+                                           : run_pipeline_se(reads->r1, *m->eng, mc, po, sk, &st);
         if (st.f) fclose(st.f);
         if (out) {
             out->n_reads = res.stats.n_reads;
             out->sam_bytes = res.sam_bytes;
-            out->sam_hash = st.hash;
+            out->sam_hash = res.sam_digest.h;
             out->sw_calls = res.stats.tot_aligner_calls;
             out->tried = res.stats.tot_all_tried;
             out->nam_rescue = res.stats.nam_rescue;
             out->mate_rescue = res.stats.tot_rescued;
             out->inconsistent = res.stats.inconsistent_nams;
             out->map_seconds = res.map_seconds;
+            out->t_seed = res.phases.seed;
+            out->t_extend = res.phases.extend;
+            out->t_part = res.phases.part;
+            out->t_collect = res.phases.collect;
+            out->t_last = res.phases.last;
+            out->t_sequential = res.phases.sequential;
         }
         return 0;
     } catch (const std::exception& e) {

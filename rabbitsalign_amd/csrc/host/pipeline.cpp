@@ -24,19 +24,27 @@ namespace rsa {
 
 namespace {
 
+using Clock = std::chrono::steady_clock;
+inline double since(Clock::time_point t) { return std::chrono::duration<double>(Clock::now() - t).count(); }
+
 struct OrderedSink {
     SamSink sink;
     void* user;
+    bool digest = false;
     std::mutex m;
-    std::map<size_t, std::string> pending;
+    std::map<size_t, std::pair<std::string, SamDigest>> pending;
     size_t next = 0;
     uint64_t bytes = 0;
+    SamDigest total;
     void put(size_t idx, std::string&& s) {
+        SamDigest d;
+        if (digest) d = SamDigest::of(s);            // in the calling worker
         std::lock_guard<std::mutex> g(m);
-        pending.emplace(idx, std::move(s));
+        pending.emplace(idx, std::make_pair(std::move(s), d));
         for (auto it = pending.find(next); it != pending.end(); it = pending.find(next)) {
-            bytes += it->second.size();
-            sink(user, it->second);
+            bytes += it->second.first.size();
+            total.append(it->second.second);
+            if (sink) sink(user, it->second.first);
             pending.erase(it);
             next++;
         }
@@ -49,6 +57,7 @@ struct PeChunk {
     std::vector<AlignTmpRes> res;
     std::minstd_rand rng;
     AlignmentStatistics stats;
+    PhaseTimes times;
 };
 
 void pe_load(PeChunk& c, const std::vector<Record>& a, const std::vector<Record>& b, size_t idx, size_t chunk) {
@@ -72,7 +81,10 @@ void pe_part(PeChunk& c, Engine& eng, const MapContext& mc, InsertSizeDistributi
     reads.reserve(2 * n);
     for (size_t i = 0; i < n; ++i) { reads.push_back(&c.r1[i].seq); reads.push_back(&c.r2[i].seq); }
     SeedBatchOut so;
+    auto t = Clock::now();
     eng.seed(reads, mc.mparams.rescue_level, (unsigned)mc.mparams.rescue_cutoff, so);
+    c.times.seed += since(t);
+    t = Clock::now();
     for (size_t i = 0; i < n; ++i) {
         std::vector<Nam> nams[2];
         bool rescued[2];
@@ -84,18 +96,22 @@ void pe_part(PeChunk& c, Engine& eng, const MapContext& mc, InsertSizeDistributi
         align_PE_read_part(c.res[i], c.r1[i], c.r2[i], nams, rescued, c.stats, isize, mc, c.rng);
         c.stats.n_reads += 2;
     }
+    c.times.part += since(t);
 }
 
 void pe_get_str(PeChunk& c, const MapContext& mc, float mu, float sigma, std::vector<SwJob>& jobs) {
+    const auto t = Clock::now();
     jobs.clear();
     for (size_t i = 0; i < c.r1.size(); ++i) {
         Read read1(c.r1[i].seq), read2(c.r2[i].seq);
         collect_jobs_pe(c.res[i], c.r1[i], c.r2[i], read1, read2, mc, mu, sigma, jobs);
     }
+    c.times.collect += since(t);
 }
 
 void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistribution& isize,
                    const std::vector<AlignmentInfo>& infos, const std::string& rg_id, std::string& out) {
+    const auto t = Clock::now();
     size_t pos = 0;
     for (size_t i = 0; i < c.r1.size(); ++i) {
         Read read1(c.r1[i].seq), read2(c.r2[i].seq);
@@ -106,6 +122,7 @@ void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistributio
     Sam sam(out, mc.refs, mc.mparams.cigar_eqx, rg_id, mc.mparams.output_unmapped, mc.mparams.details);
     for (size_t i = 0; i < c.r1.size(); ++i)
         align_PE_read_last(c.res[i], c.r1[i], c.r2[i], sam, c.stats, isize, mc, c.rng);
+    c.times.last += since(t);
 }
 
 }  // namespace
@@ -114,7 +131,7 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                                const MapContext& mc, const PipelineOptions& opt, SamSink sink, void* user) {
     auto t0 = std::chrono::steady_clock::now();
     PipelineResult result;
-    OrderedSink os{sink, user};
+    OrderedSink os{sink, user, opt.digest};
     const size_t chunk = (size_t)std::max(1, opt.chunk_size);
     const size_t n_chunks = (r1.size() + chunk - 1) / chunk;
     InsertSizeDistribution isize;
@@ -135,15 +152,20 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
             pe_part(*cur, eng, mc, isize);
         }
         next_chunk++;
+        const auto te = Clock::now();
         eng.extend(jobs, mc.aparams, infos);
+        pre->times.extend += since(te);
         pre->stats.tot_aligner_calls += jobs.size();
         std::string out;
         pe_store_last(*pre, mc, isize, infos, opt.rg_id, out);
         os.put(pre->index, std::move(out));
         result.stats.add(pre->stats);
+        result.phases.add(pre->times);
+        pre->times = PhaseTimes();
         if (!have) { pre.reset(); break; }
         pre = std::move(cur);
     }
+    result.phases.sequential = since(t0);
     // ---- frozen: chunk-parallel ----
     if (pre || next_chunk < n_chunks) {
         const InsertSizeDistribution frozen = isize;
@@ -155,6 +177,7 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
             std::vector<SwJob> wj;
             std::vector<AlignmentInfo> wi;
             AlignmentStatistics local;
+            PhaseTimes lt;
             for (;;) {
                 std::unique_ptr<PeChunk> c;
                 {
@@ -170,15 +193,19 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                     pe_part(*c, eng, mc, est);
                 }
                 pe_get_str(*c, mc, frozen.mu, frozen.sigma, wj);
+                const auto te = Clock::now();
                 eng.extend(wj, mc.aparams, wi);
+                c->times.extend += since(te);
                 c->stats.tot_aligner_calls += wj.size();
                 std::string out;
                 pe_store_last(*c, mc, frozen, wi, opt.rg_id, out);
                 os.put(c->index, std::move(out));
                 local.add(c->stats);
+                lt.add(c->times);
             }
             std::lock_guard<std::mutex> g(stat_m);
             result.stats.add(local);
+            result.phases.add(lt);
         };
         std::vector<std::thread> ws;
         const int T = std::max(1, opt.threads);
@@ -187,6 +214,7 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
     }
     result.map_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     result.sam_bytes = os.bytes;
+    result.sam_digest = os.total;
     return result;
 }
 
@@ -196,7 +224,7 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
                                const PipelineOptions& opt, SamSink sink, void* user) {
     auto t0 = std::chrono::steady_clock::now();
     PipelineResult result;
-    OrderedSink os{sink, user};
+    OrderedSink os{sink, user, opt.digest};
     const size_t chunk = (size_t)std::max(1, opt.chunk_size);
     const size_t n_chunks = (recs.size() + chunk - 1) / chunk;
     std::atomic<size_t> next{0};
@@ -250,6 +278,7 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
     for (auto& w : ws) w.join();
     result.map_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     result.sam_bytes = os.bytes;
+    result.sam_digest = os.total;
     return result;
 }
 

@@ -256,12 +256,46 @@ struct PipelineOptions {
     int chunk_size = 10000;
     bool interleaved = false;
     std::string rg_id;
+    bool digest = false;   // compute PipelineResult::sam_digest (in the workers, in parallel)
+};
+
+// Order-sensitive digest of a SAM body, independent of how it is chunked:
+// D = sum_k fnv1a64(line_k) * P^(N-1-k) mod 2^64 over the N lines (without '\n').
+struct SamDigest {
+    static constexpr uint64_t P = 0x100000001b3ULL;
+    uint64_t h = 0, lines = 0;
+    static uint64_t pow(uint64_t b, uint64_t e) {
+        uint64_t r = 1;
+        for (; e; e >>= 1, b *= b) if (e & 1) r *= b;
+        return r;
+    }
+    static SamDigest of(const std::string& s) {
+        SamDigest d;
+        uint64_t lh = 1469598103934665603ULL;
+        for (unsigned char c : s) {
+            if (c == '\n') { d.h = d.h * P + lh; d.lines++; lh = 1469598103934665603ULL; }
+            else { lh ^= c; lh *= 1099511628211ULL; }
+        }
+        return d;
+    }
+    void append(const SamDigest& o) { h = h * pow(P, o.lines) + o.h; lines += o.lines; }
+};
+
+// thread-summed seconds per phase (instrumentation of the host pipeline)
+struct PhaseTimes {
+    double seed = 0, extend = 0, part = 0, collect = 0, last = 0, sequential = 0;
+    void add(const PhaseTimes& o) {
+        seed += o.seed; extend += o.extend; part += o.part; collect += o.collect; last += o.last;
+        sequential += o.sequential;
+    }
 };
 
 struct PipelineResult {
     AlignmentStatistics stats;
     double map_seconds = 0;
     uint64_t sam_bytes = 0;
+    SamDigest sam_digest;
+    PhaseTimes phases;
 };
 
 // perform_task_async_{pe,se} (src/pc.cpp:814-1096, 1522-1887) with -t 1 semantics:

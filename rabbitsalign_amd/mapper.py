@@ -23,7 +23,9 @@ PRODUCT_LIB = os.path.join(LIB_DIR, "librsalign.so")
 class _Stats(C.Structure):
     _fields_ = [("n_reads", C.c_uint64), ("sam_bytes", C.c_uint64), ("sam_hash", C.c_uint64),
                 ("sw_calls", C.c_uint64), ("tried", C.c_uint64), ("nam_rescue", C.c_uint64),
-                ("mate_rescue", C.c_uint64), ("inconsistent", C.c_uint64), ("map_seconds", C.c_double)]
+                ("mate_rescue", C.c_uint64), ("inconsistent", C.c_uint64), ("map_seconds", C.c_double),
+                ("t_seed", C.c_double), ("t_extend", C.c_double), ("t_part", C.c_double),
+                ("t_collect", C.c_double), ("t_last", C.c_double), ("t_sequential", C.c_double)]
 
 
 class _Info(C.Structure):
@@ -85,6 +87,12 @@ class MapStats:
     mate_rescue: int
     inconsistent: int
     map_seconds: float
+    t_seed: float = 0.0
+    t_extend: float = 0.0
+    t_part: float = 0.0
+    t_collect: float = 0.0
+    t_last: float = 0.0
+    t_sequential: float = 0.0
 
 
 class Reads:

@@ -76,9 +76,10 @@ class AlnBatch(C.Structure):
                 ("cigar_used", C.c_uint64)]
 
 
-KERNELS = ["randstrobes", "lookup", "find_nams", "rescue", "compact", "ext_scan", "ext_band"]
+KERNELS = ["randstrobes", "lookup", "find_nams", "rescue", "compact", "ext_scan", "ext_band", "ext_band_lane"]
 KERNEL_SYMBOLS = {"randstrobes": "k_randstrobes", "lookup": "k_lookup", "find_nams": "k_find_nams",
-                  "rescue": "k_rescue", "compact": "k_compact", "ext_scan": "k_ext_scan", "ext_band": "k_ext_band"}
+                  "rescue": "k_rescue", "compact": "k_compact", "ext_scan": "k_ext_scan", "ext_band": "k_ext_band16",
+                  "ext_band_lane": "k_ext_band"}
 NK = len(KERNELS)
 
 

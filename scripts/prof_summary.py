@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 databases of a bench run into profiles/.
+
+    python scripts/prof_summary.py gpurun_out/prof_r01 profiles/r01
+
+reads <dir>/trace/run_results.db (--kernel-trace --stats), and, when present,
+<dir>/pmc_fetch/run_results.db and <dir>/pmc_write/run_results.db (one PMC
+counter per pass).  Writes <out>_rocprof.md (per-kernel table) and
+<out>_traffic.json (HBM bytes per launch per kernel: FETCH_SIZE doubled, the
+gfx950 correction of MI355X_MICROARCH.md "HBM", plus WRITE_SIZE, both KB->B).
+"""
+import json
+import os
+import sqlite3
+import sys
+
+
+def short(name: str) -> str:
+    return name.split("(")[0]
+
+
+def kernel_times(db):
+    c = sqlite3.connect(db)
+    rows = c.execute("select name, count(*), sum(duration), avg(duration), min(duration), max(duration) "
+                     "from kernels group by name").fetchall()
+    return {short(r[0]): {"calls": r[1], "total_ms": r[2] / 1e6, "avg_us": r[3] / 1e3, "min_us": r[4] / 1e3,
+                          "max_us": r[5] / 1e3} for r in rows}
+
+
+def counter(db, cname):
+    c = sqlite3.connect(db)
+    rows = c.execute("select kernel_name, count(*), avg(value), sum(value) from counters_collection "
+                     "where counter_name = ? group by kernel_name", (cname,)).fetchall()
+    return {short(r[0]): {"dispatches": r[1], "avg_kb": r[2], "sum_kb": r[3]} for r in rows}
+
+
+def main():
+    src, out = sys.argv[1], sys.argv[2]
+    kt = kernel_times(os.path.join(src, "trace", "run_results.db"))
+    fetch = write = {}
+    fdb = os.path.join(src, "pmc_fetch", "run_results.db")
+    wdb = os.path.join(src, "pmc_write", "run_results.db")
+    if os.path.exists(fdb):
+        fetch = counter(fdb, "FETCH_SIZE")
+    if os.path.exists(wdb):
+        write = counter(wdb, "WRITE_SIZE")
+    total = sum(v["total_ms"] for v in kt.values())
+    lines = [f"# rocprofv3 summary: {src}", "",
+             "Kernel trace (`rocprofv3 --kernel-trace --stats`), PMC in separate passes "
+             "(`--pmc FETCH_SIZE`, `--pmc WRITE_SIZE`). HBM read bytes = 2 x FETCH_SIZE (gfx950 correction).", "",
+             "| kernel | calls | total ms | % | avg us | min us | max us | HBM read B/launch | HBM write B/launch |",
+             "|---|---:|---:|---:|---:|---:|---:|---:|---:|"]
+    traffic = {}
+    for k, v in sorted(kt.items(), key=lambda kv: -kv[1]["total_ms"]):
+        rd = 2 * 1024 * fetch[k]["avg_kb"] if k in fetch else None
+        wr = 1024 * write[k]["avg_kb"] if k in write else None
+        if rd is not None or wr is not None:
+            traffic[k] = {"read_bytes": rd, "write_bytes": wr,
+                          "bytes": (rd or 0) + (wr or 0) if rd is not None and wr is not None else None}
+        lines.append(f"| {k} | {v['calls']} | {v['total_ms']:.2f} | {100 * v['total_ms'] / total:.1f} | "
+                     f"{v['avg_us']:.1f} | {v['min_us']:.1f} | {v['max_us']:.1f} | "
+                     f"{'' if rd is None else f'{rd:.0f}'} | {'' if wr is None else f'{wr:.0f}'} |")
+    with open(out + "_rocprof.md", "w") as f:
+        f.write("\n".join(lines) + "\n")
+    with open(out + "_traffic.json", "w") as f:
+        json.dump({"source": src, "kernels": kt, "traffic_per_launch": traffic}, f, indent=1)
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
