@@ -24,7 +24,8 @@ typedef struct rsam_reads rsam_reads;  /* a read set held in host memory */
 typedef struct rsam_stats {
     uint64_t n_reads;         /* reads mapped (each mate counts, pc.cpp:1596) */
     uint64_t sam_bytes;       /* SAM body bytes produced */
-    uint64_t sam_hash;        /* sum_k fnv1a64(line_k) * 0x100000001b3^(N-1-k) mod 2^64 over SAM body lines */
+    uint64_t sam_hash;        /* sum_k line_hash(line_k) * 0x100000001b3^(N-1-k) mod 2^64 over SAM body lines
+                                 (line_hash: rsa_host.hpp SamDigest) */
     uint64_t sw_calls, tried, nam_rescue, mate_rescue, inconsistent;
     double map_seconds;       /* first chunk read -> last SAM byte (consumer cost, main.cpp:446,595) */
     /* host pipeline phases, seconds summed over worker threads (PE path) */

@@ -10,6 +10,8 @@
 #include <math.h>
 #include <unordered_set>
 
+#include <emmintrin.h>
+
 #include "rsa_host.hpp"
 
 namespace rsa {
@@ -33,8 +35,6 @@ std::string reverse_complement(std::string_view s) {
     for (size_t i = 0; i < s.size(); ++i) r[i] = (char)t[(unsigned char)s[s.size() - 1 - i]];
     return r;
 }
-
-Read::Read(const std::string& s) : seq(s), rc(reverse_complement(s)) {}
 
 void to_uppercase(std::string& s) {
     for (auto& c : s) c = (char)((unsigned char)c & ~32);
@@ -216,57 +216,77 @@ static std::vector<NamPair> get_best_scoring_nam_pairs(const std::vector<Nam>& n
 }
 
 // ------------------------------------------------------------ hamming ---
-static int hamming_distance(std::string_view s, std::string_view t) {   // aligner.hpp:54-67
-    if (s.size() != t.size()) return -1;
-    int m = 0;
-    for (size_t i = 0; i < s.size(); ++i) m += s[i] != t[i];
-    return m;
+// Mismatch positions of two equal-length strings, 16 bytes per SSE2 compare.
+// Returns the mismatch count; the first `cap` positions are stored in pos.
+static int mismatch_positions(const char* q, const char* r, size_t n, int* pos, int cap) {
+    int cnt = 0;
+    size_t i = 0;
+    for (; i + 16 <= n; i += 16) {
+        const __m128i a = _mm_loadu_si128((const __m128i*)(q + i));
+        const __m128i b = _mm_loadu_si128((const __m128i*)(r + i));
+        unsigned m = ~(unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(a, b)) & 0xFFFFu;
+        while (m) {
+            const int bit = __builtin_ctz(m);
+            if (cnt < cap) pos[cnt] = (int)i + bit;
+            cnt++;
+            m &= m - 1;
+        }
+    }
+    for (; i < n; ++i)
+        if (q[i] != r[i]) { if (cnt < cap) pos[cnt] = (int)i; cnt++; }
+    return cnt;
 }
 
-// aligner.cpp:219-252
-static void highest_scoring_segment(std::string_view q, std::string_view r, int match, int mismatch, int end_bonus,
+// highest_scoring_segment (aligner.cpp:219-252), evaluated run by run: between
+// mismatches the score only grows, so the per-position updates of the
+// reference collapse to one check at the end of each run of matches.
+static void highest_scoring_segment(size_t n, const int* mm, int n_mm, int match, int mismatch, int end_bonus,
                                     size_t& bs, size_t& be, int& bsc) {
-    size_t n = q.size(), start = 0;
-    int score = end_bonus;
-    size_t best_start = 0, best_end = 0;
-    int best_score = 0;
-    for (size_t i = 0; i < n; ++i) {
-        if (q[i] == r[i]) score += match; else score -= mismatch;
-        if (score < 0) { start = i + 1; score = 0; }
-        if (score > best_score) { best_start = start; best_score = score; best_end = i + 1; }
+    size_t start = 0, best_start = 0, best_end = 0;
+    int score = end_bonus, best_score = 0;
+    size_t i = 0;
+    for (int k = 0; k <= n_mm; ++k) {
+        const size_t m = k < n_mm ? (size_t)mm[k] : n;
+        if (m > i) {
+            score += match * (int)(m - i);
+            if (score > best_score) { best_start = start; best_score = score; best_end = m; }
+        }
+        if (k == n_mm) break;
+        score -= mismatch;
+        if (score < 0) { start = m + 1; score = 0; }
+        if (score > best_score) { best_start = start; best_score = score; best_end = m + 1; }
+        i = m + 1;
     }
     if (score + end_bonus > best_score) {
         best_score = score + end_bonus;
-        best_end = q.size();
+        best_end = n;
         best_start = start;
     }
     bs = best_start; be = best_end; bsc = best_score;
 }
 
-// aligner.cpp:254-302
-static AlignmentInfo hamming_align(std::string_view q, std::string_view r, int match, int mismatch, int end_bonus) {
+// hamming_align (aligner.cpp:254-302) from the mismatch positions
+static AlignmentInfo hamming_align(size_t n, const int* mm, int n_mm, int match, int mismatch, int end_bonus) {
     AlignmentInfo aln;
-    if (q.size() != r.size()) return aln;
     size_t s, e;
     int score;
-    highest_scoring_segment(q, r, match, mismatch, end_bonus, s, e, score);
+    highest_scoring_segment(n, mm, n_mm, match, mismatch, end_bonus, s, e, score);
     Cigar cigar;
+    cigar.ops.reserve(2 * (size_t)n_mm + 4);
     if (s > 0) cigar.push(C_S, (uint32_t)s);
-    int counter = 0, mismatches = 0;
-    bool prev_is_match = false, first = true;
-    for (size_t i = s; i < e; i++) {
-        bool is_match = q[i] == r[i];
-        mismatches += is_match ? 0 : 1;
-        if (!first && is_match != prev_is_match) {
-            cigar.push(prev_is_match ? C_EQ : C_X, (uint32_t)counter);
-            counter = 0;
-        }
-        counter++;
-        prev_is_match = is_match;
-        first = false;
+    int mismatches = 0;
+    size_t cur = s;
+    for (int k = 0; k < n_mm; ++k) {
+        const size_t m = (size_t)mm[k];
+        if (m < s) continue;
+        if (m >= e) break;
+        if (m > cur) cigar.push(C_EQ, (uint32_t)(m - cur));
+        cigar.push(C_X, 1);
+        mismatches++;
+        cur = m + 1;
     }
-    if (!first) cigar.push(prev_is_match ? C_EQ : C_X, (uint32_t)counter);
-    int soft_right = (int)q.size() - (int)e;
+    if (e > cur) cigar.push(C_EQ, (uint32_t)(e - cur));
+    int soft_right = (int)n - (int)e;
     if (soft_right > 0) cigar.push(C_S, (uint32_t)soft_right);
     aln.cigar = std::move(cigar);
     aln.sw_score = score;
@@ -289,9 +309,17 @@ static bool extend_seed_part(AlignTmpRes& res, const AlignmentParameters& ap, co
     bool gapped = true;
     if (projected_ref_end - projected_ref_start == query.size() && consistent_nam) {
         std::string_view segm = sub(ref, (size_t)projected_ref_start, query.size());
-        int hd = hamming_distance(query, segm);
+        int mm[64];
+        const int hd = segm.size() == query.size()
+                           ? mismatch_positions(query.data(), segm.data(), query.size(), mm, 64) : -1;
         if (hd >= 0 && (((float)hd / query.size()) < 0.05)) {
-            info = hamming_align(query, segm, ap.match, ap.mismatch, ap.end_bonus);
+            if (hd > 64) {   // reads > 1280 bp only: positions beyond the buffer
+                std::vector<int> all(hd);
+                mismatch_positions(query.data(), segm.data(), query.size(), all.data(), hd);
+                info = hamming_align(query.size(), all.data(), hd, ap.match, ap.mismatch, ap.end_bonus);
+            } else {
+                info = hamming_align(query.size(), mm, hd, ap.match, ap.mismatch, ap.end_bonus);
+            }
             result_ref_start = projected_ref_start + (int)info.ref_start;
             gapped = false;
         }
@@ -399,9 +427,8 @@ static void rescue_read_part(int flag, AlignTmpRes& res, const Read& read2, cons
 
 // align_PE_part (aln.cpp:1372-1580)
 static void align_PE_part(AlignTmpRes& res, const MapContext& mc, std::vector<Nam>& nams1, std::vector<Nam>& nams2,
-                          const Record& r1, const Record& r2, int k, Details det[2], InsertSizeDistribution& isize) {
+                          const Read& read1, const Read& read2, int k, Details det[2], InsertSizeDistribution& isize) {
     const float mu = isize.mu, sigma = isize.sigma;
-    Read read1(r1.seq), read2(r2.seq);
     const float dropoff = mc.mparams.dropoff_threshold;
     const unsigned max_tries = (unsigned)mc.mparams.max_tries;
     if (nams1.empty() && nams2.empty()) { res.type = 0; return; }
@@ -509,7 +536,8 @@ static void align_PE_part(AlignTmpRes& res, const MapContext& mc, std::vector<Na
 }
 
 // align_PE_read_part (aln.cpp:1927-1981); the find_nams/rescue results come from the engine
-void align_PE_read_part(AlignTmpRes& res, const Record& r1, const Record& r2, std::vector<Nam> nams[2],
+void align_PE_read_part(AlignTmpRes& res, const Record&, const Record&, const Read& read1, const Read& read2,
+                        std::vector<Nam> nams[2],
                         const bool rescued[2], AlignmentStatistics& stats, InsertSizeDistribution& isize,
                         const MapContext& mc, std::minstd_rand& rng) {
     Details det[2];
@@ -519,13 +547,13 @@ void align_PE_read_part(AlignTmpRes& res, const Record& r1, const Record& r2, st
         std::sort(nams[m].begin(), nams[m].end(), by_score<Nam>);
         shuffle_top_nams(nams[m], rng);
     }
-    align_PE_part(res, mc, nams[0], nams[1], r1, r2, mc.iparams.k, det, isize);
+    align_PE_part(res, mc, nams[0], nams[1], read1, read2, mc.iparams.k, det, isize);
     stats.add(det[0]);
     stats.add(det[1]);
 }
 
 // align_SE_part (aln.cpp:95-124)
-void align_SE_read_part(AlignTmpRes& res, const Record& r, std::vector<Nam>& nams, bool rescued,
+void align_SE_read_part(AlignTmpRes& res, const Record&, const Read& read, std::vector<Nam>& nams, bool rescued,
                         AlignmentStatistics& stats, const MapContext& mc, std::minstd_rand& rng) {
     Details det;
     if (mc.mparams.rescue_level > 1 && rescued) det.nam_rescue = true;
@@ -535,7 +563,6 @@ void align_SE_read_part(AlignTmpRes& res, const Record& r, std::vector<Nam>& nam
     if (nams.empty()) {
         res.type = 0;
     } else {
-        Read read(r.seq);
         int tries = 0;
         const Nam n_max = nams[0];
         res.type = 4;
@@ -788,12 +815,12 @@ static void rescue_read_last(AlignTmpRes& res, const Read& read2, const Read& re
 }
 
 // align_PE_read_last (aln.cpp:2083-2306)
-void align_PE_read_last(AlignTmpRes& res, const Record& rec1, const Record& rec2, Sam& sam,
+void align_PE_read_last(AlignTmpRes& res, const Record& rec1, const Record& rec2, const Read& read1, const Read& read2,
+                        Sam& sam,
                         AlignmentStatistics& stats, const InsertSizeDistribution& isize, const MapContext& mc,
                         std::minstd_rand& rng) {
     Details det[2];
     const float mu = isize.mu, sigma = isize.sigma;
-    Read read1(rec1.seq), read2(rec2.seq);
     if (res.type == 0) {
         sam.add_unmapped_pair(rec1, rec2);
     } else if (res.type == 1) {
@@ -883,14 +910,13 @@ void align_PE_read_last(AlignTmpRes& res, const Record& rec1, const Record& rec2
 }
 
 // align_SE_read_last (aln.cpp:126-238)
-void align_SE_read_last(AlignTmpRes& res, const Record& rec, Sam& sam, AlignmentStatistics& stats,
+void align_SE_read_last(AlignTmpRes& res, const Record& rec, const Read& read, Sam& sam, AlignmentStatistics& stats,
                         const MapContext& mc, std::minstd_rand& rng) {
     Details det;
     if (res.type == 0) {
         sam.add_unmapped(rec);
         return;
     }
-    Read read(rec.seq);
     std::vector<Alignment> alignments;
     int tries = 0;
     const Nam n_max = res.todo_nams[0];

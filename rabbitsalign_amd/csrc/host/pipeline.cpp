@@ -54,6 +54,7 @@ struct OrderedSink {
 struct PeChunk {
     size_t index = 0, begin = 0, end = 0;
     std::vector<Record> r1, r2;               // upper-cased copies (pc.cpp:1586-1587)
+    std::vector<std::string> rc1, rc2;        // their reverse complements, computed once
     std::vector<AlignTmpRes> res;
     std::minstd_rand rng;
     AlignmentStatistics stats;
@@ -68,6 +69,12 @@ void pe_load(PeChunk& c, const std::vector<Record>& a, const std::vector<Record>
     c.r2.assign(b.begin() + c.begin, b.begin() + c.end);
     for (auto& r : c.r1) to_uppercase(r.seq);
     for (auto& r : c.r2) to_uppercase(r.seq);
+    c.rc1.resize(c.r1.size());
+    c.rc2.resize(c.r2.size());
+    for (size_t i = 0; i < c.r1.size(); ++i) {
+        c.rc1[i] = reverse_complement(c.r1[i].seq);
+        c.rc2[i] = reverse_complement(c.r2[i].seq);
+    }
     c.res.clear();
     c.res.resize(c.r1.size());
 }
@@ -93,7 +100,8 @@ void pe_part(PeChunk& c, Engine& eng, const MapContext& mc, InsertSizeDistributi
             nams[m].assign(so.nams.begin() + (long)so.offsets[r], so.nams.begin() + (long)so.offsets[r + 1]);
             rescued[m] = so.rescued[r] != 0;
         }
-        align_PE_read_part(c.res[i], c.r1[i], c.r2[i], nams, rescued, c.stats, isize, mc, c.rng);
+        const Read read1(c.r1[i].seq, c.rc1[i]), read2(c.r2[i].seq, c.rc2[i]);
+        align_PE_read_part(c.res[i], c.r1[i], c.r2[i], read1, read2, nams, rescued, c.stats, isize, mc, c.rng);
         c.stats.n_reads += 2;
     }
     c.times.part += since(t);
@@ -103,7 +111,7 @@ void pe_get_str(PeChunk& c, const MapContext& mc, float mu, float sigma, std::ve
     const auto t = Clock::now();
     jobs.clear();
     for (size_t i = 0; i < c.r1.size(); ++i) {
-        Read read1(c.r1[i].seq), read2(c.r2[i].seq);
+        const Read read1(c.r1[i].seq, c.rc1[i]), read2(c.r2[i].seq, c.rc2[i]);
         collect_jobs_pe(c.res[i], c.r1[i], c.r2[i], read1, read2, mc, mu, sigma, jobs);
     }
     c.times.collect += since(t);
@@ -114,14 +122,16 @@ void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistributio
     const auto t = Clock::now();
     size_t pos = 0;
     for (size_t i = 0; i < c.r1.size(); ++i) {
-        Read read1(c.r1[i].seq), read2(c.r2[i].seq);
+        const Read read1(c.r1[i].seq, c.rc1[i]), read2(c.r2[i].seq, c.rc2[i]);
         pos = store_results_pe(c.res[i], read1, read2, mc, isize.mu, isize.sigma, infos, pos);
     }
     out.clear();
     out.reserve(7 * (size_t)mc.mparams.r * c.r1.size());
     Sam sam(out, mc.refs, mc.mparams.cigar_eqx, rg_id, mc.mparams.output_unmapped, mc.mparams.details);
-    for (size_t i = 0; i < c.r1.size(); ++i)
-        align_PE_read_last(c.res[i], c.r1[i], c.r2[i], sam, c.stats, isize, mc, c.rng);
+    for (size_t i = 0; i < c.r1.size(); ++i) {
+        const Read read1(c.r1[i].seq, c.rc1[i]), read2(c.r2[i].seq, c.rc2[i]);
+        align_PE_read_last(c.res[i], c.r1[i], c.r2[i], read1, read2, sam, c.stats, isize, mc, c.rng);
+    }
     c.times.last += since(t);
 }
 
@@ -245,28 +255,34 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
             SeedBatchOut so;
             eng.seed(reads, mc.mparams.rescue_level, (unsigned)mc.mparams.rescue_cutoff, so);
             std::vector<AlignTmpRes> res(e - b);
+            std::vector<std::string> rcs(e - b);
+            for (size_t i = b; i < e; ++i) rcs[i - b] = reverse_complement(recs[i].seq);
             for (size_t i = b; i < e; ++i) {
                 const size_t r = i - b;
                 std::vector<Nam> nams(so.nams.begin() + (long)so.offsets[r], so.nams.begin() + (long)so.offsets[r + 1]);
-                align_SE_read_part(res[r], recs[i], nams, so.rescued[r] != 0, st, mc, rng);
+                const Read read(recs[i].seq, rcs[r]);
+                align_SE_read_part(res[r], recs[i], read, nams, so.rescued[r] != 0, st, mc, rng);
                 st.n_reads++;
             }
             jobs.clear();
             for (size_t i = b; i < e; ++i) {
-                Read read(recs[i].seq);
+                const Read read(recs[i].seq, rcs[i - b]);
                 collect_jobs_se(res[i - b], read, mc, jobs);
             }
             eng.extend(jobs, mc.aparams, infos);
             st.tot_aligner_calls += jobs.size();
             size_t pos = 0;
             for (size_t i = b; i < e; ++i) {
-                Read read(recs[i].seq);
+                const Read read(recs[i].seq, rcs[i - b]);
                 pos = store_results_se(res[i - b], read, mc, infos, pos);
             }
             std::string out;
             out.reserve(7 * (size_t)mc.mparams.r * (e - b));
             Sam sam(out, mc.refs, mc.mparams.cigar_eqx, opt.rg_id, mc.mparams.output_unmapped, mc.mparams.details);
-            for (size_t i = b; i < e; ++i) align_SE_read_last(res[i - b], recs[i], sam, st, mc, rng);
+            for (size_t i = b; i < e; ++i) {
+                const Read read(recs[i].seq, rcs[i - b]);
+                align_SE_read_last(res[i - b], recs[i], read, sam, st, mc, rng);
+            }
             os.put(idx, std::move(out));
             local.add(st);
         }
