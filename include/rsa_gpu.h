@@ -167,8 +167,14 @@ typedef struct rsa_aln_batch {
  * sentinel (sw_score -1000000), a failed SSW the -100000 sentinel. */
 int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jobs, rsa_aln_batch* out);
 
-/* upper bound of cigar_pool entries needed for a batch */
+/* upper bound of cigar_pool entries needed for a batch (the pool comes back
+ * packed: cigar_used <= bound entries, alns[i].cigar_offset indexes it) */
 uint64_t rsa_extend_cigar_bound(const rsa_job_batch* jobs);
+
+/* Page-locked host memory for batch buffers (DMA-speed H2D/D2H); any caller
+ * buffer works, these are only faster.  NULL on failure. */
+void* rsa_host_alloc(size_t bytes);
+void rsa_host_free(void* p);
 
 /* ---- instrumentation ------------------------------------------------------ */
 
@@ -181,8 +187,9 @@ enum {
     RSA_K_COMPACT = 4,     /* NAM output compaction */
     RSA_K_EXT_SCAN = 5,    /* SSW forward/reverse score scans (ssw.c:121-620) */
     RSA_K_EXT_BAND = 6,    /* banded_sw + traceback + Aligner::align, 16 lanes/job (ssw.c:622-790, aligner.cpp:114-210) */
-    RSA_K_EXT_BAND_LANE = 7, /* the same, one lane per job, for jobs the 16-lane kernel defers */
-    RSA_K_COUNT = 8
+    RSA_K_EXT_BAND_WIDE = 7, /* the same, 64 lanes/job, for the jobs the 16-lane kernel queues */
+    RSA_K_EXT_BAND_LANE = 8, /* the same, one lane per job with global scratch (bands > 64 cells) */
+    RSA_K_COUNT = 9
 };
 
 typedef struct rsa_kernel_stats {
@@ -192,6 +199,7 @@ typedef struct rsa_kernel_stats {
     uint64_t seed_calls, ext_calls;
     uint64_t reads, read_bases, query_randstrobes, lookups_found, filtered, hits, nams, rescued_reads;
     uint64_t jobs, dp_cells;         /* dp_cells: sum query_len * ref_len of the forward scan */
+    uint64_t band_deferred, band_overflow;   /* jobs handed to the 64-lane / one-lane band kernels */
 } rsa_kernel_stats;
 
 int rsa_get_stats(rsa_ctx* ctx, rsa_kernel_stats* out);

@@ -474,7 +474,8 @@ k_ext_band(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan,
 }
 
 // ---------------------------------------------------------------------------
-// k_ext_band16: banded_sw with 16 lanes per job (4 jobs per wave64).
+// Group-parallel banded_sw: G lanes per job (G = 16: 4 jobs per wave; G = 64:
+// one job per wave).
 //
 // Same result as banded_sw_dev, computed row by row with one band cell per
 // lane.  The band arrays (h_b, e_b) and the direction matrix keep the
@@ -483,54 +484,66 @@ k_ext_band(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan,
 // only serial term is F (horizontal gap); with gap_open >= gap_extend
 //     F_j = max(H'_{j-1} - gO, F_{j-1} - gE),  H' = max(E+, diag)
 // equals the reference's recurrence on the full H (the F-arm of H never wins
-// the next F), so it is a max-plus prefix scan over the 16 lanes of the group
-// (DPP row_shr 1,2,4,8).  Jobs the group cannot hold (band wider than 16
-// cells, direction bytes beyond B16_DIRCAP, long segments, gO < gE, scan
-// sentinels) are flagged in `defer` for k_ext_band.
+// the next F), so it is a max-plus prefix scan over the lanes of the group
+// (DPP row_shr 1,2,4,8 for G = 16; shuffles for the 64-lane group).
+//
+//  k_ext_band16  every job; jobs whose band is wider than 16 cells, whose
+//                direction matrix exceeds 4 KB or whose segments are long are
+//                appended to a device queue (no host round trip).
+//  k_ext_band64  drains that queue, one wave per job, 32 KB direction matrix
+//                in LDS.  Whatever still does not fit is flagged in `overflow`
+//                for the one-lane kernel with global scratch (k_ext_band).
 // ---------------------------------------------------------------------------
-#define B16_GROUPS 4
-#define B16_DIRCAP 4096
-#define B16_SEGCAP 320
-#define B16_NEG (-0x20000000)
+#define BG_NEG (-0x20000000)
 
-template <int S>
-__device__ __forceinline__ int grp_shr(int v) {
-    // lane z of a 16-lane row receives lane z-S; z < S receives B16_NEG
-    return __builtin_amdgcn_update_dpp(B16_NEG, v, 0x110 + S, 0xf, 0xf, false);
+template <int G, int S>
+__device__ __forceinline__ int gshr(int v) {
+    // lane z of the group receives lane z-S; z < S receives BG_NEG
+    if constexpr (G == 16) {
+        return __builtin_amdgcn_update_dpp(BG_NEG, v, 0x110 + S, 0xf, 0xf, false);
+    } else {
+        const int x = __shfl_up(v, S, 64);
+        return (int)(threadIdx.x & 63) < S ? BG_NEG : x;
+    }
 }
 
-__device__ __forceinline__ int grp_max(int v) {
-    for (int o = 8; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 16));
+template <int G>
+__device__ __forceinline__ int gmax(int v) {
+    for (int o = G / 2; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, G));
     return v;
+}
+
+template <int G>
+__device__ __forceinline__ int gscan_f(int A, int gE) {
+    int X = A;
+    X = max(X, gshr<G, 1>(X) - gE);
+    X = max(X, gshr<G, 2>(X) - 2 * gE);
+    X = max(X, gshr<G, 4>(X) - 4 * gE);
+    X = max(X, gshr<G, 8>(X) - 8 * gE);
+    if constexpr (G > 16) {
+        X = max(X, gshr<G, 16>(X) - 16 * gE);
+        X = max(X, gshr<G, 32>(X) - 32 * gE);
+    }
+    return X;
 }
 
 #define WSYNC() do { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); } while (0)
 
-__global__ void __launch_bounds__(64)
-k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan, int n_jobs,
-             const char* __restrict__ qbuf, const char* __restrict__ ref, uint32_t* __restrict__ cig_pool,
-             uint32_t* __restrict__ raw_pool, rsa_aln* __restrict__ out, int match, int mismatch, int gO, int gE,
-             int bonus, int* __restrict__ defer) {
-    __shared__ __attribute__((aligned(16))) int8_t s_dir[B16_GROUPS][B16_DIRCAP];
-    __shared__ int s_hb[B16_GROUPS][32];
-    __shared__ int s_eb[B16_GROUPS][32];
-    __shared__ uint8_t s_qc[B16_GROUPS][B16_SEGCAP];
-    __shared__ uint8_t s_rc[B16_GROUPS][B16_SEGCAP];
-    const int lane = threadIdx.x & 63, g = lane >> 4, z = lane & 15;
-    const int j = blockIdx.x * B16_GROUPS + g;
-    if (j >= n_jobs) return;                       // whole group leaves together
-    const ExtJobDev jb = jobs[j];
-    const ScanRes sr = scan[j];
-    if (sr.status != 0) { if (z == 0) defer[j] = 1; return; }
-    if (sr.flag != 0) {                            // aligner.cpp:131-136
-        if (z == 0) {
-            rsa_aln a;
-            a.sw_score = -100000; a.edit_distance = 100000; a.ref_start = a.ref_end = a.query_start = a.query_end = 0;
-            a.cigar_offset = jb.cig_off; a.cigar_len = 0; a.pad_ = 0;
-            out[j] = a;
-        }
-        return;
-    }
+__device__ __forceinline__ void aln_sentinel(rsa_aln* out, int j, const ExtJobDev& jb, int score) {
+    rsa_aln a;
+    a.sw_score = score; a.edit_distance = 100000; a.ref_start = a.ref_end = a.query_start = a.query_end = 0;
+    a.cigar_offset = jb.cig_off; a.cigar_len = 0; a.pad_ = 0;
+    out[j] = a;
+}
+
+// banded_sw + traceback + ext_finish of job j by a group of G lanes (z = lane in
+// group).  LDS: dir[DIRCAP], hb/eb[2G], qc[QCAP], rc[RCAP].  Returns false when
+// the job does not fit the group (nothing written).
+template <int G, int DIRCAP, int QCAP, int RCAP>
+__device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr, const char* __restrict__ qbuf,
+                           const char* __restrict__ ref, uint32_t* __restrict__ cig_pool,
+                           uint32_t* __restrict__ raw_pool, rsa_aln* __restrict__ out, int match, int mismatch,
+                           int gO, int gE, int bonus, int8_t* dir, int* hb, int* eb, uint8_t* qc, uint8_t* rc) {
     const char* q = qbuf + jb.q_off;
     const char* r = ref + jb.r_off;
     const int rlen = (int)jb.rlen;
@@ -538,22 +551,19 @@ k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
     const int ref_l = sr.ref_end1 - sr.ref_begin1 + 1;
     const int read_l = sr.read_end1 - sr.read_begin1 + 1;
     int bw = abs(ref_l - read_l) + 1;
-    if (read_l > B16_SEGCAP || ref_l > B16_SEGCAP || read_l <= 0 || ref_l <= 0 || gO < gE || 2 * bw + 1 > 16) {
-        if (z == 0) defer[j] = 1;
-        return;
+    if (read_l > QCAP || ref_l > RCAP || read_l <= 0 || ref_l <= 0 || gO < gE || 2 * bw + 1 > G) return false;
+    {   // the direction matrix of the first band must fit, too
+        int s2 = 1024;
+        while ((2 * bw + 1) * read_l * 3 >= s2) s2 *= 2;
+        if (s2 > DIRCAP) return false;
     }
-    int8_t* dir = s_dir[g];
-    int* hb = s_hb[g];
-    int* eb = s_eb[g];
-    uint8_t* qc = s_qc[g];
-    uint8_t* rc = s_rc[g];
-    for (int x = z; x < read_l; x += 16) qc[x] = (uint8_t)ssw_code((unsigned char)q[sr.read_begin1 + x]);
-    for (int x = z; x < ref_l; x += 16) {
+    for (int x = z; x < read_l; x += G) qc[x] = (uint8_t)ssw_code((unsigned char)q[sr.read_begin1 + x]);
+    for (int x = z; x < ref_l; x += G) {
         const int gj = ref_begin + x;
         rc[x] = (uint8_t)((gj >= 0 && gj < rlen) ? ssw_code((unsigned char)r[gj]) : 4);
     }
-    for (int x = z * 16; x < B16_DIRCAP; x += 256) *(int4*)(dir + x) = make_int4(0, 0, 0, 0);
-    hb[z] = 0; hb[z + 16] = 0; eb[z] = 0; eb[z + 16] = 0;
+    for (int x = z * 16; x < DIRCAP; x += G * 16) *(int4*)(dir + x) = make_int4(0, 0, 0, 0);
+    hb[z] = 0; hb[z + G] = 0; eb[z] = 0; eb[z + G] = 0;
     WSYNC();
 
     const int len = ref_l > read_l ? ref_l : read_l;
@@ -562,9 +572,9 @@ k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
     do {
         const int width = bw * 2 + 3;
         width_d = bw * 2 + 1;
-        if (width_d > 16) { deferred = true; break; }
+        if (width_d > G) { deferred = true; break; }
         while (width_d * read_l * 3 >= s2) s2 *= 2;
-        if (s2 > B16_DIRCAP) { deferred = true; break; }
+        if (s2 > DIRCAP) { deferred = true; break; }
         if (z >= 1 && z <= width - 2) hb[z] = 0;
         WSYNC();
         int lmax = 0;
@@ -588,15 +598,10 @@ k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
             const int diag = hb_d + ((rv == qv && rv < 4) ? match : -mismatch);
             const int e1 = E > 0 ? E : 0;
             const int hp = e1 > diag ? e1 : diag;
-            const int prev_hp = grp_shr<1>(hp);
+            const int prev_hp = gshr<G, 1>(hp);
             const int A = z == 0 ? -gO : prev_hp - gO;
-            int X = A;
-            X = max(X, grp_shr<1>(X) - gE);
-            X = max(X, grp_shr<2>(X) - 2 * gE);
-            X = max(X, grp_shr<4>(X) - 4 * gE);
-            X = max(X, grp_shr<8>(X) - 8 * gE);
-            const int F = max(X, -(z + 1) * gE);
-            const int f_prev = z == 0 ? 0 : grp_shr<1>(F);
+            const int F = max(gscan_f<G>(A, gE), -(z + 1) * gE);
+            const int f_prev = z == 0 ? 0 : gshr<G, 1>(F);
             const int df = A > f_prev - gE ? 5 : 4;
             const int f1 = F > 0 ? F : 0;
             const int m = e1 > f1 ? e1 : f1;
@@ -612,12 +617,12 @@ k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
             if (on) hb[u] = H;                       // h_b[1..u] = h_c[1..u]
             WSYNC();
         }
-        lmax = grp_max(lmax);
+        lmax = gmax<G>(lmax);
         if (lmax > max_v) max_v = lmax;
         bw *= 2;
     } while (max_v < sr.score1 && bw <= len);
-    if (deferred) { if (z == 0) defer[j] = 1; return; }
-    if (z != 0) return;
+    if (deferred) return false;
+    if (z != 0) return true;
     bw /= 2;
 
     // traceback (ssw.c:748-776), leader lane
@@ -643,13 +648,109 @@ k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
         else { ++l; raw[l - 1] = cig((uint32_t)ecount, prev_op); prev_op = op; ecount = 1; }
     }
     if (fail) {                                     // banded_sw failed -> flag 1 sentinel
-        a.edit_distance = 100000; a.sw_score = -100000;
-        out[j] = a;
-        return;
+        aln_sentinel(out, j, jb, -100000);
+        return true;
     }
     if (op == 0) { ++l; raw[l - 1] = cig((uint32_t)ecount + 1, op); }
     else { l += 2; raw[l - 2] = cig((uint32_t)ecount, op); raw[l - 1] = cig(1, 0); }
     for (int s = 0, t = l - 1; s < t; ++s, --t) { const uint32_t x = raw[s]; raw[s] = raw[t]; raw[t] = x; }
     ext_finish(jb, sr, q, r, raw, l, cig_pool + jb.cig_off, a, match, mismatch, bonus);
     out[j] = a;
+    return true;
+}
+
+#define B16_GROUPS 4
+#define B16_DIRCAP 4096
+#define B16_SEGCAP 320
+
+__global__ void __launch_bounds__(64)
+k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan, int n_jobs,
+             const char* __restrict__ qbuf, const char* __restrict__ ref, uint32_t* __restrict__ cig_pool,
+             uint32_t* __restrict__ raw_pool, rsa_aln* __restrict__ out, int match, int mismatch, int gO, int gE,
+             int bonus, int* __restrict__ queue, int* __restrict__ qcount) {
+    __shared__ __attribute__((aligned(16))) int8_t s_dir[B16_GROUPS][B16_DIRCAP];
+    __shared__ int s_hb[B16_GROUPS][32];
+    __shared__ int s_eb[B16_GROUPS][32];
+    __shared__ uint8_t s_qc[B16_GROUPS][B16_SEGCAP];
+    __shared__ uint8_t s_rc[B16_GROUPS][B16_SEGCAP];
+    const int lane = threadIdx.x & 63, g = lane >> 4, z = lane & 15;
+    const int j = blockIdx.x * B16_GROUPS + g;
+    if (j >= n_jobs) return;                       // whole group leaves together
+    const ExtJobDev jb = jobs[j];
+    const ScanRes sr = scan[j];
+    if (sr.status != 0) {                          // ref > 2000 (aligner.cpp:119-125)
+        if (z == 0) aln_sentinel(out, j, jb, -1000000);
+        return;
+    }
+    if (sr.flag != 0) {                            // aligner.cpp:131-136
+        if (z == 0) aln_sentinel(out, j, jb, -100000);
+        return;
+    }
+    const bool done = band_group<16, B16_DIRCAP, B16_SEGCAP, B16_SEGCAP>(
+        j, z, jb, sr, qbuf, ref, cig_pool, raw_pool, out, match, mismatch, gO, gE, bonus, s_dir[g], s_hb[g],
+        s_eb[g], s_qc[g], s_rc[g]);
+    if (!done && z == 0) queue[atomicAdd(qcount, 1)] = j;
+}
+
+#define B64_DIRCAP 32768
+#define B64_QCAP 1024
+#define B64_RCAP 2048
+
+__global__ void __launch_bounds__(64)
+k_ext_band64(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan, const char* __restrict__ qbuf,
+             const char* __restrict__ ref, uint32_t* __restrict__ cig_pool, uint32_t* __restrict__ raw_pool,
+             rsa_aln* __restrict__ out, int match, int mismatch, int gO, int gE, int bonus,
+             const int* __restrict__ queue, const int* __restrict__ qcount, int* __restrict__ overflow,
+             int* __restrict__ ocount) {
+    __shared__ __attribute__((aligned(16))) int8_t s_dir[B64_DIRCAP];
+    __shared__ int s_hb[128];
+    __shared__ int s_eb[128];
+    __shared__ uint8_t s_qc[B64_QCAP];
+    __shared__ uint8_t s_rc[B64_RCAP];
+    const int z = threadIdx.x & 63;
+    const int nq = *qcount;
+    for (int t = blockIdx.x; t < nq; t += gridDim.x) {
+        const int j = queue[t];
+        const ExtJobDev jb = jobs[j];
+        const ScanRes sr = scan[j];
+        const bool done = band_group<64, B64_DIRCAP, B64_QCAP, B64_RCAP>(
+            j, z, jb, sr, qbuf, ref, cig_pool, raw_pool, out, match, mismatch, gO, gE, bonus, s_dir, s_hb, s_eb,
+            s_qc, s_rc);
+        if (!done && z == 0) { overflow[j] = 1; atomicAdd(ocount, 1); }
+        WSYNC();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_cigar_compact: one workgroup packs every job's CIGAR (written into its
+// qlen+rlen+8 slot) back to back and rewrites cigar_offset, so the host copies
+// only the ops that exist.  count[0] receives the total.
+// ---------------------------------------------------------------------------
+#define CC_THREADS 1024
+__global__ void __launch_bounds__(CC_THREADS)
+k_cigar_compact(rsa_aln* __restrict__ alns, int n_jobs, const uint32_t* __restrict__ slots,
+                uint32_t* __restrict__ dense, uint64_t* __restrict__ total) {
+    __shared__ uint64_t s_sum[CC_THREADS];
+    const int t = threadIdx.x;
+    const int per = (n_jobs + CC_THREADS - 1) / CC_THREADS;
+    const int a = min(n_jobs, t * per), b = min(n_jobs, a + per);
+    uint64_t mine = 0;
+    for (int i = a; i < b; ++i) mine += alns[i].cigar_len;
+    s_sum[t] = mine;
+    __syncthreads();
+    for (int o = 1; o < CC_THREADS; o <<= 1) {       // inclusive Hillis-Steele scan
+        const uint64_t v = t >= o ? s_sum[t - o] : 0;
+        __syncthreads();
+        s_sum[t] += v;
+        __syncthreads();
+    }
+    uint64_t off = s_sum[t] - mine;
+    for (int i = a; i < b; ++i) {
+        const uint32_t n = alns[i].cigar_len;
+        const uint32_t* src = slots + alns[i].cigar_offset;
+        for (uint32_t k = 0; k < n; ++k) dense[off + k] = src[k];
+        alns[i].cigar_offset = off;
+        off += n;
+    }
+    if (t == CC_THREADS - 1) *total = s_sum[t];
 }

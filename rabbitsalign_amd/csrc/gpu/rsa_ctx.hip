@@ -27,7 +27,11 @@ __global__ void k_ext_band(const ExtJobDev* jobs, const ScanRes* scan, int n_job
                            int gE, int bonus, int* overflow, int over_code);
 __global__ void k_ext_band16(const ExtJobDev* jobs, const ScanRes* scan, int n_jobs, const char* qbuf, const char* ref,
                              uint32_t* cig_pool, uint32_t* raw_pool, rsa_aln* out, int match, int mismatch, int gO,
-                             int gE, int bonus, int* defer);
+                             int gE, int bonus, int* queue, int* qcount);
+__global__ void k_ext_band64(const ExtJobDev* jobs, const ScanRes* scan, const char* qbuf, const char* ref,
+                             uint32_t* cig_pool, uint32_t* raw_pool, rsa_aln* out, int match, int mismatch, int gO,
+                             int gE, int bonus, const int* queue, const int* qcount, int* overflow, int* ocount);
+__global__ void k_cigar_compact(rsa_aln* alns, int n_jobs, const uint32_t* slots, uint32_t* dense, uint64_t* total);
 
 int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, const rsa_read_batch* rb,
              int32_t rescue_level, uint32_t rescue_cutoff, rsa_nam_batch* out, std::string& err, SeedCounters& c);
@@ -82,8 +86,8 @@ struct Lane {
     KTimer kt;
     bool busy = false;
     // extension
-    DevBuf d_q, d_jobs, d_scan, d_alns, d_cig, d_raw, d_scratch, d_over, d_defer, d_idx;
-    HostBuf h_q, h_jobs, h_over;
+    DevBuf d_q, d_jobs, d_scan, d_alns, d_alns2, d_cig, d_dense, d_raw, d_scratch, d_over, d_queue, d_idx, d_status;
+    HostBuf h_jobs, h_over, h_status;
     // seeding
     SeedBufs sb;
 };
@@ -197,9 +201,10 @@ void rsa_close(rsa_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     for (Lane* l : ctx->lanes) {
         if (l->stream) (void)hipStreamSynchronize(l->stream);
-        l->d_q.release(); l->d_jobs.release(); l->d_scan.release(); l->d_alns.release(); l->d_cig.release();
-        l->d_scratch.release(); l->d_over.release(); l->d_idx.release();
-        l->h_q.release(); l->h_jobs.release(); l->h_over.release();
+        for (DevBuf* b : {&l->d_q, &l->d_jobs, &l->d_scan, &l->d_alns, &l->d_alns2, &l->d_cig, &l->d_dense, &l->d_raw,
+                          &l->d_scratch, &l->d_over, &l->d_queue, &l->d_idx, &l->d_status})
+            b->release();
+        l->h_jobs.release(); l->h_over.release(); l->h_status.release();
         seed_bufs_release(l->sb);
         l->kt.destroy();
         if (l->stream) (void)hipStreamDestroy(l->stream);
@@ -221,24 +226,29 @@ uint64_t rsa_extend_cigar_bound(const rsa_job_batch* jb) {
     return t;
 }
 
-// band kernel scratch geometry (per in-flight job)
-static const int BAND_ARR_CAP = 1024;
-static const int64_t BAND_DIR_CAP = 48 * 1024;
-static const int BAND_CHUNK = 16384;
+// band kernel scratch geometry of the one-lane fallback (per in-flight job)
 static const int BIG_ARR_CAP = 1 << 16;
 static const int64_t BIG_DIR_CAP = 64ll << 20;
 static const int BIG_CHUNK = 8;
+static const int BAND64_GRID = 512;        // waves draining the band16 deferral queue
+static const uint64_t DENSE_GUESS = 24;    // CIGAR ops per job copied before the total is known
 
 static int64_t band_stride(int arr_cap, int64_t dir_cap) {
     int64_t s = (int64_t)arr_cap * 3 * 4 + dir_cap + (int64_t)RSA_RAW_CAP * 4;
     return (s + 255) & ~(int64_t)255;
 }
 
+struct ExtStatus {            // device-side counters of one rsa_extend call
+    int qcount;               // jobs deferred by k_ext_band16
+    int ocount;               // jobs k_ext_band64 could not hold
+    uint64_t total;           // dense CIGAR ops (k_cigar_compact)
+};
+
 int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
     if (!ctx || !jb || !out) return RSA_ERR_ARG;
     const uint32_t n = jb->n_jobs;
     const uint64_t bound = rsa_extend_cigar_bound(jb);
-    out->cigar_used = bound;
+    out->cigar_used = 0;
     if (n == 0) return RSA_OK;
     if (out->cigar_capacity < bound) { set_err(ctx, "rsa_extend: cigar_pool too small"); return RSA_ERR_CAPACITY; }
     HIPCHK(hipSetDevice(ctx->device));
@@ -249,7 +259,7 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
     HIPCHK(L->h_jobs.ensure(sizeof(ExtJobDev) * n));
     ExtJobDev* hj = L->h_jobs.as<ExtJobDev>();
     uint64_t cig_off = 0;
-    uint64_t cells = 0;
+    uint64_t cells = 0, qr_bytes = 0;
     for (uint32_t i = 0; i < n; ++i) {
         const rsa_job& s = jb->jobs[i];
         if (s.ref_id < 0 || s.ref_id >= (int)ctx->contig_off.size() - 1 || s.query_offset + s.query_len > jb->queries_len) {
@@ -271,22 +281,26 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
         hj[i].rlen = s.ref_len;
         hj[i].cig_off = cig_off;
         cig_off += (uint64_t)s.query_len + s.ref_len + 8;
+        qr_bytes += (uint64_t)s.query_len + s.ref_len;
         if (s.ref_len <= 2000) cells += (uint64_t)s.query_len * s.ref_len;
     }
     HIPCHK(L->d_q.ensure(jb->queries_len + 16));
     HIPCHK(L->d_jobs.ensure(sizeof(ExtJobDev) * n));
     HIPCHK(L->d_scan.ensure(sizeof(ScanRes) * n));
     HIPCHK(L->d_alns.ensure(sizeof(rsa_aln) * n));
+    HIPCHK(L->d_alns2.ensure(sizeof(rsa_aln) * n));
     HIPCHK(L->d_cig.ensure(sizeof(uint32_t) * (bound + 16)));
+    HIPCHK(L->d_dense.ensure(sizeof(uint32_t) * (bound + 16)));
     HIPCHK(L->d_raw.ensure(sizeof(uint32_t) * (bound + 16)));
     HIPCHK(L->d_over.ensure(sizeof(int) * n));
-    HIPCHK(L->d_defer.ensure(sizeof(int) * n));
-    const int64_t stride = band_stride(BAND_ARR_CAP, BAND_DIR_CAP);
+    HIPCHK(L->d_queue.ensure(sizeof(int) * n));
+    HIPCHK(L->d_status.ensure(sizeof(ExtStatus)));
+    HIPCHK(L->h_status.ensure(sizeof(ExtStatus)));
     hipStream_t st = L->stream;
+    ExtStatus* dst = L->d_status.as<ExtStatus>();
     HIPCHK(hipMemcpyAsync(L->d_q.p, jb->queries, jb->queries_len, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(L->d_jobs.p, hj, sizeof(ExtJobDev) * n, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemsetAsync(L->d_over.p, 0, sizeof(int) * n, st));
-    HIPCHK(hipMemsetAsync(L->d_defer.p, 0, sizeof(int) * n, st));
+    HIPCHK(hipMemsetAsync(L->d_status.p, 0, sizeof(ExtStatus), st));
     L->kt.reset();
     L->kt.begin(st, RSA_K_EXT_SCAN);
     hipLaunchKernelGGL(k_ext_scan, dim3((n + 3) / 4), dim3(256), 0, st, L->d_jobs.as<ExtJobDev>(), (int)n,
@@ -294,48 +308,50 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
                        jb->gap_open, jb->gap_extend);
     HIPCHK(hipGetLastError());
     L->kt.end(st);
-    // 16 lanes per job for the common narrow bands
+    // 16 lanes per job for the common narrow bands; the rest queue for 64-lane waves
     L->kt.begin(st, RSA_K_EXT_BAND);
     hipLaunchKernelGGL(k_ext_band16, dim3((n + 3) / 4), dim3(64), 0, st, L->d_jobs.as<ExtJobDev>(),
                        L->d_scan.as<ScanRes>(), (int)n, L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(),
                        L->d_raw.as<uint32_t>(), L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open,
-                       jb->gap_extend, jb->end_bonus, L->d_defer.as<int>());
+                       jb->gap_extend, jb->end_bonus, L->d_queue.as<int>(), &dst->qcount);
     HIPCHK(hipGetLastError());
     L->kt.end(st);
-    HIPCHK(L->h_over.ensure(sizeof(int) * n));
-    HIPCHK(hipMemcpyAsync(L->h_over.p, L->d_defer.p, sizeof(int) * n, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    // deferred jobs (wide bands, sentinels, long segments): one lane per job
-    std::vector<int> dlist;
-    for (uint32_t i = 0; i < n; ++i) if (L->h_over.as<int>()[i]) dlist.push_back((int)i);
-    if (!dlist.empty()) {
-        const int chunk = (int)std::min<size_t>(dlist.size(), BAND_CHUNK);
-        HIPCHK(L->d_scratch.ensure((size_t)stride * chunk));
-        HIPCHK(L->d_idx.ensure(sizeof(int) * dlist.size()));
-        HIPCHK(hipMemcpyAsync(L->d_idx.p, dlist.data(), sizeof(int) * dlist.size(), hipMemcpyHostToDevice, st));
-        for (size_t base = 0; base < dlist.size(); base += chunk) {
-            const int cnt = (int)std::min<size_t>(chunk, dlist.size() - base);
-            L->kt.begin(st, RSA_K_EXT_BAND_LANE);
-            hipLaunchKernelGGL(k_ext_band, dim3((cnt + 63) / 64), dim3(64), 0, st, L->d_jobs.as<ExtJobDev>(),
-                               L->d_scan.as<ScanRes>(), cnt, L->d_idx.as<int>() + base, 0, L->d_q.as<char>(),
-                               ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_alns.as<rsa_aln>(),
-                               L->d_scratch.as<uint8_t>(), stride, BAND_ARR_CAP, BAND_DIR_CAP, jb->match,
-                               jb->mismatch, jb->gap_open, jb->gap_extend, jb->end_bonus, L->d_over.as<int>(), 1);
-            HIPCHK(hipGetLastError());
-            L->kt.end(st);
-        }
-    }
-    HIPCHK(hipMemcpyAsync(L->h_over.p, L->d_over.p, sizeof(int) * n, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    // rare: jobs whose band doubled past the per-job scratch get a large scratch
-    std::vector<int> big;
-    const int* ho = L->h_over.as<int>();
-    for (uint32_t i = 0; i < n; ++i) if (ho[i]) big.push_back((int)i);
-    if (!big.empty()) {
+    L->kt.begin(st, RSA_K_EXT_BAND_WIDE);
+    hipLaunchKernelGGL(k_ext_band64, dim3(std::min<uint32_t>(n, BAND64_GRID)), dim3(64), 0, st,
+                       L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(), L->d_q.as<char>(), ctx->d_ref,
+                       L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(), L->d_alns.as<rsa_aln>(), jb->match,
+                       jb->mismatch, jb->gap_open, jb->gap_extend, jb->end_bonus, L->d_queue.as<int>(),
+                       &dst->qcount, L->d_over.as<int>(), &dst->ocount);
+    HIPCHK(hipGetLastError());
+    L->kt.end(st);
+    auto compact_and_copy = [&](uint64_t guess) -> int {
+        hipLaunchKernelGGL(k_cigar_compact, dim3(1), dim3(1024), 0, st, L->d_alns.as<rsa_aln>(), (int)n,
+                           L->d_cig.as<uint32_t>(), L->d_dense.as<uint32_t>(), &dst->total);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(L->h_status.p, L->d_status.p, sizeof(ExtStatus), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(out->alns, L->d_alns.p, sizeof(rsa_aln) * n, hipMemcpyDeviceToHost, st));
+        if (guess) HIPCHK(hipMemcpyAsync(out->cigar_pool, L->d_dense.p, sizeof(uint32_t) * guess, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        return RSA_OK;
+    };
+    // k_cigar_compact rewrites cigar_offset in place: keep the slot offsets for a possible re-run
+    HIPCHK(hipMemcpyAsync(L->d_alns2.p, L->d_alns.p, sizeof(rsa_aln) * n, hipMemcpyDeviceToDevice, st));
+    const uint64_t guess = std::min<uint64_t>(bound, DENSE_GUESS * n);
+    if (int rc = compact_and_copy(guess)) return rc;
+    ExtStatus hs = *L->h_status.as<ExtStatus>();
+    if (hs.ocount > 0) {
+        // rare: bands the 64-lane kernel cannot hold -> one lane per job, large global scratch
+        HIPCHK(L->h_over.ensure(sizeof(int) * n));
+        HIPCHK(hipMemcpyAsync(L->h_over.p, L->d_over.p, sizeof(int) * n, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        std::vector<int> big;
+        for (uint32_t i = 0; i < n; ++i) if (L->h_over.as<int>()[i]) big.push_back((int)i);
         const int64_t bstride = band_stride(BIG_ARR_CAP, BIG_DIR_CAP);
         HIPCHK(L->d_scratch.ensure((size_t)bstride * BIG_CHUNK));
         HIPCHK(L->d_idx.ensure(sizeof(int) * big.size()));
         HIPCHK(hipMemcpyAsync(L->d_idx.p, big.data(), sizeof(int) * big.size(), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemsetAsync(L->d_over.p, 0, sizeof(int) * n, st));
+        HIPCHK(hipMemcpyAsync(L->d_alns.p, L->d_alns2.p, sizeof(rsa_aln) * n, hipMemcpyDeviceToDevice, st));
         for (size_t b = 0; b < big.size(); b += BIG_CHUNK) {
             const int cnt = (int)std::min<size_t>(BIG_CHUNK, big.size() - b);
             L->kt.begin(st, RSA_K_EXT_BAND_LANE);
@@ -351,27 +367,39 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
         HIPCHK(hipStreamSynchronize(st));
         for (int i : big)
             if (L->h_over.as<int>()[i] > 1) { set_err(ctx, "rsa_extend: band scratch exhausted"); return RSA_ERR_NOMEM; }
+        if (int rc = compact_and_copy(guess)) return rc;
+        hs = *L->h_status.as<ExtStatus>();
     }
-    HIPCHK(hipMemcpyAsync(out->alns, L->d_alns.p, sizeof(rsa_aln) * n, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(out->cigar_pool, L->d_cig.p, sizeof(uint32_t) * bound, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    uint64_t qr_bytes = 0, cig_ops = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        qr_bytes += (uint64_t)hj[i].qlen + hj[i].rlen;
-        cig_ops += out->alns[i].cigar_len;
+    if (hs.total > guess) {
+        HIPCHK(hipMemcpyAsync(out->cigar_pool + guess, L->d_dense.as<uint32_t>() + guess,
+                              sizeof(uint32_t) * (hs.total - guess), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
     }
+    out->cigar_used = hs.total;
     {
         std::lock_guard<std::mutex> g(ctx->stat_m);
         L->kt.collect(ctx->stats.kernel_ms, ctx->stats.launches);
-        // scan: query + window in, ScanRes out; band: the same bytes again, ScanRes in, rsa_aln + CIGAR out
+        // scan: query + window in, ScanRes out; band: the segment bytes again, ScanRes in, rsa_aln + CIGAR out
         ctx->stats.alg_bytes[RSA_K_EXT_SCAN] += (double)qr_bytes + (double)(sizeof(ExtJobDev) + sizeof(ScanRes)) * n;
         ctx->stats.alg_bytes[RSA_K_EXT_BAND] += (double)qr_bytes + (double)(sizeof(ExtJobDev) + sizeof(ScanRes) +
-                                                                            sizeof(rsa_aln)) * n + 4.0 * cig_ops;
+                                                                            sizeof(rsa_aln)) * n + 4.0 * hs.total;
         ctx->stats.ext_calls++;
         ctx->stats.jobs += n;
         ctx->stats.dp_cells += cells;
+        ctx->stats.band_deferred += (uint64_t)hs.qcount;
+        ctx->stats.band_overflow += (uint64_t)hs.ocount;
     }
     return RSA_OK;
+}
+
+void* rsa_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+
+void rsa_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
 }
 
 static int check_reads(rsa_ctx* ctx, const rsa_read_batch* rb) {

@@ -1,15 +1,38 @@
 // engine_gpu.cpp -- the product engine: every hot-path call goes through the
 // HIP C-ABI (include/rsa_gpu.h, librsa_gpu.so).  There is no CPU fallback;
 // a failed GPU call aborts the run with the library's error message.
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "rsa_host.hpp"
 
 namespace rsa {
 
 namespace {
+
+// Per-thread page-locked batch buffers (rsa_host_alloc), grown on demand and
+// reused across chunks, so batch transfers run at DMA speed without staging.
+struct Staging {
+    enum { READS, ROFF, RLEN, NAMS, QUERIES, JOBS, ALNS, POOL, N };
+    void* p[N] = {};
+    size_t cap[N] = {};
+    template <class T> T* get(int k, size_t count) {
+        const size_t bytes = std::max<size_t>(64, count * sizeof(T));
+        if (bytes > cap[k]) {
+            rsa_host_free(p[k]);
+            const size_t nb = std::max(bytes, cap[k] + cap[k] / 2);
+            p[k] = rsa_host_alloc(nb);
+            if (!p[k]) { cap[k] = 0; throw std::runtime_error("rsa_host_alloc failed"); }
+            cap[k] = nb;
+        }
+        return (T*)p[k];
+    }
+    ~Staging() { for (void* x : p) rsa_host_free(x); }
+};
 
 class GpuEngine final : public Engine {
 public:
@@ -30,31 +53,42 @@ public:
         ctx_ = rsa_open(device, &v, err, sizeof err);
         if (!ctx_) throw std::runtime_error(std::string("GPU engine: ") + err);
     }
-    ~GpuEngine() override { rsa_close(ctx_); }
+    ~GpuEngine() override {
+        free_.clear();
+        staging_.clear();                  // pinned buffers go before the context
+        rsa_close(ctx_);
+    }
     const char* name() const override { return "hip-gfx950"; }
 
     void seed(const std::vector<const std::string*>& reads, int rescue_level, unsigned rescue_cutoff,
               SeedBatchOut& out) override {
         const size_t n = reads.size();
-        std::string blob;
+        const Lease ls = lease();
+        Staging& sg = *ls.s;
         size_t tot = 0;
         for (auto* r : reads) tot += r->size();
-        blob.reserve(tot);
-        std::vector<uint64_t> offs(n);
-        std::vector<uint32_t> lens(n);
-        for (size_t i = 0; i < n; ++i) { offs[i] = blob.size(); lens[i] = (uint32_t)reads[i]->size(); blob += *reads[i]; }
-        rsa_read_batch rb{blob.data(), offs.data(), lens.data(), (uint32_t)n};
+        char* blob = sg.get<char>(Staging::READS, tot + 16);
+        uint64_t* offs = sg.get<uint64_t>(Staging::ROFF, n);
+        uint32_t* lens = sg.get<uint32_t>(Staging::RLEN, n);
+        size_t pos = 0;
+        for (size_t i = 0; i < n; ++i) {
+            offs[i] = pos;
+            lens[i] = (uint32_t)reads[i]->size();
+            memcpy(blob + pos, reads[i]->data(), reads[i]->size());
+            pos += reads[i]->size();
+        }
+        rsa_read_batch rb{blob, offs, lens, (uint32_t)n};
         out.offsets.assign(n + 1, 0);
         out.nonrep.assign(n, 0.f);
         out.rescued.assign(n, 0);
-        size_t cap = std::max<size_t>(1024, 16 * n);
+        size_t cap = std::max<size_t>(1024, 12 * n);
         for (;;) {
-            out.nams.resize(cap);
-            rsa_nam_batch nb{out.nams.data(), cap, out.offsets.data(), out.nonrep.data(), out.rescued.data(), 0};
+            rsa_nam* nams = sg.get<rsa_nam>(Staging::NAMS, cap);
+            rsa_nam_batch nb{nams, cap, out.offsets.data(), out.nonrep.data(), out.rescued.data(), 0};
             int rc = rsa_seed(ctx_, &rb, rescue_level, rescue_cutoff, &nb);
             if (rc == RSA_ERR_CAPACITY) { cap = nb.needed + 16; continue; }
             if (rc != RSA_OK) throw std::runtime_error(std::string("rsa_seed: ") + rsa_last_error(ctx_));
-            out.nams.resize(nb.needed);
+            out.nams.assign(nams, nams + nb.needed);
             break;
         }
     }
@@ -64,22 +98,27 @@ public:
         const size_t n = jobs.size();
         out.assign(n, AlignmentInfo());
         if (n == 0) return;
-        std::string q;
-        std::vector<rsa_job> js(n);
+        const Lease ls = lease();
+        Staging& sg = *ls.s;
+        size_t qtot = 0;
+        for (const auto& j : jobs) qtot += j.query.size();
+        char* q = sg.get<char>(Staging::QUERIES, qtot + 16);
+        rsa_job* js = sg.get<rsa_job>(Staging::JOBS, n);
+        size_t pos = 0;
         for (size_t i = 0; i < n; ++i) {
-            js[i].query_offset = q.size();
+            js[i].query_offset = pos;
             js[i].query_len = (uint32_t)jobs[i].query.size();
             js[i].ref_id = jobs[i].ref_id;
             js[i].ref_start = jobs[i].ref_start;
             js[i].ref_len = jobs[i].ref_len;
-            q += jobs[i].query;
+            memcpy(q + pos, jobs[i].query.data(), jobs[i].query.size());
+            pos += jobs[i].query.size();
         }
-        rsa_job_batch jb{q.data(), q.size(), js.data(), (uint32_t)n, p.match, p.mismatch, p.gap_open,
-                         p.gap_extend, p.end_bonus};
-        const uint64_t bound = rsa_extend_cigar_bound(&jb);
-        std::vector<rsa_aln> alns(n);
-        std::vector<uint32_t> pool(bound + 1);
-        rsa_aln_batch ab{alns.data(), pool.data(), bound + 1, 0};
+        rsa_job_batch jb{q, qtot, js, (uint32_t)n, p.match, p.mismatch, p.gap_open, p.gap_extend, p.end_bonus};
+        const uint64_t bound = rsa_extend_cigar_bound(&jb) + 1;
+        rsa_aln* alns = sg.get<rsa_aln>(Staging::ALNS, n);
+        uint32_t* pool = sg.get<uint32_t>(Staging::POOL, bound);
+        rsa_aln_batch ab{alns, pool, bound, 0};
         int rc = rsa_extend(ctx_, &jb, &ab);
         if (rc != RSA_OK) throw std::runtime_error(std::string("rsa_extend: ") + rsa_last_error(ctx_));
         for (size_t i = 0; i < n; ++i) {
@@ -89,7 +128,7 @@ public:
             o.edit_distance = a.edit_distance;
             o.ref_start = a.ref_start; o.ref_end = a.ref_end;
             o.query_start = a.query_start; o.query_end = a.query_end;
-            o.cigar.ops.assign(pool.begin() + (long)a.cigar_offset, pool.begin() + (long)(a.cigar_offset + a.cigar_len));
+            o.cigar.ops.assign(pool + a.cigar_offset, pool + a.cigar_offset + a.cigar_len);
         }
     }
 
@@ -97,7 +136,28 @@ public:
     void reset_kernel_stats() override { rsa_reset_stats(ctx_); }
 
 private:
+    // staging sets are checked out per call (at most one per concurrent caller)
+    struct Lease {
+        GpuEngine* e;
+        Staging* s;
+        Lease(GpuEngine* e_, Staging* s_) : e(e_), s(s_) {}
+        Lease(const Lease&) = delete;
+        ~Lease() { std::lock_guard<std::mutex> g(e->staging_m_); e->free_.push_back(s); }
+    };
+    Lease lease() {
+        std::lock_guard<std::mutex> g(staging_m_);
+        if (free_.empty()) {
+            staging_.emplace_back(new Staging());
+            return Lease{this, staging_.back().get()};
+        }
+        Staging* s = free_.back();
+        free_.pop_back();
+        return Lease{this, s};
+    }
     rsa_ctx* ctx_ = nullptr;
+    std::mutex staging_m_;
+    std::vector<std::unique_ptr<Staging>> staging_;
+    std::vector<Staging*> free_;
 };
 
 }  // namespace

@@ -76,10 +76,11 @@ class AlnBatch(C.Structure):
                 ("cigar_used", C.c_uint64)]
 
 
-KERNELS = ["randstrobes", "lookup", "find_nams", "rescue", "compact", "ext_scan", "ext_band", "ext_band_lane"]
+KERNELS = ["randstrobes", "lookup", "find_nams", "rescue", "compact", "ext_scan", "ext_band", "ext_band_wide",
+           "ext_band_lane"]
 KERNEL_SYMBOLS = {"randstrobes": "k_randstrobes", "lookup": "k_lookup", "find_nams": "k_find_nams",
                   "rescue": "k_rescue", "compact": "k_compact", "ext_scan": "k_ext_scan", "ext_band": "k_ext_band16",
-                  "ext_band_lane": "k_ext_band"}
+                  "ext_band_wide": "k_ext_band64", "ext_band_lane": "k_ext_band"}
 NK = len(KERNELS)
 
 
@@ -89,7 +90,8 @@ class KernelStats(C.Structure):
                 ("reads", C.c_uint64), ("read_bases", C.c_uint64), ("query_randstrobes", C.c_uint64),
                 ("lookups_found", C.c_uint64), ("filtered", C.c_uint64), ("hits", C.c_uint64),
                 ("nams", C.c_uint64), ("rescued_reads", C.c_uint64),
-                ("jobs", C.c_uint64), ("dp_cells", C.c_uint64)]
+                ("jobs", C.c_uint64), ("dp_cells", C.c_uint64),
+                ("band_deferred", C.c_uint64), ("band_overflow", C.c_uint64)]
 
 
 def stats_dict(ks: "KernelStats") -> dict:
@@ -102,7 +104,8 @@ def stats_dict(ks: "KernelStats") -> dict:
 
 
 EXPORTED_SYMBOLS = ["rsa_open", "rsa_close", "rsa_last_error", "rsa_resident_bytes", "rsa_randstrobes",
-                    "rsa_seed", "rsa_extend", "rsa_extend_cigar_bound", "rsa_get_stats", "rsa_reset_stats"]
+                    "rsa_seed", "rsa_extend", "rsa_extend_cigar_bound", "rsa_host_alloc", "rsa_host_free",
+                    "rsa_get_stats", "rsa_reset_stats"]
 
 _lib = None
 

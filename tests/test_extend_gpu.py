@@ -63,3 +63,19 @@ def test_extend_order_independent(ctx):
         assert x["sw_score"] == y["sw_score"] and x["ref_start"] == y["ref_start"]
         assert list(p1[x["cigar_offset"]:x["cigar_offset"] + x["cigar_len"]]) == \
             list(p2[y["cigar_offset"]:y["cigar_offset"] + y["cigar_len"]])
+
+
+@pytest.mark.gpu
+def test_extend_band_paths_exercised(ctx):
+    """Jobs whose bands the 16-lane kernel cannot hold go through the 64-lane
+    queue kernel, and bands wider than 64 cells through the one-lane kernel;
+    all three must agree with the oracle."""
+    c, ref, offs = ctx
+    c.reset_stats()
+    bad = _compare(c, ref, offs, 5, 3000, qlens=(150, 250, 400))
+    assert not bad, f"{len(bad)} mismatches, first: {bad[0]}"
+    st = c.stats()
+    assert st["band_deferred"] > 0, st
+    assert st["band_overflow"] > 0, st
+    k = st["kernels"]
+    assert k["ext_band_wide"]["launches"] > 0 and k["ext_band_lane"]["launches"] > 0
