@@ -32,6 +32,7 @@
 #include "rsa_timer.h"
 
 #define END64 0xFFFFFFFFFFFFFFFFULL
+#define WSYNC_SEED() do { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); } while (0)
 
 struct QrsInfo {            // per query randstrobe, filled by k_lookup
     uint64_t pos;           // first index with equal hash, END64 if absent
@@ -161,6 +162,150 @@ k_randstrobes(const char* __restrict__ seq, const uint64_t* __restrict__ roff, c
 }
 
 // ---------------------------------------------------------------------------
+// k_randstrobes_w: one wavefront per read.
+//   1. lanes: base codes and every canonical s-mer hash (xxh64) -> LDS
+//   2. lane 0: the reference's stateful window-minimum walk over those hashes
+//      (first fill leftmost, rescan rightmost, strictly smaller replaces,
+//      N resets; randstrobes.cpp:57-118) -> syncmer positions
+//   3. lanes: canonical k-mer hash of every syncmer, then one randstrobe per
+//      lane (strobe1 = lane), forward and reverse-complement (148-171, 207-253)
+// Reads longer than RS_MAXLEN use the one-lane kernel above.
+// ---------------------------------------------------------------------------
+#define RS_WAVES 4
+#define RS_MAXLEN 512
+#define RS_RING 32
+
+__device__ __forceinline__ void rs_pick(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sp, int n, int i,
+                                        bool rc, int len, const SeedIndexParams& p, uint64_t& h, uint32_t& a,
+                                        uint32_t& b) {
+    // syncmer x of the (possibly reversed) list: index n-1-x, position len - pos - k when reversed
+    auto pos = [&](int x) -> uint32_t { return rc ? (uint32_t)(len - (int)sp[n - 1 - x] - p.k) : sp[x]; };
+    auto hsh = [&](int x) -> uint64_t { return rc ? sh[n - 1 - x] : sh[x]; };
+    const int w_end = i + p.w_max < n - 1 ? i + p.w_max : n - 1;
+    const uint32_t pi = pos(i);
+    const uint64_t max_position = (uint64_t)pi + (unsigned)p.max_dist;
+    uint64_t min_val = END64;
+    int best = i;
+    const uint64_t hi = hsh(i);
+    for (int j = i + p.w_min; j <= w_end && pos(j) <= max_position; ++j) {
+        const uint64_t res = (uint64_t)__popcll((hi ^ hsh(j)) & p.q);
+        if (res < min_val) { min_val = res; best = j; }
+    }
+    h = hi + hsh(best);
+    a = pi;
+    b = pos(best);
+}
+
+__global__ void __launch_bounds__(64 * RS_WAVES)
+k_randstrobes_w(const char* __restrict__ seq, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
+                const uint64_t* __restrict__ qbase, int n_reads, SeedIndexParams p,
+                rsa_query_randstrobe* __restrict__ qrs, uint32_t* __restrict__ qcnt) {
+    __shared__ uint64_t s_hs[RS_WAVES][RS_MAXLEN];     // s-mer hash ending at i (valid: s_ok)
+    __shared__ uint64_t s_sh[RS_WAVES][RS_MAXLEN];     // syncmer k-mer hashes
+    __shared__ uint32_t s_sp[RS_WAVES][RS_MAXLEN];     // syncmer positions
+    __shared__ uint64_t s_ring[RS_WAVES][RS_RING];
+    __shared__ uint8_t s_c[RS_WAVES][RS_MAXLEN];
+    __shared__ int s_n[RS_WAVES];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = blockIdx.x * RS_WAVES + w;
+    if (r >= n_reads) return;                          // the whole wave leaves together
+    const int len = (int)rlen[r];
+    if (len < p.w_max) { if (lane == 0) qcnt[r] = 0; return; }   // randstrobes.cpp:209
+    const char* sq = seq + roff[r];
+    uint8_t* c = s_c[w];
+    uint64_t* hs = s_hs[w];
+    const int k = p.k, sl = p.s;
+    for (int i = lane; i < len; i += 64) c[i] = (uint8_t)nt4_code((unsigned char)sq[i]);
+    WSYNC_SEED();
+    // 1. canonical s-mer hashes (fwd = bases MSB first, rc = complements LSB first)
+    for (int i = sl - 1 + lane; i < len; i += 64) {
+        uint64_t f = 0, rv = 0;
+        bool ok = true;
+        for (int t = 0; t < sl; ++t) {
+            const int cc = c[i - sl + 1 + t];
+            ok &= cc < 4;
+            f = (f << 2) | (uint64_t)(cc & 3);
+            rv |= (uint64_t)(3 - (cc & 3)) << (2 * t);
+        }
+        hs[i] = ok ? xxh64_u64(f < rv ? f : rv) : 0;
+    }
+    WSYNC_SEED();
+    // 2. window-minimum walk (lane 0), SyncmerIterator::next
+    if (lane == 0) {
+        uint64_t* ring = s_ring[w];
+        uint32_t* sp = s_sp[w];
+        const int W = k - sl + 1;
+        int qn = 0, qhead = 0, l = 0, n = 0;
+        uint64_t min_val = END64;
+        long long min_pos = -1;
+        for (int i = 0; i < len; ++i) {
+            if (c[i] < 4) {
+                if (++l < sl) continue;
+                const uint64_t h = hs[i];
+                ring[(qhead + qn) & (RS_RING - 1)] = h;
+                qn++;
+                if (qn < W) continue;
+                if (qn == W) {
+                    for (int j = 0; j < qn; ++j) {
+                        const uint64_t v = ring[(qhead + j) & (RS_RING - 1)];
+                        if (v < min_val) { min_val = v; min_pos = (long long)i - k + j + 1; }
+                    }
+                } else {
+                    qhead = (qhead + 1) & (RS_RING - 1); qn--;
+                    if (min_pos == (long long)i - k) {
+                        min_val = END64;
+                        min_pos = (long long)i - sl + 1;
+                        for (int j = qn - 1; j >= 0; --j) {
+                            const uint64_t v = ring[(qhead + j) & (RS_RING - 1)];
+                            if (v < min_val) { min_val = v; min_pos = (long long)i - k + j + 1; }
+                        }
+                    } else if (h < min_val) {
+                        min_val = h;
+                        min_pos = (long long)i - sl + 1;
+                    }
+                }
+                if (min_pos == (long long)i - k + p.t) sp[n++] = (uint32_t)(i - k + 1);
+            } else {
+                min_val = END64; min_pos = -1;
+                l = 0; qn = 0; qhead = 0;
+            }
+        }
+        s_n[w] = n;
+    }
+    WSYNC_SEED();
+    const int n = s_n[w];
+    const uint32_t* sp = s_sp[w];
+    uint64_t* sh = s_sh[w];
+    // 3a. canonical k-mer hash of every syncmer
+    const uint64_t kmask = (k == 32) ? ~0ULL : ((1ULL << (2 * k)) - 1);
+    for (int x = lane; x < n; x += 64) {
+        const int p0 = (int)sp[x];
+        uint64_t f = 0, rv = 0;
+        for (int t = 0; t < k; ++t) {
+            const int cc = c[p0 + t] & 3;
+            f = (f << 2) | (uint64_t)cc;
+            rv |= (uint64_t)(3 - cc) << (2 * t);
+        }
+        f &= kmask;
+        sh[x] = xxh64_u64(f < rv ? f : rv);
+    }
+    WSYNC_SEED();
+    // 3b. randstrobes, forward then reverse complement
+    const int m = n > p.w_min ? n - p.w_min : 0;
+    rsa_query_randstrobe* out = qrs + qbase[r];
+    for (int x = lane; x < 2 * m; x += 64) {
+        const bool rcx = x >= m;
+        const int i = rcx ? x - m : x;
+        uint64_t h; uint32_t a, b;
+        rs_pick(sh, sp, n, i, rcx, len, p, h, a, b);
+        rsa_query_randstrobe o;
+        o.hash = h; o.start = a; o.end = b + (uint32_t)k; o.is_reverse = rcx ? 1 : 0; o.pad_ = 0;
+        out[x] = o;
+    }
+    if (lane == 0) qcnt[r] = (uint32_t)(2 * m);
+}
+
+// ---------------------------------------------------------------------------
 // k_lookup: one wavefront per read
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t lower_bound_hash(const rsa_ref_randstrobe* rs, uint64_t lo, uint64_t hi,
@@ -264,12 +409,13 @@ __device__ __forceinline__ uint32_t rh_calc_nwb(uint32_t n) { uint32_t m = rh_ca
 
 __device__ bool rh_init_data(DMap& m, uint32_t max_elements) {
     const uint32_t nwb = rh_calc_nwb(max_elements);
-    if (nwb + 16 > m.cap) { m.overflow = 1; return false; }
+    const uint32_t span = (nwb + 16 + 3) & ~3u;      // info bytes zeroed as words
+    if (span > m.cap) { m.overflow = 1; return false; }
     m.num = 0;
     m.mask = max_elements - 1;
     m.max_allowed = rh_calc_max(max_elements);
     m.nwb = nwb;
-    for (uint32_t i = 0; i < nwb + 16; ++i) m.info[i] = 0;
+    for (uint32_t i = 0; i < span; i += 4) *(uint32_t*)(m.info + i) = 0;
     m.info[nwb] = 1;
     m.info_inc = 32;
     m.info_shift = 0;
@@ -439,11 +585,20 @@ __device__ void add_hits(DMap& m, int orient, int qs, int qe, const SeedIndexPar
     }
 }
 
+// next occupied slot >= slot (slot order = robin_hood iteration order), nwb if none
+__device__ __forceinline__ uint32_t rh_next_slot(const DMap& m, uint32_t slot) {
+    while (slot < m.nwb) {
+        if ((slot & 3) == 0 && *(const uint32_t*)(m.info + slot) == 0) { slot += 4; continue; }
+        if (m.info[slot]) return slot;
+        ++slot;
+    }
+    return m.nwb;
+}
+
 // merge_hits_into_nams (nam.cpp:370-536, sort=true), all lists of one orientation
 __device__ void merge_slow(const DMap& m, int orient, const HitD* hits, int n_hits, int k, rsa_nam* open,
                            rsa_nam* out, int& n_out) {
-    for (uint32_t slot = 0; slot < m.nwb; ++slot) {
-        if (!m.info[slot]) continue;
+    for (uint32_t slot = rh_next_slot(m, 0); slot < m.nwb; slot = rh_next_slot(m, slot + 1)) {
         const int32_t lid = m.vals[slot] | (orient << 30);
         const int ref_id = (int)m.keys[slot];
         int n_open = 0;
@@ -479,8 +634,7 @@ __device__ void merge_slow(const DMap& m, int orient, const HitD* hits, int n_hi
 // merge_hits_into_nams_fast (nam.cpp:117-366, sort=false)
 __device__ void merge_fast(const DMap& m, int orient, HitD* hits, int n_hits, int k, rsa_nam* open, uint8_t* added,
                            HitD* grp, rsa_nam* out, int& n_out) {
-    for (uint32_t slot = 0; slot < m.nwb; ++slot) {
-        if (!m.info[slot]) continue;
+    for (uint32_t slot = rh_next_slot(m, 0); slot < m.nwb; slot = rh_next_slot(m, slot + 1)) {
         const int32_t lid = m.vals[slot] | (orient << 30);
         const int ref_id = (int)m.keys[slot];
         int n_open = 0;
@@ -541,24 +695,21 @@ __device__ void merge_fast(const DMap& m, int orient, HitD* hits, int n_hits, in
 }
 
 // ---------------------------------------------------------------------------
-// k_find_nams: one lane per read
+// find_nams of one read (nam.cpp:771-926) given k_lookup's per-randstrobe
+// results.  `ms` holds the read's two robin_hood maps (map_stride(map_cap)).
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(64)
-k_find_nams(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi, const uint32_t* __restrict__ qcnt,
-            const uint64_t* __restrict__ qbase, const ReadStat* __restrict__ st, const uint64_t* __restrict__ hoff,
-            int n_reads, const int* __restrict__ list, SeedIndexParams p, HitD* __restrict__ hits_buf,
-            rsa_nam* __restrict__ open_buf, rsa_nam* __restrict__ nam_buf, uint8_t* __restrict__ map_scratch,
-            uint32_t map_cap, uint32_t* __restrict__ ncnt, float* __restrict__ nonrep, uint32_t* __restrict__ flags) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n_reads) return;
-    const int r = list ? list[t] : t;
+__device__ void find_nams_read(int r, const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi,
+                               const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase,
+                               const ReadStat* __restrict__ st, const uint64_t* __restrict__ hoff,
+                               const SeedIndexParams& p, HitD* __restrict__ hits_buf, rsa_nam* __restrict__ open_buf,
+                               rsa_nam* __restrict__ nam_buf, uint8_t* ms, uint32_t map_cap,
+                               uint32_t* __restrict__ ncnt, float* __restrict__ nonrep, uint32_t* __restrict__ flags) {
     const int nq = (int)qcnt[r];
     const uint64_t base = qbase[r];
     const ReadStat s = st[r];
     // nonrepetitive_fraction (nam.cpp:920)
     nonrep[r] = s.found > 0 ? (float)s.good / (float)s.found : 1.0f;
     DMap m[2];
-    uint8_t* ms = map_scratch + (size_t)t * map_stride(map_cap);
     map_bind(m[0], ms, map_cap, 0);
     map_bind(m[1], ms, map_cap, 1);
     rh_new_reserved(m[0]);
@@ -582,6 +733,41 @@ k_find_nams(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restr
     flags[r] = 0;
 }
 
+// one lane per read, maps in global scratch (the large-map pass for the rare
+// reads whose maps rehash past the LDS tables)
+__global__ void __launch_bounds__(64)
+k_find_nams(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi, const uint32_t* __restrict__ qcnt,
+            const uint64_t* __restrict__ qbase, const ReadStat* __restrict__ st, const uint64_t* __restrict__ hoff,
+            int n_reads, const int* __restrict__ list, SeedIndexParams p, HitD* __restrict__ hits_buf,
+            rsa_nam* __restrict__ open_buf, rsa_nam* __restrict__ nam_buf, uint8_t* __restrict__ map_scratch,
+            uint32_t map_cap, uint32_t* __restrict__ ncnt, float* __restrict__ nonrep, uint32_t* __restrict__ flags) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_reads) return;
+    const int r = list ? list[t] : t;
+    find_nams_read(r, qrs, qi, qcnt, qbase, st, hoff, p, hits_buf, open_buf, nam_buf,
+                   map_scratch + (size_t)t * map_stride(map_cap), map_cap, ncnt, nonrep, flags);
+}
+
+// one wavefront per read: the read's maps live in LDS (2 maps x 2 tables x
+// 256 slots), its sequential merge runs on lane 0.  A one-lane-per-read launch
+// of a 20000-read chunk fills 313 waves, i.e. a third of the SIMDs; one wave
+// per read fills the chip and turns every map access into an LDS access.
+#define FN_WAVES 4
+#define FN_MAP_CAP 256
+__global__ void __launch_bounds__(64 * FN_WAVES)
+k_find_nams_w(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi,
+              const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, const ReadStat* __restrict__ st,
+              const uint64_t* __restrict__ hoff, int n_reads, SeedIndexParams p, HitD* __restrict__ hits_buf,
+              rsa_nam* __restrict__ open_buf, rsa_nam* __restrict__ nam_buf, uint32_t* __restrict__ ncnt,
+              float* __restrict__ nonrep, uint32_t* __restrict__ flags) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_map[FN_WAVES][FN_MAP_CAP * 9 * 4];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = blockIdx.x * FN_WAVES + w;
+    if (r >= n_reads || lane != 0) return;
+    find_nams_read(r, qrs, qi, qcnt, qbase, st, hoff, p, hits_buf, open_buf, nam_buf, s_map[w], FN_MAP_CAP, ncnt,
+                   nonrep, flags);
+}
+
 // ---------------------------------------------------------------------------
 // k_rescue: find_nams_rescue for listed reads (one lane per read)
 // ---------------------------------------------------------------------------
@@ -593,16 +779,12 @@ __device__ __forceinline__ bool rcmp1(const RescueD& a, const RescueD& b) {   //
     return a.qe < b.qe;
 }
 
-__global__ void __launch_bounds__(64)
-k_rescue(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi, const uint32_t* __restrict__ qcnt,
-         const uint64_t* __restrict__ qbase, const uint64_t* __restrict__ roff, int n_list, const int* __restrict__ list,
-         SeedIndexParams p, uint32_t rescue_cutoff, RescueD* __restrict__ rbuf, HitD* __restrict__ hits_buf,
-         rsa_nam* __restrict__ open_buf, rsa_nam* __restrict__ nam_buf, HitD* __restrict__ grp_buf,
-         uint8_t* __restrict__ added_buf, uint8_t* __restrict__ map_scratch, uint32_t map_cap,
-         uint32_t* __restrict__ ncnt, uint32_t* __restrict__ flags) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n_list) return;
-    const int r = list[t];
+__device__ void rescue_read(int r, const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi,
+                            const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase,
+                            const uint64_t* __restrict__ roff, const SeedIndexParams& p, uint32_t rescue_cutoff,
+                            RescueD* __restrict__ rbuf, HitD* __restrict__ hits_buf, rsa_nam* __restrict__ open_buf,
+                            rsa_nam* __restrict__ nam_buf, HitD* __restrict__ grp_buf, uint8_t* __restrict__ added_buf,
+                            uint8_t* ms, uint32_t map_cap, uint32_t* __restrict__ ncnt, uint32_t* __restrict__ flags) {
     const int nq = (int)qcnt[r];
     const uint64_t base = qbase[r];
     RescueD* rv = rbuf + base;        // room for nq entries (both orientations)
@@ -626,7 +808,6 @@ k_rescue(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict
     }
     const int seg_a[2] = {0, nf}, seg_n[2] = {nf, nr - nf};
     DMap m[2];
-    uint8_t* ms = map_scratch + (size_t)t * map_stride(map_cap);
     map_bind(m[0], ms, map_cap, 0);
     map_bind(m[1], ms, map_cap, 1);
     rh_new_reserved(m[0]);
@@ -685,6 +866,36 @@ k_rescue(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict
     merge_fast(m[1], 1, hits, n_hits, p.k, open, added, grp, out, n_out);
     ncnt[r] = (uint32_t)n_out;
     flags[r] = (flags[r] & ~4u) | 8u;   // bit3: rescued result present
+}
+
+// one lane per listed read, maps in global scratch (large-map pass)
+__global__ void __launch_bounds__(64)
+k_rescue(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi, const uint32_t* __restrict__ qcnt,
+         const uint64_t* __restrict__ qbase, const uint64_t* __restrict__ roff, int n_list, const int* __restrict__ list,
+         SeedIndexParams p, uint32_t rescue_cutoff, RescueD* __restrict__ rbuf, HitD* __restrict__ hits_buf,
+         rsa_nam* __restrict__ open_buf, rsa_nam* __restrict__ nam_buf, HitD* __restrict__ grp_buf,
+         uint8_t* __restrict__ added_buf, uint8_t* __restrict__ map_scratch, uint32_t map_cap,
+         uint32_t* __restrict__ ncnt, uint32_t* __restrict__ flags) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_list) return;
+    rescue_read(list[t], qrs, qi, qcnt, qbase, roff, p, rescue_cutoff, rbuf, hits_buf, open_buf, nam_buf, grp_buf,
+                added_buf, map_scratch + (size_t)t * map_stride(map_cap), map_cap, ncnt, flags);
+}
+
+// one wavefront per listed read, maps in LDS, lane 0 (see k_find_nams_w)
+__global__ void __launch_bounds__(64 * FN_WAVES)
+k_rescue_w(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi,
+           const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, const uint64_t* __restrict__ roff,
+           int n_list, const int* __restrict__ list, SeedIndexParams p, uint32_t rescue_cutoff,
+           RescueD* __restrict__ rbuf, HitD* __restrict__ hits_buf, rsa_nam* __restrict__ open_buf,
+           rsa_nam* __restrict__ nam_buf, HitD* __restrict__ grp_buf, uint8_t* __restrict__ added_buf,
+           uint32_t* __restrict__ ncnt, uint32_t* __restrict__ flags) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_map[FN_WAVES][FN_MAP_CAP * 9 * 4];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int t = blockIdx.x * FN_WAVES + w;
+    if (t >= n_list || lane != 0) return;
+    rescue_read(list[t], qrs, qi, qcnt, qbase, roff, p, rescue_cutoff, rbuf, hits_buf, open_buf, nam_buf, grp_buf,
+                added_buf, s_map[w], FN_MAP_CAP, ncnt, flags);
 }
 
 // ---------------------------------------------------------------------------
@@ -748,7 +959,6 @@ static hipError_t hens(SeedBufs& b, int i, size_t bytes) {
 #define DP(i, T) ((T*)b.p[i])
 #define HP(i, T) ((T*)b.h[i])
 
-static const uint32_t MAP_SMALL = 256;
 static const uint32_t MAP_BIG = 65536 + 512;
 
 // Stage 1 (shared by rsa_randstrobes and rsa_seed): upload reads, run k_randstrobes.
@@ -772,10 +982,18 @@ int seed_stage_randstrobes(SeedBufs& b, hipStream_t st, const SeedIndexParams& p
     SCHK(hipMemcpyAsync(b.p[B_ROFF], rb->offsets, 8ull * n, hipMemcpyHostToDevice, st));
     SCHK(hipMemcpyAsync(b.p[B_RLEN], rb->lengths, 4ull * n, hipMemcpyHostToDevice, st));
     SCHK(hipMemcpyAsync(b.p[B_QBASE], qbase.data(), 8ull * (n + 1), hipMemcpyHostToDevice, st));
+    uint32_t max_len = 0;
+    for (uint32_t i = 0; i < n; ++i) max_len = std::max(max_len, rb->lengths[i]);
+    const bool wave = max_len <= RS_MAXLEN && p.k <= 32 && p.s <= 32 && p.k - p.s + 1 <= RS_RING;
     if (kt) kt->begin(st, RSA_K_RANDSTROBES);
-    hipLaunchKernelGGL(k_randstrobes, dim3((n + 63) / 64), dim3(64), 0, st, DP(B_SEQ, char), DP(B_ROFF, uint64_t),
-                       DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n, p, DP(B_SYNC, SyncD),
-                       DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
+    if (wave)
+        hipLaunchKernelGGL(k_randstrobes_w, dim3((n + RS_WAVES - 1) / RS_WAVES), dim3(64 * RS_WAVES), 0, st,
+                           DP(B_SEQ, char), DP(B_ROFF, uint64_t), DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n,
+                           p, DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
+    else
+        hipLaunchKernelGGL(k_randstrobes, dim3((n + 63) / 64), dim3(64), 0, st, DP(B_SEQ, char), DP(B_ROFF, uint64_t),
+                           DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n, p, DP(B_SYNC, SyncD),
+                           DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
     SCHK(hipGetLastError());
     if (kt) kt->end(st);
     return RSA_OK;
@@ -844,22 +1062,15 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
     SCHK(dens(b, B_NCNT1, 4ull * n));
     SCHK(dens(b, B_NONREP, 4ull * n));
     SCHK(dens(b, B_FLAGS, 4ull * n));
-    const size_t small_stride = (size_t)MAP_SMALL * 9 * 4;
     const uint32_t chunk = 65536;
-    SCHK(dens(b, B_MAP, small_stride * std::min<uint32_t>(n, chunk)));
     SCHK(hipMemcpyAsync(b.p[B_HOFF], hoff, 8ull * (n + 1), hipMemcpyHostToDevice, st));
-    for (uint32_t a = 0; a < n; a += chunk) {
-        const uint32_t cnt = std::min(chunk, n - a);
-        // reads [a, a+cnt) use map slots [0, cnt): pass a list-less launch by offsetting pointers
-        kt.begin(st, RSA_K_FIND_NAMS);
-        hipLaunchKernelGGL(k_find_nams, dim3((cnt + 63) / 64), dim3(64), 0, st, DP(B_QRS, rsa_query_randstrobe),
-                           DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t) + a, DP(B_QBASE, uint64_t) + a, DP(B_ST, ReadStat) + a,
-                           DP(B_HOFF, uint64_t) + a, (int)cnt, (const int*)nullptr, p, DP(B_HITS, HitD),
-                           DP(B_OPEN, rsa_nam), DP(B_NAM1, rsa_nam), DP(B_MAP, uint8_t), MAP_SMALL,
-                           DP(B_NCNT1, uint32_t) + a, DP(B_NONREP, float) + a, DP(B_FLAGS, uint32_t) + a);
-        SCHK(hipGetLastError());
-        kt.end(st);
-    }
+    kt.begin(st, RSA_K_FIND_NAMS);
+    hipLaunchKernelGGL(k_find_nams_w, dim3((n + FN_WAVES - 1) / FN_WAVES), dim3(64 * FN_WAVES), 0, st,
+                       DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t), DP(B_QBASE, uint64_t),
+                       DP(B_ST, ReadStat), DP(B_HOFF, uint64_t), (int)n, p, DP(B_HITS, HitD), DP(B_OPEN, rsa_nam),
+                       DP(B_NAM1, rsa_nam), DP(B_NCNT1, uint32_t), DP(B_NONREP, float), DP(B_FLAGS, uint32_t));
+    SCHK(hipGetLastError());
+    kt.end(st);
     SCHK(hens(b, H_FLAGS, 4ull * n));
     SCHK(hipMemcpyAsync(b.h[H_FLAGS], b.p[B_FLAGS], 4ull * n, hipMemcpyDeviceToHost, st));
     SCHK(hipMemcpyAsync(b.h[H_CNT], b.p[B_NCNT1], 4ull * n, hipMemcpyDeviceToHost, st));
@@ -870,7 +1081,7 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
     if (!big.empty()) {
         const size_t big_stride = (size_t)MAP_BIG * 9 * 4;
         const uint32_t bchunk = 32;
-        SCHK(dens(b, B_MAP, std::max(big_stride * bchunk, small_stride * std::min<uint32_t>(n, chunk))));
+        SCHK(dens(b, B_MAP, big_stride * bchunk));
         SCHK(dens(b, B_LIST, 4ull * big.size()));
         SCHK(hipMemcpyAsync(b.p[B_LIST], big.data(), 4ull * big.size(), hipMemcpyHostToDevice, st));
         for (size_t a = 0; a < big.size(); a += bchunk) {
@@ -923,11 +1134,11 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
         for (size_t a = 0; a < resc.size(); a += chunk) {
             const int cnt = (int)std::min<size_t>(chunk, resc.size() - a);
             kt.begin(st, RSA_K_RESCUE);
-            hipLaunchKernelGGL(k_rescue, dim3((cnt + 63) / 64), dim3(64), 0, st, DP(B_QRS, rsa_query_randstrobe),
-                               DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t), DP(B_QBASE, uint64_t), DP(B_ROFF2, uint64_t), cnt,
-                               DP(B_LIST, int) + a, p, rescue_cutoff, DP(B_RBUF, RescueD), DP(B_HITS, HitD),
-                               DP(B_OPEN, rsa_nam), DP(B_NAM2, rsa_nam), grp, added, DP(B_MAP, uint8_t), MAP_SMALL,
-                               DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t));
+            hipLaunchKernelGGL(k_rescue_w, dim3((cnt + FN_WAVES - 1) / FN_WAVES), dim3(64 * FN_WAVES), 0, st,
+                               DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t),
+                               DP(B_QBASE, uint64_t), DP(B_ROFF2, uint64_t), cnt, DP(B_LIST, int) + a, p, rescue_cutoff,
+                               DP(B_RBUF, RescueD), DP(B_HITS, HitD), DP(B_OPEN, rsa_nam), DP(B_NAM2, rsa_nam), grp,
+                               added, DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t));
             SCHK(hipGetLastError());
             kt.end(st);
         }
