@@ -124,6 +124,7 @@ def main():
     import torch
     import torch.distributed as dist
     from rabbitsalign_amd import mapper as M
+    from rabbitsalign_amd import shard
     M.load()
 
     has_gpu = torch.cuda.is_available()
@@ -136,13 +137,6 @@ def main():
     def barrier():
         if world > 1:
             dist.barrier()
-
-    def allreduce(v: float, op) -> float:
-        if world == 1:
-            return v
-        t = torch.tensor([v], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=op)
-        return float(t.item())
 
     t = time.time()
     log(rank, f"building {wl['ref_len']/1e9:.3f} Gb reference ({wl['n_contigs']} contigs) + index, {threads} threads")
@@ -157,7 +151,7 @@ def main():
     batches = []
     t = time.time()
     for s in range(total_steps):
-        first = (rank * total_steps + s) * P
+        first = shard.first_pair(rank, s, total_steps, P)
         batches.append(m.synthetic_reads(args.read_seed, first, P, wl["read_len"], wl["mu"], wl["sigma"],
                                          wl["paired"]))
     log(rank, f"generated {total_steps} x {P} {'pairs' if wl['paired'] else 'reads'} in {time.time()-t:.1f} s")
@@ -171,10 +165,13 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     n_reads = 0
+    totals = {f: 0 for f in shard.STAT_FIELDS}
     hashes = []
     for s in range(args.warmup, total_steps):
         st = m.map(batches[s], threads=threads, chunk_size=args.chunk_size)
         n_reads += st.n_reads
+        for f in shard.STAT_FIELDS:
+            totals[f] += getattr(st, f)
         hashes.append(st.sam_hash)
         log(rank, f"step {s - args.warmup}: {st.n_reads} reads in {st.map_seconds:.3f} s "
                   f"({st.n_reads / st.map_seconds / 1e6:.4f} Mreads/s), SW {st.sw_calls}; thread-s: "
@@ -185,8 +182,9 @@ def main():
     elapsed = time.perf_counter() - t0
     ks = m.kernel_stats()
 
-    elapsed_max = allreduce(elapsed, dist.ReduceOp.MAX if world > 1 else None)
-    reads_all = allreduce(float(n_reads), dist.ReduceOp.SUM if world > 1 else None)
+    # the run's only collective: max wall time and summed statistics over ranks (RCCL)
+    elapsed_max, totals_all = shard.reduce_run(elapsed, totals, device="cuda")
+    reads_all = float(totals_all["n_reads"])
     for b in batches:
         b.close()
 
@@ -233,6 +231,7 @@ def main():
             "parity": parity,
             "kernels": kernel_table(ks),
             "device_counters": {k: v for k, v in ks.items() if k != "kernels"},
+            "mapping_stats_all_ranks": totals_all,
             "sam_hashes": [f"{h:016x}" for h in hashes],
         }
         if args.stats_out:

@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -961,6 +962,13 @@ static hipError_t hens(SeedBufs& b, int i, size_t bytes) {
 
 static const uint32_t MAP_BIG = 65536 + 512;
 
+// A/B switch for kernel experiments: RSA_RS_LANE=1 / RSA_FN_LANE=1 select the
+// one-lane-per-read variants (same results).
+static bool seed_variant_lane(const char* var) {
+    const char* v = getenv(var);
+    return v && v[0] == '1';
+}
+
 // Stage 1 (shared by rsa_randstrobes and rsa_seed): upload reads, run k_randstrobes.
 int seed_stage_randstrobes(SeedBufs& b, hipStream_t st, const SeedIndexParams& p, const rsa_read_batch* rb,
                            std::vector<uint64_t>& qbase, std::string& err, KTimer* kt) {
@@ -984,7 +992,8 @@ int seed_stage_randstrobes(SeedBufs& b, hipStream_t st, const SeedIndexParams& p
     SCHK(hipMemcpyAsync(b.p[B_QBASE], qbase.data(), 8ull * (n + 1), hipMemcpyHostToDevice, st));
     uint32_t max_len = 0;
     for (uint32_t i = 0; i < n; ++i) max_len = std::max(max_len, rb->lengths[i]);
-    const bool wave = max_len <= RS_MAXLEN && p.k <= 32 && p.s <= 32 && p.k - p.s + 1 <= RS_RING;
+    const bool wave = max_len <= RS_MAXLEN && p.k <= 32 && p.s <= 32 && p.k - p.s + 1 <= RS_RING &&
+                      !seed_variant_lane("RSA_RS_LANE");
     if (kt) kt->begin(st, RSA_K_RANDSTROBES);
     if (wave)
         hipLaunchKernelGGL(k_randstrobes_w, dim3((n + RS_WAVES - 1) / RS_WAVES), dim3(64 * RS_WAVES), 0, st,
@@ -1065,10 +1074,21 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
     const uint32_t chunk = 65536;
     SCHK(hipMemcpyAsync(b.p[B_HOFF], hoff, 8ull * (n + 1), hipMemcpyHostToDevice, st));
     kt.begin(st, RSA_K_FIND_NAMS);
-    hipLaunchKernelGGL(k_find_nams_w, dim3((n + FN_WAVES - 1) / FN_WAVES), dim3(64 * FN_WAVES), 0, st,
-                       DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t), DP(B_QBASE, uint64_t),
-                       DP(B_ST, ReadStat), DP(B_HOFF, uint64_t), (int)n, p, DP(B_HITS, HitD), DP(B_OPEN, rsa_nam),
-                       DP(B_NAM1, rsa_nam), DP(B_NCNT1, uint32_t), DP(B_NONREP, float), DP(B_FLAGS, uint32_t));
+    if (!seed_variant_lane("RSA_FN_LANE")) {
+        hipLaunchKernelGGL(k_find_nams_w, dim3((n + FN_WAVES - 1) / FN_WAVES), dim3(64 * FN_WAVES), 0, st,
+                           DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t),
+                           DP(B_QBASE, uint64_t), DP(B_ST, ReadStat), DP(B_HOFF, uint64_t), (int)n, p, DP(B_HITS, HitD),
+                           DP(B_OPEN, rsa_nam), DP(B_NAM1, rsa_nam), DP(B_NCNT1, uint32_t), DP(B_NONREP, float),
+                           DP(B_FLAGS, uint32_t));
+    } else {
+        const size_t small_stride = (size_t)FN_MAP_CAP * 9 * 4;
+        SCHK(dens(b, B_MAP, small_stride * n));
+        hipLaunchKernelGGL(k_find_nams, dim3((n + 63) / 64), dim3(64), 0, st, DP(B_QRS, rsa_query_randstrobe),
+                           DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t), DP(B_QBASE, uint64_t), DP(B_ST, ReadStat),
+                           DP(B_HOFF, uint64_t), (int)n, (const int*)nullptr, p, DP(B_HITS, HitD), DP(B_OPEN, rsa_nam),
+                           DP(B_NAM1, rsa_nam), DP(B_MAP, uint8_t), FN_MAP_CAP, DP(B_NCNT1, uint32_t),
+                           DP(B_NONREP, float), DP(B_FLAGS, uint32_t));
+    }
     SCHK(hipGetLastError());
     kt.end(st);
     SCHK(hens(b, H_FLAGS, 4ull * n));

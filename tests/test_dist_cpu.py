@@ -1,0 +1,90 @@
+"""CPU, world_size 2 over gloo: the multi-GPU sharding of bench.py.
+
+Each rank maps its own shard of synthetic pairs (rabbitsalign_amd.shard) with
+the CPU-path build of include/rsalign.h (the parity reference, test
+infrastructure), then the ranks reduce wall time and statistics exactly as
+bench.py does over RCCL.  Checks: shards are disjoint, the reduced read count
+is the sum, and every rank's SAM equals a single-process mapping of the same
+shard (placement does not change results)."""
+import os
+import socket
+
+import pytest
+
+from helpers import ROOT
+
+REF_CPU_LIB = os.path.join(ROOT, "oracle", "_ref", "librsalign_ref.so")
+CFG = dict(seed=3, ref_len=2_000_000, contigs=2, L=150, pairs=1500, steps=2)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _map_shard(m, rank, step):
+    from rabbitsalign_amd import shard
+    first = shard.first_pair(rank, step, CFG["steps"], CFG["pairs"])
+    reads = m.synthetic_reads(7, first, CFG["pairs"], CFG["L"], 300.0, 30.0, True)
+    st = m.map(reads, threads=2, chunk_size=500)
+    reads.close()
+    return st
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    from rabbitsalign_amd import mapper, shard
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = mapper.Mapper.synthetic(CFG["seed"], CFG["ref_len"], CFG["contigs"], CFG["L"], threads=2,
+                                    lib_path=REF_CPU_LIB)
+        totals = {f: 0 for f in shard.STAT_FIELDS}
+        hashes = []
+        for step in range(CFG["steps"]):
+            st = _map_shard(m, rank, step)
+            hashes.append(st.sam_hash)
+            for f in shard.STAT_FIELDS:
+                totals[f] += getattr(st, f)
+        wall, tot = shard.reduce_run(1.0 + rank, totals, device="cpu")
+        q.put((rank, hashes, totals, wall, tot))
+        m.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.skipif(not os.path.exists(REF_CPU_LIB), reason="CPU-path library not built")
+def test_two_rank_sharding_gloo():
+    import torch.multiprocessing as mp
+    from rabbitsalign_amd import mapper, shard
+    ranges = {(r, s): shard.first_pair(r, s, CFG["steps"], CFG["pairs"]) for r in range(2) for s in range(CFG["steps"])}
+    starts = sorted(ranges.values())
+    assert all(b - a >= CFG["pairs"] for a, b in zip(starts, starts[1:]))
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        rank, hashes, totals, wall, tot = q.get(timeout=600)
+        res[rank] = (hashes, totals, wall, tot)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # reduced values identical on both ranks: max wall, summed counters
+    for r in range(2):
+        assert res[r][2] == 2.0
+        assert res[r][3]["n_reads"] == 2 * CFG["steps"] * 2 * CFG["pairs"]
+        assert res[r][3] == {k: res[0][1][k] + res[1][1][k] for k in shard.STAT_FIELDS}
+    # a rank's SAM equals a single-process mapping of the same shard
+    m = mapper.Mapper.synthetic(CFG["seed"], CFG["ref_len"], CFG["contigs"], CFG["L"], threads=2,
+                                lib_path=REF_CPU_LIB)
+    for r in range(2):
+        assert _map_shard(m, r, 1).sam_hash == res[r][0][1]
+    m.close()
