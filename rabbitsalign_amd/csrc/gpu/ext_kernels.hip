@@ -44,20 +44,27 @@ struct PassOut {
 // One SSW pass over `ncol` reference columns with `nrow` query rows.
 // fwd: row p -> qc[p], column c -> rc[c]
 // rev: row p -> qc[qend - p], column c -> rc[rend - c]
+// Per cell: E, Fw and F are kept >= 0 (result-neutral, as in SSW), so
+// H' = max(0, diag + s, E, Fw) is a single max3.  The best-cell bookkeeping is
+// per column: a lane takes its column maximum over its valid rows and only
+// looks for the row when that maximum improves (same first-column /
+// smallest-row tie rules as the per-cell strict '>').
 template <int R, bool REV>
 __device__ PassOut sw_pass(const uint8_t* __restrict__ qc, int nrow, const uint8_t* __restrict__ rc, int ncol,
                            int qend, int rend, int match, int mismatch, int gO, int gE, int seg,
                            int terminate, int lane) {
     const int lanes_used = (nrow + R - 1) / R;
     int E[R], Hc[R], qv[R];
-    bool ss[R];
+    bool ss[R], valid[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         E[r] = 0;
         Hc[r] = 0;
         const int p = lane * R + r;
         ss[r] = (p % seg) == 0;
-        qv[r] = p < nrow ? (int)qc[REV ? (qend - p) : p] : 7;  // padded rows never score a match
+        valid[r] = p < nrow;
+        const int code = valid[r] ? (int)qc[REV ? (qend - p) : p] : 7;
+        qv[r] = code < 4 ? code : 7;          // N (and padding) never scores a match, not even vs N
     }
     int F_out = 0, Fw_out = 0, H_last = 0, diag_top = 0;
     int best = 0, bcol = INT_MAX, brow = INT_MAX;
@@ -70,33 +77,45 @@ __device__ PassOut sw_pass(const uint8_t* __restrict__ qc, int nrow, const uint8
         const int c = s - lane;
         if (lane < lanes_used && c >= 0 && c < ncol) {
             const int rcode = rc[REV ? (rend - c) : c];
-            int dg = diag_top, F = F_in, Fw = Fw_in;
+            int dg = diag_top, F = F_in, Fw = Fw_in, cm = 0;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 if (ss[r]) Fw = 0;
-                int hm = max(dg + subst(qv[r], rcode, match, mismatch), 0);
-                hm = max(hm, E[r]);
-                hm = max(hm, Fw);
+                const int diag = dg + (qv[r] == rcode ? match : -mismatch);
+                const int hm = max(max(diag, E[r]), Fw);
                 const int h = max(hm, F);
                 dg = Hc[r];
                 Hc[r] = h;
-                const int ho = max(hm - gO, 0);
-                E[r] = max(E[r] - gE, ho);
-                Fw = max(Fw - gE, ho);
-                F = max(F - gE, max(h - gO, 0));
-                const int p = lane * R + r;
-                if (p < nrow) {
-                    if (!REV) {
-                        if (h > best) { best = h; bcol = c; brow = p; }
-                    } else {
-                        if (h > best) best = h;
-                        if (h == terminate && tcol == INT_MAX) { tcol = c; trow = p; }
-                    }
-                }
+                const int t = hm - gO;
+                E[r] = max(max(E[r] - gE, t), 0);
+                Fw = max(max(Fw - gE, t), 0);
+                F = max(max(F - gE, h - gO), 0);
+                cm = max(cm, valid[r] ? h : 0);
             }
             F_out = F;
             Fw_out = Fw;
             H_last = Hc[R - 1];
+            if (!REV) {
+                if (cm > best) {
+                    best = cm;
+                    bcol = c;
+                    int row = INT_MAX;
+#pragma unroll
+                    for (int r = R - 1; r >= 0; --r)
+                        if (valid[r] && Hc[r] == cm) row = lane * R + r;
+                    brow = row;
+                }
+            } else {
+                if (cm > best) best = cm;
+                if (cm == terminate && tcol == INT_MAX) {
+                    tcol = c;
+                    int row = INT_MAX;
+#pragma unroll
+                    for (int r = R - 1; r >= 0; --r)
+                        if (valid[r] && Hc[r] == terminate) row = lane * R + r;
+                    trow = row;
+                }
+            }
         }
         diag_top = Hl_in;
         if (REV && (s & 7) == 7) {
@@ -318,9 +337,13 @@ __device__ __forceinline__ void cpush(uint32_t* c, int& n, uint32_t op, uint32_t
 
 // ConvertAlignment + CalculateNumberMismatch + the end-bonus step of
 // Aligner::align, given the raw banded_sw ops of a job (shared by both band kernels).
+// qcs/rcs (optional): SSW codes of the aligned segment, read_begin1.. and
+// ref_begin1.. (the band kernels hold them in LDS); without them the =/X split
+// translates the bytes from global memory.
 __device__ void ext_finish(const ExtJobDev& jb, const ScanRes& sr, const char* __restrict__ q,
                            const char* __restrict__ r, const uint32_t* __restrict__ raw, int nraw,
-                           uint32_t* __restrict__ c, rsa_aln& a, int match, int mismatch, int bonus) {
+                           uint32_t* __restrict__ c, rsa_aln& a, int match, int mismatch, int bonus,
+                           const uint8_t* qcs = nullptr, const uint8_t* rcs = nullptr) {
     const int qlen = (int)jb.qlen, rlen = (int)jb.rlen;
     // ConvertAlignment + CalculateNumberMismatch (ssw_cpp.cpp:54-90, 126-210).
     // Core ops are built after a gap of qs+2 entries (room for the left end-bonus ops).
@@ -337,8 +360,15 @@ __device__ void ext_finish(const ExtJobDev& jb, const ScanRes& sr, const char* _
         const uint32_t opk = raw[k] & 0xf, lenk = raw[k] >> 4;
         if (opk == 0) {
             for (uint32_t z = 0; z < lenk; ++z) {
-                const int rcode = (rp >= 0 && rp < rlen) ? ssw_code((unsigned char)r[rp]) : 4;
-                const int qcode = ssw_code((unsigned char)q[qp]);
+                int rcode, qcode;
+                const int qo = qp - qs0, ro = rp - sr.ref_begin1;
+                if (qcs && qo >= 0 && qo <= sr.read_end1 - qs0 && ro >= 0 && ro <= sr.ref_end1 - sr.ref_begin1) {
+                    rcode = rcs[ro];
+                    qcode = qcs[qo];
+                } else {
+                    rcode = (rp >= 0 && rp < rlen) ? ssw_code((unsigned char)r[rp]) : 4;
+                    qcode = ssw_code((unsigned char)q[qp]);
+                }
                 if (rcode != qcode) {
                     ++mism;
                     if (in_m) core[n++] = cig(len_m, 7);
@@ -654,7 +684,7 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
     if (op == 0) { ++l; raw[l - 1] = cig((uint32_t)ecount + 1, op); }
     else { l += 2; raw[l - 2] = cig((uint32_t)ecount, op); raw[l - 1] = cig(1, 0); }
     for (int s = 0, t = l - 1; s < t; ++s, --t) { const uint32_t x = raw[s]; raw[s] = raw[t]; raw[t] = x; }
-    ext_finish(jb, sr, q, r, raw, l, cig_pool + jb.cig_off, a, match, mismatch, bonus);
+    ext_finish(jb, sr, q, r, raw, l, cig_pool + jb.cig_off, a, match, mismatch, bonus, qc, rc);
     out[j] = a;
     return true;
 }

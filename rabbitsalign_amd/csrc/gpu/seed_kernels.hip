@@ -75,25 +75,57 @@ __device__ void rs_get(const SyncD* sm, int n, int i, const SeedIndexParams& p, 
     b = sm[best].pos;
 }
 
-__global__ void __launch_bounds__(64)
-k_randstrobes(const char* __restrict__ seq, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
-              const uint64_t* __restrict__ qbase, int n_reads, SeedIndexParams p, SyncD* __restrict__ sync,
-              rsa_query_randstrobe* __restrict__ qrs, uint32_t* __restrict__ qcnt) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n_reads) return;
-    const int len = (int)rlen[r];
-    const char* s = seq + roff[r];
-    SyncD* sm = sync + qbase[r] / 2;
-    rsa_query_randstrobe* out = qrs + qbase[r];
-    if (len < p.w_max) { qcnt[r] = 0; return; }     // randstrobes.cpp:209
-    // SyncmerIterator::next (randstrobes.cpp:57-118)
+// Syncmer window of the last W s-mer hashes, oldest first.  WC > 0: W == WC
+// held in registers as a shift register (all indices static); WC == 0: any W
+// in a ring buffer (private memory).
+template <int WC>
+struct SmWindow {
+    uint64_t q[WC > 0 ? WC : 32];
+    int qn = 0, qhead = 0, W;
+    __device__ explicit SmWindow(int w) : W(WC > 0 ? WC : w) {}
+    __device__ __forceinline__ uint64_t at(int j) const {
+        if constexpr (WC > 0) {
+            uint64_t v = q[0];
+#pragma unroll
+            for (int x = 1; x < WC; ++x) if (j == x) v = q[x];
+            return v;
+        } else {
+            return q[(qhead + j) & 31];
+        }
+    }
+    // push h; returns true when the window was already full (front popped)
+    __device__ __forceinline__ bool push(uint64_t h) {
+        if constexpr (WC > 0) {
+            if (qn < WC) {
+#pragma unroll
+                for (int x = 0; x < WC; ++x) if (x == qn) q[x] = h;
+                qn++;
+                return false;
+            }
+#pragma unroll
+            for (int x = 0; x + 1 < WC; ++x) q[x] = q[x + 1];
+            q[WC - 1] = h;
+            return true;
+        } else {
+            q[(qhead + qn) & 31] = h;
+            if (qn < W) { qn++; return false; }
+            qhead = (qhead + 1) & 31;
+            return true;
+        }
+    }
+    __device__ __forceinline__ void reset() { qn = 0; qhead = 0; }
+};
+
+// SyncmerIterator::next (randstrobes.cpp:57-118) over the whole read; returns
+// the number of syncmers written to sm.
+template <int WC>
+__device__ int syncmers_lane(const char* __restrict__ s, int len, const SeedIndexParams& p, SyncD* __restrict__ sm) {
     const int k = p.k, sl = p.s, t = p.t;
     const uint64_t kmask = (k == 32) ? ~0ULL : ((1ULL << (2 * k)) - 1);
     const uint64_t smask = (1ULL << (2 * sl)) - 1;
     const int kshift = (k - 1) * 2, sshift = (sl - 1) * 2;
-    const int W = k - sl + 1;
-    uint64_t ring[32];
-    int qn = 0, qhead = 0;
+    SmWindow<WC> win(k - sl + 1);
+    const int W = win.W;
     uint64_t min_val = END64;
     long long min_pos = -1;
     int l = 0, n = 0;
@@ -107,27 +139,23 @@ k_randstrobes(const char* __restrict__ seq, const uint64_t* __restrict__ roff, c
             xs1 = (xs1 >> 2) | ((uint64_t)(3 - c) << sshift);
             if (++l < sl) continue;
             const uint64_t hs = xxh64_u64(xs0 < xs1 ? xs0 : xs1);
-            ring[(qhead + qn) & 31] = hs;
-            qn++;
-            if (qn < W) continue;
-            if (qn == W) {
-                for (int j = 0; j < qn; ++j) {
-                    const uint64_t v = ring[(qhead + j) & 31];
+            const bool popped = win.push(hs);
+            if (!popped) {
+                if (win.qn < W) continue;
+                for (int j = 0; j < W; ++j) {          // first fill: leftmost minimum
+                    const uint64_t v = win.at(j);
                     if (v < min_val) { min_val = v; min_pos = (long long)i - k + j + 1; }
                 }
-            } else {
-                qhead = (qhead + 1) & 31; qn--;
-                if (min_pos == (long long)i - k) {
-                    min_val = END64;
-                    min_pos = (long long)i - sl + 1;
-                    for (int j = qn - 1; j >= 0; --j) {
-                        const uint64_t v = ring[(qhead + j) & 31];
-                        if (v < min_val) { min_val = v; min_pos = (long long)i - k + j + 1; }
-                    }
-                } else if (hs < min_val) {
-                    min_val = hs;
-                    min_pos = (long long)i - sl + 1;
+            } else if (min_pos == (long long)i - k) {   // the minimum left: rescan, rightmost wins
+                min_val = END64;
+                min_pos = (long long)i - sl + 1;
+                for (int j = W - 1; j >= 0; --j) {
+                    const uint64_t v = win.at(j);
+                    if (v < min_val) { min_val = v; min_pos = (long long)i - k + j + 1; }
                 }
+            } else if (hs < min_val) {
+                min_val = hs;
+                min_pos = (long long)i - sl + 1;
             }
             if (min_pos == (long long)i - k + t) {
                 sm[n].hash = xxh64_u64(xk0 < xk1 ? xk0 : xk1);
@@ -137,9 +165,30 @@ k_randstrobes(const char* __restrict__ seq, const uint64_t* __restrict__ roff, c
         } else {
             min_val = END64; min_pos = -1;
             l = 0; xs0 = xs1 = xk0 = xk1 = 0;
-            qn = 0; qhead = 0;
+            win.reset();
         }
     }
+    return n;
+}
+
+// one lane per read, `rpw` reads per wave (fewer reads per wave = more waves
+// in flight and less divergence per wave)
+template <int WC>
+__global__ void __launch_bounds__(64)
+k_randstrobes(const char* __restrict__ seq, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
+              const uint64_t* __restrict__ qbase, int n_reads, int rpw, SeedIndexParams p, SyncD* __restrict__ sync,
+              rsa_query_randstrobe* __restrict__ qrs, uint32_t* __restrict__ qcnt) {
+    const int lane = threadIdx.x & 63;
+    if (lane >= rpw) return;
+    const int r = blockIdx.x * rpw + lane;
+    if (r >= n_reads) return;
+    const int len = (int)rlen[r];
+    const char* s = seq + roff[r];
+    SyncD* sm = sync + qbase[r] / 2;
+    rsa_query_randstrobe* out = qrs + qbase[r];
+    if (len < p.w_max) { qcnt[r] = 0; return; }     // randstrobes.cpp:209
+    const int k = p.k;
+    const int n = syncmers_lane<WC>(s, len, p, sm);
     int cnt = 0;
     if (n > 0) {
         for (int i = 0; i + p.w_min < n; ++i) {
@@ -741,8 +790,11 @@ k_find_nams(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restr
             const uint64_t* __restrict__ qbase, const ReadStat* __restrict__ st, const uint64_t* __restrict__ hoff,
             int n_reads, const int* __restrict__ list, SeedIndexParams p, HitD* __restrict__ hits_buf,
             rsa_nam* __restrict__ open_buf, rsa_nam* __restrict__ nam_buf, uint8_t* __restrict__ map_scratch,
-            uint32_t map_cap, uint32_t* __restrict__ ncnt, float* __restrict__ nonrep, uint32_t* __restrict__ flags) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+            uint32_t map_cap, uint32_t* __restrict__ ncnt, float* __restrict__ nonrep, uint32_t* __restrict__ flags,
+            int rpw) {
+    const int lane = threadIdx.x & 63;
+    if (lane >= rpw) return;
+    const int t = blockIdx.x * rpw + lane;
     if (t >= n_reads) return;
     const int r = list ? list[t] : t;
     find_nams_read(r, qrs, qi, qcnt, qbase, st, hoff, p, hits_buf, open_buf, nam_buf,
@@ -962,11 +1014,19 @@ static hipError_t hens(SeedBufs& b, int i, size_t bytes) {
 
 static const uint32_t MAP_BIG = 65536 + 512;
 
-// A/B switch for kernel experiments: RSA_RS_LANE=1 / RSA_FN_LANE=1 select the
-// one-lane-per-read variants (same results).
+// A/B switches for kernel experiments: RSA_RS_WAVE=1 / RSA_FN_WAVE=1 select
+// the wave-per-read variants (same results, slower on the headline workload).
 static bool seed_variant_lane(const char* var) {
     const char* v = getenv(var);
     return v && v[0] == '1';
+}
+// reads per wave of the one-lane-per-read kernels (RSA_RPW_RS / RSA_RPW_FN).
+// Measured on the headline workload (profiles/r01_kab.jsonl): randstrobes is
+// fastest with 64 reads per wave, find_nams with 16 (divergent, latency-bound).
+static int seed_rpw(const char* var, int dflt) {
+    const char* v = getenv(var);
+    const int x = v ? atoi(v) : dflt;
+    return (x >= 1 && x <= 64) ? x : dflt;
 }
 
 // Stage 1 (shared by rsa_randstrobes and rsa_seed): upload reads, run k_randstrobes.
@@ -993,16 +1053,21 @@ int seed_stage_randstrobes(SeedBufs& b, hipStream_t st, const SeedIndexParams& p
     uint32_t max_len = 0;
     for (uint32_t i = 0; i < n; ++i) max_len = std::max(max_len, rb->lengths[i]);
     const bool wave = max_len <= RS_MAXLEN && p.k <= 32 && p.s <= 32 && p.k - p.s + 1 <= RS_RING &&
-                      !seed_variant_lane("RSA_RS_LANE");
+                      seed_variant_lane("RSA_RS_WAVE");
     if (kt) kt->begin(st, RSA_K_RANDSTROBES);
+    const int rpw = seed_rpw("RSA_RPW_RS", 64);
     if (wave)
         hipLaunchKernelGGL(k_randstrobes_w, dim3((n + RS_WAVES - 1) / RS_WAVES), dim3(64 * RS_WAVES), 0, st,
                            DP(B_SEQ, char), DP(B_ROFF, uint64_t), DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n,
                            p, DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
+    else if (p.k - p.s + 1 == 5)
+        hipLaunchKernelGGL(k_randstrobes<5>, dim3((n + rpw - 1) / rpw), dim3(64), 0, st, DP(B_SEQ, char),
+                           DP(B_ROFF, uint64_t), DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n, rpw, p,
+                           DP(B_SYNC, SyncD), DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
     else
-        hipLaunchKernelGGL(k_randstrobes, dim3((n + 63) / 64), dim3(64), 0, st, DP(B_SEQ, char), DP(B_ROFF, uint64_t),
-                           DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n, p, DP(B_SYNC, SyncD),
-                           DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
+        hipLaunchKernelGGL(k_randstrobes<0>, dim3((n + rpw - 1) / rpw), dim3(64), 0, st, DP(B_SEQ, char),
+                           DP(B_ROFF, uint64_t), DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n, rpw, p,
+                           DP(B_SYNC, SyncD), DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
     SCHK(hipGetLastError());
     if (kt) kt->end(st);
     return RSA_OK;
@@ -1074,7 +1139,7 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
     const uint32_t chunk = 65536;
     SCHK(hipMemcpyAsync(b.p[B_HOFF], hoff, 8ull * (n + 1), hipMemcpyHostToDevice, st));
     kt.begin(st, RSA_K_FIND_NAMS);
-    if (!seed_variant_lane("RSA_FN_LANE")) {
+    if (seed_variant_lane("RSA_FN_WAVE")) {
         hipLaunchKernelGGL(k_find_nams_w, dim3((n + FN_WAVES - 1) / FN_WAVES), dim3(64 * FN_WAVES), 0, st,
                            DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t),
                            DP(B_QBASE, uint64_t), DP(B_ST, ReadStat), DP(B_HOFF, uint64_t), (int)n, p, DP(B_HITS, HitD),
@@ -1083,11 +1148,12 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
     } else {
         const size_t small_stride = (size_t)FN_MAP_CAP * 9 * 4;
         SCHK(dens(b, B_MAP, small_stride * n));
-        hipLaunchKernelGGL(k_find_nams, dim3((n + 63) / 64), dim3(64), 0, st, DP(B_QRS, rsa_query_randstrobe),
+        const int rpw = seed_rpw("RSA_RPW_FN", 16);
+        hipLaunchKernelGGL(k_find_nams, dim3((n + rpw - 1) / rpw), dim3(64), 0, st, DP(B_QRS, rsa_query_randstrobe),
                            DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t), DP(B_QBASE, uint64_t), DP(B_ST, ReadStat),
                            DP(B_HOFF, uint64_t), (int)n, (const int*)nullptr, p, DP(B_HITS, HitD), DP(B_OPEN, rsa_nam),
                            DP(B_NAM1, rsa_nam), DP(B_MAP, uint8_t), FN_MAP_CAP, DP(B_NCNT1, uint32_t),
-                           DP(B_NONREP, float), DP(B_FLAGS, uint32_t));
+                           DP(B_NONREP, float), DP(B_FLAGS, uint32_t), rpw);
     }
     SCHK(hipGetLastError());
     kt.end(st);
@@ -1111,7 +1177,7 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
                                DP(B_QCNT, uint32_t), DP(B_QBASE, uint64_t), DP(B_ST, ReadStat), DP(B_HOFF, uint64_t), cnt,
                                DP(B_LIST, int) + a, p, DP(B_HITS, HitD), DP(B_OPEN, rsa_nam), DP(B_NAM1, rsa_nam),
                                DP(B_MAP, uint8_t), MAP_BIG, DP(B_NCNT1, uint32_t), DP(B_NONREP, float),
-                               DP(B_FLAGS, uint32_t));
+                               DP(B_FLAGS, uint32_t), 64);
             SCHK(hipGetLastError());
             kt.end(st);
         }
