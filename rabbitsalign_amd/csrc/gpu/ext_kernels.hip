@@ -41,6 +41,72 @@ struct PassOut {
     int tcol, trow;          // reverse: first column reaching terminate
 };
 
+// Variant 0: per-cell best tracking, literal SSW recurrence.
+template <int R, bool REV>
+__device__ PassOut sw_pass_v0(const uint8_t* __restrict__ qc, int nrow, const uint8_t* __restrict__ rc, int ncol,
+                           int qend, int rend, int match, int mismatch, int gO, int gE, int seg,
+                           int terminate, int lane) {
+    const int lanes_used = (nrow + R - 1) / R;
+    int E[R], Hc[R], qv[R];
+    bool ss[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        E[r] = 0;
+        Hc[r] = 0;
+        const int p = lane * R + r;
+        ss[r] = (p % seg) == 0;
+        qv[r] = p < nrow ? (int)qc[REV ? (qend - p) : p] : 7;  // padded rows never score a match
+    }
+    int F_out = 0, Fw_out = 0, H_last = 0, diag_top = 0;
+    int best = 0, bcol = INT_MAX, brow = INT_MAX;
+    int tcol = INT_MAX, trow = INT_MAX;
+    const int steps = ncol + lanes_used - 1;
+    for (int s = 0; s < steps; ++s) {
+        const int F_in = wave_shr1(F_out);
+        const int Fw_in = wave_shr1(Fw_out);
+        const int Hl_in = wave_shr1(H_last);
+        const int c = s - lane;
+        if (lane < lanes_used && c >= 0 && c < ncol) {
+            const int rcode = rc[REV ? (rend - c) : c];
+            int dg = diag_top, F = F_in, Fw = Fw_in;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (ss[r]) Fw = 0;
+                int hm = max(dg + subst(qv[r], rcode, match, mismatch), 0);
+                hm = max(hm, E[r]);
+                hm = max(hm, Fw);
+                const int h = max(hm, F);
+                dg = Hc[r];
+                Hc[r] = h;
+                const int ho = max(hm - gO, 0);
+                E[r] = max(E[r] - gE, ho);
+                Fw = max(Fw - gE, ho);
+                F = max(F - gE, max(h - gO, 0));
+                const int p = lane * R + r;
+                if (p < nrow) {
+                    if (!REV) {
+                        if (h > best) { best = h; bcol = c; brow = p; }
+                    } else {
+                        if (h > best) best = h;
+                        if (h == terminate && tcol == INT_MAX) { tcol = c; trow = p; }
+                    }
+                }
+            }
+            F_out = F;
+            Fw_out = Fw;
+            H_last = Hc[R - 1];
+        }
+        diag_top = Hl_in;
+        if (REV && (s & 7) == 7) {
+            const int m = wave_min_i32(tcol);
+            if (m != INT_MAX && s >= m + lanes_used - 1) break;
+        }
+    }
+    PassOut o;
+    o.best = best; o.col = bcol; o.row = brow; o.tcol = tcol; o.trow = trow;
+    return o;
+}
+
 // One SSW pass over `ncol` reference columns with `nrow` query rows.
 // fwd: row p -> qc[p], column c -> rc[c]
 // rev: row p -> qc[qend - p], column c -> rc[rend - c]
@@ -130,9 +196,12 @@ __device__ PassOut sw_pass(const uint8_t* __restrict__ qc, int nrow, const uint8
 
 template <bool REV>
 __device__ PassOut sw_pass_dispatch(const uint8_t* qc, int nrow, const uint8_t* rc, int ncol, int qend, int rend,
-                                    int match, int mismatch, int gO, int gE, int seg, int terminate, int lane) {
+                                    int match, int mismatch, int gO, int gE, int seg, int terminate, int lane,
+                                    int variant) {
     const int R = (nrow + 63) / 64;
-#define RSA_PASS(N) return sw_pass<N, REV>(qc, nrow, rc, ncol, qend, rend, match, mismatch, gO, gE, seg, terminate, lane)
+#define RSA_PASS(N)                                                                                         \
+    return variant ? sw_pass<N, REV>(qc, nrow, rc, ncol, qend, rend, match, mismatch, gO, gE, seg, terminate, lane) \
+                   : sw_pass_v0<N, REV>(qc, nrow, rc, ncol, qend, rend, match, mismatch, gO, gE, seg, terminate, lane)
     switch (R) {
         case 0: case 1: RSA_PASS(1);
         case 2: RSA_PASS(2);
@@ -150,7 +219,8 @@ __device__ PassOut sw_pass_dispatch(const uint8_t* qc, int nrow, const uint8_t* 
 
 __global__ void __launch_bounds__(64 * SCAN_WAVES)
 k_ext_scan(const ExtJobDev* __restrict__ jobs, int n_jobs, const char* __restrict__ qbuf,
-           const char* __restrict__ ref, ScanRes* __restrict__ out, int match, int mismatch, int gO, int gE) {
+           const char* __restrict__ ref, ScanRes* __restrict__ out, int match, int mismatch, int gO, int gE,
+           int variant) {
     __shared__ uint8_t s_q[SCAN_WAVES][MAXQ_LDS];
     __shared__ uint8_t s_r[SCAN_WAVES][MAXR_LDS];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -180,11 +250,11 @@ k_ext_scan(const ExtJobDev* __restrict__ jobs, int n_jobs, const char* __restric
 
     // forward pass, byte layout first (sw_sse2_byte), word layout on overflow (ssw.c:838-850)
     int word = 0;
-    PassOut f = sw_pass_dispatch<false>(qc, qlen, rc, rlen, 0, 0, match, mismatch, gO, gE, (qlen + 15) / 16, 0, lane);
+    PassOut f = sw_pass_dispatch<false>(qc, qlen, rc, rlen, 0, 0, match, mismatch, gO, gE, (qlen + 15) / 16, 0, lane, variant);
     int score1 = wave_max_i32(f.best);
     if (score1 + mismatch >= 255) {
         word = 1;
-        f = sw_pass_dispatch<false>(qc, qlen, rc, rlen, 0, 0, match, mismatch, gO, gE, (qlen + 7) / 8, 0, lane);
+        f = sw_pass_dispatch<false>(qc, qlen, rc, rlen, 0, 0, match, mismatch, gO, gE, (qlen + 7) / 8, 0, lane, variant);
         score1 = wave_max_i32(f.best);
     }
     int ref_end1, read_end1;
@@ -202,7 +272,7 @@ k_ext_scan(const ExtJobDev* __restrict__ jobs, int n_jobs, const char* __restric
         const int nrow = read_end1 + 1, ncol = ref_end1 + 1;
         const int seg = word ? (nrow + 7) / 8 : (nrow + 15) / 16;
         PassOut b = sw_pass_dispatch<true>(qc, nrow, rc, ncol, read_end1, ref_end1, match, mismatch, gO, gE, seg,
-                                           score1, lane);
+                                           score1, lane, variant);
         const int tcol = wave_min_i32(b.tcol);
         if (tcol == INT_MAX) {
             res.flag = 2;   // reverse max < score1: "may miss a small part"

@@ -10,6 +10,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -20,7 +21,7 @@
 #include "rsa_timer.h"
 
 __global__ void k_ext_scan(const ExtJobDev* jobs, int n_jobs, const char* qbuf, const char* ref, ScanRes* out,
-                           int match, int mismatch, int gO, int gE);
+                           int match, int mismatch, int gO, int gE, int variant);
 __global__ void k_ext_band(const ExtJobDev* jobs, const ScanRes* scan, int n_jobs, const int* idx_list, int job_base,
                            const char* qbuf, const char* ref, uint32_t* cig_pool, rsa_aln* out, uint8_t* scratch,
                            int64_t scr_stride, int arr_cap, int64_t dir_cap, int match, int mismatch, int gO,
@@ -238,6 +239,12 @@ static int64_t band_stride(int arr_cap, int64_t dir_cap) {
     return (s + 255) & ~(int64_t)255;
 }
 
+// k_ext_scan cell bookkeeping variant (RSA_SCAN_V, A/B experiments; same results)
+static int scan_variant() {
+    const char* v = getenv("RSA_SCAN_V");
+    return v ? atoi(v) : 0;
+}
+
 struct ExtStatus {            // device-side counters of one rsa_extend call
     int qcount;               // jobs deferred by k_ext_band16
     int ocount;               // jobs k_ext_band64 could not hold
@@ -305,7 +312,7 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
     L->kt.begin(st, RSA_K_EXT_SCAN);
     hipLaunchKernelGGL(k_ext_scan, dim3((n + 3) / 4), dim3(256), 0, st, L->d_jobs.as<ExtJobDev>(), (int)n,
                        L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(), jb->match, jb->mismatch,
-                       jb->gap_open, jb->gap_extend);
+                       jb->gap_open, jb->gap_extend, scan_variant());
     HIPCHK(hipGetLastError());
     L->kt.end(st);
     // 16 lanes per job for the common narrow bands; the rest queue for 64-lane waves

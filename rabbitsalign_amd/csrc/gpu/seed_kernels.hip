@@ -822,6 +822,119 @@ k_find_nams_w(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __res
 }
 
 // ---------------------------------------------------------------------------
+// k_find_nams_w2: one wavefront per read, everything the sequential merge
+// touches in LDS.
+//   1. lanes (one per query randstrobe) expand their index entries into hits
+//      in parallel: add_to_hits_per_ref's running min_diff filter per
+//      randstrobe, a wave prefix sum places every lane's hits at its offset,
+//      so the hit vector is in the reference's order (nam.cpp:68-85, 781-905)
+//   2. lane 0 inserts the keys into the two robin_hood emulations (LDS) and
+//      runs merge_hits_into_nams over LDS hits / open NAMs (nam.cpp:370-536);
+//      NAMs stream out to global memory
+// Reads with more than FN2_HCAP hits or whose maps would rehash are flagged
+// (flags = 2) for the global-scratch kernel above.
+// ---------------------------------------------------------------------------
+#define FN2_WAVES 4
+#define FN2_HCAP 128
+
+__device__ __forceinline__ int wave_excl_scan(int v, int lane, int& total) {
+    int x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    total = __shfl(x, 63, 64);
+    return x - v;
+}
+
+__global__ void __launch_bounds__(64 * FN2_WAVES)
+k_find_nams_w2(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi,
+               const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, const ReadStat* __restrict__ st,
+               const uint64_t* __restrict__ hoff, int n_reads, SeedIndexParams p, rsa_nam* __restrict__ nam_buf,
+               uint32_t* __restrict__ ncnt, float* __restrict__ nonrep, uint32_t* __restrict__ flags) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_map[FN2_WAVES][2 * FN_MAP_CAP * 9];
+    __shared__ HitD s_hits[FN2_WAVES][FN2_HCAP];
+    __shared__ rsa_nam s_open[FN2_WAVES][FN2_HCAP];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = blockIdx.x * FN2_WAVES + w;
+    if (r >= n_reads) return;                           // whole wave
+    const ReadStat rs = st[r];
+    if (rs.hits_find > FN2_HCAP) {
+        if (lane == 0) { nonrep[r] = rs.found > 0 ? (float)rs.good / (float)rs.found : 1.0f; flags[r] = 2; ncnt[r] = 0; }
+        return;
+    }
+    const int nq = (int)qcnt[r];
+    const uint64_t base = qbase[r];
+    HitD* hits = s_hits[w];
+    int off = 0;
+    for (int i0 = 0; i0 < nq; i0 += 64) {
+        const int i = i0 + lane;
+        int nh = 0;
+        QrsInfo o;
+        rsa_query_randstrobe q;
+        if (i < nq) {
+            o = qi[base + i];
+            if ((o.flags & 1) && !(o.flags & 2)) { nh = (int)o.hits; q = qrs[base + i]; }
+        }
+        int tot;
+        const int at = off + wave_excl_scan(nh, lane, tot);
+        if (nh) {
+            const int qs = (int)q.start, qe = (int)q.end;
+            int min_diff = INT_MAX, h = at;
+            for (uint64_t e = o.pos; e < o.pos + o.count; ++e) {
+                const rsa_ref_randstrobe x = p.rs[e];
+                const int rs0 = (int)x.position;
+                const int re0 = rs0 + (int)(x.packed & 0xFF) + p.k;
+                int d = (qe - qs) - (re0 - rs0);
+                d = d < 0 ? -d : d;
+                if (d <= min_diff) {
+                    HitD hd;
+                    hd.qs = qs; hd.qe = qe; hd.rs = rs0; hd.re = re0;
+                    hd.list = (int32_t)(x.packed >> 8);          // key until lane 0 assigns list ids
+                    hd.pad = q.is_reverse ? 1 : 0;
+                    hits[h++] = hd;
+                    min_diff = d;
+                }
+            }
+        }
+        off += tot;
+    }
+    WSYNC_SEED();
+    if (lane != 0) return;
+    nonrep[r] = rs.found > 0 ? (float)rs.good / (float)rs.found : 1.0f;   // nam.cpp:920
+    const int n_hits = off;
+    DMap m[2];
+    for (int o = 0; o < 2; ++o) {
+        uint8_t* b = s_map[w] + (size_t)o * FN_MAP_CAP * 9;
+        m[o].cap = FN_MAP_CAP;
+        m[o].keys = (uint32_t*)b; m[o].vals = (int32_t*)(b + (size_t)FN_MAP_CAP * 4); m[o].info = b + (size_t)FN_MAP_CAP * 8;
+        m[o].info2 = nullptr; m[o].keys2 = nullptr; m[o].vals2 = nullptr;   // a rehash overflows -> fallback
+        rh_new_reserved(m[o]);
+    }
+    int n_lists = 0, last_o = -1;
+    uint32_t last_key = 0;
+    int32_t last_lid = 0;
+    for (int h = 0; h < n_hits; ++h) {
+        const int orient = hits[h].pad;
+        const uint32_t key = (uint32_t)hits[h].list;
+        if (orient != last_o || key != last_key) {          // operator[] on a present key changes nothing
+            bool ins;
+            last_lid = rh_get_or_insert(m[orient], key, n_lists, ins);
+            if (ins) n_lists++;
+            last_o = orient; last_key = key;
+        }
+        hits[h].list = last_lid | (orient << 30);
+    }
+    if (m[0].overflow || m[1].overflow) { flags[r] = 2; ncnt[r] = 0; return; }
+    rsa_nam* out = nam_buf + hoff[r];
+    int n_out = 0;
+    merge_slow(m[0], 0, hits, n_hits, p.k, s_open[w], out, n_out);
+    merge_slow(m[1], 1, hits, n_hits, p.k, s_open[w], out, n_out);
+    ncnt[r] = (uint32_t)n_out;
+    flags[r] = 0;
+}
+
+// ---------------------------------------------------------------------------
 // k_rescue: find_nams_rescue for listed reads (one lane per read)
 // ---------------------------------------------------------------------------
 struct RescueD { uint64_t pos; uint32_t count, qs, qe, pad; };
@@ -1139,7 +1252,12 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
     const uint32_t chunk = 65536;
     SCHK(hipMemcpyAsync(b.p[B_HOFF], hoff, 8ull * (n + 1), hipMemcpyHostToDevice, st));
     kt.begin(st, RSA_K_FIND_NAMS);
-    if (seed_variant_lane("RSA_FN_WAVE")) {
+    if (!seed_variant_lane("RSA_FN_LANE")) {
+        hipLaunchKernelGGL(k_find_nams_w2, dim3((n + FN2_WAVES - 1) / FN2_WAVES), dim3(64 * FN2_WAVES), 0, st,
+                           DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t),
+                           DP(B_QBASE, uint64_t), DP(B_ST, ReadStat), DP(B_HOFF, uint64_t), (int)n, p,
+                           DP(B_NAM1, rsa_nam), DP(B_NCNT1, uint32_t), DP(B_NONREP, float), DP(B_FLAGS, uint32_t));
+    } else if (seed_variant_lane("RSA_FN_WAVE")) {
         hipLaunchKernelGGL(k_find_nams_w, dim3((n + FN_WAVES - 1) / FN_WAVES), dim3(64 * FN_WAVES), 0, st,
                            DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t),
                            DP(B_QBASE, uint64_t), DP(B_ST, ReadStat), DP(B_HOFF, uint64_t), (int)n, p, DP(B_HITS, HitD),
