@@ -194,33 +194,36 @@ __device__ PassOut sw_pass(const uint8_t* __restrict__ qc, int nrow, const uint8
     return o;
 }
 
-template <bool REV>
+// R = rows per lane; the kernel is instantiated per RMAX so its register
+// allocation (and occupancy) is that of the largest R it can take, not 16.
+template <bool REV, int RMAX, int V>
 __device__ PassOut sw_pass_dispatch(const uint8_t* qc, int nrow, const uint8_t* rc, int ncol, int qend, int rend,
-                                    int match, int mismatch, int gO, int gE, int seg, int terminate, int lane,
-                                    int variant) {
+                                    int match, int mismatch, int gO, int gE, int seg, int terminate, int lane) {
     const int R = (nrow + 63) / 64;
-#define RSA_PASS(N)                                                                                         \
-    return variant ? sw_pass<N, REV>(qc, nrow, rc, ncol, qend, rend, match, mismatch, gO, gE, seg, terminate, lane) \
-                   : sw_pass_v0<N, REV>(qc, nrow, rc, ncol, qend, rend, match, mismatch, gO, gE, seg, terminate, lane)
-    switch (R) {
-        case 0: case 1: RSA_PASS(1);
-        case 2: RSA_PASS(2);
-        case 3: RSA_PASS(3);
-        case 4: RSA_PASS(4);
-        case 5: RSA_PASS(5);
-        case 6: RSA_PASS(6);
-        case 7: RSA_PASS(7);
-        case 8: RSA_PASS(8);
-        case 9: case 10: case 11: case 12: RSA_PASS(12);
-        default: RSA_PASS(16);
+#define RSA_PASS(N)                                                                                              \
+    if constexpr (N <= RMAX) {                                                                                   \
+        if constexpr (V) return sw_pass<N, REV>(qc, nrow, rc, ncol, qend, rend, match, mismatch, gO, gE, seg,      \
+                                                terminate, lane);                                                \
+        else return sw_pass_v0<N, REV>(qc, nrow, rc, ncol, qend, rend, match, mismatch, gO, gE, seg, terminate,  \
+                                       lane);                                                                    \
     }
+    if (R <= 1) { RSA_PASS(1) }
+    if (R == 2) { RSA_PASS(2) }
+    if (R == 3) { RSA_PASS(3) }
+    if (R == 4) { RSA_PASS(4) }
+    if (R <= 6) { RSA_PASS(6) }
+    if (R <= 8) { RSA_PASS(8) }
+    if (R <= 12) { RSA_PASS(12) }
+    RSA_PASS(16)
 #undef RSA_PASS
+    PassOut o{};
+    return o;   // unreachable: the host picks RMAX >= R of every job
 }
 
+template <int RMAX, int V>
 __global__ void __launch_bounds__(64 * SCAN_WAVES)
 k_ext_scan(const ExtJobDev* __restrict__ jobs, int n_jobs, const char* __restrict__ qbuf,
-           const char* __restrict__ ref, ScanRes* __restrict__ out, int match, int mismatch, int gO, int gE,
-           int variant) {
+           const char* __restrict__ ref, ScanRes* __restrict__ out, int match, int mismatch, int gO, int gE) {
     __shared__ uint8_t s_q[SCAN_WAVES][MAXQ_LDS];
     __shared__ uint8_t s_r[SCAN_WAVES][MAXR_LDS];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -250,11 +253,13 @@ k_ext_scan(const ExtJobDev* __restrict__ jobs, int n_jobs, const char* __restric
 
     // forward pass, byte layout first (sw_sse2_byte), word layout on overflow (ssw.c:838-850)
     int word = 0;
-    PassOut f = sw_pass_dispatch<false>(qc, qlen, rc, rlen, 0, 0, match, mismatch, gO, gE, (qlen + 15) / 16, 0, lane, variant);
+    PassOut f = sw_pass_dispatch<false, RMAX, V>(qc, qlen, rc, rlen, 0, 0, match, mismatch, gO, gE, (qlen + 15) / 16, 0,
+                                                    lane);
     int score1 = wave_max_i32(f.best);
     if (score1 + mismatch >= 255) {
         word = 1;
-        f = sw_pass_dispatch<false>(qc, qlen, rc, rlen, 0, 0, match, mismatch, gO, gE, (qlen + 7) / 8, 0, lane, variant);
+        f = sw_pass_dispatch<false, RMAX, V>(qc, qlen, rc, rlen, 0, 0, match, mismatch, gO, gE, (qlen + 7) / 8, 0,
+                                                lane);
         score1 = wave_max_i32(f.best);
     }
     int ref_end1, read_end1;
@@ -271,8 +276,8 @@ k_ext_scan(const ExtJobDev* __restrict__ jobs, int n_jobs, const char* __restric
         // reverse pass (ssw.c:877-893)
         const int nrow = read_end1 + 1, ncol = ref_end1 + 1;
         const int seg = word ? (nrow + 7) / 8 : (nrow + 15) / 16;
-        PassOut b = sw_pass_dispatch<true>(qc, nrow, rc, ncol, read_end1, ref_end1, match, mismatch, gO, gE, seg,
-                                           score1, lane, variant);
+        PassOut b = sw_pass_dispatch<true, RMAX, V>(qc, nrow, rc, ncol, read_end1, ref_end1, match, mismatch, gO,
+                                                    gE, seg, score1, lane);
         const int tcol = wave_min_i32(b.tcol);
         if (tcol == INT_MAX) {
             res.flag = 2;   // reverse max < score1: "may miss a small part"
@@ -853,4 +858,17 @@ k_cigar_compact(rsa_aln* __restrict__ alns, int n_jobs, const uint32_t* __restri
         off += n;
     }
     if (t == CC_THREADS - 1) *total = s_sum[t];
+}
+
+// host-side launcher: RMAX from the longest query of the batch, V = cell
+// bookkeeping variant (0: per cell, 1: per column)
+void launch_ext_scan(int rmax, int variant, dim3 grid, dim3 block, hipStream_t st, const ExtJobDev* jobs, int n,
+                     const char* q, const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE) {
+#define RSA_L(RM, VV) hipLaunchKernelGGL((k_ext_scan<RM, VV>), grid, block, 0, st, jobs, n, q, ref, out, match, mismatch, gO, gE)
+    if (variant) {
+        if (rmax <= 2) RSA_L(2, 1); else if (rmax <= 4) RSA_L(4, 1); else if (rmax <= 8) RSA_L(8, 1); else RSA_L(16, 1);
+    } else {
+        if (rmax <= 2) RSA_L(2, 0); else if (rmax <= 4) RSA_L(4, 0); else if (rmax <= 8) RSA_L(8, 0); else RSA_L(16, 0);
+    }
+#undef RSA_L
 }

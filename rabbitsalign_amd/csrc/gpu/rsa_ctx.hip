@@ -20,8 +20,8 @@
 #include "rsa_seed.h"
 #include "rsa_timer.h"
 
-__global__ void k_ext_scan(const ExtJobDev* jobs, int n_jobs, const char* qbuf, const char* ref, ScanRes* out,
-                           int match, int mismatch, int gO, int gE, int variant);
+void launch_ext_scan(int rmax, int variant, dim3 grid, dim3 block, hipStream_t st, const ExtJobDev* jobs, int n,
+                     const char* q, const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE);
 __global__ void k_ext_band(const ExtJobDev* jobs, const ScanRes* scan, int n_jobs, const int* idx_list, int job_base,
                            const char* qbuf, const char* ref, uint32_t* cig_pool, rsa_aln* out, uint8_t* scratch,
                            int64_t scr_stride, int arr_cap, int64_t dir_cap, int match, int mismatch, int gO,
@@ -267,6 +267,7 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
     ExtJobDev* hj = L->h_jobs.as<ExtJobDev>();
     uint64_t cig_off = 0;
     uint64_t cells = 0, qr_bytes = 0;
+    int rmax = 1;
     for (uint32_t i = 0; i < n; ++i) {
         const rsa_job& s = jb->jobs[i];
         if (s.ref_id < 0 || s.ref_id >= (int)ctx->contig_off.size() - 1 || s.query_offset + s.query_len > jb->queries_len) {
@@ -289,7 +290,10 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
         hj[i].cig_off = cig_off;
         cig_off += (uint64_t)s.query_len + s.ref_len + 8;
         qr_bytes += (uint64_t)s.query_len + s.ref_len;
-        if (s.ref_len <= 2000) cells += (uint64_t)s.query_len * s.ref_len;
+        if (s.ref_len <= 2000) {
+            cells += (uint64_t)s.query_len * s.ref_len;
+            rmax = std::max(rmax, (int)((s.query_len + 63) / 64));
+        }
     }
     HIPCHK(L->d_q.ensure(jb->queries_len + 16));
     HIPCHK(L->d_jobs.ensure(sizeof(ExtJobDev) * n));
@@ -310,9 +314,9 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
     HIPCHK(hipMemsetAsync(L->d_status.p, 0, sizeof(ExtStatus), st));
     L->kt.reset();
     L->kt.begin(st, RSA_K_EXT_SCAN);
-    hipLaunchKernelGGL(k_ext_scan, dim3((n + 3) / 4), dim3(256), 0, st, L->d_jobs.as<ExtJobDev>(), (int)n,
-                       L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(), jb->match, jb->mismatch,
-                       jb->gap_open, jb->gap_extend, scan_variant());
+    launch_ext_scan(rmax, scan_variant(), dim3((n + 3) / 4), dim3(256), st, L->d_jobs.as<ExtJobDev>(), (int)n,
+                    L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(), jb->match, jb->mismatch, jb->gap_open,
+                    jb->gap_extend);
     HIPCHK(hipGetLastError());
     L->kt.end(st);
     // 16 lanes per job for the common narrow bands; the rest queue for 64-lane waves
@@ -338,7 +342,7 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
         HIPCHK(hipMemcpyAsync(L->h_status.p, L->d_status.p, sizeof(ExtStatus), hipMemcpyDeviceToHost, st));
         HIPCHK(hipMemcpyAsync(out->alns, L->d_alns.p, sizeof(rsa_aln) * n, hipMemcpyDeviceToHost, st));
         if (guess) HIPCHK(hipMemcpyAsync(out->cigar_pool, L->d_dense.p, sizeof(uint32_t) * guess, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
+        HIPCHK(stream_wait(st, L->sb.done));
         return RSA_OK;
     };
     // k_cigar_compact rewrites cigar_offset in place: keep the slot offsets for a possible re-run
@@ -350,7 +354,7 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
         // rare: bands the 64-lane kernel cannot hold -> one lane per job, large global scratch
         HIPCHK(L->h_over.ensure(sizeof(int) * n));
         HIPCHK(hipMemcpyAsync(L->h_over.p, L->d_over.p, sizeof(int) * n, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
+        HIPCHK(stream_wait(st, L->sb.done));
         std::vector<int> big;
         for (uint32_t i = 0; i < n; ++i) if (L->h_over.as<int>()[i]) big.push_back((int)i);
         const int64_t bstride = band_stride(BIG_ARR_CAP, BIG_DIR_CAP);
@@ -371,7 +375,7 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
             L->kt.end(st);
         }
         HIPCHK(hipMemcpyAsync(L->h_over.p, L->d_over.p, sizeof(int) * n, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
+        HIPCHK(stream_wait(st, L->sb.done));
         for (int i : big)
             if (L->h_over.as<int>()[i] > 1) { set_err(ctx, "rsa_extend: band scratch exhausted"); return RSA_ERR_NOMEM; }
         if (int rc = compact_and_copy(guess)) return rc;
@@ -380,7 +384,7 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
     if (hs.total > guess) {
         HIPCHK(hipMemcpyAsync(out->cigar_pool + guess, L->d_dense.as<uint32_t>() + guess,
                               sizeof(uint32_t) * (hs.total - guess), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
+        HIPCHK(stream_wait(st, L->sb.done));
     }
     out->cigar_used = hs.total;
     {

@@ -19,6 +19,19 @@ struct SeedBufs {
     size_t cap[24] = {0};
     void* h[8] = {nullptr};
     size_t hcap[8] = {0};
+    hipEvent_t done = nullptr;   // blocking-sync event: the calling thread sleeps instead of spinning
 };
+
+// Wait for everything queued on `s` so far without burning a host core
+// (hipEventBlockingSync); the host pipeline runs more workers than cores.
+inline hipError_t stream_wait(hipStream_t s, hipEvent_t& e) {
+    if (!e) {
+        hipError_t err = hipEventCreateWithFlags(&e, hipEventBlockingSync | hipEventDisableTiming);
+        if (err != hipSuccess) return err;
+    }
+    hipError_t err = hipEventRecord(e, s);
+    if (err != hipSuccess) return err;
+    return hipEventSynchronize(e);
+}
 
 void seed_bufs_release(SeedBufs& b);

@@ -645,40 +645,44 @@ __device__ __forceinline__ uint32_t rh_next_slot(const DMap& m, uint32_t slot) {
     return m.nwb;
 }
 
-// merge_hits_into_nams (nam.cpp:370-536, sort=true), all lists of one orientation
-__device__ void merge_slow(const DMap& m, int orient, const HitD* hits, int n_hits, int k, rsa_nam* open,
-                           rsa_nam* out, int& n_out) {
-    for (uint32_t slot = rh_next_slot(m, 0); slot < m.nwb; slot = rh_next_slot(m, slot + 1)) {
-        const int32_t lid = m.vals[slot] | (orient << 30);
-        const int ref_id = (int)m.keys[slot];
-        int n_open = 0;
-        unsigned prev_q_start = 0;
-        for (int hi = 0; hi < n_hits; ++hi) {
-            const HitD x = hits[hi];
-            if (x.list != lid) continue;
-            bool added = false;
-            for (int o = 0; o < n_open; ++o) {
-                rsa_nam& on = open[o];
-                if (on.query_prev_hit_startpos < x.qs && x.qs <= on.query_end && on.ref_prev_hit_startpos < x.rs &&
-                    x.rs <= on.ref_end) {
-                    if (x.qe > on.query_end && x.re > on.ref_end) {
-                        on.query_end = x.qe; on.ref_end = x.re;
-                        on.query_prev_hit_startpos = x.qs; on.ref_prev_hit_startpos = x.rs;
-                        on.n_hits++; added = true; break;
-                    } else if (x.qe <= on.query_end && x.re <= on.ref_end) {
-                        on.query_prev_hit_startpos = x.qs; on.ref_prev_hit_startpos = x.rs;
-                        on.n_hits++; added = true; break;
-                    }
+// merge_hits_into_nams (nam.cpp:370-536, sort=true) for one hit list (one
+// ref_id x orientation): emits into out[0..), nam_id = local index
+__device__ void merge_one_list(int32_t lid, int ref_id, int orient, const HitD* hits, int n_hits, int k,
+                               rsa_nam* open, rsa_nam* out, int& n_out) {
+    int n_open = 0;
+    unsigned prev_q_start = 0;
+    for (int hi = 0; hi < n_hits; ++hi) {
+        const HitD x = hits[hi];
+        if (x.list != lid) continue;
+        bool added = false;
+        for (int o = 0; o < n_open; ++o) {
+            rsa_nam& on = open[o];
+            if (on.query_prev_hit_startpos < x.qs && x.qs <= on.query_end && on.ref_prev_hit_startpos < x.rs &&
+                x.rs <= on.ref_end) {
+                if (x.qe > on.query_end && x.re > on.ref_end) {
+                    on.query_end = x.qe; on.ref_end = x.re;
+                    on.query_prev_hit_startpos = x.qs; on.ref_prev_hit_startpos = x.rs;
+                    on.n_hits++; added = true; break;
+                } else if (x.qe <= on.query_end && x.re <= on.ref_end) {
+                    on.query_prev_hit_startpos = x.qs; on.ref_prev_hit_startpos = x.rs;
+                    on.n_hits++; added = true; break;
                 }
             }
-            if (!added) open[n_open++] = nam_from_hit(x, ref_id, orient);
-            if ((unsigned)x.qs > prev_q_start + (unsigned)k) {
-                flush_passed(open, n_open, x.qs, out, n_out);
-                prev_q_start = (unsigned)x.qs;
-            }
         }
-        for (int o = 0; o < n_open; ++o) nam_emit(out, n_out, open[o]);
+        if (!added) open[n_open++] = nam_from_hit(x, ref_id, orient);
+        if ((unsigned)x.qs > prev_q_start + (unsigned)k) {
+            flush_passed(open, n_open, x.qs, out, n_out);
+            prev_q_start = (unsigned)x.qs;
+        }
     }
+    for (int o = 0; o < n_open; ++o) nam_emit(out, n_out, open[o]);
+}
+
+// all lists of one orientation, in robin_hood slot order
+__device__ void merge_slow(const DMap& m, int orient, const HitD* hits, int n_hits, int k, rsa_nam* open,
+                           rsa_nam* out, int& n_out) {
+    for (uint32_t slot = rh_next_slot(m, 0); slot < m.nwb; slot = rh_next_slot(m, slot + 1))
+        merge_one_list(m.vals[slot] | (orient << 30), (int)m.keys[slot], orient, hits, n_hits, k, open, out, n_out);
 }
 
 // merge_hits_into_nams_fast (nam.cpp:117-366, sort=false)
@@ -855,6 +859,9 @@ k_find_nams_w2(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __re
     __shared__ __attribute__((aligned(16))) uint8_t s_map[FN2_WAVES][2 * FN_MAP_CAP * 9];
     __shared__ HitD s_hits[FN2_WAVES][FN2_HCAP];
     __shared__ rsa_nam s_open[FN2_WAVES][FN2_HCAP];
+    __shared__ rsa_nam s_out[FN2_WAVES][FN2_HCAP];
+    __shared__ int2 s_order[FN2_WAVES][64];
+    __shared__ int s_ctl[FN2_WAVES][4];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int r = blockIdx.x * FN2_WAVES + w;
     if (r >= n_reads) return;                           // whole wave
@@ -900,38 +907,100 @@ k_find_nams_w2(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __re
         off += tot;
     }
     WSYNC_SEED();
-    if (lane != 0) return;
-    nonrep[r] = rs.found > 0 ? (float)rs.good / (float)rs.found : 1.0f;   // nam.cpp:920
     const int n_hits = off;
     DMap m[2];
     for (int o = 0; o < 2; ++o) {
-        uint8_t* b = s_map[w] + (size_t)o * FN_MAP_CAP * 9;
+        uint8_t* bm = s_map[w] + (size_t)o * FN_MAP_CAP * 9;
         m[o].cap = FN_MAP_CAP;
-        m[o].keys = (uint32_t*)b; m[o].vals = (int32_t*)(b + (size_t)FN_MAP_CAP * 4); m[o].info = b + (size_t)FN_MAP_CAP * 8;
+        m[o].keys = (uint32_t*)bm; m[o].vals = (int32_t*)(bm + (size_t)FN_MAP_CAP * 4);
+        m[o].info = bm + (size_t)FN_MAP_CAP * 8;
         m[o].info2 = nullptr; m[o].keys2 = nullptr; m[o].vals2 = nullptr;   // a rehash overflows -> fallback
-        rh_new_reserved(m[o]);
     }
-    int n_lists = 0, last_o = -1;
-    uint32_t last_key = 0;
-    int32_t last_lid = 0;
-    for (int h = 0; h < n_hits; ++h) {
-        const int orient = hits[h].pad;
-        const uint32_t key = (uint32_t)hits[h].list;
-        if (orient != last_o || key != last_key) {          // operator[] on a present key changes nothing
-            bool ins;
-            last_lid = rh_get_or_insert(m[orient], key, n_lists, ins);
-            if (ins) n_lists++;
-            last_o = orient; last_key = key;
+    if (lane == 0) {
+        nonrep[r] = rs.found > 0 ? (float)rs.good / (float)rs.found : 1.0f;   // nam.cpp:920
+        rh_new_reserved(m[0]);
+        rh_new_reserved(m[1]);
+        int n_lists = 0, last_o = -1;
+        uint32_t last_key = 0;
+        int32_t last_lid = 0;
+        for (int h = 0; h < n_hits; ++h) {
+            const int orient = hits[h].pad;
+            const uint32_t key = (uint32_t)hits[h].list;
+            if (orient != last_o || key != last_key) {      // operator[] on a present key changes nothing
+                bool ins;
+                last_lid = rh_get_or_insert(m[orient], key, n_lists, ins);
+                if (ins) n_lists++;
+                last_o = orient; last_key = key;
+            }
+            hits[h].list = last_lid | (orient << 30);
         }
-        hits[h].list = last_lid | (orient << 30);
+        s_ctl[w][0] = (m[0].overflow || m[1].overflow) ? 1 : 0;
+        s_ctl[w][1] = (int)m[0].nwb;
+        s_ctl[w][2] = (int)m[1].nwb;
     }
-    if (m[0].overflow || m[1].overflow) { flags[r] = 2; ncnt[r] = 0; return; }
+    WSYNC_SEED();
+    if (s_ctl[w][0]) {
+        if (lane == 0) { flags[r] = 2; ncnt[r] = 0; }
+        return;
+    }
+    // list order = occupied slots of the fwd map, then of the rc map (robin_hood iteration order)
+    int2* order = s_order[w];
+    int nl = 0;
+    for (int o = 0; o < 2; ++o) {
+        const int nwb = s_ctl[w][1 + o];
+        const uint32_t word = lane * 4 < nwb ? ((const uint32_t*)m[o].info)[lane] : 0u;
+        uint64_t mk[4];
+        int occ = 0;
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+            const bool on = ((word >> (8 * bb)) & 0xFFu) != 0 && lane * 4 + bb < nwb;
+            mk[bb] = __ballot(on);
+            occ += __popcll(mk[bb]);
+        }
+        const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+        int rank = __popcll(mk[0] & lt) + __popcll(mk[1] & lt) + __popcll(mk[2] & lt) + __popcll(mk[3] & lt);
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+            if ((mk[bb] >> lane) & 1ull) {
+                const int slot = lane * 4 + bb;
+                if (nl + rank < 64) order[nl + rank] = make_int2(m[o].vals[slot] | (o << 30), (int)m[o].keys[slot]);
+                rank++;
+            }
+        }
+        nl += occ;
+    }
+    WSYNC_SEED();
     rsa_nam* out = nam_buf + hoff[r];
+    if (nl > 64) {                                       // many lists: serial merge on lane 0
+        if (lane == 0) {
+            int n_out = 0;
+            merge_slow(m[0], 0, hits, n_hits, p.k, s_open[w], out, n_out);
+            merge_slow(m[1], 1, hits, n_hits, p.k, s_open[w], out, n_out);
+            ncnt[r] = (uint32_t)n_out;
+            flags[r] = 0;
+        }
+        return;
+    }
+    // one lane per list: hits of the list, open/out NAM space at the list's hit offset
+    int cnt = 0;
+    int2 li = make_int2(0, 0);
+    if (lane < nl) {
+        li = order[lane];
+        for (int h = 0; h < n_hits; ++h) cnt += hits[h].list == li.x;
+    }
+    int tot;
+    const int hb = wave_excl_scan(cnt, lane, tot);
     int n_out = 0;
-    merge_slow(m[0], 0, hits, n_hits, p.k, s_open[w], out, n_out);
-    merge_slow(m[1], 1, hits, n_hits, p.k, s_open[w], out, n_out);
-    ncnt[r] = (uint32_t)n_out;
-    flags[r] = 0;
+    if (lane < nl)
+        merge_one_list(li.x, li.y, (li.x >> 30) & 1, hits, n_hits, p.k, s_open[w] + hb, s_out[w] + hb, n_out);
+    int total;
+    const int ob = wave_excl_scan(n_out, lane, total);
+    for (int i = 0; i < n_out; ++i) {
+        rsa_nam x = s_out[w][hb + i];
+        x.nam_id = ob + i;                                // nam_id = position in the read's NAM vector
+        out[ob + i] = x;
+    }
+    if (lane == 0) { ncnt[r] = (uint32_t)total; flags[r] = 0; }
 }
 
 // ---------------------------------------------------------------------------
@@ -1093,6 +1162,8 @@ void seed_bufs_release(SeedBufs& b) {
     for (int i = 0; i < 8; ++i) if (b.h[i]) (void)hipHostFree(b.h[i]);
     for (int i = 0; i < 24; ++i) { b.p[i] = nullptr; b.cap[i] = 0; }
     for (int i = 0; i < 8; ++i) { b.h[i] = nullptr; b.hcap[i] = 0; }
+    if (b.done) (void)hipEventDestroy(b.done);
+    b.done = nullptr;
 }
 
 static hipError_t dens(SeedBufs& b, int i, size_t bytes) {
@@ -1194,7 +1265,7 @@ int seed_randstrobes_run(SeedBufs& b, hipStream_t st, const SeedIndexParams& p, 
     if (rc) return rc;
     std::vector<uint32_t> cnt(n);
     SCHK(hipMemcpyAsync(cnt.data(), b.p[B_QCNT], 4ull * n, hipMemcpyDeviceToHost, st));
-    SCHK(hipStreamSynchronize(st));
+    SCHK(stream_wait(st, b.done));
     uint64_t tot = 0;
     for (uint32_t i = 0; i < n; ++i) { out->offsets[i] = tot; tot += cnt[i]; }
     out->offsets[n] = tot;
@@ -1202,7 +1273,7 @@ int seed_randstrobes_run(SeedBufs& b, hipStream_t st, const SeedIndexParams& p, 
     if (tot > out->capacity) { err = "rsa_randstrobes: output too small"; return RSA_ERR_CAPACITY; }
     std::vector<rsa_query_randstrobe> all(qbase[n] + 1);
     SCHK(hipMemcpyAsync(all.data(), b.p[B_QRS], sizeof(rsa_query_randstrobe) * qbase[n], hipMemcpyDeviceToHost, st));
-    SCHK(hipStreamSynchronize(st));
+    SCHK(stream_wait(st, b.done));
     for (uint32_t i = 0; i < n; ++i)
         memcpy(out->out + out->offsets[i], all.data() + qbase[i], sizeof(rsa_query_randstrobe) * cnt[i]);
     return RSA_OK;
@@ -1225,7 +1296,7 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
     SCHK(hipMemcpyAsync(b.h[H_ST], b.p[B_ST], sizeof(ReadStat) * n, hipMemcpyDeviceToHost, st));
     SCHK(hens(b, H_CNT, 4ull * n));
     SCHK(hipMemcpyAsync(b.h[H_CNT], b.p[B_QCNT], 4ull * n, hipMemcpyDeviceToHost, st));
-    SCHK(hipStreamSynchronize(st));
+    SCHK(stream_wait(st, b.done));
     const ReadStat* hs = HP(H_ST, ReadStat);
     SCHK(hens(b, H_HOFF, 8ull * (n + 1)));
     uint64_t* hoff = HP(H_HOFF, uint64_t);
@@ -1278,7 +1349,7 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
     SCHK(hens(b, H_FLAGS, 4ull * n));
     SCHK(hipMemcpyAsync(b.h[H_FLAGS], b.p[B_FLAGS], 4ull * n, hipMemcpyDeviceToHost, st));
     SCHK(hipMemcpyAsync(b.h[H_CNT], b.p[B_NCNT1], 4ull * n, hipMemcpyDeviceToHost, st));
-    SCHK(hipStreamSynchronize(st));
+    SCHK(stream_wait(st, b.done));
     // rare: reads whose maps rehash past the small table -> big-map pass
     std::vector<int> big;
     for (uint32_t i = 0; i < n; ++i) if (HP(H_FLAGS, uint32_t)[i] & 2u) big.push_back((int)i);
@@ -1301,12 +1372,12 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
         }
         SCHK(hipMemcpyAsync(b.h[H_FLAGS], b.p[B_FLAGS], 4ull * n, hipMemcpyDeviceToHost, st));
         SCHK(hipMemcpyAsync(b.h[H_CNT], b.p[B_NCNT1], 4ull * n, hipMemcpyDeviceToHost, st));
-        SCHK(hipStreamSynchronize(st));
+        SCHK(stream_wait(st, b.done));
         for (int i : big) if (HP(H_FLAGS, uint32_t)[i] & 2u) { err = "rsa_seed: robin_hood emulation overflow"; return RSA_ERR_NOMEM; }
     }
     // nonrepetitive fraction to host
     SCHK(hipMemcpyAsync(out->nonrepetitive_fraction, b.p[B_NONREP], 4ull * n, hipMemcpyDeviceToHost, st));
-    SCHK(hipStreamSynchronize(st));
+    SCHK(stream_wait(st, b.done));
     // rescue decision (aln.cpp:1954-1962)
     std::vector<int> resc;
     std::vector<uint32_t> n1(HP(H_CNT, uint32_t), HP(H_CNT, uint32_t) + n);
@@ -1347,7 +1418,7 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
             kt.end(st);
         }
         SCHK(hipMemcpyAsync(b.h[H_FLAGS], b.p[B_FLAGS], 4ull * n, hipMemcpyDeviceToHost, st));
-        SCHK(hipStreamSynchronize(st));
+        SCHK(stream_wait(st, b.done));
         std::vector<int> bigr;
         for (int i : resc) if (HP(H_FLAGS, uint32_t)[i] & 4u) bigr.push_back(i);
         if (!bigr.empty()) {
@@ -1368,12 +1439,12 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
                 kt.end(st);
             }
             SCHK(hipMemcpyAsync(b.h[H_FLAGS], b.p[B_FLAGS], 4ull * n, hipMemcpyDeviceToHost, st));
-            SCHK(hipStreamSynchronize(st));
+            SCHK(stream_wait(st, b.done));
             for (int i : bigr) if (HP(H_FLAGS, uint32_t)[i] & 4u) { err = "rsa_seed: rescue map overflow"; return RSA_ERR_NOMEM; }
         }
         SCHK(hens(b, H_CNT2, 4ull * n));
         SCHK(hipMemcpyAsync(b.h[H_CNT2], b.p[B_NCNT2], 4ull * n, hipMemcpyDeviceToHost, st));
-        SCHK(hipStreamSynchronize(st));
+        SCHK(stream_wait(st, b.done));
         for (int i : resc) n2[i] = HP(H_CNT2, uint32_t)[i];
     } else {
         SCHK(dens(b, B_ROFF2, 8ull * (n + 1)));
@@ -1401,7 +1472,7 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
     SCHK(hipGetLastError());
     kt.end(st);
     if (total) SCHK(hipMemcpyAsync(out->nams, b.p[B_OUT], sizeof(rsa_nam) * total, hipMemcpyDeviceToHost, st));
-    SCHK(hipStreamSynchronize(st));
+    SCHK(stream_wait(st, b.done));
     // counters and algorithmic bytes (DESIGN.md "Kernels")
     uint64_t n1_tot = 0, n2_tot = 0, resc_q = 0, resc_scan = 0, resc_hits = 0;
     for (uint32_t i = 0; i < n; ++i) n1_tot += n1[i];

@@ -13,7 +13,10 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <climits>
 #include <condition_variable>
+#include <cstdint>
+#include <exception>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -56,6 +59,7 @@ struct PeChunk {
     std::vector<Record> r1, r2;               // upper-cased copies (pc.cpp:1586-1587)
     std::vector<std::string> rc1, rc2;        // their reverse complements, computed once
     std::vector<AlignTmpRes> res;
+    SeedBatchOut seeds;                       // engine output of pe_seed
     std::minstd_rand rng;
     AlignmentStatistics stats;
     PhaseTimes times;
@@ -79,19 +83,26 @@ void pe_load(PeChunk& c, const std::vector<Record>& a, const std::vector<Record>
     c.res.resize(c.r1.size());
 }
 
-// part() of every pair in chunk order (pc.cpp:1739-1766), seeding batched on the engine
-void pe_part(PeChunk& c, Engine& eng, const MapContext& mc, InsertSizeDistribution& isize) {
-    c.rng.seed((unsigned)c.index);
+// Seeding of a loaded chunk (randstrobes + find_nams + rescue on the engine).
+// Independent of the insert-size state, so it can run ahead of part().
+void pe_seed(PeChunk& c, Engine& eng, const MapContext& mc) {
     const size_t n = c.r1.size();
     if (n == 0) return;
     std::vector<const std::string*> reads;
     reads.reserve(2 * n);
     for (size_t i = 0; i < n; ++i) { reads.push_back(&c.r1[i].seq); reads.push_back(&c.r2[i].seq); }
-    SeedBatchOut so;
-    auto t = Clock::now();
-    eng.seed(reads, mc.mparams.rescue_level, (unsigned)mc.mparams.rescue_cutoff, so);
+    const auto t = Clock::now();
+    eng.seed(reads, mc.mparams.rescue_level, (unsigned)mc.mparams.rescue_cutoff, c.seeds);
     c.times.seed += since(t);
-    t = Clock::now();
+}
+
+// part() of every pair in chunk order (pc.cpp:1739-1766) on the seeded chunk
+void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize) {
+    c.rng.seed((unsigned)c.index);
+    const size_t n = c.r1.size();
+    if (n == 0) return;
+    const SeedBatchOut& so = c.seeds;
+    const auto t = Clock::now();
     for (size_t i = 0; i < n; ++i) {
         std::vector<Nam> nams[2];
         bool rescued[2];
@@ -104,6 +115,7 @@ void pe_part(PeChunk& c, Engine& eng, const MapContext& mc, InsertSizeDistributi
         align_PE_read_part(c.res[i], c.r1[i], c.r2[i], read1, read2, nams, rescued, c.stats, isize, mc, c.rng);
         c.stats.n_reads += 2;
     }
+    c.seeds = SeedBatchOut();
     c.times.part += since(t);
 }
 
@@ -137,92 +149,180 @@ void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistributio
 
 }  // namespace
 
+// Chunks flow through three stages:
+//   load + seed   any order, any worker, up to `window` chunks ahead (needs no
+//                 insert-size state, so it also fills the sequential phase)
+//   sequential    the reference's single-worker timeline (part(N) between
+//                 get_str(N-1) and store(N-1)) until the estimate freezes
+//   parallel      part, get_str, extend, store, last per chunk on any worker
+// Every GPU wait sleeps (blocking-sync events), so a worker waiting on the
+// engine leaves its core to the others.
 PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<Record>& r2, Engine& eng,
                                const MapContext& mc, const PipelineOptions& opt, SamSink sink, void* user) {
-    auto t0 = std::chrono::steady_clock::now();
+    const auto t0 = Clock::now();
     PipelineResult result;
     OrderedSink os{sink, user, opt.digest};
     const size_t chunk = (size_t)std::max(1, opt.chunk_size);
     const size_t n_chunks = (r1.size() + chunk - 1) / chunk;
-    InsertSizeDistribution isize;
-    std::vector<SwJob> jobs;
-    std::vector<AlignmentInfo> infos;
-    // ---- single-worker timeline until the insert-size estimate freezes ----
-    auto pre = std::make_unique<PeChunk>();
-    size_t next_chunk = 0;
     if (n_chunks == 0) return result;
-    pe_load(*pre, r1, r2, next_chunk++, chunk);
-    pe_part(*pre, eng, mc, isize);
-    while (!isize.frozen() && next_chunk <= n_chunks) {
-        pe_get_str(*pre, mc, isize.mu, isize.sigma, jobs);
-        auto cur = std::make_unique<PeChunk>();
-        const bool have = next_chunk < n_chunks;
-        if (have) {
-            pe_load(*cur, r1, r2, next_chunk, chunk);
-            pe_part(*cur, eng, mc, isize);
+    const int T = std::max(1, opt.threads);
+    const size_t window = 2 * (size_t)T + 2;
+
+    std::mutex m;
+    std::condition_variable cv;
+    std::map<size_t, std::unique_ptr<PeChunk>> seeded;   // stage 1 done
+    size_t next_seed = 0;          // next chunk index to claim for stage 1
+    size_t consumed = 0;           // chunks handed past stage 1
+    bool frozen = false, done = false;
+    size_t next_par = 0;           // next chunk for the parallel stage (valid once frozen)
+    std::unique_ptr<PeChunk> handed;                     // part() done in the sequential phase
+    InsertSizeDistribution isize, frozen_isize;
+    std::exception_ptr failure;
+    AlignmentStatistics stats_all;
+    PhaseTimes phases_all;
+
+    auto stage1 = [&](size_t idx) {
+        auto c = std::make_unique<PeChunk>();
+        const auto t = Clock::now();
+        pe_load(*c, r1, r2, idx, chunk);
+        c->times.load += since(t);
+        pe_seed(*c, eng, mc);
+        return c;
+    };
+    // chunk idx after stage 1: from the prefetch map, or loaded + seeded here
+    auto acquire = [&](size_t idx) -> std::unique_ptr<PeChunk> {
+        std::unique_lock<std::mutex> g(m);
+        if (idx >= next_seed) {                 // nobody claimed it yet
+            next_seed = idx + 1;
+            g.unlock();
+            auto c = stage1(idx);
+            g.lock();
+            consumed++;
+            cv.notify_all();
+            return c;
         }
-        next_chunk++;
+        cv.wait(g, [&] { return seeded.count(idx) || failure; });
+        if (failure) return nullptr;
+        auto c = std::move(seeded[idx]);
+        seeded.erase(idx);
+        consumed++;
+        cv.notify_all();
+        return c;
+    };
+    auto finish = [&](PeChunk& c, const InsertSizeDistribution& est, std::vector<SwJob>& jobs,
+                      std::vector<AlignmentInfo>& infos) {
+        pe_get_str(c, mc, est.mu, est.sigma, jobs);
         const auto te = Clock::now();
         eng.extend(jobs, mc.aparams, infos);
-        pre->times.extend += since(te);
-        pre->stats.tot_aligner_calls += jobs.size();
+        c.times.extend += since(te);
+        c.stats.tot_aligner_calls += jobs.size();
         std::string out;
-        pe_store_last(*pre, mc, isize, infos, opt.rg_id, out);
-        os.put(pre->index, std::move(out));
-        result.stats.add(pre->stats);
-        result.phases.add(pre->times);
-        pre->times = PhaseTimes();
-        if (!have) { pre.reset(); break; }
-        pre = std::move(cur);
-    }
-    result.phases.sequential = since(t0);
-    // ---- frozen: chunk-parallel ----
-    if (pre || next_chunk < n_chunks) {
-        const InsertSizeDistribution frozen = isize;
-        std::mutex stat_m;
-        std::atomic<size_t> next{next_chunk};
-        std::unique_ptr<PeChunk> handed = std::move(pre);   // part() already done, rng continues
-        std::mutex hand_m;
-        auto worker = [&]() {
-            std::vector<SwJob> wj;
-            std::vector<AlignmentInfo> wi;
-            AlignmentStatistics local;
-            PhaseTimes lt;
+        pe_store_last(c, mc, est, infos, opt.rg_id, out);
+        const auto tp = Clock::now();
+        os.put(c.index, std::move(out));
+        c.times.output += since(tp);
+    };
+
+    auto worker = [&](bool leader) {
+        std::vector<SwJob> jobs;
+        std::vector<AlignmentInfo> infos;
+        AlignmentStatistics local;
+        PhaseTimes lt;
+        try {
+            if (leader) {
+                // ---- single-worker timeline until the insert-size estimate freezes ----
+                auto pre = acquire(0);
+                if (!pre) return;
+                pe_part(*pre, mc, isize);
+                size_t next = 1;
+                for (;;) {
+                    if (isize.frozen() || next > n_chunks) break;
+                    pe_get_str(*pre, mc, isize.mu, isize.sigma, jobs);
+                    std::unique_ptr<PeChunk> cur;
+                    if (next < n_chunks) {
+                        cur = acquire(next);
+                        if (!cur) return;
+                        pe_part(*cur, mc, isize);
+                    }
+                    next++;
+                    const auto te = Clock::now();
+                    eng.extend(jobs, mc.aparams, infos);
+                    pre->times.extend += since(te);
+                    pre->stats.tot_aligner_calls += jobs.size();
+                    std::string out;
+                    pe_store_last(*pre, mc, isize, infos, opt.rg_id, out);
+                    os.put(pre->index, std::move(out));
+                    local.add(pre->stats);
+                    lt.add(pre->times);
+                    if (!cur) { pre.reset(); break; }
+                    pre = std::move(cur);
+                }
+                lt.sequential = since(t0);
+                std::lock_guard<std::mutex> g(m);
+                frozen = true;
+                frozen_isize = isize;
+                handed = std::move(pre);                 // may be null: everything was sequential
+                next_par = std::min(next, n_chunks);
+                if (next_par >= n_chunks && !handed) done = true;
+                cv.notify_all();
+            }
+            // ---- shared loop: parallel stage first, prefetch when it has nothing ----
             for (;;) {
                 std::unique_ptr<PeChunk> c;
+                size_t idx = SIZE_MAX, pf = SIZE_MAX;
                 {
-                    std::lock_guard<std::mutex> g(hand_m);
-                    if (handed) c = std::move(handed);
+                    std::unique_lock<std::mutex> g(m);
+                    for (;;) {
+                        if (failure || done) break;
+                        if (frozen && handed) { c = std::move(handed); break; }
+                        if (frozen && next_par < n_chunks) { idx = next_par++; break; }
+                        if (next_seed < n_chunks && next_seed < consumed + window) { pf = next_seed++; break; }
+                        if (frozen && next_par >= n_chunks) { done = true; cv.notify_all(); break; }
+                        cv.wait(g);
+                    }
                 }
-                if (!c) {
-                    size_t idx = next.fetch_add(1);
-                    if (idx >= n_chunks) break;
-                    c = std::make_unique<PeChunk>();
-                    pe_load(*c, r1, r2, idx, chunk);
-                    InsertSizeDistribution est = frozen;
-                    pe_part(*c, eng, mc, est);
+                if (c) {                                    // part() already done
+                    finish(*c, frozen_isize, jobs, infos);
+                    local.add(c->stats);
+                    lt.add(c->times);
+                    continue;
                 }
-                pe_get_str(*c, mc, frozen.mu, frozen.sigma, wj);
-                const auto te = Clock::now();
-                eng.extend(wj, mc.aparams, wi);
-                c->times.extend += since(te);
-                c->stats.tot_aligner_calls += wj.size();
-                std::string out;
-                pe_store_last(*c, mc, frozen, wi, opt.rg_id, out);
-                os.put(c->index, std::move(out));
-                local.add(c->stats);
-                lt.add(c->times);
+                if (idx != SIZE_MAX) {
+                    c = acquire(idx);
+                    if (!c) break;
+                    InsertSizeDistribution est = frozen_isize;
+                    pe_part(*c, mc, est);
+                    finish(*c, frozen_isize, jobs, infos);
+                    local.add(c->stats);
+                    lt.add(c->times);
+                    continue;
+                }
+                if (pf != SIZE_MAX) {
+                    auto s1 = stage1(pf);
+                    std::lock_guard<std::mutex> g(m);
+                    seeded.emplace(pf, std::move(s1));
+                    cv.notify_all();
+                    continue;
+                }
+                break;
             }
-            std::lock_guard<std::mutex> g(stat_m);
-            result.stats.add(local);
-            result.phases.add(lt);
-        };
-        std::vector<std::thread> ws;
-        const int T = std::max(1, opt.threads);
-        for (int t = 0; t < T; ++t) ws.emplace_back(worker);
-        for (auto& w : ws) w.join();
-    }
-    result.map_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        } catch (...) {
+            std::lock_guard<std::mutex> g(m);
+            if (!failure) failure = std::current_exception();
+            cv.notify_all();
+        }
+        std::lock_guard<std::mutex> g(m);
+        stats_all.add(local);
+        phases_all.add(lt);
+    };
+    std::vector<std::thread> ws;
+    for (int t = 1; t < T; ++t) ws.emplace_back(worker, false);
+    worker(true);
+    for (auto& w : ws) w.join();
+    if (failure) std::rethrow_exception(failure);
+    result.stats = stats_all;
+    result.phases = phases_all;
+    result.map_seconds = since(t0);
     result.sam_bytes = os.bytes;
     result.sam_digest = os.total;
     return result;

@@ -321,10 +321,10 @@ struct SamDigest {
 
 // thread-summed seconds per phase (instrumentation of the host pipeline)
 struct PhaseTimes {
-    double seed = 0, extend = 0, part = 0, collect = 0, last = 0, sequential = 0;
+    double seed = 0, extend = 0, part = 0, collect = 0, last = 0, sequential = 0, load = 0, output = 0;
     void add(const PhaseTimes& o) {
         seed += o.seed; extend += o.extend; part += o.part; collect += o.collect; last += o.last;
-        sequential += o.sequential;
+        sequential += o.sequential; load += o.load; output += o.output;
     }
 };
 
