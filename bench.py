@@ -58,12 +58,30 @@ def host_cores() -> int:
     return max(1, n)
 
 
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "latest_traffic.json")
+
+
+def pmc_traffic(symbol: str):
+    """HBM bytes per launch of `symbol` from the committed rocprofv3 PMC summary
+    (scripts/prof_summary.py: 2 x FETCH_SIZE + WRITE_SIZE), or None."""
+    try:
+        with open(TRAFFIC_JSON) as f:
+            t = json.load(f)
+        v = t["traffic_per_launch"].get(symbol)
+        return (round(v["bytes"], 1) if v and v.get("bytes") is not None else None), t.get("source")
+    except (OSError, ValueError, KeyError):
+        return None, None
+
+
 def roofline(ks: dict) -> dict:
     """Roofline object for the kernel with the largest total device time.
 
     achieved = algorithmic bytes per launch / average launch duration, both
     from the HIP events recorded around every launch on its own stream.
+    traffic = PMC-measured HBM bytes per launch of the same kernel (committed
+    profile), so traffic / alg_bytes_per_launch is the over-fetch factor.
     """
+    from rabbitsalign_amd.native import KERNEL_SYMBOLS
     kern = ks["kernels"]
     name = max(kern, key=lambda k: kern[k]["ms"])
     k = kern[name]
@@ -73,11 +91,16 @@ def roofline(ks: dict) -> dict:
     per_launch_bytes = k["alg_bytes"] / k["launches"]
     avg_ms = k["ms"] / k["launches"]
     achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9
-    from rabbitsalign_amd.native import KERNEL_SYMBOLS
-    return {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
-            "kernel": KERNEL_SYMBOLS[name], "alg_bytes_per_launch": round(per_launch_bytes, 1),
-            "avg_launch_us": round(avg_ms * 1e3, 3), "launches": k["launches"]}
+    sym = KERNEL_SYMBOLS[name]
+    traffic, src = pmc_traffic(sym)
+    out = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+           "kernel": sym, "alg_bytes_per_launch": round(per_launch_bytes, 1),
+           "avg_launch_us": round(avg_ms * 1e3, 3), "launches": k["launches"], "traffic_source": src}
+    if name == "ext_scan" and ks.get("dp_cells"):
+        # the DP scan is integer-VALU bound; cells/s is its natural throughput figure
+        out["dp_gcells_per_s"] = round(ks["dp_cells"] / (k["ms"] * 1e-3) / 1e9, 2)
+    return out
 
 
 def kernel_table(ks: dict) -> dict:
@@ -96,7 +119,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="pe150_3g", choices=sorted(WORKLOADS))
-    ap.add_argument("--pairs", type=int, default=500_000, help="pairs (SE: reads) per step per GPU")
+    ap.add_argument("--pairs", type=int, default=1_000_000,
+                    help="pairs (SE: reads) per step per GPU (SURVEY.md §8d: 10^6 pairs per config)")
     ap.add_argument("--threads", type=int, default=0, help="host pipeline threads (0: all host cores, max 32)")
     ap.add_argument("--chunk-size", type=int, default=10000)
     ap.add_argument("--ref-seed", type=int, default=1)

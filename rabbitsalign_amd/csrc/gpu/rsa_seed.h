@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "../../../include/rsa_gpu.h"
 
 struct SeedIndexParams {
@@ -25,6 +26,8 @@ struct SeedBufs {
 // Wait for everything queued on `s` so far without burning a host core
 // (hipEventBlockingSync); the host pipeline runs more workers than cores.
 inline hipError_t stream_wait(hipStream_t s, hipEvent_t& e) {
+    static const bool spin = [] { const char* v = getenv("RSA_SPIN_WAIT"); return v && v[0] == '1'; }();
+    if (spin) return hipStreamSynchronize(s);
     if (!e) {
         hipError_t err = hipEventCreateWithFlags(&e, hipEventBlockingSync | hipEventDisableTiming);
         if (err != hipSuccess) return err;

@@ -14,6 +14,7 @@
 #include <atomic>
 #include <chrono>
 #include <climits>
+#include <cstdlib>
 #include <condition_variable>
 #include <cstdint>
 #include <exception>
@@ -166,7 +167,9 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
     const size_t n_chunks = (r1.size() + chunk - 1) / chunk;
     if (n_chunks == 0) return result;
     const int T = std::max(1, opt.threads);
-    const size_t window = 2 * (size_t)T + 2;
+    // prefetch depth (RSA_PREFETCH chunks, default 2T+2; 0 = every worker seeds its own chunk)
+    const char* pf_env = getenv("RSA_PREFETCH");
+    const size_t window = pf_env ? (size_t)atol(pf_env) : 2 * (size_t)T + 2;
 
     std::mutex m;
     std::condition_variable cv;
