@@ -101,6 +101,9 @@ __device__ PassOut sw_pass_v0(const uint8_t* __restrict__ qc, int nrow, const ui
             const int m = wave_min_i32(tcol);
             if (m != INT_MAX && s >= m + lanes_used - 1) break;
         }
+        // forward byte pass: once the running max reaches the overflow bound
+        // the word pass recomputes everything, so the rest is moot (ssw.c:846-849)
+        if (!REV && terminate > 0 && (s & 7) == 7 && wave_max_i32(best) >= terminate) break;
     }
     PassOut o;
     o.best = best; o.col = bcol; o.row = brow; o.tcol = tcol; o.trow = trow;
@@ -188,6 +191,9 @@ __device__ PassOut sw_pass(const uint8_t* __restrict__ qc, int nrow, const uint8
             const int m = wave_min_i32(tcol);
             if (m != INT_MAX && s >= m + lanes_used - 1) break;
         }
+        // forward byte pass: once the running max reaches the overflow bound
+        // the word pass recomputes everything, so the rest is moot (ssw.c:846-849)
+        if (!REV && terminate > 0 && (s & 7) == 7 && wave_max_i32(best) >= terminate) break;
     }
     PassOut o;
     o.best = best; o.col = bcol; o.row = brow; o.tcol = tcol; o.trow = trow;
@@ -253,8 +259,8 @@ k_ext_scan(const ExtJobDev* __restrict__ jobs, int n_jobs, const char* __restric
 
     // forward pass, byte layout first (sw_sse2_byte), word layout on overflow (ssw.c:838-850)
     int word = 0;
-    PassOut f = sw_pass_dispatch<false, RMAX, V>(qc, qlen, rc, rlen, 0, 0, match, mismatch, gO, gE, (qlen + 15) / 16, 0,
-                                                    lane);
+    PassOut f = sw_pass_dispatch<false, RMAX, V>(qc, qlen, rc, rlen, 0, 0, match, mismatch, gO, gE, (qlen + 15) / 16,
+                                                 255 - mismatch, lane);
     int score1 = wave_max_i32(f.best);
     if (score1 + mismatch >= 255) {
         word = 1;

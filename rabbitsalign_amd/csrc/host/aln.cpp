@@ -591,7 +591,7 @@ static void extend_job(const Nam& nam, const Read& read, const References& refs,
     const int ext_right = (int)std::min(std::size_t(50), ref.size() - nam.ref_end);
     const size_t ref_segm_size = read.size() + diff + ext_left + ext_right;
     const size_t len = std::min(ref_segm_size, ref.size() - (size_t)ref_start);
-    jobs.push_back(SwJob{std::string(query), nam.ref_id, (uint32_t)ref_start, (uint32_t)len});
+    jobs.push_back(SwJob{query, nam.ref_id, (uint32_t)ref_start, (uint32_t)len});
 }
 
 // part2_rescue_mate_get_str (pc.cpp:333-368)
@@ -603,7 +603,7 @@ static void rescue_job(const Nam& nam, const Read& read, const References& refs,
     const size_t clen = refs.seqs[nam.ref_id].size();
     size_t start = std::min((size_t)ref_start, clen);
     size_t len = std::min((size_t)(ref_end - ref_start), clen - start);
-    jobs.push_back(SwJob{std::string(r_tmp), nam.ref_id, (uint32_t)start, (uint32_t)len});
+    jobs.push_back(SwJob{r_tmp, nam.ref_id, (uint32_t)start, (uint32_t)len});
 }
 
 void collect_jobs_pe(AlignTmpRes& res, const Record&, const Record&, const Read& read1, const Read& read2,

@@ -18,6 +18,8 @@
 #include <condition_variable>
 #include <cstdint>
 #include <exception>
+#include <cstring>
+#include <deque>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -57,7 +59,10 @@ struct OrderedSink {
 
 struct PeChunk {
     size_t index = 0, begin = 0, end = 0;
-    std::vector<Record> r1, r2;               // upper-cased copies (pc.cpp:1586-1587)
+    // the chunk's records as upper-cased (pc.cpp:1586-1587): the input record
+    // itself when upper-casing would not change it, else an upper-cased copy
+    std::vector<const Record*> r1, r2;
+    std::deque<Record> owned;
     std::vector<std::string> rc1, rc2;        // their reverse complements, computed once
     std::vector<AlignTmpRes> res;
     SeedBatchOut seeds;                       // engine output of pe_seed
@@ -66,22 +71,42 @@ struct PeChunk {
     PhaseTimes times;
 };
 
+// to_uppercase (c & ~32) leaves s unchanged iff no byte has bit 5 set
+static bool upper_already(const std::string& s) {
+    uint64_t acc = 0;
+    size_t i = 0;
+    for (; i + 8 <= s.size(); i += 8) {
+        uint64_t w;
+        memcpy(&w, s.data() + i, 8);
+        acc |= w;
+    }
+    for (; i < s.size(); ++i) acc |= (unsigned char)s[i];
+    return (acc & 0x2020202020202020ULL) == 0;
+}
+
 void pe_load(PeChunk& c, const std::vector<Record>& a, const std::vector<Record>& b, size_t idx, size_t chunk) {
     c.index = idx;
     c.begin = std::min(a.size(), idx * chunk);
     c.end = std::min(a.size(), c.begin + chunk);
-    c.r1.assign(a.begin() + c.begin, a.begin() + c.end);
-    c.r2.assign(b.begin() + c.begin, b.begin() + c.end);
-    for (auto& r : c.r1) to_uppercase(r.seq);
-    for (auto& r : c.r2) to_uppercase(r.seq);
-    c.rc1.resize(c.r1.size());
-    c.rc2.resize(c.r2.size());
-    for (size_t i = 0; i < c.r1.size(); ++i) {
-        c.rc1[i] = reverse_complement(c.r1[i].seq);
-        c.rc2[i] = reverse_complement(c.r2[i].seq);
+    const size_t n = c.end - c.begin;
+    c.r1.resize(n);
+    c.r2.resize(n);
+    auto take = [&](const Record& r) -> const Record* {
+        if (upper_already(r.seq)) return &r;
+        c.owned.push_back(r);
+        to_uppercase(c.owned.back().seq);
+        return &c.owned.back();
+    };
+    c.rc1.resize(n);
+    c.rc2.resize(n);
+    for (size_t i = 0; i < n; ++i) {
+        c.r1[i] = take(a[c.begin + i]);
+        c.r2[i] = take(b[c.begin + i]);
+        c.rc1[i] = reverse_complement(c.r1[i]->seq);
+        c.rc2[i] = reverse_complement(c.r2[i]->seq);
     }
     c.res.clear();
-    c.res.resize(c.r1.size());
+    c.res.resize(n);
 }
 
 // Seeding of a loaded chunk (randstrobes + find_nams + rescue on the engine).
@@ -91,7 +116,7 @@ void pe_seed(PeChunk& c, Engine& eng, const MapContext& mc) {
     if (n == 0) return;
     std::vector<const std::string*> reads;
     reads.reserve(2 * n);
-    for (size_t i = 0; i < n; ++i) { reads.push_back(&c.r1[i].seq); reads.push_back(&c.r2[i].seq); }
+    for (size_t i = 0; i < n; ++i) { reads.push_back(&c.r1[i]->seq); reads.push_back(&c.r2[i]->seq); }
     const auto t = Clock::now();
     eng.seed(reads, mc.mparams.rescue_level, (unsigned)mc.mparams.rescue_cutoff, c.seeds);
     c.times.seed += since(t);
@@ -104,16 +129,16 @@ void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize) {
     if (n == 0) return;
     const SeedBatchOut& so = c.seeds;
     const auto t = Clock::now();
+    std::vector<Nam> nams[2];                 // reused: assign() keeps the capacity
     for (size_t i = 0; i < n; ++i) {
-        std::vector<Nam> nams[2];
         bool rescued[2];
         for (int m = 0; m < 2; ++m) {
             const size_t r = 2 * i + m;
             nams[m].assign(so.nams.begin() + (long)so.offsets[r], so.nams.begin() + (long)so.offsets[r + 1]);
             rescued[m] = so.rescued[r] != 0;
         }
-        const Read read1(c.r1[i].seq, c.rc1[i]), read2(c.r2[i].seq, c.rc2[i]);
-        align_PE_read_part(c.res[i], c.r1[i], c.r2[i], read1, read2, nams, rescued, c.stats, isize, mc, c.rng);
+        const Read read1(c.r1[i]->seq, c.rc1[i]), read2(c.r2[i]->seq, c.rc2[i]);
+        align_PE_read_part(c.res[i], *c.r1[i], *c.r2[i], read1, read2, nams, rescued, c.stats, isize, mc, c.rng);
         c.stats.n_reads += 2;
     }
     c.seeds = SeedBatchOut();
@@ -124,8 +149,8 @@ void pe_get_str(PeChunk& c, const MapContext& mc, float mu, float sigma, std::ve
     const auto t = Clock::now();
     jobs.clear();
     for (size_t i = 0; i < c.r1.size(); ++i) {
-        const Read read1(c.r1[i].seq, c.rc1[i]), read2(c.r2[i].seq, c.rc2[i]);
-        collect_jobs_pe(c.res[i], c.r1[i], c.r2[i], read1, read2, mc, mu, sigma, jobs);
+        const Read read1(c.r1[i]->seq, c.rc1[i]), read2(c.r2[i]->seq, c.rc2[i]);
+        collect_jobs_pe(c.res[i], *c.r1[i], *c.r2[i], read1, read2, mc, mu, sigma, jobs);
     }
     c.times.collect += since(t);
 }
@@ -135,15 +160,15 @@ void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistributio
     const auto t = Clock::now();
     size_t pos = 0;
     for (size_t i = 0; i < c.r1.size(); ++i) {
-        const Read read1(c.r1[i].seq, c.rc1[i]), read2(c.r2[i].seq, c.rc2[i]);
+        const Read read1(c.r1[i]->seq, c.rc1[i]), read2(c.r2[i]->seq, c.rc2[i]);
         pos = store_results_pe(c.res[i], read1, read2, mc, isize.mu, isize.sigma, infos, pos);
     }
     out.clear();
     out.reserve(7 * (size_t)mc.mparams.r * c.r1.size());
     Sam sam(out, mc.refs, mc.mparams.cigar_eqx, rg_id, mc.mparams.output_unmapped, mc.mparams.details);
     for (size_t i = 0; i < c.r1.size(); ++i) {
-        const Read read1(c.r1[i].seq, c.rc1[i]), read2(c.r2[i].seq, c.rc2[i]);
-        align_PE_read_last(c.res[i], c.r1[i], c.r2[i], read1, read2, sam, c.stats, isize, mc, c.rng);
+        const Read read1(c.r1[i]->seq, c.rc1[i]), read2(c.r2[i]->seq, c.rc2[i]);
+        align_PE_read_last(c.res[i], *c.r1[i], *c.r2[i], read1, read2, sam, c.stats, isize, mc, c.rng);
     }
     c.times.last += since(t);
 }
@@ -174,7 +199,8 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
     std::mutex m;
     std::condition_variable cv;
     std::map<size_t, std::unique_ptr<PeChunk>> seeded;   // stage 1 done
-    size_t next_seed = 0;          // next chunk index to claim for stage 1
+    std::vector<uint8_t> claimed(n_chunks, 0);           // stage 1 taken by some worker
+    size_t next_seed = 0;          // every chunk below is claimed
     size_t consumed = 0;           // chunks handed past stage 1
     bool frozen = false, done = false;
     size_t next_par = 0;           // next chunk for the parallel stage (valid once frozen)
@@ -195,8 +221,9 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
     // chunk idx after stage 1: from the prefetch map, or loaded + seeded here
     auto acquire = [&](size_t idx) -> std::unique_ptr<PeChunk> {
         std::unique_lock<std::mutex> g(m);
-        if (idx >= next_seed) {                 // nobody claimed it yet
-            next_seed = idx + 1;
+        if (!claimed[idx]) {                    // nobody claimed it yet
+            claimed[idx] = 1;
+            while (next_seed < n_chunks && claimed[next_seed]) next_seed++;
             g.unlock();
             auto c = stage1(idx);
             g.lock();
@@ -279,7 +306,12 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                         if (failure || done) break;
                         if (frozen && handed) { c = std::move(handed); break; }
                         if (frozen && next_par < n_chunks) { idx = next_par++; break; }
-                        if (next_seed < n_chunks && next_seed < consumed + window) { pf = next_seed++; break; }
+                        if (next_seed < n_chunks && next_seed < consumed + window) {
+                            pf = next_seed;
+                            claimed[pf] = 1;
+                            while (next_seed < n_chunks && claimed[next_seed]) next_seed++;
+                            break;
+                        }
                         if (frozen && next_par >= n_chunks) { done = true; cv.notify_all(); break; }
                         cv.wait(g);
                     }

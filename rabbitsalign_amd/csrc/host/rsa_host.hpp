@@ -164,7 +164,7 @@ struct SeedBatchOut {
 };
 
 struct SwJob {                                  // query host bytes vs reference window
-    std::string query;
+    std::string_view query;                     // into the chunk's read / reverse complement, valid until store
     int ref_id;
     uint32_t ref_start, ref_len;
 };
