@@ -200,6 +200,114 @@ __device__ PassOut sw_pass(const uint8_t* __restrict__ qc, int nrow, const uint8
     return o;
 }
 
+// Fused forward pass: the byte-mode (16 stripes) and word-mode (8 stripes)
+// recurrences of SSW differ only in where the within-stripe F restarts, so
+// both run in one sweep as the two 16-bit halves of packed registers
+// (v_pk_*_i16): low half = byte layout, high half = word layout.  The caller
+// keeps the byte result unless its max reaches the overflow bound, exactly
+// like ssw_align (ssw.c:838-850) -- without the second pass.  Needs every
+// score to fit int16 (host-checked: match * qlen < 30000).
+typedef short pk16 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ pk16 pk_from(uint32_t x) { return __builtin_bit_cast(pk16, x); }
+__device__ __forceinline__ uint32_t pk_bits(pk16 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ pk16 pk_max(pk16 a, pk16 b) { return __builtin_elementwise_max(a, b); }
+
+struct FusedOut {
+    int best[2], col[2], row[2];     // [0] byte layout, [1] word layout
+};
+
+template <int R>
+__device__ FusedOut sw_fwd_fused(const uint8_t* __restrict__ qc, int nrow, const uint8_t* __restrict__ rc, int ncol,
+                                 int match, int mismatch, int gO, int gE, int lane) {
+    const int lanes_used = (nrow + R - 1) / R;
+    const int seg_b = (nrow + 15) / 16, seg_w = (nrow + 7) / 8;
+    pk16 E[R], Hc[R];
+    int qv[R];
+    uint32_t ssm[R], vm[R];
+    const pk16 zero = {0, 0};
+    const pk16 GO2 = {(short)gO, (short)gO}, GE2 = {(short)gE, (short)gE};
+    const uint32_t M2 = pk_bits((pk16){(short)match, (short)match});
+    const uint32_t X2 = pk_bits((pk16){(short)-mismatch, (short)-mismatch});
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        E[r] = zero;
+        Hc[r] = zero;
+        const int p = lane * R + r;
+        ssm[r] = ((p % seg_b) == 0 ? 0u : 0x0000FFFFu) | ((p % seg_w) == 0 ? 0u : 0xFFFF0000u);
+        vm[r] = p < nrow ? 0xFFFFFFFFu : 0u;
+        const int code = p < nrow ? (int)qc[p] : 7;
+        qv[r] = code < 4 ? code : 7;
+    }
+    uint32_t F_out = 0, Fw_out = 0, H_last = 0, diag_top = 0;
+    FusedOut o;
+    o.best[0] = o.best[1] = 0;
+    o.col[0] = o.col[1] = INT_MAX;
+    o.row[0] = o.row[1] = INT_MAX;
+    const int steps = ncol + lanes_used - 1;
+    for (int s = 0; s < steps; ++s) {
+        const uint32_t F_in = (uint32_t)wave_shr1((int)F_out);
+        const uint32_t Fw_in = (uint32_t)wave_shr1((int)Fw_out);
+        const uint32_t Hl_in = (uint32_t)wave_shr1((int)H_last);
+        const int c = s - lane;
+        if (lane < lanes_used && c >= 0 && c < ncol) {
+            const int rcode = rc[c];
+            pk16 dg = pk_from(diag_top), F = pk_from(F_in), Fw = pk_from(Fw_in), cm = zero;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                Fw = pk_from(pk_bits(Fw) & ssm[r]);
+                const pk16 diag = dg + pk_from(qv[r] == rcode ? M2 : X2);
+                const pk16 hm = pk_max(pk_max(diag, E[r]), Fw);
+                const pk16 h = pk_max(hm, F);
+                dg = Hc[r];
+                Hc[r] = h;
+                const pk16 t = hm - GO2;
+                E[r] = pk_max(pk_max(E[r] - GE2, t), zero);
+                Fw = pk_max(pk_max(Fw - GE2, t), zero);
+                F = pk_max(pk_max(F - GE2, h - GO2), zero);
+                cm = pk_max(cm, pk_from(pk_bits(h) & vm[r]));
+            }
+            F_out = pk_bits(F);
+            Fw_out = pk_bits(Fw);
+            H_last = pk_bits(Hc[R - 1]);
+            const uint32_t cmb = pk_bits(cm);
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                const int v = (int)((cmb >> (16 * hf)) & 0xFFFFu);
+                if (v > o.best[hf]) {
+                    o.best[hf] = v;
+                    o.col[hf] = c;
+                    int row = INT_MAX;
+#pragma unroll
+                    for (int r = R - 1; r >= 0; --r)
+                        if (vm[r] && (int)((pk_bits(Hc[r]) >> (16 * hf)) & 0xFFFFu) == v) row = lane * R + r;
+                    o.row[hf] = row;
+                }
+            }
+        }
+        diag_top = Hl_in;
+    }
+    return o;
+}
+
+template <int RMAX>
+__device__ FusedOut sw_fwd_fused_dispatch(const uint8_t* qc, int nrow, const uint8_t* rc, int ncol, int match,
+                                          int mismatch, int gO, int gE, int lane) {
+    const int R = (nrow + 63) / 64;
+#define RSA_FUSED(N) if constexpr (N <= RMAX) return sw_fwd_fused<N>(qc, nrow, rc, ncol, match, mismatch, gO, gE, lane);
+    if (R <= 1) { RSA_FUSED(1) }
+    if (R == 2) { RSA_FUSED(2) }
+    if (R == 3) { RSA_FUSED(3) }
+    if (R == 4) { RSA_FUSED(4) }
+    if (R <= 6) { RSA_FUSED(6) }
+    if (R <= 8) { RSA_FUSED(8) }
+    if (R <= 12) { RSA_FUSED(12) }
+    RSA_FUSED(16)
+#undef RSA_FUSED
+    FusedOut o{};
+    return o;
+}
+
 // R = rows per lane; the kernel is instantiated per RMAX so its register
 // allocation (and occupancy) is that of the largest R it can take, not 16.
 template <bool REV, int RMAX, int V>
@@ -231,6 +339,9 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES)
 k_ext_scan(const ExtJobDev* __restrict__ jobs, int n_jobs, const char* __restrict__ qbuf,
            const char* __restrict__ ref, ScanRes* __restrict__ out, int match, int mismatch, int gO, int gE) {
     __shared__ uint8_t s_q[SCAN_WAVES][MAXQ_LDS];
+    // every packed 16-bit score stays far inside int16
+    const bool fused_ok = match >= 0 && match <= 28 && mismatch >= 0 && mismatch < 4000 && gO >= 0 && gO < 4000 &&
+                          gE >= 0 && gE < 4000;
     __shared__ uint8_t s_r[SCAN_WAVES][MAXR_LDS];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int j = blockIdx.x * SCAN_WAVES + wave;
@@ -259,14 +370,24 @@ k_ext_scan(const ExtJobDev* __restrict__ jobs, int n_jobs, const char* __restric
 
     // forward pass, byte layout first (sw_sse2_byte), word layout on overflow (ssw.c:838-850)
     int word = 0;
-    PassOut f = sw_pass_dispatch<false, RMAX, V>(qc, qlen, rc, rlen, 0, 0, match, mismatch, gO, gE, (qlen + 15) / 16,
-                                                 255 - mismatch, lane);
-    int score1 = wave_max_i32(f.best);
-    if (score1 + mismatch >= 255) {
-        word = 1;
-        f = sw_pass_dispatch<false, RMAX, V>(qc, qlen, rc, rlen, 0, 0, match, mismatch, gO, gE, (qlen + 7) / 8, 0,
-                                                lane);
+    PassOut f;
+    int score1;
+    if (V == 2 && fused_ok) {
+        const FusedOut fo = sw_fwd_fused_dispatch<RMAX>(qc, qlen, rc, rlen, match, mismatch, gO, gE, lane);
+        const int sb = wave_max_i32(fo.best[0]);
+        word = sb + mismatch >= 255 ? 1 : 0;
+        f.best = fo.best[word]; f.col = fo.col[word]; f.row = fo.row[word];
+        score1 = word ? wave_max_i32(fo.best[1]) : sb;
+    } else {
+        f = sw_pass_dispatch<false, RMAX, V>(qc, qlen, rc, rlen, 0, 0, match, mismatch, gO, gE, (qlen + 15) / 16,
+                                             255 - mismatch, lane);
         score1 = wave_max_i32(f.best);
+        if (score1 + mismatch >= 255) {
+            word = 1;
+            f = sw_pass_dispatch<false, RMAX, V>(qc, qlen, rc, rlen, 0, 0, match, mismatch, gO, gE, (qlen + 7) / 8, 0,
+                                                 lane);
+            score1 = wave_max_i32(f.best);
+        }
     }
     int ref_end1, read_end1;
     if (score1 == 0) {
@@ -282,8 +403,8 @@ k_ext_scan(const ExtJobDev* __restrict__ jobs, int n_jobs, const char* __restric
         // reverse pass (ssw.c:877-893)
         const int nrow = read_end1 + 1, ncol = ref_end1 + 1;
         const int seg = word ? (nrow + 7) / 8 : (nrow + 15) / 16;
-        PassOut b = sw_pass_dispatch<true, RMAX, V>(qc, nrow, rc, ncol, read_end1, ref_end1, match, mismatch, gO,
-                                                    gE, seg, score1, lane);
+        PassOut b = sw_pass_dispatch<true, RMAX, (V ? 1 : 0)>(qc, nrow, rc, ncol, read_end1, ref_end1, match, mismatch,
+                                                             gO, gE, seg, score1, lane);
         const int tcol = wave_min_i32(b.tcol);
         if (tcol == INT_MAX) {
             res.flag = 2;   // reverse max < score1: "may miss a small part"
@@ -871,7 +992,9 @@ k_cigar_compact(rsa_aln* __restrict__ alns, int n_jobs, const uint32_t* __restri
 void launch_ext_scan(int rmax, int variant, dim3 grid, dim3 block, hipStream_t st, const ExtJobDev* jobs, int n,
                      const char* q, const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE) {
 #define RSA_L(RM, VV) hipLaunchKernelGGL((k_ext_scan<RM, VV>), grid, block, 0, st, jobs, n, q, ref, out, match, mismatch, gO, gE)
-    if (variant) {
+    if (variant == 2) {
+        if (rmax <= 2) RSA_L(2, 2); else if (rmax <= 4) RSA_L(4, 2); else if (rmax <= 8) RSA_L(8, 2); else RSA_L(16, 2);
+    } else if (variant) {
         if (rmax <= 2) RSA_L(2, 1); else if (rmax <= 4) RSA_L(4, 1); else if (rmax <= 8) RSA_L(8, 1); else RSA_L(16, 1);
     } else {
         if (rmax <= 2) RSA_L(2, 0); else if (rmax <= 4) RSA_L(4, 0); else if (rmax <= 8) RSA_L(8, 0); else RSA_L(16, 0);
