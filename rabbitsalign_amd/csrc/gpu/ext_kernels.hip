@@ -739,6 +739,20 @@ __device__ __forceinline__ int gshr(int v) {
     }
 }
 
+// lane z of the group receives lane z+1 (REG band: index z+2 held by lane z+1); the last lane receives 0
+template <int G>
+__device__ __forceinline__ int gshl1z(int v) {
+    if constexpr (G == 16) return __builtin_amdgcn_update_dpp(0, v, 0x101, 0xf, 0xf, false);
+    else return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, false);
+}
+
+// lane z receives lane z-1; lane 0 receives 0
+template <int G>
+__device__ __forceinline__ int gshr1z(int v) {
+    if constexpr (G == 16) return __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+    else return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false);
+}
+
 template <int G>
 __device__ __forceinline__ int gmax(int v) {
     for (int o = G / 2; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, G));
@@ -771,7 +785,11 @@ __device__ __forceinline__ void aln_sentinel(rsa_aln* out, int j, const ExtJobDe
 // banded_sw + traceback + ext_finish of job j by a group of G lanes (z = lane in
 // group).  LDS: dir[DIRCAP], hb/eb[2G], qc[QCAP], rc[RCAP].  Returns false when
 // the job does not fit the group (nothing written).
-template <int G, int DIRCAP, int QCAP, int RCAP>
+// REG = false: h_b / e_b in LDS (literal array semantics).  REG = true: lane z
+// keeps h_b[z+1] and e_b[z+1] in registers; the reads of h_b[e], e_b[e] and
+// h_b[e-1] become DPP shifts (index 0 and indices past the group are always
+// 0), so the row loop has no LDS round trip and no barrier.
+template <int G, int DIRCAP, int QCAP, int RCAP, bool REG>
 __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr, const char* __restrict__ qbuf,
                            const char* __restrict__ ref, uint32_t* __restrict__ cig_pool,
                            uint32_t* __restrict__ raw_pool, rsa_aln* __restrict__ out, int match, int mismatch,
@@ -801,28 +819,43 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
     const int len = ref_l > read_l ? ref_l : read_l;
     int s2 = 1024, max_v = 0, width_d = 0;
     bool deferred = false;
+    int HB = 0, EB = 0;                              // REG: h_b[z+1], e_b[z+1]
     do {
         const int width = bw * 2 + 3;
         width_d = bw * 2 + 1;
         if (width_d > G) { deferred = true; break; }
         while (width_d * read_l * 3 >= s2) s2 *= 2;
         if (s2 > DIRCAP) { deferred = true; break; }
-        if (z >= 1 && z <= width - 2) hb[z] = 0;
-        WSYNC();
+        if constexpr (REG) {
+            if (z + 1 >= 1 && z + 1 <= width - 2) HB = 0;
+        } else {
+            if (z >= 1 && z <= width - 2) hb[z] = 0;
+            WSYNC();
+        }
         int lmax = 0;
         for (int i = 0; i < read_l; ++i) {
             const int beg = max(0, i - bw), end = min(ref_l - 1, i + bw);
             const int edge = end + 1 < width - 1 ? end + 1 : width - 1;
-            if (z == 0) { hb[0] = 0; eb[0] = 0; hb[edge] = 0; eb[edge] = 0; }
-            WSYNC();
             const int jj = beg + z;
             const bool on = jj <= end;
             const int u = z + 1;
-            const int e = u + (i - bw >= 1 ? 1 : 0);
-            const int hb_e = hb[e], eb_e = eb[e], hb_d = hb[e - 1];
+            const int sh = i - bw >= 1 ? 1 : 0;
+            int hb_e, eb_e, hb_d;
+            if constexpr (REG) {
+                if (z == edge - 1) { HB = 0; EB = 0; }
+                const int HBl = gshl1z<G>(HB), EBl = gshl1z<G>(EB), HBr = gshr1z<G>(HB);
+                hb_e = sh ? HBl : HB;
+                eb_e = sh ? EBl : EB;
+                hb_d = sh ? HB : HBr;
+            } else {
+                if (z == 0) { hb[0] = 0; eb[0] = 0; hb[edge] = 0; eb[edge] = 0; }
+                WSYNC();
+                const int e = u + sh;
+                hb_e = hb[e]; eb_e = eb[e]; hb_d = hb[e - 1];
+            }
             const int qv = qc[i];
             const int rv = on ? rc[jj] : 4;
-            WSYNC();
+            if constexpr (!REG) WSYNC();
             const int t1 = i == 0 ? -gO : hb_e - gO;
             const int t2 = i == 0 ? -gE : eb_e - gE;
             const int E = t1 > t2 ? t1 : t2;
@@ -840,19 +873,24 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
             const int H = m > diag ? m : diag;
             const int dh = m <= diag ? 1 : (e1 > f1 ? de : df);
             if (on) {
-                eb[u] = E;
                 int8_t* dl = dir + width_d * 3 * i + 3 * z;
                 dl[0] = (int8_t)de; dl[1] = (int8_t)df; dl[2] = (int8_t)dh;
                 if (H > lmax) lmax = H;
             }
-            WSYNC();
-            if (on) hb[u] = H;                       // h_b[1..u] = h_c[1..u]
-            WSYNC();
+            if constexpr (REG) {
+                if (on) { EB = E; HB = H; }
+            } else {
+                if (on) eb[u] = E;
+                WSYNC();
+                if (on) hb[u] = H;                   // h_b[1..u] = h_c[1..u]
+                WSYNC();
+            }
         }
         lmax = gmax<G>(lmax);
         if (lmax > max_v) max_v = lmax;
         bw *= 2;
     } while (max_v < sr.score1 && bw <= len);
+    WSYNC();                                         // direction bytes visible to the traceback lane
     if (deferred) return false;
     if (z != 0) return true;
     bw /= 2;
@@ -895,6 +933,7 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
 #define B16_DIRCAP 4096
 #define B16_SEGCAP 320
 
+template <bool REG>
 __global__ void __launch_bounds__(64)
 k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan, int n_jobs,
              const char* __restrict__ qbuf, const char* __restrict__ ref, uint32_t* __restrict__ cig_pool,
@@ -918,7 +957,7 @@ k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
         if (z == 0) aln_sentinel(out, j, jb, -100000);
         return;
     }
-    const bool done = band_group<16, B16_DIRCAP, B16_SEGCAP, B16_SEGCAP>(
+    const bool done = band_group<16, B16_DIRCAP, B16_SEGCAP, B16_SEGCAP, REG>(
         j, z, jb, sr, qbuf, ref, cig_pool, raw_pool, out, match, mismatch, gO, gE, bonus, s_dir[g], s_hb[g],
         s_eb[g], s_qc[g], s_rc[g]);
     if (!done && z == 0) queue[atomicAdd(qcount, 1)] = j;
@@ -928,6 +967,7 @@ k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
 #define B64_QCAP 1024
 #define B64_RCAP 2048
 
+template <bool REG>
 __global__ void __launch_bounds__(64)
 k_ext_band64(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan, const char* __restrict__ qbuf,
              const char* __restrict__ ref, uint32_t* __restrict__ cig_pool, uint32_t* __restrict__ raw_pool,
@@ -945,7 +985,7 @@ k_ext_band64(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
         const int j = queue[t];
         const ExtJobDev jb = jobs[j];
         const ScanRes sr = scan[j];
-        const bool done = band_group<64, B64_DIRCAP, B64_QCAP, B64_RCAP>(
+        const bool done = band_group<64, B64_DIRCAP, B64_QCAP, B64_RCAP, REG>(
             j, z, jb, sr, qbuf, ref, cig_pool, raw_pool, out, match, mismatch, gO, gE, bonus, s_dir, s_hb, s_eb,
             s_qc, s_rc);
         if (!done && z == 0) { overflow[j] = 1; atomicAdd(ocount, 1); }
@@ -1000,4 +1040,27 @@ void launch_ext_scan(int rmax, int variant, dim3 grid, dim3 block, hipStream_t s
         if (rmax <= 2) RSA_L(2, 0); else if (rmax <= 4) RSA_L(4, 0); else if (rmax <= 8) RSA_L(8, 0); else RSA_L(16, 0);
     }
 #undef RSA_L
+}
+
+void launch_ext_band16(bool reg, dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n,
+                       const char* q, const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match,
+                       int mismatch, int gO, int gE, int bonus, int* queue, int* qcount) {
+    if (reg)
+        hipLaunchKernelGGL(k_ext_band16<true>, grid, dim3(64), 0, st, jobs, scan, n, q, ref, cig, raw, out, match,
+                           mismatch, gO, gE, bonus, queue, qcount);
+    else
+        hipLaunchKernelGGL(k_ext_band16<false>, grid, dim3(64), 0, st, jobs, scan, n, q, ref, cig, raw, out, match,
+                           mismatch, gO, gE, bonus, queue, qcount);
+}
+
+void launch_ext_band64(bool reg, dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan,
+                       const char* q, const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match,
+                       int mismatch, int gO, int gE, int bonus, const int* queue, const int* qcount, int* overflow,
+                       int* ocount) {
+    if (reg)
+        hipLaunchKernelGGL(k_ext_band64<true>, grid, dim3(64), 0, st, jobs, scan, q, ref, cig, raw, out, match,
+                           mismatch, gO, gE, bonus, queue, qcount, overflow, ocount);
+    else
+        hipLaunchKernelGGL(k_ext_band64<false>, grid, dim3(64), 0, st, jobs, scan, q, ref, cig, raw, out, match,
+                           mismatch, gO, gE, bonus, queue, qcount, overflow, ocount);
 }

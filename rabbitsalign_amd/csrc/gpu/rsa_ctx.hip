@@ -26,12 +26,13 @@ __global__ void k_ext_band(const ExtJobDev* jobs, const ScanRes* scan, int n_job
                            const char* qbuf, const char* ref, uint32_t* cig_pool, rsa_aln* out, uint8_t* scratch,
                            int64_t scr_stride, int arr_cap, int64_t dir_cap, int match, int mismatch, int gO,
                            int gE, int bonus, int* overflow, int over_code);
-__global__ void k_ext_band16(const ExtJobDev* jobs, const ScanRes* scan, int n_jobs, const char* qbuf, const char* ref,
-                             uint32_t* cig_pool, uint32_t* raw_pool, rsa_aln* out, int match, int mismatch, int gO,
-                             int gE, int bonus, int* queue, int* qcount);
-__global__ void k_ext_band64(const ExtJobDev* jobs, const ScanRes* scan, const char* qbuf, const char* ref,
-                             uint32_t* cig_pool, uint32_t* raw_pool, rsa_aln* out, int match, int mismatch, int gO,
-                             int gE, int bonus, const int* queue, const int* qcount, int* overflow, int* ocount);
+void launch_ext_band16(bool reg, dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n,
+                       const char* q, const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match,
+                       int mismatch, int gO, int gE, int bonus, int* queue, int* qcount);
+void launch_ext_band64(bool reg, dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan,
+                       const char* q, const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match,
+                       int mismatch, int gO, int gE, int bonus, const int* queue, const int* qcount, int* overflow,
+                       int* ocount);
 __global__ void k_cigar_compact(rsa_aln* alns, int n_jobs, const uint32_t* slots, uint32_t* dense, uint64_t* total);
 
 int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, const rsa_read_batch* rb,
@@ -245,6 +246,12 @@ static int scan_variant() {
     return v ? atoi(v) : 0;
 }
 
+// band kernel variant (RSA_BAND_V: 0 LDS arrays, 1 register arrays; A/B experiments, same results)
+static int band_variant() {
+    const char* v = getenv("RSA_BAND_V");
+    return v ? atoi(v) : 0;
+}
+
 struct ExtStatus {            // device-side counters of one rsa_extend call
     int qcount;               // jobs deferred by k_ext_band16
     int ocount;               // jobs k_ext_band64 could not hold
@@ -321,18 +328,19 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
     L->kt.end(st);
     // 16 lanes per job for the common narrow bands; the rest queue for 64-lane waves
     L->kt.begin(st, RSA_K_EXT_BAND);
-    hipLaunchKernelGGL(k_ext_band16, dim3((n + 3) / 4), dim3(64), 0, st, L->d_jobs.as<ExtJobDev>(),
-                       L->d_scan.as<ScanRes>(), (int)n, L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(),
-                       L->d_raw.as<uint32_t>(), L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open,
-                       jb->gap_extend, jb->end_bonus, L->d_queue.as<int>(), &dst->qcount);
+    const bool band_reg = band_variant() != 0;
+    launch_ext_band16(band_reg, dim3((n + 3) / 4), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(), (int)n,
+                      L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(),
+                      L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open, jb->gap_extend, jb->end_bonus,
+                      L->d_queue.as<int>(), &dst->qcount);
     HIPCHK(hipGetLastError());
     L->kt.end(st);
     L->kt.begin(st, RSA_K_EXT_BAND_WIDE);
-    hipLaunchKernelGGL(k_ext_band64, dim3(std::min<uint32_t>(n, BAND64_GRID)), dim3(64), 0, st,
-                       L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(), L->d_q.as<char>(), ctx->d_ref,
-                       L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(), L->d_alns.as<rsa_aln>(), jb->match,
-                       jb->mismatch, jb->gap_open, jb->gap_extend, jb->end_bonus, L->d_queue.as<int>(),
-                       &dst->qcount, L->d_over.as<int>(), &dst->ocount);
+    launch_ext_band64(band_reg, dim3(std::min<uint32_t>(n, BAND64_GRID)), st, L->d_jobs.as<ExtJobDev>(),
+                      L->d_scan.as<ScanRes>(), L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(),
+                      L->d_raw.as<uint32_t>(), L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open,
+                      jb->gap_extend, jb->end_bonus, L->d_queue.as<int>(), &dst->qcount, L->d_over.as<int>(),
+                      &dst->ocount);
     HIPCHK(hipGetLastError());
     L->kt.end(st);
     auto compact_and_copy = [&](uint64_t guess) -> int {
