@@ -212,6 +212,123 @@ k_randstrobes(const char* __restrict__ seq, const uint64_t* __restrict__ roff, c
 }
 
 // ---------------------------------------------------------------------------
+// k_randstrobes_s: one lane per read, streaming.  The reference builds the
+// whole syncmer vector, then pairs (RandstrobeIterator, randstrobes.cpp:148-171)
+// forward and on the reversed vector (207-253).  Both pairings only look
+// w_max syncmers ahead (forward) or behind (reverse complement), so each
+// randstrobe is emitted as soon as its window is complete, from a 16-entry
+// per-lane ring in LDS -- no syncmer vector in global scratch.  Reverse
+// randstrobes are produced in descending order into the tail of the read's
+// output slot and moved into place once the syncmer count is known.
+// ---------------------------------------------------------------------------
+#define RSS_RING 32
+
+template <int WC>
+__global__ void __launch_bounds__(64)
+k_randstrobes_s(const char* __restrict__ seq, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
+                const uint64_t* __restrict__ qbase, int n_reads, SeedIndexParams p,
+                rsa_query_randstrobe* __restrict__ qrs, uint32_t* __restrict__ qcnt) {
+    __shared__ uint64_t s_rh[RSS_RING][64];
+    __shared__ uint32_t s_rp[RSS_RING][64];
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * 64 + lane;
+    if (r >= n_reads) return;
+    const int len = (int)rlen[r];
+    if (len < p.w_max) { qcnt[r] = 0; return; }     // randstrobes.cpp:209
+    const char* s = seq + roff[r];
+    rsa_query_randstrobe* out = qrs + qbase[r];
+    const int k = p.k, sl = p.s, t = p.t, wmin = p.w_min, wmax = p.w_max;
+    const uint64_t kmask = (k == 32) ? ~0ULL : ((1ULL << (2 * k)) - 1);
+    const uint64_t smask = (1ULL << (2 * sl)) - 1;
+    const int kshift = (k - 1) * 2, sshift = (sl - 1) * 2;
+    auto rh = [&](int x) -> uint64_t { return s_rh[x & (RSS_RING - 1)][lane]; };
+    auto rp = [&](int x) -> uint32_t { return s_rp[x & (RSS_RING - 1)][lane]; };
+    // forward randstrobe with strobe1 = syncmer i, window end w_end (rs_get)
+    auto fwd = [&](int i, int w_end) {
+        const uint64_t hi = rh(i);
+        const uint64_t max_position = (uint64_t)rp(i) + (unsigned)p.max_dist;
+        uint64_t min_val = END64;
+        int best = i;
+        for (int j = i + wmin; j <= w_end && rp(j) <= max_position; ++j) {
+            const uint64_t res = (uint64_t)__popcll((hi ^ rh(j)) & p.q);
+            if (res < min_val) { min_val = res; best = j; }
+        }
+        rsa_query_randstrobe o;
+        o.hash = hi + rh(best); o.start = rp(i); o.end = rp(best) + (uint32_t)k; o.is_reverse = 0; o.pad_ = 0;
+        out[i] = o;
+    };
+    // reverse-complement randstrobe whose strobe1 is syncmer x (reversed index n-1-x): the
+    // window runs over syncmers x-wmin down to max(x-wmax, 0), positions len - pos - k
+    auto rcs = [&](int x) {
+        auto pos = [&](int y) -> uint32_t { return (uint32_t)(len - (int)rp(y) - k); };
+        const uint64_t hi = rh(x);
+        const uint32_t pi = pos(x);
+        const uint64_t max_position = (uint64_t)pi + (unsigned)p.max_dist;
+        uint64_t min_val = END64;
+        int best = x;
+        const int lo = x - wmax > 0 ? x - wmax : 0;
+        for (int y = x - wmin; y >= lo && pos(y) <= max_position; --y) {
+            const uint64_t res = (uint64_t)__popcll((hi ^ rh(y)) & p.q);
+            if (res < min_val) { min_val = res; best = y; }
+        }
+        rsa_query_randstrobe o;
+        o.hash = hi + rh(best); o.start = pi; o.end = pos(best) + (uint32_t)k; o.is_reverse = 1; o.pad_ = 0;
+        out[2 * len - 1 - x] = o;                     // temporary slot, moved below
+    };
+    SmWindow<WC> win(k - sl + 1);
+    const int W = win.W;
+    uint64_t min_val = END64;
+    long long min_pos = -1;
+    int l = 0, n = 0;
+    uint64_t xk0 = 0, xk1 = 0, xs0 = 0, xs1 = 0;
+    for (int i = 0; i < len; ++i) {
+        const int c = nt4_code((unsigned char)s[i]);
+        if (c < 4) {
+            xk0 = ((xk0 << 2) | (uint64_t)c) & kmask;
+            xk1 = (xk1 >> 2) | ((uint64_t)(3 - c) << kshift);
+            xs0 = ((xs0 << 2) | (uint64_t)c) & smask;
+            xs1 = (xs1 >> 2) | ((uint64_t)(3 - c) << sshift);
+            if (++l < sl) continue;
+            const uint64_t hs = xxh64_u64(xs0 < xs1 ? xs0 : xs1);
+            const bool popped = win.push(hs);
+            if (!popped) {
+                if (win.qn < W) continue;
+                for (int j = 0; j < W; ++j) {
+                    const uint64_t v = win.at(j);
+                    if (v < min_val) { min_val = v; min_pos = (long long)i - k + j + 1; }
+                }
+            } else if (min_pos == (long long)i - k) {
+                min_val = END64;
+                min_pos = (long long)i - sl + 1;
+                for (int j = W - 1; j >= 0; --j) {
+                    const uint64_t v = win.at(j);
+                    if (v < min_val) { min_val = v; min_pos = (long long)i - k + j + 1; }
+                }
+            } else if (hs < min_val) {
+                min_val = hs;
+                min_pos = (long long)i - sl + 1;
+            }
+            if (min_pos == (long long)i - k + t) {
+                s_rh[n & (RSS_RING - 1)][lane] = xxh64_u64(xk0 < xk1 ? xk0 : xk1);
+                s_rp[n & (RSS_RING - 1)][lane] = (uint32_t)(i - k + 1);
+                if (n >= wmax) fwd(n - wmax, n);
+                if (n >= wmin) rcs(n);
+                n++;
+            }
+        } else {
+            min_val = END64; min_pos = -1;
+            l = 0; xs0 = xs1 = xk0 = xk1 = 0;
+            win.reset();
+        }
+    }
+    const int m = n > wmin ? n - wmin : 0;
+    for (int i = (n - wmax > 0 ? n - wmax : 0); i < m; ++i) fwd(i, n - 1);
+    // reverse randstrobe of syncmer x sits at 2len-1-x; its place is m + (n-1-x)
+    for (int tt = 0; tt < m; ++tt) out[m + tt] = out[2 * len - n + tt];
+    qcnt[r] = (uint32_t)(2 * m);
+}
+
+// ---------------------------------------------------------------------------
 // k_randstrobes_w: one wavefront per read.
 //   1. lanes: base codes and every canonical s-mer hash (xxh64) -> LDS
 //   2. lane 0: the reference's stateful window-minimum walk over those hashes
@@ -1240,7 +1357,16 @@ int seed_stage_randstrobes(SeedBufs& b, hipStream_t st, const SeedIndexParams& p
                       seed_variant_lane("RSA_RS_WAVE");
     if (kt) kt->begin(st, RSA_K_RANDSTROBES);
     const int rpw = seed_rpw("RSA_RPW_RS", 64);
-    if (wave)
+    const bool stream = p.w_max < RSS_RING && !seed_variant_lane("RSA_RS_SCRATCH");
+    if (stream && p.k - p.s + 1 == 5)
+        hipLaunchKernelGGL(k_randstrobes_s<5>, dim3((n + 63) / 64), dim3(64), 0, st, DP(B_SEQ, char),
+                           DP(B_ROFF, uint64_t), DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n, p,
+                           DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
+    else if (stream)
+        hipLaunchKernelGGL(k_randstrobes_s<0>, dim3((n + 63) / 64), dim3(64), 0, st, DP(B_SEQ, char),
+                           DP(B_ROFF, uint64_t), DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n, p,
+                           DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
+    else if (wave)
         hipLaunchKernelGGL(k_randstrobes_w, dim3((n + RS_WAVES - 1) / RS_WAVES), dim3(64 * RS_WAVES), 0, st,
                            DP(B_SEQ, char), DP(B_ROFF, uint64_t), DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n,
                            p, DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
