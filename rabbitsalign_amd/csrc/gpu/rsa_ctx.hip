@@ -240,16 +240,18 @@ static int64_t band_stride(int arr_cap, int64_t dir_cap) {
     return (s + 255) & ~(int64_t)255;
 }
 
-// k_ext_scan cell bookkeeping variant (RSA_SCAN_V, A/B experiments; same results)
+// k_ext_scan variant (RSA_SCAN_V; same results): 0 per-cell bookkeeping, 1 per-column,
+// 2 (default) fused byte+word forward pass in packed int16 -- fastest on the headline
+// workload (profiles/r01_kab_r8.jsonl)
 static int scan_variant() {
     const char* v = getenv("RSA_SCAN_V");
-    return v ? atoi(v) : 0;
+    return v ? atoi(v) : 2;
 }
 
-// band kernel variant (RSA_BAND_V: 0 LDS arrays, 1 register arrays; A/B experiments, same results)
+// band kernel variant (RSA_BAND_V: 0 LDS arrays, 1 (default) register arrays; same results)
 static int band_variant() {
     const char* v = getenv("RSA_BAND_V");
-    return v ? atoi(v) : 0;
+    return v ? atoi(v) : 1;
 }
 
 struct ExtStatus {            // device-side counters of one rsa_extend call

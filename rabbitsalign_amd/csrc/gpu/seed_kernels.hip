@@ -1357,7 +1357,8 @@ int seed_stage_randstrobes(SeedBufs& b, hipStream_t st, const SeedIndexParams& p
                       seed_variant_lane("RSA_RS_WAVE");
     if (kt) kt->begin(st, RSA_K_RANDSTROBES);
     const int rpw = seed_rpw("RSA_RPW_RS", 64);
-    const bool stream = p.w_max < RSS_RING && !seed_variant_lane("RSA_RS_SCRATCH");
+    // the streaming kernel measured slower than the scratch one (profiles/r01_kab_r8.jsonl): opt-in
+    const bool stream = p.w_max < RSS_RING && seed_variant_lane("RSA_RS_STREAM");
     if (stream && p.k - p.s + 1 == 5)
         hipLaunchKernelGGL(k_randstrobes_s<5>, dim3((n + 63) / 64), dim3(64), 0, st, DP(B_SEQ, char),
                            DP(B_ROFF, uint64_t), DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n, p,

@@ -203,6 +203,8 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
     size_t next_seed = 0;          // every chunk below is claimed
     size_t consumed = 0;           // chunks handed past stage 1
     bool frozen = false, done = false;
+    bool lead_seeded = false;      // prefetch waits until chunk 0 is seeded: it would only queue
+                                   // other chunks' seeding ahead of the single-worker timeline
     size_t next_par = 0;           // next chunk for the parallel stage (valid once frozen)
     std::unique_ptr<PeChunk> handed;                     // part() done in the sequential phase
     InsertSizeDistribution isize, frozen_isize;
@@ -263,6 +265,11 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                 // ---- single-worker timeline until the insert-size estimate freezes ----
                 auto pre = acquire(0);
                 if (!pre) return;
+                {
+                    std::lock_guard<std::mutex> g(m);
+                    lead_seeded = true;
+                    cv.notify_all();
+                }
                 pe_part(*pre, mc, isize);
                 size_t next = 1;
                 for (;;) {
@@ -306,7 +313,7 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                         if (failure || done) break;
                         if (frozen && handed) { c = std::move(handed); break; }
                         if (frozen && next_par < n_chunks) { idx = next_par++; break; }
-                        if (next_seed < n_chunks && next_seed < consumed + window) {
+                        if (lead_seeded && next_seed < n_chunks && next_seed < consumed + window) {
                             pf = next_seed;
                             claimed[pf] = 1;
                             while (next_seed < n_chunks && claimed[next_seed]) next_seed++;
