@@ -122,8 +122,7 @@ def main():
     ap.add_argument("--pairs", type=int, default=1_000_000,
                     help="pairs (SE: reads) per step per GPU (SURVEY.md §8d: 10^6 pairs per config)")
     ap.add_argument("--threads", type=int, default=0,
-                    help="host pipeline threads (0: 1.5 x host cores, max 48; GPU waits sleep, so extra workers "
-                         "keep the cores busy while others wait on the GPU)")
+                    help="host pipeline threads (0: one per host core, max 64; r9: 16 beat 24 on 16 cores)")
     ap.add_argument("--chunk-size", type=int, default=10000)
     ap.add_argument("--ref-seed", type=int, default=1)
     ap.add_argument("--read-seed", type=int, default=7)
@@ -142,7 +141,7 @@ def main():
     if args.ref_len:
         wl["ref_len"] = args.ref_len
     cores = host_cores()
-    threads = args.threads or min(48, (3 * cores) // 2)
+    threads = args.threads or min(64, cores)
 
     # torch first: its libamdhip64 (soname libamdhip64.so.7) is then the one
     # runtime of the process and librsa_gpu.so binds to it; loading ours first

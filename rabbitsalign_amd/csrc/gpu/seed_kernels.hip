@@ -562,19 +562,35 @@ k_lookup(const rsa_query_randstrobe* __restrict__ qrs, const uint32_t* __restric
 // robin_hood::unordered_flat_map<unsigned, ...> slot-layout emulation
 // (robin_hood.h v3.11.1; same algorithm as oracle/rsa_oracle.c rh_*)
 // ---------------------------------------------------------------------------
-struct DMap {
-    uint8_t* info; uint32_t* keys; int32_t* vals;
-    uint8_t* info2; uint32_t* keys2; int32_t* vals2;
+// AS = address space of the tables: 0 (generic: global scratch) or 3 (LDS,
+// so every probe is a ds_read instead of a flat access)
+template <int AS> struct AsTypes {
+    typedef __attribute__((address_space(AS))) uint8_t U8;
+    typedef __attribute__((address_space(AS))) uint32_t U32;
+    typedef __attribute__((address_space(AS))) int32_t I32;
+};
+template <> struct AsTypes<0> { typedef uint8_t U8; typedef uint32_t U32; typedef int32_t I32; };
+
+template <int AS>
+struct DMapT {
+    typedef typename AsTypes<AS>::U8 U8;
+    typedef typename AsTypes<AS>::U32 U32;
+    typedef typename AsTypes<AS>::I32 I32;
+    U8* info; U32* keys; I32* vals;
+    U8* info2; U32* keys2; I32* vals2;
     uint32_t cap;                          // slots per table
     uint64_t mult;
     uint32_t mask, num, max_allowed, nwb, info_inc, info_shift;
     int overflow;
 };
+using DMap = DMapT<0>;
+using LMap = DMapT<3>;
 
 __device__ __forceinline__ uint32_t rh_calc_max(uint32_t n) { return (uint32_t)((uint64_t)n * 80 / 100); }
 __device__ __forceinline__ uint32_t rh_calc_nwb(uint32_t n) { uint32_t m = rh_calc_max(n); return n + (m < 255 ? m : 255); }
 
-__device__ bool rh_init_data(DMap& m, uint32_t max_elements) {
+template <class M>
+__device__ bool rh_init_data(M& m, uint32_t max_elements) {
     const uint32_t nwb = rh_calc_nwb(max_elements);
     const uint32_t span = (nwb + 16 + 3) & ~3u;      // info bytes zeroed as words
     if (span > m.cap) { m.overflow = 1; return false; }
@@ -582,14 +598,15 @@ __device__ bool rh_init_data(DMap& m, uint32_t max_elements) {
     m.mask = max_elements - 1;
     m.max_allowed = rh_calc_max(max_elements);
     m.nwb = nwb;
-    for (uint32_t i = 0; i < span; i += 4) *(uint32_t*)(m.info + i) = 0;
+    for (uint32_t i = 0; i < span; i += 4) *(typename M::U32*)(m.info + i) = 0;
     m.info[nwb] = 1;
     m.info_inc = 32;
     m.info_shift = 0;
     return true;
 }
 
-__device__ __forceinline__ void rh_key_to_idx(const DMap& m, uint32_t key, uint32_t& idx, uint32_t& info) {
+template <class M>
+__device__ __forceinline__ void rh_key_to_idx(const M& m, uint32_t key, uint32_t& idx, uint32_t& info) {
     uint64_t h = (uint64_t)key;
     h ^= h >> 33; h *= 0xff51afd7ed558ccdULL; h ^= h >> 33;
     h *= m.mult;
@@ -598,7 +615,8 @@ __device__ __forceinline__ void rh_key_to_idx(const DMap& m, uint32_t key, uint3
     idx = (uint32_t)(h >> 5) & m.mask;
 }
 
-__device__ void rh_shift_up(DMap& m, uint32_t start, uint32_t ins) {
+template <class M>
+__device__ void rh_shift_up(M& m, uint32_t start, uint32_t ins) {
     for (uint32_t i = start; i != ins; --i) { m.keys[i] = m.keys[i - 1]; m.vals[i] = m.vals[i - 1]; }
     for (uint32_t i = start; i != ins; --i) {
         m.info[i] = (uint8_t)(m.info[i - 1] + m.info_inc);
@@ -606,7 +624,8 @@ __device__ void rh_shift_up(DMap& m, uint32_t start, uint32_t ins) {
     }
 }
 
-__device__ bool rh_try_increase_info(DMap& m) {
+template <class M>
+__device__ bool rh_try_increase_info(M& m) {
     if (m.info_inc <= 2) return false;
     m.info_inc >>= 1;
     m.info_shift++;
@@ -618,7 +637,8 @@ __device__ bool rh_try_increase_info(DMap& m) {
     return true;
 }
 
-__device__ void rh_insert_move(DMap& m, uint32_t key, int32_t val) {
+template <class M>
+__device__ void rh_insert_move(M& m, uint32_t key, int32_t val) {
     if (m.max_allowed == 0 && !rh_try_increase_info(m)) { m.overflow = 2; return; }
     uint32_t idx, info;
     rh_key_to_idx(m, key, idx, info);
@@ -633,9 +653,12 @@ __device__ void rh_insert_move(DMap& m, uint32_t key, int32_t val) {
     m.num++;
 }
 
-__device__ void rh_rehash(DMap& m, uint32_t nb) {
+template <class M>
+__device__ void rh_rehash(M& m, uint32_t nb) {
     if (!m.info2) { m.overflow = 1; return; }
-    uint8_t* oi = m.info; uint32_t* ok = m.keys; int32_t* ov = m.vals;
+    typename M::U8* oi = m.info;
+    typename M::U32* ok = m.keys;
+    typename M::I32* ov = m.vals;
     const uint32_t onwb = rh_calc_nwb(m.mask + 1);
     m.info = m.info2; m.keys = m.keys2; m.vals = m.vals2;
     m.info2 = oi; m.keys2 = ok; m.vals2 = ov;
@@ -645,7 +668,8 @@ __device__ void rh_rehash(DMap& m, uint32_t nb) {
             if (oi[i] != 0) rh_insert_move(m, ok[i], ov[i]);
 }
 
-__device__ void rh_increase_size(DMap& m) {
+template <class M>
+__device__ void rh_increase_size(M& m) {
     const uint32_t maxa = rh_calc_max(m.mask + 1);
     if (m.num < maxa && rh_try_increase_info(m)) return;
     m.mult += 0xc4ceb9fe1a85ec54ULL;
@@ -654,14 +678,16 @@ __device__ void rh_increase_size(DMap& m) {
 }
 
 // default construction + reserve(100) (nam.cpp:913-914)
-__device__ void rh_new_reserved(DMap& m) {
+template <class M>
+__device__ void rh_new_reserved(M& m) {
     m.mult = 0xc4ceb9fe1a85ec53ULL;
     m.overflow = 0;
     rh_init_data(m, 128);
 }
 
 // operator[]: returns the value of key, inserting new_val if absent
-__device__ int32_t rh_get_or_insert(DMap& m, uint32_t key, int32_t new_val, bool& inserted) {
+template <class M>
+__device__ int32_t rh_get_or_insert(M& m, uint32_t key, int32_t new_val, bool& inserted) {
     inserted = false;
     for (int attempt = 0; attempt < 256 && !m.overflow; ++attempt) {
         uint32_t idx, info;
@@ -697,6 +723,35 @@ __device__ void map_bind(DMap& m, uint8_t* base, uint32_t cap, int which) {
     m.keys2 = (uint32_t*)b2; m.vals2 = (int32_t*)(b2 + (size_t)cap * 4); m.info2 = b2 + (size_t)cap * 8;
 }
 
+// field-wise copies: structs in LDS (address space 3) and generic memory are
+// different C++ types, so whole-struct assignment between them does not compile
+template <class P>
+__device__ __forceinline__ HitD ld_hit(P p) {
+    HitD h;
+    h.qs = p->qs; h.qe = p->qe; h.rs = p->rs; h.re = p->re; h.list = p->list; h.pad = p->pad;
+    return h;
+}
+template <class P>
+__device__ __forceinline__ void st_hit(P p, const HitD& h) {
+    p->qs = h.qs; p->qe = h.qe; p->rs = h.rs; p->re = h.re; p->list = h.list; p->pad = h.pad;
+}
+template <class P>
+__device__ __forceinline__ rsa_nam ld_nam(P p) {
+    rsa_nam n;
+    n.nam_id = p->nam_id; n.query_start = p->query_start; n.query_end = p->query_end;
+    n.query_prev_hit_startpos = p->query_prev_hit_startpos; n.ref_start = p->ref_start; n.ref_end = p->ref_end;
+    n.ref_prev_hit_startpos = p->ref_prev_hit_startpos; n.n_hits = p->n_hits; n.ref_id = p->ref_id;
+    n.score = p->score; n.is_rc = p->is_rc;
+    return n;
+}
+template <class P>
+__device__ __forceinline__ void st_nam(P p, const rsa_nam& n) {
+    p->nam_id = n.nam_id; p->query_start = n.query_start; p->query_end = n.query_end;
+    p->query_prev_hit_startpos = n.query_prev_hit_startpos; p->ref_start = n.ref_start; p->ref_end = n.ref_end;
+    p->ref_prev_hit_startpos = n.ref_prev_hit_startpos; p->n_hits = n.n_hits; p->ref_id = n.ref_id;
+    p->score = n.score; p->is_rc = n.is_rc;
+}
+
 // ---------------------------------------------------------------------------
 // NAM construction helpers
 // ---------------------------------------------------------------------------
@@ -706,10 +761,11 @@ __device__ __forceinline__ float nam_score(const rsa_nam& n) {   // nam.cpp:456-
     return (2 * mn - mx) > 0 ? (float)(n.n_hits * (2 * mn - mx)) : 1.0f;
 }
 
-__device__ __forceinline__ void nam_emit(rsa_nam* out, int& n_out, rsa_nam x) {
+template <class OutP>
+__device__ __forceinline__ void nam_emit(OutP out, int& n_out, rsa_nam x) {
     x.score = nam_score(x);
     x.nam_id = n_out;
-    out[n_out++] = x;
+    st_nam(&out[n_out++], x);
 }
 
 __device__ __forceinline__ rsa_nam nam_from_hit(const HitD& h, int ref_id, int is_rc) {
@@ -721,17 +777,19 @@ __device__ __forceinline__ rsa_nam nam_from_hit(const HitD& h, int ref_id, int i
     return n;
 }
 
-__device__ void flush_passed(rsa_nam* open, int& n_open, int query_start, rsa_nam* out, int& n_out) {
+template <class OpenP, class OutP>
+__device__ void flush_passed(OpenP open, int& n_open, int query_start, OutP out, int& n_out) {
     for (int i = 0; i < n_open; ++i)
-        if (open[i].query_end < query_start) nam_emit(out, n_out, open[i]);
+        if (open[i].query_end < query_start) nam_emit(out, n_out, ld_nam(&open[i]));
     int w = 0;
     for (int i = 0; i < n_open; ++i)
-        if (!(open[i].query_end < query_start)) open[w++] = open[i];
+        if (!(open[i].query_end < query_start)) { if (w != i) st_nam(&open[w], ld_nam(&open[i])); w++; }
     n_open = w;
 }
 
 // add_to_hits_per_ref (nam.cpp:68-85): appends hits of one query randstrobe
-__device__ void add_hits(DMap& m, int orient, int qs, int qe, const SeedIndexParams& p, uint64_t pos, uint32_t count,
+template <class M>
+__device__ void add_hits(M& m, int orient, int qs, int qe, const SeedIndexParams& p, uint64_t pos, uint32_t count,
                          HitD* hits, int& n_hits, int& n_lists) {
     int min_diff = INT_MAX;
     for (uint64_t e = pos; e < pos + count; ++e) {
@@ -753,9 +811,10 @@ __device__ void add_hits(DMap& m, int orient, int qs, int qe, const SeedIndexPar
 }
 
 // next occupied slot >= slot (slot order = robin_hood iteration order), nwb if none
-__device__ __forceinline__ uint32_t rh_next_slot(const DMap& m, uint32_t slot) {
+template <class M>
+__device__ __forceinline__ uint32_t rh_next_slot(const M& m, uint32_t slot) {
     while (slot < m.nwb) {
-        if ((slot & 3) == 0 && *(const uint32_t*)(m.info + slot) == 0) { slot += 4; continue; }
+        if ((slot & 3) == 0 && *(const typename M::U32*)(m.info + slot) == 0) { slot += 4; continue; }
         if (m.info[slot]) return slot;
         ++slot;
     }
@@ -764,16 +823,17 @@ __device__ __forceinline__ uint32_t rh_next_slot(const DMap& m, uint32_t slot) {
 
 // merge_hits_into_nams (nam.cpp:370-536, sort=true) for one hit list (one
 // ref_id x orientation): emits into out[0..), nam_id = local index
-__device__ void merge_one_list(int32_t lid, int ref_id, int orient, const HitD* hits, int n_hits, int k,
-                               rsa_nam* open, rsa_nam* out, int& n_out) {
+template <class HitP, class OpenP, class OutP>
+__device__ void merge_one_list(int32_t lid, int ref_id, int orient, HitP hits, int n_hits, int k, OpenP open,
+                               OutP out, int& n_out) {
     int n_open = 0;
     unsigned prev_q_start = 0;
     for (int hi = 0; hi < n_hits; ++hi) {
-        const HitD x = hits[hi];
+        const HitD x = ld_hit(&hits[hi]);
         if (x.list != lid) continue;
         bool added = false;
         for (int o = 0; o < n_open; ++o) {
-            rsa_nam& on = open[o];
+            auto& on = open[o];
             if (on.query_prev_hit_startpos < x.qs && x.qs <= on.query_end && on.ref_prev_hit_startpos < x.rs &&
                 x.rs <= on.ref_end) {
                 if (x.qe > on.query_end && x.re > on.ref_end) {
@@ -786,24 +846,25 @@ __device__ void merge_one_list(int32_t lid, int ref_id, int orient, const HitD* 
                 }
             }
         }
-        if (!added) open[n_open++] = nam_from_hit(x, ref_id, orient);
+        if (!added) st_nam(&open[n_open++], nam_from_hit(x, ref_id, orient));
         if ((unsigned)x.qs > prev_q_start + (unsigned)k) {
             flush_passed(open, n_open, x.qs, out, n_out);
             prev_q_start = (unsigned)x.qs;
         }
     }
-    for (int o = 0; o < n_open; ++o) nam_emit(out, n_out, open[o]);
+    for (int o = 0; o < n_open; ++o) nam_emit(out, n_out, ld_nam(&open[o]));
 }
 
 // all lists of one orientation, in robin_hood slot order
-__device__ void merge_slow(const DMap& m, int orient, const HitD* hits, int n_hits, int k, rsa_nam* open,
-                           rsa_nam* out, int& n_out) {
+template <class M, class HitP, class OpenP, class OutP>
+__device__ void merge_slow(const M& m, int orient, HitP hits, int n_hits, int k, OpenP open, OutP out, int& n_out) {
     for (uint32_t slot = rh_next_slot(m, 0); slot < m.nwb; slot = rh_next_slot(m, slot + 1))
         merge_one_list(m.vals[slot] | (orient << 30), (int)m.keys[slot], orient, hits, n_hits, k, open, out, n_out);
 }
 
 // merge_hits_into_nams_fast (nam.cpp:117-366, sort=false)
-__device__ void merge_fast(const DMap& m, int orient, HitD* hits, int n_hits, int k, rsa_nam* open, uint8_t* added,
+template <class M>
+__device__ void merge_fast(const M& m, int orient, HitD* hits, int n_hits, int k, rsa_nam* open, uint8_t* added,
                            HitD* grp, rsa_nam* out, int& n_out) {
     for (uint32_t slot = rh_next_slot(m, 0); slot < m.nwb; slot = rh_next_slot(m, slot + 1)) {
         const int32_t lid = m.vals[slot] | (orient << 30);
@@ -968,6 +1029,11 @@ __device__ __forceinline__ int wave_excl_scan(int v, int lane, int& total) {
     return x - v;
 }
 
+#define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
+typedef __attribute__((address_space(3))) HitD LHit;
+typedef __attribute__((address_space(3))) rsa_nam LNam;
+typedef __attribute__((address_space(3))) int2 LInt2;
+
 __global__ void __launch_bounds__(64 * FN2_WAVES)
 k_find_nams_w2(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi,
                const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, const ReadStat* __restrict__ st,
@@ -989,7 +1055,10 @@ k_find_nams_w2(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __re
     }
     const int nq = (int)qcnt[r];
     const uint64_t base = qbase[r];
-    HitD* hits = s_hits[w];
+    LHit* hits = LDS_PTR(HitD, s_hits[w]);
+    LNam* open = LDS_PTR(rsa_nam, s_open[w]);
+    LNam* outl = LDS_PTR(rsa_nam, s_out[w]);
+    // 1. hits, in parallel over query randstrobes
     int off = 0;
     for (int i0 = 0; i0 < nq; i0 += 64) {
         const int i = i0 + lane;
@@ -1016,7 +1085,7 @@ k_find_nams_w2(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __re
                     hd.qs = qs; hd.qe = qe; hd.rs = rs0; hd.re = re0;
                     hd.list = (int32_t)(x.packed >> 8);          // key until lane 0 assigns list ids
                     hd.pad = q.is_reverse ? 1 : 0;
-                    hits[h++] = hd;
+                    st_hit(&hits[h++], hd);
                     min_diff = d;
                 }
             }
@@ -1025,18 +1094,22 @@ k_find_nams_w2(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __re
     }
     WSYNC_SEED();
     const int n_hits = off;
-    DMap m[2];
-    for (int o = 0; o < 2; ++o) {
-        uint8_t* bm = s_map[w] + (size_t)o * FN_MAP_CAP * 9;
-        m[o].cap = FN_MAP_CAP;
-        m[o].keys = (uint32_t*)bm; m[o].vals = (int32_t*)(bm + (size_t)FN_MAP_CAP * 4);
-        m[o].info = bm + (size_t)FN_MAP_CAP * 8;
-        m[o].info2 = nullptr; m[o].keys2 = nullptr; m[o].vals2 = nullptr;   // a rehash overflows -> fallback
+    // 2. the two robin_hood maps (fwd, rc) in LDS; hits of the fwd map come first
+    LMap m0, m1;
+    {
+        uint8_t* b0 = s_map[w];
+        uint8_t* b1 = s_map[w] + (size_t)FN_MAP_CAP * 9;
+        m0.cap = m1.cap = FN_MAP_CAP;
+        m0.keys = LDS_PTR(uint32_t, b0); m0.vals = LDS_PTR(int32_t, b0 + (size_t)FN_MAP_CAP * 4);
+        m0.info = LDS_PTR(uint8_t, b0 + (size_t)FN_MAP_CAP * 8);
+        m1.keys = LDS_PTR(uint32_t, b1); m1.vals = LDS_PTR(int32_t, b1 + (size_t)FN_MAP_CAP * 4);
+        m1.info = LDS_PTR(uint8_t, b1 + (size_t)FN_MAP_CAP * 8);
+        m0.info2 = m1.info2 = nullptr; m0.keys2 = m1.keys2 = nullptr; m0.vals2 = m1.vals2 = nullptr;  // rehash -> fallback
     }
     if (lane == 0) {
         nonrep[r] = rs.found > 0 ? (float)rs.good / (float)rs.found : 1.0f;   // nam.cpp:920
-        rh_new_reserved(m[0]);
-        rh_new_reserved(m[1]);
+        rh_new_reserved(m0);
+        rh_new_reserved(m1);
         int n_lists = 0, last_o = -1;
         uint32_t last_key = 0;
         int32_t last_lid = 0;
@@ -1045,15 +1118,15 @@ k_find_nams_w2(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __re
             const uint32_t key = (uint32_t)hits[h].list;
             if (orient != last_o || key != last_key) {      // operator[] on a present key changes nothing
                 bool ins;
-                last_lid = rh_get_or_insert(m[orient], key, n_lists, ins);
+                last_lid = orient ? rh_get_or_insert(m1, key, n_lists, ins) : rh_get_or_insert(m0, key, n_lists, ins);
                 if (ins) n_lists++;
                 last_o = orient; last_key = key;
             }
             hits[h].list = last_lid | (orient << 30);
         }
-        s_ctl[w][0] = (m[0].overflow || m[1].overflow) ? 1 : 0;
-        s_ctl[w][1] = (int)m[0].nwb;
-        s_ctl[w][2] = (int)m[1].nwb;
+        s_ctl[w][0] = (m0.overflow || m1.overflow) ? 1 : 0;
+        s_ctl[w][1] = (int)m0.nwb;
+        s_ctl[w][2] = (int)m1.nwb;
     }
     WSYNC_SEED();
     if (s_ctl[w][0]) {
@@ -1061,11 +1134,13 @@ k_find_nams_w2(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __re
         return;
     }
     // list order = occupied slots of the fwd map, then of the rc map (robin_hood iteration order)
-    int2* order = s_order[w];
+    LInt2* order = LDS_PTR(int2, s_order[w]);
     int nl = 0;
+#pragma unroll
     for (int o = 0; o < 2; ++o) {
+        const LMap& mo = o ? m1 : m0;
         const int nwb = s_ctl[w][1 + o];
-        const uint32_t word = lane * 4 < nwb ? ((const uint32_t*)m[o].info)[lane] : 0u;
+        const uint32_t word = lane * 4 < nwb ? ((const LMap::U32*)mo.info)[lane] : 0u;
         uint64_t mk[4];
         int occ = 0;
 #pragma unroll
@@ -1080,7 +1155,10 @@ k_find_nams_w2(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __re
         for (int bb = 0; bb < 4; ++bb) {
             if ((mk[bb] >> lane) & 1ull) {
                 const int slot = lane * 4 + bb;
-                if (nl + rank < 64) order[nl + rank] = make_int2(m[o].vals[slot] | (o << 30), (int)m[o].keys[slot]);
+                if (nl + rank < 64) {
+                    order[nl + rank].x = mo.vals[slot] | (o << 30);
+                    order[nl + rank].y = (int)mo.keys[slot];
+                }
                 rank++;
             }
         }
@@ -1091,29 +1169,29 @@ k_find_nams_w2(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __re
     if (nl > 64) {                                       // many lists: serial merge on lane 0
         if (lane == 0) {
             int n_out = 0;
-            merge_slow(m[0], 0, hits, n_hits, p.k, s_open[w], out, n_out);
-            merge_slow(m[1], 1, hits, n_hits, p.k, s_open[w], out, n_out);
+            merge_slow(m0, 0, hits, n_hits, p.k, open, out, n_out);
+            merge_slow(m1, 1, hits, n_hits, p.k, open, out, n_out);
             ncnt[r] = (uint32_t)n_out;
             flags[r] = 0;
         }
         return;
     }
-    // one lane per list: hits of the list, open/out NAM space at the list's hit offset
+    // 3. one lane per list: hits of the list, open/out NAM space at the list's hit offset
     int cnt = 0;
     int2 li = make_int2(0, 0);
     if (lane < nl) {
-        li = order[lane];
+        li.x = order[lane].x;
+        li.y = order[lane].y;
         for (int h = 0; h < n_hits; ++h) cnt += hits[h].list == li.x;
     }
     int tot;
     const int hb = wave_excl_scan(cnt, lane, tot);
     int n_out = 0;
-    if (lane < nl)
-        merge_one_list(li.x, li.y, (li.x >> 30) & 1, hits, n_hits, p.k, s_open[w] + hb, s_out[w] + hb, n_out);
+    if (lane < nl) merge_one_list(li.x, li.y, (li.x >> 30) & 1, hits, n_hits, p.k, open + hb, outl + hb, n_out);
     int total;
     const int ob = wave_excl_scan(n_out, lane, total);
     for (int i = 0; i < n_out; ++i) {
-        rsa_nam x = s_out[w][hb + i];
+        rsa_nam x = ld_nam(&outl[hb + i]);
         x.nam_id = ob + i;                                // nam_id = position in the read's NAM vector
         out[ob + i] = x;
     }
