@@ -18,22 +18,28 @@ namespace rsa {
 
 // ------------------------------------------------------------ sequences ---
 static const unsigned char* revcomp_table() {      // src/revcomp.hpp:10-27
-    static unsigned char t[256];
-    static bool init = false;
-    if (!init) {
-        for (int i = 0; i < 256; ++i) t[i] = 'N';
-        t['A'] = 'T'; t['C'] = 'G'; t['G'] = 'C'; t['T'] = 'A'; t['U'] = 'A';
-        t['a'] = 'T'; t['c'] = 'G'; t['g'] = 'C'; t['t'] = 'A'; t['u'] = 'A';
-        init = true;
-    }
-    return t;
+    struct Table {
+        unsigned char t[256];
+        Table() {
+            for (int i = 0; i < 256; ++i) t[i] = 'N';
+            t['A'] = 'T'; t['C'] = 'G'; t['G'] = 'C'; t['T'] = 'A'; t['U'] = 'A';
+            t['a'] = 'T'; t['c'] = 'G'; t['g'] = 'C'; t['t'] = 'A'; t['u'] = 'A';
+        }
+    };
+    static const Table table;                       // thread-safe one-time init
+    return table.t;
 }
 
 std::string reverse_complement(std::string_view s) {
-    const unsigned char* t = revcomp_table();
     std::string r(s.size(), 'N');
-    for (size_t i = 0; i < s.size(); ++i) r[i] = (char)t[(unsigned char)s[s.size() - 1 - i]];
+    reverse_complement_into(s, r.data());
     return r;
+}
+
+void reverse_complement_into(std::string_view s, char* out) {
+    const unsigned char* t = revcomp_table();
+    const size_t n = s.size();
+    for (size_t i = 0; i < n; ++i) out[i] = (char)t[(unsigned char)s[n - 1 - i]];
 }
 
 void to_uppercase(std::string& s) {
@@ -629,7 +635,7 @@ void collect_jobs_pe(AlignTmpRes& res, const Record&, const Record&, const Read&
 
 // part2_extend_seed_store_res (pc.cpp:177-212)
 static void store_extend(AlignTmpRes& res, size_t j, const Read& read, const References& refs,
-                         const AlignmentInfo& info) {
+                         AlignmentInfo& info) {
     const Nam& nam = res.todo_nams[j];
     const std::string& ref = refs.seqs[nam.ref_id];
     const size_t qsize = read.size();
@@ -640,7 +646,7 @@ static void store_extend(AlignTmpRes& res, size_t j, const Read& read, const Ref
     int result_ref_start = ref_start + (int)info.ref_start;
     int softclipped = (int)info.query_start + ((int)qsize - (int)info.query_end);
     Alignment& a = res.align_res[j];
-    a.cigar = info.cigar;
+    a.cigar = std::move(info.cigar);               // each result is stored exactly once
     a.edit_distance = (int)info.edit_distance;
     a.global_ed = (int)info.edit_distance + softclipped;
     a.score = info.sw_score;
@@ -654,23 +660,23 @@ static void store_extend(AlignTmpRes& res, size_t j, const Read& read, const Ref
 
 // part2_rescue_mate_store_res (pc.cpp:291-331)
 static void store_rescue(AlignTmpRes& res, size_t j, const Read& read, const References& refs, float mu, float sigma,
-                         const AlignmentInfo& info) {
+                         AlignmentInfo& info) {
     const Nam& nam = res.todo_nams[j];
     int ref_start, ref_end;
     rescue_window(nam, read.size(), mu, sigma, (int)refs.seqs[nam.ref_id].size(), ref_start, ref_end);
     Alignment& a = res.align_res[j];
-    a.cigar = info.cigar;
+    a.is_unaligned = info.cigar.empty();
+    a.cigar = std::move(info.cigar);               // each result is stored exactly once
     a.edit_distance = (int)info.edit_distance;
     a.score = info.sw_score;
     a.ref_start = ref_start + (int)info.ref_start;
     a.is_rc = !nam.is_rc;
     a.ref_id = nam.ref_id;
-    a.is_unaligned = info.cigar.empty();
     a.length = info.ref_span();
 }
 
 size_t store_results_pe(AlignTmpRes& res, const Read& read1, const Read& read2, const MapContext& mc, float mu,
-                        float sigma, const std::vector<AlignmentInfo>& infos, size_t pos) {
+                        float sigma, std::vector<AlignmentInfo>& infos, size_t pos) {
     const size_t n = res.todo_nams.size();
     auto rd = [&](size_t j) -> const Read& { return res.is_read1[j] ? read1 : read2; };
     if (res.type == 1 || res.type == 2) {
@@ -698,7 +704,7 @@ void collect_jobs_se(AlignTmpRes& res, const Read& read, const MapContext& mc, s
 }
 
 size_t store_results_se(AlignTmpRes& res, const Read& read, const MapContext& mc,
-                        const std::vector<AlignmentInfo>& infos, size_t pos) {
+                        std::vector<AlignmentInfo>& infos, size_t pos) {
     if (res.type != 4) return pos;
     for (size_t j = 0; j < res.todo_nams.size(); ++j)
         if (!res.done_align[j] && res.is_extend_seed[j]) store_extend(res, j, read, mc.refs, infos[pos++]);

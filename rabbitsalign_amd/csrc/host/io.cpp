@@ -46,6 +46,20 @@ void Cigar::to_string(std::string& out) const {    // cigar.cpp:45-51
     }
 }
 
+// to_m() (=/X -> M, merged by Cigar::push) printed directly
+void Cigar::to_m_string(std::string& out) const {
+    uint32_t cur = 0xff, len = 0;
+    for (uint32_t x : ops) {
+        uint32_t op = x & 0xf;
+        if (op == C_EQ || op == C_X) op = C_M;
+        if (op == cur) { len += x >> 4; continue; }
+        if (cur != 0xff) { append_uint(out, len); out.push_back("MIDNSHP=X"[cur]); }
+        cur = op;
+        len = x >> 4;
+    }
+    if (cur != 0xff) { append_uint(out, len); out.push_back("MIDNSHP=X"[cur]); }
+}
+
 // ------------------------------------------------------------------- SAM --
 static std::string_view strip_suffix(const std::string& name) {   // sam.cpp:29-40
     size_t len = name.size();
@@ -102,7 +116,7 @@ void Sam::add_unmapped_pair(const Record& r1, const Record& r2) {
     add_unmapped(r2, 1 | 4 | 8 | 0x80);
 }
 
-void Sam::add(const Alignment& a, const Record& r, const std::string& rc, uint8_t mapq, bool primary,
+void Sam::add(const Alignment& a, const Record& r, std::string_view rc, uint8_t mapq, bool primary,
               const Details& d) {                               // sam.cpp:124-139
     int flags = 0;
     if (!a.is_unaligned && a.is_rc) flags |= 0x10;
@@ -113,7 +127,7 @@ void Sam::add(const Alignment& a, const Record& r, const std::string& rc, uint8_
 
 void Sam::add_record(const std::string& qname, uint16_t flags, const std::string& rname, uint32_t pos, uint8_t mapq,
                      const Cigar& cigar, const std::string& mate_rname, uint32_t mate_pos, int32_t tlen,
-                     const std::string& seq, const std::string& seq_rc, const std::string& qual, int ed, int score,
+                     std::string_view seq, std::string_view seq_rc, const std::string& qual, int ed, int score,
                      const Details& d) {                        // sam.cpp:141-213
     std::string& o = out_;
     o.append(strip_suffix(qname));
@@ -128,7 +142,7 @@ void Sam::add_record(const std::string& qname, uint16_t flags, const std::string
     o += '\t';
     if (cigar.empty()) o += '*';
     else if (eqx_) cigar.to_string(o);
-    else cigar.to_m().to_string(o);
+    else cigar.to_m_string(o);
     o += '\t';
     o += mate_rname;
     o += '\t';
@@ -137,8 +151,8 @@ void Sam::add_record(const std::string& qname, uint16_t flags, const std::string
     append_int(o, tlen);
     o += '\t';
     if (flags & 0x100) o += '*';
-    else if (flags & 0x10) o.append(seq_rc.empty() ? "*" : seq_rc);
-    else o.append(seq.empty() ? "*" : seq);
+    else if (flags & 0x10) o.append(seq_rc.empty() ? std::string_view("*") : seq_rc);
+    else o.append(seq.empty() ? std::string_view("*") : seq);
     if (!(flags & 4)) {
         o += '\t';
         if (flags & 0x100) o += '*';
@@ -158,8 +172,8 @@ void Sam::add_record(const std::string& qname, uint16_t flags, const std::string
     o += tail_;
 }
 
-void Sam::add_pair(const Alignment& a1, const Alignment& a2, const Record& r1, const Record& r2, const std::string& rc1,
-                   const std::string& rc2, uint8_t mapq1, uint8_t mapq2, bool proper, bool primary,
+void Sam::add_pair(const Alignment& a1, const Alignment& a2, const Record& r1, const Record& r2, std::string_view rc1,
+                   std::string_view rc2, uint8_t mapq1, uint8_t mapq2, bool proper, bool primary,
                    const Details d[2]) {                        // sam.cpp:215-313
     int f1 = 1 | 0x40, f2 = 1 | 0x80;
     if (!primary) { f1 |= 0x100; f2 |= 0x100; }

@@ -63,7 +63,12 @@ struct PeChunk {
     // itself when upper-casing would not change it, else an upper-cased copy
     std::vector<const Record*> r1, r2;
     std::deque<Record> owned;
-    std::vector<std::string> rc1, rc2;        // their reverse complements, computed once
+    std::string rcbuf;                        // reverse complements of both mates, computed once:
+    std::vector<uint64_t> rcoff;              // read i mate m at rcoff[2i+m] (length = read length)
+    std::string_view rc(size_t i, int m) const {
+        const Record& r = m ? *r2[i] : *r1[i];
+        return std::string_view(rcbuf.data() + rcoff[2 * i + m], r.seq.size());
+    }
     std::vector<AlignTmpRes> res;
     SeedBatchOut seeds;                       // engine output of pe_seed
     std::minstd_rand rng;
@@ -97,13 +102,22 @@ void pe_load(PeChunk& c, const std::vector<Record>& a, const std::vector<Record>
         to_uppercase(c.owned.back().seq);
         return &c.owned.back();
     };
-    c.rc1.resize(n);
-    c.rc2.resize(n);
+    size_t tot = 0;
     for (size_t i = 0; i < n; ++i) {
         c.r1[i] = take(a[c.begin + i]);
         c.r2[i] = take(b[c.begin + i]);
-        c.rc1[i] = reverse_complement(c.r1[i]->seq);
-        c.rc2[i] = reverse_complement(c.r2[i]->seq);
+        tot += c.r1[i]->seq.size() + c.r2[i]->seq.size();
+    }
+    c.rcbuf.resize(tot);
+    c.rcoff.resize(2 * n);
+    size_t at = 0;
+    for (size_t i = 0; i < n; ++i) {
+        for (int m = 0; m < 2; ++m) {
+            const std::string& sq = m ? c.r2[i]->seq : c.r1[i]->seq;
+            c.rcoff[2 * i + m] = at;
+            reverse_complement_into(sq, &c.rcbuf[at]);
+            at += sq.size();
+        }
     }
     c.res.clear();
     c.res.resize(n);
@@ -137,7 +151,7 @@ void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize) {
             nams[m].assign(so.nams.begin() + (long)so.offsets[r], so.nams.begin() + (long)so.offsets[r + 1]);
             rescued[m] = so.rescued[r] != 0;
         }
-        const Read read1(c.r1[i]->seq, c.rc1[i]), read2(c.r2[i]->seq, c.rc2[i]);
+        const Read read1(c.r1[i]->seq, c.rc(i, 0)), read2(c.r2[i]->seq, c.rc(i, 1));
         align_PE_read_part(c.res[i], *c.r1[i], *c.r2[i], read1, read2, nams, rescued, c.stats, isize, mc, c.rng);
         c.stats.n_reads += 2;
     }
@@ -149,25 +163,25 @@ void pe_get_str(PeChunk& c, const MapContext& mc, float mu, float sigma, std::ve
     const auto t = Clock::now();
     jobs.clear();
     for (size_t i = 0; i < c.r1.size(); ++i) {
-        const Read read1(c.r1[i]->seq, c.rc1[i]), read2(c.r2[i]->seq, c.rc2[i]);
+        const Read read1(c.r1[i]->seq, c.rc(i, 0)), read2(c.r2[i]->seq, c.rc(i, 1));
         collect_jobs_pe(c.res[i], *c.r1[i], *c.r2[i], read1, read2, mc, mu, sigma, jobs);
     }
     c.times.collect += since(t);
 }
 
 void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistribution& isize,
-                   const std::vector<AlignmentInfo>& infos, const std::string& rg_id, std::string& out) {
+                   std::vector<AlignmentInfo>& infos, const std::string& rg_id, std::string& out) {
     const auto t = Clock::now();
     size_t pos = 0;
     for (size_t i = 0; i < c.r1.size(); ++i) {
-        const Read read1(c.r1[i]->seq, c.rc1[i]), read2(c.r2[i]->seq, c.rc2[i]);
+        const Read read1(c.r1[i]->seq, c.rc(i, 0)), read2(c.r2[i]->seq, c.rc(i, 1));
         pos = store_results_pe(c.res[i], read1, read2, mc, isize.mu, isize.sigma, infos, pos);
     }
     out.clear();
     out.reserve(7 * (size_t)mc.mparams.r * c.r1.size());
     Sam sam(out, mc.refs, mc.mparams.cigar_eqx, rg_id, mc.mparams.output_unmapped, mc.mparams.details);
     for (size_t i = 0; i < c.r1.size(); ++i) {
-        const Read read1(c.r1[i]->seq, c.rc1[i]), read2(c.r2[i]->seq, c.rc2[i]);
+        const Read read1(c.r1[i]->seq, c.rc(i, 0)), read2(c.r2[i]->seq, c.rc(i, 1));
         align_PE_read_last(c.res[i], *c.r1[i], *c.r2[i], read1, read2, sam, c.stats, isize, mc, c.rng);
     }
     c.times.last += since(t);

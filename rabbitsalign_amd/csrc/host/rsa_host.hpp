@@ -31,6 +31,7 @@ struct Cigar {                                  // src/cigar.hpp:23-93
     void append(const Cigar& o) { for (uint32_t x : o.ops) push(x & 0xf, x >> 4); }
     Cigar to_m() const;
     void to_string(std::string& out) const;
+    void to_m_string(std::string& out) const;   // to_m().to_string(out) without the temporary
 };
 
 // ---------------------------------------------------------------- types ---
@@ -56,13 +57,33 @@ struct Alignment {                              // src/sam.hpp:12-25
     bool gapped = false;
 };
 
+// std::vector<bool> semantics for the per-pair flag lists of AlignTmpRes,
+// inline for up to 128 entries (2 x max_tries + 2 with the default -M 20), so
+// a pair's bookkeeping does not allocate; longer lists spill to the heap.
+class BitVec {
+public:
+    void push_back(bool b) {
+        if (n_ < 128) { if (b) w_[n_ >> 6] |= 1ull << (n_ & 63); else w_[n_ >> 6] &= ~(1ull << (n_ & 63)); }
+        else spill_.push_back(b);
+        n_++;
+    }
+    bool operator[](size_t i) const { return i < 128 ? (w_[i >> 6] >> (i & 63)) & 1 : spill_[i - 128]; }
+    size_t size() const { return n_; }
+    bool empty() const { return n_ == 0; }
+    void clear() { n_ = 0; spill_.clear(); }
+private:
+    uint64_t w_[2] = {0, 0};
+    size_t n_ = 0;
+    std::vector<bool> spill_;
+};
+
 struct AlignTmpRes {                            // src/sam.hpp:27-45
     int type = 0;
     int mapq1 = 0, mapq2 = 0;
     int type4_loop_size = 0;
-    std::vector<bool> is_extend_seed, consistent_nam, is_read1;
+    BitVec is_extend_seed, consistent_nam, is_read1;
     std::vector<Nam> type4_nams, todo_nams;
-    std::vector<bool> done_align;
+    BitVec done_align;
     std::vector<Alignment> align_res;
 };
 
@@ -107,6 +128,7 @@ struct AlignmentStatistics {
 struct Record { std::string name, comment, seq, qual; };   // klibpp::KSeq fields used
 
 std::string reverse_complement(std::string_view s);
+void reverse_complement_into(std::string_view s, char* out);   // out holds s.size() bytes
 
 // Read (src/revcomp.hpp:41-55): a sequence and its reverse complement.  The
 // pipeline computes the rc once per read per chunk and hands out views.
@@ -114,10 +136,10 @@ struct Read {
 private:
     std::string own_;                           // rc when computed by this object
 public:
-    const std::string& seq;
-    const std::string& rc;
+    std::string_view seq;
+    std::string_view rc;
     explicit Read(const std::string& s) : own_(reverse_complement(s)), seq(s), rc(own_) {}
-    Read(const std::string& s, const std::string& rc_) : seq(s), rc(rc_) {}
+    Read(std::string_view s, std::string_view rc_) : seq(s), rc(rc_) {}
     Read(const Read&) = delete;
     Read& operator=(const Read&) = delete;
     size_t size() const { return seq.size(); }
@@ -216,10 +238,10 @@ void align_SE_read_last(AlignTmpRes& res, const Record& r, const Read& read, Sam
 void collect_jobs_pe(AlignTmpRes& res, const Record& r1, const Record& r2, const Read& read1, const Read& read2,
                      const MapContext& mc, float mu, float sigma, std::vector<SwJob>& jobs);
 size_t store_results_pe(AlignTmpRes& res, const Read& read1, const Read& read2, const MapContext& mc, float mu,
-                        float sigma, const std::vector<AlignmentInfo>& infos, size_t pos);
+                        float sigma, std::vector<AlignmentInfo>& infos, size_t pos);
 void collect_jobs_se(AlignTmpRes& res, const Read& read, const MapContext& mc, std::vector<SwJob>& jobs);
 size_t store_results_se(AlignTmpRes& res, const Read& read, const MapContext& mc,
-                        const std::vector<AlignmentInfo>& infos, size_t pos);
+                        std::vector<AlignmentInfo>& infos, size_t pos);
 
 // --------------------------------------------------------------- SAM -----
 std::string sam_header(const References& refs, const std::string& rg_id, const std::vector<std::string>& rg,
@@ -229,10 +251,10 @@ class Sam {                                     // src/sam.hpp:69-120
 public:
     Sam(std::string& out, const References& refs, bool eqx, const std::string& rg_id, bool output_unmapped,
         bool details);
-    void add(const Alignment& a, const Record& r, const std::string& rc, uint8_t mapq, bool primary,
+    void add(const Alignment& a, const Record& r, std::string_view rc, uint8_t mapq, bool primary,
              const Details& d);
     void add_pair(const Alignment& a1, const Alignment& a2, const Record& r1, const Record& r2,
-                  const std::string& rc1, const std::string& rc2, uint8_t mapq1, uint8_t mapq2, bool proper,
+                  std::string_view rc1, std::string_view rc2, uint8_t mapq1, uint8_t mapq2, bool proper,
                   bool primary, const Details d[2]);
     void add_unmapped(const Record& r, uint16_t flags = 4);
     void add_unmapped_pair(const Record& r1, const Record& r2);
@@ -241,7 +263,7 @@ public:
 private:
     void add_record(const std::string& qname, uint16_t flags, const std::string& rname, uint32_t pos, uint8_t mapq,
                     const Cigar& cigar, const std::string& mate_rname, uint32_t mate_pos, int32_t tlen,
-                    const std::string& seq, const std::string& seq_rc, const std::string& qual, int ed, int score,
+                    std::string_view seq, std::string_view seq_rc, const std::string& qual, int ed, int score,
                     const Details& d);
     std::string& out_;
     const References& refs_;
