@@ -493,55 +493,101 @@ __device__ __forceinline__ uint64_t upper_bound_hash(const rsa_ref_randstrobe* r
     return lo;
 }
 
+// hits (add_to_hits_per_ref order) of reads with at most LK_HCAP of them are
+// also written to a fixed per-read slot, so k_find_nams_w2 starts from them
+// instead of re-reading the index
+#define LK_HCAP 128
+
+__device__ __forceinline__ int wave_excl_scan_lk(int v, int lane, int& total) {
+    int x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    total = __shfl(x, 63, 64);
+    return x - v;
+}
+
 __global__ void __launch_bounds__(256)
 k_lookup(const rsa_query_randstrobe* __restrict__ qrs, const uint32_t* __restrict__ qcnt,
          const uint64_t* __restrict__ qbase, int n_reads, SeedIndexParams p, QrsInfo* __restrict__ qi,
-         ReadStat* __restrict__ st) {
+         ReadStat* __restrict__ st, HitD* __restrict__ hit_slots) {
     const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (wave >= n_reads) return;
     const int r = wave;
     const int nq = (int)qcnt[r];
     const uint64_t base = qbase[r];
+    HitD* slot = hit_slots + (size_t)r * LK_HCAP;
     uint32_t found = 0, good = 0, hfind = 0, hall = 0, sfind = 0, sall = 0;
-    for (int i = lane; i < nq; i += 64) {
-        const rsa_query_randstrobe q = qrs[base + i];
+    int hoff = 0;                                      // hits of the read written so far
+    for (int i0 = 0; i0 < nq; i0 += 64) {
+        const int i = i0 + lane;
         QrsInfo o;
         o.pos = END64; o.count = 0; o.hits = 0; o.flags = 0; o.pad = 0;
-        const uint64_t top = q.hash >> (64 - p.bits);
-        const uint64_t a = p.starts[top], b = p.starts[top + 1];
-        if (a != b) {
-            const uint64_t lo = lower_bound_hash(p.rs, a, b, q.hash);
-            if (lo < b && p.rs[lo].hash == q.hash) {
-                o.pos = lo;
-                o.flags = 1;
-                const uint64_t probe = lo + p.filter_cutoff;   // is_filtered (index.hpp:91-93)
-                const uint64_t h2 = probe < p.n ? p.rs[probe].hash : END64;
-                if (h2 == q.hash) o.flags |= 2;
-                const uint64_t ub = upper_bound_hash(p.rs, lo, b, q.hash);
-                o.count = (uint32_t)min<uint64_t>(ub - lo, 0xFFFFFFFFull);
-                if (o.count <= 1000) {
-                    // add_to_hits_per_ref min_diff filter (nam.cpp:68-85)
-                    int min_diff = INT_MAX;
-                    uint32_t h = 0;
-                    const int qspan = (int)q.end - (int)q.start;
-                    for (uint64_t e = lo; e < ub; ++e) {
-                        const rsa_ref_randstrobe x = p.rs[e];
-                        const int rspan = (int)(x.packed & 0xFF) + p.k;
-                        int d = qspan - rspan;
-                        d = d < 0 ? -d : d;
-                        if (d <= min_diff) { h++; min_diff = d; }
+        rsa_query_randstrobe q;
+        uint64_t lo = 0, ub = 0;
+        if (i < nq) {
+            q = qrs[base + i];
+            const uint64_t top = q.hash >> (64 - p.bits);
+            const uint64_t a = p.starts[top], b = p.starts[top + 1];
+            if (a != b) {
+                lo = lower_bound_hash(p.rs, a, b, q.hash);
+                if (lo < b && p.rs[lo].hash == q.hash) {
+                    o.pos = lo;
+                    o.flags = 1;
+                    const uint64_t probe = lo + p.filter_cutoff;   // is_filtered (index.hpp:91-93)
+                    const uint64_t h2 = probe < p.n ? p.rs[probe].hash : END64;
+                    if (h2 == q.hash) o.flags |= 2;
+                    ub = upper_bound_hash(p.rs, lo, b, q.hash);
+                    o.count = (uint32_t)min<uint64_t>(ub - lo, 0xFFFFFFFFull);
+                    if (o.count <= 1000) {
+                        // add_to_hits_per_ref min_diff filter (nam.cpp:68-85)
+                        int min_diff = INT_MAX;
+                        uint32_t h = 0;
+                        const int qspan = (int)q.end - (int)q.start;
+                        for (uint64_t e = lo; e < ub; ++e) {
+                            const rsa_ref_randstrobe x = p.rs[e];
+                            const int rspan = (int)(x.packed & 0xFF) + p.k;
+                            int d = qspan - rspan;
+                            d = d < 0 ? -d : d;
+                            if (d <= min_diff) { h++; min_diff = d; }
+                        }
+                        o.hits = h;
                     }
-                    o.hits = h;
+                    found++;
+                    const uint32_t scanned = o.count <= 1000 ? o.count : 0;
+                    if (!(o.flags & 2)) { good++; hfind += o.hits; sfind += scanned; }
+                    if (o.count <= 1000) hall += o.hits;
+                    sall += scanned;
                 }
-                found++;
-                const uint32_t scanned = o.count <= 1000 ? o.count : 0;
-                if (!(o.flags & 2)) { good++; hfind += o.hits; sfind += scanned; }
-                if (o.count <= 1000) hall += o.hits;
-                sall += scanned;
+            }
+            qi[base + i] = o;
+        }
+        // the non-filtered randstrobes' hits, in randstrobe order, into the read's slot
+        const bool emit = (o.flags & 1) && !(o.flags & 2) && o.hits > 0;
+        int tot;
+        const int at = hoff + wave_excl_scan_lk(emit ? (int)o.hits : 0, lane, tot);
+        if (emit && at + (int)o.hits <= LK_HCAP) {
+            const int qs = (int)q.start, qe = (int)q.end;
+            int min_diff = INT_MAX, h = at;
+            for (uint64_t e = lo; e < ub; ++e) {
+                const rsa_ref_randstrobe x = p.rs[e];
+                const int rs0 = (int)x.position;
+                const int re0 = rs0 + (int)(x.packed & 0xFF) + p.k;
+                int d = (qe - qs) - (re0 - rs0);
+                d = d < 0 ? -d : d;
+                if (d <= min_diff) {
+                    HitD hd;
+                    hd.qs = qs; hd.qe = qe; hd.rs = rs0; hd.re = re0;
+                    hd.list = (int32_t)(x.packed >> 8);
+                    hd.pad = q.is_reverse ? 1 : 0;
+                    slot[h++] = hd;
+                    min_diff = d;
+                }
             }
         }
-        qi[base + i] = o;
+        hoff += tot;
     }
     for (int off = 32; off > 0; off >>= 1) {
         found += __shfl_xor(found, off, 64);
@@ -1035,8 +1081,7 @@ typedef __attribute__((address_space(3))) rsa_nam LNam;
 typedef __attribute__((address_space(3))) int2 LInt2;
 
 __global__ void __launch_bounds__(64 * FN2_WAVES)
-k_find_nams_w2(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi,
-               const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, const ReadStat* __restrict__ st,
+k_find_nams_w2(const ReadStat* __restrict__ st, const HitD* __restrict__ hit_slots,
                const uint64_t* __restrict__ hoff, int n_reads, SeedIndexParams p, rsa_nam* __restrict__ nam_buf,
                uint32_t* __restrict__ ncnt, float* __restrict__ nonrep, uint32_t* __restrict__ flags) {
     __shared__ __attribute__((aligned(16))) uint8_t s_map[FN2_WAVES][2 * FN_MAP_CAP * 9];
@@ -1049,49 +1094,18 @@ k_find_nams_w2(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __re
     const int r = blockIdx.x * FN2_WAVES + w;
     if (r >= n_reads) return;                           // whole wave
     const ReadStat rs = st[r];
-    if (rs.hits_find > FN2_HCAP) {
+    if (rs.hits_find > FN2_HCAP || rs.hits_find > LK_HCAP) {
         if (lane == 0) { nonrep[r] = rs.found > 0 ? (float)rs.good / (float)rs.found : 1.0f; flags[r] = 2; ncnt[r] = 0; }
         return;
     }
-    const int nq = (int)qcnt[r];
-    const uint64_t base = qbase[r];
     LHit* hits = LDS_PTR(HitD, s_hits[w]);
     LNam* open = LDS_PTR(rsa_nam, s_open[w]);
     LNam* outl = LDS_PTR(rsa_nam, s_out[w]);
-    // 1. hits, in parallel over query randstrobes
-    int off = 0;
-    for (int i0 = 0; i0 < nq; i0 += 64) {
-        const int i = i0 + lane;
-        int nh = 0;
-        QrsInfo o;
-        rsa_query_randstrobe q;
-        if (i < nq) {
-            o = qi[base + i];
-            if ((o.flags & 1) && !(o.flags & 2)) { nh = (int)o.hits; q = qrs[base + i]; }
-        }
-        int tot;
-        const int at = off + wave_excl_scan(nh, lane, tot);
-        if (nh) {
-            const int qs = (int)q.start, qe = (int)q.end;
-            int min_diff = INT_MAX, h = at;
-            for (uint64_t e = o.pos; e < o.pos + o.count; ++e) {
-                const rsa_ref_randstrobe x = p.rs[e];
-                const int rs0 = (int)x.position;
-                const int re0 = rs0 + (int)(x.packed & 0xFF) + p.k;
-                int d = (qe - qs) - (re0 - rs0);
-                d = d < 0 ? -d : d;
-                if (d <= min_diff) {
-                    HitD hd;
-                    hd.qs = qs; hd.qe = qe; hd.rs = rs0; hd.re = re0;
-                    hd.list = (int32_t)(x.packed >> 8);          // key until lane 0 assigns list ids
-                    hd.pad = q.is_reverse ? 1 : 0;
-                    st_hit(&hits[h++], hd);
-                    min_diff = d;
-                }
-            }
-        }
-        off += tot;
-    }
+    // 1. the read's hits, written in add_to_hits_per_ref order by k_lookup
+    const int n_hits_w = (int)rs.hits_find;
+    const HitD* slot = hit_slots + (size_t)r * LK_HCAP;
+    for (int h = lane; h < n_hits_w; h += 64) st_hit(&hits[h], slot[h]);
+    const int off = n_hits_w;
     WSYNC_SEED();
     const int n_hits = off;
     // 2. the two robin_hood maps (fwd, rc) in LDS; hits of the fwd map come first
@@ -1348,14 +1362,14 @@ __global__ void k_compact(int n_reads, const uint64_t* __restrict__ hoff, const 
 // ---------------------------------------------------------------------------
 enum {
     B_SEQ, B_ROFF, B_RLEN, B_QBASE, B_QRS, B_QCNT, B_SYNC, B_QI, B_ST, B_HOFF, B_HITS, B_OPEN, B_NAM1, B_NCNT1,
-    B_NONREP, B_FLAGS, B_MAP, B_ROFF2, B_NAM2, B_NCNT2, B_LIST, B_RBUF, B_OUT, B_OOFF
+    B_NONREP, B_FLAGS, B_MAP, B_ROFF2, B_NAM2, B_NCNT2, B_LIST, B_RBUF, B_OUT, B_OOFF, B_SLOTS
 };
 enum { H_ST, H_HOFF, H_FLAGS, H_CNT, H_ROFF, H_LIST, H_OOFF, H_CNT2 };
 
 void seed_bufs_release(SeedBufs& b) {
-    for (int i = 0; i < 24; ++i) if (b.p[i]) (void)hipFree(b.p[i]);
+    for (int i = 0; i < 32; ++i) if (b.p[i]) (void)hipFree(b.p[i]);
     for (int i = 0; i < 8; ++i) if (b.h[i]) (void)hipHostFree(b.h[i]);
-    for (int i = 0; i < 24; ++i) { b.p[i] = nullptr; b.cap[i] = 0; }
+    for (int i = 0; i < 32; ++i) { b.p[i] = nullptr; b.cap[i] = 0; }
     for (int i = 0; i < 8; ++i) { b.h[i] = nullptr; b.hcap[i] = 0; }
     if (b.done) (void)hipEventDestroy(b.done);
     b.done = nullptr;
@@ -1493,8 +1507,10 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
     SCHK(dens(b, B_QI, sizeof(QrsInfo) * (qbase[n] + 1)));
     SCHK(dens(b, B_ST, sizeof(ReadStat) * n));
     kt.begin(st, RSA_K_LOOKUP);
+    SCHK(dens(b, B_SLOTS, sizeof(HitD) * LK_HCAP * (size_t)n));
     hipLaunchKernelGGL(k_lookup, dim3((n + 3) / 4), dim3(256), 0, st, DP(B_QRS, rsa_query_randstrobe),
-                       DP(B_QCNT, uint32_t), DP(B_QBASE, uint64_t), (int)n, p, DP(B_QI, QrsInfo), DP(B_ST, ReadStat));
+                       DP(B_QCNT, uint32_t), DP(B_QBASE, uint64_t), (int)n, p, DP(B_QI, QrsInfo), DP(B_ST, ReadStat),
+                       DP(B_SLOTS, HitD));
     SCHK(hipGetLastError());
     kt.end(st);
     SCHK(hens(b, H_ST, sizeof(ReadStat) * n));
@@ -1530,8 +1546,7 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
     kt.begin(st, RSA_K_FIND_NAMS);
     if (!seed_variant_lane("RSA_FN_LANE")) {
         hipLaunchKernelGGL(k_find_nams_w2, dim3((n + FN2_WAVES - 1) / FN2_WAVES), dim3(64 * FN2_WAVES), 0, st,
-                           DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t),
-                           DP(B_QBASE, uint64_t), DP(B_ST, ReadStat), DP(B_HOFF, uint64_t), (int)n, p,
+                           DP(B_ST, ReadStat), DP(B_SLOTS, HitD), DP(B_HOFF, uint64_t), (int)n, p,
                            DP(B_NAM1, rsa_nam), DP(B_NCNT1, uint32_t), DP(B_NONREP, float), DP(B_FLAGS, uint32_t));
     } else if (seed_variant_lane("RSA_FN_WAVE")) {
         hipLaunchKernelGGL(k_find_nams_w, dim3((n + FN_WAVES - 1) / FN_WAVES), dim3(64 * FN_WAVES), 0, st,
