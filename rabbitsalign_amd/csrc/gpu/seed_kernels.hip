@@ -701,7 +701,7 @@ __device__ void rh_insert_move(M& m, uint32_t key, int32_t val) {
 
 template <class M>
 __device__ void rh_rehash(M& m, uint32_t nb) {
-    if (!m.info2) { m.overflow = 1; return; }
+    if (!m.info2) { m.overflow = 1; m.max_allowed = 0xFFFFFFFFu; return; }   // (both fields stored: keeps the map in registers)
     typename M::U8* oi = m.info;
     typename M::U32* ok = m.keys;
     typename M::I32* ov = m.vals;
@@ -1050,20 +1050,31 @@ k_find_nams_w(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __res
 }
 
 // ---------------------------------------------------------------------------
-// k_find_nams_w2: one wavefront per read, everything the sequential merge
-// touches in LDS.
-//   1. lanes (one per query randstrobe) expand their index entries into hits
-//      in parallel: add_to_hits_per_ref's running min_diff filter per
-//      randstrobe, a wave prefix sum places every lane's hits at its offset,
-//      so the hit vector is in the reference's order (nam.cpp:68-85, 781-905)
-//   2. lane 0 inserts the keys into the two robin_hood emulations (LDS) and
-//      runs merge_hits_into_nams over LDS hits / open NAMs (nam.cpp:370-536);
-//      NAMs stream out to global memory
-// Reads with more than FN2_HCAP hits or whose maps would rehash are flagged
-// (flags = 2) for the global-scratch kernel above.
+// k_find_nams_w2: one wavefront per read, everything in LDS (≈8.7 KB a read,
+// so a CU keeps ~18 reads in flight).
+//   1. the read's hits, written by k_lookup in add_to_hits_per_ref order
+//      (nam.cpp:68-85, 781-905), are copied to LDS
+//   2. lane 0 inserts the keys into the two robin_hood emulations (LDS) in
+//      hit order; the occupied slots, fwd map then rc map, give the list order
+//      merge_hits_into_nams walks (nam.cpp:370-536)
+//   3. one lane per list runs the merge.  The maps are dead by then and their
+//      LDS holds the NAMs: a list with c hits creates at most c NAMs, so it
+//      owns c entries at its hit offset.  NAMs stay where they were created
+//      and carry the sequence number of their emission (flush of passed
+//      NAMs, then the final sweep), which is their place in the output; the
+//      open set is "created and not yet emitted", in creation order, exactly
+//      the reference's open_nams vector.
+// Reads with more than FN2_HCAP hits or whose maps would rehash past
+// FN_MAP_CAP are flagged (flags = 2) for the global-scratch kernel above.
 // ---------------------------------------------------------------------------
-#define FN2_WAVES 4
+#define FN2_WAVES 2
 #define FN2_HCAP 128
+#define FN2_MAPB (2 * FN_MAP_CAP * 9)
+
+struct __attribute__((aligned(16))) SeqNam {   // a NAM under construction (nam.hpp:11-38 fields)
+    int32_t qs, qe, qprev, rs, re, rprev, n_hits, seq;   // seq < 0: open
+};
+static_assert(FN2_HCAP * sizeof(SeqNam) <= FN2_MAPB, "NAM store shares the maps' LDS");
 
 __device__ __forceinline__ int wave_excl_scan(int v, int lane, int& total) {
     int x = v;
@@ -1077,18 +1088,75 @@ __device__ __forceinline__ int wave_excl_scan(int v, int lane, int& total) {
 
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 typedef __attribute__((address_space(3))) HitD LHit;
-typedef __attribute__((address_space(3))) rsa_nam LNam;
+typedef __attribute__((address_space(3))) SeqNam LSeq;
 typedef __attribute__((address_space(3))) int2 LInt2;
+
+// merge_hits_into_nams for one list (nam.cpp:370-536); returns the NAMs emitted
+__device__ int merge_list_seq(int32_t lid, const LHit* hits, int n_hits, int k, LSeq* a, int& n_created) {
+    int n_out = 0, first_open = 0;
+    n_created = 0;
+    unsigned prev_q_start = 0;
+    for (int hi = 0; hi < n_hits; ++hi) {
+        if (hits[hi].list != lid) continue;
+        const int xqs = hits[hi].qs, xqe = hits[hi].qe, xrs = hits[hi].rs, xre = hits[hi].re;
+        bool added = false;
+        for (int o = first_open; o < n_created; ++o) {
+            LSeq& on = a[o];
+            if (on.seq >= 0) continue;
+            if (on.qprev < xqs && xqs <= on.qe && on.rprev < xrs && xrs <= on.re) {
+                if (xqe > on.qe && xre > on.re) {
+                    on.qe = xqe; on.re = xre; on.qprev = xqs; on.rprev = xrs; on.n_hits++;
+                    added = true; break;
+                } else if (xqe <= on.qe && xre <= on.re) {
+                    on.qprev = xqs; on.rprev = xrs; on.n_hits++;
+                    added = true; break;
+                }
+            }
+        }
+        if (!added) {
+            LSeq& nn = a[n_created++];
+            nn.qs = xqs; nn.qe = xqe; nn.qprev = xqs; nn.rs = xrs; nn.re = xre; nn.rprev = xrs;
+            nn.n_hits = 1; nn.seq = -1;
+        }
+        if ((unsigned)xqs > prev_q_start + (unsigned)k) {      // emit the NAMs the query has passed
+            for (int o = first_open; o < n_created; ++o)
+                if (a[o].seq < 0 && a[o].qe < xqs) a[o].seq = n_out++;
+            while (first_open < n_created && a[first_open].seq >= 0) first_open++;
+            prev_q_start = (unsigned)xqs;
+        }
+    }
+    for (int o = first_open; o < n_created; ++o)
+        if (a[o].seq < 0) a[o].seq = n_out++;
+    return n_out;
+}
+
+// inserts the keys of one orientation's hits (operator[], nam.cpp:68-85) and
+// rewrites their list field to the list id | orientation << 30
+__device__ __forceinline__ void map_insert_hits(LMap& m, int orient, LHit* hits, int n_hits) {
+    rh_new_reserved(m);
+    int n_lists = 0;
+    uint32_t last_key = 0;
+    int32_t last_lid = -1;
+    for (int h = 0; h < n_hits; ++h) {
+        if (hits[h].pad != orient) continue;
+        const uint32_t key = (uint32_t)hits[h].list;
+        if (last_lid < 0 || key != last_key) {          // operator[] on a present key changes nothing
+            bool ins;
+            last_lid = rh_get_or_insert(m, key, n_lists, ins);
+            if (ins) n_lists++;
+            last_key = key;
+        }
+        hits[h].list = last_lid | (orient << 30);
+    }
+}
 
 __global__ void __launch_bounds__(64 * FN2_WAVES)
 k_find_nams_w2(const ReadStat* __restrict__ st, const HitD* __restrict__ hit_slots,
                const uint64_t* __restrict__ hoff, int n_reads, SeedIndexParams p, rsa_nam* __restrict__ nam_buf,
                uint32_t* __restrict__ ncnt, float* __restrict__ nonrep, uint32_t* __restrict__ flags) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_map[FN2_WAVES][2 * FN_MAP_CAP * 9];
+    __shared__ __attribute__((aligned(16))) uint8_t s_map[FN2_WAVES][FN2_MAPB];   // maps, then NAMs
     __shared__ HitD s_hits[FN2_WAVES][FN2_HCAP];
-    __shared__ rsa_nam s_open[FN2_WAVES][FN2_HCAP];
-    __shared__ rsa_nam s_out[FN2_WAVES][FN2_HCAP];
-    __shared__ int2 s_order[FN2_WAVES][64];
+    __shared__ int2 s_order[FN2_WAVES][FN2_HCAP];
     __shared__ int s_ctl[FN2_WAVES][4];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int r = blockIdx.x * FN2_WAVES + w;
@@ -1099,16 +1167,12 @@ k_find_nams_w2(const ReadStat* __restrict__ st, const HitD* __restrict__ hit_slo
         return;
     }
     LHit* hits = LDS_PTR(HitD, s_hits[w]);
-    LNam* open = LDS_PTR(rsa_nam, s_open[w]);
-    LNam* outl = LDS_PTR(rsa_nam, s_out[w]);
     // 1. the read's hits, written in add_to_hits_per_ref order by k_lookup
-    const int n_hits_w = (int)rs.hits_find;
+    const int n_hits = (int)rs.hits_find;
     const HitD* slot = hit_slots + (size_t)r * LK_HCAP;
-    for (int h = lane; h < n_hits_w; h += 64) st_hit(&hits[h], slot[h]);
-    const int off = n_hits_w;
+    for (int h = lane; h < n_hits; h += 64) st_hit(&hits[h], slot[h]);
     WSYNC_SEED();
-    const int n_hits = off;
-    // 2. the two robin_hood maps (fwd, rc) in LDS; hits of the fwd map come first
+    // 2. the two robin_hood maps (fwd, rc) in LDS
     LMap m0, m1;
     {
         uint8_t* b0 = s_map[w];
@@ -1122,22 +1186,11 @@ k_find_nams_w2(const ReadStat* __restrict__ st, const HitD* __restrict__ hit_slo
     }
     if (lane == 0) {
         nonrep[r] = rs.found > 0 ? (float)rs.good / (float)rs.found : 1.0f;   // nam.cpp:920
-        rh_new_reserved(m0);
-        rh_new_reserved(m1);
-        int n_lists = 0, last_o = -1;
-        uint32_t last_key = 0;
-        int32_t last_lid = 0;
-        for (int h = 0; h < n_hits; ++h) {
-            const int orient = hits[h].pad;
-            const uint32_t key = (uint32_t)hits[h].list;
-            if (orient != last_o || key != last_key) {      // operator[] on a present key changes nothing
-                bool ins;
-                last_lid = orient ? rh_get_or_insert(m1, key, n_lists, ins) : rh_get_or_insert(m0, key, n_lists, ins);
-                if (ins) n_lists++;
-                last_o = orient; last_key = key;
-            }
-            hits[h].list = last_lid | (orient << 30);
-        }
+        // each map sees its own keys in hit order, which fixes its slot layout; list
+        // ids only have to be distinct, so each map numbers its lists itself and one
+        // pass per orientation keeps the map state in registers
+        map_insert_hits(m0, 0, hits, n_hits);
+        map_insert_hits(m1, 1, hits, n_hits);
         s_ctl[w][0] = (m0.overflow || m1.overflow) ? 1 : 0;
         s_ctl[w][1] = (int)m0.nwb;
         s_ctl[w][2] = (int)m1.nwb;
@@ -1147,14 +1200,17 @@ k_find_nams_w2(const ReadStat* __restrict__ st, const HitD* __restrict__ hit_slo
         if (lane == 0) { flags[r] = 2; ncnt[r] = 0; }
         return;
     }
-    // list order = occupied slots of the fwd map, then of the rc map (robin_hood iteration order)
+    // list order = occupied slots of the fwd map, then of the rc map (robin_hood iteration order);
+    // every list holds at least one hit, so there are at most FN2_HCAP of them
     LInt2* order = LDS_PTR(int2, s_order[w]);
     int nl = 0;
 #pragma unroll
     for (int o = 0; o < 2; ++o) {
-        const LMap& mo = o ? m1 : m0;
+        const LMap::U8* minfo = o ? m1.info : m0.info;
+        const LMap::U32* mkeys = o ? m1.keys : m0.keys;
+        const LMap::I32* mvals = o ? m1.vals : m0.vals;
         const int nwb = s_ctl[w][1 + o];
-        const uint32_t word = lane * 4 < nwb ? ((const LMap::U32*)mo.info)[lane] : 0u;
+        const uint32_t word = lane * 4 < nwb ? ((const LMap::U32*)minfo)[lane] : 0u;
         uint64_t mk[4];
         int occ = 0;
 #pragma unroll
@@ -1169,47 +1225,50 @@ k_find_nams_w2(const ReadStat* __restrict__ st, const HitD* __restrict__ hit_slo
         for (int bb = 0; bb < 4; ++bb) {
             if ((mk[bb] >> lane) & 1ull) {
                 const int slot = lane * 4 + bb;
-                if (nl + rank < 64) {
-                    order[nl + rank].x = mo.vals[slot] | (o << 30);
-                    order[nl + rank].y = (int)mo.keys[slot];
+                if (nl + rank < FN2_HCAP) {
+                    order[nl + rank].x = mvals[slot] | (o << 30);
+                    order[nl + rank].y = (int)mkeys[slot];
                 }
                 rank++;
             }
         }
         nl += occ;
     }
-    WSYNC_SEED();
+    WSYNC_SEED();                                        // maps dead from here: their LDS holds NAMs
+    LSeq* store = LDS_PTR(SeqNam, s_map[w]);
     rsa_nam* out = nam_buf + hoff[r];
-    if (nl > 64) {                                       // many lists: serial merge on lane 0
-        if (lane == 0) {
-            int n_out = 0;
-            merge_slow(m0, 0, hits, n_hits, p.k, open, out, n_out);
-            merge_slow(m1, 1, hits, n_hits, p.k, open, out, n_out);
-            ncnt[r] = (uint32_t)n_out;
-            flags[r] = 0;
+    // 3. one lane per list, 64 lists a round
+    int hbase = 0, obase = 0;
+    for (int l0 = 0; l0 < nl; l0 += 64) {
+        const int l = l0 + lane;
+        int cnt = 0;
+        int2 li = make_int2(0, 0);
+        if (l < nl) {
+            li.x = order[l].x;
+            li.y = order[l].y;
+            for (int h = 0; h < n_hits; ++h) cnt += hits[h].list == li.x;
         }
-        return;
+        int tot;
+        const int hb = hbase + wave_excl_scan(cnt, lane, tot);
+        hbase += tot;
+        int n_out = 0, n_created = 0;
+        if (l < nl) n_out = merge_list_seq(li.x, hits, n_hits, p.k, store + hb, n_created);
+        int total;
+        const int ob = obase + wave_excl_scan(n_out, lane, total);
+        obase += total;
+        const int orient = (li.x >> 30) & 1;
+        for (int c = 0; c < n_created; ++c) {
+            const LSeq& s = store[hb + c];
+            rsa_nam x;
+            x.nam_id = ob + s.seq;                        // position in the read's NAM vector
+            x.query_start = s.qs; x.query_end = s.qe; x.query_prev_hit_startpos = s.qprev;
+            x.ref_start = s.rs; x.ref_end = s.re; x.ref_prev_hit_startpos = s.rprev;
+            x.n_hits = s.n_hits; x.ref_id = li.y; x.score = 0.0f; x.is_rc = orient;
+            x.score = nam_score(x);
+            out[x.nam_id] = x;
+        }
     }
-    // 3. one lane per list: hits of the list, open/out NAM space at the list's hit offset
-    int cnt = 0;
-    int2 li = make_int2(0, 0);
-    if (lane < nl) {
-        li.x = order[lane].x;
-        li.y = order[lane].y;
-        for (int h = 0; h < n_hits; ++h) cnt += hits[h].list == li.x;
-    }
-    int tot;
-    const int hb = wave_excl_scan(cnt, lane, tot);
-    int n_out = 0;
-    if (lane < nl) merge_one_list(li.x, li.y, (li.x >> 30) & 1, hits, n_hits, p.k, open + hb, outl + hb, n_out);
-    int total;
-    const int ob = wave_excl_scan(n_out, lane, total);
-    for (int i = 0; i < n_out; ++i) {
-        rsa_nam x = ld_nam(&outl[hb + i]);
-        x.nam_id = ob + i;                                // nam_id = position in the read's NAM vector
-        out[ob + i] = x;
-    }
-    if (lane == 0) { ncnt[r] = (uint32_t)total; flags[r] = 0; }
+    if (lane == 0) { ncnt[r] = (uint32_t)obase; flags[r] = 0; }
 }
 
 // ---------------------------------------------------------------------------
