@@ -42,6 +42,7 @@ WORKLOADS = {
 }
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
+DP_PEAK_GCELLS = 6500.0        # packed-i16 DP cell updates/s model ceiling
 REF_CPU_LIB = os.path.join(ROOT, "oracle", "_ref", "librsalign_ref.so")
 
 
@@ -67,7 +68,10 @@ def pmc_traffic(symbol: str):
     try:
         with open(TRAFFIC_JSON) as f:
             t = json.load(f)
-        v = t["traffic_per_launch"].get(symbol)
+        per = t["traffic_per_launch"]
+        # rocprof names carry the return type and template arguments ("void k_ext_scan<4, 2>")
+        base = lambda n: n.split("(")[0].split("<")[0].split()[-1]
+        v = per.get(symbol) or next((per[n] for n in per if base(n) == symbol), None)
         return (round(v["bytes"], 1) if v and v.get("bytes") is not None else None), t.get("source")
     except (OSError, ValueError, KeyError):
         return None, None
@@ -100,6 +104,9 @@ def roofline(ks: dict) -> dict:
     if name == "ext_scan" and ks.get("dp_cells"):
         # the DP scan is integer-VALU bound; cells/s is its natural throughput figure
         out["dp_gcells_per_s"] = round(ks["dp_cells"] / (k["ms"] * 1e-3) / 1e9, 2)
+        # VALU view: ~6.5 T cell-updates/s for packed-i16 Gotoh on 256 CUs
+        out["valu"] = {"achieved_gcells_per_s": out["dp_gcells_per_s"], "model_peak_gcells_per_s": DP_PEAK_GCELLS,
+                       "frac": round(out["dp_gcells_per_s"] / DP_PEAK_GCELLS, 4)}
     return out
 
 

@@ -6,7 +6,7 @@ TAG=${1:-r1}
 shift
 O=gpurun_out/$TAG
 mkdir -p $O
-timeout -k 10 500 python -m pytest tests -m gpu -x -q > $O/pytest_gpu.log 2>&1 && \
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 && \
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
 timeout -k 10 600 python bench.py --stats-out $O/stats_full.json > $O/bench_full.json 2> $O/bench_full.err
 rc=$?
