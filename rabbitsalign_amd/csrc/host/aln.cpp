@@ -11,6 +11,7 @@
 #include <unordered_set>
 
 #include <emmintrin.h>
+#include <tmmintrin.h>
 
 #include "rsa_host.hpp"
 
@@ -36,10 +37,53 @@ std::string reverse_complement(std::string_view s) {
     return r;
 }
 
-void reverse_complement_into(std::string_view s, char* out) {
+// 16 bytes per step: pshufb complements by the low nibble (A=0x41 C=0x43
+// G=0x47 T=0x54 are distinct there) and reverses the block; a block holding
+// anything but upper-case ACGT takes the table.
+__attribute__((target("ssse3"))) static void rc_ssse3(const char* s, size_t n, char* out) {
     const unsigned char* t = revcomp_table();
+    const __m128i rev = _mm_setr_epi8(15, 14, 13, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0);
+    const __m128i lut = _mm_setr_epi8(0, 'T', 0, 'G', 'A', 0, 0, 'C', 0, 0, 0, 0, 0, 0, 0, 0);
+    const __m128i lo = _mm_set1_epi8(0x0F);
+    const __m128i cA = _mm_set1_epi8('A'), cC = _mm_set1_epi8('C'), cG = _mm_set1_epi8('G'), cT = _mm_set1_epi8('T');
+    size_t i = 0;
+    for (; i + 16 <= n; i += 16) {
+        const char* src = s + n - i - 16;
+        const __m128i v = _mm_loadu_si128((const __m128i*)src);
+        const __m128i ok = _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(v, cA), _mm_cmpeq_epi8(v, cC)),
+                                        _mm_or_si128(_mm_cmpeq_epi8(v, cG), _mm_cmpeq_epi8(v, cT)));
+        if (_mm_movemask_epi8(ok) == 0xFFFF) {
+            const __m128i c = _mm_shuffle_epi8(lut, _mm_and_si128(v, lo));
+            _mm_storeu_si128((__m128i*)(out + i), _mm_shuffle_epi8(c, rev));
+        } else {
+            for (int j = 0; j < 16; ++j) out[i + j] = (char)t[(unsigned char)src[15 - j]];
+        }
+    }
+    for (; i < n; ++i) out[i] = (char)t[(unsigned char)s[n - 1 - i]];
+}
+
+__attribute__((target("ssse3"))) static void rev_ssse3(const char* s, size_t n, char* out) {
+    const __m128i rev = _mm_setr_epi8(15, 14, 13, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0);
+    size_t i = 0;
+    for (; i + 16 <= n; i += 16)
+        _mm_storeu_si128((__m128i*)(out + i),
+                         _mm_shuffle_epi8(_mm_loadu_si128((const __m128i*)(s + n - i - 16)), rev));
+    for (; i < n; ++i) out[i] = s[n - 1 - i];
+}
+
+static const bool g_ssse3 = __builtin_cpu_supports("ssse3");
+
+void reverse_complement_into(std::string_view s, char* out) {
     const size_t n = s.size();
+    if (g_ssse3) { rc_ssse3(s.data(), n, out); return; }
+    const unsigned char* t = revcomp_table();
     for (size_t i = 0; i < n; ++i) out[i] = (char)t[(unsigned char)s[n - 1 - i]];
+}
+
+void reverse_into(std::string_view s, char* out) {
+    const size_t n = s.size();
+    if (g_ssse3) { rev_ssse3(s.data(), n, out); return; }
+    for (size_t i = 0; i < n; ++i) out[i] = s[n - 1 - i];
 }
 
 void to_uppercase(std::string& s) {
@@ -71,7 +115,7 @@ static bool by_score(const T& a, const T& b) { return a.score > b.score; }
 // aln.cpp:60-93
 static bool reverse_nam_if_needed(Nam& nam, const Read& read, const References& refs, int k) {
     const size_t read_len = read.size();
-    std::string_view ref = refs.seqs[nam.ref_id];
+    std::string_view ref = refs.seq(nam.ref_id);
     std::string_view ref_start_kmer = sub(ref, (size_t)nam.ref_start, (size_t)k);
     std::string_view ref_end_kmer = sub(ref, (size_t)(nam.ref_end - k), (size_t)k);
     std::string_view seq, seq_rc;
@@ -135,7 +179,15 @@ static std::vector<NamPair> get_best_scoring_nam_pairs(const std::vector<Nam>& n
     std::vector<NamPair> joint;
     if (nams1.empty() && nams2.empty()) return joint;
     joint.reserve(nams1.size() + nams2.size());
-    std::unordered_set<int> added_n1, added_n2;
+    // membership by nam_id (the NAM's index in its read's list) instead of a hash set
+    thread_local std::vector<uint8_t> added_n1, added_n2;
+    auto reset_ids = [](std::vector<uint8_t>& v, const std::vector<Nam>& ns) {
+        int mx = -1;
+        for (const Nam& n : ns) mx = std::max(mx, n.nam_id);
+        v.assign((size_t)(mx + 1), 0);
+    };
+    reset_ids(added_n1, nams1);
+    reset_ids(added_n2, nams2);
     int best_joint_hits = 0;
     std::vector<Nam> sorted2[2];
     for (const auto& n2 : nams2) sorted2[n2.is_rc ? 1 : 0].push_back(n2);
@@ -168,8 +220,8 @@ static std::vector<NamPair> get_best_scoring_nam_pairs(const std::vector<Nam>& n
                 bool r2_r1 = (a - b >= 0) && (a - b < mu + 10 * sigma);
                 if (r2_r1) {
                     joint.push_back(NamPair{joint_hits, nam1, nam2});
-                    added_n1.insert(nam1.nam_id);
-                    added_n2.insert(nam2.nam_id);
+                    added_n1[nam1.nam_id] = 1;
+                    added_n2[nam2.nam_id] = 1;
                 }
             }
         } else {
@@ -193,8 +245,8 @@ static std::vector<NamPair> get_best_scoring_nam_pairs(const std::vector<Nam>& n
                 bool r1_r2 = (b - a >= 0) && (b - a < mu + 10 * sigma);
                 if (r1_r2) {
                     joint.push_back(NamPair{joint_hits, nam1, nam2});
-                    added_n1.insert(nam1.nam_id);
-                    added_n2.insert(nam2.nam_id);
+                    added_n1[nam1.nam_id] = 1;
+                    added_n2[nam2.nam_id] = 1;
                 }
             }
         }
@@ -205,7 +257,7 @@ static std::vector<NamPair> get_best_scoring_nam_pairs(const std::vector<Nam>& n
         int best1 = best_joint_hits > 0 ? best_joint_hits : nams1[0].n_hits;
         for (const auto& nam1 : nams1) {
             if (nam1.n_hits < best1 / 2) break;
-            if (added_n1.count(nam1.nam_id)) continue;
+            if (added_n1[nam1.nam_id]) continue;
             joint.push_back(NamPair{nam1.n_hits, nam1, dummy});
         }
     }
@@ -213,7 +265,7 @@ static std::vector<NamPair> get_best_scoring_nam_pairs(const std::vector<Nam>& n
         int best2 = best_joint_hits > 0 ? best_joint_hits : nams2[0].n_hits;
         for (const auto& nam2 : nams2) {
             if (nam2.n_hits < best2 / 2) break;
-            if (added_n2.count(nam2.nam_id)) continue;
+            if (added_n2[nam2.nam_id]) continue;
             joint.push_back(NamPair{nam2.n_hits, dummy, nam2});
         }
     }
@@ -307,7 +359,7 @@ static AlignmentInfo hamming_align(size_t n, const int* mm, int n_mm, int match,
 static bool extend_seed_part(AlignTmpRes& res, const AlignmentParameters& ap, const Nam& nam, const References& refs,
                              const Read& read, bool consistent_nam) {
     std::string_view query = nam.is_rc ? std::string_view(read.rc) : std::string_view(read.seq);
-    std::string_view ref = refs.seqs[nam.ref_id];
+    std::string_view ref = refs.seq(nam.ref_id);
     const auto projected_ref_start = std::max(0, nam.ref_start - nam.query_start);
     const auto projected_ref_end = std::min(nam.ref_end + query.size() - nam.query_end, ref.size());
     AlignmentInfo info;
@@ -385,7 +437,7 @@ static bool rescue_mate_part(AlignTmpRes& res, const Nam& nam, const References&
     Alignment alignment;
     const size_t read_len = read.size();
     std::string_view r_tmp = nam.is_rc ? std::string_view(read.seq) : std::string_view(read.rc);
-    const int ref_len = (int)refs.seqs[nam.ref_id].size();
+    const int ref_len = (int)refs.seq(nam.ref_id).size();
     int ref_start, ref_end;
     rescue_window(nam, read_len, mu, sigma, ref_len, ref_start, ref_end);
     res.todo_nams.push_back(nam);
@@ -403,7 +455,7 @@ static bool rescue_mate_part(AlignTmpRes& res, const Nam& nam, const References&
         return true;
     };
     if (ref_end < ref_start + k) return unaligned();
-    std::string_view segm = sub(refs.seqs[nam.ref_id], (size_t)ref_start, (size_t)(ref_end - ref_start));
+    std::string_view segm = sub(refs.seq(nam.ref_id), (size_t)ref_start, (size_t)(ref_end - ref_start));
     if (!has_shared_substring(r_tmp, segm, k)) return unaligned();
     res.done_align.push_back(false);
     res.align_res.push_back(alignment);
@@ -589,7 +641,7 @@ void align_SE_read_part(AlignTmpRes& res, const Record&, const Read& read, std::
 // part2_extend_seed_get_str (pc.cpp:214-242)
 static void extend_job(const Nam& nam, const Read& read, const References& refs, std::vector<SwJob>& jobs) {
     std::string_view query = nam.is_rc ? std::string_view(read.rc) : std::string_view(read.seq);
-    const std::string& ref = refs.seqs[nam.ref_id];
+    const std::string_view ref = refs.seq(nam.ref_id);
     const auto projected_ref_start = std::max(0, nam.ref_start - nam.query_start);
     const int diff = std::abs((nam.ref_end - nam.ref_start) - (nam.query_end - nam.query_start));
     const int ext_left = std::min(50, projected_ref_start);
@@ -605,8 +657,8 @@ static void rescue_job(const Nam& nam, const Read& read, const References& refs,
                        std::vector<SwJob>& jobs) {
     std::string_view r_tmp = nam.is_rc ? std::string_view(read.seq) : std::string_view(read.rc);
     int ref_start, ref_end;
-    rescue_window(nam, read.size(), mu, sigma, (int)refs.seqs[nam.ref_id].size(), ref_start, ref_end);
-    const size_t clen = refs.seqs[nam.ref_id].size();
+    rescue_window(nam, read.size(), mu, sigma, (int)refs.seq(nam.ref_id).size(), ref_start, ref_end);
+    const size_t clen = refs.seq(nam.ref_id).size();
     size_t start = std::min((size_t)ref_start, clen);
     size_t len = std::min((size_t)(ref_end - ref_start), clen - start);
     jobs.push_back(SwJob{r_tmp, nam.ref_id, (uint32_t)start, (uint32_t)len});
@@ -637,7 +689,7 @@ void collect_jobs_pe(AlignTmpRes& res, const Record&, const Record&, const Read&
 static void store_extend(AlignTmpRes& res, size_t j, const Read& read, const References& refs,
                          AlignmentInfo& info) {
     const Nam& nam = res.todo_nams[j];
-    const std::string& ref = refs.seqs[nam.ref_id];
+    const std::string_view ref = refs.seq(nam.ref_id);
     const size_t qsize = read.size();
     const auto projected_ref_start = std::max(0, nam.ref_start - nam.query_start);
     const int ext_left = std::min(50, projected_ref_start);
@@ -663,7 +715,7 @@ static void store_rescue(AlignTmpRes& res, size_t j, const Read& read, const Ref
                          AlignmentInfo& info) {
     const Nam& nam = res.todo_nams[j];
     int ref_start, ref_end;
-    rescue_window(nam, read.size(), mu, sigma, (int)refs.seqs[nam.ref_id].size(), ref_start, ref_end);
+    rescue_window(nam, read.size(), mu, sigma, (int)refs.seq(nam.ref_id).size(), ref_start, ref_end);
     Alignment& a = res.align_res[j];
     a.is_unaligned = info.cigar.empty();
     a.cigar = std::move(info.cigar);               // each result is stored exactly once

@@ -42,6 +42,7 @@ static void finish_refs(References& r) {
     r.concat.clear();
     r.concat.reserve(tot);
     for (auto& s : r.seqs) r.concat += s;
+    r.make_hot();
 }
 
 static void setup_params(rsam* m) {

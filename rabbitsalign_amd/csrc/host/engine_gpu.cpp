@@ -59,6 +59,7 @@ public:
         rsa_close(ctx_);
     }
     const char* name() const override { return "hip-gfx950"; }
+    bool offloads() const override { return true; }
 
     void seed(const std::vector<const std::string*>& reads, int rescue_level, unsigned rescue_cutoff,
               SeedBatchOut& out) override {

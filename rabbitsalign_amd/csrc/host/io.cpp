@@ -1,6 +1,7 @@
 // io.cpp -- CIGAR text, SAM records, FASTA, .sti read/write/build, FASTQ input.
 // Restated from src/cigar.cpp, src/sam.cpp, src/refs.cpp, src/index.cpp,
 // src/indexparameters.cpp and the kseq++ record semantics used by src/fastq.cpp.
+#include <sys/mman.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -158,7 +159,11 @@ void Sam::add_record(const std::string& qname, uint16_t flags, const std::string
         if (flags & 0x100) o += '*';
         else if (flags & 0x10) {
             if (qual.empty()) o += '*';
-            else o.append(qual.rbegin(), qual.rend());
+            else {
+                const size_t at = o.size();
+                o.resize(at + qual.size());
+                reverse_into(qual, &o[at]);
+            }
         } else o.append(qual.empty() ? "*" : qual);
         o += "\tNM:i:";
         append_int(o, ed);
@@ -259,7 +264,23 @@ References References::from_fasta(const std::string& path) {   // refs.cpp:20-58
     for (auto& s : r.seqs) { total += s.size(); r.offsets.push_back(total); }
     r.concat.reserve(total);
     for (auto& s : r.seqs) r.concat += s;
+    r.make_hot();
     return r;
+}
+
+void References::make_hot() {
+    const size_t total = concat.size();
+    views.clear();
+    hot.reset();
+    if (total == 0) return;
+    const size_t huge = 2u << 20;
+    const size_t bytes = (total + huge - 1) / huge * huge;
+    void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (p == MAP_FAILED) return;                    // plain strings keep serving seq(i)
+    madvise(p, bytes, MADV_HUGEPAGE);               // before the first touch
+    memcpy(p, concat.data(), total);
+    hot = std::shared_ptr<char>((char*)p, [bytes](char* q) { munmap(q, bytes); });
+    for (size_t i = 0; i < seqs.size(); ++i) views.emplace_back(hot.get() + offsets[i], offsets[i + 1] - offsets[i]);
 }
 
 // ------------------------------------------------------ IndexParameters --

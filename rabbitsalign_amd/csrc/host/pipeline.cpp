@@ -33,6 +33,47 @@ namespace {
 using Clock = std::chrono::steady_clock;
 inline double since(Clock::time_point t) { return std::chrono::duration<double>(Clock::now() - t).count(); }
 
+// CPU slots: at most `threads` workers compute at once.  With an offloading
+// engine the pipeline runs extra workers, and a worker gives its slot back
+// while it sleeps on the GPU (or on another chunk), so the host cores stay busy
+// while seeding/extension run on the device.
+struct CpuSlots {
+    std::mutex m;
+    std::condition_variable cv;
+    int free = 0;
+    void acquire() {
+        std::unique_lock<std::mutex> g(m);
+        cv.wait(g, [&] { return free > 0; });
+        --free;
+    }
+    void release() {
+        {
+            std::lock_guard<std::mutex> g(m);
+            ++free;
+        }
+        cv.notify_one();
+    }
+};
+struct SlotHold {                 // a slot for the lifetime of a worker
+    CpuSlots& s;
+    explicit SlotHold(CpuSlots& s_) : s(s_) { s.acquire(); }
+    ~SlotHold() { s.release(); }
+};
+struct Unslot {                   // the slot handed back for a blocking section
+    CpuSlots& s;
+    bool on;
+    Unslot(CpuSlots& s_, bool on_) : s(s_), on(on_) { if (on) s.release(); }
+    ~Unslot() { if (on) s.acquire(); }
+};
+
+// extra workers beyond the compute slots (RSA_WAIT_WORKERS; default: as many
+// as the slots when the engine offloads, none for an engine computing in-thread)
+static int wait_workers(const Engine& eng, int threads) {
+    const char* e = getenv("RSA_WAIT_WORKERS");
+    if (e) return std::max(0, atoi(e));
+    return eng.offloads() ? threads : 0;
+}
+
 struct OrderedSink {
     SamSink sink;
     void* user;
@@ -91,6 +132,9 @@ static bool upper_already(const std::string& s) {
 
 void pe_load(PeChunk& c, const std::vector<Record>& a, const std::vector<Record>& b, size_t idx, size_t chunk) {
     c.index = idx;
+    c.owned.clear();
+    c.stats = AlignmentStatistics();
+    c.times = PhaseTimes();
     c.begin = std::min(a.size(), idx * chunk);
     c.end = std::min(a.size(), c.begin + chunk);
     const size_t n = c.end - c.begin;
@@ -119,19 +163,21 @@ void pe_load(PeChunk& c, const std::vector<Record>& a, const std::vector<Record>
             at += sq.size();
         }
     }
-    c.res.clear();
+    if (c.res.size() > n) c.res.resize(n);
+    for (auto& r : c.res) r.reset();       // recycled chunk: per-pair vectors keep their capacity
     c.res.resize(n);
 }
 
 // Seeding of a loaded chunk (randstrobes + find_nams + rescue on the engine).
 // Independent of the insert-size state, so it can run ahead of part().
-void pe_seed(PeChunk& c, Engine& eng, const MapContext& mc) {
+void pe_seed(PeChunk& c, Engine& eng, const MapContext& mc, CpuSlots& slots) {
     const size_t n = c.r1.size();
     if (n == 0) return;
     std::vector<const std::string*> reads;
     reads.reserve(2 * n);
     for (size_t i = 0; i < n; ++i) { reads.push_back(&c.r1[i]->seq); reads.push_back(&c.r2[i]->seq); }
     const auto t = Clock::now();
+    Unslot u(slots, eng.offloads());
     eng.seed(reads, mc.mparams.rescue_level, (unsigned)mc.mparams.rescue_cutoff, c.seeds);
     c.times.seed += since(t);
 }
@@ -206,9 +252,13 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
     const size_t n_chunks = (r1.size() + chunk - 1) / chunk;
     if (n_chunks == 0) return result;
     const int T = std::max(1, opt.threads);
-    // prefetch depth (RSA_PREFETCH chunks, default 2T+2; 0 = every worker seeds its own chunk)
+    const bool offl = eng.offloads();
+    const int W = T + wait_workers(eng, T);
+    CpuSlots slots;
+    slots.free = T;
+    // prefetch depth (RSA_PREFETCH chunks, default 2W+2; 0 = every worker seeds its own chunk)
     const char* pf_env = getenv("RSA_PREFETCH");
-    const size_t window = pf_env ? (size_t)atol(pf_env) : 2 * (size_t)T + 2;
+    const size_t window = pf_env ? (size_t)atol(pf_env) : 2 * (size_t)W + 2;
 
     std::mutex m;
     std::condition_variable cv;
@@ -226,12 +276,25 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
     AlignmentStatistics stats_all;
     PhaseTimes phases_all;
 
+    // finished chunks are recycled, so the per-pair result vectors stop allocating
+    std::mutex pool_m;
+    std::vector<std::unique_ptr<PeChunk>> pool;
+    auto recycle = [&](std::unique_ptr<PeChunk> c) {
+        if (!c) return;
+        std::lock_guard<std::mutex> g(pool_m);
+        pool.push_back(std::move(c));
+    };
     auto stage1 = [&](size_t idx) {
-        auto c = std::make_unique<PeChunk>();
+        std::unique_ptr<PeChunk> c;
+        {
+            std::lock_guard<std::mutex> g(pool_m);
+            if (!pool.empty()) { c = std::move(pool.back()); pool.pop_back(); }
+        }
+        if (!c) c = std::make_unique<PeChunk>();
         const auto t = Clock::now();
         pe_load(*c, r1, r2, idx, chunk);
         c->times.load += since(t);
-        pe_seed(*c, eng, mc);
+        pe_seed(*c, eng, mc, slots);
         return c;
     };
     // chunk idx after stage 1: from the prefetch map, or loaded + seeded here
@@ -247,7 +310,14 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
             cv.notify_all();
             return c;
         }
-        cv.wait(g, [&] { return seeded.count(idx) || failure; });
+        if (!(seeded.count(idx) || failure)) {
+            g.unlock();
+            Unslot u(slots, true);
+            g.lock();
+            cv.wait(g, [&] { return seeded.count(idx) || failure; });
+            g.unlock();          // the slot comes back without the lock held
+        }
+        if (!g.owns_lock()) g.lock();
         if (failure) return nullptr;
         auto c = std::move(seeded[idx]);
         seeded.erase(idx);
@@ -259,7 +329,10 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                       std::vector<AlignmentInfo>& infos) {
         pe_get_str(c, mc, est.mu, est.sigma, jobs);
         const auto te = Clock::now();
-        eng.extend(jobs, mc.aparams, infos);
+        {
+            Unslot u(slots, offl);
+            eng.extend(jobs, mc.aparams, infos);
+        }
         c.times.extend += since(te);
         c.stats.tot_aligner_calls += jobs.size();
         std::string out;
@@ -274,6 +347,7 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
         std::vector<AlignmentInfo> infos;
         AlignmentStatistics local;
         PhaseTimes lt;
+        std::unique_ptr<SlotHold> hold(new SlotHold(slots));
         try {
             if (leader) {
                 // ---- single-worker timeline until the insert-size estimate freezes ----
@@ -297,7 +371,10 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                     }
                     next++;
                     const auto te = Clock::now();
-                    eng.extend(jobs, mc.aparams, infos);
+                    {
+                        Unslot u(slots, offl);
+                        eng.extend(jobs, mc.aparams, infos);
+                    }
                     pre->times.extend += since(te);
                     pre->stats.tot_aligner_calls += jobs.size();
                     std::string out;
@@ -305,7 +382,8 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                     os.put(pre->index, std::move(out));
                     local.add(pre->stats);
                     lt.add(pre->times);
-                    if (!cur) { pre.reset(); break; }
+                    if (!cur) { recycle(std::move(pre)); break; }
+                    recycle(std::move(pre));
                     pre = std::move(cur);
                 }
                 lt.sequential = since(t0);
@@ -334,13 +412,21 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                             break;
                         }
                         if (frozen && next_par >= n_chunks) { done = true; cv.notify_all(); break; }
-                        cv.wait(g);
+                        g.unlock();
+                        {
+                            Unslot u(slots, true);
+                            g.lock();
+                            cv.wait(g);
+                            g.unlock();
+                        }
+                        g.lock();
                     }
                 }
                 if (c) {                                    // part() already done
                     finish(*c, frozen_isize, jobs, infos);
                     local.add(c->stats);
                     lt.add(c->times);
+                    recycle(std::move(c));
                     continue;
                 }
                 if (idx != SIZE_MAX) {
@@ -351,6 +437,7 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                     finish(*c, frozen_isize, jobs, infos);
                     local.add(c->stats);
                     lt.add(c->times);
+                    recycle(std::move(c));
                     continue;
                 }
                 if (pf != SIZE_MAX) {
@@ -367,12 +454,13 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
             if (!failure) failure = std::current_exception();
             cv.notify_all();
         }
+        hold.reset();
         std::lock_guard<std::mutex> g(m);
         stats_all.add(local);
         phases_all.add(lt);
     };
     std::vector<std::thread> ws;
-    for (int t = 1; t < T; ++t) ws.emplace_back(worker, false);
+    for (int t = 1; t < W; ++t) ws.emplace_back(worker, false);
     worker(true);
     for (auto& w : ws) w.join();
     if (failure) std::rethrow_exception(failure);
@@ -395,7 +483,12 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
     const size_t n_chunks = (recs.size() + chunk - 1) / chunk;
     std::atomic<size_t> next{0};
     std::mutex stat_m;
+    const int T = std::max(1, opt.threads);
+    const bool offl = eng.offloads();
+    CpuSlots slots;
+    slots.free = T;
     auto worker = [&]() {
+        SlotHold hold(slots);
         std::vector<SwJob> jobs;
         std::vector<AlignmentInfo> infos;
         AlignmentStatistics local;
@@ -409,7 +502,10 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
             std::vector<const std::string*> reads;
             for (size_t i = b; i < e; ++i) reads.push_back(&recs[i].seq);
             SeedBatchOut so;
-            eng.seed(reads, mc.mparams.rescue_level, (unsigned)mc.mparams.rescue_cutoff, so);
+            {
+                Unslot u(slots, offl);
+                eng.seed(reads, mc.mparams.rescue_level, (unsigned)mc.mparams.rescue_cutoff, so);
+            }
             std::vector<AlignTmpRes> res(e - b);
             std::vector<std::string> rcs(e - b);
             for (size_t i = b; i < e; ++i) rcs[i - b] = reverse_complement(recs[i].seq);
@@ -425,7 +521,10 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
                 const Read read(recs[i].seq, rcs[i - b]);
                 collect_jobs_se(res[i - b], read, mc, jobs);
             }
-            eng.extend(jobs, mc.aparams, infos);
+            {
+                Unslot u(slots, offl);
+                eng.extend(jobs, mc.aparams, infos);
+            }
             st.tot_aligner_calls += jobs.size();
             size_t pos = 0;
             for (size_t i = b; i < e; ++i) {
@@ -446,7 +545,7 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
         result.stats.add(local);
     };
     std::vector<std::thread> ws;
-    for (int t = 0; t < std::max(1, opt.threads); ++t) ws.emplace_back(worker);
+    for (int t = 0; t < T + wait_workers(eng, T); ++t) ws.emplace_back(worker);
     for (auto& w : ws) w.join();
     result.map_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     result.sam_bytes = os.bytes;

@@ -85,6 +85,12 @@ struct AlignTmpRes {                            // src/sam.hpp:27-45
     std::vector<Nam> type4_nams, todo_nams;
     BitVec done_align;
     std::vector<Alignment> align_res;
+    // empty again, keeping the vectors' capacity (the pipeline recycles chunks)
+    void reset() {
+        type = 0; mapq1 = mapq2 = 0; type4_loop_size = 0;
+        is_extend_seed.clear(); consistent_nam.clear(); is_read1.clear(); done_align.clear();
+        type4_nams.clear(); todo_nams.clear(); align_res.clear();
+    }
 };
 
 struct Details {                                // src/sam.hpp:60-67
@@ -129,6 +135,7 @@ struct Record { std::string name, comment, seq, qual; };   // klibpp::KSeq field
 
 std::string reverse_complement(std::string_view s);
 void reverse_complement_into(std::string_view s, char* out);   // out holds s.size() bytes
+void reverse_into(std::string_view s, char* out);              // plain byte reversal
 
 // Read (src/revcomp.hpp:41-55): a sequence and its reverse complement.  The
 // pipeline computes the rc once per read per chunk and hands out views.
@@ -153,6 +160,13 @@ struct References {                             // src/refs.hpp
     std::string concat;                         // all contigs back to back (device upload)
     size_t size() const { return seqs.size(); }
     static References from_fasta(const std::string& path);
+    // The host pipeline reads reference windows at random (NAM checks, Hamming
+    // windows, SW job windows); make_hot() copies the contigs into one mapping
+    // advised for transparent huge pages, so those reads stop missing the TLB.
+    std::shared_ptr<char> hot;
+    std::vector<std::string_view> views;        // contig i inside `hot`
+    void make_hot();
+    std::string_view seq(size_t i) const { return views.empty() ? std::string_view(seqs[i]) : views[i]; }
 };
 
 struct IndexParameters {                        // src/indexparameters.hpp
@@ -203,6 +217,8 @@ public:
                         std::vector<AlignmentInfo>& out) = 0;
     // device kernel timings/counters (GPU engine only)
     virtual bool kernel_stats(rsa_kernel_stats*) { return false; }
+    // true when seed/extend run on a device and the calling thread only waits
+    virtual bool offloads() const { return false; }
     virtual void reset_kernel_stats() {}
 };
 
