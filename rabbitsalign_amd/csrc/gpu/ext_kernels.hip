@@ -336,7 +336,7 @@ __device__ PassOut sw_pass_dispatch(const uint8_t* qc, int nrow, const uint8_t* 
 
 template <int RMAX, int V>
 __global__ void __launch_bounds__(64 * SCAN_WAVES)
-k_ext_scan(const ExtJobDev* __restrict__ jobs, int n_jobs, const char* __restrict__ qbuf,
+k_ext_scan(const ExtJobDev* __restrict__ jobs, int n_jobs, const int* __restrict__ idx, const char* __restrict__ qbuf,
            const char* __restrict__ ref, ScanRes* __restrict__ out, int match, int mismatch, int gO, int gE) {
     __shared__ uint8_t s_q[SCAN_WAVES][MAXQ_LDS];
     // every packed 16-bit score stays far inside int16
@@ -344,9 +344,10 @@ k_ext_scan(const ExtJobDev* __restrict__ jobs, int n_jobs, const char* __restric
                           gE >= 0 && gE < 4000;
     __shared__ uint8_t s_r[SCAN_WAVES][MAXR_LDS];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int j = blockIdx.x * SCAN_WAVES + wave;
+    const int k = blockIdx.x * SCAN_WAVES + wave;
     // every wave reaches the barrier; invalid / sentinel jobs skip the work after it
-    const bool in_range = j < n_jobs;
+    const bool in_range = k < n_jobs;
+    const int j = in_range ? (idx ? idx[k] : k) : 0;
     ExtJobDev jb;
     jb.q_off = 0; jb.r_off = 0; jb.qlen = 0; jb.rlen = 0; jb.cig_off = 0;
     if (in_range) jb = jobs[j];
@@ -1030,8 +1031,9 @@ k_cigar_compact(rsa_aln* __restrict__ alns, int n_jobs, const uint32_t* __restri
 // host-side launcher: RMAX from the longest query of the batch, V = cell
 // bookkeeping variant (0: per cell, 1: per column)
 void launch_ext_scan(int rmax, int variant, dim3 grid, dim3 block, hipStream_t st, const ExtJobDev* jobs, int n,
-                     const char* q, const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE) {
-#define RSA_L(RM, VV) hipLaunchKernelGGL((k_ext_scan<RM, VV>), grid, block, 0, st, jobs, n, q, ref, out, match, mismatch, gO, gE)
+                     const int* idx, const char* q, const char* ref, ScanRes* out, int match, int mismatch, int gO,
+                     int gE) {
+#define RSA_L(RM, VV) hipLaunchKernelGGL((k_ext_scan<RM, VV>), grid, block, 0, st, jobs, n, idx, q, ref, out, match, mismatch, gO, gE)
     if (variant == 2) {
         if (rmax <= 2) RSA_L(2, 2); else if (rmax <= 4) RSA_L(4, 2); else if (rmax <= 8) RSA_L(8, 2); else RSA_L(16, 2);
     } else if (variant) {

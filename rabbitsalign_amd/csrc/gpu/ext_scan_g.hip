@@ -1,0 +1,345 @@
+// ext_scan_g.hip -- grouped SSW scan for gfx950: 16 lanes per job, 4 jobs per
+// wavefront.
+//
+// Same results as k_ext_scan (ext_kernels.hip) -- the SSW forward pass with the
+// byte (16-stripe) and word (8-stripe) layouts fused in the two int16 halves of
+// packed registers, then the reverse pass that stops at the first column
+// reaching score1 (ssw.c:197-588, 838-893) -- with a different mapping:
+//
+//   * a job occupies one 16-lane DPP row; the query rows are striped R per lane
+//     (R = 10 for 150 bp reads), the reference streams through the row as an
+//     anti-diagonal systolic array, and the row-above values move one lane per
+//     step with DPP row_shr:1 (the row's first lane reads the zero boundary);
+//   * four jobs share a wavefront in lockstep, so the per-step overhead (three
+//     DPP moves, one LDS read of the reference code, the column-max bookkeeping)
+//     is paid once per R rows instead of once per 3, and the systolic ramp is
+//     15 steps instead of 50.  The host hands the jobs over sorted by window
+//     length, so the four jobs of a wave run nearly the same number of steps.
+//
+// Cell recurrence.  SSW keeps E and F saturated at >= 0; here only the
+// diagonal term is clamped (H = max(max(diag, 0), E, Fw, F)).  E, Fw and F may
+// go negative but stay >= -gap_open (their update is a max with H - gap_open),
+// and their positive parts -- the only parts that can reach H -- follow
+// exactly the saturated recurrence, so every H is SSW's.
+//
+// Column maxima of the forward pass include the padding rows of the last lane
+// (rows >= nrow) without a mask: with non-negative mismatch/gap penalties (the
+// host routes other parameters to k_ext_scan) every move into a padding row
+// loses or keeps score (never a match there) and its only entries are this
+// lane's last valid row, so a padding cell never exceeds the best valid cell of
+// the same lane so far; whenever the column max improves the lane's best it is
+// a valid cell's value, and the row search only looks at valid rows.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <climits>
+
+#include "rsa_dev.h"
+#include "rsa_ext.h"
+
+#define GS_WAVES 4
+#define GS_JOBS (GS_WAVES * 4)   // jobs per workgroup
+#define GS_MAXR 1024             // reference window bytes staged in LDS per job
+
+namespace {
+
+typedef short pk16 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ pk16 pk_from(uint32_t x) { return __builtin_bit_cast(pk16, x); }
+__device__ __forceinline__ uint32_t pk_bits(pk16 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ pk16 pk_max(pk16 a, pk16 b) { return __builtin_elementwise_max(a, b); }
+
+// lane l receives lane l-1 of its 16-lane row; the row's first lane receives 0
+__device__ __forceinline__ uint32_t row_shr1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+}
+__device__ __forceinline__ int grp_max(int v) {
+    for (int o = 8; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 16));
+    return v;
+}
+__device__ __forceinline__ int grp_min(int v) {
+    for (int o = 8; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 16));
+    return v;
+}
+
+// ssw_code as selects (no divergent branch tree)
+__device__ __forceinline__ int ssw_code_sel(uint32_t c) {
+    const uint32_t u = c | 0x20;              // 'A'..'Z' -> 'a'..'z'; other bytes map outside a/c/g/t/u
+    int r = 4;
+    r = u == 't' ? 3 : r;
+    r = u == 'g' ? 2 : r;
+    r = u == 'c' ? 1 : r;
+    r = (u == 'a' || u == 'u') ? 0 : r;
+    return r;
+}
+
+struct FwdG {
+    int best[2], col[2], row[2];     // [0] byte layout, [1] word layout
+};
+
+// forward pass, both layouts at once; row p of this lane is gl * R + r
+template <int R, bool MASK>
+__device__ __forceinline__ FwdG fwd_g(const int (&qv)[R], int nrow, const uint8_t* __restrict__ rc, int ncol, int S,
+                                      bool on, int match, int mismatch, int gO, int gE, int gl) {
+    const int seg_b = (nrow + 15) / 16, seg_w = (nrow + 7) / 8;
+    pk16 E[R], Hc[R];
+    uint32_t ssm[R], vm[R];
+    const pk16 zero = {0, 0};
+    const pk16 GO2 = {(short)gO, (short)gO}, GE2 = {(short)gE, (short)gE};
+    const uint32_t M2 = pk_bits((pk16){(short)match, (short)match});
+    const uint32_t X2 = pk_bits((pk16){(short)-mismatch, (short)-mismatch});
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        E[r] = zero;
+        Hc[r] = zero;
+        const int p = gl * R + r;
+        ssm[r] = ((p % seg_b) == 0 ? 0u : 0x0000FFFFu) | ((p % seg_w) == 0 ? 0u : 0xFFFF0000u);
+        vm[r] = p < nrow ? 0xFFFFFFFFu : 0u;
+    }
+    uint32_t F_out = 0, Fw_out = 0, H_last = 0, diag_top = 0;
+    FwdG o;
+    o.best[0] = o.best[1] = 0;
+    o.col[0] = o.col[1] = INT_MAX;
+    o.row[0] = o.row[1] = INT_MAX;
+    for (int s = 0; s < S; ++s) {
+        const uint32_t F_in = row_shr1(F_out);
+        const uint32_t Fw_in = row_shr1(Fw_out);
+        const uint32_t Hl_in = row_shr1(H_last);
+        const int c = s - gl;
+        if (on && c >= 0 && c < ncol) {
+            const int rcode = rc[c];
+            pk16 dg = pk_from(diag_top), F = pk_from(F_in), Fw = pk_from(Fw_in), cm = zero;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                Fw = pk_from(pk_bits(Fw) & ssm[r]);
+                const pk16 diag = pk_max(dg + pk_from(qv[r] == rcode ? M2 : X2), zero);
+                const pk16 hm = pk_max(pk_max(diag, E[r]), Fw);
+                const pk16 h = pk_max(hm, F);
+                dg = Hc[r];
+                Hc[r] = h;
+                const pk16 t = hm - GO2;
+                E[r] = pk_max(E[r] - GE2, t);
+                Fw = pk_max(Fw - GE2, t);
+                F = pk_max(F - GE2, h - GO2);
+                cm = pk_max(cm, MASK ? pk_from(pk_bits(h) & vm[r]) : h);
+            }
+            F_out = pk_bits(F);
+            Fw_out = pk_bits(Fw);
+            H_last = pk_bits(Hc[R - 1]);
+            const uint32_t cmb = pk_bits(cm);
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                const int v = (int)((cmb >> (16 * hf)) & 0xFFFFu);
+                if (v > o.best[hf]) {
+                    o.best[hf] = v;
+                    o.col[hf] = c;
+                    int row = INT_MAX;
+#pragma unroll
+                    for (int r = R - 1; r >= 0; --r)
+                        if (vm[r] && (int)((pk_bits(Hc[r]) >> (16 * hf)) & 0xFFFFu) == v) row = gl * R + r;
+                    o.row[hf] = row;
+                }
+            }
+        }
+        diag_top = Hl_in;
+    }
+    return o;
+}
+
+// reverse pass (one layout, int32): row p -> query qend - p, column c -> ref rend - c.
+// Returns the first column whose valid-row maximum equals `terminate` (and its
+// smallest such row) through tcol/trow, INT_MAX if none.
+template <int R>
+__device__ __forceinline__ void rev_g(const int (&qr)[R], int nrow, const uint8_t* __restrict__ rc, int ncol,
+                                      int rend, int seg, int terminate, int S, bool on, int match, int mismatch,
+                                      int gO, int gE, int gl, int& tcol, int& trow) {
+    const int lanes_used = (nrow + R - 1) / R;
+    int E[R], Hc[R], ssm[R];
+    bool valid[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        E[r] = 0;
+        Hc[r] = 0;
+        const int p = gl * R + r;
+        ssm[r] = (p % seg) == 0 ? 0 : -1;
+        valid[r] = p < nrow;
+    }
+    int F_out = 0, Fw_out = 0, H_last = 0, diag_top = 0;
+    tcol = INT_MAX;
+    trow = INT_MAX;
+    bool done = !on;
+    for (int s = 0; s < S; ++s) {
+        const int F_in = (int)row_shr1((uint32_t)F_out);
+        const int Fw_in = (int)row_shr1((uint32_t)Fw_out);
+        const int Hl_in = (int)row_shr1((uint32_t)H_last);
+        const int c = s - gl;
+        if (on && c >= 0 && c < ncol) {
+            const int rcode = rc[rend - c];
+            int dg = diag_top, F = F_in, Fw = Fw_in, cm = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                Fw &= ssm[r];
+                const int diag = max(dg + (qr[r] == rcode ? match : -mismatch), 0);
+                const int hm = max(max(diag, E[r]), Fw);
+                const int h = max(hm, F);
+                dg = Hc[r];
+                Hc[r] = h;
+                const int t = hm - gO;
+                E[r] = max(E[r] - gE, t);
+                Fw = max(Fw - gE, t);
+                F = max(F - gE, h - gO);
+                cm = max(cm, valid[r] ? h : 0);
+            }
+            F_out = F;
+            Fw_out = Fw;
+            H_last = Hc[R - 1];
+            if (cm == terminate && tcol == INT_MAX) {
+                tcol = c;
+                int row = INT_MAX;
+#pragma unroll
+                for (int r = R - 1; r >= 0; --r)
+                    if (valid[r] && Hc[r] == terminate) row = gl * R + r;
+                trow = row;
+            }
+        }
+        diag_top = Hl_in;
+        if ((s & 7) == 7) {
+            // a job is finished once its first terminating column has crossed every lane
+            const int m = grp_min(tcol);
+            if (m != INT_MAX && s >= m + lanes_used - 1) done = true;
+            if (wave_min_i32(done ? 1 : 0)) break;
+        }
+    }
+}
+
+}  // namespace
+
+// jobs[order[k]] for k < n; results land at out[order[k]].  Every job handed
+// here has 0 < qlen <= 16 * R and rlen <= GS_MAXR (the host routes the rest to
+// k_ext_scan).
+template <int R, bool MASK>
+__global__ void __launch_bounds__(64 * GS_WAVES)
+k_ext_scan_g(const ExtJobDev* __restrict__ jobs, const int* __restrict__ order, int n,
+             const char* __restrict__ qbuf, const char* __restrict__ ref, ScanRes* __restrict__ out,
+             int match, int mismatch, int gO, int gE) {
+    __shared__ uint8_t s_r[GS_JOBS][GS_MAXR];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int slot = wave * 4 + (lane >> 4), gl = lane & 15;
+    const int k = blockIdx.x * GS_JOBS + slot;
+    const bool on = k < n;
+    const int j = on ? order[k] : 0;
+    ExtJobDev jb;
+    jb.q_off = 0; jb.r_off = 0; jb.qlen = 0; jb.rlen = 0; jb.cig_off = 0;
+    if (on) jb = jobs[j];
+    const int qlen = (int)jb.qlen, rlen = (int)jb.rlen;
+    uint8_t* rc = s_r[slot];
+    {
+        // aligned dwords covering the window (the device reference carries 64 bytes of tail padding)
+        const int pre = (int)(jb.r_off & 3);
+        const uint32_t* w = (const uint32_t*)(ref + (jb.r_off - (uint64_t)pre));
+        const int nw = (pre + rlen + 3) >> 2;
+        for (int i = gl; i < nw; i += 16) {
+            const uint32_t x = w[i];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int pos = 4 * i + b - pre;
+                if (pos >= 0 && pos < rlen) rc[pos] = (uint8_t)ssw_code_sel((x >> (8 * b)) & 0xFF);
+            }
+        }
+    }
+    int qv[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int p = gl * R + r;
+        const int code = p < qlen ? ssw_code_sel((unsigned char)qbuf[jb.q_off + p]) : 7;
+        qv[r] = code < 4 ? code : 7;          // N (and padding) never scores a match, not even vs N
+    }
+    __syncthreads();
+
+    // forward pass: every job of the wave runs until the longest one is done
+    const int lanes_used = (qlen + R - 1) / R;
+    const int S = wave_max_i32(on ? rlen + lanes_used - 1 : 0);
+    const FwdG fo = fwd_g<R, MASK>(qv, qlen, rc, rlen, S, on && gl < lanes_used, match, mismatch, gO, gE, gl);
+    const int sb = grp_max(fo.best[0]);
+    const int word = sb + mismatch >= 255 ? 1 : 0;
+    const int score1 = word ? grp_max(fo.best[1]) : sb;
+    int ref_end1, read_end1;
+    if (score1 == 0) {
+        ref_end1 = word ? 0 : -1;
+        read_end1 = 0;
+    } else {
+        ref_end1 = grp_min(fo.best[word] == score1 ? fo.col[word] : INT_MAX);
+        read_end1 = grp_min((fo.best[word] == score1 && fo.col[word] == ref_end1) ? fo.row[word] : INT_MAX);
+    }
+
+    // reverse pass (ssw.c:877-893) on read[0..read_end1] x ref[0..ref_end1], reversed
+    const bool ron = on && score1 > 0;
+    const int nrow = ron ? read_end1 + 1 : 0, ncol = ron ? ref_end1 + 1 : 0;
+    const int rl_used = (nrow + R - 1) / R;
+    int qr[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int p = gl * R + r;
+        int code = 7;
+        if (p < nrow) {
+            code = ssw_code_sel((unsigned char)qbuf[jb.q_off + (read_end1 - p)]);
+            code = code < 4 ? code : 7;
+        }
+        qr[r] = code;
+    }
+    const int seg = word ? (nrow + 7) / 8 : (nrow + 15) / 16;
+    const int S2 = wave_max_i32(ron ? ncol + rl_used - 1 : 0);
+    int tc = INT_MAX, tr = INT_MAX;
+    if (S2 > 0)
+        rev_g<R>(qr, nrow, rc, ncol, ref_end1, seg > 0 ? seg : 1, score1, S2, ron && gl < rl_used, match, mismatch,
+                 gO, gE, gl, tc, tr);
+    const int tcol = grp_min(tc);
+    const int trow = grp_min(tc == tcol ? tr : INT_MAX);
+
+    if (!on || gl != 0) return;
+    ScanRes res;
+    res.score1 = score1; res.ref_end1 = ref_end1; res.read_end1 = read_end1; res.word = word;
+    res.flag = 0; res.status = 0;
+    if (score1 > 0) {
+        if (tcol == INT_MAX) {
+            res.flag = 2;   // reverse max < score1: "may miss a small part"
+            res.ref_begin1 = 0;
+            res.read_begin1 = 0;
+        } else {
+            res.ref_begin1 = ref_end1 - tcol;
+            res.read_begin1 = read_end1 - trow;
+        }
+    } else {
+        res.ref_begin1 = word ? 0 : -1;
+        res.read_begin1 = 0;
+    }
+    out[j] = res;
+}
+
+// rows per lane of the grouped scan for a query length (0: not handled here)
+int scan_g_rows(uint32_t qlen) {
+    if (qlen == 0) return 0;
+    if (qlen <= 64) return 4;
+    if (qlen <= 112) return 7;
+    if (qlen <= 160) return 10;
+    if (qlen <= 208) return 13;
+    if (qlen <= 256) return 16;
+    return 0;
+}
+
+int scan_g_max_ref() { return GS_MAXR; }
+
+void launch_ext_scan_g(int rows, bool mask, int n, hipStream_t st, const ExtJobDev* jobs, const int* order,
+                       const char* q, const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE) {
+    if (n <= 0) return;
+    const dim3 grid((n + GS_JOBS - 1) / GS_JOBS), block(64 * GS_WAVES);
+#define RSA_G(RR)                                                                                               \
+    if (rows == RR) {                                                                                           \
+        if (mask) hipLaunchKernelGGL((k_ext_scan_g<RR, true>), grid, block, 0, st, jobs, order, n, q, ref, out,  \
+                                     match, mismatch, gO, gE);                                                  \
+        else hipLaunchKernelGGL((k_ext_scan_g<RR, false>), grid, block, 0, st, jobs, order, n, q, ref, out,     \
+                                match, mismatch, gO, gE);                                                       \
+        return;                                                                                                 \
+    }
+    RSA_G(4) RSA_G(7) RSA_G(10) RSA_G(13) RSA_G(16)
+#undef RSA_G
+}

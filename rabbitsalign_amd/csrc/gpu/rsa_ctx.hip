@@ -21,7 +21,12 @@
 #include "rsa_timer.h"
 
 void launch_ext_scan(int rmax, int variant, dim3 grid, dim3 block, hipStream_t st, const ExtJobDev* jobs, int n,
-                     const char* q, const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE);
+                     const int* idx, const char* q, const char* ref, ScanRes* out, int match, int mismatch, int gO,
+                     int gE);
+int scan_g_rows(uint32_t qlen);
+int scan_g_max_ref();
+void launch_ext_scan_g(int rows, bool mask, int n, hipStream_t st, const ExtJobDev* jobs, const int* order,
+                       const char* q, const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE);
 __global__ void k_ext_band(const ExtJobDev* jobs, const ScanRes* scan, int n_jobs, const int* idx_list, int job_base,
                            const char* qbuf, const char* ref, uint32_t* cig_pool, rsa_aln* out, uint8_t* scratch,
                            int64_t scr_stride, int arr_cap, int64_t dir_cap, int match, int mismatch, int gO,
@@ -88,8 +93,9 @@ struct Lane {
     KTimer kt;
     bool busy = false;
     // extension
-    DevBuf d_q, d_jobs, d_scan, d_alns, d_alns2, d_cig, d_dense, d_raw, d_scratch, d_over, d_queue, d_idx, d_status;
-    HostBuf h_jobs, h_over, h_status;
+    DevBuf d_q, d_jobs, d_scan, d_alns, d_alns2, d_cig, d_dense, d_raw, d_scratch, d_over, d_queue, d_idx, d_status,
+        d_order;
+    HostBuf h_jobs, h_over, h_status, h_order;
     // seeding
     SeedBufs sb;
 };
@@ -248,6 +254,13 @@ static int scan_variant() {
     return v ? atoi(v) : 2;
 }
 
+// grouped scan (RSA_SCAN_G: 1 (default) 16 lanes per job, 4 jobs per wave, for
+// queries up to 256 bp; 0 = one job per wave for every job)
+static int scan_grouped() {
+    const char* v = getenv("RSA_SCAN_G");
+    return v ? atoi(v) : 1;
+}
+
 // band kernel variant (RSA_BAND_V: 0 LDS arrays, 1 (default) register arrays; same results)
 static int band_variant() {
     const char* v = getenv("RSA_BAND_V");
@@ -321,12 +334,74 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
     HIPCHK(hipMemcpyAsync(L->d_q.p, jb->queries, jb->queries_len, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(L->d_jobs.p, hj, sizeof(ExtJobDev) * n, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemsetAsync(L->d_status.p, 0, sizeof(ExtStatus), st));
+    // Scan routing: jobs the grouped kernel takes (query <= 256 bp, window <= 1 KB,
+    // packed-int16 parameters) go to it per rows-per-lane class, sorted by window
+    // length (longest first) so the four jobs of a wave run about as long; the
+    // rest -- and sentinels -- to the one-job-per-wave kernel via an index list.
+    const int variant = scan_variant();
+    const bool packed_ok = jb->match >= 0 && jb->match <= 28 && jb->mismatch >= 0 && jb->mismatch < 4000 &&
+                           jb->gap_open >= 0 && jb->gap_open < 4000 && jb->gap_extend >= 0 && jb->gap_extend < 4000;
+    const bool grouped = scan_grouped() && variant == 2 && packed_ok;
+    constexpr int NCLS = 5;
+    static const int cls_rows[NCLS] = {4, 7, 10, 13, 16};
+    uint32_t cls_n[NCLS] = {0}, rest_n = 0;
+    HIPCHK(L->h_order.ensure(sizeof(int) * (n + 1)));
+    int* ord = L->h_order.as<int>();
+    if (grouped) {
+        const uint32_t maxr = (uint32_t)scan_g_max_ref();
+        std::vector<uint32_t> cnt((size_t)NCLS * (maxr + 1), 0);
+        auto cls_of = [&](const ExtJobDev& j) -> int {
+            if (j.rlen > 2000 || j.qlen == 0 || j.qlen > 1024 || j.rlen > maxr) return -1;
+            const int r = scan_g_rows(j.qlen);
+            for (int c = 0; c < NCLS; ++c) if (cls_rows[c] == r) return c;
+            return -1;
+        };
+        std::vector<int8_t> cls(n);
+        for (uint32_t i = 0; i < n; ++i) {
+            cls[i] = (int8_t)cls_of(hj[i]);
+            if (cls[i] < 0) rest_n++;
+            else { cls_n[cls[i]]++; cnt[(size_t)cls[i] * (maxr + 1) + (maxr - hj[i].rlen)]++; }
+        }
+        // counting sort: class-major, then window length descending; the rest after
+        uint64_t at = 0;
+        for (int c = 0; c < NCLS; ++c)
+            for (uint32_t b = 0; b <= maxr; ++b) {
+                uint32_t& x = cnt[(size_t)c * (maxr + 1) + b];
+                const uint32_t k = x;
+                x = (uint32_t)at;
+                at += k;
+            }
+        uint64_t rest_at = at;
+        for (uint32_t i = 0; i < n; ++i) {
+            if (cls[i] < 0) ord[rest_at++] = (int)i;
+            else ord[cnt[(size_t)cls[i] * (maxr + 1) + (maxr - hj[i].rlen)]++] = (int)i;
+        }
+    } else {
+        rest_n = n;
+        for (uint32_t i = 0; i < n; ++i) ord[i] = (int)i;
+    }
+    HIPCHK(L->d_order.ensure(sizeof(int) * (n + 1)));
+    HIPCHK(hipMemcpyAsync(L->d_order.p, ord, sizeof(int) * n, hipMemcpyHostToDevice, st));
     L->kt.reset();
     L->kt.begin(st, RSA_K_EXT_SCAN);
-    launch_ext_scan(rmax, scan_variant(), dim3((n + 3) / 4), dim3(256), st, L->d_jobs.as<ExtJobDev>(), (int)n,
-                    L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(), jb->match, jb->mismatch, jb->gap_open,
-                    jb->gap_extend);
-    HIPCHK(hipGetLastError());
+    {
+        const int* d_ord = L->d_order.as<int>();
+        uint32_t off = 0;
+        for (int c = 0; c < NCLS; ++c) {
+            if (!cls_n[c]) continue;
+            launch_ext_scan_g(cls_rows[c], false, (int)cls_n[c], st, L->d_jobs.as<ExtJobDev>(), d_ord + off,
+                              L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(), jb->match, jb->mismatch,
+                              jb->gap_open, jb->gap_extend);
+            HIPCHK(hipGetLastError());
+            off += cls_n[c];
+        }
+        if (rest_n) {
+            launch_ext_scan(rmax, variant, dim3((rest_n + 3) / 4), dim3(256), st, L->d_jobs.as<ExtJobDev>(),
+                            (int)rest_n, d_ord + off, L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(),
+                            jb->match, jb->mismatch, jb->gap_open, jb->gap_extend);
+            HIPCHK(hipGetLastError());
+        }
+    }
     L->kt.end(st);
     // 16 lanes per job for the common narrow bands; the rest queue for 64-lane waves
     L->kt.begin(st, RSA_K_EXT_BAND);
