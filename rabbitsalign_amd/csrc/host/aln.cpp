@@ -189,7 +189,9 @@ static std::vector<NamPair> get_best_scoring_nam_pairs(const std::vector<Nam>& n
     reset_ids(added_n1, nams1);
     reset_ids(added_n2, nams2);
     int best_joint_hits = 0;
-    std::vector<Nam> sorted2[2];
+    thread_local std::vector<Nam> sorted2[2];
+    sorted2[0].clear();
+    sorted2[1].clear();
     for (const auto& n2 : nams2) sorted2[n2.is_rc ? 1 : 0].push_back(n2);
     for (int i = 0; i < 2; ++i)
         std::sort(sorted2[i].begin(), sorted2[i].end(), [](const Nam& a, const Nam& b) {
@@ -527,14 +529,22 @@ static void align_PE_part(AlignTmpRes& res, const MapContext& mc, std::vector<Na
     }
     res.type = 4;
     std::vector<NamPair> joint = get_best_scoring_nam_pairs(nams1, nams2, mu, sigma);
-    std::unordered_set<int> aligned1, aligned2;
+    // nam_id flags (the id is the NAM's index in its read's list) instead of hash sets
+    thread_local std::vector<uint8_t> aligned1, aligned2;
+    auto reset_ids = [](std::vector<uint8_t>& v, const std::vector<Nam>& ns) {
+        int mx = -1;
+        for (const Nam& x : ns) mx = std::max(mx, x.nam_id);
+        v.assign((size_t)(mx + 1), 0);
+    };
+    reset_ids(aligned1, nams1);
+    reset_ids(aligned2, nams2);
     {
         Nam n1 = nams1[0];
         bool c1 = reverse_nam_if_needed(n1, read1, mc.refs, k);
         det[0].nam_inconsistent += !c1;
         res.is_read1.push_back(true);
         bool g1 = extend_seed_part(res, mc.aparams, n1, mc.refs, read1, c1);
-        aligned1.insert(n1.nam_id);
+        aligned1[n1.nam_id] = 1;
         det[0].tried_alignment++;
         det[0].gapped += g1;
         Nam n2 = nams2[0];
@@ -542,7 +552,7 @@ static void align_PE_part(AlignTmpRes& res, const MapContext& mc, std::vector<Na
         det[1].nam_inconsistent += !c2;
         res.is_read1.push_back(false);
         bool g2 = extend_seed_part(res, mc.aparams, n2, mc.refs, read2, c2);
-        aligned2.insert(n2.nam_id);
+        aligned2[n2.nam_id] = 1;
         det[1].tried_alignment++;
         det[1].gapped += g2;
     }
@@ -558,12 +568,12 @@ static void align_PE_part(AlignTmpRes& res, const MapContext& mc, std::vector<Na
         res.type4_nams.push_back(n2);
         res.type4_loop_size++;
         if (n1.ref_start >= 0) {
-            if (!aligned1.count(n1.nam_id)) {
+            if (!aligned1[n1.nam_id]) {
                 bool c = reverse_nam_if_needed(n1, read1, mc.refs, k);
                 det[0].nam_inconsistent += !c;
                 res.is_read1.push_back(true);
                 bool g = extend_seed_part(res, mc.aparams, n1, mc.refs, read1, c);
-                aligned1.insert(n1.nam_id);
+                aligned1[n1.nam_id] = 1;
                 det[0].tried_alignment++;
                 det[0].gapped += g;
             }
@@ -574,12 +584,12 @@ static void align_PE_part(AlignTmpRes& res, const MapContext& mc, std::vector<Na
             det[0].tried_alignment++;
         }
         if (n2.ref_start >= 0) {
-            if (!aligned2.count(n2.nam_id)) {
+            if (!aligned2[n2.nam_id]) {
                 bool c = reverse_nam_if_needed(n2, read2, mc.refs, k);
                 det[1].nam_inconsistent += !c;
                 res.is_read1.push_back(false);
                 bool g = extend_seed_part(res, mc.aparams, n2, mc.refs, read2, c);
-                aligned2.insert(n2.nam_id);
+                aligned2[n2.nam_id] = 1;
                 det[1].tried_alignment++;
                 det[1].gapped += g;
             }
@@ -773,9 +783,9 @@ static inline float normal_pdf(float x, float mu, float sigma) {   // aln.cpp:52
 }
 
 // aln.cpp:535-550
-static std::vector<ScoredAlignmentPair> get_best_scoring_pairs(const std::vector<Alignment>& al1,
+static void get_best_scoring_pairs(std::vector<ScoredAlignmentPair>& pairs, const std::vector<Alignment>& al1,
                                                                const std::vector<Alignment>& al2, float mu, float sigma) {
-    std::vector<ScoredAlignmentPair> pairs;
+    pairs.clear();
     for (auto& a1 : al1) {
         for (auto& a2 : al2) {
             float dist = std::abs(a1.ref_start - a2.ref_start);
@@ -785,7 +795,6 @@ static std::vector<ScoredAlignmentPair> get_best_scoring_pairs(const std::vector
             pairs.push_back(ScoredAlignmentPair{score, a1, a2});
         }
     }
-    return pairs;
 }
 
 static std::pair<int, int> joint_mapq_from_high_scores(const std::vector<ScoredAlignmentPair>& pairs) {  // aln.cpp:506-526
@@ -831,7 +840,9 @@ static void pick_random_top_pair(std::vector<ScoredAlignmentPair>& hs, std::mins
 static void rescue_read_last(AlignTmpRes& res, const Read& read2, const Read& read1, const MapContext& mc,
                              Details det[2], float mu, float sigma, Sam& sam, const Record& rec1, const Record& rec2,
                              bool swap_r1r2, std::minstd_rand& rng) {
-    std::vector<Alignment> al1, al2;
+    thread_local std::vector<Alignment> al1, al2;
+    al1.clear();
+    al2.clear();
     const size_t n = res.todo_nams.size();
     for (size_t i = 0; i < n; i += 2) {
         al1.push_back(res.align_res[i]);
@@ -840,7 +851,8 @@ static void rescue_read_last(AlignTmpRes& res, const Read& read2, const Read& re
     }
     std::sort(al1.begin(), al1.end(), by_score<Alignment>);
     std::sort(al2.begin(), al2.end(), by_score<Alignment>);
-    auto hs = get_best_scoring_pairs(al1, al2, mu, sigma);
+    thread_local std::vector<ScoredAlignmentPair> hs;
+    get_best_scoring_pairs(hs, al1, al2, mu, sigma);
     std::sort(hs.begin(), hs.end(), by_score<ScoredAlignmentPair>);
     deduplicate_scored_pairs(hs);
     pick_random_top_pair(hs, rng);
@@ -892,7 +904,9 @@ void align_PE_read_last(AlignTmpRes& res, const Record& rec1, const Record& rec2
         sam.add_pair(a1, a2, rec1, rec2, read1.rc, read2.rc, (uint8_t)res.mapq1, (uint8_t)res.mapq2, proper, true, det);
     } else if (res.type == 4) {
         size_t pos = 0;
-        std::vector<std::pair<int, Alignment>> cache1, cache2;   // nam_id -> alignment (small; linear lookup)
+        thread_local std::vector<std::pair<int, Alignment>> cache1, cache2;   // nam_id -> alignment (small; linear lookup)
+        cache1.clear();
+        cache2.clear();
         auto find_c = [](std::vector<std::pair<int, Alignment>>& c, int id) -> Alignment* {
             for (auto& x : c) if (x.first == id) return &x.second;
             return nullptr;
@@ -903,7 +917,8 @@ void align_PE_read_last(AlignTmpRes& res, const Record& rec1, const Record& rec2
         Alignment a2_indv_max = res.align_res[pos];
         cache2.push_back({res.todo_nams[pos].nam_id, a2_indv_max});
         pos++;
-        std::vector<ScoredAlignmentPair> hs;
+        thread_local std::vector<ScoredAlignmentPair> hs;
+        hs.clear();
         for (int i = 0; i < res.type4_loop_size; ++i) {
             const Nam& n1 = res.type4_nams[2 * i];
             const Nam& n2 = res.type4_nams[2 * i + 1];

@@ -89,9 +89,9 @@ void Sam::add_unmapped(const Record& r, uint16_t flags) {   // sam.cpp:77-92
     out_ += '\t';
     append_uint(out_, flags);
     out_ += "\t*\t0\t0\t*\t*\t0\t0\t";
-    out_.append(r.seq.empty() ? "*" : r.seq);
+    out_.append(r.seq.empty() ? std::string_view("*") : std::string_view(r.seq));
     out_ += '\t';
-    out_.append(r.qual.empty() ? "*" : r.qual);
+    out_.append(r.qual.empty() ? std::string_view("*") : std::string_view(r.qual));
     out_ += tail_;
 }
 
@@ -106,9 +106,9 @@ void Sam::add_unmapped_mate(const Record& r, uint16_t flags, const std::string& 
     out_ += "\t0\t*\t=\t";
     append_uint(out_, (uint32_t)(mate_pos + 1));
     out_ += "\t0\t";
-    out_.append(r.seq.empty() ? "*" : r.seq);
+    out_.append(r.seq.empty() ? std::string_view("*") : std::string_view(r.seq));
     out_ += '\t';
-    out_.append(r.qual.empty() ? "*" : r.qual);
+    out_.append(r.qual.empty() ? std::string_view("*") : std::string_view(r.qual));
     out_ += tail_;
 }
 
@@ -164,14 +164,14 @@ void Sam::add_record(const std::string& qname, uint16_t flags, const std::string
                 o.resize(at + qual.size());
                 reverse_into(qual, &o[at]);
             }
-        } else o.append(qual.empty() ? "*" : qual);
+        } else o.append(qual.empty() ? std::string_view("*") : std::string_view(qual));
         o += "\tNM:i:";
         append_int(o, ed);
         o += "\tAS:i:";
         append_int(o, score);
     } else {
         o += '\t';
-        o.append(qual.empty() ? "*" : qual);
+        o.append(qual.empty() ? std::string_view("*") : std::string_view(qual));
     }
     if (details_) append_details(o, d, flags & 1);
     o += tail_;

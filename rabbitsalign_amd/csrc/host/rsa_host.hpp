@@ -21,8 +21,73 @@ namespace rsa {
 // ---------------------------------------------------------------- CIGAR ---
 enum CigarOp : uint8_t { C_M = 0, C_I = 1, C_D = 2, C_N = 3, C_S = 4, C_H = 5, C_P = 6, C_EQ = 7, C_X = 8 };
 
+// The std::vector<uint32_t> subset a CIGAR needs, with the first kInline ops
+// stored in the object: a read's alignments (usually a handful of =/X/S ops)
+// are built, copied and moved without touching the heap.
+class OpVec {
+public:
+    static constexpr uint32_t kInline = 12;
+    OpVec() = default;
+    OpVec(const OpVec& o) { assign(o.begin(), o.end()); }
+    OpVec(OpVec&& o) noexcept { steal(o); }
+    OpVec& operator=(const OpVec& o) {
+        if (this != &o) { n_ = 0; assign(o.begin(), o.end()); }
+        return *this;
+    }
+    OpVec& operator=(OpVec&& o) noexcept {
+        if (this != &o) { release(); steal(o); }
+        return *this;
+    }
+    ~OpVec() { release(); }
+    bool empty() const { return n_ == 0; }
+    size_t size() const { return n_; }
+    uint32_t* data() { return p_ ? p_ : buf_; }
+    const uint32_t* data() const { return p_ ? p_ : buf_; }
+    uint32_t* begin() { return data(); }
+    uint32_t* end() { return data() + n_; }
+    const uint32_t* begin() const { return data(); }
+    const uint32_t* end() const { return data() + n_; }
+    uint32_t& operator[](size_t i) { return data()[i]; }
+    uint32_t operator[](size_t i) const { return data()[i]; }
+    uint32_t& back() { return data()[n_ - 1]; }
+    uint32_t back() const { return data()[n_ - 1]; }
+    void clear() { n_ = 0; }
+    void reserve(size_t c) { if (c > cap()) grow(c); }
+    void push_back(uint32_t v) {
+        if (n_ == cap()) grow(2 * (size_t)cap());
+        data()[n_++] = v;
+    }
+    template <class It> void assign(It first, It last) {
+        const size_t n = (size_t)(last - first);
+        n_ = 0;
+        reserve(n);
+        uint32_t* d = data();
+        for (size_t i = 0; i < n; ++i) d[i] = (uint32_t)first[i];
+        n_ = (uint32_t)n;
+    }
+private:
+    uint32_t cap() const { return p_ ? cap_ : kInline; }
+    void grow(size_t c) {
+        uint32_t* q = new uint32_t[c];
+        memcpy(q, data(), sizeof(uint32_t) * n_);
+        delete[] p_;
+        p_ = q;
+        cap_ = (uint32_t)c;
+    }
+    void release() { delete[] p_; p_ = nullptr; n_ = 0; }
+    void steal(OpVec& o) {
+        n_ = o.n_;
+        if (o.p_) { p_ = o.p_; cap_ = o.cap_; o.p_ = nullptr; }
+        else memcpy(buf_, o.buf_, sizeof(uint32_t) * n_);
+        o.n_ = 0;
+    }
+    uint32_t* p_ = nullptr;                     // heap storage once past kInline
+    uint32_t n_ = 0, cap_ = 0;
+    uint32_t buf_[kInline];
+};
+
 struct Cigar {                                  // src/cigar.hpp:23-93
-    std::vector<uint32_t> ops;
+    OpVec ops;
     bool empty() const { return ops.empty(); }
     void push(uint32_t op, uint32_t len) {
         if (ops.empty() || (ops.back() & 0xf) != op) ops.push_back(len << 4 | op);
