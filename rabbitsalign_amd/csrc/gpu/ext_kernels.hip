@@ -1028,6 +1028,91 @@ k_cigar_compact(rsa_aln* __restrict__ alns, int n_jobs, const uint32_t* __restri
     if (t == CC_THREADS - 1) *total = s_sum[t];
 }
 
+// Multi-block CIGAR compaction (replaces the single-workgroup k_cigar_compact on
+// the default path): per-block totals, a scan of the block totals, then every
+// block lays its jobs' ops out back to back with a flat, coalesced copy.
+#define CCP_THREADS 256
+__device__ __forceinline__ uint64_t block_incl_scan(uint64_t v, uint64_t* s) {
+    const int t = threadIdx.x;
+    s[t] = v;
+    __syncthreads();
+    for (int o = 1; o < CCP_THREADS; o <<= 1) {
+        const uint64_t x = t >= o ? s[t - o] : 0;
+        __syncthreads();
+        s[t] += x;
+        __syncthreads();
+    }
+    return s[t];
+}
+
+__global__ void __launch_bounds__(CCP_THREADS)
+k_cig_bsum(const rsa_aln* __restrict__ alns, int n_jobs, uint64_t* __restrict__ bsum) {
+    __shared__ uint64_t s[CCP_THREADS];
+    const int i = blockIdx.x * CCP_THREADS + threadIdx.x;
+    const uint64_t v = i < n_jobs ? alns[i].cigar_len : 0;
+    const uint64_t incl = block_incl_scan(v, s);
+    if (threadIdx.x == CCP_THREADS - 1) bsum[blockIdx.x] = incl;
+}
+
+// exclusive scan of nb block totals in place (one workgroup); *total = their sum
+__global__ void __launch_bounds__(1024) k_cig_bscan(uint64_t* __restrict__ bsum, int nb, uint64_t* __restrict__ total) {
+    __shared__ uint64_t s[1024];
+    const int t = threadIdx.x;
+    const int per = (nb + 1023) / 1024;
+    const int a = min(nb, t * per), b = min(nb, a + per);
+    uint64_t mine = 0;
+    for (int i = a; i < b; ++i) mine += bsum[i];
+    s[t] = mine;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const uint64_t x = t >= o ? s[t - o] : 0;
+        __syncthreads();
+        s[t] += x;
+        __syncthreads();
+    }
+    uint64_t off = s[t] - mine;
+    for (int i = a; i < b; ++i) {
+        const uint64_t v = bsum[i];
+        bsum[i] = off;
+        off += v;
+    }
+    if (t == 1023) *total = s[t];
+}
+
+__global__ void __launch_bounds__(CCP_THREADS)
+k_cig_copy(rsa_aln* __restrict__ alns, int n_jobs, const uint64_t* __restrict__ bbase,
+           const uint32_t* __restrict__ slots, uint32_t* __restrict__ dense) {
+    __shared__ uint64_t s[CCP_THREADS];
+    __shared__ uint64_t s_src[CCP_THREADS];
+    const int t = threadIdx.x;
+    const int i = blockIdx.x * CCP_THREADS + t;
+    const uint32_t len = i < n_jobs ? alns[i].cigar_len : 0;
+    const uint64_t src = i < n_jobs ? alns[i].cigar_offset : 0;
+    const uint64_t incl = block_incl_scan(len, s);     // s[] now holds inclusive offsets
+    s_src[t] = src;
+    __syncthreads();
+    const uint64_t base = bbase[blockIdx.x];
+    const uint64_t tot = s[CCP_THREADS - 1];
+    for (uint64_t f = t; f < tot; f += CCP_THREADS) {
+        int lo = 0, hi = CCP_THREADS - 1;                // first job whose inclusive end exceeds f
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s[mid] > f) hi = mid; else lo = mid + 1;
+        }
+        const uint64_t start = lo ? s[lo - 1] : 0;
+        dense[base + f] = slots[s_src[lo] + (f - start)];
+    }
+    if (i < n_jobs) alns[i].cigar_offset = base + incl - len;
+}
+
+void launch_cigar_compact(hipStream_t st, rsa_aln* alns, int n_jobs, const uint32_t* slots, uint32_t* dense,
+                          uint64_t* bsum, uint64_t* total) {
+    const int nb = (n_jobs + CCP_THREADS - 1) / CCP_THREADS;
+    hipLaunchKernelGGL(k_cig_bsum, dim3(nb), dim3(CCP_THREADS), 0, st, alns, n_jobs, bsum);
+    hipLaunchKernelGGL(k_cig_bscan, dim3(1), dim3(1024), 0, st, bsum, nb, total);
+    hipLaunchKernelGGL(k_cig_copy, dim3(nb), dim3(CCP_THREADS), 0, st, alns, n_jobs, bsum, slots, dense);
+}
+
 // host-side launcher: RMAX from the longest query of the batch, V = cell
 // bookkeeping variant (0: per cell, 1: per column)
 void launch_ext_scan(int rmax, int variant, dim3 grid, dim3 block, hipStream_t st, const ExtJobDev* jobs, int n,

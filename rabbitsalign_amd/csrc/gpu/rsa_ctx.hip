@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -39,6 +40,8 @@ void launch_ext_band64(bool reg, dim3 grid, hipStream_t st, const ExtJobDev* job
                        int mismatch, int gO, int gE, int bonus, const int* queue, const int* qcount, int* overflow,
                        int* ocount);
 __global__ void k_cigar_compact(rsa_aln* alns, int n_jobs, const uint32_t* slots, uint32_t* dense, uint64_t* total);
+void launch_cigar_compact(hipStream_t st, rsa_aln* alns, int n_jobs, const uint32_t* slots, uint32_t* dense,
+                          uint64_t* bsum, uint64_t* total);
 
 int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, const rsa_read_batch* rb,
              int32_t rescue_level, uint32_t rescue_cutoff, rsa_nam_batch* out, std::string& err, SeedCounters& c);
@@ -94,7 +97,7 @@ struct Lane {
     bool busy = false;
     // extension
     DevBuf d_q, d_jobs, d_scan, d_alns, d_alns2, d_cig, d_dense, d_raw, d_scratch, d_over, d_queue, d_idx, d_status,
-        d_order;
+        d_order, d_bsum;
     HostBuf h_jobs, h_over, h_status, h_order;
     // seeding
     SeedBufs sb;
@@ -153,6 +156,28 @@ static void release_lane(rsa_ctx* ctx, Lane* l) {
     }
     ctx->lane_cv.notify_one();
 }
+
+// wall-time breakdown of one entry-point call into ctx->stats (call_ms / lane_wait_ms / device_wait_ms)
+struct CallTimer {
+    rsa_ctx* ctx;
+    int which;
+    std::chrono::steady_clock::time_point t0;
+    double lane_ms = 0;
+    CallTimer(rsa_ctx* c, int w) : ctx(c), which(w), t0(std::chrono::steady_clock::now()) { device_wait_ms() = 0; }
+    Lane* lane() {
+        const auto t = std::chrono::steady_clock::now();
+        Lane* l = acquire_lane(ctx);
+        lane_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+        return l;
+    }
+    ~CallTimer() {
+        const double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        std::lock_guard<std::mutex> g(ctx->stat_m);
+        ctx->stats.call_ms[which] += wall;
+        ctx->stats.lane_wait_ms[which] += lane_ms;
+        ctx->stats.device_wait_ms[which] += device_wait_ms();
+    }
+};
 
 struct LaneGuard {
     rsa_ctx* ctx; Lane* l;
@@ -254,6 +279,12 @@ static int scan_variant() {
     return v ? atoi(v) : 2;
 }
 
+// CIGAR compaction (RSA_COMPACT_V: 1 (default) multi-block scan + flat copy, 0 one workgroup)
+static int compact_variant() {
+    const char* v = getenv("RSA_COMPACT_V");
+    return v ? atoi(v) : 1;
+}
+
 // grouped scan (RSA_SCAN_G: 1 (default) 16 lanes per job, 4 jobs per wave, for
 // queries up to 256 bp; 0 = one job per wave for every job)
 static int scan_grouped() {
@@ -281,7 +312,8 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
     if (n == 0) return RSA_OK;
     if (out->cigar_capacity < bound) { set_err(ctx, "rsa_extend: cigar_pool too small"); return RSA_ERR_CAPACITY; }
     HIPCHK(hipSetDevice(ctx->device));
-    Lane* L = acquire_lane(ctx);
+    CallTimer ct(ctx, 1);
+    Lane* L = ct.lane();
     if (!L) { set_err(ctx, "rsa_extend: cannot create HIP stream"); return RSA_ERR_HIP; }
     LaneGuard guard{ctx, L};
     // host job descriptors
@@ -328,6 +360,7 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
     HIPCHK(L->d_over.ensure(sizeof(int) * n));
     HIPCHK(L->d_queue.ensure(sizeof(int) * n));
     HIPCHK(L->d_status.ensure(sizeof(ExtStatus)));
+    HIPCHK(L->d_bsum.ensure(sizeof(uint64_t) * ((n + 255) / 256 + 1)));
     HIPCHK(L->h_status.ensure(sizeof(ExtStatus)));
     hipStream_t st = L->stream;
     ExtStatus* dst = L->d_status.as<ExtStatus>();
@@ -421,8 +454,12 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
     HIPCHK(hipGetLastError());
     L->kt.end(st);
     auto compact_and_copy = [&](uint64_t guess) -> int {
-        hipLaunchKernelGGL(k_cigar_compact, dim3(1), dim3(1024), 0, st, L->d_alns.as<rsa_aln>(), (int)n,
-                           L->d_cig.as<uint32_t>(), L->d_dense.as<uint32_t>(), &dst->total);
+        if (compact_variant())
+            launch_cigar_compact(st, L->d_alns.as<rsa_aln>(), (int)n, L->d_cig.as<uint32_t>(),
+                                 L->d_dense.as<uint32_t>(), L->d_bsum.as<uint64_t>(), &dst->total);
+        else
+            hipLaunchKernelGGL(k_cigar_compact, dim3(1), dim3(1024), 0, st, L->d_alns.as<rsa_aln>(), (int)n,
+                               L->d_cig.as<uint32_t>(), L->d_dense.as<uint32_t>(), &dst->total);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(L->h_status.p, L->d_status.p, sizeof(ExtStatus), hipMemcpyDeviceToHost, st));
         HIPCHK(hipMemcpyAsync(out->alns, L->d_alns.p, sizeof(rsa_aln) * n, hipMemcpyDeviceToHost, st));
@@ -527,7 +564,8 @@ int rsa_seed(rsa_ctx* ctx, const rsa_read_batch* rb, int32_t rescue_level, uint3
     if (rb->n_reads == 0) { out->needed = 0; if (out->offsets) out->offsets[0] = 0; return RSA_OK; }
     if (!ctx->d_rs || !ctx->d_starts) { set_err(ctx, "rsa_seed: context opened without an index"); return RSA_ERR_ARG; }
     HIPCHK(hipSetDevice(ctx->device));
-    Lane* L = acquire_lane(ctx);
+    CallTimer ct(ctx, 0);
+    Lane* L = ct.lane();
     if (!L) { set_err(ctx, "cannot create HIP stream"); return RSA_ERR_HIP; }
     LaneGuard guard{ctx, L};
     std::string err;

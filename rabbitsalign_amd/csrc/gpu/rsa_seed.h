@@ -1,5 +1,6 @@
 // rsa_seed.h -- host/device shared declarations of the seeding kernels.
 #pragma once
+#include <chrono>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -25,16 +26,26 @@ struct SeedBufs {
 
 // Wait for everything queued on `s` so far without burning a host core
 // (hipEventBlockingSync); the host pipeline runs more workers than cores.
+// time this thread spent blocked in stream_wait (the entry points read and reset it)
+inline double& device_wait_ms() {
+    static thread_local double ms = 0;
+    return ms;
+}
+
 inline hipError_t stream_wait(hipStream_t s, hipEvent_t& e) {
     static const bool spin = [] { const char* v = getenv("RSA_SPIN_WAIT"); return v && v[0] == '1'; }();
-    if (spin) return hipStreamSynchronize(s);
-    if (!e) {
-        hipError_t err = hipEventCreateWithFlags(&e, hipEventBlockingSync | hipEventDisableTiming);
-        if (err != hipSuccess) return err;
+    const auto t0 = std::chrono::steady_clock::now();
+    hipError_t err;
+    if (spin) {
+        err = hipStreamSynchronize(s);
+    } else {
+        err = hipSuccess;
+        if (!e) err = hipEventCreateWithFlags(&e, hipEventBlockingSync | hipEventDisableTiming);
+        if (err == hipSuccess) err = hipEventRecord(e, s);
+        if (err == hipSuccess) err = hipEventSynchronize(e);
     }
-    hipError_t err = hipEventRecord(e, s);
-    if (err != hipSuccess) return err;
-    return hipEventSynchronize(e);
+    device_wait_ms() += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return err;
 }
 
 void seed_bufs_release(SeedBufs& b);

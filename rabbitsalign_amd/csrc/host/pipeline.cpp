@@ -208,8 +208,46 @@ void pe_seed(PeChunk& c, Engine& eng, const MapContext& mc, CpuSlots& slots) {
     c.times.seed += since(t);
 }
 
+// Seeding of several loaded chunks in one engine call (larger, fuller kernels,
+// fewer launches); the output is split back per chunk.  Seeding is a pure
+// function of each read, so the batching is invisible in the results.
+void pe_seed_multi(std::vector<PeChunk*>& cs, Engine& eng, const MapContext& mc, CpuSlots& slots) {
+    if (cs.size() == 1) { pe_seed(*cs[0], eng, mc, slots); return; }
+    std::vector<const std::string*> reads;
+    size_t tot = 0;
+    for (PeChunk* c : cs) tot += 2 * c->r1.size();
+    reads.reserve(tot);
+    for (PeChunk* c : cs)
+        for (size_t i = 0; i < c->r1.size(); ++i) { reads.push_back(&c->r1[i]->seq); reads.push_back(&c->r2[i]->seq); }
+    const auto t = Clock::now();
+    SeedBatchOut all;
+    {
+        Unslot u(slots, eng.offloads());
+        eng.seed(reads, mc.mparams.rescue_level, (unsigned)mc.mparams.rescue_cutoff, all);
+    }
+    const double dt = since(t) / (double)cs.size();
+    size_t r0 = 0;
+    for (PeChunk* c : cs) {
+        const size_t n = 2 * c->r1.size();
+        SeedBatchOut& o = c->seeds;
+        const uint64_t a = all.offsets[r0], b = all.offsets[r0 + n];
+        o.nams.assign(all.nams.begin() + (long)a, all.nams.begin() + (long)b);
+        o.offsets.resize(n + 1);
+        for (size_t i = 0; i <= n; ++i) o.offsets[i] = all.offsets[r0 + i] - a;
+        o.nonrep.assign(all.nonrep.begin() + (long)r0, all.nonrep.begin() + (long)(r0 + n));
+        o.rescued.assign(all.rescued.begin() + (long)r0, all.rescued.begin() + (long)(r0 + n));
+        c->times.seed += dt;
+        r0 += n;
+    }
+}
+
 // part() of every pair in chunk order (pc.cpp:1739-1766) on the seeded chunk
-void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize) {
+// on_frozen (sequential phase only) runs once, right after the pair whose
+// sample freezes the insert-size estimate: from there on no later chunk depends
+// on this one's remaining pairs, so the other workers can start.
+template <class OnFrozen>
+void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize, OnFrozen&& on_frozen) {
+    bool was_frozen = isize.frozen();
     c.rng.seed((unsigned)c.index);
     const size_t n = c.r1.size();
     if (n == 0) return;
@@ -258,9 +296,17 @@ void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize) {
         const Read read1(c.r1[i]->seq, c.rc(i, 0)), read2(c.r2[i]->seq, c.rc(i, 1));
         align_PE_read_part(c.res[i], *c.r1[i], *c.r2[i], read1, read2, nams, rescued, c.stats, isize, mc, c.rng);
         c.stats.n_reads += 2;
+        if (!was_frozen && isize.frozen()) {
+            was_frozen = true;
+            on_frozen(c);
+        }
     }
     c.seeds = SeedBatchOut();
     c.times.part += since(t);
+}
+
+void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize) {
+    pe_part(c, mc, isize, [](PeChunk&) {});
 }
 
 void pe_get_str(PeChunk& c, const MapContext& mc, float mu, float sigma, std::vector<SwJob>& jobs) {
@@ -325,6 +371,8 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
     size_t next_seed = 0;          // every chunk below is claimed
     size_t consumed = 0;           // chunks handed past stage 1
     bool frozen = false, done = false;
+    bool early = false;            // the parallel stage opened from inside part() (early_freeze)
+    bool leader_busy = true;       // the leader may still hand a chunk over: nobody ends the run before
     bool lead_seeded = false;      // prefetch waits until chunk 0 is seeded: it would only queue
                                    // other chunks' seeding ahead of the single-worker timeline
     size_t next_par = 0;           // next chunk for the parallel stage (valid once frozen)
@@ -337,6 +385,24 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
     // finished chunks are recycled (process-wide, across runs), so the per-pair
     // result vectors stop allocating and no run ends by freeing them one by one
     auto recycle = [&](std::unique_ptr<PeChunk> c) { chunk_pool().put(std::move(c)); };
+    // prefetch claims up to this many consecutive chunks per seeding call (RSA_SEED_BATCH,
+    // default 1: A/B on the bench, 1 -> 11.75/11.61, 4 -> 11.00/10.60 Mreads/s)
+    const size_t seed_batch = std::max<size_t>(1, getenv("RSA_SEED_BATCH") ? (size_t)atol(getenv("RSA_SEED_BATCH")) : 1);
+    auto stage1_multi = [&](const std::vector<size_t>& idxs) {
+        std::vector<std::unique_ptr<PeChunk>> cs;
+        std::vector<PeChunk*> ps;
+        for (size_t idx : idxs) {
+            std::unique_ptr<PeChunk> c = chunk_pool().take();
+            if (!c) c = std::make_unique<PeChunk>();
+            const auto t = Clock::now();
+            pe_load(*c, r1, r2, idx, chunk);
+            c->times.load += since(t);
+            ps.push_back(c.get());
+            cs.push_back(std::move(c));
+        }
+        pe_seed_multi(ps, eng, mc, slots);
+        return cs;
+    };
     auto stage1 = [&](size_t idx) {
         std::unique_ptr<PeChunk> c = chunk_pool().take();
         if (!c) c = std::make_unique<PeChunk>();
@@ -398,6 +464,16 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
         PhaseTimes lt;
         std::unique_ptr<SlotHold> hold(new SlotHold(slots));
         try {
+            // inside the leader's part(): the estimate just froze, so chunks after the one being
+            // parted no longer depend on the sequential timeline -- open the parallel stage now
+            auto early_freeze = [&](PeChunk& cur_chunk) {
+                std::lock_guard<std::mutex> g(m);
+                frozen = true;
+                frozen_isize = isize;
+                next_par = std::min(cur_chunk.index + 1, n_chunks);
+                early = true;
+                cv.notify_all();
+            };
             if (leader) {
                 // ---- single-worker timeline until the insert-size estimate freezes ----
                 auto pre = acquire(0);
@@ -407,7 +483,7 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                     lead_seeded = true;
                     cv.notify_all();
                 }
-                pe_part(*pre, mc, isize);
+                pe_part(*pre, mc, isize, early_freeze);
                 size_t next = 1;
                 for (;;) {
                     if (isize.frozen() || next > n_chunks) break;
@@ -416,7 +492,7 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                     if (next < n_chunks) {
                         cur = acquire(next);
                         if (!cur) return;
-                        pe_part(*cur, mc, isize);
+                        pe_part(*cur, mc, isize, early_freeze);
                     }
                     next++;
                     const auto te = Clock::now();
@@ -440,7 +516,8 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                 frozen = true;
                 frozen_isize = isize;
                 handed = std::move(pre);                 // may be null: everything was sequential
-                next_par = std::min(next, n_chunks);
+                leader_busy = false;
+                if (!early) next_par = std::min(next, n_chunks);
                 if (next_par >= n_chunks && !handed) done = true;
                 cv.notify_all();
             }
@@ -448,6 +525,7 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
             for (;;) {
                 std::unique_ptr<PeChunk> c;
                 size_t idx = SIZE_MAX, pf = SIZE_MAX;
+                std::vector<size_t> pfs;
                 {
                     std::unique_lock<std::mutex> g(m);
                     for (;;) {
@@ -456,11 +534,15 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                         if (frozen && next_par < n_chunks) { idx = next_par++; break; }
                         if (lead_seeded && next_seed < n_chunks && next_seed < consumed + window) {
                             pf = next_seed;
-                            claimed[pf] = 1;
+                            // a run of consecutive unclaimed chunks, seeded in one engine call
+                            for (size_t q = next_seed; q < n_chunks && pfs.size() < seed_batch && !claimed[q]; ++q) {
+                                claimed[q] = 1;
+                                pfs.push_back(q);
+                            }
                             while (next_seed < n_chunks && claimed[next_seed]) next_seed++;
                             break;
                         }
-                        if (frozen && next_par >= n_chunks) { done = true; cv.notify_all(); break; }
+                        if (frozen && next_par >= n_chunks && !leader_busy) { done = true; cv.notify_all(); break; }
                         g.unlock();
                         {
                             Unslot u(slots, true);
@@ -490,9 +572,9 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                     continue;
                 }
                 if (pf != SIZE_MAX) {
-                    auto s1 = stage1(pf);
+                    auto s1 = stage1_multi(pfs);
                     std::lock_guard<std::mutex> g(m);
-                    seeded.emplace(pf, std::move(s1));
+                    for (size_t q = 0; q < pfs.size(); ++q) seeded.emplace(pfs[q], std::move(s1[q]));
                     cv.notify_all();
                     continue;
                 }

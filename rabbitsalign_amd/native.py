@@ -91,15 +91,20 @@ class KernelStats(C.Structure):
                 ("lookups_found", C.c_uint64), ("filtered", C.c_uint64), ("hits", C.c_uint64),
                 ("nams", C.c_uint64), ("rescued_reads", C.c_uint64),
                 ("jobs", C.c_uint64), ("dp_cells", C.c_uint64),
-                ("band_deferred", C.c_uint64), ("band_overflow", C.c_uint64)]
+                ("band_deferred", C.c_uint64), ("band_overflow", C.c_uint64),
+                ("call_ms", C.c_double * 2), ("lane_wait_ms", C.c_double * 2), ("device_wait_ms", C.c_double * 2)]
 
 
 def stats_dict(ks: "KernelStats") -> dict:
     """Flatten a KernelStats into {"kernels": {name: {ms, launches, alg_bytes}}, counters...}."""
     out = {"kernels": {k: {"ms": ks.kernel_ms[i], "launches": int(ks.launches[i]), "alg_bytes": ks.alg_bytes[i]}
                        for i, k in enumerate(KERNELS)}}
-    for f, _ in KernelStats._fields_[3:]:
-        out[f] = int(getattr(ks, f))
+    for f, t in KernelStats._fields_[3:]:
+        if t in (C.c_uint64,):
+            out[f] = int(getattr(ks, f))
+    # host-side view of the engine calls: {seed|extend: {call, lane_wait, device_wait} ms}
+    out["calls_ms"] = {nm: {"call": round(ks.call_ms[i], 3), "lane_wait": round(ks.lane_wait_ms[i], 3),
+                            "device_wait": round(ks.device_wait_ms[i], 3)} for i, nm in enumerate(("seed", "extend"))}
     return out
 
 
