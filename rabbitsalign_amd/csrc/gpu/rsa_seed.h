@@ -19,8 +19,8 @@ struct SeedIndexParams {
 struct SeedBufs {
     void* p[32] = {nullptr};
     size_t cap[32] = {0};
-    void* h[8] = {nullptr};
-    size_t hcap[8] = {0};
+    void* h[12] = {nullptr};
+    size_t hcap[12] = {0};
     hipEvent_t done = nullptr;   // blocking-sync event: the calling thread sleeps instead of spinning
 };
 

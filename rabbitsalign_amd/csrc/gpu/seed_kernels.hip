@@ -1423,13 +1423,14 @@ enum {
     B_SEQ, B_ROFF, B_RLEN, B_QBASE, B_QRS, B_QCNT, B_SYNC, B_QI, B_ST, B_HOFF, B_HITS, B_OPEN, B_NAM1, B_NCNT1,
     B_NONREP, B_FLAGS, B_MAP, B_ROFF2, B_NAM2, B_NCNT2, B_LIST, B_RBUF, B_OUT, B_OOFF, B_SLOTS
 };
-enum { H_ST, H_HOFF, H_FLAGS, H_CNT, H_ROFF, H_LIST, H_OOFF, H_CNT2 };
+// every host side of a transfer is page-locked: a pageable one would make the copy synchronous
+enum { H_ST, H_HOFF, H_FLAGS, H_CNT, H_ROFF, H_LIST, H_OOFF, H_CNT2, H_QBASE, H_NONREP };
 
 void seed_bufs_release(SeedBufs& b) {
     for (int i = 0; i < 32; ++i) if (b.p[i]) (void)hipFree(b.p[i]);
-    for (int i = 0; i < 8; ++i) if (b.h[i]) (void)hipHostFree(b.h[i]);
+    for (int i = 0; i < 12; ++i) if (b.h[i]) (void)hipHostFree(b.h[i]);
     for (int i = 0; i < 32; ++i) { b.p[i] = nullptr; b.cap[i] = 0; }
-    for (int i = 0; i < 8; ++i) { b.h[i] = nullptr; b.hcap[i] = 0; }
+    for (int i = 0; i < 12; ++i) { b.h[i] = nullptr; b.hcap[i] = 0; }
     if (b.done) (void)hipEventDestroy(b.done);
     b.done = nullptr;
 }
@@ -1501,7 +1502,9 @@ int seed_stage_randstrobes(SeedBufs& b, hipStream_t st, const SeedIndexParams& p
     SCHK(hipMemcpyAsync(b.p[B_SEQ], rb->seq, total_len, hipMemcpyHostToDevice, st));
     SCHK(hipMemcpyAsync(b.p[B_ROFF], rb->offsets, 8ull * n, hipMemcpyHostToDevice, st));
     SCHK(hipMemcpyAsync(b.p[B_RLEN], rb->lengths, 4ull * n, hipMemcpyHostToDevice, st));
-    SCHK(hipMemcpyAsync(b.p[B_QBASE], qbase.data(), 8ull * (n + 1), hipMemcpyHostToDevice, st));
+    SCHK(hens(b, H_QBASE, 8ull * (n + 1)));
+    memcpy(b.h[H_QBASE], qbase.data(), 8ull * (n + 1));
+    SCHK(hipMemcpyAsync(b.p[B_QBASE], b.h[H_QBASE], 8ull * (n + 1), hipMemcpyHostToDevice, st));
     uint32_t max_len = 0;
     for (uint32_t i = 0; i < n; ++i) max_len = std::max(max_len, rb->lengths[i]);
     const bool wave = max_len <= RS_MAXLEN && p.k <= 32 && p.s <= 32 && p.k - p.s + 1 <= RS_RING &&
@@ -1655,8 +1658,10 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
         for (int i : big) if (HP(H_FLAGS, uint32_t)[i] & 2u) { err = "rsa_seed: robin_hood emulation overflow"; return RSA_ERR_NOMEM; }
     }
     // nonrepetitive fraction to host
-    SCHK(hipMemcpyAsync(out->nonrepetitive_fraction, b.p[B_NONREP], 4ull * n, hipMemcpyDeviceToHost, st));
+    SCHK(hens(b, H_NONREP, 4ull * n));
+    SCHK(hipMemcpyAsync(b.h[H_NONREP], b.p[B_NONREP], 4ull * n, hipMemcpyDeviceToHost, st));
     SCHK(stream_wait(st, b.done));
+    memcpy(out->nonrepetitive_fraction, b.h[H_NONREP], 4ull * n);
     // rescue decision (aln.cpp:1954-1962)
     std::vector<int> resc;
     std::vector<uint32_t> n1(HP(H_CNT, uint32_t), HP(H_CNT, uint32_t) + n);
@@ -1682,7 +1687,9 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
         SCHK(dens(b, B_OUT, (sizeof(HitD) + 1) * (R + 1)));
         SCHK(dens(b, B_LIST, 4ull * resc.size()));
         SCHK(hipMemcpyAsync(b.p[B_ROFF2], roff, 8ull * (n + 1), hipMemcpyHostToDevice, st));
-        SCHK(hipMemcpyAsync(b.p[B_LIST], resc.data(), 4ull * resc.size(), hipMemcpyHostToDevice, st));
+        SCHK(hens(b, H_LIST, 4ull * resc.size()));
+        memcpy(b.h[H_LIST], resc.data(), 4ull * resc.size());
+        SCHK(hipMemcpyAsync(b.p[B_LIST], b.h[H_LIST], 4ull * resc.size(), hipMemcpyHostToDevice, st));
         HitD* grp = DP(B_OUT, HitD);
         uint8_t* added = (uint8_t*)(grp + (R + 1));
         for (size_t a = 0; a < resc.size(); a += chunk) {
