@@ -133,7 +133,8 @@ def main():
     ap.add_argument("--chunk-size", type=int, default=10000)
     ap.add_argument("--ref-seed", type=int, default=1)
     ap.add_argument("--read-seed", type=int, default=7)
-    ap.add_argument("--cpu-pairs", type=int, default=200_000, help="cpu_baseline sample (pairs)")
+    ap.add_argument("--cpu-pairs", type=int, default=2_000_000,
+                    help="cpu_baseline sample (pairs; ~10 s of CPU work on 16 cores at 2x150)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ref-len", type=int, default=0, help="override reference length (testing only)")
     ap.add_argument("--stats-out", default="", help="write per-kernel stats JSON here")
@@ -176,7 +177,8 @@ def main():
                            threads=threads)
     info = m.info()
     log(rank, f"index ready in {time.time()-t:.1f} s: {info['n_randstrobes']} randstrobes, bits {info['bits']}, "
-              f"upload {info['upload_seconds']:.2f} s, engine {m.engine}")
+              f"built on {'GPU' if info['index_on_device'] else 'host'} in {info['index_seconds']:.2f} s "
+              f"(device phases ms {info['index_device_ms']}), upload {info['upload_seconds']:.2f} s, engine {m.engine}")
 
     P = args.pairs
     total_steps = args.warmup + args.steps
@@ -224,7 +226,7 @@ def main():
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if os.path.exists(REF_CPU_LIB):
-            n_cpu = min(args.cpu_pairs, P)
+            n_cpu = args.cpu_pairs
             sample = m.synthetic_reads(args.read_seed, 0, n_cpu, wl["read_len"], wl["mu"], wl["sigma"], wl["paired"])
             g = m.map(sample, threads=threads, chunk_size=args.chunk_size)
             log(rank, f"cpu_baseline: opening CPU path on the same index ({cores} cores)")
@@ -258,6 +260,11 @@ def main():
                        "read_len": wl["read_len"], "paired": wl["paired"], "pairs_per_step_per_gpu": P,
                        "host_threads": threads, "chunk_size": args.chunk_size, "index_bits": info["bits"],
                        "randstrobes": info["n_randstrobes"], "parallelism": f"dp{world} (replicated index)"},
+            "index_build": {"on": "gpu" if info["index_on_device"] else "host",
+                            "seconds": round(info["index_seconds"], 3), "device_ms": info["index_device_ms"],
+                            "replayed_segments": info["index_replayed_segments"],
+                            "note": "StrobemerIndex::populate (index.cpp:141-309) via rsa_index_build_run; "
+                                    "seconds include the D2H of the host copy"},
             "roofline": rl,
             "cpu_baseline": cpu,
             "parity": parity,

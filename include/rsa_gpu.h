@@ -15,6 +15,7 @@
  *                            gasal_fail / Aligner::align fallback (src/pc.cpp:1779-1788); the
  *                            result is exactly Aligner::align's AlignmentInfo
  *                            (src/aligner.cpp:114-210, src/aligner.hpp:20-30)
+ *   rsa_index_build_*     <- StrobemerIndex::populate (src/index.cpp:141-309)
  *
  * Threading: every entry point is thread-safe on one context; concurrent calls
  * run on distinct HIP streams of the context (one stream "lane" per call).
@@ -175,6 +176,47 @@ uint64_t rsa_extend_cigar_bound(const rsa_job_batch* jobs);
  * buffer works, these are only faster.  NULL on failure. */
 void* rsa_host_alloc(size_t bytes);
 void rsa_host_free(void* p);
+
+/* ---- index construction -------------------------------- */
+
+/* StrobemerIndex::populate (src/index.cpp:141-239) on the GPU: syncmers and
+ * randstrobes of every contig (count_all_randstrobes / assign_all_randstrobes,
+ * index.cpp:28-69, 244-309), the sort by (hash, position) (index.cpp:168),
+ * the bucket table with the reference's exact fill rule (index.cpp:174-212)
+ * and the filter cutoff (index.cpp:214-238).  The result is byte-identical to
+ * the host build (and so to the .sti the reference writes; equal (hash,
+ * position) keys in two contigs keep contig order, which pdqsort leaves
+ * unspecified). */
+typedef struct rsa_index_build_params {
+    int32_t k, s, t_syncmer;           /* SyncmerParameters */
+    int32_t w_min, w_max, max_dist;    /* RandstrobeParameters */
+    uint64_t q;
+    int32_t bits;                      /* < 0: pick_bits (index.cpp:135-139) */
+    float f;                           /* top fraction of repetitive hashes (-f, default 0.0002) */
+} rsa_index_build_params;
+
+typedef struct rsa_index_build_info {
+    uint64_t n_randstrobes, n_syncmers, unique_hashes;
+    int32_t bits, filter_cutoff;
+    uint64_t n_segments;               /* reference segments processed in parallel */
+    uint64_t replayed_segments;        /* segments whose warm-up did not converge (replayed from further back) */
+    /* HIP-event times (ms): reference upload, syncmers (all passes), randstrobes,
+     * sort (both radix passes + gathers), bucket table + counts; wall of the call */
+    double ms_upload, ms_syncmers, ms_randstrobes, ms_sort, ms_buckets, ms_total;
+} rsa_index_build_info;
+
+typedef struct rsa_index_build rsa_index_build;
+
+/* Build the index of `ref_seq` (contigs back to back, contig i at
+ * [contig_offsets[i], contig_offsets[i+1])) on `device`; the result stays in
+ * HBM until freed.  NULL on error (message in err). */
+rsa_index_build* rsa_index_build_run(int device, const char* ref_seq, const uint64_t* contig_offsets, int32_t n_contigs,
+                                     const rsa_index_build_params* params, rsa_index_build_info* info, char* err,
+                                     size_t err_len);
+/* Copy the result into caller buffers: randstrobes[info.n_randstrobes],
+ * bucket_starts[2^info.bits + 1]. */
+int rsa_index_build_download(rsa_index_build* b, rsa_ref_randstrobe* randstrobes, uint64_t* bucket_starts);
+void rsa_index_build_free(rsa_index_build* b);
 
 /* ---- instrumentation ------------------------------------------------------ */
 

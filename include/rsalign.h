@@ -48,6 +48,10 @@ typedef struct rsam_info {
     int32_t n_contigs, bits, filter_cutoff, k, canonical_read_length;
     double index_seconds, upload_seconds;
     uint64_t device_resident_bytes;
+    int32_t index_on_device;           /* 1: built on the GPU (rsa_index_build_run), 0: host build or .sti */
+    int32_t pad_;
+    double index_device_ms[6];         /* GPU build phases: upload, syncmers, randstrobes, sort, buckets, total */
+    uint64_t index_replayed_segments;  /* GPU build: segments replayed past their warm-up (tandem repeats) */
 } rsam_info;
 int rsam_get_info(const rsam* m, rsam_info* out);
 

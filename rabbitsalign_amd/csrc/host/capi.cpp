@@ -79,7 +79,7 @@ rsam* rsam_open_files(const char* ref_fa, const char* sti, int read_len, int dev
             m->idx.read(sti);
             if (!(m->idx.params == ip)) throw std::runtime_error("index parameters differ from the read length profile");
         } else {
-            m->idx.build(m->refs, ip, -1, 0.0002f, std::max(1, threads));
+            build_default_index(m->idx, m->refs, ip, -1, 0.0002f, std::max(1, threads), device);
         }
         m->index_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
     } catch (const std::exception& e) {
@@ -100,7 +100,8 @@ rsam* rsam_open_synthetic(uint64_t seed, uint64_t ref_len, int n_contigs, int re
         for (int c = 0; c < n_contigs; ++c) m->refs.names.push_back("chr" + std::to_string(c + 1));
         finish_refs(m->refs);
         auto t = std::chrono::steady_clock::now();
-        m->idx.build(m->refs, IndexParameters::from_read_length(read_len), -1, 0.0002f, std::max(1, threads));
+        build_default_index(m->idx, m->refs, IndexParameters::from_read_length(read_len), -1, 0.0002f,
+                            std::max(1, threads), device);
         m->index_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
     } catch (const std::exception& e) {
         if (err && err_len) snprintf(err, err_len, "%s", e.what());
@@ -136,6 +137,10 @@ int rsam_get_info(const rsam* m, rsam_info* out) {
     out->upload_seconds = m->upload_seconds;
     out->device_resident_bytes = m->refs.concat.size() + m->idx.randstrobes.size() * sizeof(rsa_ref_randstrobe) +
                                  m->idx.bucket_starts.size() * 8;
+    out->index_on_device = m->idx.built_on_device ? 1 : 0;
+    out->pad_ = 0;
+    for (int i = 0; i < 6; ++i) out->index_device_ms[i] = m->idx.device_build_ms[i];
+    out->index_replayed_segments = m->idx.replayed_segments;
     return 0;
 }
 

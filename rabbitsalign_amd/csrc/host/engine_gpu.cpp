@@ -167,6 +167,38 @@ std::unique_ptr<Engine> make_gpu_engine(const References& refs, const StiIndex& 
     return std::unique_ptr<Engine>(new GpuEngine(refs, index, device));
 }
 
+// StrobemerIndex::populate on the GPU (include/rsa_gpu.h rsa_index_build_run),
+// downloaded into the host StiIndex (.sti writing, the host pipeline's
+// parameters, a CPU engine opened on the same index)
+void build_default_index(StiIndex& idx, const References& refs, const IndexParameters& p, int bits_override, float f,
+                         int threads, int device) {
+    (void)threads;
+    rsa_index_build_params bp{};
+    bp.k = p.k; bp.s = p.s; bp.t_syncmer = p.t;
+    bp.w_min = (int)p.w_min; bp.w_max = (int)p.w_max; bp.max_dist = p.max_dist;
+    bp.q = (uint64_t)p.q;
+    bp.bits = bits_override;
+    bp.f = f;
+    rsa_index_build_info info{};
+    char err[512] = {0};
+    rsa_index_build* b = rsa_index_build_run(device, refs.concat.data(), refs.offsets.data(), (int)refs.size(), &bp,
+                                             &info, err, sizeof err);
+    if (!b) throw std::runtime_error(std::string("GPU index build: ") + err);
+    idx.params = p;
+    idx.bits = info.bits;
+    idx.filter_cutoff = info.filter_cutoff;
+    idx.randstrobes.resize(info.n_randstrobes);
+    idx.bucket_starts.resize((1ull << info.bits) + 1);
+    const int rc = rsa_index_build_download(b, idx.randstrobes.data(), idx.bucket_starts.data());
+    rsa_index_build_free(b);
+    if (rc != RSA_OK) throw std::runtime_error("GPU index build: download failed");
+    idx.built_on_device = true;
+    const double ms[6] = {info.ms_upload, info.ms_syncmers, info.ms_randstrobes, info.ms_sort, info.ms_buckets,
+                          info.ms_total};
+    std::copy(ms, ms + 6, idx.device_build_ms);
+    idx.replayed_segments = info.replayed_segments;
+}
+
 // engine of librsalign.so (capi.cpp)
 std::unique_ptr<Engine> make_default_engine(const References& refs, const StiIndex& index, int device) {
     return make_gpu_engine(refs, index, device);

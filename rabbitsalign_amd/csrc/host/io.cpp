@@ -558,6 +558,12 @@ void StiIndex::build(const References& refs, const IndexParameters& p, int bits_
     }
 }
 
+__attribute__((weak)) void build_default_index(StiIndex& idx, const References& refs, const IndexParameters& p,
+                                               int bits_override, float f, int threads, int device) {
+    (void)device;
+    idx.build(refs, p, bits_override, f, threads);
+}
+
 // ----------------------------------------------------------------- FASTQ --
 // kseq semantics: '@' or '>' header, name = up to the first whitespace, the
 // rest of the header line (after that whitespace) is the comment; sequence

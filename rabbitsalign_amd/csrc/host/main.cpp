@@ -24,7 +24,7 @@ struct Opts {
     std::string out_file, rg_id, ref, reads1, reads2;
     std::vector<std::string> rg;
     bool verbose = false, eqx = false, no_unmapped = false, details = false, create_index = false,
-         use_index = false, interleaved = false;
+         use_index = false, interleaved = false, cpu_index = false;
     int r = 150, m = INT32_MIN, k = INT32_MIN, l = INT32_MIN, u = INT32_MIN, s = INT32_MIN, c = INT32_MIN, bits = -1;
     bool r_set = false;
     int A = 2, B = 8, O = 12, E = 1, L = 10;
@@ -38,7 +38,7 @@ void usage(const char* prog) {
             "usage: %s [options] <ref.fa> <reads1> [reads2]\n"
             "       %s index [-r INT] [-o out.sti] [-t INT] [-b INT] <ref.fa>\n"
             "  -t INT threads [3]   --chunk-size INT [10000]   -o PATH   --eqx   -U   --details\n"
-            "  --rg-id ID  --rg TAG:VALUE   -N INT   -i/--create-index   --use-index   --device INT\n"
+            "  --rg-id ID  --rg TAG:VALUE   -N INT   -i/--create-index   --use-index   --device INT   --cpu-index\n"
             "  seeding: -r -m -k -l -u -s -c -b      alignment: -A -B -O -E -L\n"
             "  search: -f FLOAT -S FLOAT -M INT -R INT\n",
             prog, prog);
@@ -69,6 +69,7 @@ Opts parse(int argc, char** argv, bool& ok) {
         else if (a == "--index-statistics") (void)need(i);
         else if (a == "-i" || a == "--create-index") o.create_index = true;
         else if (a == "--use-index") o.use_index = true;
+        else if (a == "--cpu-index") o.cpu_index = true;
         else if (a == "--device") o.device = atoi(need(i));
         else if (a == "-r") { o.r = atoi(need(i)); o.r_set = true; }
         else if (a == "-m") o.m = atoi(need(i));
@@ -141,8 +142,13 @@ int cli_main(int argc, char** argv, EngineFactory factory, const char* prog) {
         if (refs.size() >= (1u << 24)) throw std::runtime_error("at most 2^24 contigs");
         StiIndex idx;
         const std::string sti_path = o.ref + ip.filename_extension();
+        // the index is built on the GPU (engine build) unless --cpu-index asks for the host build
+        auto build_index = [&]() {
+            if (o.cpu_index) idx.build(refs, ip, o.bits, o.f, std::max(1, o.threads));
+            else build_default_index(idx, refs, ip, o.bits, o.f, std::max(1, o.threads), o.device);
+        };
         if (index_cmd || o.create_index) {
-            idx.build(refs, ip, o.bits, o.f, std::max(1, o.threads));
+            build_index();
             std::string out = o.out_file.empty() ? sti_path : o.out_file;
             idx.write(out);
             if (o.verbose) fprintf(stderr, "wrote %s (%zu randstrobes, bits %d, filter cutoff %d)\n", out.c_str(),
@@ -153,7 +159,7 @@ int cli_main(int argc, char** argv, EngineFactory factory, const char* prog) {
             idx.read(sti_path);
             if (!(idx.params == ip)) throw std::runtime_error("Index parameters in .sti file and those specified on command line differ");
         } else {
-            idx.build(refs, ip, o.bits, o.f, std::max(1, o.threads));
+            build_index();
         }
         const double t_index = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         if (o.reads1.empty()) throw std::runtime_error("At least one file with reads must be specified.");

@@ -254,7 +254,19 @@ struct StiIndex {                               // .sti contents (src/index.cpp:
     void read(const std::string& path);
     void write(const std::string& path) const;
     void build(const References& refs, const IndexParameters& p, int bits_override, float f, int threads);
+    // how the index was made: on the GPU (rsa_index_build_run) with its phase times
+    // (upload, syncmers, randstrobes, sort, buckets, total; ms), or on the host
+    bool built_on_device = false;
+    double device_build_ms[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t replayed_segments = 0;
 };
+
+// StrobemerIndex::populate as used by the CLI and the C API.  The host build
+// (StiIndex::build) by default; the GPU engine's translation unit
+// (engine_gpu.cpp) replaces it with the HIP build, so the product makes its
+// index on the device it maps on.
+void build_default_index(StiIndex& idx, const References& refs, const IndexParameters& p, int bits_override, float f,
+                         int threads, int device);
 
 // --------------------------------------------------------------- engine ---
 struct SeedBatchOut {

@@ -32,7 +32,9 @@ class _Info(C.Structure):
     _fields_ = [("ref_bases", C.c_uint64), ("n_randstrobes", C.c_uint64), ("n_contigs", C.c_int32),
                 ("bits", C.c_int32), ("filter_cutoff", C.c_int32), ("k", C.c_int32),
                 ("canonical_read_length", C.c_int32), ("index_seconds", C.c_double),
-                ("upload_seconds", C.c_double), ("device_resident_bytes", C.c_uint64)]
+                ("upload_seconds", C.c_double), ("device_resident_bytes", C.c_uint64),
+                ("index_on_device", C.c_int32), ("pad_", C.c_int32), ("index_device_ms", C.c_double * 6),
+                ("index_replayed_segments", C.c_uint64)]
 
 
 EXPORTED_SYMBOLS = [
@@ -148,7 +150,10 @@ class Mapper:
     def info(self) -> dict:
         i = _Info()
         self._lib.rsam_get_info(self._h, C.byref(i))
-        return {f: getattr(i, f) for f, _ in _Info._fields_}
+        out = {f: getattr(i, f) for f, _ in _Info._fields_ if f != "pad_"}
+        out["index_device_ms"] = dict(zip(("upload", "syncmers", "randstrobes", "sort", "buckets", "total"),
+                                          [round(x, 3) for x in i.index_device_ms]))
+        return out
 
     def synthetic_reads(self, seed, first, n, read_len=150, mu=300.0, sigma=30.0, paired=True) -> Reads:
         return Reads(self._lib, self._lib.rsam_reads_synthetic(self._h, seed, first, n, read_len, mu, sigma,

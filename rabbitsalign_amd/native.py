@@ -79,7 +79,7 @@ class AlnBatch(C.Structure):
 KERNELS = ["randstrobes", "lookup", "find_nams", "rescue", "compact", "ext_scan", "ext_band", "ext_band_wide",
            "ext_band_lane"]
 KERNEL_SYMBOLS = {"randstrobes": "k_randstrobes", "lookup": "k_lookup", "find_nams": "k_find_nams",
-                  "rescue": "k_rescue", "compact": "k_compact", "ext_scan": "k_ext_scan", "ext_band": "k_ext_band16",
+                  "rescue": "k_rescue", "compact": "k_compact", "ext_scan": "k_ext_scan_g", "ext_band": "k_ext_band16",
                   "ext_band_wide": "k_ext_band64", "ext_band_lane": "k_ext_band"}
 NK = len(KERNELS)
 
@@ -110,7 +110,8 @@ def stats_dict(ks: "KernelStats") -> dict:
 
 EXPORTED_SYMBOLS = ["rsa_open", "rsa_close", "rsa_last_error", "rsa_resident_bytes", "rsa_randstrobes",
                     "rsa_seed", "rsa_extend", "rsa_extend_cigar_bound", "rsa_host_alloc", "rsa_host_free",
-                    "rsa_get_stats", "rsa_reset_stats"]
+                    "rsa_get_stats", "rsa_reset_stats", "rsa_index_build_run", "rsa_index_build_download",
+                    "rsa_index_build_free"]
 
 _lib = None
 
@@ -137,6 +138,11 @@ def load(path: str = GPU_LIB):
     lib.rsa_extend_cigar_bound.argtypes = [C.POINTER(JobBatch)]
     lib.rsa_get_stats.argtypes = [C.c_void_p, C.POINTER(KernelStats)]
     lib.rsa_reset_stats.argtypes = [C.c_void_p]
+    lib.rsa_index_build_run.restype = C.c_void_p
+    lib.rsa_index_build_run.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(IndexBuildParams),
+                                        C.POINTER(IndexBuildInfo), C.c_char_p, C.c_size_t]
+    lib.rsa_index_build_download.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.rsa_index_build_free.argtypes = [C.c_void_p]
     _lib = lib
     return lib
 
@@ -236,6 +242,44 @@ def load_index(fasta: str, sti: str) -> Index:
     d = read_sti(sti)
     return Index(d["randstrobes"], d["bucket_starts"], d["bits"], d["filter_cutoff"], d["r"], d["k"], d["s"],
                  d["l"], d["u"], d["q"], d["max_dist"], ref, offs, names)
+
+
+class IndexBuildParams(C.Structure):
+    _fields_ = [("k", C.c_int32), ("s", C.c_int32), ("t_syncmer", C.c_int32), ("w_min", C.c_int32),
+                ("w_max", C.c_int32), ("max_dist", C.c_int32), ("q", C.c_uint64), ("bits", C.c_int32),
+                ("f", C.c_float)]
+
+
+class IndexBuildInfo(C.Structure):
+    _fields_ = [("n_randstrobes", C.c_uint64), ("n_syncmers", C.c_uint64), ("unique_hashes", C.c_uint64),
+                ("bits", C.c_int32), ("filter_cutoff", C.c_int32), ("n_segments", C.c_uint64),
+                ("replayed_segments", C.c_uint64), ("ms_upload", C.c_double), ("ms_syncmers", C.c_double),
+                ("ms_randstrobes", C.c_double), ("ms_sort", C.c_double), ("ms_buckets", C.c_double),
+                ("ms_total", C.c_double)]
+
+
+def build_index(ref: np.ndarray, contig_offsets: np.ndarray, k=20, s=16, w_min=2, w_max=12, max_dist=80, q=255,
+                bits=-1, f=0.0002, device=0):
+    """StrobemerIndex::populate on the GPU (rsa_index_build_run): returns
+    (randstrobes [RS_DTYPE], bucket_starts [u64], filter_cutoff, info dict)."""
+    lib = load()
+    ref = np.ascontiguousarray(ref, dtype=np.uint8)
+    offs = np.ascontiguousarray(contig_offsets, dtype=np.uint64)
+    p = IndexBuildParams(k, s, (k - s) // 2 + 1, w_min, w_max, max_dist, q, bits, f)
+    info = IndexBuildInfo()
+    err = C.create_string_buffer(512)
+    h = lib.rsa_index_build_run(device, _ptr(ref), _ptr(offs), len(offs) - 1, C.byref(p), C.byref(info), err, 512)
+    if not h:
+        raise RuntimeError(err.value.decode())
+    try:
+        rs = np.zeros(info.n_randstrobes, dtype=RS_DTYPE)
+        st = np.zeros((1 << info.bits) + 1, dtype=np.uint64)
+        rc = lib.rsa_index_build_download(h, _ptr(rs), _ptr(st))
+        if rc != 0:
+            raise RuntimeError(f"rsa_index_build_download failed ({rc})")
+    finally:
+        lib.rsa_index_build_free(h)
+    return rs, st, int(info.filter_cutoff), {f: getattr(info, f) for f, _ in IndexBuildInfo._fields_}
 
 
 def empty_index(ref: np.ndarray, offs: np.ndarray, names=None) -> Index:

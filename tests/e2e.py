@@ -15,7 +15,9 @@ def run(*args, **kw):
 
 
 def make_dataset(d, name="ds", ref_len=300_000, contigs=3, pairs=4000, L=150, mu=300, sigma=30, seed=1,
-                 repeat_frac=0.03, n_runs=3, n_rate=0.001, se=False):
+                 repeat_frac=0.03, n_runs=3, n_rate=0.001, se=False, cpu_index=False):
+    """FASTA + FASTQ + the .sti next to the FASTA; the index is built on the GPU
+    (rsalign's default) unless cpu_index asks for the host build."""
     fa = os.path.join(d, f"{name}.fa")
     run(GEN, "ref", seed, ref_len, contigs, fa, repeat_frac, n_runs)
     if se:
@@ -26,7 +28,7 @@ def make_dataset(d, name="ds", ref_len=300_000, contigs=3, pairs=4000, L=150, mu
         f1, f2 = os.path.join(d, f"{name}_1.fq"), os.path.join(d, f"{name}_2.fq")
         run(GEN, "reads", seed + 1, fa, pairs, L, mu, sigma, f1, f2, n_rate)
         reads = [f1, f2]
-    run(RSALIGN, "index", "-r", L, "-t", 4, fa)
+    run(RSALIGN, "index", "-r", L, "-t", 4, *(["--cpu-index"] if cpu_index else []), fa)
     return fa, reads
 
 

@@ -10,7 +10,7 @@ from e2e import CPU_PORT, CPU_REF, make_dataset, map_reads, sam_body
 @pytest.fixture(scope="module")
 def data(tmp_path_factory):
     d = tmp_path_factory.mktemp("e2e_cpu")
-    return d, make_dataset(str(d), pairs=3000, ref_len=200_000)
+    return d, make_dataset(str(d), pairs=3000, ref_len=200_000, cpu_index=True)
 
 
 @pytest.mark.skipif(not os.path.exists(CPU_REF), reason="reference build absent")
