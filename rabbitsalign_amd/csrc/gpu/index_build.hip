@@ -165,7 +165,9 @@ struct SegTable {
 };
 
 // mode 0: warm-up probe (converged flag + syncmer count); 1: count from the
-// replay start; 2: write the syncmers at out[off[seg]..]
+// replay start; 2: write the syncmers at out[off[seg]..].  The reference
+// buffer is 16-B aligned with 64 bytes of slack past its end (aligned loads
+// never leave the allocation).
 template <int WC>
 __global__ void __launch_bounds__(TPB)
 k_seg_syncmers(const char* __restrict__ ref, SegTable st, BuildParams p, int mode, uint32_t* __restrict__ count,
@@ -187,15 +189,31 @@ k_seg_syncmers(const char* __restrict__ ref, SegTable st, BuildParams p, int mod
     const int kshift = (p.k - 1) * 2, sshift = (p.s - 1) * 2;
     SyncState<WC> S;
     SyncmerOut sm;
+    // bases come from aligned 16-B loads kept in registers: one load per 16 steps
+    // instead of one byte load per step (a wave's lanes walk 64 segments 4 KB apart)
+    const uint64_t c0 = (uint64_t)(cs - ref);
+    uint64_t wbase = ~0ull;
+    uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+    auto base_at = [&](uint64_t i) -> int {
+        const uint64_t g = c0 + i, a = g & ~15ull;
+        if (a != wbase) {
+            const uint4 v = *reinterpret_cast<const uint4*>(ref + a);
+            w0 = v.x; w1 = v.y; w2 = v.z; w3 = v.w;
+            wbase = a;
+        }
+        const unsigned o = (unsigned)(g & 15);
+        const uint32_t x = o < 8 ? (o < 4 ? w0 : w1) : (o < 12 ? w2 : w3);
+        return nt4_code((unsigned char)(x >> ((o & 3) * 8)));
+    };
     uint64_t i = from;
     for (; i < b; ++i) {                                   // replay, no output
-        const int r = S.step(nt4_code((unsigned char)cs[i]), (long long)i, p, W, kmask, smask, kshift, sshift, sm);
+        const int r = S.step(base_at(i), (long long)i, p, W, kmask, smask, kshift, sshift, sm);
         if (mode == 0 && !ok) ok = r < 0 || S.converged(W);
     }
     uint32_t n = 0;
     SyncmerOut* o = mode == 2 ? out + off[sg] : nullptr;
     for (; i < e; ++i) {
-        if (S.step(nt4_code((unsigned char)cs[i]), (long long)i, p, W, kmask, smask, kshift, sshift, sm) == 1) {
+        if (S.step(base_at(i), (long long)i, p, W, kmask, smask, kshift, sshift, sm) == 1) {
             if (mode == 2) o[n] = sm;
             n++;
         }
@@ -296,16 +314,19 @@ k_run_counts(const rsa_ref_randstrobe* __restrict__ rs, uint64_t n, unsigned lon
     for (int j = threadIdx.x; j < 103; j += TPB) lh[j] = 0;
     __syncthreads();
     const uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x;
+    bool start = false;
     if (i < n) {
         const uint64_t h = rs[i].hash;
-        if (i == 0 || rs[i - 1].hash != h) {
-            atomicAdd(&lh[102], 1ull);                     // unique hashes
-            uint64_t j = i + 1;
+        start = i == 0 || rs[i - 1].hash != h;
+        if (start && i + 1 < n && rs[i + 1].hash == h) {  // a run longer than one
+            uint64_t j = i + 2;
             while (j < n && j - i <= 100 && rs[j].hash == h) ++j;
             const uint64_t len = j - i;
-            if (len > 1) atomicAdd(&lh[len > 100 ? 101 : len], 1ull);
+            atomicAdd(&lh[len > 100 ? 101 : len], 1ull);
         }
     }
+    const uint64_t starts = __popcll(__ballot(start));   // unique hashes: one LDS atomic per wave
+    if ((threadIdx.x & 63) == 0 && starts) atomicAdd(&lh[102], starts);
     __syncthreads();
     for (int j = threadIdx.x; j < 103; j += TPB)
         if (lh[j]) atomicAdd(&hist[j], lh[j]);

@@ -16,6 +16,7 @@ import sys
 
 
 def short(name: str) -> str:
+    name = name.replace("(anonymous namespace)::", "")
     return name.split("(")[0]
 
 
