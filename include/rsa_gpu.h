@@ -110,6 +110,23 @@ typedef struct rsa_nam {
     int32_t is_rc;
 } rsa_nam;
 
+/* Per-NAM site checks, what align_*_read_part computes next
+ * for a NAM against the reference window: reverse_nam_if_needed
+ * (src/aln.cpp:60-93) and the Hamming test + mismatch positions of
+ * extend_seed_part (src/aln.cpp:374-431, aligner.cpp:219-302). */
+enum {
+    RSA_SITE_ORIENT_MASK = 3,    /* 0 consistent as is, 1 consistent once reversed, 2 inconsistent */
+    RSA_SITE_HAMMING = 4,        /* (reversed if 1) projection is read-length and consistent: n_mm = Hamming distance */
+    RSA_SITE_POSITIONS = 8,      /* n_mm / read length < 0.05 and mm_pool[mm_offset .. + n_mm) holds the positions */
+    RSA_SITE_POOL_FULL = 16      /* as 8, but the pool was too small: the positions were not stored */
+};
+typedef struct rsa_nam_site {
+    uint8_t flags;
+    uint8_t pad_;
+    uint16_t n_mm;               /* mismatches of the read-length window (RSA_SITE_HAMMING), capped at 65535 */
+    uint32_t mm_offset;          /* into mm_pool (RSA_SITE_POSITIONS) */
+} rsa_nam_site;
+
 typedef struct rsa_nam_batch {
     rsa_nam* nams;               /* caller-owned, NAMs of read i at [offsets[i], offsets[i+1]) */
     uint64_t capacity;
@@ -117,6 +134,12 @@ typedef struct rsa_nam_batch {
     float* nonrepetitive_fraction; /* [n_reads], bit-equal to find_nams' .first */
     uint8_t* rescued;            /* [n_reads], 1 if find_nams_rescue produced the list */
     uint64_t needed;             /* out: total NAM count */
+    /* optional (NULL: not computed): one site per NAM, mismatch positions (query
+     * coordinates of the oriented read) in mm_pool[mm_capacity] */
+    rsa_nam_site* sites;
+    uint16_t* mm_pool;
+    uint64_t mm_capacity;
+    uint64_t mm_used;            /* out */
 } rsa_nam_batch;
 
 /* For every read: NAMs = find_nams(randstrobes_query(read)); if rescue_level > 1
@@ -231,7 +254,8 @@ enum {
     RSA_K_EXT_BAND = 6,    /* banded_sw + traceback + Aligner::align, 16 lanes/job (ssw.c:622-790, aligner.cpp:114-210) */
     RSA_K_EXT_BAND_WIDE = 7, /* the same, 64 lanes/job, for the jobs the 16-lane kernel queues */
     RSA_K_EXT_BAND_LANE = 8, /* the same, one lane per job with global scratch (bands > 64 cells) */
-    RSA_K_COUNT = 9
+    RSA_K_SITES = 9,       /* per-NAM orientation + Hamming site checks (aln.cpp:60-93, 374-431) */
+    RSA_K_COUNT = 10
 };
 
 typedef struct rsa_kernel_stats {

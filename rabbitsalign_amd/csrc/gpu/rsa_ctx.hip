@@ -114,6 +114,7 @@ struct rsa_ctx {
     uint64_t ref_bytes = 0;
     std::vector<uint64_t> contig_off;  // host copy [n+1]
     rsa_ref_randstrobe* d_rs = nullptr;
+    uint64_t* d_coff = nullptr;        // contig offsets (device copy)
     uint64_t n_rs = 0;
     uint64_t* d_starts = nullptr;
     SeedIndexParams ip{};
@@ -208,6 +209,9 @@ rsa_ctx* rsa_open(int device, const rsa_index_view* v, char* errbuf, size_t err_
         e = hipMalloc(&ctx->d_rs, sizeof(rsa_ref_randstrobe) * (ctx->n_rs + 1));
         if (e == hipSuccess) e = hipMemcpy(ctx->d_rs, v->randstrobes, sizeof(rsa_ref_randstrobe) * ctx->n_rs, hipMemcpyHostToDevice);
     }
+    if (e == hipSuccess) e = hipMalloc(&ctx->d_coff, sizeof(uint64_t) * ctx->contig_off.size());
+    if (e == hipSuccess)
+        e = hipMemcpy(ctx->d_coff, ctx->contig_off.data(), sizeof(uint64_t) * ctx->contig_off.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess && v->bucket_starts) {
         e = hipMalloc(&ctx->d_starts, sizeof(uint64_t) * n_starts);
         if (e == hipSuccess) e = hipMemcpy(ctx->d_starts, v->bucket_starts, sizeof(uint64_t) * n_starts, hipMemcpyHostToDevice);
@@ -225,6 +229,8 @@ rsa_ctx* rsa_open(int device, const rsa_index_view* v, char* errbuf, size_t err_
     ctx->ip.k = v->k; ctx->ip.s = v->s; ctx->ip.t = v->t_syncmer;
     ctx->ip.w_min = v->w_min; ctx->ip.w_max = v->w_max; ctx->ip.max_dist = v->max_dist;
     ctx->ip.q = v->q;
+    ctx->ip.ref = ctx->d_ref;
+    ctx->ip.coff = ctx->d_coff;
     ctx->resident = ctx->ref_bytes + sizeof(rsa_ref_randstrobe) * ctx->n_rs + sizeof(uint64_t) * n_starts;
     return ctx;
 }
@@ -246,6 +252,7 @@ void rsa_close(rsa_ctx* ctx) {
     if (ctx->d_ref) (void)hipFree(ctx->d_ref);
     if (ctx->d_rs) (void)hipFree(ctx->d_rs);
     if (ctx->d_starts) (void)hipFree(ctx->d_starts);
+    if (ctx->d_coff) (void)hipFree(ctx->d_coff);
     delete ctx;
 }
 

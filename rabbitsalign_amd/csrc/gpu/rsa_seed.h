@@ -14,6 +14,8 @@ struct SeedIndexParams {
     uint32_t filter_cutoff;
     int k, s, t, w_min, w_max, max_dist;
     uint64_t q;
+    const char* ref;            // resident reference (contigs back to back), for the site checks
+    const uint64_t* coff;       // [n_contigs + 1] contig offsets in ref (device)
 };
 
 struct SeedBufs {

@@ -1407,13 +1407,156 @@ k_rescue_w(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restri
 __global__ void k_compact(int n_reads, const uint64_t* __restrict__ hoff, const uint64_t* __restrict__ roff,
                           const uint32_t* __restrict__ ncnt1, const uint32_t* __restrict__ ncnt2,
                           const uint32_t* __restrict__ flags, const rsa_nam* __restrict__ nam1,
-                          const rsa_nam* __restrict__ nam2, const uint64_t* __restrict__ ooff, rsa_nam* __restrict__ out) {
+                          const rsa_nam* __restrict__ nam2, const uint64_t* __restrict__ ooff, rsa_nam* __restrict__ out,
+                          uint32_t* __restrict__ nam_read) {
     const int r = blockIdx.x;
     if (r >= n_reads) return;
     const bool resc = flags[r] & 8u;
     const rsa_nam* src = resc ? nam2 + roff[r] : nam1 + hoff[r];
     const uint32_t n = resc ? ncnt2[r] : ncnt1[r];
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) out[ooff[r] + i] = src[i];
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        out[ooff[r] + i] = src[i];
+        if (nam_read) nam_read[ooff[r] + i] = (uint32_t)r;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_sites: per-NAM site checks, 16 lanes per final NAM.
+// reverse_nam_if_needed (src/aln.cpp:60-93): the NAM's first and last k-mers
+// against the reference, as is or with the read reversed; then, for the
+// (reversed) NAM, extend_seed_part's test (aln.cpp:374-431): a read-length
+// projection gets its Hamming distance and, when hd / len < 0.05 (float
+// quotient, double compare), its mismatch positions.  The host then builds
+// hamming_align's result without touching the reference.
+// ---------------------------------------------------------------------------
+// complement of src/revcomp.hpp:10-27 (A/C/G/T/U either case, all else N)
+__device__ __forceinline__ unsigned char rc_base(unsigned char c) {
+    switch (c) {
+        case 'A': case 'a': return 'T';
+        case 'C': case 'c': return 'G';
+        case 'G': case 'g': return 'C';
+        case 'T': case 't': case 'U': case 'u': return 'A';
+        default: return 'N';
+    }
+}
+
+struct SiteRead {
+    const char* s;
+    int64_t len;
+    __device__ __forceinline__ unsigned char at(bool rc, int64_t i) const {
+        return rc ? rc_base((unsigned char)s[len - 1 - i]) : (unsigned char)s[i];
+    }
+};
+
+// 16 lanes per NAM, 4 NAMs per wave: a lane compares every 16th byte and the
+// group combines its ballot bits (in position order, so mismatch positions come
+// out sorted without a sort)
+__device__ __forceinline__ uint32_t grp_ballot(bool v) {
+    const uint64_t b = __ballot(v);
+    return (uint32_t)(b >> (threadIdx.x & 48)) & 0xFFFFu;
+}
+
+// sub(ref, rpos, k) == sub(read view, qpos, k) with std::string::substr clamping
+// (a position past the end -- negative ints included, as size_t -- gives "")
+__device__ bool site_kmer_eq(const char* ref, int64_t rlen, int64_t rpos, const SiteRead& rd, bool rc, int64_t qpos,
+                             int k, int l16) {
+    const uint64_t rp = (uint64_t)rpos, qp = (uint64_t)qpos;
+    const uint64_t ra = rp > (uint64_t)rlen ? (uint64_t)rlen : rp, qa = qp > (uint64_t)rd.len ? (uint64_t)rd.len : qp;
+    const uint64_t rl = min((uint64_t)k, (uint64_t)rlen - ra), ql = min((uint64_t)k, (uint64_t)rd.len - qa);
+    bool bad = rl != ql;
+    for (uint64_t j = l16; j < rl && !bad; j += 16)
+        bad = (unsigned char)ref[ra + j] != rd.at(rc, (int64_t)(qa + j));
+    return grp_ballot(bad) == 0;
+}
+
+__global__ void __launch_bounds__(256)
+k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read, uint64_t total,
+        const char* __restrict__ seq, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
+        SeedIndexParams p, rsa_nam_site* __restrict__ sites, uint16_t* __restrict__ pool, uint64_t pool_cap,
+        unsigned long long* __restrict__ pool_used) {
+    __shared__ uint32_t s_need[16], s_base[16];
+    __shared__ unsigned long long s_at;
+    const int l16 = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const uint64_t g0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+    const bool valid = g0 < total;
+    const uint64_t g = valid ? g0 : total - 1;             // idle groups shadow the last NAM (ballots stay uniform)
+    const uint32_t r = nam_read[g];
+    const SiteRead rd{seq + roff[r], (int64_t)rlen[r]};
+    const rsa_nam nam = nams[g];
+    const char* ref = p.ref + p.coff[nam.ref_id];
+    const int64_t ref_len = (int64_t)(p.coff[nam.ref_id + 1] - p.coff[nam.ref_id]);
+    const int k = p.k;
+    bool is_rc = nam.is_rc != 0;
+    int64_t qs = nam.query_start, qe = nam.query_end;
+    uint32_t flags;
+    const bool fwd_ok = site_kmer_eq(ref, ref_len, nam.ref_start, rd, is_rc, qs, k, l16) &
+                        site_kmer_eq(ref, ref_len, (int64_t)nam.ref_end - k, rd, is_rc, qe - k, k, l16);
+    if (fwd_ok) {
+        flags = 0;
+    } else {
+        const int64_t qs2 = rd.len - nam.query_end, qe2 = rd.len - nam.query_start;
+        const bool rev_ok = site_kmer_eq(ref, ref_len, nam.ref_start, rd, !is_rc, qs2, k, l16) &
+                            site_kmer_eq(ref, ref_len, (int64_t)nam.ref_end - k, rd, !is_rc, qe2 - k, k, l16);
+        if (rev_ok) {
+            flags = 1;
+            is_rc = !is_rc;
+            qs = qs2;
+            qe = qe2;
+        } else {
+            flags = 2;
+        }
+    }
+    uint32_t hd = 0, mm_off = 0;
+    bool want = false;
+    int64_t ps = 0;
+    if (flags != 2) {
+        // projected_ref_start = max(0, ref_start - query_start); projected_ref_end =
+        // min(ref_end + |read| - query_end, |contig|) (size_t arithmetic)
+        ps = max((int64_t)0, (int64_t)nam.ref_start - qs);
+        const uint64_t pe = min((uint64_t)((int64_t)nam.ref_end + rd.len - qe), (uint64_t)ref_len);
+        if (pe - (uint64_t)ps == (uint64_t)rd.len) {
+            flags |= RSA_SITE_HAMMING;
+            for (int64_t i0 = 0; i0 < rd.len; i0 += 16) {
+                const int64_t i = i0 + l16;
+                hd += __popc(grp_ballot(i < rd.len && (unsigned char)ref[ps + i] != rd.at(is_rc, i)));
+            }
+            want = (double)((float)hd / (float)rd.len) < 0.05;
+        }
+    }
+    // pool space: a block-wide prefix over its 16 NAMs and one atomic per block
+    if (l16 == 0) s_need[grp] = (want && valid) ? hd : 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int j = 0; j < 16; ++j) { s_base[j] = acc; acc += s_need[j]; }
+        s_at = acc ? atomicAdd(pool_used, (unsigned long long)acc) : 0ull;
+    }
+    __syncthreads();
+    if (want) {
+        const unsigned long long at = s_at + s_base[grp];
+        if (at + hd <= pool_cap) {
+            flags |= RSA_SITE_POSITIONS;
+            mm_off = (uint32_t)at;
+            uint32_t m = 0;
+            for (int64_t i0 = 0; i0 < rd.len && m < hd; i0 += 16) {
+                const int64_t i = i0 + l16;
+                const bool mis = i < rd.len && (unsigned char)ref[ps + i] != rd.at(is_rc, i);
+                const uint32_t bits = grp_ballot(mis);
+                if (mis && valid) pool[at + m + __popc(bits & ((1u << l16) - 1))] = (uint16_t)i;
+                m += __popc(bits);
+            }
+        } else {
+            flags |= RSA_SITE_POOL_FULL;
+        }
+    }
+    if (valid && l16 == 0) {
+        rsa_nam_site out;
+        out.flags = (uint8_t)flags;
+        out.pad_ = 0;
+        out.n_mm = (uint16_t)min(hd, 65535u);
+        out.mm_offset = mm_off;
+        sites[g] = out;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1421,10 +1564,11 @@ __global__ void k_compact(int n_reads, const uint64_t* __restrict__ hoff, const 
 // ---------------------------------------------------------------------------
 enum {
     B_SEQ, B_ROFF, B_RLEN, B_QBASE, B_QRS, B_QCNT, B_SYNC, B_QI, B_ST, B_HOFF, B_HITS, B_OPEN, B_NAM1, B_NCNT1,
-    B_NONREP, B_FLAGS, B_MAP, B_ROFF2, B_NAM2, B_NCNT2, B_LIST, B_RBUF, B_OUT, B_OOFF, B_SLOTS
+    B_NONREP, B_FLAGS, B_MAP, B_ROFF2, B_NAM2, B_NCNT2, B_LIST, B_RBUF, B_OUT, B_OOFF, B_SLOTS, B_SITES, B_POOL,
+    B_PUSED, B_NREAD
 };
 // every host side of a transfer is page-locked: a pageable one would make the copy synchronous
-enum { H_ST, H_HOFF, H_FLAGS, H_CNT, H_ROFF, H_LIST, H_OOFF, H_CNT2, H_QBASE, H_NONREP };
+enum { H_ST, H_HOFF, H_FLAGS, H_CNT, H_ROFF, H_LIST, H_OOFF, H_CNT2, H_QBASE, H_NONREP, H_PUSED };
 
 void seed_bufs_release(SeedBufs& b) {
     for (int i = 0; i < 32; ++i) if (b.p[i]) (void)hipFree(b.p[i]);
@@ -1751,13 +1895,41 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
     SCHK(dens(b, B_OOFF, 8ull * (n + 1)));
     SCHK(dens(b, B_OUT, std::max(b.cap[B_OUT], sizeof(rsa_nam) * (total + 1))));
     SCHK(hipMemcpyAsync(b.p[B_OOFF], ooff, 8ull * (n + 1), hipMemcpyHostToDevice, st));
+    if (out->sites) SCHK(dens(b, B_NREAD, 4ull * (total + 1)));
     kt.begin(st, RSA_K_COMPACT);
     hipLaunchKernelGGL(k_compact, dim3(n), dim3(64), 0, st, (int)n, DP(B_HOFF, uint64_t), DP(B_ROFF2, uint64_t),
                        DP(B_NCNT1, uint32_t), DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t), DP(B_NAM1, rsa_nam),
-                       DP(B_NAM2, rsa_nam), DP(B_OOFF, uint64_t), DP(B_OUT, rsa_nam));
+                       DP(B_NAM2, rsa_nam), DP(B_OOFF, uint64_t), DP(B_OUT, rsa_nam),
+                       out->sites ? DP(B_NREAD, uint32_t) : nullptr);
     SCHK(hipGetLastError());
     kt.end(st);
     if (total) SCHK(hipMemcpyAsync(out->nams, b.p[B_OUT], sizeof(rsa_nam) * total, hipMemcpyDeviceToHost, st));
+    // site checks (optional output)
+    double site_bytes = 0;
+    if (out->sites && total) {
+        SCHK(dens(b, B_SITES, sizeof(rsa_nam_site) * total));
+        SCHK(dens(b, B_POOL, 2 * std::max<uint64_t>(1, out->mm_capacity)));
+        SCHK(dens(b, B_PUSED, 8));
+        SCHK(hipMemsetAsync(b.p[B_PUSED], 0, 8, st));
+        kt.begin(st, RSA_K_SITES);
+        hipLaunchKernelGGL(k_sites, dim3((unsigned)((16 * total + 255) / 256)), dim3(256), 0, st, DP(B_OUT, rsa_nam),
+                           DP(B_NREAD, uint32_t), total, DP(B_SEQ, char), DP(B_ROFF, uint64_t),
+                           DP(B_RLEN, uint32_t), p, DP(B_SITES, rsa_nam_site), DP(B_POOL, uint16_t), out->mm_capacity,
+                           DP(B_PUSED, unsigned long long));
+        SCHK(hipGetLastError());
+        kt.end(st);
+        SCHK(hipMemcpyAsync(out->sites, b.p[B_SITES], sizeof(rsa_nam_site) * total, hipMemcpyDeviceToHost, st));
+        SCHK(hens(b, H_PUSED, 8));
+        SCHK(hipMemcpyAsync(b.h[H_PUSED], b.p[B_PUSED], 8, hipMemcpyDeviceToHost, st));
+        SCHK(stream_wait(st, b.done));
+        const uint64_t used = std::min<uint64_t>(*HP(H_PUSED, uint64_t), out->mm_capacity);
+        out->mm_used = used;
+        if (used) SCHK(hipMemcpyAsync(out->mm_pool, b.p[B_POOL], 2 * used, hipMemcpyDeviceToHost, st));
+        // NAM + read bytes read, window bytes compared, site + positions written
+        site_bytes = (double)total * (sizeof(rsa_nam) + sizeof(rsa_nam_site) + 2.0 * 20 + 150) + 2.0 * used;
+    } else if (out->sites == nullptr) {
+        out->mm_used = 0;
+    }
     SCHK(stream_wait(st, b.done));
     // counters and algorithmic bytes (DESIGN.md "Kernels")
     uint64_t n1_tot = 0, n2_tot = 0, resc_q = 0, resc_scan = 0, resc_hits = 0;
@@ -1772,5 +1944,6 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
     c.alg_bytes[RSA_K_FIND_NAMS] = (QRS + QI) * n_qrs + RS * scan_find + 2 * HIT * H + NAM * n1_tot + 16.0 * n;
     c.alg_bytes[RSA_K_RESCUE] = (QRS + QI) * resc_q + RS * resc_scan + 2 * HIT * resc_hits + NAM * n2_tot;
     c.alg_bytes[RSA_K_COMPACT] = 2 * NAM * total + 28.0 * n;
+    c.alg_bytes[RSA_K_SITES] = (double)site_bytes;
     return RSA_OK;
 }

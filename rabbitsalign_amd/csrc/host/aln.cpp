@@ -115,6 +115,17 @@ static bool by_score(const T& a, const T& b) { return a.score > b.score; }
 // aln.cpp:60-93
 static bool reverse_nam_if_needed(Nam& nam, const Read& read, const References& refs, int k) {
     const size_t read_len = read.size();
+    if (const rsa_nam_site* st = read.site.find(nam)) {   // checked on the GPU (k_sites)
+        const int o = st->flags & RSA_SITE_ORIENT_MASK;
+        if (o != 1) return o == 0;
+        const Nam& orig = read.site.orig[nam.nam_id];
+        if (nam.is_rc == orig.is_rc) {                      // not reversed yet (a second call keeps it)
+            nam.is_rc = !orig.is_rc;
+            nam.query_start = (int)read_len - orig.query_end;
+            nam.query_end = (int)read_len - orig.query_start;
+        }
+        return true;
+    }
     std::string_view ref = refs.seq(nam.ref_id);
     std::string_view ref_start_kmer = sub(ref, (size_t)nam.ref_start, (size_t)k);
     std::string_view ref_end_kmer = sub(ref, (size_t)(nam.ref_end - k), (size_t)k);
@@ -367,7 +378,19 @@ static bool extend_seed_part(AlignTmpRes& res, const AlignmentParameters& ap, co
     AlignmentInfo info;
     int result_ref_start = 0;
     bool gapped = true;
-    if (projected_ref_end - projected_ref_start == query.size() && consistent_nam) {
+    const rsa_nam_site* st = consistent_nam ? read.site.find(nam) : nullptr;
+    if (st && !(st->flags & RSA_SITE_POOL_FULL)) {         // the GPU checked this window (k_sites)
+        if (st->flags & RSA_SITE_POSITIONS) {
+            int mm[64];
+            std::vector<int> big;
+            int* pos = mm;
+            if (st->n_mm > 64) { big.resize(st->n_mm); pos = big.data(); }
+            for (int i = 0; i < st->n_mm; ++i) pos[i] = read.site.pool[st->mm_offset + i];
+            info = hamming_align(query.size(), pos, st->n_mm, ap.match, ap.mismatch, ap.end_bonus);
+            result_ref_start = projected_ref_start + (int)info.ref_start;
+            gapped = false;
+        }
+    } else if (projected_ref_end - projected_ref_start == query.size() && consistent_nam) {
         std::string_view segm = sub(ref, (size_t)projected_ref_start, query.size());
         int mm[64];
         const int hd = segm.size() == query.size()

@@ -2,6 +2,7 @@
 // HIP C-ABI (include/rsa_gpu.h, librsa_gpu.so).  There is no CPU fallback;
 // a failed GPU call aborts the run with the library's error message.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <mutex>
@@ -17,7 +18,7 @@ namespace {
 // Per-thread page-locked batch buffers (rsa_host_alloc), grown on demand and
 // reused across chunks, so batch transfers run at DMA speed without staging.
 struct Staging {
-    enum { READS, ROFF, RLEN, NAMS, QUERIES, JOBS, ALNS, POOL, N };
+    enum { READS, ROFF, RLEN, NAMS, QUERIES, JOBS, ALNS, POOL, SITES, MMPOOL, N };
     void* p[N] = {};
     size_t cap[N] = {};
     template <class T> T* get(int k, size_t count) {
@@ -85,11 +86,25 @@ public:
         size_t cap = std::max<size_t>(1024, 12 * n);
         for (;;) {
             rsa_nam* nams = sg.get<rsa_nam>(Staging::NAMS, cap);
-            rsa_nam_batch nb{nams, cap, out.offsets.data(), out.nonrep.data(), out.rescued.data(), 0};
+            // site checks on the device (k_sites): the host's NAM orientation and
+            // Hamming windows then never read the reference
+            static const bool want_sites = !(getenv("RSA_SITES") && getenv("RSA_SITES")[0] == '0');   // A/B switch
+            rsa_nam_site* sites = want_sites ? sg.get<rsa_nam_site>(Staging::SITES, cap) : nullptr;
+            const size_t mm_cap = 4 * cap;           // overflow is flagged per NAM and handled on the host
+            uint16_t* mm = sg.get<uint16_t>(Staging::MMPOOL, mm_cap);
+            rsa_nam_batch nb{nams, cap, out.offsets.data(), out.nonrep.data(), out.rescued.data(), 0,
+                             sites, mm, mm_cap, 0};
             int rc = rsa_seed(ctx_, &rb, rescue_level, rescue_cutoff, &nb);
             if (rc == RSA_ERR_CAPACITY) { cap = nb.needed + 16; continue; }
             if (rc != RSA_OK) throw std::runtime_error(std::string("rsa_seed: ") + rsa_last_error(ctx_));
             out.nams.assign(nams, nams + nb.needed);
+            if (sites) {
+                out.sites.assign(sites, sites + nb.needed);
+                out.mm_pool.assign(mm, mm + nb.mm_used);
+            } else {
+                out.sites.clear();
+                out.mm_pool.clear();
+            }
             break;
         }
     }

@@ -236,6 +236,10 @@ void pe_seed_multi(std::vector<PeChunk*>& cs, Engine& eng, const MapContext& mc,
         for (size_t i = 0; i <= n; ++i) o.offsets[i] = all.offsets[r0 + i] - a;
         o.nonrep.assign(all.nonrep.begin() + (long)r0, all.nonrep.begin() + (long)(r0 + n));
         o.rescued.assign(all.rescued.begin() + (long)r0, all.rescued.begin() + (long)(r0 + n));
+        if (!all.sites.empty()) {   // sites follow the NAMs; positions keep their pool offsets
+            o.sites.assign(all.sites.begin() + (long)a, all.sites.begin() + (long)b);
+            o.mm_pool = all.mm_pool;
+        }
         c->times.seed += dt;
         r0 += n;
     }
@@ -293,7 +297,9 @@ void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize, On
             nams[m].assign(so.nams.begin() + (long)so.offsets[r], so.nams.begin() + (long)so.offsets[r + 1]);
             rescued[m] = so.rescued[r] != 0;
         }
-        const Read read1(c.r1[i]->seq, c.rc(i, 0)), read2(c.r2[i]->seq, c.rc(i, 1));
+        Read read1(c.r1[i]->seq, c.rc(i, 0)), read2(c.r2[i]->seq, c.rc(i, 1));
+        read1.site = so.site_view(2 * i);
+        read2.site = so.site_view(2 * i + 1);
         align_PE_read_part(c.res[i], *c.r1[i], *c.r2[i], read1, read2, nams, rescued, c.stats, isize, mc, c.rng);
         c.stats.n_reads += 2;
         if (!was_frozen && isize.frozen()) {
@@ -643,7 +649,8 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
             for (size_t i = b; i < e; ++i) {
                 const size_t r = i - b;
                 std::vector<Nam> nams(so.nams.begin() + (long)so.offsets[r], so.nams.begin() + (long)so.offsets[r + 1]);
-                const Read read(recs[i].seq, rcs[r]);
+                Read read(recs[i].seq, rcs[r]);
+                read.site = so.site_view(r);
                 align_SE_read_part(res[r], recs[i], read, nams, so.rescued[r] != 0, st, mc, rng);
                 st.n_reads++;
             }

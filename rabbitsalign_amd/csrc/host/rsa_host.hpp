@@ -204,12 +204,28 @@ void reverse_into(std::string_view s, char* out);              // plain byte rev
 
 // Read (src/revcomp.hpp:41-55): a sequence and its reverse complement.  The
 // pipeline computes the rc once per read per chunk and hands out views.
+// GPU site checks of one read's NAM list (rsa_nam_site, include/rsa_gpu.h),
+// indexed by nam_id; empty for the CPU engines (the host computes them)
+struct SiteView {
+    const rsa_nam_site* sites = nullptr;
+    const rsa_nam* orig = nullptr;              // the read's NAMs as the engine returned them
+    size_t n = 0;
+    const uint16_t* pool = nullptr;             // mismatch positions
+    const rsa_nam_site* find(const rsa_nam& nam) const {
+        if (!sites || nam.nam_id < 0 || (size_t)nam.nam_id >= n) return nullptr;
+        const rsa_nam& o = orig[nam.nam_id];
+        if (o.ref_id != nam.ref_id || o.ref_start != nam.ref_start || o.ref_end != nam.ref_end) return nullptr;
+        return &sites[nam.nam_id];
+    }
+};
+
 struct Read {
 private:
     std::string own_;                           // rc when computed by this object
 public:
     std::string_view seq;
     std::string_view rc;
+    SiteView site;
     explicit Read(const std::string& s) : own_(reverse_complement(s)), seq(s), rc(own_) {}
     Read(std::string_view s, std::string_view rc_) : seq(s), rc(rc_) {}
     Read(const Read&) = delete;
@@ -274,6 +290,18 @@ struct SeedBatchOut {
     std::vector<uint64_t> offsets;              // [n+1]
     std::vector<float> nonrep;
     std::vector<uint8_t> rescued;
+    std::vector<rsa_nam_site> sites;            // one per NAM when the engine computes the site checks
+    std::vector<uint16_t> mm_pool;              // their mismatch positions
+    // site view of read r's NAM list (empty without site checks)
+    SiteView site_view(size_t r) const {
+        SiteView v;
+        if (sites.empty()) return v;
+        v.sites = sites.data() + offsets[r];
+        v.orig = nams.data() + offsets[r];
+        v.n = offsets[r + 1] - offsets[r];
+        v.pool = mm_pool.data();
+        return v;
+    }
 };
 
 struct SwJob {                                  // query host bytes vs reference window

@@ -62,7 +62,11 @@ ALN_DTYPE = np.dtype([("sw_score", "<i4"), ("edit_distance", "<u4"), ("ref_start
 
 class NamBatch(C.Structure):
     _fields_ = [("nams", C.c_void_p), ("capacity", C.c_uint64), ("offsets", C.c_void_p),
-                ("nonrepetitive_fraction", C.c_void_p), ("rescued", C.c_void_p), ("needed", C.c_uint64)]
+                ("nonrepetitive_fraction", C.c_void_p), ("rescued", C.c_void_p), ("needed", C.c_uint64),
+                ("sites", C.c_void_p), ("mm_pool", C.c_void_p), ("mm_capacity", C.c_uint64), ("mm_used", C.c_uint64)]
+
+
+SITE_DTYPE = np.dtype([("flags", "u1"), ("pad_", "u1"), ("n_mm", "<u2"), ("mm_offset", "<u4")])
 
 
 class JobBatch(C.Structure):
@@ -77,10 +81,11 @@ class AlnBatch(C.Structure):
 
 
 KERNELS = ["randstrobes", "lookup", "find_nams", "rescue", "compact", "ext_scan", "ext_band", "ext_band_wide",
-           "ext_band_lane"]
+           "ext_band_lane", "sites"]
 KERNEL_SYMBOLS = {"randstrobes": "k_randstrobes", "lookup": "k_lookup", "find_nams": "k_find_nams_w2",
                   "rescue": "k_rescue_w", "compact": "k_compact", "ext_scan": "k_ext_scan_g", "ext_band": "k_ext_band16",
-                  "ext_band_wide": "k_ext_band64", "ext_band_lane": "k_ext_band"}
+                  "ext_band_wide": "k_ext_band64", "ext_band_lane": "k_ext_band",
+                  "sites": "k_sites"}
 NK = len(KERNELS)
 
 
@@ -347,7 +352,9 @@ class GpuContext:
         self._check(self.lib.rsa_randstrobes(self.ctx, C.byref(rb), C.byref(b)), "rsa_randstrobes")
         return [out[int(offs[i]):int(offs[i + 1])] for i in range(len(seqs))]
 
-    def seed(self, seqs, rescue_level=2, rescue_cutoff=None):
+    def seed(self, seqs, rescue_level=2, rescue_cutoff=None, sites=False, mm_capacity=None):
+        """NAM lists per read (+ nonrepetitive fraction, rescued flags); with sites=True
+        also the per-NAM site checks and the mismatch-position pool (rsa_nam_site)."""
         if rescue_cutoff is None:
             rescue_cutoff = rescue_level * self.index.filter_cutoff if rescue_level < 100 else 1000
         rb, keep = self._reads(seqs)
@@ -357,13 +364,21 @@ class GpuContext:
             offs = np.zeros(len(seqs) + 1, dtype=np.uint64)
             nonrep = np.zeros(len(seqs), dtype=np.float32)
             resc = np.zeros(len(seqs), dtype=np.uint8)
-            b = NamBatch(_ptr(nams), cap, _ptr(offs), _ptr(nonrep), _ptr(resc), 0)
+            st = np.zeros(cap if sites else 0, dtype=SITE_DTYPE)
+            mcap = (4 * cap if mm_capacity is None else mm_capacity) if sites else 0
+            pool = np.zeros(max(1, mcap), dtype=np.uint16)
+            b = NamBatch(_ptr(nams), cap, _ptr(offs), _ptr(nonrep), _ptr(resc), 0,
+                         _ptr(st) if sites else 0, _ptr(pool) if sites else 0, mcap, 0)
             rc = self.lib.rsa_seed(self.ctx, C.byref(rb), rescue_level, rescue_cutoff, C.byref(b))
             if rc == -3:
                 cap = int(b.needed) + 1
                 continue
             self._check(rc, "rsa_seed")
-            return [nams[int(offs[i]):int(offs[i + 1])] for i in range(len(seqs))], nonrep, resc
+            lists = [nams[int(offs[i]):int(offs[i + 1])] for i in range(len(seqs))]
+            if sites:
+                return lists, nonrep, resc, [st[int(offs[i]):int(offs[i + 1])] for i in range(len(seqs))], \
+                    pool[:int(b.mm_used)]
+            return lists, nonrep, resc
 
     def extend(self, queries, jobs, match=2, mismatch=8, gap_open=12, gap_extend=1, end_bonus=10):
         """queries: bytes blob; jobs: structured array JOB_DTYPE.  Returns (alns, cigar_pool)."""
