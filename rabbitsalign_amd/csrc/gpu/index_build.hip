@@ -306,27 +306,29 @@ k_fill_u64(uint64_t* __restrict__ p, uint64_t n, uint64_t v) {
     if (i < n) p[i] = v;
 }
 
-// one lane per entry; run starts count the unique hashes and histogram the run
-// length (clamped to 101) of runs longer than one (index.cpp:186-224)
+// grid-stride over the entries; run starts count the unique hashes and
+// histogram the run length (clamped to 101) of runs longer than one
+// (index.cpp:186-224).  One global atomic per block and bin.
+constexpr int RC_BLOCKS = 2048;
 __global__ void __launch_bounds__(TPB)
 k_run_counts(const rsa_ref_randstrobe* __restrict__ rs, uint64_t n, unsigned long long* __restrict__ hist) {
     __shared__ unsigned long long lh[103];
     for (int j = threadIdx.x; j < 103; j += TPB) lh[j] = 0;
     __syncthreads();
-    const uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x;
-    bool start = false;
-    if (i < n) {
+    unsigned long long starts = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * TPB) {
         const uint64_t h = rs[i].hash;
-        start = i == 0 || rs[i - 1].hash != h;
-        if (start && i + 1 < n && rs[i + 1].hash == h) {  // a run longer than one
-            uint64_t j = i + 2;
-            while (j < n && j - i <= 100 && rs[j].hash == h) ++j;
-            const uint64_t len = j - i;
-            atomicAdd(&lh[len > 100 ? 101 : len], 1ull);
+        if (i == 0 || rs[i - 1].hash != h) {
+            starts++;
+            if (i + 1 < n && rs[i + 1].hash == h) {          // a run longer than one
+                uint64_t j = i + 2;
+                while (j < n && j - i <= 100 && rs[j].hash == h) ++j;
+                const uint64_t len = j - i;
+                atomicAdd(&lh[len > 100 ? 101 : len], 1ull);
+            }
         }
     }
-    const uint64_t starts = __popcll(__ballot(start));   // unique hashes: one LDS atomic per wave
-    if ((threadIdx.x & 63) == 0 && starts) atomicAdd(&lh[102], starts);
+    atomicAdd(&lh[102], starts);
     __syncthreads();
     for (int j = threadIdx.x; j < 103; j += TPB)
         if (lh[j]) atomicAdd(&hist[j], lh[j]);
@@ -606,7 +608,7 @@ rsa_index_build* rsa_index_build_run(int device, const char* ref_seq, const uint
         BCHK(hipGetLastError());
     }
     if (n) {
-        k_run_counts<<<grid_of(n), TPB, 0, st>>>(B->d_rs, n, d_hist);
+        k_run_counts<<<(unsigned)std::min<uint64_t>(RC_BLOCKS, grid_of(n)), TPB, 0, st>>>(B->d_rs, n, d_hist);
         BCHK(hipGetLastError());
     }
     BCHK(hipEventRecord(ev[7], st));

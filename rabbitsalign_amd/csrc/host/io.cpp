@@ -28,6 +28,39 @@ Cigar Cigar::to_m() const {                        // cigar.cpp:6-18
     return c;
 }
 
+// raw writers for the SAM record: the caller sizes the buffer first, so the
+// fields go in without a capacity check per character
+static const char kDigitPairs[201] =
+    "00010203040506070809101112131415161718192021222324252627282930313233343536373839"
+    "40414243444546474849505152535455565758596061626364656667686970717273747576777879"
+    "8081828384858687888990919293949596979899";
+
+static inline char* put_uint(char* p, uint64_t v) {
+    char buf[24];
+    char* q = buf + sizeof buf;
+    while (v >= 100) {
+        const unsigned r = (unsigned)(v % 100);
+        v /= 100;
+        q -= 2;
+        memcpy(q, kDigitPairs + 2 * r, 2);
+    }
+    if (v >= 10) { q -= 2; memcpy(q, kDigitPairs + 2 * v, 2); }
+    else *--q = (char)('0' + v);
+    const size_t n = (size_t)(buf + sizeof buf - q);
+    memcpy(p, q, n);
+    return p + n;
+}
+
+static inline char* put_int(char* p, int64_t v) {
+    if (v < 0) { *p++ = '-'; return put_uint(p, (uint64_t)(-v)); }
+    return put_uint(p, (uint64_t)v);
+}
+
+static inline char* put_str(char* p, std::string_view s) {
+    memcpy(p, s.data(), s.size());
+    return p + s.size();
+}
+
 static inline void append_uint(std::string& out, uint64_t v) {
     char buf[24];
     int n = 0;
@@ -126,55 +159,83 @@ void Sam::add(const Alignment& a, const Record& r, std::string_view rc, uint8_t 
                (uint32_t)-1, 0, r.seq, rc, r.qual, a.edit_distance, a.score, d);
 }
 
+// CIGAR text straight into a sized buffer: `=`/`X` kept (eqx) or merged into M
+// (Cigar::to_m, cigar.cpp:6-18)
+static char* put_cigar(char* p, const Cigar& c, bool eqx) {
+    if (eqx) {
+        for (uint32_t x : c.ops) { p = put_uint(p, x >> 4); *p++ = "MIDNSHP=X"[x & 0xf]; }
+        return p;
+    }
+    uint32_t cur = 0xff, len = 0;
+    for (uint32_t x : c.ops) {
+        uint32_t op = x & 0xf;
+        if (op == C_EQ || op == C_X) op = C_M;
+        if (op == cur) { len += x >> 4; continue; }
+        if (cur != 0xff) { p = put_uint(p, len); *p++ = "MIDNSHP=X"[cur]; }
+        cur = op;
+        len = x >> 4;
+    }
+    if (cur != 0xff) { p = put_uint(p, len); *p++ = "MIDNSHP=X"[cur]; }
+    return p;
+}
+
 void Sam::add_record(const std::string& qname, uint16_t flags, const std::string& rname, uint32_t pos, uint8_t mapq,
                      const Cigar& cigar, const std::string& mate_rname, uint32_t mate_pos, int32_t tlen,
                      std::string_view seq, std::string_view seq_rc, const std::string& qual, int ed, int score,
                      const Details& d) {                        // sam.cpp:141-213
     std::string& o = out_;
-    o.append(strip_suffix(qname));
-    o += '\t';
-    append_uint(o, flags);
-    o += '\t';
-    o += rname;
-    o += '\t';
-    append_uint(o, (uint32_t)(pos + 1));
-    o += '\t';
-    append_uint(o, mapq);
-    o += '\t';
-    if (cigar.empty()) o += '*';
-    else if (eqx_) cigar.to_string(o);
-    else cigar.to_m_string(o);
-    o += '\t';
-    o += mate_rname;
-    o += '\t';
-    append_uint(o, (uint32_t)(mate_pos + 1));
-    o += '\t';
-    append_int(o, tlen);
-    o += '\t';
-    if (flags & 0x100) o += '*';
-    else if (flags & 0x10) o.append(seq_rc.empty() ? std::string_view("*") : seq_rc);
-    else o.append(seq.empty() ? std::string_view("*") : seq);
+    const std::string_view name = strip_suffix(qname);
+    // upper bound of the record: fixed fields + numbers + CIGAR (<= 11 chars an op) + SEQ/QUAL + tags
+    const size_t bound = name.size() + rname.size() + mate_rname.size() + std::max(seq.size(), seq_rc.size()) +
+                         qual.size() + 11 * cigar.ops.size() + tail_.size() + 160;
+    const size_t at = o.size();
+    o.resize(at + bound);
+    char* const p0 = &o[at];
+    char* p = p0;
+    p = put_str(p, name);
+    *p++ = '\t';
+    p = put_uint(p, flags);
+    *p++ = '\t';
+    p = put_str(p, rname);
+    *p++ = '\t';
+    p = put_uint(p, (uint32_t)(pos + 1));
+    *p++ = '\t';
+    p = put_uint(p, mapq);
+    *p++ = '\t';
+    if (cigar.empty()) *p++ = '*';
+    else p = put_cigar(p, cigar, eqx_);
+    *p++ = '\t';
+    p = put_str(p, mate_rname);
+    *p++ = '\t';
+    p = put_uint(p, (uint32_t)(mate_pos + 1));
+    *p++ = '\t';
+    p = put_int(p, tlen);
+    *p++ = '\t';
+    if (flags & 0x100) *p++ = '*';
+    else if (flags & 0x10) p = put_str(p, seq_rc.empty() ? std::string_view("*") : seq_rc);
+    else p = put_str(p, seq.empty() ? std::string_view("*") : seq);
+    *p++ = '\t';
     if (!(flags & 4)) {
-        o += '\t';
-        if (flags & 0x100) o += '*';
+        if (flags & 0x100) *p++ = '*';
         else if (flags & 0x10) {
-            if (qual.empty()) o += '*';
-            else {
-                const size_t at = o.size();
-                o.resize(at + qual.size());
-                reverse_into(qual, &o[at]);
-            }
-        } else o.append(qual.empty() ? std::string_view("*") : std::string_view(qual));
-        o += "\tNM:i:";
-        append_int(o, ed);
-        o += "\tAS:i:";
-        append_int(o, score);
+            if (qual.empty()) *p++ = '*';
+            else { reverse_into(qual, p); p += qual.size(); }
+        } else p = put_str(p, qual.empty() ? std::string_view("*") : std::string_view(qual));
+        p = put_str(p, "\tNM:i:");
+        p = put_int(p, ed);
+        p = put_str(p, "\tAS:i:");
+        p = put_int(p, score);
     } else {
-        o += '\t';
-        o.append(qual.empty() ? std::string_view("*") : std::string_view(qual));
+        p = put_str(p, qual.empty() ? std::string_view("*") : std::string_view(qual));
     }
-    if (details_) append_details(o, d, flags & 1);
-    o += tail_;
+    if (details_) {
+        o.resize(at + (size_t)(p - p0));
+        append_details(o, d, flags & 1);
+        o += tail_;
+        return;
+    }
+    p = put_str(p, tail_);
+    o.resize(at + (size_t)(p - p0));
 }
 
 void Sam::add_pair(const Alignment& a1, const Alignment& a2, const Record& r1, const Record& r2, std::string_view rc1,
