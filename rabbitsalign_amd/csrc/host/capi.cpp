@@ -146,19 +146,15 @@ int rsam_get_info(const rsam* m, rsam_info* out) {
 
 rsam_reads* rsam_reads_load(const char* fq1, const char* fq2) {
     try {
-        auto* r = new rsam_reads();
-        Record rec;
-        {
-            FastxReader in(fq1);
-            while (in.next(rec)) r->r1.push_back(rec);
-        }
+        std::unique_ptr<rsam_reads> r(new rsam_reads());
         if (fq2 && *fq2) {
-            FastxReader in(fq2);
-            while (in.next(rec)) r->r2.push_back(rec);
+            FastxReader::read_pair(fq1, fq2, r->r1, r->r2);
             r->paired = true;
             if (r->r1.size() != r->r2.size()) throw std::runtime_error("read files have different record counts");
+        } else {
+            r->r1 = FastxReader::read_all(fq1);
         }
-        return r;
+        return r.release();
     } catch (const std::exception& e) {
         g_err = e.what();
         return nullptr;

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <exception>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -626,84 +627,136 @@ __attribute__((weak)) void build_default_index(StiIndex& idx, const References& 
 }
 
 // ----------------------------------------------------------------- FASTQ --
-// kseq semantics: '@' or '>' header, name = up to the first whitespace, the
-// rest of the header line (after that whitespace) is the comment; sequence
-// lines are concatenated until '+' (FASTQ) or the next header (FASTA);
-// quality is read until it is as long as the sequence.
 struct FastxReader::Impl {
+    // block reader: 4 MB gzread()s, lines found with memchr; a line is a view
+    // into the buffer, valid until the next refill
     gzFile f = nullptr;
     std::vector<char> buf;
     size_t pos = 0, len = 0;
     bool eof = false;
-    int last_char = -1;   // header char of the next record, if already read
-    int getc() {
-        if (pos >= len) {
-            if (eof) return -1;
-            int n = gzread(f, buf.data(), (unsigned)buf.size());
-            if (n <= 0) { eof = true; return -1; }
-            len = (size_t)n; pos = 0;
+    int last_char = -1;   // header char of the next record, if already consumed
+    bool fill() {
+        if (eof) return false;
+        if (pos > 0) {
+            memmove(buf.data(), buf.data() + pos, len - pos);
+            len -= pos;
+            pos = 0;
         }
+        if (len == buf.size()) buf.resize(buf.size() * 2);
+        const int n = gzread(f, buf.data() + len, (unsigned)(buf.size() - len));
+        if (n <= 0) { eof = true; return false; }
+        len += (size_t)n;
+        return true;
+    }
+    int getc() {
+        if (pos >= len && !fill()) return -1;
         return (unsigned char)buf[pos++];
     }
-    bool getline(std::string& s) {
-        s.clear();
-        int c;
-        bool any = false;
-        while ((c = getc()) != -1) {
-            any = true;
-            if (c == '\n') break;
-            s.push_back((char)c);
+    // the rest of the current line without its '\n'; false when nothing was left
+    bool raw_line(std::string_view& out) {
+        size_t from = pos;
+        for (;;) {
+            const char* e = (const char*)memchr(buf.data() + from, '\n', len - from);
+            if (e) {
+                const size_t n = (size_t)(e - (buf.data() + pos));
+                out = std::string_view(buf.data() + pos, n);
+                pos += n + 1;
+                return true;
+            }
+            from = len - pos;                 // offset of the unscanned part after a refill
+            if (!fill()) {
+                if (pos < len) { out = std::string_view(buf.data() + pos, len - pos); pos = len; return true; }
+                return false;
+            }
+            from += pos;
         }
-        if (!s.empty() && s.back() == '\r') s.pop_back();
-        return any;
+    }
+    // kseq getline: the line with one trailing '\r' removed
+    bool getline(std::string_view& out) {
+        if (!raw_line(out)) return false;
+        if (!out.empty() && out.back() == '\r') out.remove_suffix(1);
+        return true;
     }
 };
 
 FastxReader::FastxReader(const std::string& path) : impl_(new Impl) {
     impl_->f = gzopen(path == "-" ? "/dev/stdin" : path.c_str(), "r");
     if (!impl_->f) throw std::runtime_error("Could not open FASTQ file: " + path);
-    impl_->buf.resize(1 << 20);
+    impl_->buf.resize(4 << 20);
     (void)gzbuffer(impl_->f, 1 << 20);
 }
 
 FastxReader::~FastxReader() { if (impl_->f) gzclose(impl_->f); }
 
+// kseq semantics: '@' or '>' header, name = up to the first whitespace, the
+// rest of the header line (after that whitespace) is the comment; sequence
+// lines are concatenated until '+' (FASTQ) or the next header (FASTA);
+// quality is read until it is as long as the sequence.
 bool FastxReader::next(Record& r) {
     Impl& I = *impl_;
     int c = I.last_char;
     if (c == -1) {
-        while ((c = I.getc()) != -1 && c != '>' && c != '@') {}
-        if (c == -1) return false;
+        for (;;) {                            // skip to the next '>' or '@' (any byte position)
+            if (I.pos >= I.len && !I.fill()) return false;
+            const char* s = I.buf.data() + I.pos;
+            const size_t n = I.len - I.pos;
+            size_t k = 0;
+            while (k < n && s[k] != '>' && s[k] != '@') ++k;
+            I.pos += k;
+            if (k < n) { c = (unsigned char)I.buf[I.pos++]; break; }
+        }
     }
-    std::string line;
+    std::string_view line;
     I.getline(line);
-    size_t ws = line.find_first_of(" \t\v\f\r");
-    if (ws == std::string::npos) { r.name = line; r.comment.clear(); }
+    const size_t ws = line.find_first_of(" \t\v\f\r");
+    if (ws == std::string_view::npos) { r.name.assign(line); r.comment.clear(); }
     else {
-        r.name = line.substr(0, ws);
-        size_t cs = line.find_first_not_of(" \t\v\f\r", ws);
-        r.comment = cs == std::string::npos ? std::string() : line.substr(cs);
+        r.name.assign(line.substr(0, ws));
+        const size_t cs = line.find_first_not_of(" \t\v\f\r", ws);
+        if (cs == std::string_view::npos) r.comment.clear();
+        else r.comment.assign(line.substr(cs));
     }
     r.seq.clear();
     r.qual.clear();
     I.last_char = -1;
-    while ((c = I.getc()) != -1 && c != '>' && c != '@' && c != '+') {
+    for (;;) {                                // sequence lines
+        c = I.getc();
+        if (c == -1 || c == '>' || c == '@' || c == '+') break;
         if (c == '\n') continue;
-        std::string rest;
-        I.getline(rest);
+        std::string_view rest;
+        I.getline(rest);                      // '\r' stripped from the rest only (kseq reads c first)
         r.seq.push_back((char)c);
-        r.seq += rest;
+        r.seq.append(rest);
         while (!r.seq.empty() && (r.seq.back() == ' ' || r.seq.back() == '\t')) r.seq.pop_back();
     }
     if (c == '>' || c == '@') { I.last_char = c; return true; }
     if (c == -1) return true;
-    I.getline(line);   // rest of '+' line
+    I.getline(line);                          // rest of the '+' line
     while (r.qual.size() < r.seq.size()) {
         if (!I.getline(line)) break;
-        r.qual += line;
+        r.qual.append(line);
     }
     if (r.qual.size() != r.seq.size()) throw std::runtime_error("FASTQ quality length differs from sequence length");
     return true;
+}
+
+std::vector<Record> FastxReader::read_all(const std::string& path) {
+    std::vector<Record> v;
+    FastxReader in(path);
+    Record r;
+    while (in.next(r)) { v.push_back(std::move(r)); r = Record(); }
+    return v;
+}
+
+void FastxReader::read_pair(const std::string& p1, const std::string& p2, std::vector<Record>& r1,
+                            std::vector<Record>& r2) {
+    std::exception_ptr err;
+    std::thread t([&]() {
+        try { r2 = read_all(p2); } catch (...) { err = std::current_exception(); }
+    });
+    try { r1 = read_all(p1); } catch (...) { t.join(); throw; }
+    t.join();
+    if (err) std::rethrow_exception(err);
 }
 
 }  // namespace rsa

@@ -99,13 +99,6 @@ Opts parse(int argc, char** argv, bool& ok) {
     return o;
 }
 
-std::vector<Record> read_all(const std::string& path) {
-    std::vector<Record> v;
-    FastxReader in(path);
-    Record r;
-    while (in.next(r)) v.push_back(r);
-    return v;
-}
 
 void write_sink(void* user, const std::string& chunk) {
     fwrite(chunk.data(), 1, chunk.size(), (FILE*)user);
@@ -124,8 +117,8 @@ int cli_main(int argc, char** argv, EngineFactory factory, const char* prog) {
         // read length (main.cpp:254-258: average of the first 500 records of each file)
         std::vector<Record> recs1, recs2;
         if (!o.reads1.empty() && !index_cmd) {
-            recs1 = read_all(o.reads1);
-            if (!o.reads2.empty()) recs2 = read_all(o.reads2);
+            if (o.reads2.empty()) recs1 = FastxReader::read_all(o.reads1);
+            else FastxReader::read_pair(o.reads1, o.reads2, recs1, recs2);
             if (!o.r_set) {
                 uint64_t tot = 0, num = 0;
                 for (size_t i = 0; i < std::min<size_t>(500, recs1.size()); ++i) { tot += recs1[i].seq.size(); num++; }

@@ -400,6 +400,10 @@ public:
     explicit FastxReader(const std::string& path);
     ~FastxReader();
     bool next(Record& r);
+    // every record of a file; read_pair() parses the two mate files on two threads
+    static std::vector<Record> read_all(const std::string& path);
+    static void read_pair(const std::string& p1, const std::string& p2, std::vector<Record>& r1,
+                          std::vector<Record>& r2);
 private:
     struct Impl;
     std::unique_ptr<Impl> impl_;
