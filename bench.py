@@ -50,11 +50,32 @@ def log(rank, *a):
     print(f"[bench r{rank} {time.strftime('%H:%M:%S')}]", *a, file=sys.stderr, flush=True)
 
 
+def _cgroup_cpus():
+    """CPUs granted by the cgroup v2 quota (cpu.max), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        return None if quota == "max" else max(1, int(int(quota) / int(period)))
+    except (OSError, ValueError):
+        return None
+
+
 def host_cores() -> int:
+    """Host threads for this rank: the CPUs this process may use (affinity, cgroup
+    quota) shared among the ranks of the node, capped by OMP_NUM_THREADS / MAX_JOBS.
+    torch.distributed.run exports OMP_NUM_THREADS=1 to every rank when the variable
+    is unset; that default says nothing about the host pipeline and is ignored."""
+    local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
     n = len(os.sched_getaffinity(0))
+    q = _cgroup_cpus()
+    if q:
+        n = min(n, q)
+    n = max(1, n // local)
     for var in ("OMP_NUM_THREADS", "MAX_JOBS"):
         v = os.environ.get(var)
         if v and v.isdigit() and int(v) > 0:
+            if var == "OMP_NUM_THREADS" and int(v) == 1 and local > 1:
+                continue
             n = min(n, int(v))
     return max(1, n)
 
