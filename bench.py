@@ -284,8 +284,8 @@ def main():
             "index_build": {"on": "gpu" if info["index_on_device"] else "host",
                             "seconds": round(info["index_seconds"], 3), "device_ms": info["index_device_ms"],
                             "replayed_segments": info["index_replayed_segments"],
-                            "note": "StrobemerIndex::populate (index.cpp:141-309) via rsa_index_build_run; "
-                                    "seconds include the D2H of the host copy"},
+                            "note": "StrobemerIndex::populate (index.cpp:141-309) via rsa_index_build_run; the "
+                                    "index stays in HBM and the engine adopts it (rsa_open_built)"},
             "roofline": rl,
             "cpu_baseline": cpu,
             "parity": parity,

@@ -241,6 +241,15 @@ rsa_index_build* rsa_index_build_run(int device, const char* ref_seq, const uint
 int rsa_index_build_download(rsa_index_build* b, rsa_ref_randstrobe* randstrobes, uint64_t* bucket_starts);
 void rsa_index_build_free(rsa_index_build* b);
 
+/* Open a context on a GPU-built index without a copy: the context adopts the
+ * build's device buffers (reference, entries, bucket table) and `b` is freed;
+ * on error `b` stays valid.  `view` supplies the parameters, bits, filter cutoff
+ * and contig offsets; its randstrobes, bucket_starts and ref_seq are not read. */
+rsa_ctx* rsa_open_built(rsa_index_build* b, const rsa_index_view* view, char* err, size_t err_len);
+/* Copy a context's resident index into caller buffers: randstrobes[n_randstrobes],
+ * bucket_starts[2^bits + 1] (the host copy a GPU-built index does not keep). */
+int rsa_index_download(rsa_ctx* ctx, rsa_ref_randstrobe* randstrobes, uint64_t* bucket_starts);
+
 /* ---- instrumentation ------------------------------------------------------ */
 
 /* kernels of the path, in stats arrays */

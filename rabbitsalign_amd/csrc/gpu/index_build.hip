@@ -360,6 +360,18 @@ struct rsa_index_build {
     int bits = 0;
 };
 
+// hands the device buffers of a build to a context (rsa_open_built) and frees the handle
+void index_build_release(rsa_index_build* b, int* device, char** ref, rsa_ref_randstrobe** rs, uint64_t** starts,
+                         uint64_t* n, int* bits) {
+    *device = b->device;
+    *ref = b->d_ref;
+    *rs = b->d_rs;
+    *starts = b->d_starts;
+    *n = b->n;
+    *bits = b->bits;
+    delete b;
+}
+
 extern "C" {
 
 void rsa_index_build_free(rsa_index_build* b) {

@@ -43,6 +43,9 @@ __global__ void k_cigar_compact(rsa_aln* alns, int n_jobs, const uint32_t* slots
 void launch_cigar_compact(hipStream_t st, rsa_aln* alns, int n_jobs, const uint32_t* slots, uint32_t* dense,
                           uint64_t* bsum, uint64_t* total);
 
+void index_build_release(rsa_index_build* b, int* device, char** ref, rsa_ref_randstrobe** rs, uint64_t** starts,
+                         uint64_t* n, int* bits);
+
 int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, const rsa_read_batch* rb,
              int32_t rescue_level, uint32_t rescue_cutoff, rsa_nam_batch* out, std::string& err, SeedCounters& c);
 int seed_randstrobes_run(SeedBufs& b, hipStream_t st, const SeedIndexParams& p, const rsa_read_batch* rb,
@@ -233,6 +236,56 @@ rsa_ctx* rsa_open(int device, const rsa_index_view* v, char* errbuf, size_t err_
     ctx->ip.coff = ctx->d_coff;
     ctx->resident = ctx->ref_bytes + sizeof(rsa_ref_randstrobe) * ctx->n_rs + sizeof(uint64_t) * n_starts;
     return ctx;
+}
+
+rsa_ctx* rsa_open_built(rsa_index_build* b, const rsa_index_view* v, char* errbuf, size_t err_len) {
+    auto fail = [&](const std::string& s) -> rsa_ctx* {
+        if (errbuf && err_len) { snprintf(errbuf, err_len, "%s", s.c_str()); }
+        return nullptr;
+    };
+    if (!b || !v || !v->contig_offsets) return fail("rsa_open_built: null build or view");
+    rsa_ctx* ctx = new rsa_ctx();
+    ctx->contig_off.assign(v->contig_offsets, v->contig_offsets + v->n_contigs + 1);
+    ctx->ref_bytes = ctx->contig_off.back();
+    int bits = 0;
+    index_build_release(b, &ctx->device, &ctx->d_ref, &ctx->d_rs, &ctx->d_starts, &ctx->n_rs, &bits);
+    if (bits != v->bits) {
+        std::string s = "rsa_open_built: view bits differ from the build's";
+        rsa_close(ctx);
+        return fail(s);
+    }
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e == hipSuccess) e = hipMalloc(&ctx->d_coff, sizeof(uint64_t) * ctx->contig_off.size());
+    if (e == hipSuccess)
+        e = hipMemcpy(ctx->d_coff, ctx->contig_off.data(), sizeof(uint64_t) * ctx->contig_off.size(), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        std::string s = std::string("rsa_open_built: ") + hipGetErrorString(e);
+        rsa_close(ctx);
+        return fail(s);
+    }
+    ctx->ip.rs = ctx->d_rs;
+    ctx->ip.starts = ctx->d_starts;
+    ctx->ip.n = ctx->n_rs;
+    ctx->ip.bits = v->bits;
+    ctx->ip.filter_cutoff = (uint32_t)v->filter_cutoff;
+    ctx->ip.k = v->k; ctx->ip.s = v->s; ctx->ip.t = v->t_syncmer;
+    ctx->ip.w_min = v->w_min; ctx->ip.w_max = v->w_max; ctx->ip.max_dist = v->max_dist;
+    ctx->ip.q = v->q;
+    ctx->ip.ref = ctx->d_ref;
+    ctx->ip.coff = ctx->d_coff;
+    ctx->resident = ctx->ref_bytes + sizeof(rsa_ref_randstrobe) * ctx->n_rs + sizeof(uint64_t) * (((size_t)1 << v->bits) + 1);
+    return ctx;
+}
+
+int rsa_index_download(rsa_ctx* ctx, rsa_ref_randstrobe* randstrobes, uint64_t* bucket_starts) {
+    if (!ctx) return RSA_ERR_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    if (randstrobes && ctx->n_rs)
+        HIPCHK(hipMemcpy(randstrobes, ctx->d_rs, sizeof(rsa_ref_randstrobe) * ctx->n_rs, hipMemcpyDeviceToHost));
+    if (bucket_starts && ctx->d_starts)
+        HIPCHK(hipMemcpy(bucket_starts, ctx->d_starts, sizeof(uint64_t) * (((size_t)1 << ctx->ip.bits) + 1),
+                         hipMemcpyDeviceToHost));
+    return RSA_OK;
 }
 
 void rsa_close(rsa_ctx* ctx) {

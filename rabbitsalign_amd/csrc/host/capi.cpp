@@ -79,7 +79,7 @@ rsam* rsam_open_files(const char* ref_fa, const char* sti, int read_len, int dev
             m->idx.read(sti);
             if (!(m->idx.params == ip)) throw std::runtime_error("index parameters differ from the read length profile");
         } else {
-            build_default_index(m->idx, m->refs, ip, -1, 0.0002f, std::max(1, threads), device);
+            build_default_index(m->idx, m->refs, ip, -1, 0.0002f, std::max(1, threads), device, false);
         }
         m->index_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
     } catch (const std::exception& e) {
@@ -101,7 +101,7 @@ rsam* rsam_open_synthetic(uint64_t seed, uint64_t ref_len, int n_contigs, int re
         finish_refs(m->refs);
         auto t = std::chrono::steady_clock::now();
         build_default_index(m->idx, m->refs, IndexParameters::from_read_length(read_len), -1, 0.0002f,
-                            std::max(1, threads), device);
+                            std::max(1, threads), device, false);
         m->index_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
     } catch (const std::exception& e) {
         if (err && err_len) snprintf(err, err_len, "%s", e.what());
@@ -117,6 +117,13 @@ rsam* rsam_open_like(const rsam* o, int device, int threads, char* err, size_t e
     rsam* m = new rsam();
     m->read_len = o->read_len;
     m->refs = o->refs;
+    // an index that lives only in the other mapper's HBM comes to the host first
+    if (!o->idx.host_copy() && !(o->eng && o->eng->download_index(const_cast<StiIndex&>(o->idx)))) {
+        g_err = "rsam_open_like: the index has no host copy";
+        if (err && err_len) snprintf(err, err_len, "%s", g_err.c_str());
+        delete m;
+        return nullptr;
+    }
     m->idx = o->idx;
     m->index_seconds = o->index_seconds;
     return open_common(m, device, err, err_len);
@@ -127,7 +134,7 @@ void rsam_close(rsam* m) { delete m; }
 int rsam_get_info(const rsam* m, rsam_info* out) {
     if (!m || !out) return -1;
     out->ref_bases = m->refs.concat.size();
-    out->n_randstrobes = m->idx.randstrobes.size();
+    out->n_randstrobes = m->idx.size();
     out->n_contigs = (int32_t)m->refs.size();
     out->bits = m->idx.bits;
     out->filter_cutoff = m->idx.filter_cutoff;
@@ -135,8 +142,8 @@ int rsam_get_info(const rsam* m, rsam_info* out) {
     out->canonical_read_length = m->idx.params.canonical_read_length;
     out->index_seconds = m->index_seconds;
     out->upload_seconds = m->upload_seconds;
-    out->device_resident_bytes = m->refs.concat.size() + m->idx.randstrobes.size() * sizeof(rsa_ref_randstrobe) +
-                                 m->idx.bucket_starts.size() * 8;
+    out->device_resident_bytes = m->refs.concat.size() + m->idx.size() * sizeof(rsa_ref_randstrobe) +
+                                 (((size_t)1 << m->idx.bits) + 1) * 8;
     out->index_on_device = m->idx.built_on_device ? 1 : 0;
     out->pad_ = 0;
     for (int i = 0; i < 6; ++i) out->index_device_ms[i] = m->idx.device_build_ms[i];

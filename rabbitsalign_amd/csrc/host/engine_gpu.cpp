@@ -39,6 +39,7 @@ class GpuEngine final : public Engine {
 public:
     GpuEngine(const References& refs, const StiIndex& idx, int device) {
         rsa_index_view v{};
+        const bool adopt = idx.device_build && idx.device_build->handle && idx.randstrobes.empty();
         v.randstrobes = idx.randstrobes.data();
         v.n_randstrobes = idx.randstrobes.size();
         v.bucket_starts = idx.bucket_starts.data();
@@ -51,8 +52,24 @@ public:
         v.contig_offsets = refs.offsets.data();
         v.n_contigs = (int)refs.size();
         char err[512] = {0};
-        ctx_ = rsa_open(device, &v, err, sizeof err);
+        if (adopt) {   // the index built on this device stays where it is (no D2H + H2D)
+            v.n_randstrobes = idx.n_device;
+            ctx_ = rsa_open_built((rsa_index_build*)idx.device_build->handle, &v, err, sizeof err);
+            if (ctx_) idx.device_build->handle = nullptr;
+        } else {
+            if (!idx.host_copy()) throw std::runtime_error("GPU engine: index has no host copy and no device build");
+            ctx_ = rsa_open(device, &v, err, sizeof err);
+        }
         if (!ctx_) throw std::runtime_error(std::string("GPU engine: ") + err);
+    }
+    bool download_index(StiIndex& idx) override {
+        if (idx.host_copy()) return true;
+        std::vector<rsa_ref_randstrobe> rs(idx.n_device);
+        std::vector<uint64_t> st((1ull << idx.bits) + 1);
+        if (rsa_index_download(ctx_, rs.data(), st.data()) != RSA_OK) return false;
+        idx.randstrobes.swap(rs);
+        idx.bucket_starts.swap(st);
+        return true;
     }
     ~GpuEngine() override {
         free_.clear();
@@ -186,7 +203,7 @@ std::unique_ptr<Engine> make_gpu_engine(const References& refs, const StiIndex& 
 // downloaded into the host StiIndex (.sti writing, the host pipeline's
 // parameters, a CPU engine opened on the same index)
 void build_default_index(StiIndex& idx, const References& refs, const IndexParameters& p, int bits_override, float f,
-                         int threads, int device) {
+                         int threads, int device, bool host_copy) {
     (void)threads;
     rsa_index_build_params bp{};
     bp.k = p.k; bp.s = p.s; bp.t_syncmer = p.t;
@@ -202,11 +219,22 @@ void build_default_index(StiIndex& idx, const References& refs, const IndexParam
     idx.params = p;
     idx.bits = info.bits;
     idx.filter_cutoff = info.filter_cutoff;
-    idx.randstrobes.resize(info.n_randstrobes);
-    idx.bucket_starts.resize((1ull << info.bits) + 1);
-    const int rc = rsa_index_build_download(b, idx.randstrobes.data(), idx.bucket_starts.data());
-    rsa_index_build_free(b);
-    if (rc != RSA_OK) throw std::runtime_error("GPU index build: download failed");
+    idx.randstrobes.clear();
+    idx.bucket_starts.clear();
+    idx.device_build.reset();
+    idx.n_device = 0;
+    if (host_copy) {
+        idx.randstrobes.resize(info.n_randstrobes);
+        idx.bucket_starts.resize((1ull << info.bits) + 1);
+        const int rc = rsa_index_build_download(b, idx.randstrobes.data(), idx.bucket_starts.data());
+        rsa_index_build_free(b);
+        if (rc != RSA_OK) throw std::runtime_error("GPU index build: download failed");
+    } else {
+        idx.device_build = std::make_shared<StiIndex::DeviceBuild>();
+        idx.device_build->handle = b;
+        idx.device_build->release = [](void* h) { rsa_index_build_free((rsa_index_build*)h); };
+        idx.n_device = info.n_randstrobes;
+    }
     idx.built_on_device = true;
     const double ms[6] = {info.ms_upload, info.ms_syncmers, info.ms_randstrobes, info.ms_sort, info.ms_buckets,
                           info.ms_total};

@@ -621,8 +621,9 @@ void StiIndex::build(const References& refs, const IndexParameters& p, int bits_
 }
 
 __attribute__((weak)) void build_default_index(StiIndex& idx, const References& refs, const IndexParameters& p,
-                                               int bits_override, float f, int threads, int device) {
+                                               int bits_override, float f, int threads, int device, bool host_copy) {
     (void)device;
+    (void)host_copy;
     idx.build(refs, p, bits_override, f, threads);
 }
 

@@ -136,23 +136,23 @@ int cli_main(int argc, char** argv, EngineFactory factory, const char* prog) {
         StiIndex idx;
         const std::string sti_path = o.ref + ip.filename_extension();
         // the index is built on the GPU (engine build) unless --cpu-index asks for the host build
-        auto build_index = [&]() {
+        auto build_index = [&](bool host_copy) {
             if (o.cpu_index) idx.build(refs, ip, o.bits, o.f, std::max(1, o.threads));
-            else build_default_index(idx, refs, ip, o.bits, o.f, std::max(1, o.threads), o.device);
+            else build_default_index(idx, refs, ip, o.bits, o.f, std::max(1, o.threads), o.device, host_copy);
         };
         if (index_cmd || o.create_index) {
-            build_index();
+            build_index(true);
             std::string out = o.out_file.empty() ? sti_path : o.out_file;
             idx.write(out);
             if (o.verbose) fprintf(stderr, "wrote %s (%zu randstrobes, bits %d, filter cutoff %d)\n", out.c_str(),
-                                   idx.randstrobes.size(), idx.bits, idx.filter_cutoff);
+                                   (size_t)idx.size(), idx.bits, idx.filter_cutoff);
             return 0;
         }
         if (o.use_index) {
             idx.read(sti_path);
             if (!(idx.params == ip)) throw std::runtime_error("Index parameters in .sti file and those specified on command line differ");
         } else {
-            build_index();
+            build_index(false);   // a GPU build stays in HBM for the engine
         }
         const double t_index = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         if (o.reads1.empty()) throw std::runtime_error("At least one file with reads must be specified.");

@@ -275,14 +275,26 @@ struct StiIndex {                               // .sti contents (src/index.cpp:
     bool built_on_device = false;
     double device_build_ms[6] = {0, 0, 0, 0, 0, 0};
     uint64_t replayed_segments = 0;
+    // a GPU build kept in HBM (no host copy): the GPU engine adopts it; a host
+    // copy is downloaded only when something needs one (.sti write, a CPU engine)
+    struct DeviceBuild {
+        void* handle = nullptr;                 // rsa_index_build*, until an engine adopts it
+        void (*release)(void*) = nullptr;
+        ~DeviceBuild() { if (handle && release) release(handle); }
+    };
+    std::shared_ptr<DeviceBuild> device_build;
+    uint64_t n_device = 0;                      // entries of the device-only index
+    uint64_t size() const { return randstrobes.empty() ? n_device : randstrobes.size(); }
+    bool host_copy() const { return !randstrobes.empty() || n_device == 0; }
 };
 
 // StrobemerIndex::populate as used by the CLI and the C API.  The host build
 // (StiIndex::build) by default; the GPU engine's translation unit
 // (engine_gpu.cpp) replaces it with the HIP build, so the product makes its
 // index on the device it maps on.
+// host_copy = false lets a GPU build stay in HBM for the engine to adopt.
 void build_default_index(StiIndex& idx, const References& refs, const IndexParameters& p, int bits_override, float f,
-                         int threads, int device);
+                         int threads, int device, bool host_copy = true);
 
 // --------------------------------------------------------------- engine ---
 struct SeedBatchOut {
@@ -325,6 +337,8 @@ public:
     // true when seed/extend run on a device and the calling thread only waits
     virtual bool offloads() const { return false; }
     virtual void reset_kernel_stats() {}
+    // the host copy of an index the engine holds on its device (GPU engine only)
+    virtual bool download_index(StiIndex&) { return false; }
 };
 
 // GPU engine over the C-ABI (engine_gpu.cpp)

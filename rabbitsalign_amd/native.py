@@ -116,7 +116,7 @@ def stats_dict(ks: "KernelStats") -> dict:
 EXPORTED_SYMBOLS = ["rsa_open", "rsa_close", "rsa_last_error", "rsa_resident_bytes", "rsa_randstrobes",
                     "rsa_seed", "rsa_extend", "rsa_extend_cigar_bound", "rsa_host_alloc", "rsa_host_free",
                     "rsa_get_stats", "rsa_reset_stats", "rsa_index_build_run", "rsa_index_build_download",
-                    "rsa_index_build_free"]
+                    "rsa_index_build_free", "rsa_open_built", "rsa_index_download"]
 
 _lib = None
 
