@@ -1,7 +1,10 @@
 // rsa_seed.h -- host/device shared declarations of the seeding kernels.
 #pragma once
 #include <chrono>
+#include <condition_variable>
+#include <cstring>
 #include <hip/hip_runtime.h>
+#include <mutex>
 #include <stdint.h>
 #include <stdlib.h>
 #include "../../../include/rsa_gpu.h"
@@ -23,28 +26,69 @@ struct SeedBufs {
     size_t cap[32] = {0};
     void* h[12] = {nullptr};
     size_t hcap[12] = {0};
-    hipEvent_t done = nullptr;   // blocking-sync event: the calling thread sleeps instead of spinning
+    hipEvent_t done = nullptr;   // blocking-sync event (RSA_WAIT=event)
 };
 
-// Wait for everything queued on `s` so far without burning a host core
-// (hipEventBlockingSync); the host pipeline runs more workers than cores.
+// Wait for everything queued on `s` so far without burning a host core; the
+// host pipeline runs more workers than cores and a waiting worker hands its
+// core to one that computes.
 // time this thread spent blocked in stream_wait (the entry points read and reset it)
 inline double& device_wait_ms() {
     static thread_local double ms = 0;
     return ms;
 }
 
+// The stream calls back (hipLaunchHostFunc) into a condition variable the
+// thread sleeps on.  A blocking-sync event is not enough: the runtime spins on
+// the HSA signal (with sched_yield) for a while before it sleeps, and with
+// several waits a chunk that spinning took ~20 % of the workers' CPU time
+// (RSA_PC_SAMPLE profile on the box).  Heap-held, so a wait abandoned on a
+// stream error never leaves the callback a dangling pointer.
+struct HostWaiter {
+    std::mutex m;
+    std::condition_variable cv;
+    bool done = false;
+};
+inline void host_waiter_wake(void* p) {
+    HostWaiter* w = (HostWaiter*)p;
+    {
+        std::lock_guard<std::mutex> g(w->m);
+        w->done = true;
+    }
+    w->cv.notify_one();
+}
+
+// RSA_WAIT: "callback" (default), "event" (blocking-sync event), "spin" (hipStreamSynchronize)
 inline hipError_t stream_wait(hipStream_t s, hipEvent_t& e) {
-    static const bool spin = [] { const char* v = getenv("RSA_SPIN_WAIT"); return v && v[0] == '1'; }();
+    static const int mode = [] {
+        const char* v = getenv("RSA_WAIT");
+        if (v && strcmp(v, "event") == 0) return 1;
+        if (v && strcmp(v, "spin") == 0) return 2;
+        return 0;
+    }();
     const auto t0 = std::chrono::steady_clock::now();
-    hipError_t err;
-    if (spin) {
+    hipError_t err = hipSuccess;
+    if (mode == 2) {
         err = hipStreamSynchronize(s);
-    } else {
-        err = hipSuccess;
+    } else if (mode == 1) {
         if (!e) err = hipEventCreateWithFlags(&e, hipEventBlockingSync | hipEventDisableTiming);
         if (err == hipSuccess) err = hipEventRecord(e, s);
         if (err == hipSuccess) err = hipEventSynchronize(e);
+    } else {
+        HostWaiter* w = new HostWaiter();
+        err = hipLaunchHostFunc(s, host_waiter_wake, w);
+        if (err != hipSuccess) {
+            delete w;
+        } else {
+            std::unique_lock<std::mutex> l(w->m);
+            while (!w->cv.wait_for(l, std::chrono::seconds(1), [&] { return w->done; })) {
+                const hipError_t q = hipStreamQuery(s);     // a failed stream never calls back
+                if (q != hipErrorNotReady && q != hipSuccess) { err = q; break; }
+            }
+            const bool done = w->done;
+            l.unlock();
+            if (done) delete w;                             // else left to a callback that may still come
+        }
     }
     device_wait_ms() += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return err;

@@ -1,5 +1,15 @@
 // capi.cpp -- include/rsalign.h: the mapping path as a C library.
+#include <atomic>
 #include <chrono>
+#include <map>
+
+#include <dlfcn.h>
+#include <signal.h>
+#include <sys/syscall.h>
+#include <sys/time.h>
+#include <time.h>
+#include <ucontext.h>
+#include <unistd.h>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -19,6 +29,76 @@ std::unique_ptr<Engine> make_default_engine(const References& refs, const StiInd
 using namespace rsa;
 
 static thread_local std::string g_err;
+
+// Host PC sampler for profiling the mapping on the GPU box (RSA_PC_SAMPLE=file):
+// during rsam_map every pipeline worker (g_worker_start_hook) gets a timer on its
+// own CPU clock firing every 500 us of CPU; the handler records the interrupted PC.
+// Output: "pc count" lines and the process's executable mappings ("#map"), so
+// scripts/pc_report.py can attribute and symbolise them offline.  Instrumentation only.
+namespace {
+constexpr size_t kMaxPcs = 1 << 22;
+uint64_t* g_pcs = nullptr;
+std::atomic<size_t> g_npc{0};
+std::mutex g_tid_m;
+void on_prof(int, siginfo_t*, void* uc) {
+    const size_t i = g_npc.fetch_add(1, std::memory_order_relaxed);
+    if (i < kMaxPcs) g_pcs[i] = (uint64_t)((ucontext_t*)uc)->uc_mcontext.gregs[REG_RIP];
+}
+std::vector<timer_t> g_timers;
+// a CPU-time timer per worker (CLOCK_THREAD_CPUTIME_ID, signal to that thread):
+// samples land only where the worker spends CPU, blocked waits never show up
+void register_worker() {
+    sigevent sev{};
+    sev.sigev_notify = SIGEV_THREAD_ID;
+    sev.sigev_signo = SIGPROF;
+    sev._sigev_un._tid = (pid_t)syscall(SYS_gettid);
+    timer_t t;
+    if (timer_create(CLOCK_THREAD_CPUTIME_ID, &sev, &t) != 0) return;
+    itimerspec its{{0, 500000}, {0, 500000}};
+    timer_settime(t, 0, &its, nullptr);
+    std::lock_guard<std::mutex> g(g_tid_m);
+    g_timers.push_back(t);
+}
+struct PcSampler {
+    const char* path = getenv("RSA_PC_SAMPLE");
+    PcSampler() {
+        if (!path) return;
+        if (!g_pcs) g_pcs = new uint64_t[kMaxPcs];
+        g_npc = 0;
+        struct sigaction sa{};
+        sa.sa_sigaction = on_prof;
+        sa.sa_flags = SA_SIGINFO | SA_RESTART;
+        sigaction(SIGPROF, &sa, nullptr);
+        rsa::g_worker_start_hook = register_worker;
+    }
+    ~PcSampler() {
+        if (!path) return;
+        rsa::g_worker_start_hook = nullptr;
+        {
+            std::lock_guard<std::mutex> g(g_tid_m);
+            for (timer_t t : g_timers) timer_delete(t);
+            g_timers.clear();
+        }
+        Dl_info di{};
+        dladdr((void*)&on_prof, &di);
+        const uint64_t base = (uint64_t)di.dli_fbase;
+        std::map<uint64_t, uint64_t> h;
+        const size_t n = std::min(kMaxPcs, g_npc.load());
+        for (size_t i = 0; i < n; ++i) h[g_pcs[i]]++;
+        FILE* f = fopen(path, "a");
+        if (!f) return;
+        fprintf(f, "# base %lx lib %s samples %zu\n", (unsigned long)base, di.dli_fname ? di.dli_fname : "?", n);
+        for (auto& kv : h) fprintf(f, "%lx %lu\n", (unsigned long)kv.first, (unsigned long)kv.second);
+        if (FILE* mp = fopen("/proc/self/maps", "r")) {      // to attribute PCs to libraries offline
+            char line[1024];
+            while (fgets(line, sizeof line, mp))
+                if (strstr(line, " r-xp ") || strstr(line, " r--p ")) fprintf(f, "#map %s", line);
+            fclose(mp);
+        }
+        fclose(f);
+    }
+};
+}  // namespace
 
 struct rsam {
     References refs;
@@ -205,6 +285,7 @@ static void sink_fn(void* user, const std::string& chunk) {
 
 int rsam_map(rsam* m, const rsam_reads* reads, int threads, int chunk_size, const char* sam_path, rsam_stats* out) {
     if (!m || !reads) return -1;
+    PcSampler sampler;
     try {
         SinkState st;
         if (sam_path && *sam_path) {

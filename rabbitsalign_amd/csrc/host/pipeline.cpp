@@ -28,6 +28,8 @@
 
 namespace rsa {
 
+void (*g_worker_start_hook)() = nullptr;
+
 namespace {
 
 using Clock = std::chrono::steady_clock;
@@ -464,6 +466,7 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
     };
 
     auto worker = [&](bool leader) {
+        if (g_worker_start_hook) g_worker_start_hook();
         std::vector<SwJob> jobs;
         std::vector<AlignmentInfo> infos;
         AlignmentStatistics local;

@@ -424,6 +424,9 @@ private:
 };
 
 // ------------------------------------------------------------ pipeline ---
+// called at the start of every pipeline worker thread (profiling hooks; null by default)
+extern void (*g_worker_start_hook)();
+
 struct PipelineOptions {
     int threads = 3;
     int chunk_size = 10000;
