@@ -1773,8 +1773,10 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
     SCHK(hipGetLastError());
     kt.end(st);
     SCHK(hens(b, H_FLAGS, 4ull * n));
+    SCHK(hens(b, H_NONREP, 4ull * n));
     SCHK(hipMemcpyAsync(b.h[H_FLAGS], b.p[B_FLAGS], 4ull * n, hipMemcpyDeviceToHost, st));
     SCHK(hipMemcpyAsync(b.h[H_CNT], b.p[B_NCNT1], 4ull * n, hipMemcpyDeviceToHost, st));
+    SCHK(hipMemcpyAsync(b.h[H_NONREP], b.p[B_NONREP], 4ull * n, hipMemcpyDeviceToHost, st));
     SCHK(stream_wait(st, b.done));
     // rare: reads whose maps rehash past the small table -> big-map pass
     std::vector<int> big;
@@ -1798,13 +1800,11 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
         }
         SCHK(hipMemcpyAsync(b.h[H_FLAGS], b.p[B_FLAGS], 4ull * n, hipMemcpyDeviceToHost, st));
         SCHK(hipMemcpyAsync(b.h[H_CNT], b.p[B_NCNT1], 4ull * n, hipMemcpyDeviceToHost, st));
+        SCHK(hipMemcpyAsync(b.h[H_NONREP], b.p[B_NONREP], 4ull * n, hipMemcpyDeviceToHost, st));
         SCHK(stream_wait(st, b.done));
         for (int i : big) if (HP(H_FLAGS, uint32_t)[i] & 2u) { err = "rsa_seed: robin_hood emulation overflow"; return RSA_ERR_NOMEM; }
     }
-    // nonrepetitive fraction to host
-    SCHK(hens(b, H_NONREP, 4ull * n));
-    SCHK(hipMemcpyAsync(b.h[H_NONREP], b.p[B_NONREP], 4ull * n, hipMemcpyDeviceToHost, st));
-    SCHK(stream_wait(st, b.done));
+    // nonrepetitive fraction (copied with the flags above)
     memcpy(out->nonrepetitive_fraction, b.h[H_NONREP], 4ull * n);
     // rescue decision (aln.cpp:1954-1962)
     std::vector<int> resc;
