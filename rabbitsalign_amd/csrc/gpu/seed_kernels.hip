@@ -1847,7 +1847,9 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
             SCHK(hipGetLastError());
             kt.end(st);
         }
+        SCHK(hens(b, H_CNT2, 4ull * n));
         SCHK(hipMemcpyAsync(b.h[H_FLAGS], b.p[B_FLAGS], 4ull * n, hipMemcpyDeviceToHost, st));
+        SCHK(hipMemcpyAsync(b.h[H_CNT2], b.p[B_NCNT2], 4ull * n, hipMemcpyDeviceToHost, st));
         SCHK(stream_wait(st, b.done));
         std::vector<int> bigr;
         for (int i : resc) if (HP(H_FLAGS, uint32_t)[i] & 4u) bigr.push_back(i);
@@ -1869,12 +1871,10 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
                 kt.end(st);
             }
             SCHK(hipMemcpyAsync(b.h[H_FLAGS], b.p[B_FLAGS], 4ull * n, hipMemcpyDeviceToHost, st));
+            SCHK(hipMemcpyAsync(b.h[H_CNT2], b.p[B_NCNT2], 4ull * n, hipMemcpyDeviceToHost, st));
             SCHK(stream_wait(st, b.done));
             for (int i : bigr) if (HP(H_FLAGS, uint32_t)[i] & 4u) { err = "rsa_seed: rescue map overflow"; return RSA_ERR_NOMEM; }
         }
-        SCHK(hens(b, H_CNT2, 4ull * n));
-        SCHK(hipMemcpyAsync(b.h[H_CNT2], b.p[B_NCNT2], 4ull * n, hipMemcpyDeviceToHost, st));
-        SCHK(stream_wait(st, b.done));
         for (int i : resc) n2[i] = HP(H_CNT2, uint32_t)[i];
     } else {
         SCHK(dens(b, B_ROFF2, 8ull * (n + 1)));
@@ -1921,16 +1921,24 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
         SCHK(hipMemcpyAsync(out->sites, b.p[B_SITES], sizeof(rsa_nam_site) * total, hipMemcpyDeviceToHost, st));
         SCHK(hens(b, H_PUSED, 8));
         SCHK(hipMemcpyAsync(b.h[H_PUSED], b.p[B_PUSED], 8, hipMemcpyDeviceToHost, st));
+        // positions: one per NAM comes back with the rest (synthetic 2x150: ~0.5 a NAM); more
+        // only in a second copy after the wait
+        const uint64_t guess = std::min<uint64_t>(out->mm_capacity, total);
+        if (guess) SCHK(hipMemcpyAsync(out->mm_pool, b.p[B_POOL], 2 * guess, hipMemcpyDeviceToHost, st));
         SCHK(stream_wait(st, b.done));
         const uint64_t used = std::min<uint64_t>(*HP(H_PUSED, uint64_t), out->mm_capacity);
         out->mm_used = used;
-        if (used) SCHK(hipMemcpyAsync(out->mm_pool, b.p[B_POOL], 2 * used, hipMemcpyDeviceToHost, st));
+        if (used > guess) {
+            SCHK(hipMemcpyAsync(out->mm_pool + guess, DP(B_POOL, uint16_t) + guess, 2 * (used - guess),
+                                hipMemcpyDeviceToHost, st));
+            SCHK(stream_wait(st, b.done));
+        }
         // NAM + read bytes read, window bytes compared, site + positions written
         site_bytes = (double)total * (sizeof(rsa_nam) + sizeof(rsa_nam_site) + 2.0 * 20 + 150) + 2.0 * used;
-    } else if (out->sites == nullptr) {
-        out->mm_used = 0;
+    } else {
+        if (out->sites == nullptr) out->mm_used = 0;
+        SCHK(stream_wait(st, b.done));
     }
-    SCHK(stream_wait(st, b.done));
     // counters and algorithmic bytes (DESIGN.md "Kernels")
     uint64_t n1_tot = 0, n2_tot = 0, resc_q = 0, resc_scan = 0, resc_hits = 0;
     for (uint32_t i = 0; i < n; ++i) n1_tot += n1[i];
