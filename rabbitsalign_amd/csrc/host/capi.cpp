@@ -38,11 +38,15 @@ static thread_local std::string g_err;
 namespace {
 constexpr size_t kMaxPcs = 1 << 22;
 uint64_t* g_pcs = nullptr;
+uint64_t* g_ras = nullptr;     // the word at the interrupted stack pointer: a leaf's return address
 std::atomic<size_t> g_npc{0};
 std::mutex g_tid_m;
 void on_prof(int, siginfo_t*, void* uc) {
     const size_t i = g_npc.fetch_add(1, std::memory_order_relaxed);
-    if (i < kMaxPcs) g_pcs[i] = (uint64_t)((ucontext_t*)uc)->uc_mcontext.gregs[REG_RIP];
+    if (i >= kMaxPcs) return;
+    const greg_t* r = ((ucontext_t*)uc)->uc_mcontext.gregs;
+    g_pcs[i] = (uint64_t)r[REG_RIP];
+    g_ras[i] = *(const uint64_t*)r[REG_RSP];
 }
 std::vector<timer_t> g_timers;
 // a CPU-time timer per worker (CLOCK_THREAD_CPUTIME_ID, signal to that thread):
@@ -64,6 +68,7 @@ struct PcSampler {
     PcSampler() {
         if (!path) return;
         if (!g_pcs) g_pcs = new uint64_t[kMaxPcs];
+        if (!g_ras) g_ras = new uint64_t[kMaxPcs];
         g_npc = 0;
         struct sigaction sa{};
         sa.sa_sigaction = on_prof;
@@ -89,6 +94,11 @@ struct PcSampler {
         if (!f) return;
         fprintf(f, "# base %lx lib %s samples %zu\n", (unsigned long)base, di.dli_fname ? di.dli_fname : "?", n);
         for (auto& kv : h) fprintf(f, "%lx %lu\n", (unsigned long)kv.first, (unsigned long)kv.second);
+        std::map<std::pair<uint64_t, uint64_t>, uint64_t> hr;
+        for (size_t i = 0; i < n; ++i) hr[{g_pcs[i], g_ras[i]}]++;
+        for (auto& kv : hr)
+            fprintf(f, "#ra %lx %lx %lu\n", (unsigned long)kv.first.first, (unsigned long)kv.first.second,
+                    (unsigned long)kv.second);
         if (FILE* mp = fopen("/proc/self/maps", "r")) {      // to attribute PCs to libraries offline
             char line[1024];
             while (fgets(line, sizeof line, mp))

@@ -86,6 +86,17 @@ struct OrderedSink {
     size_t next = 0;
     uint64_t bytes = 0;
     SamDigest total;
+    // written chunks' buffers, kept at capacity for the next chunks: a fresh
+    // ~10 MB buffer per chunk is mmap'd memory the first write page-faults in
+    std::vector<std::string> spare;
+    std::string take() {
+        static const bool off = getenv("RSA_SAM_REUSE") && atoi(getenv("RSA_SAM_REUSE")) == 0;
+        std::lock_guard<std::mutex> g(m);
+        if (off || spare.empty()) return std::string();
+        std::string s = std::move(spare.back());
+        spare.pop_back();
+        return s;
+    }
     void put(size_t idx, std::string&& s) {
         SamDigest d;
         if (digest) d = SamDigest::of(s);            // in the calling worker
@@ -95,6 +106,10 @@ struct OrderedSink {
             bytes += it->second.first.size();
             total.append(it->second.second);
             if (sink) sink(user, it->second.first);
+            if (spare.size() < 48) {
+                it->second.first.clear();
+                spare.push_back(std::move(it->second.first));
+            }
             pending.erase(it);
             next++;
         }
@@ -458,7 +473,7 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
         }
         c.times.extend += since(te);
         c.stats.tot_aligner_calls += jobs.size();
-        std::string out;
+        std::string out = os.take();
         pe_store_last(c, mc, est, infos, opt.rg_id, out);
         const auto tp = Clock::now();
         os.put(c.index, std::move(out));
@@ -511,7 +526,7 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                     }
                     pre->times.extend += since(te);
                     pre->stats.tot_aligner_calls += jobs.size();
-                    std::string out;
+                    std::string out = os.take();
                     pe_store_last(*pre, mc, isize, infos, opt.rg_id, out);
                     os.put(pre->index, std::move(out));
                     local.add(pre->stats);
@@ -672,7 +687,7 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
                 const Read read(recs[i].seq, rcs[i - b]);
                 pos = store_results_se(res[i - b], read, mc, infos, pos);
             }
-            std::string out;
+            std::string out = os.take();
             out.reserve(7 * (size_t)mc.mparams.r * (e - b));
             Sam sam(out, mc.refs, mc.mparams.cigar_eqx, opt.rg_id, mc.mparams.output_unmapped, mc.mparams.details);
             for (size_t i = b; i < e; ++i) {

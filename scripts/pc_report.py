@@ -1,57 +1,80 @@
 #!/usr/bin/env python3
 """Attribute RSA_PC_SAMPLE output (capi.cpp PcSampler) to libraries and functions.
 
-    python scripts/pc_report.py gpurun_out/pcsN/pcs.txt [top]
+    python scripts/pc_report.py gpurun_out/pcsN/pcs.txt [top] [callee-substring]
 
 Each "pc count" sample is mapped through the recorded /proc/self/maps lines to
 (library, file offset) and symbolised with addr2line; libraries from the box
-resolve here because the image is the same."""
+resolve here because the image is the same.  With a callee substring, the
+samples whose function matches it are also broken down by the word at the
+stack pointer ("#ra" lines), which is the caller for a leaf such as memmove."""
 import collections
 import os
 import subprocess
 import sys
 
 
+def symbolise(maps, pcs):
+    """{pc: "function [library]"} for a set of absolute addresses."""
+    bylib = collections.defaultdict(list)
+    for pc in pcs:
+        for lo, hi, off, name in maps:
+            if lo <= pc < hi:
+                bylib[name].append((pc, pc - lo + off))
+                break
+        else:
+            bylib["?"].append((pc, pc))
+    sym = {}
+    for name, v in bylib.items():
+        lib = name.replace("/tmp/code/RabbitBio__RabbitSAlign/repo", os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        if not os.path.exists(lib):
+            for pc, _ in v:
+                sym[pc] = f"[{os.path.basename(name)}]"
+            continue
+        offs = sorted(set(o for _, o in v))
+        out = subprocess.run(["addr2line", "-f", "-C", "-e", lib] + [hex(o) for o in offs], capture_output=True,
+                             text=True).stdout.split("\n")
+        by_off = {o: out[2 * i] for i, o in enumerate(offs)}
+        for pc, o in v:
+            sym[pc] = f"{by_off.get(o, '??')[:100]} [{os.path.basename(name)}]"
+    return sym, bylib
+
+
 def main():
     path = sys.argv[1]
     top = int(sys.argv[2]) if len(sys.argv) > 2 else 40
-    maps, pcs = [], collections.Counter()
+    callee = sys.argv[3] if len(sys.argv) > 3 else None
+    maps, pcs, ras = [], collections.Counter(), collections.Counter()
     for line in open(path):
         if line.startswith("#map "):
             f = line[5:].split()
             lo, hi = (int(x, 16) for x in f[0].split("-"))
             maps.append((lo, hi, int(f[2], 16), f[5] if len(f) > 5 else "?"))
+        elif line.startswith("#ra "):
+            _, a, r, c = line.split()
+            ras[(int(a, 16), int(r, 16))] += int(c)
         elif not line.startswith("#"):
             a, c = line.split()
             pcs[int(a, 16)] += int(c)
     tot = sum(pcs.values())
-    bylib = collections.defaultdict(list)
-    for pc, c in pcs.items():
-        for lo, hi, off, name in maps:
-            if lo <= pc < hi:
-                bylib[name].append((pc - lo + off, c))
-                break
-        else:
-            bylib["?"].append((pc, c))
+    sym, bylib = symbolise(maps, pcs)
     print(f"samples {tot}")
-    for name, v in sorted(bylib.items(), key=lambda kv: -sum(c for _, c in kv[1])):
-        print(f"{100 * sum(c for _, c in v) / tot:5.1f}%  {name}")
+    for name, v in sorted(bylib.items(), key=lambda kv: -sum(pcs[pc] for pc, _ in kv[1])):
+        print(f"{100 * sum(pcs[pc] for pc, _ in v) / tot:5.1f}%  {name}")
     fn = collections.Counter()
-    for name, v in bylib.items():
-        lib = name.replace("/tmp/code/RabbitBio__RabbitSAlign/repo", os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-        if not os.path.exists(lib):
-            for off, c in v:
-                fn[f"[{os.path.basename(name)}]"] += c
-            continue
-        offs = sorted(set(o for o, _ in v))
-        out = subprocess.run(["addr2line", "-f", "-C", "-e", lib] + [hex(o) for o in offs], capture_output=True,
-                             text=True).stdout.split("\n")
-        sym = {o: out[2 * i] for i, o in enumerate(offs)}
-        for off, c in v:
-            s = sym.get(off, "??")
-            fn[f"{s[:100]} [{os.path.basename(name)}]"] += c
+    for pc, c in pcs.items():
+        fn[sym[pc]] += c
     for f, c in fn.most_common(top):
         print(f"{100 * c / tot:5.1f}%  {f}")
+    if callee:
+        hit = {(pc, ra): c for (pc, ra), c in ras.items() if callee in sym.get(pc, "")}
+        rsym, _ = symbolise(maps, set(ra for _, ra in hit))
+        callers = collections.Counter()
+        for (pc, ra), c in hit.items():
+            callers[rsym[ra]] += c
+        print(f"\ncallers of samples in '{callee}' ({sum(hit.values())} samples):")
+        for f, c in callers.most_common(top):
+            print(f"{100 * c / tot:5.1f}%  {f}")
 
 
 if __name__ == "__main__":
