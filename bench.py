@@ -145,7 +145,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--workload", default="pe150_3g", choices=sorted(WORKLOADS))
     ap.add_argument("--pairs", type=int, default=1_000_000,
                     help="pairs (SE: reads) per step per GPU (SURVEY.md §8d: 10^6 pairs per config)")

@@ -173,6 +173,20 @@ static bool upper_already(const std::string& s) {
     return (acc & 0x2020202020202020ULL) == 0;
 }
 
+// Each read's name, sequence and qualities are separate heap strings the
+// hardware prefetcher cannot follow: loading a chunk (sequences) and writing its
+// SAM records (all three, last touched at load) request them a few pairs ahead.
+constexpr size_t kRecAhead = 4;
+static inline void prefetch_str(const std::string& s) {
+    const char* p = s.data();
+    for (size_t o = 0; o < s.size(); o += 64) __builtin_prefetch(p + o);
+}
+static inline void prefetch_record(const Record& r) {
+    prefetch_str(r.name);
+    prefetch_str(r.seq);
+    prefetch_str(r.qual);
+}
+
 void pe_load(PeChunk& c, const std::vector<Record>& a, const std::vector<Record>& b, size_t idx, size_t chunk) {
     c.index = idx;
     c.owned.clear();
@@ -191,6 +205,10 @@ void pe_load(PeChunk& c, const std::vector<Record>& a, const std::vector<Record>
     };
     size_t tot = 0;
     for (size_t i = 0; i < n; ++i) {
+        if (i + kRecAhead < n) {
+            prefetch_str(a[c.begin + i + kRecAhead].seq);
+            prefetch_str(b[c.begin + i + kRecAhead].seq);
+        }
         c.r1[i] = take(a[c.begin + i]);
         c.r2[i] = take(b[c.begin + i]);
         tot += c.r1[i]->seq.size() + c.r2[i]->seq.size();
@@ -353,7 +371,13 @@ void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistributio
     out.clear();
     out.reserve(7 * (size_t)mc.mparams.r * c.r1.size());
     Sam sam(out, mc.refs, mc.mparams.cigar_eqx, rg_id, mc.mparams.output_unmapped, mc.mparams.details);
-    for (size_t i = 0; i < c.r1.size(); ++i) {
+    static const bool pf = !(getenv("RSA_PREFETCH") && atoi(getenv("RSA_PREFETCH")) == 0);
+    const size_t n = c.r1.size();
+    for (size_t i = 0; i < n; ++i) {
+        if (pf && i + kRecAhead < n) {
+            prefetch_record(*c.r1[i + kRecAhead]);
+            prefetch_record(*c.r2[i + kRecAhead]);
+        }
         const Read read1(c.r1[i]->seq, c.rc(i, 0)), read2(c.r2[i]->seq, c.rc(i, 1));
         align_PE_read_last(c.res[i], *c.r1[i], *c.r2[i], read1, read2, sam, c.stats, isize, mc, c.rng);
     }
@@ -691,6 +715,7 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
             out.reserve(7 * (size_t)mc.mparams.r * (e - b));
             Sam sam(out, mc.refs, mc.mparams.cigar_eqx, opt.rg_id, mc.mparams.output_unmapped, mc.mparams.details);
             for (size_t i = b; i < e; ++i) {
+                if (i + kRecAhead < e) prefetch_record(recs[i + kRecAhead]);
                 const Read read(recs[i].seq, rcs[i - b]);
                 align_SE_read_last(res[i - b], recs[i], read, sam, st, mc, rng);
             }
