@@ -186,6 +186,18 @@ static inline void prefetch_record(const Record& r) {
     prefetch_str(r.seq);
     prefetch_str(r.qual);
 }
+template <class T>
+static inline void prefetch_vec(const std::vector<T>& v) {
+    const char* p = (const char*)v.data();
+    const size_t n = std::min<size_t>(v.size() * sizeof(T), 1024);
+    for (size_t o = 0; o < n; o += 64) __builtin_prefetch(p + o);
+}
+// a pair's alignments and NAM lists, written by part() and extend, read back when stored
+static inline void prefetch_res(const AlignTmpRes& r) {
+    prefetch_vec(r.align_res);
+    prefetch_vec(r.todo_nams);
+    prefetch_vec(r.type4_nams);
+}
 
 void pe_load(PeChunk& c, const std::vector<Record>& a, const std::vector<Record>& b, size_t idx, size_t chunk) {
     c.index = idx;
@@ -364,19 +376,21 @@ void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistributio
                    std::vector<AlignmentInfo>& infos, const std::string& rg_id, std::string& out) {
     const auto t = Clock::now();
     size_t pos = 0;
-    for (size_t i = 0; i < c.r1.size(); ++i) {
+    const size_t n = c.r1.size();
+    static const bool pf = !(getenv("RSA_PREFETCH") && atoi(getenv("RSA_PREFETCH")) == 0);
+    for (size_t i = 0; i < n; ++i) {
+        if (pf && i + kRecAhead < n) prefetch_res(c.res[i + kRecAhead]);
         const Read read1(c.r1[i]->seq, c.rc(i, 0)), read2(c.r2[i]->seq, c.rc(i, 1));
         pos = store_results_pe(c.res[i], read1, read2, mc, isize.mu, isize.sigma, infos, pos);
     }
     out.clear();
     out.reserve(7 * (size_t)mc.mparams.r * c.r1.size());
     Sam sam(out, mc.refs, mc.mparams.cigar_eqx, rg_id, mc.mparams.output_unmapped, mc.mparams.details);
-    static const bool pf = !(getenv("RSA_PREFETCH") && atoi(getenv("RSA_PREFETCH")) == 0);
-    const size_t n = c.r1.size();
     for (size_t i = 0; i < n; ++i) {
         if (pf && i + kRecAhead < n) {
             prefetch_record(*c.r1[i + kRecAhead]);
             prefetch_record(*c.r2[i + kRecAhead]);
+            prefetch_res(c.res[i + kRecAhead]);
         }
         const Read read1(c.r1[i]->seq, c.rc(i, 0)), read2(c.r2[i]->seq, c.rc(i, 1));
         align_PE_read_last(c.res[i], *c.r1[i], *c.r2[i], read1, read2, sam, c.stats, isize, mc, c.rng);

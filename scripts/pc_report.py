@@ -32,9 +32,20 @@ def symbolise(maps, pcs):
                 sym[pc] = f"[{os.path.basename(name)}]"
             continue
         offs = sorted(set(o for _, o in v))
-        out = subprocess.run(["addr2line", "-f", "-C", "-e", lib] + [hex(o) for o in offs], capture_output=True,
-                             text=True).stdout.split("\n")
-        by_off = {o: out[2 * i] for i, o in enumerate(offs)}
+        # -i: the inline chain of each address; OUTER=1 reports its outermost
+        # (really called) function instead of the innermost inlined one
+        out = subprocess.run(["addr2line", "-a", "-i", "-f", "-C", "-e", lib] + [hex(o) for o in offs],
+                             capture_output=True, text=True).stdout.split("\n")
+        chains, cur = [], None
+        for ln in out:
+            if ln.startswith("0x"):
+                cur = []
+                chains.append(cur)
+            elif cur is not None and ln and not (":" in ln and ln.split(":")[-1].split(" ")[0].isdigit()) \
+                    and not ln.startswith("??:"):
+                cur.append(ln)
+        outer = os.environ.get("OUTER") == "1"
+        by_off = {o: ((c[-1] if outer else c[0]) if c else "??") for o, c in zip(offs, chains)}
         for pc, o in v:
             sym[pc] = f"{by_off.get(o, '??')[:100]} [{os.path.basename(name)}]"
     return sym, bylib
