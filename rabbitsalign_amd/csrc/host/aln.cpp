@@ -111,6 +111,22 @@ void InsertSizeDistribution::update(int dist) {      // aln.cpp:1880-1903
 template <typename T>
 static bool by_score(const T& a, const T& b) { return a.score > b.score; }
 
+// std::sort(by_score) of a read's NAM list, the same permutation: libstdc++'s
+// std::sort of <= 16 elements is exactly its (stable) insertion sort, done here
+// with plain element moves instead of a memmove per shift; longer lists go to std::sort.
+static void sort_nams_by_score(std::vector<Nam>& v) {
+    const size_t n = v.size();
+    if (n > 16) { std::sort(v.begin(), v.end(), by_score<Nam>); return; }
+    Nam* a = v.data();
+    for (size_t i = 1; i < n; ++i) {
+        if (!(a[i].score > a[i - 1].score)) continue;
+        const Nam x = a[i];
+        size_t j = i;
+        do { a[j] = a[j - 1]; --j; } while (j > 0 && x.score > a[j - 1].score);
+        a[j] = x;
+    }
+}
+
 // ------------------------------------------------------------- NAM ops ---
 // aln.cpp:60-93
 static bool reverse_nam_if_needed(Nam& nam, const Read& read, const References& refs, int k) {
@@ -635,7 +651,7 @@ void align_PE_read_part(AlignTmpRes& res, const Record&, const Record&, const Re
     for (int m = 0; m < 2; ++m) {
         if (mc.mparams.rescue_level > 1 && rescued[m]) det[m].nam_rescue = true;
         det[m].nams = nams[m].size();
-        std::sort(nams[m].begin(), nams[m].end(), by_score<Nam>);
+        sort_nams_by_score(nams[m]);
         shuffle_top_nams(nams[m], rng);
     }
     align_PE_part(res, mc, nams[0], nams[1], read1, read2, mc.iparams.k, det, isize);
@@ -649,7 +665,7 @@ void align_SE_read_part(AlignTmpRes& res, const Record&, const Read& read, std::
     Details det;
     if (mc.mparams.rescue_level > 1 && rescued) det.nam_rescue = true;
     det.nams = nams.size();
-    std::sort(nams.begin(), nams.end(), by_score<Nam>);
+    sort_nams_by_score(nams);
     shuffle_top_nams(nams, rng);
     if (nams.empty()) {
         res.type = 0;

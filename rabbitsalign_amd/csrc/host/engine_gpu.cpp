@@ -91,6 +91,10 @@ public:
         uint32_t* lens = sg.get<uint32_t>(Staging::RLEN, n);
         size_t pos = 0;
         for (size_t i = 0; i < n; ++i) {
+            if (i + 8 < n) {                       // scattered heap strings: request them ahead
+                const char* a = reads[i + 8]->data();
+                for (size_t o = 0; o < reads[i + 8]->size(); o += 64) __builtin_prefetch(a + o);
+            }
             offs[i] = pos;
             lens[i] = (uint32_t)reads[i]->size();
             memcpy(blob + pos, reads[i]->data(), reads[i]->size());
@@ -139,6 +143,10 @@ public:
         rsa_job* js = sg.get<rsa_job>(Staging::JOBS, n);
         size_t pos = 0;
         for (size_t i = 0; i < n; ++i) {
+            if (i + 8 < n) {
+                const char* a = jobs[i + 8].query.data();
+                for (size_t o = 0; o < jobs[i + 8].query.size(); o += 64) __builtin_prefetch(a + o);
+            }
             js[i].query_offset = pos;
             js[i].query_len = (uint32_t)jobs[i].query.size();
             js[i].ref_id = jobs[i].ref_id;

@@ -216,6 +216,11 @@ void pe_load(PeChunk& c, const std::vector<Record>& a, const std::vector<Record>
         return &c.owned.back();
     };
     size_t tot = 0;
+    for (size_t i = 0; i < n; ++i) tot += a[c.begin + i].seq.size() + b[c.begin + i].seq.size();
+    c.rcbuf.resize(tot);
+    c.rcoff.resize(2 * n);
+    size_t at = 0;
+    // one pass: the reverse complement is taken while the sequence is in cache
     for (size_t i = 0; i < n; ++i) {
         if (i + kRecAhead < n) {
             prefetch_str(a[c.begin + i + kRecAhead].seq);
@@ -223,12 +228,6 @@ void pe_load(PeChunk& c, const std::vector<Record>& a, const std::vector<Record>
         }
         c.r1[i] = take(a[c.begin + i]);
         c.r2[i] = take(b[c.begin + i]);
-        tot += c.r1[i]->seq.size() + c.r2[i]->seq.size();
-    }
-    c.rcbuf.resize(tot);
-    c.rcoff.resize(2 * n);
-    size_t at = 0;
-    for (size_t i = 0; i < n; ++i) {
         for (int m = 0; m < 2; ++m) {
             const std::string& sq = m ? c.r2[i]->seq : c.r1[i]->seq;
             c.rcoff[2 * i + m] = at;
