@@ -86,16 +86,32 @@ struct OrderedSink {
     size_t next = 0;
     uint64_t bytes = 0;
     SamDigest total;
-    // written chunks' buffers, kept at capacity for the next chunks: a fresh
-    // ~10 MB buffer per chunk is mmap'd memory the first write page-faults in
-    std::vector<std::string> spare;
+    // written chunks' buffers, kept at capacity for the next chunks (and the next
+    // mapping calls): a fresh ~10 MB buffer per chunk is memory the first write
+    // page-faults in
+    struct Spares {
+        std::mutex m;
+        std::vector<std::string> v;
+    };
+    static Spares& spares() {
+        static Spares* p = new Spares();     // never destroyed: no exit-time teardown
+        return *p;
+    }
     std::string take() {
         static const bool off = getenv("RSA_SAM_REUSE") && atoi(getenv("RSA_SAM_REUSE")) == 0;
-        std::lock_guard<std::mutex> g(m);
-        if (off || spare.empty()) return std::string();
-        std::string s = std::move(spare.back());
-        spare.pop_back();
+        Spares& sp = spares();
+        std::lock_guard<std::mutex> g(sp.m);
+        if (off || sp.v.empty()) return std::string();
+        std::string s = std::move(sp.v.back());
+        sp.v.pop_back();
         return s;
+    }
+    void give_back(std::string& s) {
+        Spares& sp = spares();
+        std::lock_guard<std::mutex> g(sp.m);
+        if (sp.v.size() >= 48) return;
+        s.clear();
+        sp.v.push_back(std::move(s));
     }
     void put(size_t idx, std::string&& s) {
         SamDigest d;
@@ -106,10 +122,7 @@ struct OrderedSink {
             bytes += it->second.first.size();
             total.append(it->second.second);
             if (sink) sink(user, it->second.first);
-            if (spare.size() < 48) {
-                it->second.first.clear();
-                spare.push_back(std::move(it->second.first));
-            }
+            give_back(it->second.first);
             pending.erase(it);
             next++;
         }
