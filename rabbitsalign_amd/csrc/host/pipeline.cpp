@@ -168,6 +168,35 @@ struct ChunkPool {
         c.reset();                              // over the cap: freed by this worker, outside the lock
     }
 };
+// A worker's SW job and result lists, kept at capacity across mapping calls
+// (each bench step is one call, with new worker threads) like the chunks.
+struct WorkerScratch {
+    std::vector<SwJob> jobs;
+    std::vector<AlignmentInfo> infos;
+};
+struct ScratchLease {
+    std::unique_ptr<WorkerScratch> s;
+    static std::mutex& mu() {
+        static std::mutex* m = new std::mutex();
+        return *m;
+    }
+    static std::vector<std::unique_ptr<WorkerScratch>>& pool() {
+        static auto* p = new std::vector<std::unique_ptr<WorkerScratch>>();   // never destroyed
+        return *p;
+    }
+    ScratchLease() {
+        {
+            std::lock_guard<std::mutex> g(mu());
+            if (!pool().empty()) { s = std::move(pool().back()); pool().pop_back(); }
+        }
+        if (!s) s.reset(new WorkerScratch());
+    }
+    ~ScratchLease() {
+        std::lock_guard<std::mutex> g(mu());
+        if (pool().size() < 64) pool().push_back(std::move(s));
+    }
+};
+
 ChunkPool& chunk_pool() {
     static ChunkPool* p = new ChunkPool();     // never destroyed: no exit-time teardown
     return *p;
@@ -532,8 +561,9 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
 
     auto worker = [&](bool leader) {
         if (g_worker_start_hook) g_worker_start_hook();
-        std::vector<SwJob> jobs;
-        std::vector<AlignmentInfo> infos;
+        ScratchLease scratch;
+        std::vector<SwJob>& jobs = scratch.s->jobs;
+        std::vector<AlignmentInfo>& infos = scratch.s->infos;
         AlignmentStatistics local;
         PhaseTimes lt;
         std::unique_ptr<SlotHold> hold(new SlotHold(slots));
@@ -694,8 +724,9 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
     slots.free = T;
     auto worker = [&]() {
         SlotHold hold(slots);
-        std::vector<SwJob> jobs;
-        std::vector<AlignmentInfo> infos;
+        ScratchLease scratch;
+        std::vector<SwJob>& jobs = scratch.s->jobs;
+        std::vector<AlignmentInfo>& infos = scratch.s->infos;
         AlignmentStatistics local;
         for (;;) {
             size_t idx = next.fetch_add(1);
