@@ -488,7 +488,8 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
     // result vectors stop allocating and no run ends by freeing them one by one
     auto recycle = [&](std::unique_ptr<PeChunk> c) { chunk_pool().put(std::move(c)); };
     // prefetch claims up to this many consecutive chunks per seeding call (RSA_SEED_BATCH,
-    // default 1: A/B on the bench, 1 -> 11.75/11.61, 4 -> 11.00/10.60 Mreads/s)
+    // default 1: A/B on the bench, 1 -> 11.75/11.61, 4 -> 11.00/10.60 Mreads/s; r26 code:
+    // 1 -> 15.5/16.5/13.8, 2 -> 13.8/12.9/15.2, profiles/r01_ab_seed_batch.jsonl)
     const size_t seed_batch = std::max<size_t>(1, getenv("RSA_SEED_BATCH") ? (size_t)atol(getenv("RSA_SEED_BATCH")) : 1);
     auto stage1_multi = [&](const std::vector<size_t>& idxs) {
         std::vector<std::unique_ptr<PeChunk>> cs;
