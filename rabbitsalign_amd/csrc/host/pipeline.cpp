@@ -68,13 +68,14 @@ struct Unslot {                   // the slot handed back for a blocking section
     ~Unslot() { if (on) s.acquire(); }
 };
 
-// extra workers beyond the compute slots (RSA_WAIT_WORKERS; default: half as
-// many as the slots when the engine offloads -- A/B on 16 cores: +0 9.0/8.8,
-// +8 9.4, +16 8.3 Mreads/s -- none for an engine computing in-thread)
+// extra workers beyond the compute slots (RSA_WAIT_WORKERS; default: three
+// quarters as many as the slots when the engine offloads -- A/B on 16 cores:
+// +0 9.0/8.8, +8 9.4, +16 8.3 Mreads/s; on the r26 code +4 14.4/14.8, +8
+// 15.7/15.5, +12 15.8/16.3 -- none for an engine computing in-thread)
 static int wait_workers(const Engine& eng, int threads) {
     const char* e = getenv("RSA_WAIT_WORKERS");
     if (e) return std::max(0, atoi(e));
-    return eng.offloads() ? threads / 2 : 0;
+    return eng.offloads() ? (3 * threads) / 4 : 0;
 }
 
 struct OrderedSink {
