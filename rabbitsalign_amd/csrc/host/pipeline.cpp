@@ -71,7 +71,8 @@ struct Unslot {                   // the slot handed back for a blocking section
 // extra workers beyond the compute slots (RSA_WAIT_WORKERS; default: three
 // quarters as many as the slots when the engine offloads -- A/B on 16 cores:
 // +0 9.0/8.8, +8 9.4, +16 8.3 Mreads/s; on the r26 code +4 14.4/14.8, +8
-// 15.7/15.5, +12 15.8/16.3 -- none for an engine computing in-thread)
+// 15.7/15.5, +12 15.8/16.3; r27: +12 17.2/17.6, +16 15.9/16.1, +20 15.9/15.7
+// -- none for an engine computing in-thread)
 static int wait_workers(const Engine& eng, int threads) {
     const char* e = getenv("RSA_WAIT_WORKERS");
     if (e) return std::max(0, atoi(e));

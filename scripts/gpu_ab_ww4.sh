@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 O=gpurun_out/${1:-abww4}
 mkdir -p $O
 for i in 1 2; do
-  for v in 8 4 12; do
+  for v in ${WW_LIST:-8 4 12}; do
     RSA_WAIT_WORKERS=$v timeout -k 10 300 python bench.py --no-cpu-baseline > $O/b_${v}_$i.json 2> $O/b_${v}_$i.err || exit $?
   done
 done
