@@ -220,7 +220,10 @@ static bool upper_already(const std::string& s) {
 // Each read's name, sequence and qualities are separate heap strings the
 // hardware prefetcher cannot follow: loading a chunk (sequences) and writing its
 // SAM records (all three, last touched at load) request them a few pairs ahead.
-constexpr size_t kRecAhead = 4;
+static size_t rec_ahead() {                 // RSA_PREFETCH_AHEAD, default 4 pairs
+    static const size_t d = getenv("RSA_PREFETCH_AHEAD") ? (size_t)std::max(1, atoi(getenv("RSA_PREFETCH_AHEAD"))) : 4;
+    return d;
+}
 static inline void prefetch_str(const std::string& s) {
     const char* p = s.data();
     for (size_t o = 0; o < s.size(); o += 64) __builtin_prefetch(p + o);
@@ -264,11 +267,12 @@ void pe_load(PeChunk& c, const std::vector<Record>& a, const std::vector<Record>
     c.rcbuf.resize(tot);
     c.rcoff.resize(2 * n);
     size_t at = 0;
+    const size_t ahead = rec_ahead();
     // one pass: the reverse complement is taken while the sequence is in cache
     for (size_t i = 0; i < n; ++i) {
-        if (i + kRecAhead < n) {
-            prefetch_str(a[c.begin + i + kRecAhead].seq);
-            prefetch_str(b[c.begin + i + kRecAhead].seq);
+        if (i + ahead < n) {
+            prefetch_str(a[c.begin + i + ahead].seq);
+            prefetch_str(b[c.begin + i + ahead].seq);
         }
         c.r1[i] = take(a[c.begin + i]);
         c.r2[i] = take(b[c.begin + i]);
@@ -421,8 +425,9 @@ void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistributio
     size_t pos = 0;
     const size_t n = c.r1.size();
     static const bool pf = !(getenv("RSA_PREFETCH") && atoi(getenv("RSA_PREFETCH")) == 0);
+    const size_t ahead = rec_ahead();
     for (size_t i = 0; i < n; ++i) {
-        if (pf && i + kRecAhead < n) prefetch_res(c.res[i + kRecAhead]);
+        if (pf && i + ahead < n) prefetch_res(c.res[i + ahead]);
         const Read read1(c.r1[i]->seq, c.rc(i, 0)), read2(c.r2[i]->seq, c.rc(i, 1));
         pos = store_results_pe(c.res[i], read1, read2, mc, isize.mu, isize.sigma, infos, pos);
     }
@@ -430,10 +435,10 @@ void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistributio
     out.reserve(7 * (size_t)mc.mparams.r * c.r1.size());
     Sam sam(out, mc.refs, mc.mparams.cigar_eqx, rg_id, mc.mparams.output_unmapped, mc.mparams.details);
     for (size_t i = 0; i < n; ++i) {
-        if (pf && i + kRecAhead < n) {
-            prefetch_record(*c.r1[i + kRecAhead]);
-            prefetch_record(*c.r2[i + kRecAhead]);
-            prefetch_res(c.res[i + kRecAhead]);
+        if (pf && i + ahead < n) {
+            prefetch_record(*c.r1[i + ahead]);
+            prefetch_record(*c.r2[i + ahead]);
+            prefetch_res(c.res[i + ahead]);
         }
         const Read read1(c.r1[i]->seq, c.rc(i, 0)), read2(c.r2[i]->seq, c.rc(i, 1));
         align_PE_read_last(c.res[i], *c.r1[i], *c.r2[i], read1, read2, sam, c.stats, isize, mc, c.rng);
@@ -775,7 +780,7 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
             out.reserve(7 * (size_t)mc.mparams.r * (e - b));
             Sam sam(out, mc.refs, mc.mparams.cigar_eqx, opt.rg_id, mc.mparams.output_unmapped, mc.mparams.details);
             for (size_t i = b; i < e; ++i) {
-                if (i + kRecAhead < e) prefetch_record(recs[i + kRecAhead]);
+                if (i + rec_ahead() < e) prefetch_record(recs[i + rec_ahead()]);
                 const Read read(recs[i].seq, rcs[i - b]);
                 align_SE_read_last(res[i - b], recs[i], read, sam, st, mc, rng);
             }
