@@ -68,6 +68,8 @@ typedef struct rsa_ctx rsa_ctx;
 /* Upload index + reference to `device` (replicated per GPU). NULL on error. */
 rsa_ctx* rsa_open(int device, const rsa_index_view* view, char* err, size_t err_len);
 void rsa_close(rsa_ctx* ctx);
+/* message of the CALLING THREAD's last failed call (valid until that thread's next
+ * failing call); concurrent calls on one context never see each other's messages */
 const char* rsa_last_error(rsa_ctx* ctx);
 /* bytes of HBM the context holds resident (index + reference) */
 uint64_t rsa_resident_bytes(const rsa_ctx* ctx);

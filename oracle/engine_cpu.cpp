@@ -2,6 +2,8 @@
 // aln.cpp/pc.cpp/sam.cpp) driven by the C restatement of the hot path
 // (rsa_oracle.c) instead of the GPU.  TEST INFRASTRUCTURE ONLY: it is the
 // parity reference for end-to-end SAM and bench.py's cpu_baseline leg.
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -57,6 +59,10 @@ public:
     }
     void extend(const std::vector<rsa::SwJob>& jobs, const rsa::AlignmentParameters& p,
                 std::vector<rsa::AlignmentInfo>& out) override {
+        // fault injection for the pipeline's error path (tests only): RSA_TEST_FAIL_EXTEND=N
+        // makes the N-th extend call throw, as a failed GPU call does in the product engine
+        static const long fail_at = getenv("RSA_TEST_FAIL_EXTEND") ? atol(getenv("RSA_TEST_FAIL_EXTEND")) : 0;
+        if (fail_at > 0 && ++calls_ == fail_at) throw std::runtime_error("injected extend failure");
         out.assign(jobs.size(), rsa::AlignmentInfo());
         std::vector<uint32_t> cig;
         for (size_t i = 0; i < jobs.size(); ++i) {
@@ -75,6 +81,7 @@ public:
     }
 private:
     const rsa::References& refs_;
+    std::atomic<long> calls_{0};
     ora_index ix_;
     ora_params p_;
 };

@@ -1037,3 +1037,73 @@ void ora_aligner_align_with(const char* query, int qlen, const char* ref, int rl
     memcpy(cigar, c.v, sizeof(uint32_t) * (size_t)c.n);
     free(conv); free(tq); free(tr); free(raw);
 }
+
+/* ---- per-NAM site checks ------------------------------ */
+
+/* revcomp_table + reverse_complement (revcomp.hpp:11-38): A->T, C->G, G->C,
+ * T/U->A (either case, upper-case result), anything else -> N. */
+void ora_reverse_complement(const char* s, int len, char* out) {
+    for (int i = 0; i < len; ++i) {
+        char o;
+        switch (s[len - 1 - i]) {
+            case 'A': case 'a': o = 'T'; break;
+            case 'C': case 'c': o = 'G'; break;
+            case 'G': case 'g': o = 'C'; break;
+            case 'T': case 't': case 'U': case 'u': o = 'A'; break;
+            default: o = 'N';
+        }
+        out[i] = o;
+    }
+}
+
+/* a.substr(pa, k) == b.substr(pb, k) (std::string semantics: the substring is
+ * cut at the end; a position past the end is treated as empty here -- the
+ * reference's substr would throw there, which valid NAM coordinates never reach) */
+static int sub_eq(const char* a, int64_t alen, int64_t pa, const char* b, int64_t blen, int64_t pb, int k) {
+    if (pa < 0 || pa > alen) pa = alen;
+    if (pb < 0 || pb > blen) pb = blen;
+    int64_t na = alen - pa < k ? alen - pa : k, nb = blen - pb < k ? blen - pb : k;
+    return na == nb && memcmp(a + pa, b + pb, (size_t)na) == 0;
+}
+
+/* reverse_nam_if_needed (aln.cpp:60-93) on a copy of the NAM, then
+ * extend_seed_part's ungapped test (aln.cpp:374-395): projected window
+ * [max(0, ref_start - query_start), min(ref_end + L - query_end, |contig|)),
+ * Hamming distance when it is read-length and the NAM consistent
+ * (hamming_distance, aligner.hpp:54-67), accepted when (float)hd / L < 0.05.
+ * Returns rsa_nam_site flags: orientation 0 (as is) / 1 (reversed) / 2
+ * (inconsistent), | 4 Hamming computed (*n_mm), | 8 accepted with the mismatch
+ * positions (query coordinates of the oriented read) in mm_pos[0 .. *n_mm). */
+int ora_nam_site(const ora_nam* nam, const char* read, const char* read_rc, int L, const char* contig, int64_t clen,
+                 int k, uint16_t* mm_pos, int* n_mm) {
+    int is_rc = nam->is_rc, qs = nam->query_start, qe = nam->query_end;
+    const int rs = nam->ref_start, re = nam->ref_end;
+    const char* seq = is_rc ? read_rc : read;
+    const char* seq_rc = is_rc ? read : read_rc;
+    int flags;
+    *n_mm = 0;
+    if (sub_eq(contig, clen, rs, seq, L, qs, k) && sub_eq(contig, clen, re - k, seq, L, qe - k, k)) {
+        flags = 0;
+    } else if (sub_eq(contig, clen, rs, seq_rc, L, L - qe, k) &&
+               sub_eq(contig, clen, re - k, seq_rc, L, L - qs - k, k)) {
+        const int t = qs;
+        flags = 1; is_rc = !is_rc; qs = L - qe; qe = L - t;
+    } else {
+        return 2;
+    }
+    const char* q = is_rc ? read_rc : read;
+    const int64_t ps = rs - qs > 0 ? rs - qs : 0;
+    const int64_t pe0 = (int64_t)re + L - qe;
+    const int64_t pe = pe0 < clen ? pe0 : clen;
+    if (pe - ps != L) return flags;
+    int hd = 0;
+    for (int i = 0; i < L; ++i) if (contig[ps + i] != q[i]) hd++;
+    flags |= 4;
+    *n_mm = hd;
+    if ((float)hd / (float)L < 0.05f) {
+        int m = 0;
+        for (int i = 0; i < L; ++i) if (contig[ps + i] != q[i]) mm_pos[m++] = (uint16_t)i;
+        flags |= 8;
+    }
+    return flags;
+}

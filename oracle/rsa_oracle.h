@@ -72,6 +72,14 @@ int ora_find_nams(const ora_index* idx, const ora_qrs* q, int nq, ora_nam* out, 
 int ora_find_nams_rescue(const ora_index* idx, const ora_qrs* q, int nq, unsigned rescue_cutoff,
                          ora_nam* out, int cap);
 
+/* reverse_complement (revcomp.hpp:11-38) */
+void ora_reverse_complement(const char* s, int len, char* out);
+/* reverse_nam_if_needed (aln.cpp:60-93) + extend_seed_part's Hamming test
+ * (aln.cpp:374-395) for one NAM; returns rsa_nam_site flags (rsa_gpu.h),
+ * mismatch positions into mm_pos[L] when accepted (flag 8) */
+int ora_nam_site(const ora_nam* nam, const char* read, const char* read_rc, int L, const char* contig, int64_t clen,
+                 int k, uint16_t* mm_pos, int* n_mm);
+
 /* ---- extension -------------------------------------------------------- */
 
 typedef struct ora_ssw_res {    /* s_align (ssw.h) fields used by the C++ wrapper */

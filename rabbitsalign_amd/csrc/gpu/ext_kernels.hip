@@ -41,75 +41,6 @@ struct PassOut {
     int tcol, trow;          // reverse: first column reaching terminate
 };
 
-// Variant 0: per-cell best tracking, literal SSW recurrence.
-template <int R, bool REV>
-__device__ PassOut sw_pass_v0(const uint8_t* __restrict__ qc, int nrow, const uint8_t* __restrict__ rc, int ncol,
-                           int qend, int rend, int match, int mismatch, int gO, int gE, int seg,
-                           int terminate, int lane) {
-    const int lanes_used = (nrow + R - 1) / R;
-    int E[R], Hc[R], qv[R];
-    bool ss[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        E[r] = 0;
-        Hc[r] = 0;
-        const int p = lane * R + r;
-        ss[r] = (p % seg) == 0;
-        qv[r] = p < nrow ? (int)qc[REV ? (qend - p) : p] : 7;  // padded rows never score a match
-    }
-    int F_out = 0, Fw_out = 0, H_last = 0, diag_top = 0;
-    int best = 0, bcol = INT_MAX, brow = INT_MAX;
-    int tcol = INT_MAX, trow = INT_MAX;
-    const int steps = ncol + lanes_used - 1;
-    for (int s = 0; s < steps; ++s) {
-        const int F_in = wave_shr1(F_out);
-        const int Fw_in = wave_shr1(Fw_out);
-        const int Hl_in = wave_shr1(H_last);
-        const int c = s - lane;
-        if (lane < lanes_used && c >= 0 && c < ncol) {
-            const int rcode = rc[REV ? (rend - c) : c];
-            int dg = diag_top, F = F_in, Fw = Fw_in;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                if (ss[r]) Fw = 0;
-                int hm = max(dg + subst(qv[r], rcode, match, mismatch), 0);
-                hm = max(hm, E[r]);
-                hm = max(hm, Fw);
-                const int h = max(hm, F);
-                dg = Hc[r];
-                Hc[r] = h;
-                const int ho = max(hm - gO, 0);
-                E[r] = max(E[r] - gE, ho);
-                Fw = max(Fw - gE, ho);
-                F = max(F - gE, max(h - gO, 0));
-                const int p = lane * R + r;
-                if (p < nrow) {
-                    if (!REV) {
-                        if (h > best) { best = h; bcol = c; brow = p; }
-                    } else {
-                        if (h > best) best = h;
-                        if (h == terminate && tcol == INT_MAX) { tcol = c; trow = p; }
-                    }
-                }
-            }
-            F_out = F;
-            Fw_out = Fw;
-            H_last = Hc[R - 1];
-        }
-        diag_top = Hl_in;
-        if (REV && (s & 7) == 7) {
-            const int m = wave_min_i32(tcol);
-            if (m != INT_MAX && s >= m + lanes_used - 1) break;
-        }
-        // forward byte pass: once the running max reaches the overflow bound
-        // the word pass recomputes everything, so the rest is moot (ssw.c:846-849)
-        if (!REV && terminate > 0 && (s & 7) == 7 && wave_max_i32(best) >= terminate) break;
-    }
-    PassOut o;
-    o.best = best; o.col = bcol; o.row = brow; o.tcol = tcol; o.trow = trow;
-    return o;
-}
-
 // One SSW pass over `ncol` reference columns with `nrow` query rows.
 // fwd: row p -> qc[p], column c -> rc[c]
 // rev: row p -> qc[qend - p], column c -> rc[rend - c]
@@ -310,17 +241,13 @@ __device__ FusedOut sw_fwd_fused_dispatch(const uint8_t* qc, int nrow, const uin
 
 // R = rows per lane; the kernel is instantiated per RMAX so its register
 // allocation (and occupancy) is that of the largest R it can take, not 16.
-template <bool REV, int RMAX, int V>
+template <bool REV, int RMAX>
 __device__ PassOut sw_pass_dispatch(const uint8_t* qc, int nrow, const uint8_t* rc, int ncol, int qend, int rend,
                                     int match, int mismatch, int gO, int gE, int seg, int terminate, int lane) {
     const int R = (nrow + 63) / 64;
 #define RSA_PASS(N)                                                                                              \
-    if constexpr (N <= RMAX) {                                                                                   \
-        if constexpr (V) return sw_pass<N, REV>(qc, nrow, rc, ncol, qend, rend, match, mismatch, gO, gE, seg,      \
-                                                terminate, lane);                                                \
-        else return sw_pass_v0<N, REV>(qc, nrow, rc, ncol, qend, rend, match, mismatch, gO, gE, seg, terminate,  \
-                                       lane);                                                                    \
-    }
+    if constexpr (N <= RMAX) return sw_pass<N, REV>(qc, nrow, rc, ncol, qend, rend, match, mismatch, gO, gE, seg, \
+                                                    terminate, lane);
     if (R <= 1) { RSA_PASS(1) }
     if (R == 2) { RSA_PASS(2) }
     if (R == 3) { RSA_PASS(3) }
@@ -334,7 +261,7 @@ __device__ PassOut sw_pass_dispatch(const uint8_t* qc, int nrow, const uint8_t* 
     return o;   // unreachable: the host picks RMAX >= R of every job
 }
 
-template <int RMAX, int V>
+template <int RMAX>
 __global__ void __launch_bounds__(64 * SCAN_WAVES)
 k_ext_scan(const ExtJobDev* __restrict__ jobs, int n_jobs, const int* __restrict__ idx, const char* __restrict__ qbuf,
            const char* __restrict__ ref, ScanRes* __restrict__ out, int match, int mismatch, int gO, int gE) {
@@ -373,19 +300,19 @@ k_ext_scan(const ExtJobDev* __restrict__ jobs, int n_jobs, const int* __restrict
     int word = 0;
     PassOut f;
     int score1;
-    if (V == 2 && fused_ok) {
+    if (fused_ok) {
         const FusedOut fo = sw_fwd_fused_dispatch<RMAX>(qc, qlen, rc, rlen, match, mismatch, gO, gE, lane);
         const int sb = wave_max_i32(fo.best[0]);
         word = sb + mismatch >= 255 ? 1 : 0;
         f.best = fo.best[word]; f.col = fo.col[word]; f.row = fo.row[word];
         score1 = word ? wave_max_i32(fo.best[1]) : sb;
     } else {
-        f = sw_pass_dispatch<false, RMAX, V>(qc, qlen, rc, rlen, 0, 0, match, mismatch, gO, gE, (qlen + 15) / 16,
+        f = sw_pass_dispatch<false, RMAX>(qc, qlen, rc, rlen, 0, 0, match, mismatch, gO, gE, (qlen + 15) / 16,
                                              255 - mismatch, lane);
         score1 = wave_max_i32(f.best);
         if (score1 + mismatch >= 255) {
             word = 1;
-            f = sw_pass_dispatch<false, RMAX, V>(qc, qlen, rc, rlen, 0, 0, match, mismatch, gO, gE, (qlen + 7) / 8, 0,
+            f = sw_pass_dispatch<false, RMAX>(qc, qlen, rc, rlen, 0, 0, match, mismatch, gO, gE, (qlen + 7) / 8, 0,
                                                  lane);
             score1 = wave_max_i32(f.best);
         }
@@ -404,7 +331,7 @@ k_ext_scan(const ExtJobDev* __restrict__ jobs, int n_jobs, const int* __restrict
         // reverse pass (ssw.c:877-893)
         const int nrow = read_end1 + 1, ncol = ref_end1 + 1;
         const int seg = word ? (nrow + 7) / 8 : (nrow + 15) / 16;
-        PassOut b = sw_pass_dispatch<true, RMAX, (V ? 1 : 0)>(qc, nrow, rc, ncol, read_end1, ref_end1, match, mismatch,
+        PassOut b = sw_pass_dispatch<true, RMAX>(qc, nrow, rc, ncol, read_end1, ref_end1, match, mismatch,
                                                              gO, gE, seg, score1, lane);
         const int tcol = wave_min_i32(b.tcol);
         if (tcol == INT_MAX) {
@@ -669,7 +596,7 @@ k_ext_band(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan,
     rsa_aln a;
     a.sw_score = 0; a.edit_distance = 0; a.ref_start = a.ref_end = a.query_start = a.query_end = 0;
     a.cigar_offset = jb.cig_off; a.cigar_len = 0; a.pad_ = 0;
-    if (sr.status == 1) {                       // ref > 2000 (aligner.cpp:119-125)
+    if (sr.status != 0) {                       // ref > 2000 (aligner.cpp:119-125)
         a.edit_distance = 100000; a.sw_score = -1000000;
         out[j] = a;
         return;
@@ -740,7 +667,7 @@ __device__ __forceinline__ int gshr(int v) {
     }
 }
 
-// lane z of the group receives lane z+1 (REG band: index z+2 held by lane z+1); the last lane receives 0
+// lane z of the group receives lane z+1 (band index z+2 is held by lane z+1); the last lane receives 0
 template <int G>
 __device__ __forceinline__ int gshl1z(int v) {
     if constexpr (G == 16) return __builtin_amdgcn_update_dpp(0, v, 0x101, 0xf, 0xf, false);
@@ -784,17 +711,16 @@ __device__ __forceinline__ void aln_sentinel(rsa_aln* out, int j, const ExtJobDe
 }
 
 // banded_sw + traceback + ext_finish of job j by a group of G lanes (z = lane in
-// group).  LDS: dir[DIRCAP], hb/eb[2G], qc[QCAP], rc[RCAP].  Returns false when
-// the job does not fit the group (nothing written).
-// REG = false: h_b / e_b in LDS (literal array semantics).  REG = true: lane z
-// keeps h_b[z+1] and e_b[z+1] in registers; the reads of h_b[e], e_b[e] and
-// h_b[e-1] become DPP shifts (index 0 and indices past the group are always
-// 0), so the row loop has no LDS round trip and no barrier.
-template <int G, int DIRCAP, int QCAP, int RCAP, bool REG>
+// group).  LDS: dir[DIRCAP], qc[QCAP], rc[RCAP].  Returns false when the job does
+// not fit the group (nothing written).  Lane z keeps the reference's h_b[z+1] and
+// e_b[z+1] in registers; its reads of h_b[e], e_b[e] and h_b[e-1] are DPP shifts
+// (index 0 and indices past the group are always 0), so the row loop has no LDS
+// round trip and no barrier.
+template <int G, int DIRCAP, int QCAP, int RCAP>
 __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr, const char* __restrict__ qbuf,
                            const char* __restrict__ ref, uint32_t* __restrict__ cig_pool,
                            uint32_t* __restrict__ raw_pool, rsa_aln* __restrict__ out, int match, int mismatch,
-                           int gO, int gE, int bonus, int8_t* dir, int* hb, int* eb, uint8_t* qc, uint8_t* rc) {
+                           int gO, int gE, int bonus, int8_t* dir, uint8_t* qc, uint8_t* rc) {
     const char* q = qbuf + jb.q_off;
     const char* r = ref + jb.r_off;
     const int rlen = (int)jb.rlen;
@@ -814,49 +740,33 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
         rc[x] = (uint8_t)((gj >= 0 && gj < rlen) ? ssw_code((unsigned char)r[gj]) : 4);
     }
     for (int x = z * 16; x < DIRCAP; x += G * 16) *(int4*)(dir + x) = make_int4(0, 0, 0, 0);
-    hb[z] = 0; hb[z + G] = 0; eb[z] = 0; eb[z + G] = 0;
     WSYNC();
 
     const int len = ref_l > read_l ? ref_l : read_l;
     int s2 = 1024, max_v = 0, width_d = 0;
     bool deferred = false;
-    int HB = 0, EB = 0;                              // REG: h_b[z+1], e_b[z+1]
+    int HB = 0, EB = 0;                              // h_b[z+1], e_b[z+1]
     do {
         const int width = bw * 2 + 3;
         width_d = bw * 2 + 1;
         if (width_d > G) { deferred = true; break; }
         while (width_d * read_l * 3 >= s2) s2 *= 2;
         if (s2 > DIRCAP) { deferred = true; break; }
-        if constexpr (REG) {
-            if (z + 1 >= 1 && z + 1 <= width - 2) HB = 0;
-        } else {
-            if (z >= 1 && z <= width - 2) hb[z] = 0;
-            WSYNC();
-        }
+        if (z + 1 >= 1 && z + 1 <= width - 2) HB = 0;
         int lmax = 0;
         for (int i = 0; i < read_l; ++i) {
             const int beg = max(0, i - bw), end = min(ref_l - 1, i + bw);
             const int edge = end + 1 < width - 1 ? end + 1 : width - 1;
             const int jj = beg + z;
             const bool on = jj <= end;
-            const int u = z + 1;
             const int sh = i - bw >= 1 ? 1 : 0;
-            int hb_e, eb_e, hb_d;
-            if constexpr (REG) {
-                if (z == edge - 1) { HB = 0; EB = 0; }
-                const int HBl = gshl1z<G>(HB), EBl = gshl1z<G>(EB), HBr = gshr1z<G>(HB);
-                hb_e = sh ? HBl : HB;
-                eb_e = sh ? EBl : EB;
-                hb_d = sh ? HB : HBr;
-            } else {
-                if (z == 0) { hb[0] = 0; eb[0] = 0; hb[edge] = 0; eb[edge] = 0; }
-                WSYNC();
-                const int e = u + sh;
-                hb_e = hb[e]; eb_e = eb[e]; hb_d = hb[e - 1];
-            }
+            if (z == edge - 1) { HB = 0; EB = 0; }
+            const int HBl = gshl1z<G>(HB), EBl = gshl1z<G>(EB), HBr = gshr1z<G>(HB);
+            const int hb_e = sh ? HBl : HB;
+            const int eb_e = sh ? EBl : EB;
+            const int hb_d = sh ? HB : HBr;
             const int qv = qc[i];
             const int rv = on ? rc[jj] : 4;
-            if constexpr (!REG) WSYNC();
             const int t1 = i == 0 ? -gO : hb_e - gO;
             const int t2 = i == 0 ? -gE : eb_e - gE;
             const int E = t1 > t2 ? t1 : t2;
@@ -878,14 +788,7 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
                 dl[0] = (int8_t)de; dl[1] = (int8_t)df; dl[2] = (int8_t)dh;
                 if (H > lmax) lmax = H;
             }
-            if constexpr (REG) {
-                if (on) { EB = E; HB = H; }
-            } else {
-                if (on) eb[u] = E;
-                WSYNC();
-                if (on) hb[u] = H;                   // h_b[1..u] = h_c[1..u]
-                WSYNC();
-            }
+            if (on) { EB = E; HB = H; }                  // h_b[1..u] = h_c[1..u]
         }
         lmax = gmax<G>(lmax);
         if (lmax > max_v) max_v = lmax;
@@ -934,15 +837,12 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
 #define B16_DIRCAP 4096
 #define B16_SEGCAP 320
 
-template <bool REG>
 __global__ void __launch_bounds__(64)
 k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan, int n_jobs,
              const char* __restrict__ qbuf, const char* __restrict__ ref, uint32_t* __restrict__ cig_pool,
              uint32_t* __restrict__ raw_pool, rsa_aln* __restrict__ out, int match, int mismatch, int gO, int gE,
              int bonus, int* __restrict__ queue, int* __restrict__ qcount) {
     __shared__ __attribute__((aligned(16))) int8_t s_dir[B16_GROUPS][B16_DIRCAP];
-    __shared__ int s_hb[B16_GROUPS][32];
-    __shared__ int s_eb[B16_GROUPS][32];
     __shared__ uint8_t s_qc[B16_GROUPS][B16_SEGCAP];
     __shared__ uint8_t s_rc[B16_GROUPS][B16_SEGCAP];
     const int lane = threadIdx.x & 63, g = lane >> 4, z = lane & 15;
@@ -958,9 +858,8 @@ k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
         if (z == 0) aln_sentinel(out, j, jb, -100000);
         return;
     }
-    const bool done = band_group<16, B16_DIRCAP, B16_SEGCAP, B16_SEGCAP, REG>(
-        j, z, jb, sr, qbuf, ref, cig_pool, raw_pool, out, match, mismatch, gO, gE, bonus, s_dir[g], s_hb[g],
-        s_eb[g], s_qc[g], s_rc[g]);
+    const bool done = band_group<16, B16_DIRCAP, B16_SEGCAP, B16_SEGCAP>(
+        j, z, jb, sr, qbuf, ref, cig_pool, raw_pool, out, match, mismatch, gO, gE, bonus, s_dir[g], s_qc[g], s_rc[g]);
     if (!done && z == 0) queue[atomicAdd(qcount, 1)] = j;
 }
 
@@ -968,7 +867,6 @@ k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
 #define B64_QCAP 1024
 #define B64_RCAP 2048
 
-template <bool REG>
 __global__ void __launch_bounds__(64)
 k_ext_band64(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan, const char* __restrict__ qbuf,
              const char* __restrict__ ref, uint32_t* __restrict__ cig_pool, uint32_t* __restrict__ raw_pool,
@@ -976,8 +874,6 @@ k_ext_band64(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
              const int* __restrict__ queue, const int* __restrict__ qcount, int* __restrict__ overflow,
              int* __restrict__ ocount) {
     __shared__ __attribute__((aligned(16))) int8_t s_dir[B64_DIRCAP];
-    __shared__ int s_hb[128];
-    __shared__ int s_eb[128];
     __shared__ uint8_t s_qc[B64_QCAP];
     __shared__ uint8_t s_rc[B64_RCAP];
     const int z = threadIdx.x & 63;
@@ -986,51 +882,19 @@ k_ext_band64(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
         const int j = queue[t];
         const ExtJobDev jb = jobs[j];
         const ScanRes sr = scan[j];
-        const bool done = band_group<64, B64_DIRCAP, B64_QCAP, B64_RCAP, REG>(
-            j, z, jb, sr, qbuf, ref, cig_pool, raw_pool, out, match, mismatch, gO, gE, bonus, s_dir, s_hb, s_eb,
-            s_qc, s_rc);
+        const bool done = band_group<64, B64_DIRCAP, B64_QCAP, B64_RCAP>(
+            j, z, jb, sr, qbuf, ref, cig_pool, raw_pool, out, match, mismatch, gO, gE, bonus, s_dir, s_qc, s_rc);
         if (!done && z == 0) { overflow[j] = 1; atomicAdd(ocount, 1); }
         WSYNC();
     }
 }
 
 // ---------------------------------------------------------------------------
-// k_cigar_compact: one workgroup packs every job's CIGAR (written into its
-// qlen+rlen+8 slot) back to back and rewrites cigar_offset, so the host copies
-// only the ops that exist.  count[0] receives the total.
+// CIGAR compaction: every job's CIGAR is written into its qlen+rlen+8 slot; these
+// kernels pack them back to back and rewrite cigar_offset, so the host copies only
+// the ops that exist.  Per-block totals, a scan of the block totals, then every
+// block lays its jobs' ops out with a flat, coalesced copy.
 // ---------------------------------------------------------------------------
-#define CC_THREADS 1024
-__global__ void __launch_bounds__(CC_THREADS)
-k_cigar_compact(rsa_aln* __restrict__ alns, int n_jobs, const uint32_t* __restrict__ slots,
-                uint32_t* __restrict__ dense, uint64_t* __restrict__ total) {
-    __shared__ uint64_t s_sum[CC_THREADS];
-    const int t = threadIdx.x;
-    const int per = (n_jobs + CC_THREADS - 1) / CC_THREADS;
-    const int a = min(n_jobs, t * per), b = min(n_jobs, a + per);
-    uint64_t mine = 0;
-    for (int i = a; i < b; ++i) mine += alns[i].cigar_len;
-    s_sum[t] = mine;
-    __syncthreads();
-    for (int o = 1; o < CC_THREADS; o <<= 1) {       // inclusive Hillis-Steele scan
-        const uint64_t v = t >= o ? s_sum[t - o] : 0;
-        __syncthreads();
-        s_sum[t] += v;
-        __syncthreads();
-    }
-    uint64_t off = s_sum[t] - mine;
-    for (int i = a; i < b; ++i) {
-        const uint32_t n = alns[i].cigar_len;
-        const uint32_t* src = slots + alns[i].cigar_offset;
-        for (uint32_t k = 0; k < n; ++k) dense[off + k] = src[k];
-        alns[i].cigar_offset = off;
-        off += n;
-    }
-    if (t == CC_THREADS - 1) *total = s_sum[t];
-}
-
-// Multi-block CIGAR compaction (replaces the single-workgroup k_cigar_compact on
-// the default path): per-block totals, a scan of the block totals, then every
-// block lays its jobs' ops out back to back with a flat, coalesced copy.
 #define CCP_THREADS 256
 __device__ __forceinline__ uint64_t block_incl_scan(uint64_t v, uint64_t* s) {
     const int t = threadIdx.x;
@@ -1113,41 +977,24 @@ void launch_cigar_compact(hipStream_t st, rsa_aln* alns, int n_jobs, const uint3
     hipLaunchKernelGGL(k_cig_copy, dim3(nb), dim3(CCP_THREADS), 0, st, alns, n_jobs, bsum, slots, dense);
 }
 
-// host-side launcher: RMAX from the longest query of the batch, V = cell
-// bookkeeping variant (0: per cell, 1: per column)
-void launch_ext_scan(int rmax, int variant, dim3 grid, dim3 block, hipStream_t st, const ExtJobDev* jobs, int n,
-                     const int* idx, const char* q, const char* ref, ScanRes* out, int match, int mismatch, int gO,
-                     int gE) {
-#define RSA_L(RM, VV) hipLaunchKernelGGL((k_ext_scan<RM, VV>), grid, block, 0, st, jobs, n, idx, q, ref, out, match, mismatch, gO, gE)
-    if (variant == 2) {
-        if (rmax <= 2) RSA_L(2, 2); else if (rmax <= 4) RSA_L(4, 2); else if (rmax <= 8) RSA_L(8, 2); else RSA_L(16, 2);
-    } else if (variant) {
-        if (rmax <= 2) RSA_L(2, 1); else if (rmax <= 4) RSA_L(4, 1); else if (rmax <= 8) RSA_L(8, 1); else RSA_L(16, 1);
-    } else {
-        if (rmax <= 2) RSA_L(2, 0); else if (rmax <= 4) RSA_L(4, 0); else if (rmax <= 8) RSA_L(8, 0); else RSA_L(16, 0);
-    }
+// host-side launcher: RMAX from the longest query of the batch
+void launch_ext_scan(int rmax, dim3 grid, dim3 block, hipStream_t st, const ExtJobDev* jobs, int n, const int* idx,
+                     const char* q, const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE) {
+#define RSA_L(RM) hipLaunchKernelGGL((k_ext_scan<RM>), grid, block, 0, st, jobs, n, idx, q, ref, out, match, mismatch, gO, gE)
+    if (rmax <= 2) RSA_L(2); else if (rmax <= 4) RSA_L(4); else if (rmax <= 8) RSA_L(8); else RSA_L(16);
 #undef RSA_L
 }
 
-void launch_ext_band16(bool reg, dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n,
-                       const char* q, const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match,
-                       int mismatch, int gO, int gE, int bonus, int* queue, int* qcount) {
-    if (reg)
-        hipLaunchKernelGGL(k_ext_band16<true>, grid, dim3(64), 0, st, jobs, scan, n, q, ref, cig, raw, out, match,
-                           mismatch, gO, gE, bonus, queue, qcount);
-    else
-        hipLaunchKernelGGL(k_ext_band16<false>, grid, dim3(64), 0, st, jobs, scan, n, q, ref, cig, raw, out, match,
-                           mismatch, gO, gE, bonus, queue, qcount);
+void launch_ext_band16(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n, const char* q,
+                       const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match, int mismatch, int gO,
+                       int gE, int bonus, int* queue, int* qcount) {
+    hipLaunchKernelGGL(k_ext_band16, grid, dim3(64), 0, st, jobs, scan, n, q, ref, cig, raw, out, match, mismatch, gO,
+                       gE, bonus, queue, qcount);
 }
 
-void launch_ext_band64(bool reg, dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan,
-                       const char* q, const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match,
-                       int mismatch, int gO, int gE, int bonus, const int* queue, const int* qcount, int* overflow,
-                       int* ocount) {
-    if (reg)
-        hipLaunchKernelGGL(k_ext_band64<true>, grid, dim3(64), 0, st, jobs, scan, q, ref, cig, raw, out, match,
-                           mismatch, gO, gE, bonus, queue, qcount, overflow, ocount);
-    else
-        hipLaunchKernelGGL(k_ext_band64<false>, grid, dim3(64), 0, st, jobs, scan, q, ref, cig, raw, out, match,
-                           mismatch, gO, gE, bonus, queue, qcount, overflow, ocount);
+void launch_ext_band64(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, const char* q,
+                       const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match, int mismatch, int gO,
+                       int gE, int bonus, const int* queue, const int* qcount, int* overflow, int* ocount) {
+    hipLaunchKernelGGL(k_ext_band64, grid, dim3(64), 0, st, jobs, scan, q, ref, cig, raw, out, match, mismatch, gO, gE,
+                       bonus, queue, qcount, overflow, ocount);
 }

@@ -360,6 +360,12 @@ struct rsa_index_build {
     int bits = 0;
 };
 
+// shape of a build, read before a context takes it over (nothing changes hands)
+void index_build_peek(const rsa_index_build* b, int* device, int* bits) {
+    *device = b->device;
+    *bits = b->bits;
+}
+
 // hands the device buffers of a build to a context (rsa_open_built) and frees the handle
 void index_build_release(rsa_index_build* b, int* device, char** ref, rsa_ref_randstrobe** rs, uint64_t** starts,
                          uint64_t* n, int* bits) {

@@ -21,9 +21,8 @@
 #include "rsa_seed.h"
 #include "rsa_timer.h"
 
-void launch_ext_scan(int rmax, int variant, dim3 grid, dim3 block, hipStream_t st, const ExtJobDev* jobs, int n,
-                     const int* idx, const char* q, const char* ref, ScanRes* out, int match, int mismatch, int gO,
-                     int gE);
+void launch_ext_scan(int rmax, dim3 grid, dim3 block, hipStream_t st, const ExtJobDev* jobs, int n, const int* idx,
+                     const char* q, const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE);
 int scan_g_rows(uint32_t qlen);
 int scan_g_max_ref();
 void launch_ext_scan_g(int rows, bool mask, int n, hipStream_t st, const ExtJobDev* jobs, const int* order,
@@ -32,17 +31,16 @@ __global__ void k_ext_band(const ExtJobDev* jobs, const ScanRes* scan, int n_job
                            const char* qbuf, const char* ref, uint32_t* cig_pool, rsa_aln* out, uint8_t* scratch,
                            int64_t scr_stride, int arr_cap, int64_t dir_cap, int match, int mismatch, int gO,
                            int gE, int bonus, int* overflow, int over_code);
-void launch_ext_band16(bool reg, dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n,
-                       const char* q, const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match,
-                       int mismatch, int gO, int gE, int bonus, int* queue, int* qcount);
-void launch_ext_band64(bool reg, dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan,
-                       const char* q, const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match,
-                       int mismatch, int gO, int gE, int bonus, const int* queue, const int* qcount, int* overflow,
-                       int* ocount);
-__global__ void k_cigar_compact(rsa_aln* alns, int n_jobs, const uint32_t* slots, uint32_t* dense, uint64_t* total);
+void launch_ext_band16(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n, const char* q,
+                       const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match, int mismatch, int gO,
+                       int gE, int bonus, int* queue, int* qcount);
+void launch_ext_band64(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, const char* q,
+                       const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match, int mismatch, int gO,
+                       int gE, int bonus, const int* queue, const int* qcount, int* overflow, int* ocount);
 void launch_cigar_compact(hipStream_t st, rsa_aln* alns, int n_jobs, const uint32_t* slots, uint32_t* dense,
                           uint64_t* bsum, uint64_t* total);
 
+void index_build_peek(const rsa_index_build* b, int* device, int* bits);
 void index_build_release(rsa_index_build* b, int* device, char** ref, rsa_ref_randstrobe** rs, uint64_t** starts,
                          uint64_t* n, int* bits);
 
@@ -131,7 +129,12 @@ struct rsa_ctx {
     rsa_kernel_stats stats{};
 };
 
+// the message of the calling thread's last failed call: concurrent calls on one
+// context (the host pipeline's workers) never see each other's messages
+static thread_local std::string t_err;
+
 static void set_err(rsa_ctx* ctx, const std::string& s) {
+    t_err = s;
     if (!ctx) return;
     std::lock_guard<std::mutex> g(ctx->err_m);
     ctx->err = s;
@@ -244,25 +247,25 @@ rsa_ctx* rsa_open_built(rsa_index_build* b, const rsa_index_view* v, char* errbu
         return nullptr;
     };
     if (!b || !v || !v->contig_offsets) return fail("rsa_open_built: null build or view");
-    rsa_ctx* ctx = new rsa_ctx();
-    ctx->contig_off.assign(v->contig_offsets, v->contig_offsets + v->n_contigs + 1);
-    ctx->ref_bytes = ctx->contig_off.back();
-    int bits = 0;
-    index_build_release(b, &ctx->device, &ctx->d_ref, &ctx->d_rs, &ctx->d_starts, &ctx->n_rs, &bits);
-    if (bits != v->bits) {
-        std::string s = "rsa_open_built: view bits differ from the build's";
-        rsa_close(ctx);
-        return fail(s);
-    }
-    hipError_t e = hipSetDevice(ctx->device);
-    if (e == hipSuccess) e = hipMalloc(&ctx->d_coff, sizeof(uint64_t) * ctx->contig_off.size());
-    if (e == hipSuccess)
-        e = hipMemcpy(ctx->d_coff, ctx->contig_off.data(), sizeof(uint64_t) * ctx->contig_off.size(), hipMemcpyHostToDevice);
+    // everything that can fail happens before the build's buffers change hands:
+    // on error `b` stays valid and owned by the caller (rsa_gpu.h)
+    int dev = 0, bits = 0;
+    index_build_peek(b, &dev, &bits);
+    if (bits != v->bits) return fail("rsa_open_built: view bits differ from the build's");
+    std::vector<uint64_t> coff(v->contig_offsets, v->contig_offsets + v->n_contigs + 1);
+    uint64_t* d_coff = nullptr;
+    hipError_t e = hipSetDevice(dev);
+    if (e == hipSuccess) e = hipMalloc(&d_coff, sizeof(uint64_t) * coff.size());
+    if (e == hipSuccess) e = hipMemcpy(d_coff, coff.data(), sizeof(uint64_t) * coff.size(), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
-        std::string s = std::string("rsa_open_built: ") + hipGetErrorString(e);
-        rsa_close(ctx);
-        return fail(s);
+        if (d_coff) (void)hipFree(d_coff);
+        return fail(std::string("rsa_open_built: ") + hipGetErrorString(e));
     }
+    rsa_ctx* ctx = new rsa_ctx();
+    ctx->contig_off.swap(coff);
+    ctx->ref_bytes = ctx->contig_off.back();
+    ctx->d_coff = d_coff;
+    index_build_release(b, &ctx->device, &ctx->d_ref, &ctx->d_rs, &ctx->d_starts, &ctx->n_rs, &bits);
     ctx->ip.rs = ctx->d_rs;
     ctx->ip.starts = ctx->d_starts;
     ctx->ip.n = ctx->n_rs;
@@ -294,9 +297,9 @@ void rsa_close(rsa_ctx* ctx) {
     for (Lane* l : ctx->lanes) {
         if (l->stream) (void)hipStreamSynchronize(l->stream);
         for (DevBuf* b : {&l->d_q, &l->d_jobs, &l->d_scan, &l->d_alns, &l->d_alns2, &l->d_cig, &l->d_dense, &l->d_raw,
-                          &l->d_scratch, &l->d_over, &l->d_queue, &l->d_idx, &l->d_status})
+                          &l->d_scratch, &l->d_over, &l->d_queue, &l->d_idx, &l->d_status, &l->d_order, &l->d_bsum})
             b->release();
-        l->h_jobs.release(); l->h_over.release(); l->h_status.release();
+        l->h_jobs.release(); l->h_over.release(); l->h_status.release(); l->h_order.release();
         seed_bufs_release(l->sb);
         l->kt.destroy();
         if (l->stream) (void)hipStreamDestroy(l->stream);
@@ -309,7 +312,7 @@ void rsa_close(rsa_ctx* ctx) {
     delete ctx;
 }
 
-const char* rsa_last_error(rsa_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+const char* rsa_last_error(rsa_ctx* ctx) { return ctx ? t_err.c_str() : "null context"; }
 
 uint64_t rsa_resident_bytes(const rsa_ctx* ctx) { return ctx ? ctx->resident : 0; }
 
@@ -329,33 +332,6 @@ static const uint64_t DENSE_GUESS = 24;    // CIGAR ops per job copied before th
 static int64_t band_stride(int arr_cap, int64_t dir_cap) {
     int64_t s = (int64_t)arr_cap * 3 * 4 + dir_cap + (int64_t)RSA_RAW_CAP * 4;
     return (s + 255) & ~(int64_t)255;
-}
-
-// k_ext_scan variant (RSA_SCAN_V; same results): 0 per-cell bookkeeping, 1 per-column,
-// 2 (default) fused byte+word forward pass in packed int16 -- fastest on the headline
-// workload (profiles/r01_kab_r8.jsonl)
-static int scan_variant() {
-    const char* v = getenv("RSA_SCAN_V");
-    return v ? atoi(v) : 2;
-}
-
-// CIGAR compaction (RSA_COMPACT_V: 1 (default) multi-block scan + flat copy, 0 one workgroup)
-static int compact_variant() {
-    const char* v = getenv("RSA_COMPACT_V");
-    return v ? atoi(v) : 1;
-}
-
-// grouped scan (RSA_SCAN_G: 1 (default) 16 lanes per job, 4 jobs per wave, for
-// queries up to 256 bp; 0 = one job per wave for every job)
-static int scan_grouped() {
-    const char* v = getenv("RSA_SCAN_G");
-    return v ? atoi(v) : 1;
-}
-
-// band kernel variant (RSA_BAND_V: 0 LDS arrays, 1 (default) register arrays; same results)
-static int band_variant() {
-    const char* v = getenv("RSA_BAND_V");
-    return v ? atoi(v) : 1;
 }
 
 struct ExtStatus {            // device-side counters of one rsa_extend call
@@ -431,10 +407,9 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
     // packed-int16 parameters) go to it per rows-per-lane class, sorted by window
     // length (longest first) so the four jobs of a wave run about as long; the
     // rest -- and sentinels -- to the one-job-per-wave kernel via an index list.
-    const int variant = scan_variant();
     const bool packed_ok = jb->match >= 0 && jb->match <= 28 && jb->mismatch >= 0 && jb->mismatch < 4000 &&
                            jb->gap_open >= 0 && jb->gap_open < 4000 && jb->gap_extend >= 0 && jb->gap_extend < 4000;
-    const bool grouped = scan_grouped() && variant == 2 && packed_ok;
+    const bool grouped = packed_ok;
     constexpr int NCLS = 5;
     static const int cls_rows[NCLS] = {4, 7, 10, 13, 16};
     uint32_t cls_n[NCLS] = {0}, rest_n = 0;
@@ -489,7 +464,7 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
             off += cls_n[c];
         }
         if (rest_n) {
-            launch_ext_scan(rmax, variant, dim3((rest_n + 3) / 4), dim3(256), st, L->d_jobs.as<ExtJobDev>(),
+            launch_ext_scan(rmax, dim3((rest_n + 3) / 4), dim3(256), st, L->d_jobs.as<ExtJobDev>(),
                             (int)rest_n, d_ord + off, L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(),
                             jb->match, jb->mismatch, jb->gap_open, jb->gap_extend);
             HIPCHK(hipGetLastError());
@@ -498,15 +473,15 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
     L->kt.end(st);
     // 16 lanes per job for the common narrow bands; the rest queue for 64-lane waves
     L->kt.begin(st, RSA_K_EXT_BAND);
-    const bool band_reg = band_variant() != 0;
-    launch_ext_band16(band_reg, dim3((n + 3) / 4), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(), (int)n,
+    launch_ext_band16(dim3((n + 3) / 4), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(), (int)n,
                       L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(),
                       L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open, jb->gap_extend, jb->end_bonus,
                       L->d_queue.as<int>(), &dst->qcount);
     HIPCHK(hipGetLastError());
     L->kt.end(st);
     L->kt.begin(st, RSA_K_EXT_BAND_WIDE);
-    launch_ext_band64(band_reg, dim3(std::min<uint32_t>(n, BAND64_GRID)), st, L->d_jobs.as<ExtJobDev>(),
+    HIPCHK(hipMemsetAsync(L->d_over.p, 0, sizeof(int) * n, st));   // band64 writes only the 1s
+    launch_ext_band64(dim3(std::min<uint32_t>(n, BAND64_GRID)), st, L->d_jobs.as<ExtJobDev>(),
                       L->d_scan.as<ScanRes>(), L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(),
                       L->d_raw.as<uint32_t>(), L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open,
                       jb->gap_extend, jb->end_bonus, L->d_queue.as<int>(), &dst->qcount, L->d_over.as<int>(),
@@ -514,12 +489,8 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
     HIPCHK(hipGetLastError());
     L->kt.end(st);
     auto compact_and_copy = [&](uint64_t guess) -> int {
-        if (compact_variant())
-            launch_cigar_compact(st, L->d_alns.as<rsa_aln>(), (int)n, L->d_cig.as<uint32_t>(),
-                                 L->d_dense.as<uint32_t>(), L->d_bsum.as<uint64_t>(), &dst->total);
-        else
-            hipLaunchKernelGGL(k_cigar_compact, dim3(1), dim3(1024), 0, st, L->d_alns.as<rsa_aln>(), (int)n,
-                               L->d_cig.as<uint32_t>(), L->d_dense.as<uint32_t>(), &dst->total);
+        launch_cigar_compact(st, L->d_alns.as<rsa_aln>(), (int)n, L->d_cig.as<uint32_t>(), L->d_dense.as<uint32_t>(),
+                             L->d_bsum.as<uint64_t>(), &dst->total);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(L->h_status.p, L->d_status.p, sizeof(ExtStatus), hipMemcpyDeviceToHost, st));
         HIPCHK(hipMemcpyAsync(out->alns, L->d_alns.p, sizeof(rsa_aln) * n, hipMemcpyDeviceToHost, st));

@@ -171,17 +171,16 @@ __device__ int syncmers_lane(const char* __restrict__ s, int len, const SeedInde
     return n;
 }
 
-// one lane per read, `rpw` reads per wave (fewer reads per wave = more waves
-// in flight and less divergence per wave)
+// one lane per read: reads longer than RW_MAXLEN and seeding parameters the
+// wave kernel below does not take (list: the reads, NULL = all of them)
 template <int WC>
 __global__ void __launch_bounds__(64)
 k_randstrobes(const char* __restrict__ seq, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
-              const uint64_t* __restrict__ qbase, int n_reads, int rpw, SeedIndexParams p, SyncD* __restrict__ sync,
-              rsa_query_randstrobe* __restrict__ qrs, uint32_t* __restrict__ qcnt) {
-    const int lane = threadIdx.x & 63;
-    if (lane >= rpw) return;
-    const int r = blockIdx.x * rpw + lane;
-    if (r >= n_reads) return;
+              const uint64_t* __restrict__ qbase, int n_reads, const int* __restrict__ list, SeedIndexParams p,
+              SyncD* __restrict__ sync, rsa_query_randstrobe* __restrict__ qrs, uint32_t* __restrict__ qcnt) {
+    const int t = blockIdx.x * 64 + (threadIdx.x & 63);
+    if (t >= n_reads) return;
+    const int r = list ? list[t] : t;
     const int len = (int)rlen[r];
     const char* s = seq + roff[r];
     SyncD* sm = sync + qbase[r] / 2;
@@ -212,135 +211,55 @@ k_randstrobes(const char* __restrict__ seq, const uint64_t* __restrict__ roff, c
 }
 
 // ---------------------------------------------------------------------------
-// k_randstrobes_s: one lane per read, streaming.  The reference builds the
-// whole syncmer vector, then pairs (RandstrobeIterator, randstrobes.cpp:148-171)
-// forward and on the reversed vector (207-253).  Both pairings only look
-// w_max syncmers ahead (forward) or behind (reverse complement), so each
-// randstrobe is emitted as soon as its window is complete, from a 16-entry
-// per-lane ring in LDS -- no syncmer vector in global scratch.  Reverse
-// randstrobes are produced in descending order into the tail of the read's
-// output slot and moved into place once the syncmer count is known.
+// k_rs_wave: one wavefront per read (reads of up to RW_MAXLEN bases), every
+// step lane-parallel and LDS-resident -- no global scratch:
+//   1. the read is loaded coalesced (one base a lane) into two LDS bit arrays:
+//      2-bit base codes (ds_or) and an N mask (wave ballot);
+//   2. every s-mer ending at i: canonical value = min(fwd, rc) of the rolling
+//      registers of SyncmerIterator::next (randstrobes.cpp:57-118), extracted
+//      from the code array (rc = complemented codes, first base lowest; fwd = the
+//      2-bit groups reversed), xxh64 -> LDS;
+//   3. every k-mer ending at p without an N: the window of its k-s+1 s-mer
+//      hashes.  The iterator's tracked minimum always holds the window's
+//      minimum value, so when that value occurs once the syncmer test is
+//      stateless (argmin at offset t-1).  Only equal minima depend on history
+//      (first fill keeps the leftmost, a rescan the rightmost, an equal
+//      newcomer does not replace): a read with such a tie anywhere runs the
+//      reference's walk exactly, on lane 0, over the same LDS hashes.  Random
+//      reads never tie (equal 64-bit hashes need a repeated s-mer within k-s+1
+//      bases); low-complexity reads do.  Syncmer positions are compacted in
+//      order with a ballot prefix;
+//   4. lanes: canonical k-mer hash of every syncmer, then one randstrobe per
+//      lane (RandstrobeIterator::get, 148-171), forward then reverse complement
+//      (207-253), stored coalesced.
 // ---------------------------------------------------------------------------
-#define RSS_RING 32
+#define RW_WAVES 4
+#define RW_MAXLEN 512
+#define RW_WMAX 16            // window k - s + 1 the wave kernel takes
 
-template <int WC>
-__global__ void __launch_bounds__(64)
-k_randstrobes_s(const char* __restrict__ seq, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
-                const uint64_t* __restrict__ qbase, int n_reads, SeedIndexParams p,
-                rsa_query_randstrobe* __restrict__ qrs, uint32_t* __restrict__ qcnt) {
-    __shared__ uint64_t s_rh[RSS_RING][64];
-    __shared__ uint32_t s_rp[RSS_RING][64];
-    const int lane = threadIdx.x & 63;
-    const int r = blockIdx.x * 64 + lane;
-    if (r >= n_reads) return;
-    const int len = (int)rlen[r];
-    if (len < p.w_max) { qcnt[r] = 0; return; }     // randstrobes.cpp:209
-    const char* s = seq + roff[r];
-    rsa_query_randstrobe* out = qrs + qbase[r];
-    const int k = p.k, sl = p.s, t = p.t, wmin = p.w_min, wmax = p.w_max;
-    const uint64_t kmask = (k == 32) ? ~0ULL : ((1ULL << (2 * k)) - 1);
-    const uint64_t smask = (1ULL << (2 * sl)) - 1;
-    const int kshift = (k - 1) * 2, sshift = (sl - 1) * 2;
-    auto rh = [&](int x) -> uint64_t { return s_rh[x & (RSS_RING - 1)][lane]; };
-    auto rp = [&](int x) -> uint32_t { return s_rp[x & (RSS_RING - 1)][lane]; };
-    // forward randstrobe with strobe1 = syncmer i, window end w_end (rs_get)
-    auto fwd = [&](int i, int w_end) {
-        const uint64_t hi = rh(i);
-        const uint64_t max_position = (uint64_t)rp(i) + (unsigned)p.max_dist;
-        uint64_t min_val = END64;
-        int best = i;
-        for (int j = i + wmin; j <= w_end && rp(j) <= max_position; ++j) {
-            const uint64_t res = (uint64_t)__popcll((hi ^ rh(j)) & p.q);
-            if (res < min_val) { min_val = res; best = j; }
-        }
-        rsa_query_randstrobe o;
-        o.hash = hi + rh(best); o.start = rp(i); o.end = rp(best) + (uint32_t)k; o.is_reverse = 0; o.pad_ = 0;
-        out[i] = o;
-    };
-    // reverse-complement randstrobe whose strobe1 is syncmer x (reversed index n-1-x): the
-    // window runs over syncmers x-wmin down to max(x-wmax, 0), positions len - pos - k
-    auto rcs = [&](int x) {
-        auto pos = [&](int y) -> uint32_t { return (uint32_t)(len - (int)rp(y) - k); };
-        const uint64_t hi = rh(x);
-        const uint32_t pi = pos(x);
-        const uint64_t max_position = (uint64_t)pi + (unsigned)p.max_dist;
-        uint64_t min_val = END64;
-        int best = x;
-        const int lo = x - wmax > 0 ? x - wmax : 0;
-        for (int y = x - wmin; y >= lo && pos(y) <= max_position; --y) {
-            const uint64_t res = (uint64_t)__popcll((hi ^ rh(y)) & p.q);
-            if (res < min_val) { min_val = res; best = y; }
-        }
-        rsa_query_randstrobe o;
-        o.hash = hi + rh(best); o.start = pi; o.end = pos(best) + (uint32_t)k; o.is_reverse = 1; o.pad_ = 0;
-        out[2 * len - 1 - x] = o;                     // temporary slot, moved below
-    };
-    SmWindow<WC> win(k - sl + 1);
-    const int W = win.W;
-    uint64_t min_val = END64;
-    long long min_pos = -1;
-    int l = 0, n = 0;
-    uint64_t xk0 = 0, xk1 = 0, xs0 = 0, xs1 = 0;
-    for (int i = 0; i < len; ++i) {
-        const int c = nt4_code((unsigned char)s[i]);
-        if (c < 4) {
-            xk0 = ((xk0 << 2) | (uint64_t)c) & kmask;
-            xk1 = (xk1 >> 2) | ((uint64_t)(3 - c) << kshift);
-            xs0 = ((xs0 << 2) | (uint64_t)c) & smask;
-            xs1 = (xs1 >> 2) | ((uint64_t)(3 - c) << sshift);
-            if (++l < sl) continue;
-            const uint64_t hs = xxh64_u64(xs0 < xs1 ? xs0 : xs1);
-            const bool popped = win.push(hs);
-            if (!popped) {
-                if (win.qn < W) continue;
-                for (int j = 0; j < W; ++j) {
-                    const uint64_t v = win.at(j);
-                    if (v < min_val) { min_val = v; min_pos = (long long)i - k + j + 1; }
-                }
-            } else if (min_pos == (long long)i - k) {
-                min_val = END64;
-                min_pos = (long long)i - sl + 1;
-                for (int j = W - 1; j >= 0; --j) {
-                    const uint64_t v = win.at(j);
-                    if (v < min_val) { min_val = v; min_pos = (long long)i - k + j + 1; }
-                }
-            } else if (hs < min_val) {
-                min_val = hs;
-                min_pos = (long long)i - sl + 1;
-            }
-            if (min_pos == (long long)i - k + t) {
-                s_rh[n & (RSS_RING - 1)][lane] = xxh64_u64(xk0 < xk1 ? xk0 : xk1);
-                s_rp[n & (RSS_RING - 1)][lane] = (uint32_t)(i - k + 1);
-                if (n >= wmax) fwd(n - wmax, n);
-                if (n >= wmin) rcs(n);
-                n++;
-            }
-        } else {
-            min_val = END64; min_pos = -1;
-            l = 0; xs0 = xs1 = xk0 = xk1 = 0;
-            win.reset();
-        }
-    }
-    const int m = n > wmin ? n - wmin : 0;
-    for (int i = (n - wmax > 0 ? n - wmax : 0); i < m; ++i) fwd(i, n - 1);
-    // reverse randstrobe of syncmer x sits at 2len-1-x; its place is m + (n-1-x)
-    for (int tt = 0; tt < m; ++tt) out[m + tt] = out[2 * len - n + tt];
-    qcnt[r] = (uint32_t)(2 * m);
+// base codes [a, a + n) (first base in the low bits), n <= 32
+__device__ __forceinline__ uint64_t rw_bases(const uint32_t* w, int a, int n) {
+    const int wi = a >> 4, off = 2 * (a & 15);
+    uint64_t x = ((uint64_t)w[wi] | ((uint64_t)w[wi + 1] << 32)) >> off;
+    if (off) x |= (uint64_t)w[wi + 2] << (64 - off);
+    return n >= 32 ? x : (x & ((1ULL << (2 * n)) - 1));
 }
-
-// ---------------------------------------------------------------------------
-// k_randstrobes_w: one wavefront per read.
-//   1. lanes: base codes and every canonical s-mer hash (xxh64) -> LDS
-//   2. lane 0: the reference's stateful window-minimum walk over those hashes
-//      (first fill leftmost, rescan rightmost, strictly smaller replaces,
-//      N resets; randstrobes.cpp:57-118) -> syncmer positions
-//   3. lanes: canonical k-mer hash of every syncmer, then one randstrobe per
-//      lane (strobe1 = lane), forward and reverse-complement (148-171, 207-253)
-// Reads longer than RS_MAXLEN use the one-lane kernel above.
-// ---------------------------------------------------------------------------
-#define RS_WAVES 4
-#define RS_MAXLEN 512
-#define RS_RING 32
+// an N among bases [a, a + n), n <= 32
+__device__ __forceinline__ bool rw_has_n(const uint32_t* nm, int a, int n) {
+    const int wi = a >> 5, off = a & 31;
+    const uint64_t x = ((uint64_t)nm[wi] | ((uint64_t)nm[wi + 1] << 32)) >> off;
+    return (x & ((1ULL << n) - 1)) != 0;
+}
+// min(xk[0], xk[1]) of the n-mer whose codes X holds: xk[1] (complement, first
+// base lowest) is X ^ mask; xk[0] (first base highest) is X with its 2-bit groups reversed
+__device__ __forceinline__ uint64_t rw_canon(uint64_t X, int n) {
+    const uint64_t mask = n >= 32 ? ~0ULL : ((1ULL << (2 * n)) - 1);
+    const uint64_t rc = X ^ mask;
+    uint64_t r = __builtin_bitreverse64(X);
+    r = ((r >> 1) & 0x5555555555555555ULL) | ((r & 0x5555555555555555ULL) << 1);
+    const uint64_t fwd = r >> (64 - 2 * n);
+    return fwd < rc ? fwd : rc;
+}
 
 __device__ __forceinline__ void rs_pick(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sp, int n, int i,
                                         bool rc, int len, const SeedIndexParams& p, uint64_t& h, uint32_t& a,
@@ -363,108 +282,110 @@ __device__ __forceinline__ void rs_pick(const uint64_t* __restrict__ sh, const u
     b = pos(best);
 }
 
-__global__ void __launch_bounds__(64 * RS_WAVES)
-k_randstrobes_w(const char* __restrict__ seq, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
-                const uint64_t* __restrict__ qbase, int n_reads, SeedIndexParams p,
-                rsa_query_randstrobe* __restrict__ qrs, uint32_t* __restrict__ qcnt) {
-    __shared__ uint64_t s_hs[RS_WAVES][RS_MAXLEN];     // s-mer hash ending at i (valid: s_ok)
-    __shared__ uint64_t s_sh[RS_WAVES][RS_MAXLEN];     // syncmer k-mer hashes
-    __shared__ uint32_t s_sp[RS_WAVES][RS_MAXLEN];     // syncmer positions
-    __shared__ uint64_t s_ring[RS_WAVES][RS_RING];
-    __shared__ uint8_t s_c[RS_WAVES][RS_MAXLEN];
-    __shared__ int s_n[RS_WAVES];
+__global__ void __launch_bounds__(64 * RW_WAVES)
+k_rs_wave(const char* __restrict__ seq, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
+          const uint64_t* __restrict__ qbase, int n_reads, SeedIndexParams p, rsa_query_randstrobe* __restrict__ qrs,
+          uint32_t* __restrict__ qcnt) {
+    __shared__ uint32_t s_code[RW_WAVES][RW_MAXLEN / 16 + 4];
+    __shared__ uint32_t s_nm[RW_WAVES][RW_MAXLEN / 32 + 4];
+    __shared__ uint64_t s_h[RW_WAVES][RW_MAXLEN];       // s-mer hash by end position, then syncmer k-mer hashes
+    __shared__ uint32_t s_sp[RW_WAVES][RW_MAXLEN];      // syncmer positions
+    __shared__ int s_n[RW_WAVES];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int r = blockIdx.x * RS_WAVES + w;
-    if (r >= n_reads) return;                          // the whole wave leaves together
+    const int r = blockIdx.x * RW_WAVES + w;
+    if (r >= n_reads) return;                           // the whole wave leaves together
     const int len = (int)rlen[r];
+    if (len > RW_MAXLEN) return;                        // k_randstrobes takes it
     if (len < p.w_max) { if (lane == 0) qcnt[r] = 0; return; }   // randstrobes.cpp:209
     const char* sq = seq + roff[r];
-    uint8_t* c = s_c[w];
-    uint64_t* hs = s_hs[w];
-    const int k = p.k, sl = p.s;
-    for (int i = lane; i < len; i += 64) c[i] = (uint8_t)nt4_code((unsigned char)sq[i]);
+    uint32_t* cw = s_code[w];
+    uint32_t* nm = s_nm[w];
+    uint64_t* hs = s_h[w];
+    uint32_t* sp = s_sp[w];
+    const int k = p.k, sl = p.s, W = k - sl + 1;
+    // 1. codes and N mask
+    for (int i = lane; i < RW_MAXLEN / 16 + 4; i += 64) cw[i] = 0;
     WSYNC_SEED();
-    // 1. canonical s-mer hashes (fwd = bases MSB first, rc = complements LSB first)
+    for (int base = 0; base < len; base += 64) {
+        const int i = base + lane;
+        const int c = i < len ? nt4_code((unsigned char)sq[i]) : 4;
+        const uint64_t nb = __ballot(c >= 4);
+        if (c < 4) atomicOr(&cw[i >> 4], (uint32_t)c << (2 * (i & 15)));
+        if (lane == 0) { nm[base >> 5] = (uint32_t)nb; nm[(base >> 5) + 1] = (uint32_t)(nb >> 32); }
+    }
+    WSYNC_SEED();
+    // 2. s-mer hashes (only s-mers without an N are ever read)
     for (int i = sl - 1 + lane; i < len; i += 64) {
-        uint64_t f = 0, rv = 0;
-        bool ok = true;
-        for (int t = 0; t < sl; ++t) {
-            const int cc = c[i - sl + 1 + t];
-            ok &= cc < 4;
-            f = (f << 2) | (uint64_t)(cc & 3);
-            rv |= (uint64_t)(3 - (cc & 3)) << (2 * t);
-        }
-        hs[i] = ok ? xxh64_u64(f < rv ? f : rv) : 0;
+        const int a = i - sl + 1;
+        hs[i] = rw_has_n(nm, a, sl) ? 0 : xxh64_u64(rw_canon(rw_bases(cw, a, sl), sl));
     }
     WSYNC_SEED();
-    // 2. window-minimum walk (lane 0), SyncmerIterator::next
-    if (lane == 0) {
-        uint64_t* ring = s_ring[w];
-        uint32_t* sp = s_sp[w];
-        const int W = k - sl + 1;
-        int qn = 0, qhead = 0, l = 0, n = 0;
-        uint64_t min_val = END64;
-        long long min_pos = -1;
-        for (int i = 0; i < len; ++i) {
-            if (c[i] < 4) {
-                if (++l < sl) continue;
-                const uint64_t h = hs[i];
-                ring[(qhead + qn) & (RS_RING - 1)] = h;
-                qn++;
-                if (qn < W) continue;
-                if (qn == W) {
-                    for (int j = 0; j < qn; ++j) {
-                        const uint64_t v = ring[(qhead + j) & (RS_RING - 1)];
-                        if (v < min_val) { min_val = v; min_pos = (long long)i - k + j + 1; }
-                    }
-                } else {
-                    qhead = (qhead + 1) & (RS_RING - 1); qn--;
-                    if (min_pos == (long long)i - k) {
-                        min_val = END64;
-                        min_pos = (long long)i - sl + 1;
-                        for (int j = qn - 1; j >= 0; --j) {
-                            const uint64_t v = ring[(qhead + j) & (RS_RING - 1)];
-                            if (v < min_val) { min_val = v; min_pos = (long long)i - k + j + 1; }
-                        }
-                    } else if (h < min_val) {
-                        min_val = h;
-                        min_pos = (long long)i - sl + 1;
-                    }
-                }
-                if (min_pos == (long long)i - k + p.t) sp[n++] = (uint32_t)(i - k + 1);
-            } else {
-                min_val = END64; min_pos = -1;
-                l = 0; qn = 0; qhead = 0;
+    // 3. syncmer test per k-mer end p
+    int n = 0;
+    bool tie = false;
+    for (int base = 0; base < len; base += 64) {
+        const int pe = base + lane;
+        bool sync = false;
+        if (pe >= k - 1 && pe < len && !rw_has_n(nm, pe - k + 1, k)) {
+            const uint64_t* hw = hs + (pe - k + sl);      // window s-mers, by start offset 0..W-1
+            uint64_t mv = hw[0];
+            int mo = 0, cnt = 1;
+            for (int o = 1; o < W; ++o) {
+                const uint64_t v = hw[o];
+                if (v < mv) { mv = v; mo = o; cnt = 1; }
+                else if (v == mv) cnt++;
             }
+            tie |= cnt > 1;
+            sync = mo == p.t - 1;
         }
-        s_n[w] = n;
+        const uint64_t b = __ballot(sync);
+        if (sync) sp[n + __popcll(b & ((1ULL << lane) - 1))] = (uint32_t)(pe - k + 1);
+        n += __popcll(b);
     }
-    WSYNC_SEED();
-    const int n = s_n[w];
-    const uint32_t* sp = s_sp[w];
-    uint64_t* sh = s_sh[w];
-    // 3a. canonical k-mer hash of every syncmer
-    const uint64_t kmask = (k == 32) ? ~0ULL : ((1ULL << (2 * k)) - 1);
-    for (int x = lane; x < n; x += 64) {
-        const int p0 = (int)sp[x];
-        uint64_t f = 0, rv = 0;
-        for (int t = 0; t < k; ++t) {
-            const int cc = c[p0 + t] & 3;
-            f = (f << 2) | (uint64_t)cc;
-            rv |= (uint64_t)(3 - cc) << (2 * t);
+    if (__ballot(tie)) {                                // wave-uniform
+        WSYNC_SEED();
+        if (lane == 0) {
+            // SyncmerIterator::next exactly (randstrobes.cpp:57-118); the window of the
+            // k-mer ending at i is hs[i-W+1 .. i], all valid once l >= k
+            int l = 0, nn = 0;
+            uint64_t min_val = END64;
+            int min_pos = -1;
+            for (int i = 0; i < len; ++i) {
+                if ((nm[i >> 5] >> (i & 31)) & 1u) { l = 0; min_val = END64; min_pos = -1; continue; }
+                if (++l < sl) continue;
+                const int qn = l - sl + 1;
+                if (qn < W) continue;
+                const uint64_t* hw = hs + (i - W + 1);
+                if (qn == W) {                            // first fill: leftmost minimum
+                    for (int j = 0; j < W; ++j)
+                        if (hw[j] < min_val) { min_val = hw[j]; min_pos = i - k + j + 1; }
+                } else if (min_pos == i - k) {            // the minimum left: rescan, rightmost wins
+                    min_val = END64;
+                    min_pos = i - sl + 1;
+                    for (int j = W - 1; j >= 0; --j)
+                        if (hw[j] < min_val) { min_val = hw[j]; min_pos = i - k + j + 1; }
+                } else if (hw[W - 1] < min_val) {
+                    min_val = hw[W - 1];
+                    min_pos = i - sl + 1;
+                }
+                if (min_pos == i - k + p.t) sp[nn++] = (uint32_t)(i - k + 1);
+            }
+            s_n[w] = nn;
         }
-        f &= kmask;
-        sh[x] = xxh64_u64(f < rv ? f : rv);
+        WSYNC_SEED();
+        n = s_n[w];
     }
+    WSYNC_SEED();                                       // every read of the s-mer hashes is done
+    // 4a. syncmer k-mer hashes (into the s-mer hash array)
+    for (int x = lane; x < n; x += 64) hs[x] = xxh64_u64(rw_canon(rw_bases(cw, (int)sp[x], k), k));
     WSYNC_SEED();
-    // 3b. randstrobes, forward then reverse complement
+    // 4b. randstrobes, forward then reverse complement
     const int m = n > p.w_min ? n - p.w_min : 0;
     rsa_query_randstrobe* out = qrs + qbase[r];
     for (int x = lane; x < 2 * m; x += 64) {
         const bool rcx = x >= m;
-        const int i = rcx ? x - m : x;
         uint64_t h; uint32_t a, b;
-        rs_pick(sh, sp, n, i, rcx, len, p, h, a, b);
+        rs_pick(hs, sp, n, rcx ? x - m : x, rcx, len, p, h, a, b);
         rsa_query_randstrobe o;
         o.hash = h; o.start = a; o.end = b + (uint32_t)k; o.is_reverse = rcx ? 1 : 0; o.pad_ = 0;
         out[x] = o;
@@ -1029,25 +950,8 @@ k_find_nams(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restr
                    map_scratch + (size_t)t * map_stride(map_cap), map_cap, ncnt, nonrep, flags);
 }
 
-// one wavefront per read: the read's maps live in LDS (2 maps x 2 tables x
-// 256 slots), its sequential merge runs on lane 0.  A one-lane-per-read launch
-// of a 20000-read chunk fills 313 waves, i.e. a third of the SIMDs; one wave
-// per read fills the chip and turns every map access into an LDS access.
 #define FN_WAVES 4
 #define FN_MAP_CAP 256
-__global__ void __launch_bounds__(64 * FN_WAVES)
-k_find_nams_w(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi,
-              const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, const ReadStat* __restrict__ st,
-              const uint64_t* __restrict__ hoff, int n_reads, SeedIndexParams p, HitD* __restrict__ hits_buf,
-              rsa_nam* __restrict__ open_buf, rsa_nam* __restrict__ nam_buf, uint32_t* __restrict__ ncnt,
-              float* __restrict__ nonrep, uint32_t* __restrict__ flags) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_map[FN_WAVES][FN_MAP_CAP * 9 * 4];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int r = blockIdx.x * FN_WAVES + w;
-    if (r >= n_reads || lane != 0) return;
-    find_nams_read(r, qrs, qi, qcnt, qbase, st, hoff, p, hits_buf, open_buf, nam_buf, s_map[w], FN_MAP_CAP, ncnt,
-                   nonrep, flags);
-}
 
 // ---------------------------------------------------------------------------
 // k_find_nams_w2: one wavefront per read, everything in LDS (≈8.7 KB a read,
@@ -1565,10 +1469,10 @@ k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read,
 enum {
     B_SEQ, B_ROFF, B_RLEN, B_QBASE, B_QRS, B_QCNT, B_SYNC, B_QI, B_ST, B_HOFF, B_HITS, B_OPEN, B_NAM1, B_NCNT1,
     B_NONREP, B_FLAGS, B_MAP, B_ROFF2, B_NAM2, B_NCNT2, B_LIST, B_RBUF, B_OUT, B_OOFF, B_SLOTS, B_SITES, B_POOL,
-    B_PUSED, B_NREAD
+    B_PUSED, B_NREAD, B_RSLIST
 };
 // every host side of a transfer is page-locked: a pageable one would make the copy synchronous
-enum { H_ST, H_HOFF, H_FLAGS, H_CNT, H_ROFF, H_LIST, H_OOFF, H_CNT2, H_QBASE, H_NONREP, H_PUSED };
+enum { H_ST, H_HOFF, H_FLAGS, H_CNT, H_ROFF, H_LIST, H_OOFF, H_CNT2, H_QBASE, H_NONREP, H_PUSED, H_RSLIST };
 
 void seed_bufs_release(SeedBufs& b) {
     for (int i = 0; i < 32; ++i) if (b.p[i]) (void)hipFree(b.p[i]);
@@ -1611,21 +1515,6 @@ static hipError_t hens(SeedBufs& b, int i, size_t bytes) {
 
 static const uint32_t MAP_BIG = 65536 + 512;
 
-// A/B switches for kernel experiments: RSA_RS_WAVE=1 / RSA_FN_WAVE=1 select
-// the wave-per-read variants (same results, slower on the headline workload).
-static bool seed_variant_lane(const char* var) {
-    const char* v = getenv(var);
-    return v && v[0] == '1';
-}
-// reads per wave of the one-lane-per-read kernels (RSA_RPW_RS / RSA_RPW_FN).
-// Measured on the headline workload (profiles/r01_kab.jsonl): randstrobes is
-// fastest with 64 reads per wave, find_nams with 16 (divergent, latency-bound).
-static int seed_rpw(const char* var, int dflt) {
-    const char* v = getenv(var);
-    const int x = v ? atoi(v) : dflt;
-    return (x >= 1 && x <= 64) ? x : dflt;
-}
-
 // Stage 1 (shared by rsa_randstrobes and rsa_seed): upload reads, run k_randstrobes.
 int seed_stage_randstrobes(SeedBufs& b, hipStream_t st, const SeedIndexParams& p, const rsa_read_batch* rb,
                            std::vector<uint64_t>& qbase, std::string& err, KTimer* kt) {
@@ -1642,41 +1531,44 @@ int seed_stage_randstrobes(SeedBufs& b, hipStream_t st, const SeedIndexParams& p
     SCHK(dens(b, B_QBASE, 8ull * (n + 1)));
     SCHK(dens(b, B_QRS, sizeof(rsa_query_randstrobe) * (qbase[n] + 1)));
     SCHK(dens(b, B_QCNT, 4ull * n));
-    SCHK(dens(b, B_SYNC, sizeof(SyncD) * (qbase[n] / 2 + 1)));
     SCHK(hipMemcpyAsync(b.p[B_SEQ], rb->seq, total_len, hipMemcpyHostToDevice, st));
     SCHK(hipMemcpyAsync(b.p[B_ROFF], rb->offsets, 8ull * n, hipMemcpyHostToDevice, st));
     SCHK(hipMemcpyAsync(b.p[B_RLEN], rb->lengths, 4ull * n, hipMemcpyHostToDevice, st));
     SCHK(hens(b, H_QBASE, 8ull * (n + 1)));
     memcpy(b.h[H_QBASE], qbase.data(), 8ull * (n + 1));
     SCHK(hipMemcpyAsync(b.p[B_QBASE], b.h[H_QBASE], 8ull * (n + 1), hipMemcpyHostToDevice, st));
-    uint32_t max_len = 0;
-    for (uint32_t i = 0; i < n; ++i) max_len = std::max(max_len, rb->lengths[i]);
-    const bool wave = max_len <= RS_MAXLEN && p.k <= 32 && p.s <= 32 && p.k - p.s + 1 <= RS_RING &&
-                      seed_variant_lane("RSA_RS_WAVE");
+    // one wave per read (k_rs_wave); reads longer than RW_MAXLEN, and parameters
+    // outside its window / k-mer limits, one lane per read (k_randstrobes)
+    const bool wave_ok = p.k <= 32 && p.s <= 32 && p.s >= 1 && p.k - p.s + 1 <= RW_WMAX && p.k - p.s + 1 >= 1;
+    uint32_t n_long = 0;
+    for (uint32_t i = 0; i < n; ++i) n_long += rb->lengths[i] > RW_MAXLEN ? 1 : 0;
+    const int* lane_list = nullptr;
+    uint32_t n_lane = wave_ok ? n_long : n;
+    if (wave_ok && n_long) {
+        SCHK(hens(b, H_RSLIST, 4ull * n_long));
+        int* hl = HP(H_RSLIST, int);
+        uint32_t at = 0;
+        for (uint32_t i = 0; i < n; ++i) if (rb->lengths[i] > RW_MAXLEN) hl[at++] = (int)i;
+        SCHK(dens(b, B_RSLIST, 4ull * n_long));
+        SCHK(hipMemcpyAsync(b.p[B_RSLIST], hl, 4ull * n_long, hipMemcpyHostToDevice, st));
+        lane_list = DP(B_RSLIST, int);
+    }
     if (kt) kt->begin(st, RSA_K_RANDSTROBES);
-    const int rpw = seed_rpw("RSA_RPW_RS", 64);
-    // the streaming kernel measured slower than the scratch one (profiles/r01_kab_r8.jsonl): opt-in
-    const bool stream = p.w_max < RSS_RING && seed_variant_lane("RSA_RS_STREAM");
-    if (stream && p.k - p.s + 1 == 5)
-        hipLaunchKernelGGL(k_randstrobes_s<5>, dim3((n + 63) / 64), dim3(64), 0, st, DP(B_SEQ, char),
+    if (wave_ok)
+        hipLaunchKernelGGL(k_rs_wave, dim3((n + RW_WAVES - 1) / RW_WAVES), dim3(64 * RW_WAVES), 0, st, DP(B_SEQ, char),
                            DP(B_ROFF, uint64_t), DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n, p,
                            DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
-    else if (stream)
-        hipLaunchKernelGGL(k_randstrobes_s<0>, dim3((n + 63) / 64), dim3(64), 0, st, DP(B_SEQ, char),
-                           DP(B_ROFF, uint64_t), DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n, p,
-                           DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
-    else if (wave)
-        hipLaunchKernelGGL(k_randstrobes_w, dim3((n + RS_WAVES - 1) / RS_WAVES), dim3(64 * RS_WAVES), 0, st,
-                           DP(B_SEQ, char), DP(B_ROFF, uint64_t), DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n,
-                           p, DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
-    else if (p.k - p.s + 1 == 5)
-        hipLaunchKernelGGL(k_randstrobes<5>, dim3((n + rpw - 1) / rpw), dim3(64), 0, st, DP(B_SEQ, char),
-                           DP(B_ROFF, uint64_t), DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n, rpw, p,
-                           DP(B_SYNC, SyncD), DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
-    else
-        hipLaunchKernelGGL(k_randstrobes<0>, dim3((n + rpw - 1) / rpw), dim3(64), 0, st, DP(B_SEQ, char),
-                           DP(B_ROFF, uint64_t), DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n, rpw, p,
-                           DP(B_SYNC, SyncD), DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
+    if (n_lane) {
+        SCHK(dens(b, B_SYNC, sizeof(SyncD) * (qbase[n] / 2 + 1)));
+        if (p.k - p.s + 1 == 5)
+            hipLaunchKernelGGL(k_randstrobes<5>, dim3((n_lane + 63) / 64), dim3(64), 0, st, DP(B_SEQ, char),
+                               DP(B_ROFF, uint64_t), DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n_lane,
+                               lane_list, p, DP(B_SYNC, SyncD), DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
+        else
+            hipLaunchKernelGGL(k_randstrobes<0>, dim3((n_lane + 63) / 64), dim3(64), 0, st, DP(B_SEQ, char),
+                               DP(B_ROFF, uint64_t), DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n_lane,
+                               lane_list, p, DP(B_SYNC, SyncD), DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
+    }
     SCHK(hipGetLastError());
     if (kt) kt->end(st);
     return RSA_OK;
@@ -1750,26 +1642,9 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
     const uint32_t chunk = 65536;
     SCHK(hipMemcpyAsync(b.p[B_HOFF], hoff, 8ull * (n + 1), hipMemcpyHostToDevice, st));
     kt.begin(st, RSA_K_FIND_NAMS);
-    if (!seed_variant_lane("RSA_FN_LANE")) {
-        hipLaunchKernelGGL(k_find_nams_w2, dim3((n + FN2_WAVES - 1) / FN2_WAVES), dim3(64 * FN2_WAVES), 0, st,
-                           DP(B_ST, ReadStat), DP(B_SLOTS, HitD), DP(B_HOFF, uint64_t), (int)n, p,
-                           DP(B_NAM1, rsa_nam), DP(B_NCNT1, uint32_t), DP(B_NONREP, float), DP(B_FLAGS, uint32_t));
-    } else if (seed_variant_lane("RSA_FN_WAVE")) {
-        hipLaunchKernelGGL(k_find_nams_w, dim3((n + FN_WAVES - 1) / FN_WAVES), dim3(64 * FN_WAVES), 0, st,
-                           DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t),
-                           DP(B_QBASE, uint64_t), DP(B_ST, ReadStat), DP(B_HOFF, uint64_t), (int)n, p, DP(B_HITS, HitD),
-                           DP(B_OPEN, rsa_nam), DP(B_NAM1, rsa_nam), DP(B_NCNT1, uint32_t), DP(B_NONREP, float),
-                           DP(B_FLAGS, uint32_t));
-    } else {
-        const size_t small_stride = (size_t)FN_MAP_CAP * 9 * 4;
-        SCHK(dens(b, B_MAP, small_stride * n));
-        const int rpw = seed_rpw("RSA_RPW_FN", 16);
-        hipLaunchKernelGGL(k_find_nams, dim3((n + rpw - 1) / rpw), dim3(64), 0, st, DP(B_QRS, rsa_query_randstrobe),
-                           DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t), DP(B_QBASE, uint64_t), DP(B_ST, ReadStat),
-                           DP(B_HOFF, uint64_t), (int)n, (const int*)nullptr, p, DP(B_HITS, HitD), DP(B_OPEN, rsa_nam),
-                           DP(B_NAM1, rsa_nam), DP(B_MAP, uint8_t), FN_MAP_CAP, DP(B_NCNT1, uint32_t),
-                           DP(B_NONREP, float), DP(B_FLAGS, uint32_t), rpw);
-    }
+    hipLaunchKernelGGL(k_find_nams_w2, dim3((n + FN2_WAVES - 1) / FN2_WAVES), dim3(64 * FN2_WAVES), 0, st,
+                       DP(B_ST, ReadStat), DP(B_SLOTS, HitD), DP(B_HOFF, uint64_t), (int)n, p, DP(B_NAM1, rsa_nam),
+                       DP(B_NCNT1, uint32_t), DP(B_NONREP, float), DP(B_FLAGS, uint32_t));
     SCHK(hipGetLastError());
     kt.end(st);
     SCHK(hens(b, H_FLAGS, 4ull * n));

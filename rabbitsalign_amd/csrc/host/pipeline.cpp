@@ -730,13 +730,18 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
     const bool offl = eng.offloads();
     CpuSlots slots;
     slots.free = T;
+    std::exception_ptr failure;
+    std::atomic<bool> failed{false};
     auto worker = [&]() {
-        SlotHold hold(slots);
+        if (g_worker_start_hook) g_worker_start_hook();
+        std::unique_ptr<SlotHold> hold(new SlotHold(slots));
         ScratchLease scratch;
         std::vector<SwJob>& jobs = scratch.s->jobs;
         std::vector<AlignmentInfo>& infos = scratch.s->infos;
         AlignmentStatistics local;
+        try {
         for (;;) {
+            if (failed.load()) break;
             size_t idx = next.fetch_add(1);
             if (idx >= n_chunks) break;
             const size_t b = idx * chunk, e = std::min(recs.size(), b + chunk);
@@ -787,12 +792,22 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
             os.put(idx, std::move(out));
             local.add(st);
         }
+        } catch (...) {
+            // an engine error on any worker ends the run: the others stop at their next
+            // chunk and rsam_map / the CLI report it (an exception escaping a std::thread
+            // would terminate the process)
+            std::lock_guard<std::mutex> g(stat_m);
+            if (!failure) failure = std::current_exception();
+            failed = true;
+        }
+        hold.reset();
         std::lock_guard<std::mutex> g(stat_m);
         result.stats.add(local);
     };
     std::vector<std::thread> ws;
     for (int t = 0; t < T + wait_workers(eng, T); ++t) ws.emplace_back(worker);
     for (auto& w : ws) w.join();
+    if (failure) std::rethrow_exception(failure);
     result.map_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     result.sam_bytes = os.bytes;
     result.sam_digest = os.total;

@@ -148,6 +148,8 @@ def load(path: str = GPU_LIB):
                                         C.POINTER(IndexBuildInfo), C.c_char_p, C.c_size_t]
     lib.rsa_index_build_download.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     lib.rsa_index_build_free.argtypes = [C.c_void_p]
+    lib.rsa_open_built.restype = C.c_void_p
+    lib.rsa_open_built.argtypes = [C.c_void_p, C.POINTER(IndexView), C.c_char_p, C.c_size_t]
     _lib = lib
     return lib
 

@@ -57,6 +57,9 @@ def lib():
         L.ora_find_nams.argtypes = [C.POINTER(Index), C.c_void_p, C.c_int, C.c_void_p, C.c_int,
                                     C.POINTER(C.c_float)]
         L.ora_find_nams_rescue.argtypes = [C.POINTER(Index), C.c_void_p, C.c_int, C.c_uint, C.c_void_p, C.c_int]
+        L.ora_reverse_complement.argtypes = [C.c_char_p, C.c_int, C.c_char_p]
+        L.ora_nam_site.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int, C.c_char_p, C.c_int64, C.c_int,
+                                   C.c_void_p, C.POINTER(C.c_int)]
         _lib = L
     return _lib
 
@@ -124,3 +127,22 @@ class OracleIndex:
             nams = self.find_nams_rescue(q, rescue_cutoff)
             rescued = True
         return nams, np.float32(nonrep), rescued
+
+
+def reverse_complement(seq: bytes) -> bytes:
+    """revcomp.hpp:11-38"""
+    out = C.create_string_buffer(len(seq) + 1)
+    lib().ora_reverse_complement(seq, len(seq), out)
+    return out.raw[:len(seq)]
+
+
+def nam_site(nam, read: bytes, contig: bytes, k: int):
+    """reverse_nam_if_needed (aln.cpp:60-93) + extend_seed_part's Hamming test
+    (aln.cpp:374-395): (flags, n_mm, mismatch positions) as rsa_nam_site reports them."""
+    n = np.zeros(1, dtype=NAM_DTYPE)
+    n[0] = nam
+    pos = np.zeros(max(1, len(read)), dtype=np.uint16)
+    n_mm = C.c_int()
+    f = lib().ora_nam_site(n.ctypes.data, read, reverse_complement(read), len(read), contig, len(contig), k,
+                           pos.ctypes.data, C.byref(n_mm))
+    return int(f), int(n_mm.value), [int(x) for x in pos[:n_mm.value]] if f & 8 else []

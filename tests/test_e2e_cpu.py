@@ -30,3 +30,17 @@ def test_thread_and_chunk_invariance(data, chunk):
     for t in ("4", "8"):
         map_reads(CPU_PORT, fa, reads, str(d / f"t{t}.sam"), "-t", t, "--chunk-size", chunk)
         assert sam_body(d / "t1.sam") == sam_body(d / f"t{t}.sam")
+
+
+@pytest.mark.parametrize("se", [True, False])
+def test_engine_error_is_reported_not_aborted(tmp_path, se):
+    """An engine call that throws (a failed GPU call in the product engine) ends the
+    run with an error message and exit status 1, on the single-end path as on the
+    paired-end one -- never std::terminate (ADVICE r1: SE worker had no handler)."""
+    import subprocess
+    fa, reads = make_dataset(str(tmp_path), pairs=2000, ref_len=100_000, cpu_index=True, se=se)
+    env = dict(os.environ, RSA_TEST_FAIL_EXTEND="2")
+    r = subprocess.run([CPU_PORT, "--use-index", "-t", "4", "--chunk-size", "200", "-o", str(tmp_path / "x.sam"),
+                        fa, *reads], capture_output=True, text=True, env=env)
+    assert r.returncode == 1, (r.returncode, r.stderr[-500:])
+    assert "injected extend failure" in r.stderr

@@ -148,3 +148,41 @@ def test_gpu_index_medium_random(tmp_path):
     g = _index(fa, tmp_path / "g.sti", "-r", "150")
     c = _index(fa, tmp_path / "c.sti", "-r", "150", "--cpu-index")
     assert g == c
+
+
+@pytest.mark.gpu
+def test_open_built_failure_leaves_build_valid():
+    """rsa_open_built with a view whose bits differ from the build's fails and leaves
+    the build owned by the caller (rsa_gpu.h): it can still be downloaded and freed,
+    and a matching view then adopts it (the failure path freed it)."""
+    import ctypes as C
+    from rabbitsalign_amd import native
+    lib = native.load()
+    rng = np.random.default_rng(5)
+    ref = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, 200_000)].copy()
+    offs = np.array([0, 120_000, 200_000], dtype=np.uint64)
+    p = native.IndexBuildParams(20, 16, 3, 5, 11, 80, 255, -1, 0.0002)
+    info = native.IndexBuildInfo()
+    err = C.create_string_buffer(512)
+    h = lib.rsa_index_build_run(0, ref.ctypes.data, offs.ctypes.data, 2, C.byref(p), C.byref(info), err, 512)
+    assert h, err.value
+    v = native.IndexView()
+    v.bits = info.bits + 1
+    v.filter_cutoff = info.filter_cutoff
+    v.k, v.s, v.t_syncmer, v.w_min, v.w_max, v.max_dist, v.q = 20, 16, 3, 5, 11, 80, 255
+    v.contig_offsets = offs.ctypes.data
+    v.n_contigs = 2
+    assert not lib.rsa_open_built(h, C.byref(v), err, 512)
+    assert b"bits" in err.value
+    rs = np.zeros(info.n_randstrobes, dtype=native.RS_DTYPE)
+    st = np.zeros((1 << info.bits) + 1, dtype=np.uint64)
+    assert lib.rsa_index_build_download(h, rs.ctypes.data, st.ctypes.data) == 0
+    assert st[-1] == info.n_randstrobes and np.all(np.diff(rs["hash"].astype(np.float64)) >= 0)
+    v.bits = info.bits
+    ctx = lib.rsa_open_built(h, C.byref(v), err, 512)
+    assert ctx, err.value
+    back = np.zeros_like(rs)
+    lib.rsa_index_download.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    assert lib.rsa_index_download(ctx, back.ctypes.data, 0) == 0
+    assert back.tobytes() == rs.tobytes()
+    lib.rsa_close(ctx)

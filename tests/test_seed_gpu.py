@@ -71,59 +71,22 @@ def test_seed_batch_independent(setup):
         assert _nam_equal(x, y)
 
 
-_COMP = bytes.maketrans(b"ACGTUacgtu", b"TGCAATGCAA")
-
-
-def _revcomp(r):
-    out = bytes(c if c in b"ACGTUacgtu" else ord("N") for c in r).translate(_COMP)
-    return out[::-1]
-
-
-def _sub(s, pos, n):
-    if pos < 0 or pos > len(s):          # a negative int cast to size_t clamps to the end
-        pos = len(s)
-    return s[pos:pos + n]
-
-
-def _site_ref(nam, read, ref, coff, k):
-    """reverse_nam_if_needed (src/aln.cpp:60-93) then extend_seed_part's Hamming
-    test (aln.cpp:374-431), restated; returns (flags, n_mm, positions)."""
-    L = len(read)
-    rc = _revcomp(read)
-    contig = ref[int(coff[nam["ref_id"]]):int(coff[nam["ref_id"] + 1])]
-    is_rc, qs, qe, rs, re_ = bool(nam["is_rc"]), int(nam["query_start"]), int(nam["query_end"]), \
-        int(nam["ref_start"]), int(nam["ref_end"])
-    seq, seq_rc = (rc, read) if is_rc else (read, rc)
-    if _sub(contig, rs, k) == _sub(seq, qs, k) and _sub(contig, re_ - k, k) == _sub(seq, qe - k, k):
-        flags = 0
-    elif _sub(contig, rs, k) == _sub(seq_rc, L - qe, k) and _sub(contig, re_ - k, k) == _sub(seq_rc, L - qs - k, k):
-        flags, is_rc, qs, qe = 1, not is_rc, L - qe, L - qs
-    else:
-        return 2, 0, []
-    q = rc if is_rc else read
-    ps, pe = max(0, rs - qs), min(re_ + L - qe, len(contig))
-    if pe - ps != L:
-        return flags, 0, []
-    pos = [i for i in range(L) if contig[ps + i] != q[i]]
-    flags |= 4
-    if np.float32(len(pos)) / np.float32(L) < 0.05:
-        return flags | 8, len(pos), pos
-    return flags, len(pos), []
-
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("mm_capacity", [None, 8])
 def test_sites(setup, mm_capacity):
-    """k_sites against the restated host checks, for every NAM of
+    """k_sites against the oracle's ora_nam_site (reverse_nam_if_needed
+    aln.cpp:60-93 + extend_seed_part's Hamming test aln.cpp:374-395), for every NAM of
     every golden read; a tiny position pool must flag POOL_FULL instead of writing."""
     name, idx, ctx, ora = setup
     reads = _reads(name)
     ref = idx.ref_seq.tobytes()
+    coff = idx.contig_offsets
     nams, _, _, sites, pool = ctx.seed(reads, sites=True, mm_capacity=mm_capacity)
     n_pos = n_checked = 0
     for r, ns, ss in zip(reads, nams, sites):
         for nam, st in zip(ns, ss):
-            flags, n_mm, pos = _site_ref(nam, r, ref, idx.contig_offsets, idx.k)
+            c = int(nam["ref_id"])
+            flags, n_mm, pos = oracle_lib.nam_site(nam, r, ref[int(coff[c]):int(coff[c + 1])], idx.k)
             got = int(st["flags"])
             if got & 16:                       # pool full: positions withheld, everything else equal
                 assert flags & 8 and mm_capacity is not None
@@ -138,3 +101,57 @@ def test_sites(setup, mm_capacity):
                 assert int(st["n_mm"]) == n_mm
                 n_checked += 1
     assert n_checked > 0 and (n_pos > 0 or mm_capacity is not None)
+
+
+def _adversarial_reads(rng):
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+
+    def rnd(n):
+        return acgt[rng.integers(0, 4, n)].tobytes()
+
+    reads = [b"", b"A", rnd(10), rnd(149), rnd(150), rnd(250), rnd(511), rnd(512), rnd(513), rnd(1000),
+             b"A" * 150, b"AC" * 75, b"ACG" * 50, b"ACGT" * 40, b"AAAAC" * 30, b"N" * 150,
+             rnd(60) + b"N" + rnd(89), rnd(40) + b"NNNNN" + rnd(40) + b"A" * 30 + rnd(35),
+             rnd(150).lower(), rnd(70).replace(b"T", b"U") + rnd(80), rnd(100) + b"A" * 600,
+             (rnd(7) * 30)[:200], rnd(30) + b"CACACACACACACACACACACACACA" + rnd(100)]
+    for _ in range(200):                  # random tandem repeats (ties in the syncmer window)
+        unit = rnd(int(rng.integers(1, 7)))
+        body = (unit * 200)[:int(rng.integers(20, 300))]
+        reads.append(rnd(int(rng.integers(0, 40))) + body + rnd(int(rng.integers(0, 40))))
+    for _ in range(300):
+        r = bytearray(rnd(int(rng.choice([100, 150, 250, 400, 600]))))
+        for i in rng.integers(0, len(r), int(rng.integers(0, 4))):
+            r[i] = ord("N")
+        reads.append(bytes(r))
+    return reads
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kslu", [(20, 16, 1, 7), (22, 18, 2, 12), (18, 14, -2, 3), (24, 18, 2, 12),
+                                  (30, 12, 1, 4), (32, 30, 1, 8), (20, 20, 1, 4)])
+def test_randstrobes_adversarial(kslu):
+    """k_rs_wave (one wave a read) and the one-lane kernel it hands long reads and
+    wide windows to, vs the oracle: empty, short, max-length (512/513) and long reads;
+    tandem repeats whose equal s-mer hashes make the syncmer window's tie rules
+    matter (the wave kernel's serial walk); N runs, lowercase, U; window widths
+    k-s+1 = 1, 2, 5, 7 (wave kernel) and 19 (one-lane kernel)."""
+    from rabbitsalign_amd import native
+    k, s, l, u = kslu
+    rng = np.random.default_rng(k * 100 + s)
+    ref, offs = np.frombuffer(b"ACGT" * 64, np.uint8).copy(), np.array([0, 256], np.uint64)
+    idx = native.empty_index(ref, offs)
+    idx.k, idx.s, idx.l, idx.u = k, s, l, u
+    ctx = native.GpuContext(idx)
+    try:
+        ora = oracle_lib.OracleIndex(idx)
+        reads = _adversarial_reads(rng)
+        got = ctx.randstrobes(reads)
+        bad = []
+        for i, (r, g) in enumerate(zip(reads, got)):
+            w = ora.randstrobes(r)
+            if len(g) != len(w) or not all(np.array_equal(g[f], w[f]) for f in ("hash", "start", "end", "is_reverse")):
+                bad.append(i)
+        assert not bad, f"{len(bad)} reads differ, first {[reads[i][:40] for i in bad[:3]]}"
+        assert sum(len(g) for g in got) > 1000
+    finally:
+        ctx.close()
