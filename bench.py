@@ -41,8 +41,11 @@ WORKLOADS = {
                      desc="SE 1x100 vs 5 Mb synthetic reference"),
 }
 
-HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
-DP_PEAK_GCELLS = 6500.0        # packed-i16 DP cell updates/s model ceiling
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md "Chip-level parameters")
+# VALU ceiling of the DP scan (DESIGN.md §3 "Roofline reporting"): 256 CUs x 128 lane-ops/clk
+# (4 SIMD-32 per CU, MI355X_MICROARCH.md "Wave scheduling") x 2.4 GHz = 78.6 T int ops/s;
+# x 2 for packed int16 / 12 ops per cell update = 13.1 T cells/s
+DP_PEAK_GCELLS = 256 * 128 * 2.4 * 2 / 12
 REF_CPU_LIB = os.path.join(ROOT, "oracle", "_ref", "librsalign_ref.so")
 
 
@@ -98,37 +101,88 @@ def pmc_traffic(symbol: str):
         return None, None
 
 
-def roofline(ks: dict) -> dict:
-    """Roofline object for the kernel with the largest total device time.
+def kernel_roofline(name: str, k: dict, ks: dict) -> dict:
+    """Roofline of one kernel of the path from its live HIP-event times.
 
-    achieved = algorithmic bytes per launch / average launch duration, both
-    from the HIP events recorded around every launch on its own stream.
-    traffic = PMC-measured HBM bytes per launch of the same kernel (committed
-    profile), so traffic / alg_bytes_per_launch is the over-fetch factor.
+    k_ext_scan (integer DP, no MFMA) is VALU-bound: achieved = forward DP cells
+    per launch / average launch duration, against DP_PEAK_GCELLS.  The seeding,
+    site and band kernels are memory kernels: achieved = algorithmic bytes per
+    launch / average launch duration, against HBM peak.
+    traffic = PMC HBM bytes per launch of the same kernel (committed profile).
     """
     from rabbitsalign_amd.native import KERNEL_SYMBOLS
-    kern = ks["kernels"]
-    name = max(kern, key=lambda k: kern[k]["ms"])
-    k = kern[name]
-    if k["launches"] == 0 or k["ms"] <= 0:
-        return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-                "traffic": None, "kernel": None}
-    per_launch_bytes = k["alg_bytes"] / k["launches"]
-    avg_ms = k["ms"] / k["launches"]
-    achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9
     sym = KERNEL_SYMBOLS[name]
+    avg_s = k["ms"] * 1e-3 / k["launches"]
+    per_launch_bytes = k["alg_bytes"] / k["launches"]
     traffic, src = pmc_traffic(sym)
-    out = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-           "kernel": sym, "alg_bytes_per_launch": round(per_launch_bytes, 1),
-           "avg_launch_us": round(avg_ms * 1e3, 3), "launches": k["launches"], "traffic_source": src}
+    out = {"kernel": sym, "launches": k["launches"], "avg_launch_us": round(avg_s * 1e6, 3),
+           "alg_bytes_per_launch": round(per_launch_bytes, 1), "traffic": traffic, "traffic_source": src}
     if name == "ext_scan" and ks.get("dp_cells"):
-        # the DP scan is integer-VALU bound; cells/s is its natural throughput figure
-        out["dp_gcells_per_s"] = round(ks["dp_cells"] / (k["ms"] * 1e-3) / 1e9, 2)
-        # VALU view (SURVEY.md §8d): ~6.5 T cell-updates/s for packed-i16 Gotoh on 256 CUs
-        out["valu"] = {"achieved_gcells_per_s": out["dp_gcells_per_s"], "model_peak_gcells_per_s": DP_PEAK_GCELLS,
-                       "frac": round(out["dp_gcells_per_s"] / DP_PEAK_GCELLS, 4)}
+        cells = ks["dp_cells"] / k["launches"]
+        achieved = cells / avg_s / 1e9
+        out.update({"bound": "valu", "achieved": round(achieved, 2), "peak": round(DP_PEAK_GCELLS, 1),
+                    "unit": "Gcells/s", "frac": round(achieved / DP_PEAK_GCELLS, 5),
+                    "cells_per_launch": round(cells, 1),
+                    "hbm_GBps": round(per_launch_bytes / avg_s / 1e9, 3)})
+    else:
+        achieved = per_launch_bytes / avg_s / 1e9
+        out.update({"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 6)})
     return out
+
+
+def roofline(ks: dict, elapsed: float) -> dict:
+    """Roofline object: the kernel with the largest total device time (k_ext_scan_g on
+    the headline workload), plus the top three kernels and the whole path's HBM view."""
+    kern = {n: k for n, k in ks["kernels"].items() if k["launches"] and k["ms"] > 0}
+    if not kern:
+        return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None}
+    top = sorted(kern, key=lambda n: -kern[n]["ms"])
+    out = kernel_roofline(top[0], kern[top[0]], ks)
+    out["top_kernels"] = [kernel_roofline(n, kern[n], ks) for n in top[:3]]
+    # whole path: the algorithmic bytes of every kernel of the timed steps / wall time
+    reads = max(1, ks.get("reads", 0))
+    alg = sum(k["alg_bytes"] for k in kern.values())
+    path = {"alg_bytes_per_read": round(alg / reads, 1), "achieved": round(alg / elapsed / 1e9, 3),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(alg / elapsed / 1e9 / HBM_PEAK_GBS, 6)}
+    # SURVEY.md §8d's B_alg with this run's counters: 32 n_q + 24 n_hit + L n_site + n_sw (L + t + 16)
+    if ks.get("reads") and ks.get("jobs"):
+        L = ks["read_bases"] / ks["reads"]
+        n_q = ks["query_randstrobes"] / ks["reads"]
+        n_hit = ks["hits"] / ks["reads"]
+        n_site = ks["nams"] / ks["reads"]
+        n_sw = ks["jobs"] / ks["reads"]
+        t_bar = ks["dp_cells"] / max(1, ks["jobs"]) / max(1.0, L)
+        b = 32 * n_q + 24 * n_hit + L * n_site + n_sw * (L + t_bar + 16)
+        path["survey_formula"] = {"bytes_per_read": round(b, 1), "n_q": round(n_q, 2), "n_hit": round(n_hit, 2),
+                                  "n_site": round(n_site, 2), "n_sw": round(n_sw, 4), "t_bar": round(t_bar, 1),
+                                  "frac": round(b * reads / elapsed / 1e9 / HBM_PEAK_GBS, 6)}
+    out["path"] = path
+    return out
+
+
+def host_cpu() -> dict:
+    """CPU model and NUMA layout of the box (cpu_baseline context)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    nodes = {}
+    base = "/sys/devices/system/node"
+    try:
+        for d in sorted(os.listdir(base)):
+            if d.startswith("node") and d[4:].isdigit():
+                with open(os.path.join(base, d, "cpulist")) as f:
+                    nodes[d] = f.read().strip()
+    except OSError:
+        pass
+    return {"cpu_model": model, "numa_nodes": nodes, "affinity_cpus": len(os.sched_getaffinity(0)),
+            "machine_cpus": os.cpu_count()}
 
 
 def kernel_table(ks: dict) -> dict:
@@ -255,7 +309,7 @@ def main():
             c = cm.map(sample, threads=cores, chunk_size=args.chunk_size)
             cm.close()
             cpu = {"value": round(c.n_reads / c.map_seconds / 1e6, 6), "unit": "Mreads/s", "cores": cores,
-                   "kind": "reference",
+                   "kind": "reference", "host": host_cpu(),
                    "sample": f"{n_cpu} {'pairs' if wl['paired'] else 'reads'} of the same workload "
                              f"({c.n_reads} reads, {c.map_seconds:.2f} s wall), -t {cores}, chunk {args.chunk_size}; "
                              "reference randstrobes/nam/ssw.c objects + restated host pipeline"}
@@ -269,7 +323,7 @@ def main():
 
     if rank == 0:
         value = reads_all / elapsed_max / 1e6
-        rl = roofline(ks)
+        rl = roofline(ks, elapsed_max)
         line = {
             "metric": "Mreads/s aligned (PE 2x150 vs 3 Gb, SAM bit-exact vs CPU)" if args.workload == "pe150_3g"
             else f"Mreads/s aligned ({args.workload})",

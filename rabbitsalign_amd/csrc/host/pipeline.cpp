@@ -73,6 +73,9 @@ struct Unslot {                   // the slot handed back for a blocking section
 // +0 9.0/8.8, +8 9.4, +16 8.3 Mreads/s; on the r26 code +4 14.4/14.8, +8
 // 15.7/15.5, +12 15.8/16.3; r27: +12 17.2/17.6, +16 15.9/16.1, +20 15.9/15.7
 // -- none for an engine computing in-thread)
+// chunks per extend call (A/B on the box: see DESIGN.md §5)
+constexpr int kDefaultExtGroup = 1;
+
 static int wait_workers(const Engine& eng, int threads) {
     const char* e = getenv("RSA_WAIT_WORKERS");
     if (e) return std::max(0, atoi(e));
@@ -409,9 +412,9 @@ void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize) {
     pe_part(c, mc, isize, [](PeChunk&) {});
 }
 
+// appends the chunk's SW jobs (pc.cpp:214-242, 333-368) to `jobs`
 void pe_get_str(PeChunk& c, const MapContext& mc, float mu, float sigma, std::vector<SwJob>& jobs) {
     const auto t = Clock::now();
-    jobs.clear();
     for (size_t i = 0; i < c.r1.size(); ++i) {
         const Read read1(c.r1[i]->seq, c.rc(i, 0)), read2(c.r2[i]->seq, c.rc(i, 1));
         collect_jobs_pe(c.res[i], *c.r1[i], *c.r2[i], read1, read2, mc, mu, sigma, jobs);
@@ -419,10 +422,10 @@ void pe_get_str(PeChunk& c, const MapContext& mc, float mu, float sigma, std::ve
     c.times.collect += since(t);
 }
 
+// the chunk's extension results start at infos[pos]
 void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistribution& isize,
-                   std::vector<AlignmentInfo>& infos, const std::string& rg_id, std::string& out) {
+                   std::vector<AlignmentInfo>& infos, size_t pos, const std::string& rg_id, std::string& out) {
     const auto t = Clock::now();
-    size_t pos = 0;
     const size_t n = c.r1.size();
     static const bool pf = !(getenv("RSA_PREFETCH") && atoi(getenv("RSA_PREFETCH")) == 0);
     const size_t ahead = rec_ahead();
@@ -498,6 +501,10 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
     // default 1: A/B on the bench, 1 -> 11.75/11.61, 4 -> 11.00/10.60 Mreads/s; r26 code:
     // 1 -> 15.5/16.5/13.8, 2 -> 13.8/12.9/15.2, profiles/r01_ab_seed_batch.jsonl)
     const size_t seed_batch = std::max<size_t>(1, getenv("RSA_SEED_BATCH") ? (size_t)atol(getenv("RSA_SEED_BATCH")) : 1);
+    // chunks per extend call in the parallel stage (PipelineOptions::ext_group, RSA_EXT_GROUP)
+    const size_t ext_group = (size_t)std::max(1, opt.ext_group > 0 ? opt.ext_group
+                                                   : getenv("RSA_EXT_GROUP") ? atoi(getenv("RSA_EXT_GROUP"))
+                                                   : kDefaultExtGroup);
     auto stage1_multi = [&](const std::vector<size_t>& idxs) {
         std::vector<std::unique_ptr<PeChunk>> cs;
         std::vector<PeChunk*> ps;
@@ -550,21 +557,31 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
         cv.notify_all();
         return c;
     };
-    auto finish = [&](PeChunk& c, const InsertSizeDistribution& est, std::vector<SwJob>& jobs,
-                      std::vector<AlignmentInfo>& infos) {
-        pe_get_str(c, mc, est.mu, est.sigma, jobs);
+    // SW jobs of a group of parted chunks in one engine call, then store + last per chunk
+    auto finish = [&](std::vector<std::unique_ptr<PeChunk>>& cs, const InsertSizeDistribution& est,
+                      std::vector<SwJob>& jobs, std::vector<AlignmentInfo>& infos) {
+        jobs.clear();
+        std::vector<size_t> first(cs.size());
+        for (size_t g = 0; g < cs.size(); ++g) {
+            first[g] = jobs.size();
+            pe_get_str(*cs[g], mc, est.mu, est.sigma, jobs);
+            cs[g]->stats.tot_aligner_calls += jobs.size() - first[g];
+        }
         const auto te = Clock::now();
         {
             Unslot u(slots, offl);
             eng.extend(jobs, mc.aparams, infos);
         }
-        c.times.extend += since(te);
-        c.stats.tot_aligner_calls += jobs.size();
-        std::string out = os.take();
-        pe_store_last(c, mc, est, infos, opt.rg_id, out);
-        const auto tp = Clock::now();
-        os.put(c.index, std::move(out));
-        c.times.output += since(tp);
+        const double dt = since(te) / (double)cs.size();
+        for (size_t g = 0; g < cs.size(); ++g) {
+            PeChunk& c = *cs[g];
+            c.times.extend += dt;
+            std::string out = os.take();
+            pe_store_last(c, mc, est, infos, first[g], opt.rg_id, out);
+            const auto tp = Clock::now();
+            os.put(c.index, std::move(out));
+            c.times.output += since(tp);
+        }
     };
 
     auto worker = [&](bool leader) {
@@ -599,6 +616,7 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                 size_t next = 1;
                 for (;;) {
                     if (isize.frozen() || next > n_chunks) break;
+                    jobs.clear();
                     pe_get_str(*pre, mc, isize.mu, isize.sigma, jobs);
                     std::unique_ptr<PeChunk> cur;
                     if (next < n_chunks) {
@@ -615,7 +633,7 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                     pre->times.extend += since(te);
                     pre->stats.tot_aligner_calls += jobs.size();
                     std::string out = os.take();
-                    pe_store_last(*pre, mc, isize, infos, opt.rg_id, out);
+                    pe_store_last(*pre, mc, isize, infos, 0, opt.rg_id, out);
                     os.put(pre->index, std::move(out));
                     local.add(pre->stats);
                     lt.add(pre->times);
@@ -636,14 +654,19 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
             // ---- shared loop: parallel stage first, prefetch when it has nothing ----
             for (;;) {
                 std::unique_ptr<PeChunk> c;
-                size_t idx = SIZE_MAX, pf = SIZE_MAX;
+                size_t idx = SIZE_MAX, pf = SIZE_MAX, cnt = 0;
                 std::vector<size_t> pfs;
                 {
                     std::unique_lock<std::mutex> g(m);
                     for (;;) {
                         if (failure || done) break;
                         if (frozen && handed) { c = std::move(handed); break; }
-                        if (frozen && next_par < n_chunks) { idx = next_par++; break; }
+                        if (frozen && next_par < n_chunks) {
+                            idx = next_par;
+                            cnt = std::min(ext_group, n_chunks - next_par);
+                            next_par += cnt;
+                            break;
+                        }
                         if (lead_seeded && next_seed < n_chunks && next_seed < consumed + window) {
                             pf = next_seed;
                             // a run of consecutive unclaimed chunks, seeded in one engine call
@@ -665,22 +688,24 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                         g.lock();
                     }
                 }
-                if (c) {                                    // part() already done
-                    finish(*c, frozen_isize, jobs, infos);
-                    local.add(c->stats);
-                    lt.add(c->times);
-                    recycle(std::move(c));
-                    continue;
-                }
-                if (idx != SIZE_MAX) {
-                    c = acquire(idx);
-                    if (!c) break;
-                    InsertSizeDistribution est = frozen_isize;
-                    pe_part(*c, mc, est);
-                    finish(*c, frozen_isize, jobs, infos);
-                    local.add(c->stats);
-                    lt.add(c->times);
-                    recycle(std::move(c));
+                if (c || idx != SIZE_MAX) {
+                    std::vector<std::unique_ptr<PeChunk>> cs;
+                    if (c) cs.push_back(std::move(c));     // part() already done
+                    bool lost = false;
+                    for (size_t q = idx; q != SIZE_MAX && q < idx + cnt; ++q) {
+                        auto x = acquire(q);
+                        if (!x) { lost = true; break; }
+                        InsertSizeDistribution est = frozen_isize;
+                        pe_part(*x, mc, est);
+                        cs.push_back(std::move(x));
+                    }
+                    if (lost) break;
+                    finish(cs, frozen_isize, jobs, infos);
+                    for (auto& x : cs) {
+                        local.add(x->stats);
+                        lt.add(x->times);
+                        recycle(std::move(x));
+                    }
                     continue;
                 }
                 if (pf != SIZE_MAX) {

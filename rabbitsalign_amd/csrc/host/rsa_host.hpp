@@ -433,6 +433,10 @@ struct PipelineOptions {
     bool interleaved = false;
     std::string rg_id;
     bool digest = false;   // compute PipelineResult::sam_digest (in the workers, in parallel)
+    // chunks whose SW jobs go to the engine in one extend call (parallel stage, PE);
+    // 0: RSA_EXT_GROUP or the default.  Bigger calls fill the GPU (one chunk is ~7 k jobs,
+    // < 2 waves per SIMD of the scan kernel); results do not depend on it
+    int ext_group = 0;
 };
 
 // Order-sensitive digest of a SAM body, independent of how it is chunked:

@@ -44,3 +44,17 @@ def test_engine_error_is_reported_not_aborted(tmp_path, se):
                         fa, *reads], capture_output=True, text=True, env=env)
     assert r.returncode == 1, (r.returncode, r.stderr[-500:])
     assert "injected extend failure" in r.stderr
+
+
+@pytest.mark.parametrize("group", ["2", "5"])
+def test_extension_group_invariance(data, group):
+    """Several chunks' SW jobs in one extend call (RSA_EXT_GROUP) give the same SAM."""
+    import subprocess
+    d, (fa, reads) = data
+    base = str(d / "g1.sam")
+    map_reads(CPU_PORT, fa, reads, base, "-t", "4", "--chunk-size", "200")
+    env = dict(os.environ, RSA_EXT_GROUP=group)
+    out = str(d / f"g{group}.sam")
+    subprocess.run([CPU_PORT, "--use-index", "-t", "4", "--chunk-size", "200", "-o", out, fa, *reads],
+                   check=True, capture_output=True, env=env)
+    assert sam_body(base) == sam_body(out)
