@@ -56,6 +56,11 @@ typedef struct rsam_info {
 int rsam_get_info(const rsam* m, rsam_info* out);
 
 rsam_reads* rsam_reads_load(const char* fq1, const char* fq2 /* NULL: single-end */);
+/* --interleaved input (one file, mates as consecutive records): rsam_map pairs the
+ * records per chunk of 2 x chunk_size records as the reference's InputBuffer does
+ * (src/pc.cpp:23-107) and maps the pairs; unpaired records are not mapped, as in
+ * the reference's paired-end task (perform_task_async_pe). */
+rsam_reads* rsam_reads_load_interleaved(const char* fq);
 /* pairs p in [first, first + n) of the synthetic stream `seed` (paired or SE with mate 1 only) */
 rsam_reads* rsam_reads_synthetic(const rsam* m, uint64_t seed, uint64_t first, uint64_t n, int read_len,
                                  double mu, double sigma, int paired);

@@ -6,7 +6,7 @@
 //   seeds   : randstrobes_query / find_nams / find_nams_rescue
 //             (src/randstrobes.cpp:207-253, src/nam.cpp:771-1012)
 //   ssw     : ssw_init + ssw_align                  (ext/ssw/ssw.c:789-922)
-//   sam     : Sam::add_pair / add / add_unmapped*   (src/sam.cpp)
+//   sam     : Sam::add / add_pair / add_unmapped*   (src/sam.cpp), reverse_complement (revcomp.hpp)
 // Only FASTA parsing (refs.cpp needs the un-vendored zstr) and the SSW base
 // translation table (ssw_cpp.cpp includes a CUDA header) are restated here.
 #include <cinttypes>
@@ -26,6 +26,9 @@
 #include "randstrobes.hpp"
 #include "refs.hpp"
 #include "sam.hpp"
+#include "revcomp.hpp"
+#include <memory>
+#include <array>
 #include "ssw/ssw.h"
 
 // refs.cpp:8-58 semantics: name cut at the first ' ', sequence uppercased with c & ~32
@@ -180,11 +183,26 @@ static int cmd_sswrand(int argc, char** argv) {
     return 0;
 }
 
-// sam <fasta> <records.txt> <out> : format records through the reference Sam class.
-// Input lines (whitespace separated):
-//  P name1 seq1 qual1 name2 seq2 qual2 mapq1 mapq2 proper primary eqx  <aln1> <aln2>
-//  aln = ref_id ref_start length edit_distance score is_rc is_unaligned ncig cig...
-//  U name1 seq1 qual1 name2 seq2 qual2          (unmapped pair)
+// sam <fasta> <calls.txt> <out> : replay a list of Sam calls through the
+// reference's Sam class (src/sam.cpp) -- the expected bytes of
+// tests/golden/sam_calls.*; oracle/sam_replay.cpp replays the same list through
+// the product's Sam (csrc/host/io.cpp).  One call per line, whitespace separated
+// ("*" = empty string, "-" = empty read group):
+//   S eqx rg_id output_unmapped details          new Sam (sam.hpp:72-92)
+//   A name seq qual mapq primary <det> <aln>     add (sam.cpp:125-147)
+//   P name1 seq1 qual1 name2 seq2 qual2 mapq1 mapq2 proper primary <det1> <det2> <aln1> <aln2>   add_pair
+//   U name seq qual flags                        add_unmapped
+//   UP name1 seq1 qual1 name2 seq2 qual2         add_unmapped_pair
+//   UM name seq qual flags mate_ref mate_pos     add_unmapped_mate
+//   det = nam_rescue nams nam_inconsistent mate_rescue tried_alignment gapped
+//   aln = ref_id ref_start length edit_distance score is_rc is_unaligned ncig op...
+// The reverse complements come from the reference's reverse_complement (revcomp.hpp).
+static std::string tok(std::istream& s) {
+    std::string t;
+    s >> t;
+    return t == "*" ? std::string() : t;
+}
+
 static Alignment parse_aln(std::istream& s) {
     Alignment a;
     int rc, un, nc;
@@ -196,41 +214,76 @@ static Alignment parse_aln(std::istream& s) {
     return a;
 }
 
+static Details parse_det(std::istream& s) {
+    Details d;
+    int nr;
+    s >> nr >> d.nams >> d.nam_inconsistent >> d.mate_rescue >> d.tried_alignment >> d.gapped;
+    d.nam_rescue = nr;
+    return d;
+}
+
+static klibpp::KSeq parse_rec(std::istream& s) {
+    klibpp::KSeq r;
+    r.name = tok(s);
+    r.seq = tok(s);
+    r.qual = tok(s);
+    return r;
+}
+
 static int cmd_sam(int argc, char** argv) {
-    if (argc < 5) { fprintf(stderr, "sam <fasta> <records> <out>\n"); return 2; }
+    if (argc < 5) { fprintf(stderr, "sam <fasta> <calls> <out>\n"); return 2; }
     References refs = read_fasta(argv[2]);
     std::ifstream in(argv[3]);
-    std::string out_all;
+    std::string out;
+    std::unique_ptr<Sam> sam;
     std::string line;
     while (std::getline(in, line)) {
         std::istringstream s(line);
         std::string kind;
         s >> kind;
-        klibpp::KSeq r1, r2;
-        s >> r1.name >> r1.seq >> r1.qual >> r2.name >> r2.seq >> r2.qual;
-        if (r1.qual == "*") r1.qual.clear();
-        if (r2.qual == "*") r2.qual.clear();
-        std::string out;
-        if (kind == "U") {
-            Sam sam(out, refs, CigarOps::M);
-            sam.add_unmapped_pair(r1, r2);
-        } else {
-            int m1, m2, proper, primary, eqx;
-            s >> m1 >> m2 >> proper >> primary >> eqx;
+        if (kind == "S") {
+            int eqx, unmapped, details;
+            std::string rg;
+            s >> eqx >> rg >> unmapped >> details;
+            if (rg == "-") rg.clear();
+            sam.reset(new Sam(out, refs, eqx ? CigarOps::EQX : CigarOps::M, rg, unmapped, details));
+        } else if (kind == "A") {
+            klibpp::KSeq r = parse_rec(s);
+            int mapq, primary;
+            s >> mapq >> primary;
+            Details d = parse_det(s);
+            Alignment a = parse_aln(s);
+            sam->add(a, r, reverse_complement(r.seq), (uint8_t)mapq, primary, d);
+        } else if (kind == "P") {
+            klibpp::KSeq r1 = parse_rec(s), r2 = parse_rec(s);
+            int m1, m2, proper, primary;
+            s >> m1 >> m2 >> proper >> primary;
+            std::array<Details, 2> det{parse_det(s), parse_det(s)};
             Alignment a1 = parse_aln(s), a2 = parse_aln(s);
-            Sam sam(out, refs, eqx ? CigarOps::EQX : CigarOps::M);
-            std::string rc1, rc2;
-            static const char* comp = "TGCA";
-            for (auto it = r1.seq.rbegin(); it != r1.seq.rend(); ++it) rc1 += *it == 'A' ? 'T' : *it == 'C' ? 'G' : *it == 'G' ? 'C' : *it == 'T' ? 'A' : 'N';
-            for (auto it = r2.seq.rbegin(); it != r2.seq.rend(); ++it) rc2 += *it == 'A' ? 'T' : *it == 'C' ? 'G' : *it == 'G' ? 'C' : *it == 'T' ? 'A' : 'N';
-            (void)comp;
-            std::array<Details, 2> det;
-            sam.add_pair(a1, a2, r1, r2, rc1, rc2, (uint8_t)m1, (uint8_t)m2, proper, primary, det);
+            sam->add_pair(a1, a2, r1, r2, reverse_complement(r1.seq), reverse_complement(r2.seq), (uint8_t)m1,
+                          (uint8_t)m2, proper, primary, det);
+        } else if (kind == "U") {
+            klibpp::KSeq r = parse_rec(s);
+            int flags;
+            s >> flags;
+            sam->add_unmapped(r, (uint16_t)flags);
+        } else if (kind == "UP") {
+            klibpp::KSeq r1 = parse_rec(s), r2 = parse_rec(s);
+            sam->add_unmapped_pair(r1, r2);
+        } else if (kind == "UM") {
+            klibpp::KSeq r = parse_rec(s);
+            int flags;
+            uint32_t pos;
+            std::string ref;
+            s >> flags >> ref >> pos;
+            sam->add_unmapped_mate(r, (uint16_t)flags, ref, pos);
+        } else if (!kind.empty()) {
+            fprintf(stderr, "bad call line: %s\n", line.c_str());
+            return 2;
         }
-        out_all += out;
     }
     FILE* o = fopen(argv[4], "w");
-    fwrite(out_all.data(), 1, out_all.size(), o);
+    fwrite(out.data(), 1, out.size(), o);
     fclose(o);
     return 0;
 }

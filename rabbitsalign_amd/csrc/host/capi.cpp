@@ -123,6 +123,7 @@ struct rsam {
 struct rsam_reads {
     std::vector<Record> r1, r2;
     bool paired = false;
+    std::vector<Record> interleaved;   // rsam_reads_load_interleaved: paired up per chunk size in rsam_map
 };
 
 static void finish_refs(References& r) {
@@ -258,6 +259,18 @@ rsam_reads* rsam_reads_load(const char* fq1, const char* fq2) {
     }
 }
 
+rsam_reads* rsam_reads_load_interleaved(const char* fq) {
+    try {
+        std::unique_ptr<rsam_reads> r(new rsam_reads());
+        r->interleaved = FastxReader::read_all(fq);
+        r->paired = true;
+        return r.release();
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return nullptr;
+    }
+}
+
 rsam_reads* rsam_reads_synthetic(const rsam* m, uint64_t seed, uint64_t first, uint64_t n, int read_len, double mu,
                                  double sigma, int paired) {
     auto* r = new rsam_reads();
@@ -281,7 +294,9 @@ rsam_reads* rsam_reads_synthetic(const rsam* m, uint64_t seed, uint64_t first, u
     return r;
 }
 
-uint64_t rsam_reads_count(const rsam_reads* r) { return r ? r->r1.size() + r->r2.size() : 0; }
+uint64_t rsam_reads_count(const rsam_reads* r) {
+    return r ? r->r1.size() + r->r2.size() + r->interleaved.size() : 0;
+}
 void rsam_reads_free(rsam_reads* r) { delete r; }
 
 struct SinkState {
@@ -310,8 +325,15 @@ int rsam_map(rsam* m, const rsam_reads* reads, int threads, int chunk_size, cons
         po.chunk_size = chunk_size;
         po.digest = true;
         SamSink sk = st.f ? sink_fn : nullptr;
-        PipelineResult res = reads->paired ? run_pipeline_pe(reads->r1, reads->r2, *m->eng, mc, po, sk, &st)
-                                           : run_pipeline_se(reads->r1, *m->eng, mc, po, sk, &st);
+        PipelineResult res;
+        if (!reads->interleaved.empty()) {          // pairs per chunk of 2 * chunk_size records (pc.cpp:38-107)
+            std::vector<Record> all(reads->interleaved), r1, r2;
+            distribute_interleaved(std::move(all), (size_t)std::max(1, chunk_size), r1, r2, po.chunk_starts);
+            res = run_pipeline_pe(r1, r2, *m->eng, mc, po, sk, &st);
+        } else {
+            res = reads->paired ? run_pipeline_pe(reads->r1, reads->r2, *m->eng, mc, po, sk, &st)
+                                : run_pipeline_se(reads->r1, *m->eng, mc, po, sk, &st);
+        }
         if (st.f) fclose(st.f);
         if (out) {
             out->n_reads = res.stats.n_reads;

@@ -113,17 +113,28 @@ int cli_main(int argc, char** argv, EngineFactory factory, const char* prog) {
         Opts o = parse(argc - (index_cmd ? 1 : 0), argv + (index_cmd ? 1 : 0), ok);
         if (!ok || o.ref.empty()) { usage(prog); return 1; }
         if (o.c != INT32_MIN && (o.c >= 64 || o.c <= 0)) throw std::runtime_error("c must be greater than 0 and less than 64");
-        if (o.interleaved) throw std::runtime_error("--interleaved input is not supported yet");
-        // read length (main.cpp:254-258: average of the first 500 records of each file)
+        if (o.interleaved && !o.reads2.empty())        // main.cpp:136-139
+            throw std::runtime_error("Cannot specify both --interleaved and specify two read files");
+        // read length (main.cpp:254-258, readlen.cpp:16-29: average over the first read_records(500):
+        // 500 records of each file, or the first 1000 records of an interleaved file)
         std::vector<Record> recs1, recs2;
+        std::vector<size_t> chunk_starts;
+        size_t singletons = 0;
         if (!o.reads1.empty() && !index_cmd) {
             if (o.reads2.empty()) recs1 = FastxReader::read_all(o.reads1);
             else FastxReader::read_pair(o.reads1, o.reads2, recs1, recs2);
             if (!o.r_set) {
                 uint64_t tot = 0, num = 0;
-                for (size_t i = 0; i < std::min<size_t>(500, recs1.size()); ++i) { tot += recs1[i].seq.size(); num++; }
+                const size_t first = o.interleaved ? 1000 : 500;
+                for (size_t i = 0; i < std::min<size_t>(first, recs1.size()); ++i) { tot += recs1[i].seq.size(); num++; }
                 for (size_t i = 0; i < std::min<size_t>(500, recs2.size()); ++i) { tot += recs2[i].seq.size(); num++; }
                 o.r = num ? (int)(tot / num) : 150;
+            }
+            if (o.interleaved) {
+                std::vector<Record> all;
+                all.swap(recs1);
+                singletons = distribute_interleaved(std::move(all), (size_t)std::max(1, o.chunk_size), recs1, recs2,
+                                                    chunk_starts);
             }
         }
         IndexParameters ip = IndexParameters::from_read_length(o.r, o.k, o.s, o.l, o.u, o.c, o.m);
@@ -174,8 +185,12 @@ int cli_main(int argc, char** argv, EngineFactory factory, const char* prog) {
         MapContext mc{refs, idx.params, ap, mp};
         PipelineOptions po;
         po.threads = o.threads; po.chunk_size = o.chunk_size; po.rg_id = o.rg_id;
-        PipelineResult res = recs2.empty() ? run_pipeline_se(recs1, *eng, mc, po, write_sink, out)
-                                           : run_pipeline_pe(recs1, recs2, *eng, mc, po, write_sink, out);
+        po.chunk_starts = std::move(chunk_starts);
+        if (o.interleaved && o.verbose)
+            fprintf(stderr, "[%s] interleaved input: %zu pairs, %zu unpaired records (not mapped, as in the "
+                            "reference's paired-end task)\n", prog, recs1.size(), singletons);
+        PipelineResult res = (recs2.empty() && !o.interleaved) ? run_pipeline_se(recs1, *eng, mc, po, write_sink, out)
+                                                               : run_pipeline_pe(recs1, recs2, *eng, mc, po, write_sink, out);
         if (out != stdout) fclose(out); else fflush(out);
         fprintf(stderr,
                 "[%s] engine %s | index %.2f s, upload %.2f s | mapped %lu reads in %.3f s = %.4f Mreads/s | "

@@ -22,6 +22,7 @@
 #include <deque>
 #include <map>
 #include <mutex>
+#include <stdexcept>
 #include <thread>
 
 #include "rsa_host.hpp"
@@ -249,13 +250,14 @@ static inline void prefetch_res(const AlignTmpRes& r) {
     prefetch_vec(r.type4_nams);
 }
 
-void pe_load(PeChunk& c, const std::vector<Record>& a, const std::vector<Record>& b, size_t idx, size_t chunk) {
+void pe_load(PeChunk& c, const std::vector<Record>& a, const std::vector<Record>& b, size_t idx, size_t chunk,
+             const std::vector<size_t>& starts) {
     c.index = idx;
     c.owned.clear();
     c.stats = AlignmentStatistics();
     c.times = PhaseTimes();
-    c.begin = std::min(a.size(), idx * chunk);
-    c.end = std::min(a.size(), c.begin + chunk);
+    c.begin = starts.empty() ? std::min(a.size(), idx * chunk) : starts[idx];
+    c.end = starts.empty() ? std::min(a.size(), c.begin + chunk) : starts[idx + 1];
     const size_t n = c.end - c.begin;
     c.r1.resize(n);
     c.r2.resize(n);
@@ -451,6 +453,40 @@ void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistributio
 
 }  // namespace
 
+bool same_name(const std::string& n1, const std::string& n2) {      // pc.cpp:23-35
+    if (n1.length() != n2.length()) return false;
+    if (n1.length() <= 2) return n1 == n2;
+    size_t i = 0;
+    for (; i < n1.length() - 1; ++i)
+        if (n1[i] != n2[i]) return false;
+    if (n1[i - 1] == '/' && n1[i] == '1' && n2[i] == '2') return true;
+    return n1[i] == n2[i];
+}
+
+size_t distribute_interleaved(std::vector<Record>&& recs, size_t chunk_size, std::vector<Record>& r1,
+                              std::vector<Record>& r2, std::vector<size_t>& chunk_starts) {
+    const size_t block = 2 * std::max<size_t>(1, chunk_size);   // read_records: ks1->stream().read(to_read * 2)
+    r1.clear();
+    r2.clear();
+    chunk_starts.assign(1, 0);
+    size_t singles = 0;
+    for (size_t b = 0; b < recs.size(); b += block) {
+        const size_t e = std::min(recs.size(), b + block);
+        for (size_t i = b; i < e; ++i) {
+            if (i + 1 < e && same_name(recs[i].name, recs[i + 1].name)) {
+                r1.push_back(std::move(recs[i]));
+                r2.push_back(std::move(recs[i + 1]));
+                ++i;
+            } else {
+                singles++;
+            }
+        }
+        chunk_starts.push_back(r1.size());
+    }
+    recs.clear();
+    return singles;
+}
+
 // Chunks flow through three stages:
 //   load + seed   any order, any worker, up to `window` chunks ahead (needs no
 //                 insert-size state, so it also fills the sequential phase)
@@ -465,7 +501,9 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
     PipelineResult result;
     OrderedSink os{sink, user, opt.digest};
     const size_t chunk = (size_t)std::max(1, opt.chunk_size);
-    const size_t n_chunks = (r1.size() + chunk - 1) / chunk;
+    if (!opt.chunk_starts.empty() && (opt.chunk_starts.front() != 0 || opt.chunk_starts.back() != r1.size()))
+        throw std::runtime_error("chunk_starts do not cover the pairs");
+    const size_t n_chunks = opt.chunk_starts.empty() ? (r1.size() + chunk - 1) / chunk : opt.chunk_starts.size() - 1;
     if (n_chunks == 0) return result;
     const int T = std::max(1, opt.threads);
     const bool offl = eng.offloads();
@@ -512,7 +550,7 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
             std::unique_ptr<PeChunk> c = chunk_pool().take();
             if (!c) c = std::make_unique<PeChunk>();
             const auto t = Clock::now();
-            pe_load(*c, r1, r2, idx, chunk);
+            pe_load(*c, r1, r2, idx, chunk, opt.chunk_starts);
             c->times.load += since(t);
             ps.push_back(c.get());
             cs.push_back(std::move(c));
@@ -524,7 +562,7 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
         std::unique_ptr<PeChunk> c = chunk_pool().take();
         if (!c) c = std::make_unique<PeChunk>();
         const auto t = Clock::now();
-        pe_load(*c, r1, r2, idx, chunk);
+        pe_load(*c, r1, r2, idx, chunk, opt.chunk_starts);
         c->times.load += since(t);
         pe_seed(*c, eng, mc, slots);
         return c;

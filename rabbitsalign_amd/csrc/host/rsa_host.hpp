@@ -437,7 +437,24 @@ struct PipelineOptions {
     // 0: RSA_EXT_GROUP or the default.  Bigger calls fill the GPU (one chunk is ~7 k jobs,
     // < 2 waves per SIMD of the scan kernel); results do not depend on it
     int ext_group = 0;
+    // explicit chunk boundaries in pairs ([n_chunks + 1], first 0): chunk i holds
+    // pairs [chunk_starts[i], chunk_starts[i+1]); empty = every chunk_size pairs.
+    // Interleaved input sets them (its chunks hold up to chunk_size pairs each)
+    std::vector<size_t> chunk_starts;
 };
+
+// --interleaved input (InputBuffer::read_records + distribute_interleaved,
+// src/pc.cpp:23-107): the file is read in blocks of 2 * chunk_size records, one
+// block per chunk; within a block two consecutive records whose names are the
+// same (ignoring /1 on the first and /2 on the second, same_name) form a pair,
+// every other record is a singleton.  The reference's paired-end task
+// (perform_task_async_pe, pc.cpp:1522-1887) maps only the pairs -- singletons
+// are read and dropped -- and a pair split across two blocks is two singletons
+// (the lookahead of distribute_interleaved is never set).  Returns the number of
+// singletons; r1/r2/chunk_starts receive the pairs and their chunk boundaries.
+size_t distribute_interleaved(std::vector<Record>&& recs, size_t chunk_size, std::vector<Record>& r1,
+                              std::vector<Record>& r2, std::vector<size_t>& chunk_starts);
+bool same_name(const std::string& n1, const std::string& n2);
 
 // Order-sensitive digest of a SAM body, independent of how it is chunked:
 // D = sum_k line_hash(line_k) * P^(N-1-k) mod 2^64 over the N lines (without '\n').

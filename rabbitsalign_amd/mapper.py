@@ -39,7 +39,7 @@ class _Info(C.Structure):
 
 EXPORTED_SYMBOLS = [
     "rsam_open_files", "rsam_open_synthetic", "rsam_open_like", "rsam_close", "rsam_get_info",
-    "rsam_reads_load", "rsam_reads_synthetic", "rsam_reads_count", "rsam_reads_free", "rsam_map",
+    "rsam_reads_load", "rsam_reads_load_interleaved", "rsam_reads_synthetic", "rsam_reads_count", "rsam_reads_free", "rsam_map",
     "rsam_kernel_stats", "rsam_reset_kernel_stats", "rsam_engine_name", "rsam_last_error",
 ]
 
@@ -63,6 +63,8 @@ def load(path: str = PRODUCT_LIB) -> C.CDLL:
     lib.rsam_get_info.argtypes = [vp, C.POINTER(_Info)]
     lib.rsam_reads_load.restype = vp
     lib.rsam_reads_load.argtypes = [cp, cp]
+    lib.rsam_reads_load_interleaved.restype = vp
+    lib.rsam_reads_load_interleaved.argtypes = [cp]
     lib.rsam_reads_synthetic.restype = vp
     lib.rsam_reads_synthetic.argtypes = [vp, u64, u64, u64, i32, C.c_double, C.c_double, i32]
     lib.rsam_reads_count.restype = u64
@@ -159,8 +161,11 @@ class Mapper:
         return Reads(self._lib, self._lib.rsam_reads_synthetic(self._h, seed, first, n, read_len, mu, sigma,
                                                                1 if paired else 0))
 
-    def load_reads(self, fq1, fq2=None) -> Reads:
-        h = self._lib.rsam_reads_load(str(fq1).encode(), str(fq2).encode() if fq2 else None)
+    def load_reads(self, fq1, fq2=None, interleaved=False) -> Reads:
+        if interleaved:
+            h = self._lib.rsam_reads_load_interleaved(str(fq1).encode())
+        else:
+            h = self._lib.rsam_reads_load(str(fq1).encode(), str(fq2).encode() if fq2 else None)
         if not h:
             raise RuntimeError(self._lib.rsam_last_error().decode())
         return Reads(self._lib, h)

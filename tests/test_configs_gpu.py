@@ -1,0 +1,58 @@
+"""GPU parity at the BASELINE.json configurations' own reference sizes.
+
+Each case builds the synthetic reference of the config (SURVEY.md Appendix D:
+i.i.d. ACGT, 1 contig of 250 Mb / 24 contigs of 125 Mb / 1 contig of 5 Mb), builds
+its index on the GPU (bits 24 / 28 / 18, 50 M / 600 M randstrobes), maps a sample
+of the config's synthetic reads with the product (librsalign.so: HIP seeding, NAMs,
+extension) and with the CPU path (oracle/_ref/librsalign_ref.so: the reference's
+own randstrobes / find_nams / ssw.c behind the same host pipeline, on a host copy
+of the same index), and requires the SAM body to be identical: same order-sensitive
+line digest and byte count.  The 8-GPU config differs from PE150@3Gb only in how
+chunks are placed (tests/test_dist_cpu.py, test_multi_device_*)."""
+import os
+
+import pytest
+
+from helpers import ROOT
+
+REF_CPU_LIB = os.path.join(ROOT, "oracle", "_ref", "librsalign_ref.so")
+
+CONFIGS = {
+    # name: ref bp, contigs, read length, insert mean / sd, paired, pairs (SE: reads), index bits
+    "pe150_250m": (250_000_000, 1, 150, 300.0, 30.0, True, 200_000, 24),
+    "pe150_3g": (3_000_000_000, 24, 150, 300.0, 30.0, True, 200_000, 28),
+    "pe250_3g": (3_000_000_000, 24, 250, 500.0, 50.0, True, 100_000, 28),
+    "se100_5m": (5_000_000, 1, 100, 300.0, 30.0, False, 200_000, 18),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("name", sorted(CONFIGS))
+def test_baseline_config_sam_identical(name):
+    import torch  # noqa: F401  (HIP runtime of the process first, see bench.py)
+    from rabbitsalign_amd import mapper as M
+    if not os.path.exists(REF_CPU_LIB):
+        pytest.skip("CPU path library not built")
+    ref_len, contigs, L, mu, sigma, paired, n, bits = CONFIGS[name]
+    threads = min(16, os.cpu_count() or 4)
+    m = M.Mapper.synthetic(1, ref_len, contigs, L, device=0, threads=threads)
+    try:
+        info = m.info()
+        assert info["bits"] == bits and info["n_contigs"] == contigs and info["index_on_device"] == 1
+        reads = m.synthetic_reads(7, 0, n, L, mu, sigma, paired)
+        g = m.map(reads, threads=threads)
+        ks = m.kernel_stats()
+        assert ks["kernels"]["ext_scan"]["launches"] > 0 and ks["kernels"]["lookup"]["launches"] > 0
+        cm = m.like(device=0, threads=threads, lib_path=REF_CPU_LIB)
+        try:
+            c = cm.map(reads, threads=threads)
+        finally:
+            cm.close()
+        assert g.n_reads == c.n_reads == (2 * n if paired else n)
+        assert (g.sam_hash, g.sam_bytes) == (c.sam_hash, c.sam_bytes), \
+            f"{name}: gpu {g.sam_hash:016x}/{g.sam_bytes} cpu {c.sam_hash:016x}/{c.sam_bytes}"
+        assert g.sw_calls == c.sw_calls and g.mate_rescue == c.mate_rescue
+        reads.close()
+    finally:
+        m.close()
