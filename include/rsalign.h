@@ -71,7 +71,13 @@ void rsam_reads_free(rsam_reads* r);
 int rsam_map(rsam* m, const rsam_reads* reads, int threads, int chunk_size, const char* sam_path,
              rsam_stats* out);
 
-/* GPU kernel statistics of the engine (zeros for a CPU engine). */
+/* Map on more devices of this node: each listed device gets its own engine with a
+ * full replica of the index; rsam_map then sends every seeding / extension call to
+ * the least busy device.  The SAM is the same for any number of devices (one chunk
+ * queue, global chunk_index seeding, one insert-size freeze, one ordered writer). */
+int rsam_add_devices(rsam* m, const int* devices, int n);
+
+/* GPU kernel statistics of the engine (summed over devices; zeros for a CPU engine). */
 int rsam_kernel_stats(rsam* m, rsa_kernel_stats* out);
 void rsam_reset_kernel_stats(rsam* m);
 const char* rsam_engine_name(const rsam* m);

@@ -51,6 +51,7 @@
 
 #include "rsa_dev.h"
 #include "../../../include/rsa_gpu.h"
+#include "rsa_seed.h"
 
 namespace {
 
@@ -420,7 +421,7 @@ rsa_index_build* rsa_index_build_run(int device, const char* ref_seq, const uint
     auto dalloc = [&](void** p, size_t bytes) -> hipError_t {
         hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 64));
         if (e == hipSuccess) tmp.push_back(*p); else *p = nullptr;
-        return e;
+        return e == hipSuccess ? rsa_poison(*p, std::max<size_t>(bytes, 64)) : e;
     };
     auto dfree = [&](void* p) {
         if (!p) return;

@@ -70,7 +70,7 @@ struct DevBuf {
         hipError_t e = hipMalloc(&p, n);
         if (e != hipSuccess) { p = nullptr; cap = 0; return e; }
         cap = n;
-        return hipSuccess;
+        return rsa_poison(p, n);
     }
     template <class T> T* as() const { return (T*)p; }
     void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
@@ -471,6 +471,10 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
         }
     }
     L->kt.end(st);
+    // every job's result is defined before any kernel reads it: the band kernels write
+    // the jobs they finish, and the CIGAR compaction below runs over all jobs, including
+    // the ones the 64-lane kernel leaves for the one-lane pass (empty CIGAR until then)
+    HIPCHK(hipMemsetAsync(L->d_alns.p, 0, sizeof(rsa_aln) * n, st));
     // 16 lanes per job for the common narrow bands; the rest queue for 64-lane waves
     L->kt.begin(st, RSA_K_EXT_BAND);
     launch_ext_band16(dim3((n + 3) / 4), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(), (int)n,

@@ -82,8 +82,12 @@ inline hipError_t stream_wait(hipStream_t s, hipEvent_t& e) {
         } else {
             std::unique_lock<std::mutex> l(w->m);
             while (!w->cv.wait_for(l, std::chrono::seconds(1), [&] { return w->done; })) {
-                const hipError_t q = hipStreamQuery(s);     // a failed stream never calls back
-                if (q != hipErrorNotReady && q != hipSuccess) { err = q; break; }
+                // a failed stream never calls back: look at it every second -- without
+                // holding w->m, which the runtime's callback thread needs to wake us
+                l.unlock();
+                const hipError_t q = hipStreamQuery(s);
+                l.lock();
+                if (q != hipErrorNotReady && q != hipSuccess && !w->done) { err = q; break; }
             }
             const bool done = w->done;
             l.unlock();
@@ -95,3 +99,12 @@ inline hipError_t stream_wait(hipStream_t s, hipEvent_t& e) {
 }
 
 void seed_bufs_release(SeedBufs& b);
+
+// RSA_POISON=1 (tests): fill every new device buffer with 0xA5 bytes, so a kernel
+// that reads memory nothing wrote sees the same garbage in every run instead of
+// whatever a freed allocation left (fresh pages happen to be zero).  Results never
+// depend on it; an uninitialised read then fails every time, not now and then.
+inline hipError_t rsa_poison(void* p, size_t n) {
+    static const bool on = getenv("RSA_POISON") && getenv("RSA_POISON")[0] == '1';
+    return on ? hipMemset(p, 0xA5, n) : hipSuccess;
+}

@@ -1491,7 +1491,7 @@ static hipError_t dens(SeedBufs& b, int i, size_t bytes) {
     hipError_t e = hipMalloc(&b.p[i], n);
     if (e != hipSuccess) { b.p[i] = nullptr; b.cap[i] = 0; return e; }
     b.cap[i] = n;
-    return hipSuccess;
+    return rsa_poison(b.p[i], n);
 }
 
 static hipError_t hens(SeedBufs& b, int i, size_t bytes) {

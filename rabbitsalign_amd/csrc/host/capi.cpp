@@ -359,6 +359,34 @@ int rsam_map(rsam* m, const rsam_reads* reads, int threads, int chunk_size, cons
     }
 }
 
+int rsam_add_devices(rsam* m, const int* devices, int n) {
+    if (!m || !m->eng || n < 0 || (n > 0 && !devices)) return -1;
+    try {
+        if (n == 0) return 0;
+        // a device-only index comes to the host once; every added device uploads it
+        if (!m->idx.host_copy() && !m->eng->download_index(m->idx))
+            throw std::runtime_error("rsam_add_devices: the index could not be copied to the host");
+        std::vector<std::unique_ptr<Engine>> more((size_t)n);
+        std::vector<std::exception_ptr> errs((size_t)n);
+        std::vector<std::thread> ts;
+        for (int i = 0; i < n; ++i)
+            ts.emplace_back([&, i]() {
+                try { more[i] = make_default_engine(m->refs, m->idx, devices[i]); }
+                catch (...) { errs[i] = std::current_exception(); }
+            });
+        for (auto& t : ts) t.join();
+        for (auto& e : errs) if (e) std::rethrow_exception(e);
+        std::vector<std::unique_ptr<Engine>> all;
+        all.push_back(std::move(m->eng));
+        for (auto& e : more) all.push_back(std::move(e));
+        m->eng = make_multi_engine(std::move(all));
+        return 0;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
 int rsam_kernel_stats(rsam* m, rsa_kernel_stats* out) {
     if (!m || !out) return -1;
     memset(out, 0, sizeof *out);

@@ -21,7 +21,7 @@ namespace {
 
 struct Opts {
     int threads = 3, chunk_size = 10000, device = 0, max_secondary = 0;
-    std::string out_file, rg_id, ref, reads1, reads2;
+    std::string out_file, rg_id, ref, reads1, reads2, devices;
     std::vector<std::string> rg;
     bool verbose = false, eqx = false, no_unmapped = false, details = false, create_index = false,
          use_index = false, interleaved = false, cpu_index = false;
@@ -39,6 +39,7 @@ void usage(const char* prog) {
             "       %s index [-r INT] [-o out.sti] [-t INT] [-b INT] <ref.fa>\n"
             "  -t INT threads [3]   --chunk-size INT [10000]   -o PATH   --eqx   -U   --details\n"
             "  --rg-id ID  --rg TAG:VALUE   -N INT   -i/--create-index   --use-index   --device INT   --cpu-index\n"
+            "  --devices LIST  map on several GPUs of this node (e.g. 0,1,2,3; index replicated per device)\n"
             "  seeding: -r -m -k -l -u -s -c -b      alignment: -A -B -O -E -L\n"
             "  search: -f FLOAT -S FLOAT -M INT -R INT\n",
             prog, prog);
@@ -71,6 +72,7 @@ Opts parse(int argc, char** argv, bool& ok) {
         else if (a == "--use-index") o.use_index = true;
         else if (a == "--cpu-index") o.cpu_index = true;
         else if (a == "--device") o.device = atoi(need(i));
+        else if (a == "--devices") o.devices = need(i);
         else if (a == "-r") { o.r = atoi(need(i)); o.r_set = true; }
         else if (a == "-m") o.m = atoi(need(i));
         else if (a == "-k") o.k = atoi(need(i));
@@ -174,7 +176,8 @@ int cli_main(int argc, char** argv, EngineFactory factory, const char* prog) {
         if (mp.max_tries < 1) throw std::runtime_error("max_tries must be greater than zero");
         mp.rescue_cutoff = mp.rescue_level < 100 ? mp.rescue_level * idx.filter_cutoff : 1000;
         auto t1 = std::chrono::steady_clock::now();
-        std::unique_ptr<Engine> eng = factory(refs, idx, o.device);
+        const std::vector<int> devs = o.devices.empty() ? std::vector<int>{o.device} : parse_devices(o.devices);
+        std::unique_ptr<Engine> eng = open_engines(factory, refs, idx, devs);
         const double t_upload = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
         FILE* out = o.out_file.empty() ? stdout : fopen(o.out_file.c_str(), "wb");
         if (!out) throw std::runtime_error("cannot open " + o.out_file);

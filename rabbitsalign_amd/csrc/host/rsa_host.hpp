@@ -532,6 +532,16 @@ PipelineResult run_pipeline_se(const std::vector<Record>& r, Engine& eng, const 
 
 // CLI entry (main.cpp); the oracle CPU binary reuses it with its own engine factory
 using EngineFactory = std::unique_ptr<Engine> (*)(const References&, const StiIndex&, int device);
+
+// Several engines behind one (multi.cpp): every seed/extend call goes to the engine
+// with the fewest calls in flight; the pipeline's chunk queue, chunk_index seeding,
+// insert-size freeze and ordered writer are shared, so the SAM does not depend on
+// the number of devices.  open_engines: one engine per device, each with a full
+// index replica (a device-only index is copied to the host once and uploaded).
+std::unique_ptr<Engine> make_multi_engine(std::vector<std::unique_ptr<Engine>> engines);
+std::unique_ptr<Engine> open_engines(EngineFactory factory, const References& refs, StiIndex& idx,
+                                     const std::vector<int>& devices);
+std::vector<int> parse_devices(const std::string& s);   // comma-separated ordinals
 int cli_main(int argc, char** argv, EngineFactory factory, const char* prog);
 
 }  // namespace rsa

@@ -40,7 +40,7 @@ class _Info(C.Structure):
 EXPORTED_SYMBOLS = [
     "rsam_open_files", "rsam_open_synthetic", "rsam_open_like", "rsam_close", "rsam_get_info",
     "rsam_reads_load", "rsam_reads_load_interleaved", "rsam_reads_synthetic", "rsam_reads_count", "rsam_reads_free", "rsam_map",
-    "rsam_kernel_stats", "rsam_reset_kernel_stats", "rsam_engine_name", "rsam_last_error",
+    "rsam_add_devices", "rsam_kernel_stats", "rsam_reset_kernel_stats", "rsam_engine_name", "rsam_last_error",
 ]
 
 _LIBS: dict = {}
@@ -63,6 +63,7 @@ def load(path: str = PRODUCT_LIB) -> C.CDLL:
     lib.rsam_get_info.argtypes = [vp, C.POINTER(_Info)]
     lib.rsam_reads_load.restype = vp
     lib.rsam_reads_load.argtypes = [cp, cp]
+    lib.rsam_add_devices.argtypes = [vp, C.POINTER(C.c_int), i32]
     lib.rsam_reads_load_interleaved.restype = vp
     lib.rsam_reads_load_interleaved.argtypes = [cp]
     lib.rsam_reads_synthetic.restype = vp
@@ -177,6 +178,12 @@ class Mapper:
         if rc != 0:
             raise RuntimeError(f"rsam_map: {self._lib.rsam_last_error().decode()}")
         return MapStats(**{f: getattr(st, f) for f, _ in _Stats._fields_})
+
+    def add_devices(self, devices):
+        """Replicate the index on more devices and spread the mapping calls over them."""
+        arr = (C.c_int * len(devices))(*devices)
+        if self._lib.rsam_add_devices(self._h, arr, len(devices)) != 0:
+            raise RuntimeError(f"rsam_add_devices: {self._lib.rsam_last_error().decode()}")
 
     def kernel_stats(self) -> dict:
         ks = KernelStats()

@@ -79,3 +79,33 @@ def test_extend_band_paths_exercised(ctx):
     assert st["band_overflow"] > 0, st
     k = st["kernels"]
     assert k["ext_band_wide"]["launches"] > 0 and k["ext_band_lane"]["launches"] > 0
+
+
+@pytest.mark.gpu
+def test_extend_hand_derived_cases():
+    """The GPU path on the hand-derived Aligner::align cases (tests/wrapper_cases.py)."""
+    from rabbitsalign_amd import native
+    from wrapper_cases import cases
+    from jobgen import JOB_DTYPE
+    cs = cases()
+    ref = b"".join(r for _, _, r, _ in cs)
+    offs = np.zeros(len(cs) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(r) for _, _, r, _ in cs])
+    ctx = native.GpuContext(native.empty_index(np.frombuffer(ref, np.uint8).copy(), offs))
+    try:
+        queries = b"".join(q for _, q, _, _ in cs)
+        jobs = np.zeros(len(cs), dtype=JOB_DTYPE)
+        qo = 0
+        for i, (_, q, r, _) in enumerate(cs):
+            jobs[i] = (qo, len(q), i, 0, len(r))
+            qo += len(q)
+        alns, pool = ctx.extend(queries, jobs)
+        for i, (name, q, r, want) in enumerate(cs):
+            a = alns[i]
+            got = dict(sw_score=int(a["sw_score"]), edit_distance=int(a["edit_distance"]), ref_start=int(a["ref_start"]),
+                       ref_end=int(a["ref_end"]), query_start=int(a["query_start"]), query_end=int(a["query_end"]),
+                       cigar=[int(x) for x in pool[int(a["cigar_offset"]):int(a["cigar_offset"]) + int(a["cigar_len"])]])
+            for k, v in want.items():
+                assert got[k] == v, (name, k, got[k], v)
+    finally:
+        ctx.close()

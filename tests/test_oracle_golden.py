@@ -63,3 +63,16 @@ def test_aligner_wrapper_basic():
     q2 = b"T" + q[1:]
     a2 = oracle_lib.align(q2, r)
     assert a2["query_start"] == 0 and a2["cigar"][0] == (1 << 4) | 8
+
+
+def test_aligner_wrapper_hand_derived():
+    """The oracle's Aligner::align restatement on hand-derived cases (tests/wrapper_cases.py):
+    end bonus at both ends, front/back extension replacing a soft clip, the equal-score
+    case that keeps it, N == N as '=', a clip at reference start, the >2000 sentinel."""
+    from wrapper_cases import cases
+    for name, q, r, want in cases():
+        got = oracle_lib.align(q, r)
+        if want is None:
+            continue
+        for k, v in want.items():
+            assert got[k] == v, (name, k, got[k], v)
