@@ -42,10 +42,15 @@ WORKLOADS = {
 }
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md "Chip-level parameters")
-# VALU ceiling of the DP scan (DESIGN.md §3 "Roofline reporting"): 256 CUs x 128 lane-ops/clk
-# (4 SIMD-32 per CU, MI355X_MICROARCH.md "Wave scheduling") x 2.4 GHz = 78.6 T int ops/s;
-# x 2 for packed int16 / 12 ops per cell update = 13.1 T cells/s
-DP_PEAK_GCELLS = 256 * 128 * 2.4 * 2 / 12
+# VALU ceilings of the DP scan (DESIGN.md §3 "Roofline reporting"), in cell updates/s with
+# SURVEY.md §8d's model of 12 ops per cell and 2 cells per packed op:
+#  - measured: 600 G wave64 VALU instructions/s chip-wide, the issue ceiling of independent
+#    packed-f16 / int32 streams at 4-8 waves per SIMD (scripts/micro/valu_lat.hip,
+#    profiles/r02_valu_ceiling.txt) -> 600e9 x 64 lanes x 2 / 12 = 6.4 T cells/s (the roofline peak);
+#  - spec model: 256 CUs x 128 lane-ops/clk x 2.4 GHz x 2 / 12 = 13.1 T cells/s (reported beside it)
+VALU_WAVE_INSTR_PER_S = 600e9
+DP_PEAK_GCELLS = VALU_WAVE_INSTR_PER_S * 64 * 2 / 12 / 1e9
+DP_SPEC_GCELLS = 256 * 128 * 2.4 * 2 / 12
 REF_CPU_LIB = os.path.join(ROOT, "oracle", "_ref", "librsalign_ref.so")
 
 
@@ -122,6 +127,9 @@ def kernel_roofline(name: str, k: dict, ks: dict) -> dict:
         achieved = cells / avg_s / 1e9
         out.update({"bound": "valu", "achieved": round(achieved, 2), "peak": round(DP_PEAK_GCELLS, 1),
                     "unit": "Gcells/s", "frac": round(achieved / DP_PEAK_GCELLS, 5),
+                    "peak_source": "measured VALU issue ceiling, profiles/r02_valu_ceiling.txt",
+                    "spec_model": {"peak": round(DP_SPEC_GCELLS, 1),
+                                   "frac": round(achieved / DP_SPEC_GCELLS, 5)},
                     "cells_per_launch": round(cells, 1),
                     "hbm_GBps": round(per_launch_bytes / avg_s / 1e9, 3)})
     else:

@@ -3,6 +3,8 @@
 // (rsa_oracle.c) instead of the GPU.  TEST INFRASTRUCTURE ONLY: it is the
 // parity reference for end-to-end SAM and bench.py's cpu_baseline leg.
 #include <atomic>
+#include <cstdio>
+#include <mutex>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -63,6 +65,16 @@ public:
         // makes the N-th extend call throw, as a failed GPU call does in the product engine
         static const long fail_at = getenv("RSA_TEST_FAIL_EXTEND") ? atol(getenv("RSA_TEST_FAIL_EXTEND")) : 0;
         if (fail_at > 0 && ++calls_ == fail_at) throw std::runtime_error("injected extend failure");
+        // job-shape histogram for kernel design (RSA_TEST_JOB_HIST=file; test infrastructure)
+        static const char* hist_path = getenv("RSA_TEST_JOB_HIST");
+        if (hist_path) {
+            static std::mutex hm;
+            std::lock_guard<std::mutex> g(hm);
+            if (FILE* f = fopen(hist_path, "a")) {
+                for (const auto& j : jobs) fprintf(f, "%zu %u\n", j.query.size(), (unsigned)j.ref_len);
+                fclose(f);
+            }
+        }
         out.assign(jobs.size(), rsa::AlignmentInfo());
         std::vector<uint32_t> cig;
         for (size_t i = 0; i < jobs.size(); ++i) {

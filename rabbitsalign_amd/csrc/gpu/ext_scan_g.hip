@@ -16,19 +16,28 @@
 //     15 steps instead of 50.  The host hands the jobs over sorted by window
 //     length, so the four jobs of a wave run nearly the same number of steps.
 //
-// Cell recurrence.  SSW keeps E and F saturated at >= 0; here only the
-// diagonal term is clamped (H = max(max(diag, 0), E, Fw, F)).  E, Fw and F may
-// go negative but stay >= -gap_open (their update is a max with H - gap_open),
-// and their positive parts -- the only parts that can reach H -- follow
-// exactly the saturated recurrence, so every H is SSW's.
+// Cell recurrence (SSW's, ssw.c:197-588): E, Fw (within-stripe F) and F are
+// kept >= 0 as SSW saturates them, so H = max(diag, E, Fw, F, 0) is
+// max3(diag, E, Fw) then a max with F; E and Fw take hm - gap_open, where hm
+// leaves out the cross-stripe F (the striping artefact: that F never feeds E).
+// F' = max(F - gE, H - gO) = max(F - gE, hm - gO) because F - gO <= F - gE
+// (the host routes gap_open < gap_extend elsewhere): F's dependency chain
+// through the rows is two instructions.
+//
+// Arithmetic: the forward pass runs in packed half precision (v_pk_*_f16 and
+// gfx950's three-input v_pk_maximum3_f16): every value is an integer of
+// magnitude < 2048 (host-checked: match * 256 <= 2048 and penalties <= 1024),
+// which f16 holds exactly, so every H is SSW's.  Scores are >= +0, whose f16
+// bit patterns order like the values: the column maximum is tracked on bits.
+// The reverse pass is int32 with v_max3_i32.
 //
 // Column maxima of the forward pass include the padding rows of the last lane
-// (rows >= nrow) without a mask: with non-negative mismatch/gap penalties (the
-// host routes other parameters to k_ext_scan) every move into a padding row
-// loses or keeps score (never a match there) and its only entries are this
-// lane's last valid row, so a padding cell never exceeds the best valid cell of
-// the same lane so far; whenever the column max improves the lane's best it is
-// a valid cell's value, and the row search only looks at valid rows.
+// (rows >= nrow) without a mask: with non-negative mismatch/gap penalties
+// every move into a padding row loses or keeps score (never a match there) and
+// its only entries are this lane's last valid row, so a padding cell never
+// exceeds the best valid cell of the same lane so far; whenever the column max
+// improves the lane's best it is a valid cell's value, and the row search only
+// looks at valid rows.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <climits>
@@ -42,11 +51,21 @@
 
 namespace {
 
-typedef short pk16 __attribute__((ext_vector_type(2)));
+typedef _Float16 hh2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ pk16 pk_from(uint32_t x) { return __builtin_bit_cast(pk16, x); }
-__device__ __forceinline__ uint32_t pk_bits(pk16 x) { return __builtin_bit_cast(uint32_t, x); }
-__device__ __forceinline__ pk16 pk_max(pk16 a, pk16 b) { return __builtin_elementwise_max(a, b); }
+__device__ __forceinline__ hh2 h2_from(uint32_t x) { return __builtin_bit_cast(hh2, x); }
+__device__ __forceinline__ uint32_t h2_bits(hh2 x) { return __builtin_bit_cast(uint32_t, x); }
+// IEEE maximum: one v_pk_maximum3_f16, no canonicalisation (values are never NaN)
+__device__ __forceinline__ hh2 hmax(hh2 a, hh2 b) { return __builtin_elementwise_maximum(a, b); }
+__device__ __forceinline__ hh2 hmax3(hh2 a, hh2 b, hh2 c) { return hmax(hmax(a, b), c); }
+__device__ __forceinline__ uint32_t h2_pair(int v) {
+    const _Float16 h = (_Float16)v;
+    const uint32_t b = (uint32_t)__builtin_bit_cast(uint16_t, h);
+    return b | (b << 16);
+}
+__device__ __forceinline__ int h_bits_to_int(uint32_t bits16) {
+    return (int)(float)__builtin_bit_cast(_Float16, (uint16_t)bits16);
+}
 
 // lane l receives lane l-1 of its 16-lane row; the row's first lane receives 0
 __device__ __forceinline__ uint32_t row_shr1(uint32_t v) {
@@ -73,59 +92,63 @@ __device__ __forceinline__ int ssw_code_sel(uint32_t c) {
 }
 
 struct FwdG {
-    int best[2], col[2], row[2];     // [0] byte layout, [1] word layout
+    int best[2], col[2], row[2];     // [0] byte layout, [1] word layout; best as f16 bits
 };
 
-// forward pass, both layouts at once; row p of this lane is gl * R + r
-template <int R, bool MASK>
+// forward pass, both layouts at once (low half: byte layout, 16 stripes; high
+// half: word layout, 8 stripes); row p of this lane is gl * R + r
+template <int R>
 __device__ __forceinline__ FwdG fwd_g(const int (&qv)[R], int nrow, const uint8_t* __restrict__ rc, int ncol, int S,
                                       bool on, int match, int mismatch, int gO, int gE, int gl) {
     const int seg_b = (nrow + 15) / 16, seg_w = (nrow + 7) / 8;
-    pk16 E[R], Hc[R];
-    uint32_t ssm[R], vm[R];
-    const pk16 zero = {0, 0};
-    const pk16 GO2 = {(short)gO, (short)gO}, GE2 = {(short)gE, (short)gE};
-    const uint32_t M2 = pk_bits((pk16){(short)match, (short)match});
-    const uint32_t X2 = pk_bits((pk16){(short)-mismatch, (short)-mismatch});
+    hh2 E[R], Hc[R];
+    uint32_t ssm[R];
+    const hh2 zero = h2_from(0u);
+    const hh2 GO2 = h2_from(h2_pair(gO)), GE2 = h2_from(h2_pair(gE));
+    uint32_t M2 = h2_pair(match), X2 = h2_pair(-mismatch);
+    // keep the two packed scores in registers: otherwise the compiler selects the
+    // integer score per row and converts it to packed f16 there (4 more ops a cell)
+    asm volatile("" : "+v"(M2), "+v"(X2));
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         E[r] = zero;
         Hc[r] = zero;
         const int p = gl * R + r;
         ssm[r] = ((p % seg_b) == 0 ? 0u : 0x0000FFFFu) | ((p % seg_w) == 0 ? 0u : 0xFFFF0000u);
-        vm[r] = p < nrow ? 0xFFFFFFFFu : 0u;
     }
     uint32_t F_out = 0, Fw_out = 0, H_last = 0, diag_top = 0;
     FwdG o;
     o.best[0] = o.best[1] = 0;
     o.col[0] = o.col[1] = INT_MAX;
     o.row[0] = o.row[1] = INT_MAX;
+    int rnext = (on && gl == 0 && ncol > 0) ? rc[0] : 0;     // the next step's reference code, loaded a step ahead
     for (int s = 0; s < S; ++s) {
         const uint32_t F_in = row_shr1(F_out);
         const uint32_t Fw_in = row_shr1(Fw_out);
         const uint32_t Hl_in = row_shr1(H_last);
         const int c = s - gl;
+        const int rcode = rnext;
+        if (on && c + 1 >= 0 && c + 1 < ncol) rnext = rc[c + 1];
         if (on && c >= 0 && c < ncol) {
-            const int rcode = rc[c];
-            pk16 dg = pk_from(diag_top), F = pk_from(F_in), Fw = pk_from(Fw_in), cm = zero;
+            hh2 dg = h2_from(diag_top), F = h2_from(F_in), Fw = h2_from(Fw_in), cm = zero;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                Fw = pk_from(pk_bits(Fw) & ssm[r]);
-                const pk16 diag = pk_max(dg + pk_from(qv[r] == rcode ? M2 : X2), zero);
-                const pk16 hm = pk_max(pk_max(diag, E[r]), Fw);
-                const pk16 h = pk_max(hm, F);
+                Fw = h2_from(h2_bits(Fw) & ssm[r]);
+                const hh2 diag = dg + h2_from(qv[r] == rcode ? M2 : X2);
+                const hh2 hm = hmax3(diag, E[r], Fw);
+                const hh2 h = hmax(hm, F);
                 dg = Hc[r];
                 Hc[r] = h;
-                const pk16 t = hm - GO2;
-                E[r] = pk_max(E[r] - GE2, t);
-                Fw = pk_max(Fw - GE2, t);
-                F = pk_max(F - GE2, h - GO2);
-                cm = pk_max(cm, MASK ? pk_from(pk_bits(h) & vm[r]) : h);
+                const hh2 t = hm - GO2;
+                E[r] = hmax3(E[r] - GE2, t, zero);
+                Fw = hmax3(Fw - GE2, t, zero);
+                F = hmax3(F - GE2, t, zero);
+                cm = hmax(cm, h);
             }
-            F_out = pk_bits(F);
-            Fw_out = pk_bits(Fw);
-            H_last = pk_bits(Hc[R - 1]);
-            const uint32_t cmb = pk_bits(cm);
+            F_out = h2_bits(F);
+            Fw_out = h2_bits(Fw);
+            H_last = h2_bits(Hc[R - 1]);
+            const uint32_t cmb = h2_bits(cm);
 #pragma unroll
             for (int hf = 0; hf < 2; ++hf) {
                 const int v = (int)((cmb >> (16 * hf)) & 0xFFFFu);
@@ -135,7 +158,7 @@ __device__ __forceinline__ FwdG fwd_g(const int (&qv)[R], int nrow, const uint8_
                     int row = INT_MAX;
 #pragma unroll
                     for (int r = R - 1; r >= 0; --r)
-                        if (vm[r] && (int)((pk_bits(Hc[r]) >> (16 * hf)) & 0xFFFFu) == v) row = gl * R + r;
+                        if (gl * R + r < nrow && (int)((h2_bits(Hc[r]) >> (16 * hf)) & 0xFFFFu) == v) row = gl * R + r;
                     o.row[hf] = row;
                 }
             }
@@ -144,6 +167,8 @@ __device__ __forceinline__ FwdG fwd_g(const int (&qv)[R], int nrow, const uint8_
     }
     return o;
 }
+
+__device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
 
 // reverse pass (one layout, int32): row p -> query qend - p, column c -> ref rend - c.
 // Returns the first column whose valid-row maximum equals `terminate` (and its
@@ -167,38 +192,43 @@ __device__ __forceinline__ void rev_g(const int (&qr)[R], int nrow, const uint8_
     tcol = INT_MAX;
     trow = INT_MAX;
     bool done = !on;
+    int rnext = (on && gl == 0 && ncol > 0) ? rc[rend] : 0;   // the next step's reference code, a step ahead
     for (int s = 0; s < S; ++s) {
         const int F_in = (int)row_shr1((uint32_t)F_out);
         const int Fw_in = (int)row_shr1((uint32_t)Fw_out);
         const int Hl_in = (int)row_shr1((uint32_t)H_last);
         const int c = s - gl;
+        const int rcode = rnext;
+        if (on && c + 1 >= 0 && c + 1 < ncol) rnext = rc[rend - (c + 1)];
         if (on && c >= 0 && c < ncol) {
-            const int rcode = rc[rend - c];
             int dg = diag_top, F = F_in, Fw = Fw_in, cm = 0;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 Fw &= ssm[r];
-                const int diag = max(dg + (qr[r] == rcode ? match : -mismatch), 0);
-                const int hm = max(max(diag, E[r]), Fw);
+                const int diag = dg + (qr[r] == rcode ? match : -mismatch);
+                const int hm = max3i(diag, E[r], Fw);          // E, Fw >= 0: the 0 of max(diag, 0)
                 const int h = max(hm, F);
                 dg = Hc[r];
                 Hc[r] = h;
                 const int t = hm - gO;
-                E[r] = max(E[r] - gE, t);
-                Fw = max(Fw - gE, t);
-                F = max(F - gE, h - gO);
+                E[r] = max3i(E[r] - gE, t, 0);
+                Fw = max3i(Fw - gE, t, 0);
+                F = max3i(F - gE, t, 0);
                 cm = max(cm, valid[r] ? h : 0);
             }
             F_out = F;
             Fw_out = Fw;
             H_last = Hc[R - 1];
-            if (cm == terminate && tcol == INT_MAX) {
-                tcol = c;
-                int row = INT_MAX;
+            const bool hit = cm == terminate && tcol == INT_MAX;
+            if (__builtin_amdgcn_ballot_w64(hit)) {        // at most once a job: skip the row search otherwise
+                if (hit) {
+                    tcol = c;
+                    int row = INT_MAX;
 #pragma unroll
-                for (int r = R - 1; r >= 0; --r)
-                    if (valid[r] && Hc[r] == terminate) row = gl * R + r;
-                trow = row;
+                    for (int r = R - 1; r >= 0; --r)
+                        if (valid[r] && Hc[r] == terminate) row = gl * R + r;
+                    trow = row;
+                }
             }
         }
         diag_top = Hl_in;
@@ -216,7 +246,7 @@ __device__ __forceinline__ void rev_g(const int (&qr)[R], int nrow, const uint8_
 // jobs[order[k]] for k < n; results land at out[order[k]].  Every job handed
 // here has 0 < qlen <= 16 * R and rlen <= GS_MAXR (the host routes the rest to
 // k_ext_scan).
-template <int R, bool MASK>
+template <int R>
 __global__ void __launch_bounds__(64 * GS_WAVES)
 k_ext_scan_g(const ExtJobDev* __restrict__ jobs, const int* __restrict__ order, int n,
              const char* __restrict__ qbuf, const char* __restrict__ ref, ScanRes* __restrict__ out,
@@ -258,17 +288,20 @@ k_ext_scan_g(const ExtJobDev* __restrict__ jobs, const int* __restrict__ order, 
     // forward pass: every job of the wave runs until the longest one is done
     const int lanes_used = (qlen + R - 1) / R;
     const int S = wave_max_i32(on ? rlen + lanes_used - 1 : 0);
-    const FwdG fo = fwd_g<R, MASK>(qv, qlen, rc, rlen, S, on && gl < lanes_used, match, mismatch, gO, gE, gl);
-    const int sb = grp_max(fo.best[0]);
+    const FwdG fo = fwd_g<R>(qv, qlen, rc, rlen, S, on && gl < lanes_used, match, mismatch, gO, gE, gl);
+    // maxima as f16 bit patterns (order-preserving for values >= +0)
+    const int bb = grp_max(fo.best[0]);
+    const int sb = h_bits_to_int((uint32_t)bb);
     const int word = sb + mismatch >= 255 ? 1 : 0;
-    const int score1 = word ? grp_max(fo.best[1]) : sb;
+    const int bw = word ? grp_max(fo.best[1]) : bb;
+    const int score1 = word ? h_bits_to_int((uint32_t)bw) : sb;
     int ref_end1, read_end1;
     if (score1 == 0) {
         ref_end1 = word ? 0 : -1;
         read_end1 = 0;
     } else {
-        ref_end1 = grp_min(fo.best[word] == score1 ? fo.col[word] : INT_MAX);
-        read_end1 = grp_min((fo.best[word] == score1 && fo.col[word] == ref_end1) ? fo.row[word] : INT_MAX);
+        ref_end1 = grp_min(fo.best[word] == bw ? fo.col[word] : INT_MAX);
+        read_end1 = grp_min((fo.best[word] == bw && fo.col[word] == ref_end1) ? fo.row[word] : INT_MAX);
     }
 
     // reverse pass (ssw.c:877-893) on read[0..read_end1] x ref[0..ref_end1], reversed
@@ -328,18 +361,24 @@ int scan_g_rows(uint32_t qlen) {
 
 int scan_g_max_ref() { return GS_MAXR; }
 
-void launch_ext_scan_g(int rows, bool mask, int n, hipStream_t st, const ExtJobDev* jobs, const int* order,
-                       const char* q, const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE) {
+void launch_ext_scan_g(int rows, int n, hipStream_t st, const ExtJobDev* jobs, const int* order, const char* q,
+                       const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE) {
     if (n <= 0) return;
     const dim3 grid((n + GS_JOBS - 1) / GS_JOBS), block(64 * GS_WAVES);
 #define RSA_G(RR)                                                                                               \
     if (rows == RR) {                                                                                           \
-        if (mask) hipLaunchKernelGGL((k_ext_scan_g<RR, true>), grid, block, 0, st, jobs, order, n, q, ref, out,  \
-                                     match, mismatch, gO, gE);                                                  \
-        else hipLaunchKernelGGL((k_ext_scan_g<RR, false>), grid, block, 0, st, jobs, order, n, q, ref, out,     \
-                                match, mismatch, gO, gE);                                                       \
+        hipLaunchKernelGGL((k_ext_scan_g<RR>), grid, block, 0, st, jobs, order, n, q, ref, out, match, mismatch, \
+                           gO, gE);                                                                             \
         return;                                                                                                 \
     }
     RSA_G(4) RSA_G(7) RSA_G(10) RSA_G(13) RSA_G(16)
 #undef RSA_G
+}
+
+// parameters the grouped scan computes exactly: half-precision integers stay
+// below 2048 in magnitude (scores up to match * 256, penalties), and F's
+// shortened recurrence needs gap_open >= gap_extend
+bool scan_g_params_ok(int match, int mismatch, int gO, int gE) {
+    return match >= 0 && match * 256 <= 2048 && mismatch >= 0 && mismatch <= 1024 && gO >= 0 && gO <= 1024 &&
+           gE >= 0 && gE <= gO;
 }

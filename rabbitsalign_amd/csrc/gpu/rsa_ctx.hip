@@ -25,8 +25,9 @@ void launch_ext_scan(int rmax, dim3 grid, dim3 block, hipStream_t st, const ExtJ
                      const char* q, const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE);
 int scan_g_rows(uint32_t qlen);
 int scan_g_max_ref();
-void launch_ext_scan_g(int rows, bool mask, int n, hipStream_t st, const ExtJobDev* jobs, const int* order,
-                       const char* q, const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE);
+void launch_ext_scan_g(int rows, int n, hipStream_t st, const ExtJobDev* jobs, const int* order, const char* q,
+                       const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE);
+bool scan_g_params_ok(int match, int mismatch, int gO, int gE);
 __global__ void k_ext_band(const ExtJobDev* jobs, const ScanRes* scan, int n_jobs, const int* idx_list, int job_base,
                            const char* qbuf, const char* ref, uint32_t* cig_pool, rsa_aln* out, uint8_t* scratch,
                            int64_t scr_stride, int arr_cap, int64_t dir_cap, int match, int mismatch, int gO,
@@ -404,12 +405,10 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
     HIPCHK(hipMemcpyAsync(L->d_jobs.p, hj, sizeof(ExtJobDev) * n, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemsetAsync(L->d_status.p, 0, sizeof(ExtStatus), st));
     // Scan routing: jobs the grouped kernel takes (query <= 256 bp, window <= 1 KB,
-    // packed-int16 parameters) go to it per rows-per-lane class, sorted by window
+    // parameters it computes exactly) go to it per rows-per-lane class, sorted by window
     // length (longest first) so the four jobs of a wave run about as long; the
     // rest -- and sentinels -- to the one-job-per-wave kernel via an index list.
-    const bool packed_ok = jb->match >= 0 && jb->match <= 28 && jb->mismatch >= 0 && jb->mismatch < 4000 &&
-                           jb->gap_open >= 0 && jb->gap_open < 4000 && jb->gap_extend >= 0 && jb->gap_extend < 4000;
-    const bool grouped = packed_ok;
+    const bool grouped = scan_g_params_ok(jb->match, jb->mismatch, jb->gap_open, jb->gap_extend);
     constexpr int NCLS = 5;
     static const int cls_rows[NCLS] = {4, 7, 10, 13, 16};
     uint32_t cls_n[NCLS] = {0}, rest_n = 0;
@@ -457,7 +456,7 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
         uint32_t off = 0;
         for (int c = 0; c < NCLS; ++c) {
             if (!cls_n[c]) continue;
-            launch_ext_scan_g(cls_rows[c], false, (int)cls_n[c], st, L->d_jobs.as<ExtJobDev>(), d_ord + off,
+            launch_ext_scan_g(cls_rows[c], (int)cls_n[c], st, L->d_jobs.as<ExtJobDev>(), d_ord + off,
                               L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(), jb->match, jb->mismatch,
                               jb->gap_open, jb->gap_extend);
             HIPCHK(hipGetLastError());
