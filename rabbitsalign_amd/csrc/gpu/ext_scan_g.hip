@@ -46,7 +46,8 @@
 #include "rsa_ext.h"
 
 #define GS_WAVES 4
-#define GS_JOBS (GS_WAVES * 4)   // jobs per workgroup
+#define GS_G 16                  // lanes per job: a DPP row (32, half a wave, measured slower at chunk size)
+#define GS_JOBS (GS_WAVES * (64 / GS_G))   // jobs per workgroup
 #define GS_MAXR 1024             // reference window bytes staged in LDS per job
 
 namespace {
@@ -67,16 +68,22 @@ __device__ __forceinline__ int h_bits_to_int(uint32_t bits16) {
     return (int)(float)__builtin_bit_cast(_Float16, (uint16_t)bits16);
 }
 
-// lane l receives lane l-1 of its 16-lane row; the row's first lane receives 0
+// lane l of a job's lane group receives lane l-1; the group's first lane receives 0
+// (16 lanes: DPP row_shr:1; 32 lanes: DPP wave_shr:1 with the group's first lane cleared)
 __device__ __forceinline__ uint32_t row_shr1(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+    if constexpr (GS_G == 16) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+    } else {
+        const uint32_t x = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+        return (threadIdx.x & (GS_G - 1)) ? x : 0u;
+    }
 }
 __device__ __forceinline__ int grp_max(int v) {
-    for (int o = 8; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 16));
+    for (int o = GS_G / 2; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, GS_G));
     return v;
 }
 __device__ __forceinline__ int grp_min(int v) {
-    for (int o = 8; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 16));
+    for (int o = GS_G / 2; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, GS_G));
     return v;
 }
 
@@ -244,7 +251,7 @@ __device__ __forceinline__ void rev_g(const int (&qr)[R], int nrow, const uint8_
 }  // namespace
 
 // jobs[order[k]] for k < n; results land at out[order[k]].  Every job handed
-// here has 0 < qlen <= 16 * R and rlen <= GS_MAXR (the host routes the rest to
+// here has 0 < qlen <= GS_G * R and rlen <= GS_MAXR (the host routes the rest to
 // k_ext_scan).
 template <int R>
 __global__ void __launch_bounds__(64 * GS_WAVES)
@@ -253,7 +260,7 @@ k_ext_scan_g(const ExtJobDev* __restrict__ jobs, const int* __restrict__ order, 
              int match, int mismatch, int gO, int gE) {
     __shared__ uint8_t s_r[GS_JOBS][GS_MAXR];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int slot = wave * 4 + (lane >> 4), gl = lane & 15;
+    const int slot = wave * (64 / GS_G) + lane / GS_G, gl = lane & (GS_G - 1);
     const int k = blockIdx.x * GS_JOBS + slot;
     const bool on = k < n;
     const int j = on ? order[k] : 0;
@@ -267,7 +274,7 @@ k_ext_scan_g(const ExtJobDev* __restrict__ jobs, const int* __restrict__ order, 
         const int pre = (int)(jb.r_off & 3);
         const uint32_t* w = (const uint32_t*)(ref + (jb.r_off - (uint64_t)pre));
         const int nw = (pre + rlen + 3) >> 2;
-        for (int i = gl; i < nw; i += 16) {
+        for (int i = gl; i < nw; i += GS_G) {
             const uint32_t x = w[i];
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
@@ -351,15 +358,29 @@ k_ext_scan_g(const ExtJobDev* __restrict__ jobs, const int* __restrict__ order, 
 // rows per lane of the grouped scan for a query length (0: not handled here)
 int scan_g_rows(uint32_t qlen) {
     if (qlen == 0) return 0;
-    if (qlen <= 64) return 4;
-    if (qlen <= 112) return 7;
-    if (qlen <= 160) return 10;
-    if (qlen <= 208) return 13;
-    if (qlen <= 256) return 16;
+    if constexpr (GS_G == 16) {
+        if (qlen <= 64) return 4;
+        if (qlen <= 112) return 7;
+        if (qlen <= 160) return 10;
+        if (qlen <= 208) return 13;
+        if (qlen <= 256) return 16;
+    } else {
+        if (qlen <= 64) return 2;
+        if (qlen <= 128) return 4;
+        if (qlen <= 160) return 5;
+        if (qlen <= 224) return 7;
+        if (qlen <= 256) return 8;
+    }
     return 0;
 }
 
 int scan_g_max_ref() { return GS_MAXR; }
+
+// the five rows-per-lane classes, ascending
+void scan_g_classes(int* rows5) {
+    static const int r16[5] = {4, 7, 10, 13, 16}, r32[5] = {2, 4, 5, 7, 8};
+    for (int i = 0; i < 5; ++i) rows5[i] = GS_G == 16 ? r16[i] : r32[i];
+}
 
 void launch_ext_scan_g(int rows, int n, hipStream_t st, const ExtJobDev* jobs, const int* order, const char* q,
                        const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE) {
@@ -371,7 +392,8 @@ void launch_ext_scan_g(int rows, int n, hipStream_t st, const ExtJobDev* jobs, c
                            gO, gE);                                                                             \
         return;                                                                                                 \
     }
-    RSA_G(4) RSA_G(7) RSA_G(10) RSA_G(13) RSA_G(16)
+    if constexpr (GS_G == 16) { RSA_G(4) RSA_G(7) RSA_G(10) RSA_G(13) RSA_G(16) }
+    else { RSA_G(2) RSA_G(4) RSA_G(5) RSA_G(7) RSA_G(8) }
 #undef RSA_G
 }
 

@@ -24,6 +24,7 @@
 void launch_ext_scan(int rmax, dim3 grid, dim3 block, hipStream_t st, const ExtJobDev* jobs, int n, const int* idx,
                      const char* q, const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE);
 int scan_g_rows(uint32_t qlen);
+void scan_g_classes(int* rows5);
 int scan_g_max_ref();
 void launch_ext_scan_g(int rows, int n, hipStream_t st, const ExtJobDev* jobs, const int* order, const char* q,
                        const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE);
@@ -410,7 +411,8 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
     // rest -- and sentinels -- to the one-job-per-wave kernel via an index list.
     const bool grouped = scan_g_params_ok(jb->match, jb->mismatch, jb->gap_open, jb->gap_extend);
     constexpr int NCLS = 5;
-    static const int cls_rows[NCLS] = {4, 7, 10, 13, 16};
+    int cls_rows[NCLS];
+    scan_g_classes(cls_rows);
     uint32_t cls_n[NCLS] = {0}, rest_n = 0;
     HIPCHK(L->h_order.ensure(sizeof(int) * (n + 1)));
     int* ord = L->h_order.as<int>();
