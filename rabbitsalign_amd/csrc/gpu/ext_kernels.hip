@@ -661,6 +661,8 @@ __device__ __forceinline__ int gshr(int v) {
     // lane z of the group receives lane z-S; z < S receives BG_NEG
     if constexpr (G == 16) {
         return __builtin_amdgcn_update_dpp(BG_NEG, v, 0x110 + S, 0xf, 0xf, false);
+    } else if constexpr (S == 1) {
+        return __builtin_amdgcn_update_dpp(BG_NEG, v, 0x138, 0xf, 0xf, false);   // DPP wave_shr:1
     } else {
         const int x = __shfl_up(v, S, 64);
         return (int)(threadIdx.x & 63) < S ? BG_NEG : x;
@@ -687,18 +689,34 @@ __device__ __forceinline__ int gmax(int v) {
     return v;
 }
 
+// X_z = max over m <= z of (A_m - (z - m) gE): a max-plus prefix scan.  16 lanes:
+// DPP row_shr 1, 2, 4, 8.  64 lanes: the same within each 16-lane row, then the
+// rows joined with the GFX9 DPP broadcasts (row_bcast:15 hands lane 15 of rows
+// 0 and 2 to rows 1 and 3, row_bcast:31 lane 31 to rows 2 and 3), each lane
+// charging the gap extension over its distance to the broadcasting lane -- no
+// LDS round trip (ds_bpermute) in the row loop.
 template <int G>
 __device__ __forceinline__ int gscan_f(int A, int gE) {
-    int X = A;
-    X = max(X, gshr<G, 1>(X) - gE);
-    X = max(X, gshr<G, 2>(X) - 2 * gE);
-    X = max(X, gshr<G, 4>(X) - 4 * gE);
-    X = max(X, gshr<G, 8>(X) - 8 * gE);
-    if constexpr (G > 16) {
-        X = max(X, gshr<G, 16>(X) - 16 * gE);
-        X = max(X, gshr<G, 32>(X) - 32 * gE);
+    if constexpr (G == 16) {
+        int X = A;
+        X = max(X, gshr<G, 1>(X) - gE);
+        X = max(X, gshr<G, 2>(X) - 2 * gE);
+        X = max(X, gshr<G, 4>(X) - 4 * gE);
+        X = max(X, gshr<G, 8>(X) - 8 * gE);
+        return X;
+    } else {
+        const int z = (int)(threadIdx.x & 63), zr = z & 15;
+        int X = A;
+        X = max(X, __builtin_amdgcn_update_dpp(BG_NEG, X, 0x111, 0xf, 0xf, false) - gE);
+        X = max(X, __builtin_amdgcn_update_dpp(BG_NEG, X, 0x112, 0xf, 0xf, false) - 2 * gE);
+        X = max(X, __builtin_amdgcn_update_dpp(BG_NEG, X, 0x114, 0xf, 0xf, false) - 4 * gE);
+        X = max(X, __builtin_amdgcn_update_dpp(BG_NEG, X, 0x118, 0xf, 0xf, false) - 8 * gE);
+        const int b15 = __builtin_amdgcn_update_dpp(BG_NEG, X, 0x142, 0xa, 0xf, false);   // row_bcast:15
+        X = max(X, b15 - (zr + 1) * gE);
+        const int b31 = __builtin_amdgcn_update_dpp(BG_NEG, X, 0x143, 0xc, 0xf, false);   // row_bcast:31
+        X = max(X, b31 - (z - 31) * gE);
+        return X;
     }
-    return X;
 }
 
 #define WSYNC() do { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); } while (0)

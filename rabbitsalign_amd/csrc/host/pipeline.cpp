@@ -18,6 +18,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <exception>
+#include <functional>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -201,6 +202,60 @@ struct ScratchLease {
         std::lock_guard<std::mutex> g(mu());
         if (pool().size() < 64) pool().push_back(std::move(s));
     }
+};
+
+// Worker threads outlive the mapping calls (each bench step is one call, and
+// creating ~30 threads a call cost their stacks' mmap/mprotect, TLS setup and
+// teardown on every step): run(n, f) runs f on n pool threads and returns when
+// all are done.  Jobs never block on each other through the pool itself.
+class WorkerPool {
+public:
+    void run(int n, const std::function<void()>& f) {
+        // one mapping call at a time uses the pool; a concurrent one gets its own threads
+        std::unique_lock<std::mutex> busy(run_m_, std::try_to_lock);
+        if (!busy.owns_lock()) {
+            std::vector<std::thread> ws;
+            for (int t = 0; t < n; ++t) ws.emplace_back(f);
+            for (auto& w : ws) w.join();
+            return;
+        }
+        std::unique_lock<std::mutex> g(m_);
+        while ((int)threads_.size() < n) threads_.emplace_back([this] { loop(); });
+        pending_ = n;
+        job_ = &f;
+        generation_++;
+        cv_.notify_all();
+        done_cv_.wait(g, [&] { return pending_ == 0 && running_ == 0; });
+        job_ = nullptr;
+    }
+    static WorkerPool& get() {
+        static WorkerPool* p = new WorkerPool();     // never destroyed: no exit-time teardown
+        return *p;
+    }
+
+private:
+    void loop() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> g(m_);
+        for (;;) {
+            cv_.wait(g, [&] { return generation_ != seen && pending_ > 0; });
+            seen = generation_;
+            pending_--;
+            running_++;
+            const std::function<void()>* f = job_;
+            g.unlock();
+            (*f)();
+            g.lock();
+            running_--;
+            if (pending_ == 0 && running_ == 0) done_cv_.notify_all();
+        }
+    }
+    std::mutex run_m_, m_;
+    std::condition_variable cv_, done_cv_;
+    std::vector<std::thread> threads_;
+    const std::function<void()>* job_ = nullptr;
+    int pending_ = 0, running_ = 0;
+    uint64_t generation_ = 0;
 };
 
 ChunkPool& chunk_pool() {
@@ -765,10 +820,8 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
         stats_all.add(local);
         phases_all.add(lt);
     };
-    std::vector<std::thread> ws;
-    for (int t = 1; t < W; ++t) ws.emplace_back(worker, false);
-    worker(true);
-    for (auto& w : ws) w.join();
+    std::atomic<bool> lead_taken{false};
+    WorkerPool::get().run(W, [&] { worker(!lead_taken.exchange(true)); });
     if (failure) std::rethrow_exception(failure);
     result.stats = stats_all;
     result.phases = phases_all;
@@ -867,9 +920,7 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
         std::lock_guard<std::mutex> g(stat_m);
         result.stats.add(local);
     };
-    std::vector<std::thread> ws;
-    for (int t = 0; t < T + wait_workers(eng, T); ++t) ws.emplace_back(worker);
-    for (auto& w : ws) w.join();
+    WorkerPool::get().run(T + wait_workers(eng, T), worker);
     if (failure) std::rethrow_exception(failure);
     result.map_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     result.sam_bytes = os.bytes;
