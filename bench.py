@@ -219,6 +219,9 @@ def main():
     ap.add_argument("--cpu-pairs", type=int, default=2_000_000,
                     help="cpu_baseline sample (pairs; ~10 s of CPU work on 16 cores at 2x150)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-io", action="store_true",
+                    help="skip the consumer-cost leg (FASTQ in, SAM file out, not the headline value)")
+    ap.add_argument("--io-dir", default="/tmp", help="where the consumer-cost leg writes its FASTQ and SAM")
     ap.add_argument("--ref-len", type=int, default=0, help="override reference length (testing only)")
     ap.add_argument("--stats-out", default="", help="write per-kernel stats JSON here")
     args = ap.parse_args()
@@ -305,6 +308,39 @@ def main():
     for b in batches:
         b.close()
 
+    # consumer-cost leg (rank 0, N=1): the reference's own timeline, first chunk read ->
+    # last SAM byte written (main.cpp:446,595): FASTQ parse + mapping + SAM file, on one
+    # step's worth of the same synthetic pairs (files in --io-dir; page cache warm)
+    io = None
+    if rank == 0 and world == 1 and not args.no_io:
+        sample = m.synthetic_reads(args.read_seed, 0, P, wl["read_len"], wl["mu"], wl["sigma"], wl["paired"])
+        fq1 = os.path.join(args.io_dir, f"rsa_bench_{os.getpid()}_1.fq")
+        fq2 = os.path.join(args.io_dir, f"rsa_bench_{os.getpid()}_2.fq") if wl["paired"] else None
+        sam = os.path.join(args.io_dir, f"rsa_bench_{os.getpid()}.sam")
+        try:
+            sample.write_fastq(fq1, fq2)
+            sample.close()
+            fq_bytes = os.path.getsize(fq1) + (os.path.getsize(fq2) if fq2 else 0)
+            t_io = time.perf_counter()
+            loaded = m.load_reads(fq1, fq2)
+            t_loaded = time.perf_counter()
+            st = m.map(loaded, threads=threads, chunk_size=args.chunk_size, sam_path=sam)
+            t_end = time.perf_counter()
+            loaded.close()
+            io = {"value": round(st.n_reads / (t_end - t_io) / 1e6, 6), "unit": "Mreads/s",
+                  "load_s": round(t_loaded - t_io, 3), "map_and_write_s": round(t_end - t_loaded, 3),
+                  "fastq_bytes": fq_bytes, "sam_file_bytes": os.path.getsize(sam), "reads": st.n_reads,
+                  "note": "FASTQ files -> rsam_reads_load -> rsam_map with a SAM file (header + body); "
+                          "the headline value keeps reads in RAM and SAM in memory"}
+            log(rank, f"consumer cost: {io['value']} Mreads/s (load {io['load_s']} s, map+write "
+                      f"{io['map_and_write_s']} s)")
+        except (OSError, RuntimeError) as e:
+            io = {"skipped": str(e)}
+        finally:
+            for f in (fq1, fq2, sam):
+                if f and os.path.exists(f):
+                    os.remove(f)
+
     cpu = None
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -350,6 +386,7 @@ def main():
                                     "index stays in HBM and the engine adopts it (rsa_open_built)"},
             "roofline": rl,
             "cpu_baseline": cpu,
+            "consumer_cost": io,
             "parity": parity,
             "kernels": kernel_table(ks),
             "device_counters": {k: v for k, v in ks.items() if k != "kernels"},

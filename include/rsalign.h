@@ -64,6 +64,8 @@ rsam_reads* rsam_reads_load_interleaved(const char* fq);
 /* pairs p in [first, first + n) of the synthetic stream `seed` (paired or SE with mate 1 only) */
 rsam_reads* rsam_reads_synthetic(const rsam* m, uint64_t seed, uint64_t first, uint64_t n, int read_len,
                                  double mu, double sigma, int paired);
+/* FASTQ of a read set (mate 2 to fq2 when paired): test data and the I/O-inclusive bench leg */
+int rsam_reads_write_fastq(const rsam_reads* r, const char* fq1, const char* fq2);
 uint64_t rsam_reads_count(const rsam_reads* r);
 void rsam_reads_free(rsam_reads* r);
 

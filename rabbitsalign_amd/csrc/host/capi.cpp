@@ -294,6 +294,27 @@ rsam_reads* rsam_reads_synthetic(const rsam* m, uint64_t seed, uint64_t first, u
     return r;
 }
 
+int rsam_reads_write_fastq(const rsam_reads* r, const char* fq1, const char* fq2) {
+    if (!r || !fq1) return -1;
+    auto write = [](const std::vector<Record>& v, const char* path) -> bool {
+        FILE* f = fopen(path, "wb");
+        if (!f) return false;
+        std::string buf;
+        buf.reserve(1 << 22);
+        for (const Record& x : v) {
+            buf += '@'; buf += x.name;
+            if (!x.comment.empty()) { buf += ' '; buf += x.comment; }
+            buf += '\n'; buf += x.seq; buf += "\n+\n"; buf += x.qual; buf += '\n';
+            if (buf.size() > (1 << 22)) { fwrite(buf.data(), 1, buf.size(), f); buf.clear(); }
+        }
+        fwrite(buf.data(), 1, buf.size(), f);
+        return fclose(f) == 0;
+    };
+    if (!write(r->r1, fq1)) { g_err = std::string("cannot write ") + fq1; return -1; }
+    if (r->paired && fq2 && !write(r->r2, fq2)) { g_err = std::string("cannot write ") + fq2; return -1; }
+    return 0;
+}
+
 uint64_t rsam_reads_count(const rsam_reads* r) {
     return r ? r->r1.size() + r->r2.size() + r->interleaved.size() : 0;
 }

@@ -1,3 +1,6 @@
+#include <unistd.h>
+#include <fcntl.h>
+#include <sys/stat.h>
 // io.cpp -- CIGAR text, SAM records, FASTA, .sti read/write/build, FASTQ input.
 // Restated from src/cigar.cpp, src/sam.cpp, src/refs.cpp, src/index.cpp,
 // src/indexparameters.cpp and the kseq++ record semantics used by src/fastq.cpp.
@@ -741,8 +744,129 @@ bool FastxReader::next(Record& r) {
     return true;
 }
 
+namespace {
+
+// Uncompressed FASTQ in the plain 4-line layout, parsed by several threads over
+// byte ranges of the mapped file.  Every record must be header / one sequence
+// line / '+' line / one quality line of the same length: then each range can
+// find its first record (a line starting with '@' whose next-but-one line
+// starts with '+': a quality line starting with '@' is followed two lines
+// later by a sequence line) and the records are exactly what next() returns.
+// Anything else (gzip, FASTA, wrapped lines, empty lines, length mismatch)
+// returns false and the caller reads the file sequentially.
+struct Mapped {
+    const char* p = nullptr;
+    size_t n = 0;
+    int fd = -1;
+    ~Mapped() {
+        if (p && n) munmap((void*)p, n);
+        if (fd >= 0) close(fd);
+    }
+};
+
+inline std::string_view strip_cr(std::string_view l) {
+    if (!l.empty() && l.back() == '\r') l.remove_suffix(1);
+    return l;
+}
+
+bool parse_range(const char* b, const char* e, std::vector<Record>& out) {
+    auto next_line = [&](const char*& p, std::string_view& l) -> bool {
+        if (p >= e) return false;
+        const char* q = (const char*)memchr(p, '\n', (size_t)(e - p));
+        const char* end = q ? q : e;
+        l = std::string_view(p, (size_t)(end - p));
+        p = q ? q + 1 : e;
+        return true;
+    };
+    const char* p = b;
+    std::string_view h, sq, pl, ql;
+    while (p < e) {
+        if (*p != '@') return false;
+        if (!next_line(p, h) || !next_line(p, sq) || !next_line(p, pl) || !next_line(p, ql)) return false;
+        if (pl.empty() || pl[0] != '+') return false;
+        Record r;
+        h = strip_cr(h.substr(1));
+        const size_t ws = h.find_first_of(" \t\v\f\r");
+        if (ws == std::string_view::npos) r.name.assign(h);
+        else {
+            r.name.assign(h.substr(0, ws));
+            const size_t cs = h.find_first_not_of(" \t\v\f\r", ws);
+            if (cs != std::string_view::npos) r.comment.assign(h.substr(cs));
+        }
+        // next(): '\r' is stripped from the sequence line after its first byte, then trailing blanks
+        if (sq.empty()) return false;
+        std::string_view body = sq.substr(1);
+        body = strip_cr(body);
+        r.seq.reserve(1 + body.size());
+        r.seq.push_back(sq[0]);
+        r.seq.append(body);
+        if (r.seq[0] == '>' || r.seq[0] == '@' || r.seq[0] == '+' || r.seq[0] == '\r') return false;
+        while (!r.seq.empty() && (r.seq.back() == ' ' || r.seq.back() == '\t')) r.seq.pop_back();
+        r.qual.assign(strip_cr(ql));
+        if (r.qual.size() != r.seq.size() || r.seq.empty()) return false;
+        out.push_back(std::move(r));
+    }
+    return true;
+}
+
+bool parse_parallel(const std::string& path, int threads, std::vector<Record>& out) {
+    if (path == "-" || threads < 2) return false;
+    Mapped m;
+    m.fd = open(path.c_str(), O_RDONLY);
+    if (m.fd < 0) return false;
+    struct stat st;
+    if (fstat(m.fd, &st) != 0 || st.st_size < (1 << 20)) return false;       // small files: not worth it
+    m.n = (size_t)st.st_size;
+    void* p = mmap(nullptr, m.n, PROT_READ, MAP_PRIVATE | MAP_POPULATE, m.fd, 0);
+    if (p == MAP_FAILED) { m.n = 0; return false; }
+    m.p = (const char*)p;
+    if ((unsigned char)m.p[0] == 0x1f && (unsigned char)m.p[1] == 0x8b) return false;   // gzip
+    if (m.p[0] != '@') return false;
+    const char* end = m.p + m.n;
+    // range starts, each moved to the next record header
+    std::vector<const char*> cut(threads + 1, end);
+    cut[0] = m.p;
+    auto line_after = [&](const char* q) -> const char* {
+        const char* nl = (const char*)memchr(q, '\n', (size_t)(end - q));
+        return nl ? nl + 1 : end;
+    };
+    for (int t = 1; t < threads; ++t) {
+        const char* q = line_after(m.p + m.n * (size_t)t / (size_t)threads);
+        while (q < end) {
+            if (*q == '@') {
+                const char* l2 = line_after(line_after(q));
+                if (l2 < end && *l2 == '+') break;
+            }
+            q = line_after(q);
+        }
+        cut[t] = std::max(q, cut[t - 1]);
+    }
+    std::vector<std::vector<Record>> parts(threads);
+    std::vector<char> ok(threads, 0);
+    std::vector<std::thread> ts;
+    for (int t = 0; t < threads; ++t)
+        ts.emplace_back([&, t]() { ok[t] = parse_range(cut[t], cut[t + 1], parts[t]) ? 1 : 0; });
+    for (auto& t : ts) t.join();
+    for (char c : ok) if (!c) return false;
+    size_t total = 0;
+    for (auto& v : parts) total += v.size();
+    out.clear();
+    out.reserve(total);
+    for (auto& v : parts) for (auto& r : v) out.push_back(std::move(r));
+    return true;
+}
+
+int reader_threads() {
+    const unsigned hc = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(16u, hc));
+}
+
+}  // namespace
+
 std::vector<Record> FastxReader::read_all(const std::string& path) {
     std::vector<Record> v;
+    if (parse_parallel(path, reader_threads(), v)) return v;
+    v.clear();
     FastxReader in(path);
     Record r;
     while (in.next(r)) { v.push_back(std::move(r)); r = Record(); }
@@ -752,10 +876,21 @@ std::vector<Record> FastxReader::read_all(const std::string& path) {
 void FastxReader::read_pair(const std::string& p1, const std::string& p2, std::vector<Record>& r1,
                             std::vector<Record>& r2) {
     std::exception_ptr err;
+    // each file on half of the reader threads (both parses run at once)
+    const int half = std::max(1, reader_threads() / 2);
+    auto read = [&](const std::string& p) {
+        std::vector<Record> v;
+        if (parse_parallel(p, half, v)) return v;
+        v.clear();
+        FastxReader in(p);
+        Record r;
+        while (in.next(r)) { v.push_back(std::move(r)); r = Record(); }
+        return v;
+    };
     std::thread t([&]() {
-        try { r2 = read_all(p2); } catch (...) { err = std::current_exception(); }
+        try { r2 = read(p2); } catch (...) { err = std::current_exception(); }
     });
-    try { r1 = read_all(p1); } catch (...) { t.join(); throw; }
+    try { r1 = read(p1); } catch (...) { t.join(); throw; }
     t.join();
     if (err) std::rethrow_exception(err);
 }

@@ -39,7 +39,7 @@ class _Info(C.Structure):
 
 EXPORTED_SYMBOLS = [
     "rsam_open_files", "rsam_open_synthetic", "rsam_open_like", "rsam_close", "rsam_get_info",
-    "rsam_reads_load", "rsam_reads_load_interleaved", "rsam_reads_synthetic", "rsam_reads_count", "rsam_reads_free", "rsam_map",
+    "rsam_reads_load", "rsam_reads_load_interleaved", "rsam_reads_synthetic", "rsam_reads_write_fastq", "rsam_reads_count", "rsam_reads_free", "rsam_map",
     "rsam_add_devices", "rsam_kernel_stats", "rsam_reset_kernel_stats", "rsam_engine_name", "rsam_last_error",
 ]
 
@@ -64,6 +64,7 @@ def load(path: str = PRODUCT_LIB) -> C.CDLL:
     lib.rsam_reads_load.restype = vp
     lib.rsam_reads_load.argtypes = [cp, cp]
     lib.rsam_add_devices.argtypes = [vp, C.POINTER(C.c_int), i32]
+    lib.rsam_reads_write_fastq.argtypes = [vp, cp, cp]
     lib.rsam_reads_load_interleaved.restype = vp
     lib.rsam_reads_load_interleaved.argtypes = [cp]
     lib.rsam_reads_synthetic.restype = vp
@@ -106,6 +107,10 @@ class Reads:
 
     def __len__(self):
         return int(self._lib.rsam_reads_count(self._h))
+
+    def write_fastq(self, fq1, fq2=None):
+        if self._lib.rsam_reads_write_fastq(self._h, str(fq1).encode(), str(fq2).encode() if fq2 else None) != 0:
+            raise RuntimeError(f"rsam_reads_write_fastq: {self._lib.rsam_last_error().decode()}")
 
     def close(self):
         if self._h:

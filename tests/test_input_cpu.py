@@ -146,3 +146,52 @@ def test_interleaved_with_two_files_is_an_error(data):
     r = subprocess.run([CPU_PORT, "--use-index", "--interleaved", "-o", str(d / "x.sam"), fa, f1, f2],
                        capture_output=True, text=True)
     assert r.returncode == 1 and "interleaved" in r.stderr
+
+
+@pytest.fixture(scope="module")
+def big(tmp_path_factory):
+    d = tmp_path_factory.mktemp("input_big")
+    fa, (f1, f2) = make_dataset(str(d), pairs=6000, ref_len=200_000, cpu_index=True, n_rate=0.002)
+    return d, fa, f1, f2
+
+
+def _tricky(recs, k):
+    """Header comments, quality lines starting with '@' or '+', trailing blanks after sequences."""
+    out = []
+    for i, (h, s, p, q) in enumerate(recs):
+        if i % 3 == k % 3:
+            h = h + " BX:Z:cmt\tmore"
+        if i % 5 == 1:
+            q = "@" + q[1:]
+        elif i % 5 == 2:
+            q = "+" + q[1:]
+        if i % 7 == 3:
+            s = s + " \t"
+        if i % 11 == 4:
+            p = "+" + h[1:]
+        out.append((h, s, p, q))
+    return out
+
+
+@pytest.mark.parametrize("variant", ["plain", "crlf_tricky", "wrapped"])
+def test_parallel_fastq_parse_matches_sequential(big, variant):
+    """Files over 1 MB in the plain 4-line layout are parsed by several threads
+    (io.cpp parse_parallel); the gzip copy of the same text takes the sequential
+    kseq reader.  Both must give the same SAM; a wrapped file falls back."""
+    d, fa, f1, f2 = big
+    opts = dict(plain=dict(), crlf_tricky=dict(nl="\r\n"), wrapped=dict(wrap=60))[variant]
+    sams = []
+    for ext in (".fq", ".fq.gz"):
+        paths = []
+        for m, f in ((1, f1), (2, f2)):
+            recs = _records(f)
+            if variant == "crlf_tricky":
+                recs = _tricky(recs, m)
+            p = d / f"{variant}_{m}{ext}"
+            _write(p, recs, **opts)
+            paths.append(str(p))
+        assert os.path.getsize(paths[0]) > (1 << 20) or ext == ".fq.gz"
+        out = d / f"{variant}{ext}.sam"
+        map_reads(CPU_PORT, fa, paths, str(out), "-t", "4", "--chunk-size", "1000")
+        sams.append(sam_body(out))
+    assert len(sams[0]) > 12000 and sams[0] == sams[1]
