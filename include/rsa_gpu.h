@@ -39,6 +39,7 @@ extern "C" {
 #define RSA_ERR_ARG (-2)
 #define RSA_ERR_CAPACITY (-3)   /* an output buffer is too small; *_needed fields say how much */
 #define RSA_ERR_NOMEM (-4)
+#define RSA_ERR_BUSY (-5)       /* rsa_extend_async: RSA_MAX_PENDING calls not yet waited for */
 
 /* RefRandstrobe exactly as stored in a .sti file (src/randstrobes.hpp:20-49) */
 typedef struct rsa_ref_randstrobe {
@@ -192,6 +193,23 @@ typedef struct rsa_aln_batch {
 /* Aligner::align for every job.  ref_len > 2000 gives the reference's
  * sentinel (sw_score -1000000), a failed SSW the -100000 sentinel. */
 int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jobs, rsa_aln_batch* out);
+
+/* The same call split at the device boundary, so one host thread can overlap
+ * its CPU work with the GPU, as the reference's worker does with gasal_aln_async
+ * + gasal_is_aln_async_done (src/gasal2_ssw.cpp:114-249; pc.cpp:1699-1770 runs
+ * part(N+1) while batch N extends).  rsa_extend_async validates the jobs, stages
+ * them and enqueues every kernel and copy on a stream of its own, and returns;
+ * `jobs` may be released then, but the query bytes and `out` must stay valid
+ * until rsa_wait.  rsa_ready says whether the device part has finished (never
+ * blocks); rsa_wait finishes the call (the rare one-lane band pass and the CIGAR
+ * tail copy need the host), frees the handle and returns the call's status.
+ * Results equal rsa_extend's.  At most RSA_MAX_PENDING calls per context may be
+ * pending; the next one returns RSA_ERR_BUSY. */
+#define RSA_MAX_PENDING 12
+typedef struct rsa_pending rsa_pending;
+int rsa_extend_async(rsa_ctx* ctx, const rsa_job_batch* jobs, rsa_aln_batch* out, rsa_pending** pending);
+int rsa_ready(const rsa_pending* pending);
+int rsa_wait(rsa_pending* pending);
 
 /* upper bound of cigar_pool entries needed for a batch (the pool comes back
  * packed: cigar_used <= bound entries, alns[i].cigar_offset indexes it) */

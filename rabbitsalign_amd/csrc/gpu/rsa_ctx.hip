@@ -126,6 +126,7 @@ struct rsa_ctx {
     std::vector<Lane*> lanes;
     std::mutex lane_m;
     std::condition_variable lane_cv;
+    int n_pending = 0;                 // rsa_extend_async calls not yet waited for
     // stats
     std::mutex stat_m;
     rsa_kernel_stats stats{};
@@ -142,12 +143,14 @@ static void set_err(rsa_ctx* ctx, const std::string& s) {
     ctx->err = s;
 }
 
+static const int RSA_MAX_LANES = 16;
+
 static Lane* acquire_lane(rsa_ctx* ctx) {
     std::unique_lock<std::mutex> g(ctx->lane_m);
     for (;;) {
         for (Lane* l : ctx->lanes)
             if (!l->busy) { l->busy = true; return l; }
-        if (ctx->lanes.size() < 16) {
+        if (ctx->lanes.size() < (size_t)RSA_MAX_LANES) {
             Lane* l = new Lane();
             if (hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking) != hipSuccess) { delete l; return nullptr; }
             l->busy = true;
@@ -342,18 +345,45 @@ struct ExtStatus {            // device-side counters of one rsa_extend call
     uint64_t total;           // dense CIGAR ops (k_cigar_compact)
 };
 
-int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
-    if (!ctx || !jb || !out) return RSA_ERR_ARG;
+}  // extern "C"
+
+// One extension call between its enqueue and its completion: rsa_extend runs
+// both halves back to back, rsa_extend_async returns between them.
+struct rsa_pending {
+    rsa_ctx* ctx = nullptr;
+    Lane* L = nullptr;
+    rsa_aln_batch* out = nullptr;
+    uint32_t n = 0;
+    int32_t match = 0, mismatch = 0, gap_open = 0, gap_extend = 0, end_bonus = 0;
+    uint64_t guess = 0, cells = 0, qr_bytes = 0;
+};
+
+// k_cigar_compact, then the status, results and the first `guess` CIGAR entries
+// to the host; nothing waits here
+static int ext_compact_copy(rsa_pending& P) {
+    rsa_ctx* ctx = P.ctx;
+    Lane* L = P.L;
+    hipStream_t st = L->stream;
+    ExtStatus* dst = L->d_status.as<ExtStatus>();
+    launch_cigar_compact(st, L->d_alns.as<rsa_aln>(), (int)P.n, L->d_cig.as<uint32_t>(), L->d_dense.as<uint32_t>(),
+                         L->d_bsum.as<uint64_t>(), &dst->total);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(L->h_status.p, L->d_status.p, sizeof(ExtStatus), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(P.out->alns, L->d_alns.p, sizeof(rsa_aln) * P.n, hipMemcpyDeviceToHost, st));
+    if (P.guess)
+        HIPCHK(hipMemcpyAsync(P.out->cigar_pool, L->d_dense.p, sizeof(uint32_t) * P.guess, hipMemcpyDeviceToHost, st));
+    return RSA_OK;
+}
+
+// first half: validate, stage, launch every kernel and the result copies on lane L
+static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out, rsa_pending& P) {
+    Lane* L = P.L;
     const uint32_t n = jb->n_jobs;
     const uint64_t bound = rsa_extend_cigar_bound(jb);
-    out->cigar_used = 0;
-    if (n == 0) return RSA_OK;
-    if (out->cigar_capacity < bound) { set_err(ctx, "rsa_extend: cigar_pool too small"); return RSA_ERR_CAPACITY; }
-    HIPCHK(hipSetDevice(ctx->device));
-    CallTimer ct(ctx, 1);
-    Lane* L = ct.lane();
-    if (!L) { set_err(ctx, "rsa_extend: cannot create HIP stream"); return RSA_ERR_HIP; }
-    LaneGuard guard{ctx, L};
+    P.out = out;
+    P.n = n;
+    P.match = jb->match; P.mismatch = jb->mismatch; P.gap_open = jb->gap_open; P.gap_extend = jb->gap_extend;
+    P.end_bonus = jb->end_bonus;
     // host job descriptors
     HIPCHK(L->h_jobs.ensure(sizeof(ExtJobDev) * n));
     ExtJobDev* hj = L->h_jobs.as<ExtJobDev>();
@@ -387,6 +417,8 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
             rmax = std::max(rmax, (int)((s.query_len + 63) / 64));
         }
     }
+    P.cells = cells;
+    P.qr_bytes = qr_bytes;
     HIPCHK(L->d_q.ensure(jb->queries_len + 16));
     HIPCHK(L->d_jobs.ensure(sizeof(ExtJobDev) * n));
     HIPCHK(L->d_scan.ensure(sizeof(ScanRes) * n));
@@ -493,20 +525,22 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
                       &dst->ocount);
     HIPCHK(hipGetLastError());
     L->kt.end(st);
-    auto compact_and_copy = [&](uint64_t guess) -> int {
-        launch_cigar_compact(st, L->d_alns.as<rsa_aln>(), (int)n, L->d_cig.as<uint32_t>(), L->d_dense.as<uint32_t>(),
-                             L->d_bsum.as<uint64_t>(), &dst->total);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(L->h_status.p, L->d_status.p, sizeof(ExtStatus), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(out->alns, L->d_alns.p, sizeof(rsa_aln) * n, hipMemcpyDeviceToHost, st));
-        if (guess) HIPCHK(hipMemcpyAsync(out->cigar_pool, L->d_dense.p, sizeof(uint32_t) * guess, hipMemcpyDeviceToHost, st));
-        HIPCHK(stream_wait(st, L->sb.done));
-        return RSA_OK;
-    };
     // k_cigar_compact rewrites cigar_offset in place: keep the slot offsets for a possible re-run
     HIPCHK(hipMemcpyAsync(L->d_alns2.p, L->d_alns.p, sizeof(rsa_aln) * n, hipMemcpyDeviceToDevice, st));
-    const uint64_t guess = std::min<uint64_t>(bound, DENSE_GUESS * n);
-    if (int rc = compact_and_copy(guess)) return rc;
+    P.guess = std::min<uint64_t>(bound, DENSE_GUESS * n);
+    return ext_compact_copy(P);
+}
+
+// second half: wait, the rare one-lane pass for bands the 64-lane kernel could
+// not hold, the CIGAR entries past the first guess, statistics
+static int ext_finish(rsa_pending& P) {
+    rsa_ctx* ctx = P.ctx;
+    Lane* L = P.L;
+    const uint32_t n = P.n;
+    rsa_aln_batch* out = P.out;
+    hipStream_t st = L->stream;
+    const uint64_t guess = P.guess;
+    HIPCHK(stream_wait(st, L->sb.done));
     ExtStatus hs = *L->h_status.as<ExtStatus>();
     if (hs.ocount > 0) {
         // rare: bands the 64-lane kernel cannot hold -> one lane per job, large global scratch
@@ -527,7 +561,7 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
             hipLaunchKernelGGL(k_ext_band, dim3(1), dim3(64), 0, st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(),
                                cnt, L->d_idx.as<int>() + b, 0, L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(),
                                L->d_alns.as<rsa_aln>(), L->d_scratch.as<uint8_t>(), bstride, BIG_ARR_CAP, BIG_DIR_CAP,
-                               jb->match, jb->mismatch, jb->gap_open, jb->gap_extend, jb->end_bonus,
+                               P.match, P.mismatch, P.gap_open, P.gap_extend, P.end_bonus,
                                L->d_over.as<int>(), 2);
             HIPCHK(hipGetLastError());
             L->kt.end(st);
@@ -536,7 +570,8 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
         HIPCHK(stream_wait(st, L->sb.done));
         for (int i : big)
             if (L->h_over.as<int>()[i] > 1) { set_err(ctx, "rsa_extend: band scratch exhausted"); return RSA_ERR_NOMEM; }
-        if (int rc = compact_and_copy(guess)) return rc;
+        if (int rc = ext_compact_copy(P)) return rc;
+        HIPCHK(stream_wait(st, L->sb.done));
         hs = *L->h_status.as<ExtStatus>();
     }
     if (hs.total > guess) {
@@ -549,16 +584,105 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
         std::lock_guard<std::mutex> g(ctx->stat_m);
         L->kt.collect(ctx->stats.kernel_ms, ctx->stats.launches);
         // scan: query + window in, ScanRes out; band: the segment bytes again, ScanRes in, rsa_aln + CIGAR out
-        ctx->stats.alg_bytes[RSA_K_EXT_SCAN] += (double)qr_bytes + (double)(sizeof(ExtJobDev) + sizeof(ScanRes)) * n;
-        ctx->stats.alg_bytes[RSA_K_EXT_BAND] += (double)qr_bytes + (double)(sizeof(ExtJobDev) + sizeof(ScanRes) +
+        ctx->stats.alg_bytes[RSA_K_EXT_SCAN] += (double)P.qr_bytes + (double)(sizeof(ExtJobDev) + sizeof(ScanRes)) * n;
+        ctx->stats.alg_bytes[RSA_K_EXT_BAND] += (double)P.qr_bytes + (double)(sizeof(ExtJobDev) + sizeof(ScanRes) +
                                                                             sizeof(rsa_aln)) * n + 4.0 * hs.total;
         ctx->stats.ext_calls++;
         ctx->stats.jobs += n;
-        ctx->stats.dp_cells += cells;
+        ctx->stats.dp_cells += P.cells;
         ctx->stats.band_deferred += (uint64_t)hs.qcount;
         ctx->stats.band_overflow += (uint64_t)hs.ocount;
     }
     return RSA_OK;
+}
+
+
+extern "C" {
+
+int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
+    if (!ctx || !jb || !out) return RSA_ERR_ARG;
+    out->cigar_used = 0;
+    if (jb->n_jobs == 0) return RSA_OK;
+    if (out->cigar_capacity < rsa_extend_cigar_bound(jb)) {
+        set_err(ctx, "rsa_extend: cigar_pool too small");
+        return RSA_ERR_CAPACITY;
+    }
+    HIPCHK(hipSetDevice(ctx->device));
+    CallTimer ct(ctx, 1);
+    rsa_pending P;
+    P.ctx = ctx;
+    P.L = ct.lane();
+    if (!P.L) { set_err(ctx, "rsa_extend: cannot create HIP stream"); return RSA_ERR_HIP; }
+    LaneGuard guard{ctx, P.L};
+    if (int rc = ext_enqueue(ctx, jb, out, P)) return rc;
+    return ext_finish(P);
+}
+
+int rsa_extend_async(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out, rsa_pending** pending) {
+    if (!ctx || !jb || !out || !pending) return RSA_ERR_ARG;
+    *pending = nullptr;
+    out->cigar_used = 0;
+    if (out->cigar_capacity < rsa_extend_cigar_bound(jb)) {
+        set_err(ctx, "rsa_extend_async: cigar_pool too small");
+        return RSA_ERR_CAPACITY;
+    }
+    HIPCHK(hipSetDevice(ctx->device));
+    {
+        // every lane held by a pending call would make the acquire below wait forever
+        std::lock_guard<std::mutex> g(ctx->lane_m);
+        if (ctx->n_pending >= RSA_MAX_PENDING) {
+            set_err(ctx, "rsa_extend_async: too many pending calls (rsa_wait some first)");
+            return RSA_ERR_BUSY;
+        }
+        ctx->n_pending++;
+    }
+    auto unpend = [&]() {
+        std::lock_guard<std::mutex> g(ctx->lane_m);
+        ctx->n_pending--;
+    };
+    rsa_pending* P = new rsa_pending();
+    P->ctx = ctx;
+    P->out = out;
+    if (jb->n_jobs == 0) { *pending = P; return RSA_OK; }   // nothing enqueued: rsa_wait returns at once
+    P->L = acquire_lane(ctx);
+    if (!P->L) {
+        delete P;
+        unpend();
+        set_err(ctx, "rsa_extend_async: cannot create HIP stream");
+        return RSA_ERR_HIP;
+    }
+    if (int rc = ext_enqueue(ctx, jb, out, *P)) {
+        (void)hipStreamSynchronize(P->L->stream);   // the lane is reused: let what was enqueued drain
+        release_lane(ctx, P->L);
+        delete P;
+        unpend();
+        return rc;
+    }
+    *pending = P;
+    return RSA_OK;
+}
+
+int rsa_ready(const rsa_pending* p) {
+    if (!p || !p->L) return 1;
+    return hipStreamQuery(p->L->stream) == hipErrorNotReady ? 0 : 1;
+}
+
+int rsa_wait(rsa_pending* p) {
+    if (!p) return RSA_ERR_ARG;
+    rsa_ctx* ctx = p->ctx;
+    int rc = RSA_OK;
+    if (p->L) {
+        if (hipSetDevice(ctx->device) != hipSuccess) rc = RSA_ERR_HIP;
+        if (rc == RSA_OK) rc = ext_finish(*p);
+        if (rc != RSA_OK) (void)hipStreamSynchronize(p->L->stream);
+        release_lane(ctx, p->L);
+    }
+    {
+        std::lock_guard<std::mutex> g(ctx->lane_m);
+        ctx->n_pending--;
+    }
+    delete p;
+    return rc;
 }
 
 void* rsa_host_alloc(size_t bytes) {

@@ -116,7 +116,8 @@ def stats_dict(ks: "KernelStats") -> dict:
 EXPORTED_SYMBOLS = ["rsa_open", "rsa_close", "rsa_last_error", "rsa_resident_bytes", "rsa_randstrobes",
                     "rsa_seed", "rsa_extend", "rsa_extend_cigar_bound", "rsa_host_alloc", "rsa_host_free",
                     "rsa_get_stats", "rsa_reset_stats", "rsa_index_build_run", "rsa_index_build_download",
-                    "rsa_index_build_free", "rsa_open_built", "rsa_index_download"]
+                    "rsa_index_build_free", "rsa_open_built", "rsa_index_download", "rsa_extend_async",
+                    "rsa_ready", "rsa_wait"]
 
 _lib = None
 
@@ -139,6 +140,9 @@ def load(path: str = GPU_LIB):
     lib.rsa_randstrobes.argtypes = [C.c_void_p, C.POINTER(ReadBatch), C.POINTER(RandstrobeBatch)]
     lib.rsa_seed.argtypes = [C.c_void_p, C.POINTER(ReadBatch), C.c_int32, C.c_uint32, C.POINTER(NamBatch)]
     lib.rsa_extend.argtypes = [C.c_void_p, C.POINTER(JobBatch), C.POINTER(AlnBatch)]
+    lib.rsa_extend_async.argtypes = [C.c_void_p, C.POINTER(JobBatch), C.POINTER(AlnBatch), C.POINTER(C.c_void_p)]
+    lib.rsa_ready.argtypes = [C.c_void_p]
+    lib.rsa_wait.argtypes = [C.c_void_p]
     lib.rsa_extend_cigar_bound.restype = C.c_uint64
     lib.rsa_extend_cigar_bound.argtypes = [C.POINTER(JobBatch)]
     lib.rsa_get_stats.argtypes = [C.c_void_p, C.POINTER(KernelStats)]
@@ -382,18 +386,32 @@ class GpuContext:
                     pool[:int(b.mm_used)]
             return lists, nonrep, resc
 
-    def extend(self, queries, jobs, match=2, mismatch=8, gap_open=12, gap_extend=1, end_bonus=10):
-        """queries: bytes blob; jobs: structured array JOB_DTYPE.  Returns (alns, cigar_pool)."""
+    @staticmethod
+    def _ext_batches(queries, jobs, match, mismatch, gap_open, gap_extend, end_bonus, lib):
         qb = np.frombuffer(queries, dtype=np.uint8) if len(queries) else np.zeros(1, np.uint8)
         jobs = np.ascontiguousarray(jobs, dtype=JOB_DTYPE)
         jb = JobBatch(_ptr(qb), len(queries), _ptr(jobs), len(jobs), match, mismatch, gap_open, gap_extend,
                       end_bonus)
-        bound = int(self.lib.rsa_extend_cigar_bound(C.byref(jb)))
+        bound = int(lib.rsa_extend_cigar_bound(C.byref(jb)))
         alns = np.zeros(len(jobs), dtype=ALN_DTYPE)
         pool = np.zeros(bound + 1, dtype=np.uint32)
         ab = AlnBatch(_ptr(alns), _ptr(pool), bound + 1, 0)
+        return jb, ab, alns, pool, (qb, jobs)
+
+    def extend(self, queries, jobs, match=2, mismatch=8, gap_open=12, gap_extend=1, end_bonus=10):
+        """queries: bytes blob; jobs: structured array JOB_DTYPE.  Returns (alns, cigar_pool)."""
+        jb, ab, alns, pool, keep = self._ext_batches(queries, jobs, match, mismatch, gap_open, gap_extend,
+                                                     end_bonus, self.lib)
         self._check(self.lib.rsa_extend(self.ctx, C.byref(jb), C.byref(ab)), "rsa_extend")
         return alns, pool
+
+    def extend_async(self, queries, jobs, match=2, mismatch=8, gap_open=12, gap_extend=1, end_bonus=10):
+        """rsa_extend_async: returns a PendingExtend; .ready() polls, .wait() -> (alns, cigar_pool)."""
+        jb, ab, alns, pool, keep = self._ext_batches(queries, jobs, match, mismatch, gap_open, gap_extend,
+                                                     end_bonus, self.lib)
+        h = C.c_void_p()
+        self._check(self.lib.rsa_extend_async(self.ctx, C.byref(jb), C.byref(ab), C.byref(h)), "rsa_extend_async")
+        return PendingExtend(self, h, ab, alns, pool, keep)
 
     def stats(self) -> dict:
         s = KernelStats()
@@ -405,3 +423,20 @@ class GpuContext:
 
     def resident_bytes(self) -> int:
         return int(self.lib.rsa_resident_bytes(self.ctx))
+
+
+class PendingExtend:
+    """An rsa_extend_async call: the batches it reads and writes live here until wait()."""
+
+    def __init__(self, ctx, handle, ab, alns, pool, keep):
+        self._ctx, self._h, self._ab, self.alns, self.pool, self._keep = ctx, handle, ab, alns, pool, keep
+
+    def ready(self) -> bool:
+        return bool(self._ctx.lib.rsa_ready(self._h))
+
+    def wait(self):
+        if self._h is None:
+            raise RuntimeError("rsa_wait: already waited")
+        h, self._h = self._h, None
+        self._ctx._check(self._ctx.lib.rsa_wait(h), "rsa_wait")
+        return self.alns, self.pool

@@ -1,0 +1,20 @@
+# A/B of host tuning switches on the default bench, alternating settings, REPS rounds.
+# Usage: [REPS=2] [STEPS=10] bash scripts/gpu_ab_env.sh TAG "RSA_PREFETCH=1" "RSA_PREFETCH=0" ...
+# (each argument is one setting: space-separated VAR=value pairs, "" for the defaults)
+# Earlier one-off scripts this replaces produced profiles/r01_ab_*.jsonl and
+# profiles/r02/ab_ext_group.jsonl, e.g. gpu_ab_env.sh abg "RSA_EXT_GROUP=1" "RSA_EXT_GROUP=2".
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/${1:-abenv}
+shift
+mkdir -p $O
+for i in $(seq 1 ${REPS:-2}); do
+  k=0
+  for setting in "$@"; do
+    k=$((k + 1))
+    env $setting timeout -k 10 300 python bench.py --no-cpu-baseline --steps ${STEPS:-10} > $O/b_${k}_$i.json 2> $O/b_${k}_$i.err || exit $?
+    python -c "import json;d=json.load(open('$O/b_${k}_$i.json'));print(json.dumps({'setting':'$setting','rep':$i,'value':d['value'],'ms_per_step':d['ms_per_step']}))" | tee -a $O/ab.jsonl
+  done
+done
+echo "exit 0"

@@ -109,3 +109,41 @@ def test_extend_hand_derived_cases():
                 assert got[k] == v, (name, k, got[k], v)
     finally:
         ctx.close()
+
+
+@pytest.mark.gpu
+def test_extend_async_equals_sync(ctx):
+    """rsa_extend_async / rsa_ready / rsa_wait (the split of the boundary the reference
+    uses to overlap chunks, gasal2_ssw.cpp:114-249): several calls pending at once,
+    waited out of order, give rsa_extend's results; past RSA_MAX_PENDING the call
+    returns RSA_ERR_BUSY instead of blocking."""
+    c, ref, offs = ctx
+    batches = []
+    for seed in range(4):
+        rng = np.random.default_rng(100 + seed)
+        queries, jobs, _ = make_jobs(rng, ref, offs, 700 + 300 * seed, (100, 150, 250, 400))
+        batches.append((queries, jobs))
+    want = [c.extend(q, j) for q, j in batches]
+    pend = [c.extend_async(q, j) for q, j in batches]
+    for k in (2, 0, 3, 1):
+        alns, pool = pend[k].wait()
+        wa, wp = want[k]
+        assert (alns == wa).all()
+        for x, y in zip(alns, wa):
+            assert list(pool[x["cigar_offset"]:x["cigar_offset"] + x["cigar_len"]]) == \
+                list(wp[y["cigar_offset"]:y["cigar_offset"] + y["cigar_len"]])
+    # the pending limit
+    q, j = batches[0]
+    many = []
+    try:
+        for _ in range(12):
+            many.append(c.extend_async(q, j[:50]))
+        with pytest.raises(RuntimeError, match=r"\(-5\)"):
+            c.extend_async(q, j[:50])
+        assert c.extend(q, j[:50])[0].shape == (50,)      # synchronous calls still get a lane
+    finally:
+        for p in many:
+            p.wait()
+    empty = c.extend_async(q, j[:0])
+    assert empty.ready()
+    assert empty.wait()[0].shape == (0,)
