@@ -457,10 +457,11 @@ k_lookup(const rsa_query_randstrobe* __restrict__ qrs, const uint32_t* __restric
                 if (lo < b && p.rs[lo].hash == q.hash) {
                     o.pos = lo;
                     o.flags = 1;
-                    const uint64_t probe = lo + p.filter_cutoff;   // is_filtered (index.hpp:91-93)
-                    const uint64_t h2 = probe < p.n ? p.rs[probe].hash : END64;
-                    if (h2 == q.hash) o.flags |= 2;
                     ub = upper_bound_hash(p.rs, lo, b, q.hash);
+                    // is_filtered (index.hpp:91-93) probes rs[lo + filter_cutoff].hash == hash;
+                    // equal hashes are contiguous from lo to ub (one bucket), so that is
+                    // ub - lo > filter_cutoff, and the probe's random line is not fetched
+                    if (ub - lo > (uint64_t)p.filter_cutoff) o.flags |= 2;
                     o.count = (uint32_t)min<uint64_t>(ub - lo, 0xFFFFFFFFull);
                     if (o.count <= 1000) {
                         // add_to_hits_per_ref min_diff filter (nam.cpp:68-85)
