@@ -102,24 +102,45 @@ struct FwdG {
     int best[2], col[2], row[2];     // [0] byte layout, [1] word layout; best as f16 bits
 };
 
-// forward pass, both layouts at once (low half: byte layout, 16 stripes; high
-// half: word layout, 8 stripes); row p of this lane is gl * R + r
+// query profile of one job in LDS: [code 0..4][lane][GS_RP] f16 scores (match or
+// -mismatch) of the lane's rows, so a step reads its column's R scores with
+// ds_read_b64s instead of a compare + select per row
+template <int R> struct ProfDim {
+    static constexpr int RP = (R + 3) & ~3;                  // rows padded to 8 bytes
+    static constexpr int CODE_STRIDE = GS_G * RP;            // u16 entries per reference code
+    static constexpr int JOB = 5 * CODE_STRIDE;              // u16 entries per job
+};
+
 template <int R>
-__device__ __forceinline__ FwdG fwd_g(const int (&qv)[R], int nrow, const uint8_t* __restrict__ rc, int ncol, int S,
-                                      bool on, int match, int mismatch, int gO, int gE, int gl) {
+__device__ __forceinline__ void prof_load(const uint16_t* __restrict__ lane_prof, int code, uint32_t (&w)[ProfDim<R>::RP / 2]) {
+    const uint2* src = reinterpret_cast<const uint2*>(lane_prof + code * ProfDim<R>::CODE_STRIDE);
+#pragma unroll
+    for (int k = 0; k < ProfDim<R>::RP / 4; ++k) {
+        const uint2 v = src[k];
+        w[2 * k] = v.x;
+        w[2 * k + 1] = v.y;
+    }
+}
+
+// forward pass, both layouts at once (low half: byte layout, 16 stripes; high
+// half: word layout, 8 stripes); row p of this lane is gl * R + r.  lane_prof is
+// this lane's profile slice; code(x) of column x is rc[x] for 0 <= x < ncol.
+template <int R>
+__device__ __forceinline__ FwdG fwd_g(const uint16_t* __restrict__ lane_prof, int nrow,
+                                      const uint8_t* __restrict__ rc, int ncol, int S, bool on, int gO, int gE,
+                                      int gl) {
+    constexpr int RP = ProfDim<R>::RP;
     const int seg_b = (nrow + 15) / 16, seg_w = (nrow + 7) / 8;
     hh2 E[R], Hc[R];
-    uint32_t ssm[R];
+    uint32_t ssm[R], B0[R], B1[R];
     const hh2 zero = h2_from(0u);
     const hh2 GO2 = h2_from(h2_pair(gO)), GE2 = h2_from(h2_pair(gE));
-    uint32_t M2 = h2_pair(match), X2 = h2_pair(-mismatch);
-    // keep the two packed scores in registers: otherwise the compiler selects the
-    // integer score per row and converts it to packed f16 there (4 more ops a cell)
-    asm volatile("" : "+v"(M2), "+v"(X2));
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         E[r] = zero;
         Hc[r] = zero;
+        B0[r] = 0;
+        B1[r] = 0;
         const int p = gl * R + r;
         ssm[r] = ((p % seg_b) == 0 ? 0u : 0x0000FFFFu) | ((p % seg_w) == 0 ? 0u : 0xFFFF0000u);
     }
@@ -128,20 +149,28 @@ __device__ __forceinline__ FwdG fwd_g(const int (&qv)[R], int nrow, const uint8_
     o.best[0] = o.best[1] = 0;
     o.col[0] = o.col[1] = INT_MAX;
     o.row[0] = o.row[1] = INT_MAX;
-    int rnext = (on && gl == 0 && ncol > 0) ? rc[0] : 0;     // the next step's reference code, loaded a step ahead
+    // software pipeline over columns: at step s this lane works on column c = s - gl
+    // with the profile words P of code(c); code(c + 1) is known, and the step loads
+    // the profile of code(c + 1) and the code of c + 2 (LDS latency hidden by a step)
+    auto code_at = [&](int x) -> int { return (on && x >= 0 && x < ncol) ? (int)rc[x] : 4; };
+    uint32_t P[RP / 2], Pn[RP / 2];
+    prof_load<R>(lane_prof, code_at(-gl), P);
+    int code1 = code_at(1 - gl);
     for (int s = 0; s < S; ++s) {
         const uint32_t F_in = row_shr1(F_out);
         const uint32_t Fw_in = row_shr1(Fw_out);
         const uint32_t Hl_in = row_shr1(H_last);
         const int c = s - gl;
-        const int rcode = rnext;
-        if (on && c + 1 >= 0 && c + 1 < ncol) rnext = rc[c + 1];
+        prof_load<R>(lane_prof, code1, Pn);
+        const int code2 = code_at(c + 2);
         if (on && c >= 0 && c < ncol) {
             hh2 dg = h2_from(diag_top), F = h2_from(F_in), Fw = h2_from(Fw_in), cm = zero;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 Fw = h2_from(h2_bits(Fw) & ssm[r]);
-                const hh2 diag = dg + h2_from(qv[r] == rcode ? M2 : X2);
+                const hh2 pw = h2_from(P[r >> 1]);
+                const hh2 sc = (r & 1) ? __builtin_shufflevector(pw, pw, 1, 1) : __builtin_shufflevector(pw, pw, 0, 0);
+                const hh2 diag = dg + sc;
                 const hh2 hm = hmax3(diag, E[r], Fw);
                 const hh2 h = hmax(hm, F);
                 dg = Hc[r];
@@ -156,21 +185,38 @@ __device__ __forceinline__ FwdG fwd_g(const int (&qv)[R], int nrow, const uint8_
             Fw_out = h2_bits(Fw);
             H_last = h2_bits(Hc[R - 1]);
             const uint32_t cmb = h2_bits(cm);
+            // a new best of a layout: remember the column and this column's rows; the
+            // row itself is searched once after the pass
+            const int v0 = (int)(cmb & 0xFFFFu), v1 = (int)(cmb >> 16);
+            if (v0 > o.best[0]) {
+                o.best[0] = v0;
+                o.col[0] = c;
 #pragma unroll
-            for (int hf = 0; hf < 2; ++hf) {
-                const int v = (int)((cmb >> (16 * hf)) & 0xFFFFu);
-                if (v > o.best[hf]) {
-                    o.best[hf] = v;
-                    o.col[hf] = c;
-                    int row = INT_MAX;
+                for (int r = 0; r < R; ++r) B0[r] = h2_bits(Hc[r]);
+            }
+            if (v1 > o.best[1]) {
+                o.best[1] = v1;
+                o.col[1] = c;
 #pragma unroll
-                    for (int r = R - 1; r >= 0; --r)
-                        if (gl * R + r < nrow && (int)((h2_bits(Hc[r]) >> (16 * hf)) & 0xFFFFu) == v) row = gl * R + r;
-                    o.row[hf] = row;
-                }
+                for (int r = 0; r < R; ++r) B1[r] = h2_bits(Hc[r]);
             }
         }
         diag_top = Hl_in;
+#pragma unroll
+        for (int k = 0; k < RP / 2; ++k) P[k] = Pn[k];
+        code1 = code2;
+    }
+    // the smallest valid row of the best column reaching the best (per layout)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+        if (o.col[hf] == INT_MAX) continue;
+        int row = INT_MAX;
+#pragma unroll
+        for (int r = R - 1; r >= 0; --r) {
+            const uint32_t b = hf ? B1[r] : B0[r];
+            if (gl * R + r < nrow && (int)((b >> (16 * hf)) & 0xFFFFu) == o.best[hf]) row = gl * R + r;
+        }
+        o.row[hf] = row;
     }
     return o;
 }
@@ -178,12 +224,14 @@ __device__ __forceinline__ FwdG fwd_g(const int (&qv)[R], int nrow, const uint8_
 __device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
 
 // reverse pass (one layout, int32): row p -> query qend - p, column c -> ref rend - c.
+// lane_prof holds this lane's rows of the reversed query's profile (int16 scores).
 // Returns the first column whose valid-row maximum equals `terminate` (and its
 // smallest such row) through tcol/trow, INT_MAX if none.
 template <int R>
-__device__ __forceinline__ void rev_g(const int (&qr)[R], int nrow, const uint8_t* __restrict__ rc, int ncol,
-                                      int rend, int seg, int terminate, int S, bool on, int match, int mismatch,
-                                      int gO, int gE, int gl, int& tcol, int& trow) {
+__device__ __forceinline__ void rev_g(const uint16_t* __restrict__ lane_prof, int nrow, const uint8_t* __restrict__ rc,
+                                      int ncol, int rend, int seg, int terminate, int S, bool on, int gO, int gE,
+                                      int gl, int& tcol, int& trow) {
+    constexpr int RP = ProfDim<R>::RP;
     const int lanes_used = (nrow + R - 1) / R;
     int E[R], Hc[R], ssm[R];
     bool valid[R];
@@ -199,20 +247,25 @@ __device__ __forceinline__ void rev_g(const int (&qr)[R], int nrow, const uint8_
     tcol = INT_MAX;
     trow = INT_MAX;
     bool done = !on;
-    int rnext = (on && gl == 0 && ncol > 0) ? rc[rend] : 0;   // the next step's reference code, a step ahead
+    auto code_at = [&](int x) -> int { return (on && x >= 0 && x < ncol) ? (int)rc[rend - x] : 4; };
+    uint32_t P[RP / 2], Pn[RP / 2];
+    prof_load<R>(lane_prof, code_at(-gl), P);
+    int code1 = code_at(1 - gl);
     for (int s = 0; s < S; ++s) {
         const int F_in = (int)row_shr1((uint32_t)F_out);
         const int Fw_in = (int)row_shr1((uint32_t)Fw_out);
         const int Hl_in = (int)row_shr1((uint32_t)H_last);
         const int c = s - gl;
-        const int rcode = rnext;
-        if (on && c + 1 >= 0 && c + 1 < ncol) rnext = rc[rend - (c + 1)];
+        prof_load<R>(lane_prof, code1, Pn);
+        const int code2 = code_at(c + 2);
         if (on && c >= 0 && c < ncol) {
             int dg = diag_top, F = F_in, Fw = Fw_in, cm = 0;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 Fw &= ssm[r];
-                const int diag = dg + (qr[r] == rcode ? match : -mismatch);
+                const uint32_t w = P[r >> 1];
+                const int sc = (r & 1) ? ((int)w >> 16) : ((int)(w << 16) >> 16);
+                const int diag = dg + sc;
                 const int hm = max3i(diag, E[r], Fw);          // E, Fw >= 0: the 0 of max(diag, 0)
                 const int h = max(hm, F);
                 dg = Hc[r];
@@ -239,11 +292,37 @@ __device__ __forceinline__ void rev_g(const int (&qr)[R], int nrow, const uint8_
             }
         }
         diag_top = Hl_in;
+#pragma unroll
+        for (int k = 0; k < RP / 2; ++k) P[k] = Pn[k];
+        code1 = code2;
         if ((s & 7) == 7) {
             // a job is finished once its first terminating column has crossed every lane
             const int m = grp_min(tcol);
             if (m != INT_MAX && s >= m + lanes_used - 1) done = true;
             if (wave_min_i32(done ? 1 : 0)) break;
+        }
+    }
+}
+
+// this lane's rows of a query profile: the f16 (fwd) or int16 (rev) score of row
+// p (query code q[r], 7 = never matches) against reference code 0..4
+template <int R>
+__device__ __forceinline__ void prof_build(uint16_t* __restrict__ lane_prof, const int (&q)[ProfDim<R>::RP], uint32_t m16,
+                                           uint32_t x16) {
+    constexpr int RP = ProfDim<R>::RP;
+#pragma unroll
+    for (int code = 0; code < 5; ++code) {
+        uint2* dst = reinterpret_cast<uint2*>(lane_prof + code * ProfDim<R>::CODE_STRIDE);
+#pragma unroll
+        for (int k = 0; k < RP / 4; ++k) {
+            uint32_t w[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t lo = q[4 * k + 2 * h] == code ? m16 : x16;
+                const uint32_t hi = q[4 * k + 2 * h + 1] == code ? m16 : x16;
+                w[h] = lo | (hi << 16);
+            }
+            dst[k] = make_uint2(w[0], w[1]);
         }
     }
 }
@@ -259,6 +338,7 @@ k_ext_scan_g(const ExtJobDev* __restrict__ jobs, const int* __restrict__ order, 
              const char* __restrict__ qbuf, const char* __restrict__ ref, ScanRes* __restrict__ out,
              int match, int mismatch, int gO, int gE) {
     __shared__ uint8_t s_r[GS_JOBS][GS_MAXR];
+    __shared__ __attribute__((aligned(16))) uint16_t s_prof[GS_JOBS][ProfDim<R>::JOB];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int slot = wave * (64 / GS_G) + lane / GS_G, gl = lane & (GS_G - 1);
     const int k = blockIdx.x * GS_JOBS + slot;
@@ -283,19 +363,25 @@ k_ext_scan_g(const ExtJobDev* __restrict__ jobs, const int* __restrict__ order, 
             }
         }
     }
-    int qv[R];
+    // this lane's rows of the query profile: score of row p against reference code
+    // 0..4 (N and padding rows never score a match, not even vs N)
+    uint16_t* lane_prof = s_prof[slot] + gl * ProfDim<R>::RP;
+    {
+        int qv[ProfDim<R>::RP];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int p = gl * R + r;
-        const int code = p < qlen ? ssw_code_sel((unsigned char)qbuf[jb.q_off + p]) : 7;
-        qv[r] = code < 4 ? code : 7;          // N (and padding) never scores a match, not even vs N
+        for (int r = 0; r < ProfDim<R>::RP; ++r) {
+            const int p = gl * R + r;
+            const int code = (r < R && p < qlen) ? ssw_code_sel((unsigned char)qbuf[jb.q_off + p]) : 7;
+            qv[r] = code < 4 ? code : 7;
+        }
+        prof_build<R>(lane_prof, qv, h2_pair(match) & 0xFFFFu, h2_pair(-mismatch) & 0xFFFFu);
     }
     __syncthreads();
 
     // forward pass: every job of the wave runs until the longest one is done
     const int lanes_used = (qlen + R - 1) / R;
     const int S = wave_max_i32(on ? rlen + lanes_used - 1 : 0);
-    const FwdG fo = fwd_g<R>(qv, qlen, rc, rlen, S, on && gl < lanes_used, match, mismatch, gO, gE, gl);
+    const FwdG fo = fwd_g<R>(lane_prof, qlen, rc, rlen, S, on && gl < lanes_used, gO, gE, gl);
     // maxima as f16 bit patterns (order-preserving for values >= +0)
     const int bb = grp_max(fo.best[0]);
     const int sb = h_bits_to_int((uint32_t)bb);
@@ -315,23 +401,31 @@ k_ext_scan_g(const ExtJobDev* __restrict__ jobs, const int* __restrict__ order, 
     const bool ron = on && score1 > 0;
     const int nrow = ron ? read_end1 + 1 : 0, ncol = ron ? ref_end1 + 1 : 0;
     const int rl_used = (nrow + R - 1) / R;
-    int qr[R];
+    // the reversed query's profile replaces the forward one in this job's LDS slot
+    // (only this job's 16 lanes, one wavefront, read and write it: LDS operations of
+    // a wave complete in order, and the fence orders the writes before the reads)
+    {
+        int qr[ProfDim<R>::RP];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int p = gl * R + r;
-        int code = 7;
-        if (p < nrow) {
-            code = ssw_code_sel((unsigned char)qbuf[jb.q_off + (read_end1 - p)]);
-            code = code < 4 ? code : 7;
+        for (int r = 0; r < ProfDim<R>::RP; ++r) {
+            const int p = gl * R + r;
+            int code = 7;
+            if (r < R && p < nrow) {
+                code = ssw_code_sel((unsigned char)qbuf[jb.q_off + (read_end1 - p)]);
+                code = code < 4 ? code : 7;
+            }
+            qr[r] = code;
         }
-        qr[r] = code;
+        prof_build<R>(lane_prof, qr, (uint32_t)match & 0xFFFFu, (uint32_t)(-mismatch) & 0xFFFFu);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
     }
     const int seg = word ? (nrow + 7) / 8 : (nrow + 15) / 16;
     const int S2 = wave_max_i32(ron ? ncol + rl_used - 1 : 0);
     int tc = INT_MAX, tr = INT_MAX;
     if (S2 > 0)
-        rev_g<R>(qr, nrow, rc, ncol, ref_end1, seg > 0 ? seg : 1, score1, S2, ron && gl < rl_used, match, mismatch,
-                 gO, gE, gl, tc, tr);
+        rev_g<R>(lane_prof, nrow, rc, ncol, ref_end1, seg > 0 ? seg : 1, score1, S2, ron && gl < rl_used, gO, gE, gl,
+                 tc, tr);
     const int tcol = grp_min(tc);
     const int trow = grp_min(tc == tcol ? tr : INT_MAX);
 
