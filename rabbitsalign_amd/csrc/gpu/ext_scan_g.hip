@@ -49,6 +49,8 @@
 #define GS_G 16                  // lanes per job: a DPP row (32, half a wave, measured slower at chunk size)
 #define GS_JOBS (GS_WAVES * (64 / GS_G))   // jobs per workgroup
 #define GS_MAXR 1024             // reference window bytes staged in LDS per job
+#define GS_RPAD 32               // code-4 bytes staged on both sides of a window: the scans read
+                                 // a column's code ahead of time without a range check
 
 namespace {
 
@@ -152,11 +154,14 @@ __device__ __forceinline__ FwdG fwd_g(const uint16_t* __restrict__ lane_prof, in
     // software pipeline over columns: at step s this lane works on column c = s - gl
     // with the profile words P of code(c); code(c + 1) is known, and the step loads
     // the profile of code(c + 1) and the code of c + 2 (LDS latency hidden by a step)
-    auto code_at = [&](int x) -> int { return (on && x >= 0 && x < ncol) ? (int)rc[x] : 4; };
+    // columns outside [0, ncol) read the padding (or bytes of no active column)
+    auto code_at = [&](int x) -> int { return (int)rc[x]; };
     uint32_t P[RP / 2], Pn[RP / 2];
     prof_load<R>(lane_prof, code_at(-gl), P);
     int code1 = code_at(1 - gl);
-    for (int s = 0; s < S; ++s) {
+    // one step; the loop below runs two per iteration with the profile buffers
+    // swapped, so no register copies carry P between steps
+    auto step = [&](int s, const uint32_t (&P)[RP / 2], uint32_t (&Pn)[RP / 2]) {
         const uint32_t F_in = row_shr1(F_out);
         const uint32_t Fw_in = row_shr1(Fw_out);
         const uint32_t Hl_in = row_shr1(H_last);
@@ -202,10 +207,14 @@ __device__ __forceinline__ FwdG fwd_g(const uint16_t* __restrict__ lane_prof, in
             }
         }
         diag_top = Hl_in;
-#pragma unroll
-        for (int k = 0; k < RP / 2; ++k) P[k] = Pn[k];
         code1 = code2;
+    };
+    int s = 0;
+    for (; s + 1 < S; s += 2) {
+        step(s, P, Pn);
+        step(s + 1, Pn, P);
     }
+    if (s < S) step(s, P, Pn);
     // the smallest valid row of the best column reaching the best (per layout)
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
@@ -247,7 +256,7 @@ __device__ __forceinline__ void rev_g(const uint16_t* __restrict__ lane_prof, in
     tcol = INT_MAX;
     trow = INT_MAX;
     bool done = !on;
-    auto code_at = [&](int x) -> int { return (on && x >= 0 && x < ncol) ? (int)rc[rend - x] : 4; };
+    auto code_at = [&](int x) -> int { return (int)rc[rend - x]; };   // padded window: no range check
     uint32_t P[RP / 2], Pn[RP / 2];
     prof_load<R>(lane_prof, code_at(-gl), P);
     int code1 = code_at(1 - gl);
@@ -337,7 +346,7 @@ __global__ void __launch_bounds__(64 * GS_WAVES)
 k_ext_scan_g(const ExtJobDev* __restrict__ jobs, const int* __restrict__ order, int n,
              const char* __restrict__ qbuf, const char* __restrict__ ref, ScanRes* __restrict__ out,
              int match, int mismatch, int gO, int gE) {
-    __shared__ uint8_t s_r[GS_JOBS][GS_MAXR];
+    __shared__ uint8_t s_r[GS_JOBS][GS_RPAD + GS_MAXR + GS_RPAD];
     __shared__ __attribute__((aligned(16))) uint16_t s_prof[GS_JOBS][ProfDim<R>::JOB];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int slot = wave * (64 / GS_G) + lane / GS_G, gl = lane & (GS_G - 1);
@@ -348,7 +357,11 @@ k_ext_scan_g(const ExtJobDev* __restrict__ jobs, const int* __restrict__ order, 
     jb.q_off = 0; jb.r_off = 0; jb.qlen = 0; jb.rlen = 0; jb.cig_off = 0;
     if (on) jb = jobs[j];
     const int qlen = (int)jb.qlen, rlen = (int)jb.rlen;
-    uint8_t* rc = s_r[slot];
+    uint8_t* rc = s_r[slot] + GS_RPAD;
+    for (int i = gl; i < GS_RPAD; i += GS_G) {
+        rc[i - GS_RPAD] = 4;
+        rc[rlen + i] = 4;
+    }
     {
         // aligned dwords covering the window (the device reference carries 64 bytes of tail padding)
         const int pre = (int)(jb.r_off & 3);
