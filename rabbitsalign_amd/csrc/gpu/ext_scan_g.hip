@@ -260,7 +260,9 @@ __device__ __forceinline__ void rev_g(const uint16_t* __restrict__ lane_prof, in
     uint32_t P[RP / 2], Pn[RP / 2];
     prof_load<R>(lane_prof, code_at(-gl), P);
     int code1 = code_at(1 - gl);
-    for (int s = 0; s < S; ++s) {
+    // one step (two per loop iteration, profile buffers swapped); true once every
+    // job of the wave is finished
+    auto step = [&](int s, const uint32_t (&P)[RP / 2], uint32_t (&Pn)[RP / 2]) -> bool {
         const int F_in = (int)row_shr1((uint32_t)F_out);
         const int Fw_in = (int)row_shr1((uint32_t)Fw_out);
         const int Hl_in = (int)row_shr1((uint32_t)H_last);
@@ -301,16 +303,21 @@ __device__ __forceinline__ void rev_g(const uint16_t* __restrict__ lane_prof, in
             }
         }
         diag_top = Hl_in;
-#pragma unroll
-        for (int k = 0; k < RP / 2; ++k) P[k] = Pn[k];
         code1 = code2;
         if ((s & 7) == 7) {
             // a job is finished once its first terminating column has crossed every lane
             const int m = grp_min(tcol);
             if (m != INT_MAX && s >= m + lanes_used - 1) done = true;
-            if (wave_min_i32(done ? 1 : 0)) break;
+            if (wave_min_i32(done ? 1 : 0)) return true;
         }
+        return false;
+    };
+    int s = 0;
+    for (; s + 1 < S; s += 2) {
+        if (step(s, P, Pn)) return;
+        if (step(s + 1, Pn, P)) return;
     }
+    if (s < S) (void)step(s, P, Pn);
 }
 
 // this lane's rows of a query profile: the f16 (fwd) or int16 (rev) score of row
