@@ -52,7 +52,7 @@ int main(int argc, char** argv) {
     if (argc < 4) { fprintf(stderr, "sam_replay <fasta> <calls> <out>\n"); return 2; }
     References refs = References::from_fasta(argv[1]);
     std::ifstream in(argv[2]);
-    std::string out;
+    SamText out;
     std::unique_ptr<Sam> sam;
     std::string line;
     while (std::getline(in, line)) {

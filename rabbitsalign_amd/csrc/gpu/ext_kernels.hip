@@ -859,7 +859,7 @@ __global__ void __launch_bounds__(64)
 k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan, int n_jobs,
              const char* __restrict__ qbuf, const char* __restrict__ ref, uint32_t* __restrict__ cig_pool,
              uint32_t* __restrict__ raw_pool, rsa_aln* __restrict__ out, int match, int mismatch, int gO, int gE,
-             int bonus, int* __restrict__ queue, int* __restrict__ qcount) {
+             int bonus, int* __restrict__ queue, int* __restrict__ qcount, int* __restrict__ overflow) {
     __shared__ __attribute__((aligned(16))) int8_t s_dir[B16_GROUPS][B16_DIRCAP];
     __shared__ uint8_t s_qc[B16_GROUPS][B16_SEGCAP];
     __shared__ uint8_t s_rc[B16_GROUPS][B16_SEGCAP];
@@ -868,6 +868,7 @@ k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
     if (j >= n_jobs) return;                       // whole group leaves together
     const ExtJobDev jb = jobs[j];
     const ScanRes sr = scan[j];
+    if (z == 0) overflow[j] = 0;                   // k_ext_band64 sets the jobs it cannot hold
     if (sr.status != 0) {                          // ref > 2000 (aligner.cpp:119-125)
         if (z == 0) aln_sentinel(out, j, jb, -1000000);
         return;
@@ -878,7 +879,15 @@ k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
     }
     const bool done = band_group<16, B16_DIRCAP, B16_SEGCAP, B16_SEGCAP>(
         j, z, jb, sr, qbuf, ref, cig_pool, raw_pool, out, match, mismatch, gO, gE, bonus, s_dir[g], s_qc[g], s_rc[g]);
-    if (!done && z == 0) queue[atomicAdd(qcount, 1)] = j;
+    if (!done && z == 0) {
+        // an empty result until a wider kernel writes it: the CIGAR compaction reads
+        // every job, including one the 64-lane kernel leaves to the one-lane pass
+        rsa_aln a;
+        a.sw_score = 0; a.edit_distance = 0; a.ref_start = a.ref_end = a.query_start = a.query_end = 0;
+        a.cigar_offset = jb.cig_off; a.cigar_len = 0; a.pad_ = 0;
+        out[j] = a;
+        queue[atomicAdd(qcount, 1)] = j;
+    }
 }
 
 #define B64_DIRCAP 32768
@@ -962,8 +971,8 @@ __global__ void __launch_bounds__(1024) k_cig_bscan(uint64_t* __restrict__ bsum,
 }
 
 __global__ void __launch_bounds__(CCP_THREADS)
-k_cig_copy(rsa_aln* __restrict__ alns, int n_jobs, const uint64_t* __restrict__ bbase,
-           const uint32_t* __restrict__ slots, uint32_t* __restrict__ dense) {
+k_cig_copy(const rsa_aln* __restrict__ alns, rsa_aln* __restrict__ alns_out, int n_jobs,
+           const uint64_t* __restrict__ bbase, const uint32_t* __restrict__ slots, uint32_t* __restrict__ dense) {
     __shared__ uint64_t s[CCP_THREADS];
     __shared__ uint64_t s_src[CCP_THREADS];
     const int t = threadIdx.x;
@@ -984,15 +993,19 @@ k_cig_copy(rsa_aln* __restrict__ alns, int n_jobs, const uint64_t* __restrict__ 
         const uint64_t start = lo ? s[lo - 1] : 0;
         dense[base + f] = slots[s_src[lo] + (f - start)];
     }
-    if (i < n_jobs) alns[i].cigar_offset = base + incl - len;
+    if (i < n_jobs) {                                // the results with packed offsets; alns keeps the slots
+        rsa_aln a = alns[i];
+        a.cigar_offset = base + incl - len;
+        alns_out[i] = a;
+    }
 }
 
-void launch_cigar_compact(hipStream_t st, rsa_aln* alns, int n_jobs, const uint32_t* slots, uint32_t* dense,
-                          uint64_t* bsum, uint64_t* total) {
+void launch_cigar_compact(hipStream_t st, const rsa_aln* alns, rsa_aln* alns_out, int n_jobs, const uint32_t* slots,
+                          uint32_t* dense, uint64_t* bsum, uint64_t* total) {
     const int nb = (n_jobs + CCP_THREADS - 1) / CCP_THREADS;
     hipLaunchKernelGGL(k_cig_bsum, dim3(nb), dim3(CCP_THREADS), 0, st, alns, n_jobs, bsum);
     hipLaunchKernelGGL(k_cig_bscan, dim3(1), dim3(1024), 0, st, bsum, nb, total);
-    hipLaunchKernelGGL(k_cig_copy, dim3(nb), dim3(CCP_THREADS), 0, st, alns, n_jobs, bsum, slots, dense);
+    hipLaunchKernelGGL(k_cig_copy, dim3(nb), dim3(CCP_THREADS), 0, st, alns, alns_out, n_jobs, bsum, slots, dense);
 }
 
 // host-side launcher: RMAX from the longest query of the batch
@@ -1005,9 +1018,9 @@ void launch_ext_scan(int rmax, dim3 grid, dim3 block, hipStream_t st, const ExtJ
 
 void launch_ext_band16(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n, const char* q,
                        const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match, int mismatch, int gO,
-                       int gE, int bonus, int* queue, int* qcount) {
+                       int gE, int bonus, int* queue, int* qcount, int* overflow) {
     hipLaunchKernelGGL(k_ext_band16, grid, dim3(64), 0, st, jobs, scan, n, q, ref, cig, raw, out, match, mismatch, gO,
-                       gE, bonus, queue, qcount);
+                       gE, bonus, queue, qcount, overflow);
 }
 
 void launch_ext_band64(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, const char* q,

@@ -35,12 +35,12 @@ __global__ void k_ext_band(const ExtJobDev* jobs, const ScanRes* scan, int n_job
                            int gE, int bonus, int* overflow, int over_code);
 void launch_ext_band16(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n, const char* q,
                        const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match, int mismatch, int gO,
-                       int gE, int bonus, int* queue, int* qcount);
+                       int gE, int bonus, int* queue, int* qcount, int* overflow);
 void launch_ext_band64(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, const char* q,
                        const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match, int mismatch, int gO,
                        int gE, int bonus, const int* queue, const int* qcount, int* overflow, int* ocount);
-void launch_cigar_compact(hipStream_t st, rsa_aln* alns, int n_jobs, const uint32_t* slots, uint32_t* dense,
-                          uint64_t* bsum, uint64_t* total);
+void launch_cigar_compact(hipStream_t st, const rsa_aln* alns, rsa_aln* alns_out, int n_jobs, const uint32_t* slots,
+                          uint32_t* dense, uint64_t* bsum, uint64_t* total);
 
 void index_build_peek(const rsa_index_build* b, int* device, int* bits);
 void index_build_release(rsa_index_build* b, int* device, char** ref, rsa_ref_randstrobe** rs, uint64_t** starts,
@@ -99,9 +99,10 @@ struct Lane {
     KTimer kt;
     bool busy = false;
     // extension
-    DevBuf d_q, d_jobs, d_scan, d_alns, d_alns2, d_cig, d_dense, d_raw, d_scratch, d_over, d_queue, d_idx, d_status,
-        d_order, d_bsum;
-    HostBuf h_jobs, h_over, h_status, h_order;
+    // d_jobs / h_jobs: one staged upload per call, [ExtJobDev x n | scan order x n | ExtStatus (zeroed)];
+    // d_alns holds results with CIGAR slot offsets, d_alns_out the copy with packed offsets
+    DevBuf d_q, d_jobs, d_scan, d_alns, d_alns_out, d_cig, d_dense, d_raw, d_scratch, d_over, d_queue, d_idx, d_bsum;
+    HostBuf h_jobs, h_over, h_status;
     // seeding
     SeedBufs sb;
 };
@@ -301,10 +302,10 @@ void rsa_close(rsa_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     for (Lane* l : ctx->lanes) {
         if (l->stream) (void)hipStreamSynchronize(l->stream);
-        for (DevBuf* b : {&l->d_q, &l->d_jobs, &l->d_scan, &l->d_alns, &l->d_alns2, &l->d_cig, &l->d_dense, &l->d_raw,
-                          &l->d_scratch, &l->d_over, &l->d_queue, &l->d_idx, &l->d_status, &l->d_order, &l->d_bsum})
+        for (DevBuf* b : {&l->d_q, &l->d_jobs, &l->d_scan, &l->d_alns, &l->d_alns_out, &l->d_cig, &l->d_dense, &l->d_raw,
+                          &l->d_scratch, &l->d_over, &l->d_queue, &l->d_idx, &l->d_bsum})
             b->release();
-        l->h_jobs.release(); l->h_over.release(); l->h_status.release(); l->h_order.release();
+        l->h_jobs.release(); l->h_over.release(); l->h_status.release();
         seed_bufs_release(l->sb);
         l->kt.destroy();
         if (l->stream) (void)hipStreamDestroy(l->stream);
@@ -345,6 +346,11 @@ struct ExtStatus {            // device-side counters of one rsa_extend call
     uint64_t total;           // dense CIGAR ops (k_cigar_compact)
 };
 
+// byte offsets of the scan order and the status in the staged job upload of n jobs
+static size_t stage_order_off(uint32_t n) { return sizeof(ExtJobDev) * (size_t)n; }
+static size_t stage_status_off(uint32_t n) { return (stage_order_off(n) + sizeof(int) * (size_t)n + 15) & ~(size_t)15; }
+static size_t stage_bytes(uint32_t n) { return stage_status_off(n) + sizeof(ExtStatus); }
+
 }  // extern "C"
 
 // One extension call between its enqueue and its completion: rsa_extend runs
@@ -356,6 +362,7 @@ struct rsa_pending {
     uint32_t n = 0;
     int32_t match = 0, mismatch = 0, gap_open = 0, gap_extend = 0, end_bonus = 0;
     uint64_t guess = 0, cells = 0, qr_bytes = 0;
+    ExtStatus* d_status = nullptr;     // in the lane's staged upload
 };
 
 // k_cigar_compact, then the status, results and the first `guess` CIGAR entries
@@ -364,12 +371,11 @@ static int ext_compact_copy(rsa_pending& P) {
     rsa_ctx* ctx = P.ctx;
     Lane* L = P.L;
     hipStream_t st = L->stream;
-    ExtStatus* dst = L->d_status.as<ExtStatus>();
-    launch_cigar_compact(st, L->d_alns.as<rsa_aln>(), (int)P.n, L->d_cig.as<uint32_t>(), L->d_dense.as<uint32_t>(),
-                         L->d_bsum.as<uint64_t>(), &dst->total);
+    launch_cigar_compact(st, L->d_alns.as<rsa_aln>(), L->d_alns_out.as<rsa_aln>(), (int)P.n, L->d_cig.as<uint32_t>(),
+                         L->d_dense.as<uint32_t>(), L->d_bsum.as<uint64_t>(), &P.d_status->total);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(L->h_status.p, L->d_status.p, sizeof(ExtStatus), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(P.out->alns, L->d_alns.p, sizeof(rsa_aln) * P.n, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(L->h_status.p, P.d_status, sizeof(ExtStatus), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(P.out->alns, L->d_alns_out.p, sizeof(rsa_aln) * P.n, hipMemcpyDeviceToHost, st));
     if (P.guess)
         HIPCHK(hipMemcpyAsync(P.out->cigar_pool, L->d_dense.p, sizeof(uint32_t) * P.guess, hipMemcpyDeviceToHost, st));
     return RSA_OK;
@@ -385,7 +391,7 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
     P.match = jb->match; P.mismatch = jb->mismatch; P.gap_open = jb->gap_open; P.gap_extend = jb->gap_extend;
     P.end_bonus = jb->end_bonus;
     // host job descriptors
-    HIPCHK(L->h_jobs.ensure(sizeof(ExtJobDev) * n));
+    HIPCHK(L->h_jobs.ensure(stage_bytes(n)));
     ExtJobDev* hj = L->h_jobs.as<ExtJobDev>();
     uint64_t cig_off = 0;
     uint64_t cells = 0, qr_bytes = 0;
@@ -420,23 +426,22 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
     P.cells = cells;
     P.qr_bytes = qr_bytes;
     HIPCHK(L->d_q.ensure(jb->queries_len + 16));
-    HIPCHK(L->d_jobs.ensure(sizeof(ExtJobDev) * n));
+    HIPCHK(L->d_jobs.ensure(stage_bytes(n)));
     HIPCHK(L->d_scan.ensure(sizeof(ScanRes) * n));
     HIPCHK(L->d_alns.ensure(sizeof(rsa_aln) * n));
-    HIPCHK(L->d_alns2.ensure(sizeof(rsa_aln) * n));
+    HIPCHK(L->d_alns_out.ensure(sizeof(rsa_aln) * n));
     HIPCHK(L->d_cig.ensure(sizeof(uint32_t) * (bound + 16)));
     HIPCHK(L->d_dense.ensure(sizeof(uint32_t) * (bound + 16)));
     HIPCHK(L->d_raw.ensure(sizeof(uint32_t) * (bound + 16)));
     HIPCHK(L->d_over.ensure(sizeof(int) * n));
     HIPCHK(L->d_queue.ensure(sizeof(int) * n));
-    HIPCHK(L->d_status.ensure(sizeof(ExtStatus)));
     HIPCHK(L->d_bsum.ensure(sizeof(uint64_t) * ((n + 255) / 256 + 1)));
     HIPCHK(L->h_status.ensure(sizeof(ExtStatus)));
     hipStream_t st = L->stream;
-    ExtStatus* dst = L->d_status.as<ExtStatus>();
+    ExtStatus* dst = reinterpret_cast<ExtStatus*>(L->d_jobs.as<char>() + stage_status_off(n));
+    P.d_status = dst;
+    memset(L->h_jobs.as<char>() + stage_status_off(n), 0, sizeof(ExtStatus));
     HIPCHK(hipMemcpyAsync(L->d_q.p, jb->queries, jb->queries_len, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(L->d_jobs.p, hj, sizeof(ExtJobDev) * n, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemsetAsync(L->d_status.p, 0, sizeof(ExtStatus), st));
     // Scan routing: jobs the grouped kernel takes (query <= 256 bp, window <= 1 KB,
     // parameters it computes exactly) go to it per rows-per-lane class, sorted by window
     // length (longest first) so the four jobs of a wave run about as long; the
@@ -446,8 +451,7 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
     int cls_rows[NCLS];
     scan_g_classes(cls_rows);
     uint32_t cls_n[NCLS] = {0}, rest_n = 0;
-    HIPCHK(L->h_order.ensure(sizeof(int) * (n + 1)));
-    int* ord = L->h_order.as<int>();
+    int* ord = reinterpret_cast<int*>(L->h_jobs.as<char>() + stage_order_off(n));
     if (grouped) {
         const uint32_t maxr = (uint32_t)scan_g_max_ref();
         std::vector<uint32_t> cnt((size_t)NCLS * (maxr + 1), 0);
@@ -481,12 +485,12 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
         rest_n = n;
         for (uint32_t i = 0; i < n; ++i) ord[i] = (int)i;
     }
-    HIPCHK(L->d_order.ensure(sizeof(int) * (n + 1)));
-    HIPCHK(hipMemcpyAsync(L->d_order.p, ord, sizeof(int) * n, hipMemcpyHostToDevice, st));
+    // jobs, scan order and the zeroed status in one copy
+    HIPCHK(hipMemcpyAsync(L->d_jobs.p, L->h_jobs.p, stage_bytes(n), hipMemcpyHostToDevice, st));
     L->kt.reset();
     L->kt.begin(st, RSA_K_EXT_SCAN);
     {
-        const int* d_ord = L->d_order.as<int>();
+        const int* d_ord = reinterpret_cast<const int*>(L->d_jobs.as<char>() + stage_order_off(n));
         uint32_t off = 0;
         for (int c = 0; c < NCLS; ++c) {
             if (!cls_n[c]) continue;
@@ -504,20 +508,18 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
         }
     }
     L->kt.end(st);
-    // every job's result is defined before any kernel reads it: the band kernels write
-    // the jobs they finish, and the CIGAR compaction below runs over all jobs, including
-    // the ones the 64-lane kernel leaves for the one-lane pass (empty CIGAR until then)
-    HIPCHK(hipMemsetAsync(L->d_alns.p, 0, sizeof(rsa_aln) * n, st));
-    // 16 lanes per job for the common narrow bands; the rest queue for 64-lane waves
+    // 16 lanes per job for the common narrow bands; the rest queue for 64-lane waves.
+    // k_ext_band16 writes every job's result (an empty one for the jobs it queues, so
+    // the compaction below never reads an unwritten result) and clears every job's
+    // overflow flag, which k_ext_band64 sets for the bands it cannot hold
     L->kt.begin(st, RSA_K_EXT_BAND);
     launch_ext_band16(dim3((n + 3) / 4), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(), (int)n,
                       L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(),
                       L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open, jb->gap_extend, jb->end_bonus,
-                      L->d_queue.as<int>(), &dst->qcount);
+                      L->d_queue.as<int>(), &dst->qcount, L->d_over.as<int>());
     HIPCHK(hipGetLastError());
     L->kt.end(st);
     L->kt.begin(st, RSA_K_EXT_BAND_WIDE);
-    HIPCHK(hipMemsetAsync(L->d_over.p, 0, sizeof(int) * n, st));   // band64 writes only the 1s
     launch_ext_band64(dim3(std::min<uint32_t>(n, BAND64_GRID)), st, L->d_jobs.as<ExtJobDev>(),
                       L->d_scan.as<ScanRes>(), L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(),
                       L->d_raw.as<uint32_t>(), L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open,
@@ -525,8 +527,6 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
                       &dst->ocount);
     HIPCHK(hipGetLastError());
     L->kt.end(st);
-    // k_cigar_compact rewrites cigar_offset in place: keep the slot offsets for a possible re-run
-    HIPCHK(hipMemcpyAsync(L->d_alns2.p, L->d_alns.p, sizeof(rsa_aln) * n, hipMemcpyDeviceToDevice, st));
     P.guess = std::min<uint64_t>(bound, DENSE_GUESS * n);
     return ext_compact_copy(P);
 }
@@ -554,7 +554,6 @@ static int ext_finish(rsa_pending& P) {
         HIPCHK(L->d_idx.ensure(sizeof(int) * big.size()));
         HIPCHK(hipMemcpyAsync(L->d_idx.p, big.data(), sizeof(int) * big.size(), hipMemcpyHostToDevice, st));
         HIPCHK(hipMemsetAsync(L->d_over.p, 0, sizeof(int) * n, st));
-        HIPCHK(hipMemcpyAsync(L->d_alns.p, L->d_alns2.p, sizeof(rsa_aln) * n, hipMemcpyDeviceToDevice, st));
         for (size_t b = 0; b < big.size(); b += BIG_CHUNK) {
             const int cnt = (int)std::min<size_t>(BIG_CHUNK, big.size() - b);
             L->kt.begin(st, RSA_K_EXT_BAND_LANE);

@@ -324,9 +324,9 @@ struct SinkState {
     FILE* f = nullptr;
 };
 
-static void sink_fn(void* user, const std::string& chunk) {
+static void sink_fn(void* user, const char* chunk, size_t bytes) {
     auto* s = (SinkState*)user;
-    if (s->f) fwrite(chunk.data(), 1, chunk.size(), s->f);
+    if (s->f) fwrite(chunk, 1, bytes, s->f);
 }
 
 int rsam_map(rsam* m, const rsam_reads* reads, int threads, int chunk_size, const char* sam_path, rsam_stats* out) {

@@ -106,47 +106,66 @@ static std::string_view strip_suffix(const std::string& name) {   // sam.cpp:29-
     return name;
 }
 
-Sam::Sam(std::string& out, const References& refs, bool eqx, const std::string& rg_id, bool output_unmapped,
+Sam::Sam(SamText& out, const References& refs, bool eqx, const std::string& rg_id, bool output_unmapped,
          bool details)
     : out_(out), refs_(refs), eqx_(eqx), output_unmapped_(output_unmapped), details_(details) {
     tail_ = rg_id.empty() ? "\n" : "\tRG:Z:" + rg_id + "\n";
 }
 
-static void append_details(std::string& out, const Details& d, bool paired) {   // sam.cpp:46-60
-    out += "\tna:i:"; append_uint(out, d.nams);
-    out += "\tnr:i:"; append_uint(out, d.nam_rescue ? 1 : 0);
-    out += "\tal:i:"; append_uint(out, d.tried_alignment);
-    out += "\tga:i:"; append_uint(out, d.gapped);
-    if (paired) { out += "\tmr:i:"; append_uint(out, d.mate_rescue); }
+// room for `bound` more bytes at the end of o (uninitialised); returns where they start
+static inline char* sam_room(SamText& o, size_t bound, size_t& at) {
+    at = o.size();
+    o.resize(at + bound);
+    return o.data() + at;
 }
+static inline void sam_trim(SamText& o, size_t at, const char* p0, const char* p) { o.resize(at + (size_t)(p - p0)); }
+
+static char* put_details(char* p, const Details& d, bool paired) {   // sam.cpp:46-60
+    p = put_str(p, "\tna:i:"); p = put_uint(p, d.nams);
+    p = put_str(p, "\tnr:i:"); p = put_uint(p, d.nam_rescue ? 1 : 0);
+    p = put_str(p, "\tal:i:"); p = put_uint(p, d.tried_alignment);
+    p = put_str(p, "\tga:i:"); p = put_uint(p, d.gapped);
+    if (paired) { p = put_str(p, "\tmr:i:"); p = put_uint(p, d.mate_rescue); }
+    return p;
+}
+static const size_t kDetailsBound = 5 * (6 + 20);
 
 void Sam::add_unmapped(const Record& r, uint16_t flags) {   // sam.cpp:77-92
     if (!output_unmapped_) return;
-    out_.append(strip_suffix(r.name));
-    out_ += '\t';
-    append_uint(out_, flags);
-    out_ += "\t*\t0\t0\t*\t*\t0\t0\t";
-    out_.append(r.seq.empty() ? std::string_view("*") : std::string_view(r.seq));
-    out_ += '\t';
-    out_.append(r.qual.empty() ? std::string_view("*") : std::string_view(r.qual));
-    out_ += tail_;
+    const std::string_view name = strip_suffix(r.name);
+    size_t at;
+    char* const p0 = sam_room(out_, name.size() + r.seq.size() + r.qual.size() + tail_.size() + 48, at);
+    char* p = put_str(p0, name);
+    *p++ = '\t';
+    p = put_uint(p, flags);
+    p = put_str(p, "\t*\t0\t0\t*\t*\t0\t0\t");
+    p = put_str(p, r.seq.empty() ? std::string_view("*") : std::string_view(r.seq));
+    *p++ = '\t';
+    p = put_str(p, r.qual.empty() ? std::string_view("*") : std::string_view(r.qual));
+    p = put_str(p, tail_);
+    sam_trim(out_, at, p0, p);
 }
 
-void Sam::add_unmapped_mate(const Record& r, uint16_t flags, const std::string& mate_ref, uint32_t mate_pos) {
-    out_.append(strip_suffix(r.name));                       // sam.cpp:94-116
-    out_ += '\t';
-    append_uint(out_, flags);
-    out_ += '\t';
-    out_ += mate_ref;
-    out_ += '\t';
-    append_uint(out_, (uint32_t)(mate_pos + 1));
-    out_ += "\t0\t*\t=\t";
-    append_uint(out_, (uint32_t)(mate_pos + 1));
-    out_ += "\t0\t";
-    out_.append(r.seq.empty() ? std::string_view("*") : std::string_view(r.seq));
-    out_ += '\t';
-    out_.append(r.qual.empty() ? std::string_view("*") : std::string_view(r.qual));
-    out_ += tail_;
+void Sam::add_unmapped_mate(const Record& r, uint16_t flags, std::string_view mate_ref, uint32_t mate_pos) {
+    const std::string_view name = strip_suffix(r.name);      // sam.cpp:94-116
+    size_t at;
+    char* const p0 =
+        sam_room(out_, name.size() + mate_ref.size() + r.seq.size() + r.qual.size() + tail_.size() + 64, at);
+    char* p = put_str(p0, name);
+    *p++ = '\t';
+    p = put_uint(p, flags);
+    *p++ = '\t';
+    p = put_str(p, mate_ref);
+    *p++ = '\t';
+    p = put_uint(p, (uint32_t)(mate_pos + 1));
+    p = put_str(p, "\t0\t*\t=\t");
+    p = put_uint(p, (uint32_t)(mate_pos + 1));
+    p = put_str(p, "\t0\t");
+    p = put_str(p, r.seq.empty() ? std::string_view("*") : std::string_view(r.seq));
+    *p++ = '\t';
+    p = put_str(p, r.qual.empty() ? std::string_view("*") : std::string_view(r.qual));
+    p = put_str(p, tail_);
+    sam_trim(out_, at, p0, p);
 }
 
 void Sam::add_unmapped_pair(const Record& r1, const Record& r2) {
@@ -183,18 +202,16 @@ static char* put_cigar(char* p, const Cigar& c, bool eqx) {
     return p;
 }
 
-void Sam::add_record(const std::string& qname, uint16_t flags, const std::string& rname, uint32_t pos, uint8_t mapq,
-                     const Cigar& cigar, const std::string& mate_rname, uint32_t mate_pos, int32_t tlen,
+void Sam::add_record(const std::string& qname, uint16_t flags, std::string_view rname, uint32_t pos, uint8_t mapq,
+                     const Cigar& cigar, std::string_view mate_rname, uint32_t mate_pos, int32_t tlen,
                      std::string_view seq, std::string_view seq_rc, const std::string& qual, int ed, int score,
                      const Details& d) {                        // sam.cpp:141-213
-    std::string& o = out_;
     const std::string_view name = strip_suffix(qname);
     // upper bound of the record: fixed fields + numbers + CIGAR (<= 11 chars an op) + SEQ/QUAL + tags
     const size_t bound = name.size() + rname.size() + mate_rname.size() + std::max(seq.size(), seq_rc.size()) +
-                         qual.size() + 11 * cigar.ops.size() + tail_.size() + 160;
-    const size_t at = o.size();
-    o.resize(at + bound);
-    char* const p0 = &o[at];
+                         qual.size() + 11 * cigar.ops.size() + tail_.size() + 160 + (details_ ? kDetailsBound : 0);
+    size_t at;
+    char* const p0 = sam_room(out_, bound, at);
     char* p = p0;
     p = put_str(p, name);
     *p++ = '\t';
@@ -232,14 +249,9 @@ void Sam::add_record(const std::string& qname, uint16_t flags, const std::string
     } else {
         p = put_str(p, qual.empty() ? std::string_view("*") : std::string_view(qual));
     }
-    if (details_) {
-        o.resize(at + (size_t)(p - p0));
-        append_details(o, d, flags & 1);
-        o += tail_;
-        return;
-    }
+    if (details_) p = put_details(p, d, flags & 1);
     p = put_str(p, tail_);
-    o.resize(at + (size_t)(p - p0));
+    sam_trim(out_, at, p0, p);
 }
 
 void Sam::add_pair(const Alignment& a1, const Alignment& a2, const Record& r1, const Record& r2, std::string_view rc1,
@@ -255,13 +267,13 @@ void Sam::add_pair(const Alignment& a1, const Alignment& a2, const Record& r1, c
         else tlen1 = dist - a1.length;
     }
     if (proper) { f1 |= 2; f2 |= 2; }
-    std::string rn1, rn2;
+    std::string_view rn1, rn2;
     int pos1 = a1.ref_start, pos2 = a2.ref_start;
     if (a1.is_unaligned) { f1 |= 4; f2 |= 8; pos1 = -1; rn1 = "*"; }
     else { if (a1.is_rc) { f1 |= 0x10; f2 |= 0x20; } rn1 = refs_.names[a1.ref_id]; }
     if (a2.is_unaligned) { f2 |= 4; f1 |= 8; pos2 = -1; rn2 = "*"; }
     else { if (a2.is_rc) { f1 |= 0x20; f2 |= 0x10; } rn2 = refs_.names[a2.ref_id]; }
-    std::string mrn1 = rn1, mrn2 = rn2;
+    std::string_view mrn1 = rn1, mrn2 = rn2;
     if ((both && a1.ref_id == a2.ref_id) || (a1.is_unaligned != a2.is_unaligned)) { mrn1 = "="; mrn2 = "="; }
     if (a1.is_unaligned != a2.is_unaligned) {
         if (a1.is_unaligned) pos1 = pos2; else pos2 = pos1;

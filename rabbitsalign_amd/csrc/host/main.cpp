@@ -102,8 +102,8 @@ Opts parse(int argc, char** argv, bool& ok) {
 }
 
 
-void write_sink(void* user, const std::string& chunk) {
-    fwrite(chunk.data(), 1, chunk.size(), (FILE*)user);
+void write_sink(void* user, const char* chunk, size_t bytes) {
+    fwrite(chunk, 1, bytes, (FILE*)user);
 }
 
 }  // namespace

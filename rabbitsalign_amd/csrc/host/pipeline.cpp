@@ -89,7 +89,7 @@ struct OrderedSink {
     void* user;
     bool digest = false;
     std::mutex m;
-    std::map<size_t, std::pair<std::string, SamDigest>> pending;
+    std::map<size_t, std::pair<SamText, SamDigest>> pending;
     size_t next = 0;
     uint64_t bytes = 0;
     SamDigest total;
@@ -98,37 +98,37 @@ struct OrderedSink {
     // page-faults in
     struct Spares {
         std::mutex m;
-        std::vector<std::string> v;
+        std::vector<SamText> v;
     };
     static Spares& spares() {
         static Spares* p = new Spares();     // never destroyed: no exit-time teardown
         return *p;
     }
-    std::string take() {
+    SamText take() {
         static const bool off = getenv("RSA_SAM_REUSE") && atoi(getenv("RSA_SAM_REUSE")) == 0;
         Spares& sp = spares();
         std::lock_guard<std::mutex> g(sp.m);
-        if (off || sp.v.empty()) return std::string();
-        std::string s = std::move(sp.v.back());
+        if (off || sp.v.empty()) return SamText();
+        SamText s = std::move(sp.v.back());
         sp.v.pop_back();
         return s;
     }
-    void give_back(std::string& s) {
+    void give_back(SamText& s) {
         Spares& sp = spares();
         std::lock_guard<std::mutex> g(sp.m);
         if (sp.v.size() >= 48) return;
         s.clear();
         sp.v.push_back(std::move(s));
     }
-    void put(size_t idx, std::string&& s) {
+    void put(size_t idx, SamText&& s) {
         SamDigest d;
-        if (digest) d = SamDigest::of(s);            // in the calling worker
+        if (digest) d = SamDigest::of(s.data(), s.size());   // in the calling worker
         std::lock_guard<std::mutex> g(m);
         pending.emplace(idx, std::make_pair(std::move(s), d));
         for (auto it = pending.find(next); it != pending.end(); it = pending.find(next)) {
             bytes += it->second.first.size();
             total.append(it->second.second);
-            if (sink) sink(user, it->second.first);
+            if (sink) sink(user, it->second.first.data(), it->second.first.size());
             give_back(it->second.first);
             pending.erase(it);
             next++;
@@ -481,7 +481,7 @@ void pe_get_str(PeChunk& c, const MapContext& mc, float mu, float sigma, std::ve
 
 // the chunk's extension results start at infos[pos]
 void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistribution& isize,
-                   std::vector<AlignmentInfo>& infos, size_t pos, const std::string& rg_id, std::string& out) {
+                   std::vector<AlignmentInfo>& infos, size_t pos, const std::string& rg_id, SamText& out) {
     const auto t = Clock::now();
     const size_t n = c.r1.size();
     static const bool pf = !(getenv("RSA_PREFETCH") && atoi(getenv("RSA_PREFETCH")) == 0);
@@ -669,7 +669,7 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
         for (size_t g = 0; g < cs.size(); ++g) {
             PeChunk& c = *cs[g];
             c.times.extend += dt;
-            std::string out = os.take();
+            SamText out = os.take();
             pe_store_last(c, mc, est, infos, first[g], opt.rg_id, out);
             const auto tp = Clock::now();
             os.put(c.index, std::move(out));
@@ -725,7 +725,7 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                     }
                     pre->times.extend += since(te);
                     pre->stats.tot_aligner_calls += jobs.size();
-                    std::string out = os.take();
+                    SamText out = os.take();
                     pe_store_last(*pre, mc, isize, infos, 0, opt.rg_id, out);
                     os.put(pre->index, std::move(out));
                     local.add(pre->stats);
@@ -897,7 +897,7 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
                 const Read read(recs[i].seq, rcs[i - b]);
                 pos = store_results_se(res[i - b], read, mc, infos, pos);
             }
-            std::string out = os.take();
+            SamText out = os.take();
             out.reserve(7 * (size_t)mc.mparams.r * (e - b));
             Sam sam(out, mc.refs, mc.mparams.cigar_eqx, opt.rg_id, mc.mparams.output_unmapped, mc.mparams.details);
             for (size_t i = b; i < e; ++i) {

@@ -382,9 +382,22 @@ size_t store_results_se(AlignTmpRes& res, const Read& read, const MapContext& mc
 std::string sam_header(const References& refs, const std::string& rg_id, const std::vector<std::string>& rg,
                        const std::string& cmd_line);
 
+// SAM text of a chunk.  A vector whose allocator leaves new elements
+// uninitialised: a record is written into room reserved with resize() (an upper
+// bound of its length) and the unused tail is cut off again, without the
+// zero fill a std::string::resize would spend on every record.
+template <class T> struct NoInitAlloc : std::allocator<T> {
+    template <class U> struct rebind { using other = NoInitAlloc<U>; };
+    NoInitAlloc() = default;
+    template <class U> NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+    template <class U> void construct(U* p) noexcept { ::new ((void*)p) U; }
+    template <class U, class... A> void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+};
+using SamText = std::vector<char, NoInitAlloc<char>>;
+
 class Sam {                                     // src/sam.hpp:69-120
 public:
-    Sam(std::string& out, const References& refs, bool eqx, const std::string& rg_id, bool output_unmapped,
+    Sam(SamText& out, const References& refs, bool eqx, const std::string& rg_id, bool output_unmapped,
         bool details);
     void add(const Alignment& a, const Record& r, std::string_view rc, uint8_t mapq, bool primary,
              const Details& d);
@@ -393,14 +406,14 @@ public:
                   bool primary, const Details d[2]);
     void add_unmapped(const Record& r, uint16_t flags = 4);
     void add_unmapped_pair(const Record& r1, const Record& r2);
-    void add_unmapped_mate(const Record& r, uint16_t flags, const std::string& mate_ref, uint32_t mate_pos);
+    void add_unmapped_mate(const Record& r, uint16_t flags, std::string_view mate_ref, uint32_t mate_pos);
 
 private:
-    void add_record(const std::string& qname, uint16_t flags, const std::string& rname, uint32_t pos, uint8_t mapq,
-                    const Cigar& cigar, const std::string& mate_rname, uint32_t mate_pos, int32_t tlen,
+    void add_record(const std::string& qname, uint16_t flags, std::string_view rname, uint32_t pos, uint8_t mapq,
+                    const Cigar& cigar, std::string_view mate_rname, uint32_t mate_pos, int32_t tlen,
                     std::string_view seq, std::string_view seq_rc, const std::string& qual, int ed, int score,
                     const Details& d);
-    std::string& out_;
+    SamText& out_;
     const References& refs_;
     bool eqx_, output_unmapped_, details_;
     std::string tail_;
@@ -488,10 +501,10 @@ struct SamDigest {
         h ^= h >> 33; h *= 0xff51afd7ed558ccdULL; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ULL; h ^= h >> 33;
         return h;
     }
-    static SamDigest of(const std::string& s) {
+    static SamDigest of(const std::string& s) { return of(s.data(), s.size()); }
+    static SamDigest of(const char* p, size_t n) {
         SamDigest d;
-        const char* p = s.data();
-        const char* e = p + s.size();
+        const char* e = p + n;
         while (p < e) {
             const char* nl = (const char*)std::memchr(p, '\n', (size_t)(e - p));
             if (!nl) break;                      // an unterminated tail is not a line
@@ -524,7 +537,7 @@ struct PipelineResult {
 // perform_task_async_{pe,se} (src/pc.cpp:814-1096, 1522-1887) with -t 1 semantics:
 // chunks are processed strictly in the single-worker timeline until the insert
 // size estimate freezes, then chunk-parallel over `threads` host workers.
-using SamSink = void (*)(void* user, const std::string& chunk);
+using SamSink = void (*)(void* user, const char* chunk, size_t bytes);
 PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<Record>& r2, Engine& eng,
                                const MapContext& mc, const PipelineOptions& opt, SamSink sink, void* user);
 PipelineResult run_pipeline_se(const std::vector<Record>& r, Engine& eng, const MapContext& mc,
