@@ -117,14 +117,26 @@ static bool by_score(const T& a, const T& b) { return a.score > b.score; }
 static void sort_nams_by_score(std::vector<Nam>& v) {
     const size_t n = v.size();
     if (n > 16) { std::sort(v.begin(), v.end(), by_score<Nam>); return; }
-    Nam* a = v.data();
+    if (n < 2) return;
+    // the insertion sort runs on (score, index) keys; the NAMs move once, at the end
+    float sc[16];
+    uint8_t ix[16];
+    bool moved = false;
+    for (size_t i = 0; i < n; ++i) { sc[i] = v[i].score; ix[i] = (uint8_t)i; }
     for (size_t i = 1; i < n; ++i) {
-        if (!(a[i].score > a[i - 1].score)) continue;
-        const Nam x = a[i];
+        if (!(sc[i] > sc[i - 1])) continue;
+        const float xs = sc[i];
+        const uint8_t xi = ix[i];
         size_t j = i;
-        do { a[j] = a[j - 1]; --j; } while (j > 0 && x.score > a[j - 1].score);
-        a[j] = x;
+        do { sc[j] = sc[j - 1]; ix[j] = ix[j - 1]; --j; } while (j > 0 && xs > sc[j - 1]);
+        sc[j] = xs;
+        ix[j] = xi;
+        moved = true;
     }
+    if (!moved) return;
+    Nam tmp[16];
+    for (size_t i = 0; i < n; ++i) tmp[i] = v[ix[i]];
+    std::copy(tmp, tmp + n, v.begin());
 }
 
 // ------------------------------------------------------------- NAM ops ---

@@ -142,7 +142,7 @@ struct PeChunk {
     // itself when upper-casing would not change it, else an upper-cased copy
     std::vector<const Record*> r1, r2;
     std::deque<Record> owned;
-    std::string rcbuf;                        // reverse complements of both mates, computed once:
+    SamText rcbuf;                            // reverse complements of both mates, computed once (resize: no fill):
     std::vector<uint64_t> rcoff;              // read i mate m at rcoff[2i+m] (length = read length)
     std::string_view rc(size_t i, int m) const {
         const Record& r = m ? *r2[i] : *r1[i];
