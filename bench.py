@@ -23,6 +23,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import resource
 import sys
 import time
 
@@ -283,6 +284,7 @@ def main():
 
     barrier()
     torch.cuda.synchronize()
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.perf_counter()
     n_reads = 0
     totals = {f: 0 for f in shard.STAT_FIELDS}
@@ -300,6 +302,10 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    # host CPU time of this rank's timed steps (all threads, user + system): the
+    # host-bound part of the path, steadier than wall-time throughput on a shared box
+    host_cpu_s = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
     ks = m.kernel_stats()
 
     # the run's only collective: max wall time and summed statistics over ranks (RCCL)
@@ -390,6 +396,10 @@ def main():
             "parity": parity,
             "kernels": kernel_table(ks),
             "device_counters": {k: v for k, v in ks.items() if k != "kernels"},
+            "host_cpu": {"cpu_s_per_step": round(host_cpu_s / args.steps, 4),
+                         "core_us_per_read": round(1e6 * host_cpu_s / max(1, n_reads), 4),
+                         "sys_fraction": round((ru1.ru_stime - ru0.ru_stime) / max(1e-9, host_cpu_s), 4),
+                         "note": "rank 0 process CPU time (getrusage) over the timed steps"},
             "mapping_stats_all_ranks": totals_all,
             "sam_hashes": [f"{h:016x}" for h in hashes],
         }

@@ -160,6 +160,7 @@ extern "C" {
 
 rsam* rsam_open_files(const char* ref_fa, const char* sti, int read_len, int device, int threads, char* err,
                       size_t err_len) {
+    tune_malloc();
     rsam* m = new rsam();
     try {
         m->read_len = read_len;
@@ -184,6 +185,7 @@ rsam* rsam_open_files(const char* ref_fa, const char* sti, int read_len, int dev
 
 rsam* rsam_open_synthetic(uint64_t seed, uint64_t ref_len, int n_contigs, int read_len, int device, int threads,
                           char* err, size_t err_len) {
+    tune_malloc();
     rsam* m = new rsam();
     try {
         m->read_len = read_len;
@@ -204,6 +206,7 @@ rsam* rsam_open_synthetic(uint64_t seed, uint64_t ref_len, int n_contigs, int re
 }
 
 rsam* rsam_open_like(const rsam* o, int device, int threads, char* err, size_t err_len) {
+    tune_malloc();
     (void)threads;
     rsam* m = new rsam();
     m->read_len = o->read_len;
@@ -243,6 +246,7 @@ int rsam_get_info(const rsam* m, rsam_info* out) {
 }
 
 rsam_reads* rsam_reads_load(const char* fq1, const char* fq2) {
+    tune_malloc();
     try {
         std::unique_ptr<rsam_reads> r(new rsam_reads());
         if (fq2 && *fq2) {
@@ -260,6 +264,7 @@ rsam_reads* rsam_reads_load(const char* fq1, const char* fq2) {
 }
 
 rsam_reads* rsam_reads_load_interleaved(const char* fq) {
+    tune_malloc();
     try {
         std::unique_ptr<rsam_reads> r(new rsam_reads());
         r->interleaved = FastxReader::read_all(fq);
@@ -273,6 +278,7 @@ rsam_reads* rsam_reads_load_interleaved(const char* fq) {
 
 rsam_reads* rsam_reads_synthetic(const rsam* m, uint64_t seed, uint64_t first, uint64_t n, int read_len, double mu,
                                  double sigma, int paired) {
+    tune_malloc();
     auto* r = new rsam_reads();
     r->paired = paired != 0;
     r->r1.resize(n);
@@ -330,6 +336,7 @@ static void sink_fn(void* user, const char* chunk, size_t bytes) {
 }
 
 int rsam_map(rsam* m, const rsam_reads* reads, int threads, int chunk_size, const char* sam_path, rsam_stats* out) {
+    tune_malloc();
     if (!m || !reads) return -1;
     PcSampler sampler;
     try {

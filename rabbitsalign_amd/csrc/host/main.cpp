@@ -109,6 +109,7 @@ void write_sink(void* user, const char* chunk, size_t bytes) {
 }  // namespace
 
 int cli_main(int argc, char** argv, EngineFactory factory, const char* prog) {
+    tune_malloc();
     try {
         bool index_cmd = argc > 1 && std::string(argv[1]) == "index";
         bool ok = true;

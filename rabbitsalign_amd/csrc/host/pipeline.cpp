@@ -26,6 +26,8 @@
 #include <stdexcept>
 #include <thread>
 
+#include <malloc.h>
+
 #include "rsa_host.hpp"
 
 namespace rsa {
@@ -507,6 +509,15 @@ void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistributio
 }
 
 }  // namespace
+
+void tune_malloc() {
+    static std::once_flag once;
+    std::call_once(once, [] {
+        mallopt(M_TRIM_THRESHOLD, 1 << 30);
+        mallopt(M_TOP_PAD, 64 << 20);
+        mallopt(M_MMAP_THRESHOLD, 256 << 20);
+    });
+}
 
 bool same_name(const std::string& n1, const std::string& n2) {      // pc.cpp:23-35
     if (n1.length() != n2.length()) return false;

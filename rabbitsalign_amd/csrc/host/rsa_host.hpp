@@ -469,6 +469,14 @@ size_t distribute_interleaved(std::vector<Record>&& recs, size_t chunk_size, std
                               std::vector<Record>& r2, std::vector<size_t>& chunk_starts);
 bool same_name(const std::string& n1, const std::string& n2);
 
+// glibc malloc settings for the mapping process (once; library entry points and
+// the CLI call it): free memory stays in the heap instead of being trimmed and
+// re-faulted, and buffers up to 256 MB come from the heap instead of a fresh
+// mmap each time.  The per-chunk work allocates and frees steadily; with glibc's
+// defaults that cost 0.93-1.00 core-us a read on the box, with these 0.77-0.87
+// (A/B, profiles/r02/ab_malloc.jsonl).  Only memory retention changes.
+void tune_malloc();
+
 // Order-sensitive digest of a SAM body, independent of how it is chunked:
 // D = sum_k line_hash(line_k) * P^(N-1-k) mod 2^64 over the N lines (without '\n').
 // line_hash runs four independent 64-bit multiply-rotate lanes over 32-byte
