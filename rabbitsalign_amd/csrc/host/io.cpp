@@ -143,6 +143,7 @@ void Sam::add_unmapped(const Record& r, uint16_t flags) {   // sam.cpp:77-92
     *p++ = '\t';
     p = put_str(p, r.qual.empty() ? std::string_view("*") : std::string_view(r.qual));
     p = put_str(p, tail_);
+    line_done(p0, p);
     sam_trim(out_, at, p0, p);
 }
 
@@ -165,6 +166,7 @@ void Sam::add_unmapped_mate(const Record& r, uint16_t flags, std::string_view ma
     *p++ = '\t';
     p = put_str(p, r.qual.empty() ? std::string_view("*") : std::string_view(r.qual));
     p = put_str(p, tail_);
+    line_done(p0, p);
     sam_trim(out_, at, p0, p);
 }
 
@@ -251,6 +253,7 @@ void Sam::add_record(const std::string& qname, uint16_t flags, std::string_view 
     }
     if (details_) p = put_details(p, d, flags & 1);
     p = put_str(p, tail_);
+    line_done(p0, p);
     sam_trim(out_, at, p0, p);
 }
 

@@ -122,9 +122,10 @@ struct OrderedSink {
         s.clear();
         sp.v.push_back(std::move(s));
     }
-    void put(size_t idx, SamText&& s) {
+    // `made`: the chunk's digest, folded in while its text was written (Sam::digest_into)
+    void put(size_t idx, SamText&& s, const SamDigest* made = nullptr) {
         SamDigest d;
-        if (digest) d = SamDigest::of(s.data(), s.size());   // in the calling worker
+        if (digest) d = made ? *made : SamDigest::of(s.data(), s.size());   // in the calling worker
         std::lock_guard<std::mutex> g(m);
         pending.emplace(idx, std::make_pair(std::move(s), d));
         for (auto it = pending.find(next); it != pending.end(); it = pending.find(next)) {
@@ -483,7 +484,8 @@ void pe_get_str(PeChunk& c, const MapContext& mc, float mu, float sigma, std::ve
 
 // the chunk's extension results start at infos[pos]
 void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistribution& isize,
-                   std::vector<AlignmentInfo>& infos, size_t pos, const std::string& rg_id, SamText& out) {
+                   std::vector<AlignmentInfo>& infos, size_t pos, const std::string& rg_id, SamText& out,
+                   SamDigest* digest) {
     const auto t = Clock::now();
     const size_t n = c.r1.size();
     static const bool pf = !(getenv("RSA_PREFETCH") && atoi(getenv("RSA_PREFETCH")) == 0);
@@ -496,6 +498,7 @@ void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistributio
     out.clear();
     out.reserve(7 * (size_t)mc.mparams.r * c.r1.size());
     Sam sam(out, mc.refs, mc.mparams.cigar_eqx, rg_id, mc.mparams.output_unmapped, mc.mparams.details);
+    sam.digest_into(digest);
     for (size_t i = 0; i < n; ++i) {
         if (pf && i + ahead < n) {
             prefetch_record(*c.r1[i + ahead]);
@@ -681,9 +684,10 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
             PeChunk& c = *cs[g];
             c.times.extend += dt;
             SamText out = os.take();
-            pe_store_last(c, mc, est, infos, first[g], opt.rg_id, out);
+            SamDigest dg;
+            pe_store_last(c, mc, est, infos, first[g], opt.rg_id, out, os.digest ? &dg : nullptr);
             const auto tp = Clock::now();
-            os.put(c.index, std::move(out));
+            os.put(c.index, std::move(out), os.digest ? &dg : nullptr);
             c.times.output += since(tp);
         }
     };
@@ -737,8 +741,9 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                     pre->times.extend += since(te);
                     pre->stats.tot_aligner_calls += jobs.size();
                     SamText out = os.take();
-                    pe_store_last(*pre, mc, isize, infos, 0, opt.rg_id, out);
-                    os.put(pre->index, std::move(out));
+                    SamDigest dg;
+                    pe_store_last(*pre, mc, isize, infos, 0, opt.rg_id, out, os.digest ? &dg : nullptr);
+                    os.put(pre->index, std::move(out), os.digest ? &dg : nullptr);
                     local.add(pre->stats);
                     lt.add(pre->times);
                     if (!cur) { recycle(std::move(pre)); break; }
@@ -911,12 +916,14 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
             SamText out = os.take();
             out.reserve(7 * (size_t)mc.mparams.r * (e - b));
             Sam sam(out, mc.refs, mc.mparams.cigar_eqx, opt.rg_id, mc.mparams.output_unmapped, mc.mparams.details);
+            SamDigest dg;
+            if (os.digest) sam.digest_into(&dg);
             for (size_t i = b; i < e; ++i) {
                 if (i + rec_ahead() < e) prefetch_record(recs[i + rec_ahead()]);
                 const Read read(recs[i].seq, rcs[i - b]);
                 align_SE_read_last(res[i - b], recs[i], read, sam, st, mc, rng);
             }
-            os.put(idx, std::move(out));
+            os.put(idx, std::move(out), os.digest ? &dg : nullptr);
             local.add(st);
         }
         } catch (...) {

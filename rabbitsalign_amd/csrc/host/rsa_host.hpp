@@ -378,6 +378,54 @@ void collect_jobs_se(AlignTmpRes& res, const Read& read, const MapContext& mc, s
 size_t store_results_se(AlignTmpRes& res, const Read& read, const MapContext& mc,
                         std::vector<AlignmentInfo>& infos, size_t pos);
 
+// Order-sensitive digest of a SAM body, independent of how it is chunked:
+// D = sum_k line_hash(line_k) * P^(N-1-k) mod 2^64 over the N lines (without '\n').
+// line_hash runs four independent 64-bit multiply-rotate lanes over 32-byte
+// blocks (about 0.3 cycles/byte) so digesting stays off the critical path.
+struct SamDigest {
+    static constexpr uint64_t P = 0x100000001b3ULL;
+    uint64_t h = 0, lines = 0;
+    static uint64_t pow(uint64_t b, uint64_t e) {
+        uint64_t r = 1;
+        for (; e; e >>= 1, b *= b) if (e & 1) r *= b;
+        return r;
+    }
+    static inline uint64_t rd64(const char* p) { uint64_t w; std::memcpy(&w, p, 8); return w; }
+    static inline uint64_t mix(uint64_t a, uint64_t w) {
+        a ^= w * 0xC2B2AE3D27D4EB4FULL;
+        return ((a << 31) | (a >> 33)) * 0x9E3779B185EBCA87ULL;
+    }
+    static uint64_t line_hash(const char* p, size_t n) {
+        uint64_t a = 0x9E3779B97F4A7C15ULL ^ n, b = 0x165667B19E3779F9ULL, c = 0x85EBCA77C2B2AE63ULL,
+                 d = 0x27D4EB2F165667C5ULL;
+        size_t i = 0;
+        for (; i + 32 <= n; i += 32) {
+            a = mix(a, rd64(p + i)); b = mix(b, rd64(p + i + 8));
+            c = mix(c, rd64(p + i + 16)); d = mix(d, rd64(p + i + 24));
+        }
+        for (; i + 8 <= n; i += 8) a = mix(a, rd64(p + i));
+        uint64_t t = 0;
+        std::memcpy(&t, p + i, n - i);
+        uint64_t h = mix(a, t) ^ ((b << 17) | (b >> 47)) ^ ((c << 29) | (c >> 35)) ^ ((d << 43) | (d >> 21));
+        h ^= h >> 33; h *= 0xff51afd7ed558ccdULL; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ULL; h ^= h >> 33;
+        return h;
+    }
+    static SamDigest of(const std::string& s) { return of(s.data(), s.size()); }
+    static SamDigest of(const char* p, size_t n) {
+        SamDigest d;
+        const char* e = p + n;
+        while (p < e) {
+            const char* nl = (const char*)std::memchr(p, '\n', (size_t)(e - p));
+            if (!nl) break;                      // an unterminated tail is not a line
+            d.h = d.h * P + line_hash(p, (size_t)(nl - p));
+            d.lines++;
+            p = nl + 1;
+        }
+        return d;
+    }
+    void append(const SamDigest& o) { h = h * pow(P, o.lines) + o.h; lines += o.lines; }
+};
+
 // --------------------------------------------------------------- SAM -----
 std::string sam_header(const References& refs, const std::string& rg_id, const std::vector<std::string>& rg,
                        const std::string& cmd_line);
@@ -407,8 +455,17 @@ public:
     void add_unmapped(const Record& r, uint16_t flags = 4);
     void add_unmapped_pair(const Record& r1, const Record& r2);
     void add_unmapped_mate(const Record& r, uint16_t flags, std::string_view mate_ref, uint32_t mate_pos);
+    // fold every line into *d as it is written (while it is in cache) instead of a
+    // second pass over the chunk's text; same value as SamDigest::of on the text
+    void digest_into(SamDigest* d) { digest_ = d; }
 
 private:
+    void line_done(const char* p0, const char* p) {
+        if (digest_) {
+            digest_->h = digest_->h * SamDigest::P + SamDigest::line_hash(p0, (size_t)(p - p0) - 1);
+            digest_->lines++;
+        }
+    }
     void add_record(const std::string& qname, uint16_t flags, std::string_view rname, uint32_t pos, uint8_t mapq,
                     const Cigar& cigar, std::string_view mate_rname, uint32_t mate_pos, int32_t tlen,
                     std::string_view seq, std::string_view seq_rc, const std::string& qual, int ed, int score,
@@ -417,6 +474,7 @@ private:
     const References& refs_;
     bool eqx_, output_unmapped_, details_;
     std::string tail_;
+    SamDigest* digest_ = nullptr;
 };
 
 bool is_proper_pair(const Alignment& a1, const Alignment& a2, float mu, float sigma);
@@ -476,54 +534,6 @@ bool same_name(const std::string& n1, const std::string& n2);
 // defaults that cost 0.93-1.00 core-us a read on the box, with these 0.77-0.87
 // (A/B, profiles/r02/ab_malloc.jsonl).  Only memory retention changes.
 void tune_malloc();
-
-// Order-sensitive digest of a SAM body, independent of how it is chunked:
-// D = sum_k line_hash(line_k) * P^(N-1-k) mod 2^64 over the N lines (without '\n').
-// line_hash runs four independent 64-bit multiply-rotate lanes over 32-byte
-// blocks (about 0.3 cycles/byte) so digesting stays off the critical path.
-struct SamDigest {
-    static constexpr uint64_t P = 0x100000001b3ULL;
-    uint64_t h = 0, lines = 0;
-    static uint64_t pow(uint64_t b, uint64_t e) {
-        uint64_t r = 1;
-        for (; e; e >>= 1, b *= b) if (e & 1) r *= b;
-        return r;
-    }
-    static inline uint64_t rd64(const char* p) { uint64_t w; std::memcpy(&w, p, 8); return w; }
-    static inline uint64_t mix(uint64_t a, uint64_t w) {
-        a ^= w * 0xC2B2AE3D27D4EB4FULL;
-        return ((a << 31) | (a >> 33)) * 0x9E3779B185EBCA87ULL;
-    }
-    static uint64_t line_hash(const char* p, size_t n) {
-        uint64_t a = 0x9E3779B97F4A7C15ULL ^ n, b = 0x165667B19E3779F9ULL, c = 0x85EBCA77C2B2AE63ULL,
-                 d = 0x27D4EB2F165667C5ULL;
-        size_t i = 0;
-        for (; i + 32 <= n; i += 32) {
-            a = mix(a, rd64(p + i)); b = mix(b, rd64(p + i + 8));
-            c = mix(c, rd64(p + i + 16)); d = mix(d, rd64(p + i + 24));
-        }
-        for (; i + 8 <= n; i += 8) a = mix(a, rd64(p + i));
-        uint64_t t = 0;
-        std::memcpy(&t, p + i, n - i);
-        uint64_t h = mix(a, t) ^ ((b << 17) | (b >> 47)) ^ ((c << 29) | (c >> 35)) ^ ((d << 43) | (d >> 21));
-        h ^= h >> 33; h *= 0xff51afd7ed558ccdULL; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ULL; h ^= h >> 33;
-        return h;
-    }
-    static SamDigest of(const std::string& s) { return of(s.data(), s.size()); }
-    static SamDigest of(const char* p, size_t n) {
-        SamDigest d;
-        const char* e = p + n;
-        while (p < e) {
-            const char* nl = (const char*)std::memchr(p, '\n', (size_t)(e - p));
-            if (!nl) break;                      // an unterminated tail is not a line
-            d.h = d.h * P + line_hash(p, (size_t)(nl - p));
-            d.lines++;
-            p = nl + 1;
-        }
-        return d;
-    }
-    void append(const SamDigest& o) { h = h * pow(P, o.lines) + o.h; lines += o.lines; }
-};
 
 // thread-summed seconds per phase (instrumentation of the host pipeline)
 struct PhaseTimes {
