@@ -103,7 +103,6 @@ int main(int argc, char** argv) {
             return 2;
         }
     }
-    sam.reset();                                    // staged records reach `out`
     FILE* o = fopen(argv[3], "w");
     if (!o) return 2;
     fwrite(out.data(), 1, out.size(), o);

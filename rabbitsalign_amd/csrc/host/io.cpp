@@ -17,8 +17,6 @@
 #include <stdexcept>
 #include <thread>
 
-#include <emmintrin.h>
-
 #include "rsa_host.hpp"
 
 namespace rsa {
@@ -110,53 +108,17 @@ static std::string_view strip_suffix(const std::string& name) {   // sam.cpp:29-
 
 Sam::Sam(SamText& out, const References& refs, bool eqx, const std::string& rg_id, bool output_unmapped,
          bool details)
-    : out_(out), refs_(refs), eqx_(eqx), output_unmapped_(output_unmapped), details_(details), stage_(kStage) {
+    : out_(out), refs_(refs), eqx_(eqx), output_unmapped_(output_unmapped), details_(details) {
     tail_ = rg_id.empty() ? "\n" : "\tRG:Z:" + rg_id + "\n";
 }
 
-// Records are formatted into a small staging buffer (cache resident) and moved to
-// the chunk's text in blocks with non-temporal stores: the text is written once
-// and read (if at all) much later by the sink, so its lines need not be fetched
-// into the cache before they are overwritten.
-static void stream_append(SamText& o, const char* src, size_t n) {
-    if (!n) return;
-    const size_t at = o.size();
-    o.resize(at + n);
-    char* dst = o.data() + at;
-    const size_t head = std::min(n, (size_t)((64 - ((uintptr_t)dst & 63)) & 63));
-    memcpy(dst, src, head);
-    dst += head; src += head; n -= head;
-    for (; n >= 64; n -= 64, dst += 64, src += 64) {
-        const __m128i a = _mm_loadu_si128((const __m128i*)src), b = _mm_loadu_si128((const __m128i*)(src + 16)),
-                      c = _mm_loadu_si128((const __m128i*)(src + 32)), d = _mm_loadu_si128((const __m128i*)(src + 48));
-        _mm_stream_si128((__m128i*)dst, a);
-        _mm_stream_si128((__m128i*)(dst + 16), b);
-        _mm_stream_si128((__m128i*)(dst + 32), c);
-        _mm_stream_si128((__m128i*)(dst + 48), d);
-    }
-    memcpy(dst, src, n);
+// room for `bound` more bytes at the end of o (uninitialised); returns where they start
+static inline char* sam_room(SamText& o, size_t bound, size_t& at) {
+    at = o.size();
+    o.resize(at + bound);
+    return o.data() + at;
 }
-
-void Sam::flush() {
-    stream_append(out_, stage_.data(), staged_);
-    staged_ = 0;
-    _mm_sfence();                                   // the streamed text is visible before the chunk is handed on
-}
-
-Sam::~Sam() { flush(); }
-
-// room for `bound` bytes of one record in the staging buffer
-char* Sam::room(size_t bound) {
-    if (staged_ + bound > stage_.size()) {
-        flush();
-        if (bound > stage_.size()) stage_.resize(bound);
-    }
-    return stage_.data() + staged_;
-}
-void Sam::commit(const char* p0, const char* p) {
-    line_done(p0, p);
-    staged_ += (size_t)(p - p0);
-}
+static inline void sam_trim(SamText& o, size_t at, const char* p0, const char* p) { o.resize(at + (size_t)(p - p0)); }
 
 static char* put_details(char* p, const Details& d, bool paired) {   // sam.cpp:46-60
     p = put_str(p, "\tna:i:"); p = put_uint(p, d.nams);
@@ -171,7 +133,8 @@ static const size_t kDetailsBound = 5 * (6 + 20);
 void Sam::add_unmapped(const Record& r, uint16_t flags) {   // sam.cpp:77-92
     if (!output_unmapped_) return;
     const std::string_view name = strip_suffix(r.name);
-    char* const p0 = room(name.size() + r.seq.size() + r.qual.size() + tail_.size() + 48);
+    size_t at;
+    char* const p0 = sam_room(out_, name.size() + r.seq.size() + r.qual.size() + tail_.size() + 48, at);
     char* p = put_str(p0, name);
     *p++ = '\t';
     p = put_uint(p, flags);
@@ -180,12 +143,15 @@ void Sam::add_unmapped(const Record& r, uint16_t flags) {   // sam.cpp:77-92
     *p++ = '\t';
     p = put_str(p, r.qual.empty() ? std::string_view("*") : std::string_view(r.qual));
     p = put_str(p, tail_);
-    commit(p0, p);
+    line_done(p0, p);
+    sam_trim(out_, at, p0, p);
 }
 
 void Sam::add_unmapped_mate(const Record& r, uint16_t flags, std::string_view mate_ref, uint32_t mate_pos) {
     const std::string_view name = strip_suffix(r.name);      // sam.cpp:94-116
-    char* const p0 = room(name.size() + mate_ref.size() + r.seq.size() + r.qual.size() + tail_.size() + 64);
+    size_t at;
+    char* const p0 =
+        sam_room(out_, name.size() + mate_ref.size() + r.seq.size() + r.qual.size() + tail_.size() + 64, at);
     char* p = put_str(p0, name);
     *p++ = '\t';
     p = put_uint(p, flags);
@@ -200,7 +166,8 @@ void Sam::add_unmapped_mate(const Record& r, uint16_t flags, std::string_view ma
     *p++ = '\t';
     p = put_str(p, r.qual.empty() ? std::string_view("*") : std::string_view(r.qual));
     p = put_str(p, tail_);
-    commit(p0, p);
+    line_done(p0, p);
+    sam_trim(out_, at, p0, p);
 }
 
 void Sam::add_unmapped_pair(const Record& r1, const Record& r2) {
@@ -245,7 +212,8 @@ void Sam::add_record(const std::string& qname, uint16_t flags, std::string_view 
     // upper bound of the record: fixed fields + numbers + CIGAR (<= 11 chars an op) + SEQ/QUAL + tags
     const size_t bound = name.size() + rname.size() + mate_rname.size() + std::max(seq.size(), seq_rc.size()) +
                          qual.size() + 11 * cigar.ops.size() + tail_.size() + 160 + (details_ ? kDetailsBound : 0);
-    char* const p0 = room(bound);
+    size_t at;
+    char* const p0 = sam_room(out_, bound, at);
     char* p = p0;
     p = put_str(p, name);
     *p++ = '\t';
@@ -285,7 +253,8 @@ void Sam::add_record(const std::string& qname, uint16_t flags, std::string_view 
     }
     if (details_) p = put_details(p, d, flags & 1);
     p = put_str(p, tail_);
-    commit(p0, p);
+    line_done(p0, p);
+    sam_trim(out_, at, p0, p);
 }
 
 void Sam::add_pair(const Alignment& a1, const Alignment& a2, const Record& r1, const Record& r2, std::string_view rc1,

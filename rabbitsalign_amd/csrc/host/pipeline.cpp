@@ -923,7 +923,6 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
                 const Read read(recs[i].seq, rcs[i - b]);
                 align_SE_read_last(res[i - b], recs[i], read, sam, st, mc, rng);
             }
-            sam.flush();
             os.put(idx, std::move(out), os.digest ? &dg : nullptr);
             local.add(st);
         }

@@ -458,17 +458,8 @@ public:
     // fold every line into *d as it is written (while it is in cache) instead of a
     // second pass over the chunk's text; same value as SamDigest::of on the text
     void digest_into(SamDigest* d) { digest_ = d; }
-    // move the staged records to the text (the destructor does it too): call before
-    // the text is read or handed on while this object lives
-    void flush();
-    ~Sam();
-    Sam(const Sam&) = delete;
-    Sam& operator=(const Sam&) = delete;
 
 private:
-    static constexpr size_t kStage = 32 << 10;
-    char* room(size_t bound);
-    void commit(const char* p0, const char* p);
     void line_done(const char* p0, const char* p) {
         if (digest_) {
             digest_->h = digest_->h * SamDigest::P + SamDigest::line_hash(p0, (size_t)(p - p0) - 1);
@@ -484,8 +475,6 @@ private:
     bool eqx_, output_unmapped_, details_;
     std::string tail_;
     SamDigest* digest_ = nullptr;
-    std::vector<char> stage_;                   // formatted records not yet in out_
-    size_t staged_ = 0;
 };
 
 bool is_proper_pair(const Alignment& a1, const Alignment& a2, float mu, float sigma);
