@@ -137,7 +137,23 @@ def kernel_roofline(name: str, k: dict, ks: dict) -> dict:
         achieved = per_launch_bytes / avg_s / 1e9
         out.update({"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 6)})
+        if name in KERNEL_LIMITER:
+            out["limiter"] = KERNEL_LIMITER[name]
     return out
+
+
+# what actually limits the kernels reported against HBM: their HBM
+# fraction is shown for the bytes they must move, not as their ceiling
+KERNEL_LIMITER = {
+    "ext_band": "dependent-issue latency: one 16-lane group walks a job's band row by row (F prefix scan "
+                "over DPP row_shr), 4 jobs a wave, < 2 waves per SIMD at chunk size",
+    "ext_band_wide": "latency of the few (~3 a call) 64-lane jobs, one wave each",
+    "find_nams": "LDS latency and divergence of the robin_hood map emulation, one wave per read",
+    "sites": "latency of random reference windows (one read per NAM)",
+    "lookup": "random HBM lines: two per query randstrobe (bucket bounds + entries)",
+    "randstrobes": "xxh64 and the syncmer window in LDS, one wave per read",
+    "rescue": "latency, rescued reads only",
+}
 
 
 def roofline(ks: dict, elapsed: float) -> dict:
