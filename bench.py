@@ -69,17 +69,36 @@ def _cgroup_cpus():
         return None
 
 
-def host_cores() -> int:
+def pin_rank_cpus(local_rank: int, local_world: int):
+    """N>1: give each rank of the node its own physical cores on the NUMA node its
+    GPU number maps to (rabbitsalign_amd.shard.rank_cpu_groups); returns the CPU
+    list, or None when nothing was pinned.  Threads started afterwards (the host
+    pipeline's workers) inherit it."""
+    if local_world <= 1 or os.environ.get("RSA_BENCH_NO_PIN"):
+        return None
+    from rabbitsalign_amd import shard
+    allowed = sorted(os.sched_getaffinity(0))
+    node_cpus, siblings = shard.host_topology(allowed)
+    cpus = shard.rank_cpu_groups(node_cpus, siblings, local_world)[local_rank]
+    if not cpus:
+        return None
+    os.sched_setaffinity(0, cpus)
+    return cpus
+
+
+def host_cores(pinned: bool = False) -> int:
     """Host threads for this rank: the CPUs this process may use (affinity, cgroup
     quota) shared among the ranks of the node, capped by OMP_NUM_THREADS / MAX_JOBS.
     torch.distributed.run exports OMP_NUM_THREADS=1 to every rank when the variable
-    is unset; that default says nothing about the host pipeline and is ignored."""
+    is unset; that default says nothing about the host pipeline and is ignored.
+    `pinned`: the affinity is already this rank's share (pin_rank_cpus)."""
     local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
     n = len(os.sched_getaffinity(0))
-    q = _cgroup_cpus()
-    if q:
-        n = min(n, q)
-    n = max(1, n // local)
+    q = _cgroup_cpus()                       # the quota covers every rank of the node
+    if pinned:
+        n = min(n, max(1, q // local)) if q else n
+    else:
+        n = max(1, (min(n, q) if q else n) // local)
     for var in ("OMP_NUM_THREADS", "MAX_JOBS"):
         v = os.environ.get(var)
         if v and v.isdigit() and int(v) > 0:
@@ -251,7 +270,9 @@ def main():
     wl = dict(WORKLOADS[args.workload])
     if args.ref_len:
         wl["ref_len"] = args.ref_len
-    cores = host_cores()
+    local_world = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+    pinned = pin_rank_cpus(local_rank, local_world)
+    cores = host_cores(pinned is not None)
     threads = args.threads or min(64, cores)
 
     # torch first: its libamdhip64 (soname libamdhip64.so.7) is then the one
@@ -399,7 +420,8 @@ def main():
             "data": "synthetic (seeded reference + reads, SURVEY.md Appendix D)",
             "config": {"workload": wl["desc"], "reference_bp": wl["ref_len"], "contigs": wl["n_contigs"],
                        "read_len": wl["read_len"], "paired": wl["paired"], "pairs_per_step_per_gpu": P,
-                       "host_threads": threads, "chunk_size": args.chunk_size, "index_bits": info["bits"],
+                       "host_threads": threads, "host_cpus_pinned": len(pinned) if pinned else None,
+                       "chunk_size": args.chunk_size, "index_bits": info["bits"],
                        "randstrobes": info["n_randstrobes"], "parallelism": f"dp{world} (replicated index)"},
             "index_build": {"on": "gpu" if info["index_on_device"] else "host",
                             "seconds": round(info["index_seconds"], 3), "device_ms": info["index_device_ms"],

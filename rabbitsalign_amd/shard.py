@@ -34,3 +34,76 @@ def reduce_run(elapsed_s: float, stats: dict, device="cpu") -> tuple[float, dict
     keys = sorted(stats)
     summed = _reduce([float(stats[k]) for k in keys], dist.ReduceOp.SUM, device)
     return wall, {k: int(round(v)) for k, v in zip(keys, summed)}
+
+
+def rank_cpu_groups(node_cpus, siblings, local_world):
+    """Host CPUs of each of the `local_world` ranks of a node.
+
+    node_cpus: per NUMA node, the CPUs this process may use; siblings: cpu ->
+    tuple of its SMT siblings.  Ranks spread over the nodes in order (rank r on
+    node r * n_nodes // local_world, matching the usual GPU numbering of a
+    two-socket node), and each node's physical cores -- siblings kept together --
+    are split into contiguous runs among its ranks, so no two ranks share a core
+    and each rank's cores share its node's memory and last-level caches."""
+    nodes = [sorted(c) for c in node_cpus if c]
+    if not nodes or local_world < 1:
+        return [[] for _ in range(max(local_world, 0))]
+    n = len(nodes)
+    on_node = [[r for r in range(local_world) if r * n // local_world == k] for k in range(n)]
+    groups = [[] for _ in range(local_world)]
+    for k, cpus in enumerate(nodes):
+        ranks = on_node[k]
+        if not ranks:
+            continue
+        allowed = set(cpus)
+        cores, seen = [], set()
+        for c in cpus:                               # physical cores in CPU order
+            if c in seen:
+                continue
+            core = tuple(sorted(s for s in siblings.get(c, (c,)) if s in allowed)) or (c,)
+            seen.update(core)
+            cores.append(core)
+        for j, r in enumerate(ranks):
+            a = j * len(cores) // len(ranks)
+            b = (j + 1) * len(cores) // len(ranks)
+            groups[r] = sorted(c for core in cores[a:b] for c in core)
+    # a node with more ranks than cores leaves some ranks empty: they share the node's CPUs
+    for k, cpus in enumerate(nodes):
+        for r in on_node[k]:
+            if not groups[r]:
+                groups[r] = sorted(cpus)
+    return groups
+
+
+def _parse_cpulist(s):
+    out = []
+    for part in s.strip().split(","):
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-")
+            out.extend(range(int(a), int(b) + 1))
+        else:
+            out.append(int(part))
+    return out
+
+
+def host_topology(allowed):
+    """(node_cpus, siblings) of this machine from sysfs, restricted to `allowed`."""
+    import glob
+    allowed = set(allowed)
+    node_cpus = []
+    for path in sorted(glob.glob("/sys/devices/system/node/node[0-9]*/cpulist"),
+                       key=lambda p: int(p.split("/node")[-1].split("/")[0])):
+        with open(path) as f:
+            node_cpus.append([c for c in _parse_cpulist(f.read()) if c in allowed])
+    if not any(node_cpus):
+        node_cpus = [sorted(allowed)]
+    siblings = {}
+    for c in allowed:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                siblings[c] = tuple(_parse_cpulist(f.read()))
+        except OSError:
+            siblings[c] = (c,)
+    return node_cpus, siblings
