@@ -133,14 +133,19 @@ __device__ __forceinline__ FwdG fwd_g(const uint16_t* __restrict__ lane_prof, in
                                       int gl) {
     constexpr int RP = ProfDim<R>::RP;
     const int seg_b = (nrow + 15) / 16, seg_w = (nrow + 7) / 8;
-    hh2 E[R], Hc[R];
+    // H of the previous and of the current column in two arrays that trade roles
+    // every step (the loop runs two steps an iteration), so no register copies
+    // rotate the column; both start at zero, and an inactive step (column outside
+    // the window) only ever precedes the first active one or follows the last
+    hh2 E[R], HA[R], HB[R];
     uint32_t ssm[R], B0[R], B1[R];
     const hh2 zero = h2_from(0u);
     const hh2 GO2 = h2_from(h2_pair(gO)), GE2 = h2_from(h2_pair(gE));
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         E[r] = zero;
-        Hc[r] = zero;
+        HA[r] = zero;
+        HB[r] = zero;
         B0[r] = 0;
         B1[r] = 0;
         const int p = gl * R + r;
@@ -161,7 +166,7 @@ __device__ __forceinline__ FwdG fwd_g(const uint16_t* __restrict__ lane_prof, in
     int code1 = code_at(1 - gl);
     // one step; the loop below runs two per iteration with the profile buffers
     // swapped, so no register copies carry P between steps
-    auto step = [&](int s, const uint32_t (&P)[RP / 2], uint32_t (&Pn)[RP / 2]) {
+    auto step = [&](int s, const uint32_t (&P)[RP / 2], uint32_t (&Pn)[RP / 2], const hh2 (&Hin)[R], hh2 (&Hout)[R]) {
         const uint32_t F_in = row_shr1(F_out);
         const uint32_t Fw_in = row_shr1(Fw_out);
         const uint32_t Hl_in = row_shr1(H_last);
@@ -178,8 +183,8 @@ __device__ __forceinline__ FwdG fwd_g(const uint16_t* __restrict__ lane_prof, in
                 const hh2 diag = dg + sc;
                 const hh2 hm = hmax3(diag, E[r], Fw);
                 const hh2 h = hmax(hm, F);
-                dg = Hc[r];
-                Hc[r] = h;
+                dg = Hin[r];
+                Hout[r] = h;
                 const hh2 t = hm - GO2;
                 E[r] = hmax3(E[r] - GE2, t, zero);
                 Fw = hmax3(Fw - GE2, t, zero);
@@ -188,7 +193,7 @@ __device__ __forceinline__ FwdG fwd_g(const uint16_t* __restrict__ lane_prof, in
             }
             F_out = h2_bits(F);
             Fw_out = h2_bits(Fw);
-            H_last = h2_bits(Hc[R - 1]);
+            H_last = h2_bits(Hout[R - 1]);
             const uint32_t cmb = h2_bits(cm);
             // a new best of a layout: remember the column and this column's rows; the
             // row itself is searched once after the pass
@@ -197,13 +202,13 @@ __device__ __forceinline__ FwdG fwd_g(const uint16_t* __restrict__ lane_prof, in
                 o.best[0] = v0;
                 o.col[0] = c;
 #pragma unroll
-                for (int r = 0; r < R; ++r) B0[r] = h2_bits(Hc[r]);
+                for (int r = 0; r < R; ++r) B0[r] = h2_bits(Hout[r]);
             }
             if (v1 > o.best[1]) {
                 o.best[1] = v1;
                 o.col[1] = c;
 #pragma unroll
-                for (int r = 0; r < R; ++r) B1[r] = h2_bits(Hc[r]);
+                for (int r = 0; r < R; ++r) B1[r] = h2_bits(Hout[r]);
             }
         }
         diag_top = Hl_in;
@@ -211,10 +216,10 @@ __device__ __forceinline__ FwdG fwd_g(const uint16_t* __restrict__ lane_prof, in
     };
     int s = 0;
     for (; s + 1 < S; s += 2) {
-        step(s, P, Pn);
-        step(s + 1, Pn, P);
+        step(s, P, Pn, HA, HB);
+        step(s + 1, Pn, P, HB, HA);
     }
-    if (s < S) step(s, P, Pn);
+    if (s < S) step(s, P, Pn, HA, HB);
     // the smallest valid row of the best column reaching the best (per layout)
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
@@ -242,12 +247,13 @@ __device__ __forceinline__ void rev_g(const uint16_t* __restrict__ lane_prof, in
                                       int gl, int& tcol, int& trow) {
     constexpr int RP = ProfDim<R>::RP;
     const int lanes_used = (nrow + R - 1) / R;
-    int E[R], Hc[R], ssm[R];
+    int E[R], HA[R], HB[R], ssm[R];                    // HA / HB: previous / current column, trading roles
     bool valid[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         E[r] = 0;
-        Hc[r] = 0;
+        HA[r] = 0;
+        HB[r] = 0;
         const int p = gl * R + r;
         ssm[r] = (p % seg) == 0 ? 0 : -1;
         valid[r] = p < nrow;
@@ -262,7 +268,8 @@ __device__ __forceinline__ void rev_g(const uint16_t* __restrict__ lane_prof, in
     int code1 = code_at(1 - gl);
     // one step (two per loop iteration, profile buffers swapped); true once every
     // job of the wave is finished
-    auto step = [&](int s, const uint32_t (&P)[RP / 2], uint32_t (&Pn)[RP / 2]) -> bool {
+    auto step = [&](int s, const uint32_t (&P)[RP / 2], uint32_t (&Pn)[RP / 2], const int (&Hin)[R],
+                    int (&Hout)[R]) -> bool {
         const int F_in = (int)row_shr1((uint32_t)F_out);
         const int Fw_in = (int)row_shr1((uint32_t)Fw_out);
         const int Hl_in = (int)row_shr1((uint32_t)H_last);
@@ -279,8 +286,8 @@ __device__ __forceinline__ void rev_g(const uint16_t* __restrict__ lane_prof, in
                 const int diag = dg + sc;
                 const int hm = max3i(diag, E[r], Fw);          // E, Fw >= 0: the 0 of max(diag, 0)
                 const int h = max(hm, F);
-                dg = Hc[r];
-                Hc[r] = h;
+                dg = Hin[r];
+                Hout[r] = h;
                 const int t = hm - gO;
                 E[r] = max3i(E[r] - gE, t, 0);
                 Fw = max3i(Fw - gE, t, 0);
@@ -289,7 +296,7 @@ __device__ __forceinline__ void rev_g(const uint16_t* __restrict__ lane_prof, in
             }
             F_out = F;
             Fw_out = Fw;
-            H_last = Hc[R - 1];
+            H_last = Hout[R - 1];
             const bool hit = cm == terminate && tcol == INT_MAX;
             if (__builtin_amdgcn_ballot_w64(hit)) {        // at most once a job: skip the row search otherwise
                 if (hit) {
@@ -297,7 +304,7 @@ __device__ __forceinline__ void rev_g(const uint16_t* __restrict__ lane_prof, in
                     int row = INT_MAX;
 #pragma unroll
                     for (int r = R - 1; r >= 0; --r)
-                        if (valid[r] && Hc[r] == terminate) row = gl * R + r;
+                        if (valid[r] && Hout[r] == terminate) row = gl * R + r;
                     trow = row;
                 }
             }
@@ -314,10 +321,10 @@ __device__ __forceinline__ void rev_g(const uint16_t* __restrict__ lane_prof, in
     };
     int s = 0;
     for (; s + 1 < S; s += 2) {
-        if (step(s, P, Pn)) return;
-        if (step(s + 1, Pn, P)) return;
+        if (step(s, P, Pn, HA, HB)) return;
+        if (step(s + 1, Pn, P, HB, HA)) return;
     }
-    if (s < S) (void)step(s, P, Pn);
+    if (s < S) (void)step(s, P, Pn, HA, HB);
 }
 
 // this lane's rows of a query profile: the f16 (fwd) or int16 (rev) score of row
