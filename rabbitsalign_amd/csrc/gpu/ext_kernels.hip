@@ -670,18 +670,27 @@ __device__ __forceinline__ int gshr(int v) {
 }
 
 // lane z of the group receives lane z+1 (band index z+2 is held by lane z+1); the last lane receives 0
+// (16 lanes: DPP bound_ctrl writes the 0 itself, so no register is preset with it)
 template <int G>
 __device__ __forceinline__ int gshl1z(int v) {
-    if constexpr (G == 16) return __builtin_amdgcn_update_dpp(0, v, 0x101, 0xf, 0xf, false);
+    if constexpr (G == 16) return __builtin_amdgcn_mov_dpp(v, 0x101, 0xf, 0xf, true);
     else return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, false);
 }
 
 // lane z receives lane z-1; lane 0 receives 0
 template <int G>
 __device__ __forceinline__ int gshr1z(int v) {
-    if constexpr (G == 16) return __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+    if constexpr (G == 16) return __builtin_amdgcn_mov_dpp(v, 0x111, 0xf, 0xf, true);
     else return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false);
 }
+
+// 16 lanes: lane z receives lane z-S, lanes z < S receive 0 (bound_ctrl)
+template <int S>
+__device__ __forceinline__ int rshr0(int v) { return __builtin_amdgcn_mov_dpp(v, 0x110 + S, 0xf, 0xf, true); }
+
+// max-plus prefix scan offset so that the 0 a DPP shift brings in at the group's
+// start is below every real value: X + GSCAN_OFF stays positive for |X| < 2^20
+#define GSCAN_OFF (1 << 24)
 
 template <int G>
 __device__ __forceinline__ int gmax(int v) {
@@ -698,12 +707,14 @@ __device__ __forceinline__ int gmax(int v) {
 template <int G>
 __device__ __forceinline__ int gscan_f(int A, int gE) {
     if constexpr (G == 16) {
-        int X = A;
-        X = max(X, gshr<G, 1>(X) - gE);
-        X = max(X, gshr<G, 2>(X) - 2 * gE);
-        X = max(X, gshr<G, 4>(X) - 4 * gE);
-        X = max(X, gshr<G, 8>(X) - 8 * gE);
-        return X;
+        // values offset by GSCAN_OFF, so the 0 shifted in below lane S loses every max
+        // (A >= -gO - 64 gE here): bound_ctrl shifts, no preset registers
+        int X = A + GSCAN_OFF;
+        X = max(X, rshr0<1>(X) - gE);
+        X = max(X, rshr0<2>(X) - 2 * gE);
+        X = max(X, rshr0<4>(X) - 4 * gE);
+        X = max(X, rshr0<8>(X) - 8 * gE);
+        return X - GSCAN_OFF;
     } else {
         const int z = (int)(threadIdx.x & 63), zr = z & 15;
         int X = A;
@@ -778,13 +789,15 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
             const int jj = beg + z;
             const bool on = jj <= end;
             const int sh = i - bw >= 1 ? 1 : 0;
-            if (z == edge - 1) { HB = 0; EB = 0; }
+            const bool clr = z == edge - 1;
+            HB = clr ? 0 : HB;
+            EB = clr ? 0 : EB;
             const int HBl = gshl1z<G>(HB), EBl = gshl1z<G>(EB), HBr = gshr1z<G>(HB);
             const int hb_e = sh ? HBl : HB;
             const int eb_e = sh ? EBl : EB;
             const int hb_d = sh ? HB : HBr;
             const int qv = qc[i];
-            const int rv = on ? rc[jj] : 4;
+            const int rv = on ? rc[min(jj, RCAP - 1)] : 4;   // in-bounds read, no branch
             const int t1 = i == 0 ? -gO : hb_e - gO;
             const int t2 = i == 0 ? -gE : eb_e - gE;
             const int E = t1 > t2 ? t1 : t2;
@@ -792,10 +805,11 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
             const int diag = hb_d + ((rv == qv && rv < 4) ? match : -mismatch);
             const int e1 = E > 0 ? E : 0;
             const int hp = e1 > diag ? e1 : diag;
-            const int prev_hp = gshr<G, 1>(hp);
+            // lane 0's shifted-in value is never used (A, f_prev take their boundary values)
+            const int prev_hp = G == 16 ? rshr0<1>(hp) : gshr<G, 1>(hp);
             const int A = z == 0 ? -gO : prev_hp - gO;
             const int F = max(gscan_f<G>(A, gE), -(z + 1) * gE);
-            const int f_prev = z == 0 ? 0 : gshr<G, 1>(F);
+            const int f_prev = G == 16 ? rshr0<1>(F) : (z == 0 ? 0 : gshr<G, 1>(F));
             const int df = A > f_prev - gE ? 5 : 4;
             const int f1 = F > 0 ? F : 0;
             const int m = e1 > f1 ? e1 : f1;
@@ -804,9 +818,10 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
             if (on) {
                 int8_t* dl = dir + width_d * 3 * i + 3 * z;
                 dl[0] = (int8_t)de; dl[1] = (int8_t)df; dl[2] = (int8_t)dh;
-                if (H > lmax) lmax = H;
             }
-            if (on) { EB = E; HB = H; }                  // h_b[1..u] = h_c[1..u]
+            lmax = (on && H > lmax) ? H : lmax;
+            EB = on ? E : EB;                            // h_b[1..u] = h_c[1..u]
+            HB = on ? H : HB;
         }
         lmax = gmax<G>(lmax);
         if (lmax > max_v) max_v = lmax;
