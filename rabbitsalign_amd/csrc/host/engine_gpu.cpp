@@ -104,24 +104,30 @@ public:
         out.offsets.assign(n + 1, 0);
         out.nonrep.assign(n, 0.f);
         out.rescued.assign(n, 0);
+        // the NAMs, site checks and mismatch positions come back by DMA straight into
+        // the output vectors, whose storage is page-locked (no staging copy)
+        static const HostAllocFns kPinned{rsa_host_alloc, rsa_host_free};
+        if (out.nams.get_allocator().fns != &kPinned) out.nams = decltype(out.nams)(HostAlloc<Nam>(&kPinned));
+        if (out.sites.get_allocator().fns != &kPinned) out.sites = decltype(out.sites)(HostAlloc<rsa_nam_site>(&kPinned));
+        if (out.mm_pool.get_allocator().fns != &kPinned) out.mm_pool = decltype(out.mm_pool)(HostAlloc<uint16_t>(&kPinned));
+        // site checks on the device (k_sites): the host's NAM orientation and
+        // Hamming windows then never read the reference
+        static const bool want_sites = !(getenv("RSA_SITES") && getenv("RSA_SITES")[0] == '0');   // A/B switch
         size_t cap = std::max<size_t>(1024, 12 * n);
         for (;;) {
-            rsa_nam* nams = sg.get<rsa_nam>(Staging::NAMS, cap);
-            // site checks on the device (k_sites): the host's NAM orientation and
-            // Hamming windows then never read the reference
-            static const bool want_sites = !(getenv("RSA_SITES") && getenv("RSA_SITES")[0] == '0');   // A/B switch
-            rsa_nam_site* sites = want_sites ? sg.get<rsa_nam_site>(Staging::SITES, cap) : nullptr;
             const size_t mm_cap = 4 * cap;           // overflow is flagged per NAM and handled on the host
-            uint16_t* mm = sg.get<uint16_t>(Staging::MMPOOL, mm_cap);
-            rsa_nam_batch nb{nams, cap, out.offsets.data(), out.nonrep.data(), out.rescued.data(), 0,
-                             sites, mm, mm_cap, 0};
+            out.nams.resize(cap);
+            out.sites.resize(want_sites ? cap : 0);
+            out.mm_pool.resize(mm_cap);
+            rsa_nam_batch nb{out.nams.data(), cap, out.offsets.data(), out.nonrep.data(), out.rescued.data(), 0,
+                             want_sites ? out.sites.data() : nullptr, out.mm_pool.data(), mm_cap, 0};
             int rc = rsa_seed(ctx_, &rb, rescue_level, rescue_cutoff, &nb);
             if (rc == RSA_ERR_CAPACITY) { cap = nb.needed + 16; continue; }
             if (rc != RSA_OK) throw std::runtime_error(std::string("rsa_seed: ") + rsa_last_error(ctx_));
-            out.nams.assign(nams, nams + nb.needed);
-            if (sites) {
-                out.sites.assign(sites, sites + nb.needed);
-                out.mm_pool.assign(mm, mm + nb.mm_used);
+            out.nams.resize(nb.needed);
+            if (want_sites) {
+                out.sites.resize(nb.needed);
+                out.mm_pool.resize(nb.mm_used);
             } else {
                 out.sites.clear();
                 out.mm_pool.clear();

@@ -464,7 +464,7 @@ void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize, On
             on_frozen(c);
         }
     }
-    c.seeds = SeedBatchOut();
+    c.seeds.clear();
     c.times.part += since(t);
 }
 
@@ -871,6 +871,7 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
         std::vector<SwJob>& jobs = scratch.s->jobs;
         std::vector<AlignmentInfo>& infos = scratch.s->infos;
         AlignmentStatistics local;
+        SeedBatchOut so;                             // the worker's, reused chunk after chunk
         try {
         for (;;) {
             if (failed.load()) break;
@@ -882,7 +883,7 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
             rng.seed((unsigned)idx);
             std::vector<const std::string*> reads;
             for (size_t i = b; i < e; ++i) reads.push_back(&recs[i].seq);
-            SeedBatchOut so;
+            so.clear();
             {
                 Unslot u(slots, offl);
                 eng.seed(reads, mc.mparams.rescue_level, (unsigned)mc.mparams.rescue_cutoff, so);

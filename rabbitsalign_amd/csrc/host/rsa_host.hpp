@@ -7,8 +7,10 @@
 // the Engine interface; the product engine is the HIP C-ABI (include/rsa_gpu.h).
 #pragma once
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <new>
 #include <random>
 #include <string>
 #include <string_view>
@@ -297,13 +299,47 @@ void build_default_index(StiIndex& idx, const References& refs, const IndexParam
                          int threads, int device, bool host_copy = true);
 
 // --------------------------------------------------------------- engine ---
+// Storage of engine outputs that an engine may fill by DMA: an allocator that is
+// malloc by default and the engine's page-locked host memory when the engine
+// installs it (the GPU engine copies its NAM / site output straight into it
+// instead of through a staging buffer).  New elements are left uninitialised.
+struct HostAllocFns {
+    void* (*alloc)(size_t);
+    void (*free)(void*);
+};
+template <class T> struct HostAlloc {
+    using value_type = T;
+    const HostAllocFns* fns = nullptr;          // nullptr: malloc / free
+    HostAlloc() = default;
+    explicit HostAlloc(const HostAllocFns* f) : fns(f) {}
+    template <class U> HostAlloc(const HostAlloc<U>& o) noexcept : fns(o.fns) {}
+    template <class U> struct rebind { using other = HostAlloc<U>; };
+    T* allocate(size_t n) {
+        void* p = fns ? fns->alloc(n * sizeof(T)) : std::malloc(n * sizeof(T));
+        if (!p) throw std::bad_alloc();
+        return (T*)p;
+    }
+    void deallocate(T* p, size_t) noexcept { if (fns) fns->free(p); else std::free(p); }
+    template <class U> void construct(U* p) noexcept { ::new ((void*)p) U; }
+    template <class U, class... A> void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+    using propagate_on_container_move_assignment = std::true_type;
+    using propagate_on_container_copy_assignment = std::true_type;
+    using propagate_on_container_swap = std::true_type;
+    template <class U> bool operator==(const HostAlloc<U>& o) const { return fns == o.fns; }
+    template <class U> bool operator!=(const HostAlloc<U>& o) const { return fns != o.fns; }
+};
+
 struct SeedBatchOut {
-    std::vector<Nam> nams;
+    std::vector<Nam, HostAlloc<Nam>> nams;
     std::vector<uint64_t> offsets;              // [n+1]
     std::vector<float> nonrep;
     std::vector<uint8_t> rescued;
-    std::vector<rsa_nam_site> sites;            // one per NAM when the engine computes the site checks
-    std::vector<uint16_t> mm_pool;              // their mismatch positions
+    std::vector<rsa_nam_site, HostAlloc<rsa_nam_site>> sites;   // one per NAM when the engine computes the site checks
+    std::vector<uint16_t, HostAlloc<uint16_t>> mm_pool;         // their mismatch positions
+    // empty, keeping the storage (page-locked storage is expensive to allocate)
+    void clear() {
+        nams.clear(); offsets.clear(); nonrep.clear(); rescued.clear(); sites.clear(); mm_pool.clear();
+    }
     // site view of read r's NAM list (empty without site checks)
     SiteView site_view(size_t r) const {
         SiteView v;
