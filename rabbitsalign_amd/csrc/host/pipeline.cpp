@@ -83,7 +83,9 @@ constexpr int kDefaultExtGroup = 1;
 static int wait_workers(const Engine& eng, int threads) {
     const char* e = getenv("RSA_WAIT_WORKERS");
     if (e) return std::max(0, atoi(e));
-    return eng.offloads() ? (3 * threads) / 4 : 0;
+    // A/B on the box (16 threads): 4 extra workers 0.76-0.78 core-us a read, 12 0.87-0.92
+    // (profiles/r02/ab_wait_workers*.jsonl); round 1 had chosen 3/4 of the threads
+    return eng.offloads() ? threads / 4 : 0;
 }
 
 struct OrderedSink {
