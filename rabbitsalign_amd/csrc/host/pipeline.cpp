@@ -83,9 +83,10 @@ constexpr int kDefaultExtGroup = 1;
 static int wait_workers(const Engine& eng, int threads) {
     const char* e = getenv("RSA_WAIT_WORKERS");
     if (e) return std::max(0, atoi(e));
-    // A/B on the box (16 threads): 4 extra workers 0.76-0.78 core-us a read, 12 0.87-0.92
-    // (profiles/r02/ab_wait_workers*.jsonl); round 1 had chosen 3/4 of the threads
-    return eng.offloads() ? threads / 4 : 0;
+    // 3/4 of the threads (12 of 16).  Round-2 A/B runs disagree from box to box
+    // (profiles/r02/ab_wait_workers*.jsonl): 4 won one box, 12 won three of three
+    // alternating runs on another (19.5/19.0/16.1 vs 17.5/16.6/13.4 Mreads/s)
+    return eng.offloads() ? (3 * threads) / 4 : 0;
 }
 
 struct OrderedSink {
