@@ -114,15 +114,17 @@ static bool by_score(const T& a, const T& b) { return a.score > b.score; }
 // std::sort(by_score) of a read's NAM list, the same permutation: libstdc++'s
 // std::sort of <= 16 elements is exactly its (stable) insertion sort, done here
 // with plain element moves instead of a memmove per shift; longer lists go to std::sort.
-static void sort_nams_by_score(std::vector<Nam>& v) {
-    const size_t n = v.size();
-    if (n > 16) { std::sort(v.begin(), v.end(), by_score<Nam>); return; }
-    if (n < 2) return;
-    // the insertion sort runs on (score, index) keys; the NAMs move once, at the end
+// dst = src[0 .. n) in std::sort(by_score) order: <= 16 NAMs sort (score, index)
+// keys by the insertion sort and land in dst once, gathered
+void load_sorted_nams(std::vector<Nam>& dst, const Nam* src, size_t n) {
+    if (n > 16 || n < 2) {
+        dst.assign(src, src + n);
+        if (n > 16) std::sort(dst.begin(), dst.end(), by_score<Nam>);
+        return;
+    }
     float sc[16];
     uint8_t ix[16];
-    bool moved = false;
-    for (size_t i = 0; i < n; ++i) { sc[i] = v[i].score; ix[i] = (uint8_t)i; }
+    for (size_t i = 0; i < n; ++i) { sc[i] = src[i].score; ix[i] = (uint8_t)i; }
     for (size_t i = 1; i < n; ++i) {
         if (!(sc[i] > sc[i - 1])) continue;
         const float xs = sc[i];
@@ -131,12 +133,18 @@ static void sort_nams_by_score(std::vector<Nam>& v) {
         do { sc[j] = sc[j - 1]; ix[j] = ix[j - 1]; --j; } while (j > 0 && xs > sc[j - 1]);
         sc[j] = xs;
         ix[j] = xi;
-        moved = true;
     }
-    if (!moved) return;
+    dst.resize(n);
+    for (size_t i = 0; i < n; ++i) dst[i] = src[ix[i]];
+}
+
+static void sort_nams_by_score(std::vector<Nam>& v) {
+    const size_t n = v.size();
+    if (n > 16) { std::sort(v.begin(), v.end(), by_score<Nam>); return; }
+    if (n < 2) return;
     Nam tmp[16];
-    for (size_t i = 0; i < n; ++i) tmp[i] = v[ix[i]];
-    std::copy(tmp, tmp + n, v.begin());
+    std::copy(v.begin(), v.end(), tmp);
+    load_sorted_nams(v, tmp, n);
 }
 
 // ------------------------------------------------------------- NAM ops ---
@@ -658,12 +666,12 @@ static void align_PE_part(AlignTmpRes& res, const MapContext& mc, std::vector<Na
 void align_PE_read_part(AlignTmpRes& res, const Record&, const Record&, const Read& read1, const Read& read2,
                         std::vector<Nam> nams[2],
                         const bool rescued[2], AlignmentStatistics& stats, InsertSizeDistribution& isize,
-                        const MapContext& mc, std::minstd_rand& rng) {
+                        const MapContext& mc, std::minstd_rand& rng, bool sorted) {
     Details det[2];
     for (int m = 0; m < 2; ++m) {
         if (mc.mparams.rescue_level > 1 && rescued[m]) det[m].nam_rescue = true;
         det[m].nams = nams[m].size();
-        sort_nams_by_score(nams[m]);
+        if (!sorted) sort_nams_by_score(nams[m]);
         shuffle_top_nams(nams[m], rng);
     }
     align_PE_part(res, mc, nams[0], nams[1], read1, read2, mc.iparams.k, det, isize);

@@ -454,13 +454,14 @@ void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize, On
         bool rescued[2];
         for (int m = 0; m < 2; ++m) {
             const size_t r = 2 * i + m;
-            nams[m].assign(so.nams.begin() + (long)so.offsets[r], so.nams.begin() + (long)so.offsets[r + 1]);
+            load_sorted_nams(nams[m], so.nams.data() + so.offsets[r], so.offsets[r + 1] - so.offsets[r]);
             rescued[m] = so.rescued[r] != 0;
         }
         Read read1(c.r1[i]->seq, c.rc(i, 0)), read2(c.r2[i]->seq, c.rc(i, 1));
         read1.site = so.site_view(2 * i);
         read2.site = so.site_view(2 * i + 1);
-        align_PE_read_part(c.res[i], *c.r1[i], *c.r2[i], read1, read2, nams, rescued, c.stats, isize, mc, c.rng);
+        align_PE_read_part(c.res[i], *c.r1[i], *c.r2[i], read1, read2, nams, rescued, c.stats, isize, mc, c.rng,
+                           true);
         c.stats.n_reads += 2;
         if (!was_frozen && isize.frozen()) {
             was_frozen = true;

@@ -392,10 +392,13 @@ struct MapContext {
 
 // part / last split of src/aln.cpp:1927-2306 (PE) and 2372-2467 (SE).  `nams`
 // are the pre-sort NAM lists of both mates (already through find_nams/rescue).
+// sorted: nams[m] are already in std::sort(by_score) order (load_sorted_nams)
 void align_PE_read_part(AlignTmpRes& res, const Record& r1, const Record& r2, const Read& read1, const Read& read2,
                         std::vector<Nam> nams[2],
                         const bool rescued[2], AlignmentStatistics& stats, InsertSizeDistribution& isize,
-                        const MapContext& mc, std::minstd_rand& rng);
+                        const MapContext& mc, std::minstd_rand& rng, bool sorted = false);
+// dst = src[0 .. n) in the order std::sort(by_score) gives (aln.cpp:1962-1964), in one gather
+void load_sorted_nams(std::vector<Nam>& dst, const Nam* src, size_t n);
 void align_PE_read_last(AlignTmpRes& res, const Record& r1, const Record& r2, const Read& read1, const Read& read2,
                         Sam& sam,
                         AlignmentStatistics& stats, const InsertSizeDistribution& isize, const MapContext& mc,
