@@ -79,6 +79,18 @@ public:
     const char* name() const override { return "hip-gfx950"; }
     bool offloads() const override { return true; }
 
+    const HostAllocFns* io_alloc() const override { return &pinned_fns(); }
+    static const HostAllocFns& pinned_fns() {
+        static const HostAllocFns f{rsa_host_alloc, rsa_host_free};
+        return f;
+    }
+
+    void seed_packed(const char* blob, const uint64_t* offs, const uint32_t* lens, size_t n, int rescue_level,
+                     unsigned rescue_cutoff, SeedBatchOut& out) override {
+        rsa_read_batch rb{blob, offs, lens, (uint32_t)n};
+        seed_batch(rb, rescue_level, rescue_cutoff, out);
+    }
+
     void seed(const std::vector<const std::string*>& reads, int rescue_level, unsigned rescue_cutoff,
               SeedBatchOut& out) override {
         const size_t n = reads.size();
@@ -101,12 +113,17 @@ public:
             pos += reads[i]->size();
         }
         rsa_read_batch rb{blob, offs, lens, (uint32_t)n};
+        seed_batch(rb, rescue_level, rescue_cutoff, out);
+    }
+
+    void seed_batch(const rsa_read_batch& rb, int rescue_level, unsigned rescue_cutoff, SeedBatchOut& out) {
+        const size_t n = rb.n_reads;
         out.offsets.assign(n + 1, 0);
         out.nonrep.assign(n, 0.f);
         out.rescued.assign(n, 0);
         // the NAMs, site checks and mismatch positions come back by DMA straight into
         // the output vectors, whose storage is page-locked (no staging copy)
-        static const HostAllocFns kPinned{rsa_host_alloc, rsa_host_free};
+        const HostAllocFns& kPinned = pinned_fns();
         if (out.nams.get_allocator().fns != &kPinned) out.nams = decltype(out.nams)(HostAlloc<Nam>(&kPinned));
         if (out.sites.get_allocator().fns != &kPinned) out.sites = decltype(out.sites)(HostAlloc<rsa_nam_site>(&kPinned));
         if (out.mm_pool.get_allocator().fns != &kPinned) out.mm_pool = decltype(out.mm_pool)(HostAlloc<uint16_t>(&kPinned));

@@ -51,6 +51,13 @@ public:
         Hold h(*this);
         e_[h.i]->seed(reads, rescue_level, rescue_cutoff, out);
     }
+    void seed_packed(const char* blob, const uint64_t* offs, const uint32_t* lens, size_t n, int rescue_level,
+                     unsigned rescue_cutoff, SeedBatchOut& out) override {
+        Hold h(*this);
+        e_[h.i]->seed_packed(blob, offs, lens, n, rescue_level, rescue_cutoff, out);
+    }
+    // every device's engine shares the process's page-locked allocator (or none)
+    const HostAllocFns* io_alloc() const override { return e_[0]->io_alloc(); }
     void extend(const std::vector<SwJob>& jobs, const AlignmentParameters& p,
                 std::vector<AlignmentInfo>& out) override {
         Hold h(*this);

@@ -148,6 +148,11 @@ struct PeChunk {
     // itself when upper-casing would not change it, else an upper-cased copy
     std::vector<const Record*> r1, r2;
     std::deque<Record> owned;
+    // both mates' (upper-cased) sequences back to back, read 2i + m at seqoff[2i + m], in
+    // memory the engine can DMA from (Engine::io_alloc): the seeding call takes them as is
+    std::vector<char, HostAlloc<char>> seqbuf;
+    std::vector<uint64_t> seqoff;
+    std::vector<uint32_t> seqlen;
     SamText rcbuf;                            // reverse complements of both mates, computed once (resize: no fill):
     std::vector<uint64_t> rcoff;              // read i mate m at rcoff[2i+m] (length = read length)
     std::string_view rc(size_t i, int m) const {
@@ -312,7 +317,7 @@ static inline void prefetch_res(const AlignTmpRes& r) {
 }
 
 void pe_load(PeChunk& c, const std::vector<Record>& a, const std::vector<Record>& b, size_t idx, size_t chunk,
-             const std::vector<size_t>& starts) {
+             const std::vector<size_t>& starts, const HostAllocFns* io) {
     c.index = idx;
     c.owned.clear();
     c.stats = AlignmentStatistics();
@@ -332,6 +337,12 @@ void pe_load(PeChunk& c, const std::vector<Record>& a, const std::vector<Record>
     for (size_t i = 0; i < n; ++i) tot += a[c.begin + i].seq.size() + b[c.begin + i].seq.size();
     c.rcbuf.resize(tot);
     c.rcoff.resize(2 * n);
+    if (io) {
+        if (c.seqbuf.get_allocator().fns != io) c.seqbuf = decltype(c.seqbuf)(HostAlloc<char>(io));
+        c.seqbuf.resize(tot + 16);
+        c.seqoff.resize(2 * n);
+        c.seqlen.resize(2 * n);
+    }
     size_t at = 0;
     const size_t ahead = rec_ahead();
     // one pass: the reverse complement is taken while the sequence is in cache
@@ -346,6 +357,11 @@ void pe_load(PeChunk& c, const std::vector<Record>& a, const std::vector<Record>
             const std::string& sq = m ? c.r2[i]->seq : c.r1[i]->seq;
             c.rcoff[2 * i + m] = at;
             reverse_complement_into(sq, &c.rcbuf[at]);
+            if (io) {
+                memcpy(c.seqbuf.data() + at, sq.data(), sq.size());
+                c.seqoff[2 * i + m] = at;
+                c.seqlen[2 * i + m] = (uint32_t)sq.size();
+            }
             at += sq.size();
         }
     }
@@ -359,6 +375,14 @@ void pe_load(PeChunk& c, const std::vector<Record>& a, const std::vector<Record>
 void pe_seed(PeChunk& c, Engine& eng, const MapContext& mc, CpuSlots& slots) {
     const size_t n = c.r1.size();
     if (n == 0) return;
+    if (eng.io_alloc() && c.seqoff.size() == 2 * n) {     // packed by pe_load in DMA-able memory
+        const auto t = Clock::now();
+        Unslot u(slots, eng.offloads());
+        eng.seed_packed(c.seqbuf.data(), c.seqoff.data(), c.seqlen.data(), 2 * n, mc.mparams.rescue_level,
+                        (unsigned)mc.mparams.rescue_cutoff, c.seeds);
+        c.times.seed += since(t);
+        return;
+    }
     std::vector<const std::string*> reads;
     reads.reserve(2 * n);
     for (size_t i = 0; i < n; ++i) { reads.push_back(&c.r1[i]->seq); reads.push_back(&c.r2[i]->seq); }
@@ -623,7 +647,7 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
             std::unique_ptr<PeChunk> c = chunk_pool().take();
             if (!c) c = std::make_unique<PeChunk>();
             const auto t = Clock::now();
-            pe_load(*c, r1, r2, idx, chunk, opt.chunk_starts);
+            pe_load(*c, r1, r2, idx, chunk, opt.chunk_starts, eng.io_alloc());
             c->times.load += since(t);
             ps.push_back(c.get());
             cs.push_back(std::move(c));
@@ -635,7 +659,7 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
         std::unique_ptr<PeChunk> c = chunk_pool().take();
         if (!c) c = std::make_unique<PeChunk>();
         const auto t = Clock::now();
-        pe_load(*c, r1, r2, idx, chunk, opt.chunk_starts);
+        pe_load(*c, r1, r2, idx, chunk, opt.chunk_starts, eng.io_alloc());
         c->times.load += since(t);
         pe_seed(*c, eng, mc, slots);
         return c;

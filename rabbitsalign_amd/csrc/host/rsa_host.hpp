@@ -12,6 +12,7 @@
 #include <memory>
 #include <new>
 #include <random>
+#include <stdexcept>
 #include <string>
 #include <string_view>
 #include <vector>
@@ -365,6 +366,16 @@ public:
     // NAMs (pre-sort order) for every read, as align_*_read_part computes them (aln.cpp:1946-1962)
     virtual void seed(const std::vector<const std::string*>& reads, int rescue_level, unsigned rescue_cutoff,
                       SeedBatchOut& out) = 0;
+    // The same for reads already packed back to back (read i at blob[offs[i] ..
+    // offs[i] + lens[i])), in memory from io_alloc() -- engines that offer it
+    // (io_alloc() != nullptr) take the batch without a packing copy.
+    virtual void seed_packed(const char* blob, const uint64_t* offs, const uint32_t* lens, size_t n,
+                             int rescue_level, unsigned rescue_cutoff, SeedBatchOut& out) {
+        (void)blob; (void)offs; (void)lens; (void)n; (void)rescue_level; (void)rescue_cutoff; (void)out;
+        throw std::runtime_error("seed_packed: not supported by this engine");
+    }
+    // allocator of host buffers this engine can DMA from / to (nullptr: none)
+    virtual const HostAllocFns* io_alloc() const { return nullptr; }
     // Aligner::align for every job (aligner.cpp:114-210)
     virtual void extend(const std::vector<SwJob>& jobs, const AlignmentParameters& p,
                         std::vector<AlignmentInfo>& out) = 0;
