@@ -147,3 +147,27 @@ def test_extend_async_equals_sync(ctx):
     empty = c.extend_async(q, j[:0])
     assert empty.ready()
     assert empty.wait()[0].shape == (0,)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["pairs", "two_layout", "forced_rescan"])
+def test_extend_scan_modes(ctx, monkeypatch, mode):
+    """The two-layout grouped scan (k_ext_scan_g, default), the word-layout pair scan
+    (RSA_SCAN_W2=1, k_ext_scan_w2) and the pair scan with every result sent through the
+    exact rescan (+ RSA_W2_FORCE_RESCAN=1, the path the band kernels take when an
+    alignment does not prove the byte layout saturated) all give Aligner::align's results."""
+    c, ref, offs = ctx
+    if mode != "two_layout":
+        monkeypatch.setenv("RSA_SCAN_W2", "1")
+    if mode == "forced_rescan":
+        monkeypatch.setenv("RSA_W2_FORCE_RESCAN", "1")
+    c.reset_stats()
+    bad = _compare(c, ref, offs, 11, 3000, qlens=(150, 100, 250, 64, 129, 300))
+    assert not bad, f"{len(bad)} mismatches, first: {bad[0]}"
+    st = c.stats()
+    if mode == "two_layout":
+        assert st["scan_pair_jobs"] == 0, st
+    else:
+        assert st["scan_pair_jobs"] > 0, st
+    if mode == "forced_rescan":
+        assert st["scan_rescans"] > 0, st
