@@ -31,10 +31,10 @@ class OpVec {
 public:
     static constexpr uint32_t kInline = 12;
     OpVec() = default;
-    OpVec(const OpVec& o) { assign(o.begin(), o.end()); }
+    OpVec(const OpVec& o) { copy_from(o); }
     OpVec(OpVec&& o) noexcept { steal(o); }
     OpVec& operator=(const OpVec& o) {
-        if (this != &o) { n_ = 0; assign(o.begin(), o.end()); }
+        if (this != &o) copy_from(o);
         return *this;
     }
     OpVec& operator=(OpVec&& o) noexcept {
@@ -78,10 +78,21 @@ private:
         cap_ = (uint32_t)c;
     }
     void release() { delete[] p_; p_ = nullptr; n_ = 0; }
+    // inline contents move as one fixed-size block (no libc memcpy call for a
+    // variable length; the bytes past n_ are never read)
+    void copy_from(const OpVec& o) {
+        if (!o.p_ && !p_) {
+            memcpy(buf_, o.buf_, sizeof(buf_));
+            n_ = o.n_;
+        } else {
+            n_ = 0;
+            assign(o.begin(), o.end());
+        }
+    }
     void steal(OpVec& o) {
         n_ = o.n_;
         if (o.p_) { p_ = o.p_; cap_ = o.cap_; o.p_ = nullptr; }
-        else memcpy(buf_, o.buf_, sizeof(uint32_t) * n_);
+        else memcpy(buf_, o.buf_, sizeof(buf_));
         o.n_ = 0;
     }
     uint32_t* p_ = nullptr;                     // heap storage once past kInline
