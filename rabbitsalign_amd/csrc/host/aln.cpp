@@ -15,6 +15,11 @@
 
 #include "rsa_host.hpp"
 
+// per-thread pairing scratch: initial-exec TLS (one %fs-relative access instead of
+// a __tls_get_addr call per use; the whole block is a few hundred bytes of the
+// static TLS surplus glibc keeps for dlopen'ed libraries)
+#define RSA_TLS thread_local __attribute__((tls_model("initial-exec")))
+
 namespace rsa {
 
 // ------------------------------------------------------------ sequences ---
@@ -221,13 +226,14 @@ static bool is_proper_nam_pair(const Nam& nam1, const Nam& nam2, float mu, float
 struct NamPair { int score; Nam nam1; Nam nam2; };
 
 // aln.cpp:583-918 (use_fast_loop3 variant)
-static std::vector<NamPair> get_best_scoring_nam_pairs(const std::vector<Nam>& nams1, const std::vector<Nam>& nams2,
-                                                       float mu, float sigma) {
-    std::vector<NamPair> joint;
-    if (nams1.empty() && nams2.empty()) return joint;
+// into `joint` (cleared first; the caller's per-thread vector, so no allocation per pair)
+static void get_best_scoring_nam_pairs(std::vector<NamPair>& joint, const std::vector<Nam>& nams1,
+                                       const std::vector<Nam>& nams2, float mu, float sigma) {
+    joint.clear();
+    if (nams1.empty() && nams2.empty()) return;
     joint.reserve(nams1.size() + nams2.size());
     // membership by nam_id (the NAM's index in its read's list) instead of a hash set
-    thread_local std::vector<uint8_t> added_n1, added_n2;
+    RSA_TLS std::vector<uint8_t> added_n1, added_n2;
     auto reset_ids = [](std::vector<uint8_t>& v, const std::vector<Nam>& ns) {
         int mx = -1;
         for (const Nam& n : ns) mx = std::max(mx, n.nam_id);
@@ -236,7 +242,7 @@ static std::vector<NamPair> get_best_scoring_nam_pairs(const std::vector<Nam>& n
     reset_ids(added_n1, nams1);
     reset_ids(added_n2, nams2);
     int best_joint_hits = 0;
-    thread_local std::vector<Nam> sorted2[2];
+    RSA_TLS std::vector<Nam> sorted2[2];
     sorted2[0].clear();
     sorted2[1].clear();
     for (const auto& n2 : nams2) sorted2[n2.is_rc ? 1 : 0].push_back(n2);
@@ -319,7 +325,6 @@ static std::vector<NamPair> get_best_scoring_nam_pairs(const std::vector<Nam>& n
         }
     }
     std::sort(joint.begin(), joint.end(), [](const NamPair& a, const NamPair& b) { return a.score > b.score; });
-    return joint;
 }
 
 // ------------------------------------------------------------ hamming ---
@@ -587,9 +592,10 @@ static void align_PE_part(AlignTmpRes& res, const MapContext& mc, std::vector<Na
         return;
     }
     res.type = 4;
-    std::vector<NamPair> joint = get_best_scoring_nam_pairs(nams1, nams2, mu, sigma);
+    RSA_TLS std::vector<NamPair> joint;
+    get_best_scoring_nam_pairs(joint, nams1, nams2, mu, sigma);
     // nam_id flags (the id is the NAM's index in its read's list) instead of hash sets
-    thread_local std::vector<uint8_t> aligned1, aligned2;
+    RSA_TLS std::vector<uint8_t> aligned1, aligned2;
     auto reset_ids = [](std::vector<uint8_t>& v, const std::vector<Nam>& ns) {
         int mx = -1;
         for (const Nam& x : ns) mx = std::max(mx, x.nam_id);
@@ -899,18 +905,18 @@ static void pick_random_top_pair(std::vector<ScoredAlignmentPair>& hs, std::mins
 static void rescue_read_last(AlignTmpRes& res, const Read& read2, const Read& read1, const MapContext& mc,
                              Details det[2], float mu, float sigma, Sam& sam, const Record& rec1, const Record& rec2,
                              bool swap_r1r2, std::minstd_rand& rng) {
-    thread_local std::vector<Alignment> al1, al2;
+    RSA_TLS std::vector<Alignment> al1, al2;
     al1.clear();
     al2.clear();
     const size_t n = res.todo_nams.size();
-    for (size_t i = 0; i < n; i += 2) {
-        al1.push_back(res.align_res[i]);
-        al2.push_back(res.align_res[i + 1]);
+    for (size_t i = 0; i < n; i += 2) {              // res is not read again: the alignments move
         det[1].mate_rescue += !res.align_res[i + 1].is_unaligned;
+        al1.push_back(std::move(res.align_res[i]));
+        al2.push_back(std::move(res.align_res[i + 1]));
     }
     std::sort(al1.begin(), al1.end(), by_score<Alignment>);
     std::sort(al2.begin(), al2.end(), by_score<Alignment>);
-    thread_local std::vector<ScoredAlignmentPair> hs;
+    RSA_TLS std::vector<ScoredAlignmentPair> hs;
     get_best_scoring_pairs(hs, al1, al2, mu, sigma);
     std::sort(hs.begin(), hs.end(), by_score<ScoredAlignmentPair>);
     deduplicate_scored_pairs(hs);
@@ -963,43 +969,47 @@ void align_PE_read_last(AlignTmpRes& res, const Record& rec1, const Record& rec2
         sam.add_pair(a1, a2, rec1, rec2, read1.rc, read2.rc, (uint8_t)res.mapq1, (uint8_t)res.mapq2, proper, true, det);
     } else if (res.type == 4) {
         size_t pos = 0;
-        thread_local std::vector<std::pair<int, Alignment>> cache1, cache2;   // nam_id -> alignment (small; linear lookup)
+        // nam_id -> the alignment computed for it (small; linear lookup).  The cache and
+        // the loop hold pointers into res.align_res, which does not change here, so an
+        // alignment is copied once, into its scored pair
+        RSA_TLS std::vector<std::pair<int, const Alignment*>> cache1, cache2;
         cache1.clear();
         cache2.clear();
-        auto find_c = [](std::vector<std::pair<int, Alignment>>& c, int id) -> Alignment* {
-            for (auto& x : c) if (x.first == id) return &x.second;
+        auto find_c = [](const std::vector<std::pair<int, const Alignment*>>& c, int id) -> const Alignment* {
+            for (const auto& x : c) if (x.first == id) return x.second;
             return nullptr;
         };
-        Alignment a1_indv_max = res.align_res[pos];
+        const Alignment* a1_indv_max = &res.align_res[pos];
         cache1.push_back({res.todo_nams[pos].nam_id, a1_indv_max});
         pos++;
-        Alignment a2_indv_max = res.align_res[pos];
+        const Alignment* a2_indv_max = &res.align_res[pos];
         cache2.push_back({res.todo_nams[pos].nam_id, a2_indv_max});
         pos++;
-        thread_local std::vector<ScoredAlignmentPair> hs;
+        RSA_TLS std::vector<ScoredAlignmentPair> hs;
         hs.clear();
         for (int i = 0; i < res.type4_loop_size; ++i) {
             const Nam& n1 = res.type4_nams[2 * i];
             const Nam& n2 = res.type4_nams[2 * i + 1];
-            Alignment a1, a2;
+            const Alignment* p1;
+            const Alignment* p2;
             if (n1.ref_start >= 0) {
-                Alignment* c = find_c(cache1, n1.nam_id);
-                if (c) a1 = *c;
-                else { a1 = res.align_res[pos]; pos++; cache1.push_back({n1.nam_id, a1}); }
+                p1 = find_c(cache1, n1.nam_id);
+                if (!p1) { p1 = &res.align_res[pos]; pos++; cache1.push_back({n1.nam_id, p1}); }
             } else {
-                a1 = res.align_res[pos]; pos++;
-                det[0].mate_rescue += !a1.is_unaligned;
+                p1 = &res.align_res[pos]; pos++;
+                det[0].mate_rescue += !p1->is_unaligned;
             }
-            if (a1.score > a1_indv_max.score) a1_indv_max = a1;
+            if (p1->score > a1_indv_max->score) a1_indv_max = p1;
             if (n2.ref_start >= 0) {
-                Alignment* c = find_c(cache2, n2.nam_id);
-                if (c) a2 = *c;
-                else { a2 = res.align_res[pos]; pos++; cache2.push_back({n2.nam_id, a2}); }
+                p2 = find_c(cache2, n2.nam_id);
+                if (!p2) { p2 = &res.align_res[pos]; pos++; cache2.push_back({n2.nam_id, p2}); }
             } else {
-                a2 = res.align_res[pos]; pos++;
-                det[1].mate_rescue += !a2.is_unaligned;
+                p2 = &res.align_res[pos]; pos++;
+                det[1].mate_rescue += !p2->is_unaligned;
             }
-            if (a2.score > a2_indv_max.score) a2_indv_max = a2;
+            if (p2->score > a2_indv_max->score) a2_indv_max = p2;
+            const Alignment& a1 = *p1;
+            const Alignment& a2 = *p2;
             bool r1_r2 = a2.is_rc && (a1.ref_start <= a2.ref_start) && ((a2.ref_start - a1.ref_start) < mu + 10 * sigma);
             bool r2_r1 = a1.is_rc && (a2.ref_start <= a1.ref_start) && ((a1.ref_start - a2.ref_start) < mu + 10 * sigma);
             double combined;
@@ -1009,10 +1019,10 @@ void align_PE_read_last(AlignTmpRes& res, const Record& rec1, const Record& rec2
             } else {
                 combined = (double)a1.score + (double)a2.score - 20;
             }
-            hs.push_back(ScoredAlignmentPair{combined, std::move(a1), std::move(a2)});
+            hs.push_back(ScoredAlignmentPair{combined, a1, a2});
         }
-        double combined = (double)a1_indv_max.score + (double)a2_indv_max.score - 20;
-        hs.push_back(ScoredAlignmentPair{combined, a1_indv_max, a2_indv_max});
+        double combined = (double)a1_indv_max->score + (double)a2_indv_max->score - 20;
+        hs.push_back(ScoredAlignmentPair{combined, *a1_indv_max, *a2_indv_max});
         std::sort(hs.begin(), hs.end(), by_score<ScoredAlignmentPair>);
         deduplicate_scored_pairs(hs);
         pick_random_top_pair(hs, rng);
