@@ -839,7 +839,9 @@ size_t store_results_se(AlignTmpRes& res, const Read& read, const MapContext& mc
 }
 
 // -------------------------------------------------------------- last ---
-struct ScoredAlignmentPair { double score; Alignment alignment1; Alignment alignment2; };
+// the alignments stay where they are (the pair's results, or the rescue lists):
+// sorting and deduplicating the pairs moves two pointers, not two CIGARs
+struct ScoredAlignmentPair { double score; const Alignment* alignment1; const Alignment* alignment2; };
 
 static inline float normal_pdf(float x, float mu, float sigma) {   // aln.cpp:528-533
     static const float inv_sqrt_2pi = 0.3989422804014327;
@@ -857,7 +859,7 @@ static void get_best_scoring_pairs(std::vector<ScoredAlignmentPair>& pairs, cons
             double score = a1.score + a2.score;
             if ((a1.is_rc ^ a2.is_rc) && (dist < mu + 4 * sigma)) score += log(normal_pdf(dist, mu, sigma));
             else score -= 10;
-            pairs.push_back(ScoredAlignmentPair{score, a1, a2});
+            pairs.push_back(ScoredAlignmentPair{score, &a1, &a2});
         }
     }
 }
@@ -876,12 +878,12 @@ static std::pair<int, int> joint_mapq_from_high_scores(const std::vector<ScoredA
 }
 
 static void deduplicate_scored_pairs(std::vector<ScoredAlignmentPair>& pairs) {   // aln.cpp:1082-1105
-    int p1 = pairs[0].alignment1.ref_start, p2 = pairs[0].alignment2.ref_start;
-    int i1 = pairs[0].alignment1.ref_id, i2 = pairs[0].alignment2.ref_id;
+    int p1 = pairs[0].alignment1->ref_start, p2 = pairs[0].alignment2->ref_start;
+    int i1 = pairs[0].alignment1->ref_id, i2 = pairs[0].alignment2->ref_id;
     size_t j = 1;
     for (size_t i = 1; i < pairs.size(); i++) {
-        int s1 = pairs[i].alignment1.ref_start, s2 = pairs[i].alignment2.ref_start;
-        int d1 = pairs[i].alignment1.ref_id, d2 = pairs[i].alignment2.ref_id;
+        int s1 = pairs[i].alignment1->ref_start, s2 = pairs[i].alignment2->ref_start;
+        int d1 = pairs[i].alignment1->ref_id, d2 = pairs[i].alignment2->ref_id;
         if (s1 != p1 || s2 != p2 || d1 != i1 || d2 != i2) {
             p1 = s1; p2 = s2; i1 = d1; i2 = d2;
             pairs[j] = pairs[i];
@@ -924,8 +926,8 @@ static void rescue_read_last(AlignTmpRes& res, const Read& read2, const Read& re
     auto [mapq1, mapq2] = joint_mapq_from_high_scores(hs);
     const double secondary_dropoff = 2 * mc.aparams.mismatch + mc.aparams.gap_open;
     if (mc.mparams.max_secondary == 0) {
-        const Alignment& a1 = hs[0].alignment1;
-        const Alignment& a2 = hs[0].alignment2;
+        const Alignment& a1 = *hs[0].alignment1;
+        const Alignment& a2 = *hs[0].alignment2;
         if (swap_r1r2) sam.add_pair(a2, a1, rec2, rec1, read2.rc, read1.rc, mapq2, mapq1, is_proper_pair(a2, a1, mu, sigma), true, det);
         else sam.add_pair(a1, a2, rec1, rec2, read1.rc, read2.rc, mapq1, mapq2, is_proper_pair(a1, a2, mu, sigma), true, det);
     } else {
@@ -937,12 +939,12 @@ static void rescue_read_last(AlignTmpRes& res, const Read& read2, const Read& re
             const auto& ap = hs[i];
             if (s_max - ap.score < secondary_dropoff) {
                 if (swap_r1r2) {
-                    bool proper = is_proper_pair(ap.alignment2, ap.alignment1, mu, sigma);
+                    bool proper = is_proper_pair(*ap.alignment2, *ap.alignment1, mu, sigma);
                     Details sw[2] = {det[1], det[0]};
-                    sam.add_pair(ap.alignment2, ap.alignment1, rec2, rec1, read2.rc, read1.rc, mapq2, mapq1, proper, is_primary, sw);
+                    sam.add_pair(*ap.alignment2, *ap.alignment1, rec2, rec1, read2.rc, read1.rc, mapq2, mapq1, proper, is_primary, sw);
                 } else {
-                    bool proper = is_proper_pair(ap.alignment1, ap.alignment2, mu, sigma);
-                    sam.add_pair(ap.alignment1, ap.alignment2, rec1, rec2, read1.rc, read2.rc, mapq1, mapq2, proper, is_primary, det);
+                    bool proper = is_proper_pair(*ap.alignment1, *ap.alignment2, mu, sigma);
+                    sam.add_pair(*ap.alignment1, *ap.alignment2, rec1, rec2, read1.rc, read2.rc, mapq1, mapq2, proper, is_primary, det);
                 }
             } else break;
         }
@@ -1019,18 +1021,18 @@ void align_PE_read_last(AlignTmpRes& res, const Record& rec1, const Record& rec2
             } else {
                 combined = (double)a1.score + (double)a2.score - 20;
             }
-            hs.push_back(ScoredAlignmentPair{combined, a1, a2});
+            hs.push_back(ScoredAlignmentPair{combined, p1, p2});
         }
         double combined = (double)a1_indv_max->score + (double)a2_indv_max->score - 20;
-        hs.push_back(ScoredAlignmentPair{combined, *a1_indv_max, *a2_indv_max});
+        hs.push_back(ScoredAlignmentPair{combined, a1_indv_max, a2_indv_max});
         std::sort(hs.begin(), hs.end(), by_score<ScoredAlignmentPair>);
         deduplicate_scored_pairs(hs);
         pick_random_top_pair(hs, rng);
         auto [mapq1, mapq2] = joint_mapq_from_high_scores(hs);
         const auto& best = hs[0];
         if (mc.mparams.max_secondary == 0) {
-            bool proper = is_proper_pair(best.alignment1, best.alignment2, mu, sigma);
-            sam.add_pair(best.alignment1, best.alignment2, rec1, rec2, read1.rc, read2.rc, mapq1, mapq2, proper, true, det);
+            bool proper = is_proper_pair(*best.alignment1, *best.alignment2, mu, sigma);
+            sam.add_pair(*best.alignment1, *best.alignment2, rec1, rec2, read1.rc, read2.rc, mapq1, mapq2, proper, true, det);
         } else {
             auto max_out = std::min(hs.size(), (size_t)mc.mparams.max_secondary);
             float s_max = best.score;
@@ -1041,8 +1043,8 @@ void align_PE_read_last(AlignTmpRes& res, const Record& rec1, const Record& rec2
                 float s_score = ap.score;
                 if (i > 0) { is_primary = false; mapq1 = 255; mapq2 = 255; }
                 if (s_max - s_score < sd) {
-                    bool proper = is_proper_pair(ap.alignment1, ap.alignment2, mu, sigma);
-                    sam.add_pair(ap.alignment1, ap.alignment2, rec1, rec2, read1.rc, read2.rc, mapq1, mapq2, proper, is_primary, det);
+                    bool proper = is_proper_pair(*ap.alignment1, *ap.alignment2, mu, sigma);
+                    sam.add_pair(*ap.alignment1, *ap.alignment2, rec1, rec2, read1.rc, read2.rc, mapq1, mapq2, proper, is_primary, det);
                 } else break;
             }
         }
