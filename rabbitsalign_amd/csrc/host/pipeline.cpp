@@ -503,7 +503,9 @@ void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize) {
 // appends the chunk's SW jobs (pc.cpp:214-242, 333-368) to `jobs`
 void pe_get_str(PeChunk& c, const MapContext& mc, float mu, float sigma, std::vector<SwJob>& jobs) {
     const auto t = Clock::now();
-    for (size_t i = 0; i < c.r1.size(); ++i) {
+    const size_t n = c.r1.size(), ahead = rec_ahead();
+    for (size_t i = 0; i < n; ++i) {
+        if (i + ahead < n) prefetch_vec(c.res[i + ahead].todo_nams);   // written by part(), cold by now
         const Read read1(c.r1[i]->seq, c.rc(i, 0)), read2(c.r2[i]->seq, c.rc(i, 1));
         collect_jobs_pe(c.res[i], *c.r1[i], *c.r2[i], read1, read2, mc, mu, sigma, jobs);
     }
