@@ -1290,7 +1290,7 @@ k_rescue(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict
                 added_buf, map_scratch + (size_t)t * map_stride(map_cap), map_cap, ncnt, flags);
 }
 
-// one wavefront per listed read, maps in LDS, lane 0 (see k_find_nams_w)
+// one wavefront per listed read, maps in LDS, lane 0 (the LDS map layout of k_find_nams_w2)
 __global__ void __launch_bounds__(64 * FN_WAVES)
 k_rescue_w(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi,
            const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, const uint64_t* __restrict__ roff,
