@@ -39,9 +39,13 @@ static const char kDigitPairs[201] =
     "40414243444546474849505152535455565758596061626364656667686970717273747576777879"
     "8081828384858687888990919293949596979899";
 
+// digits written in place from the end backwards, two at a time (no staging buffer,
+// so no variable-length memcpy call per number)
 static inline char* put_uint(char* p, uint64_t v) {
-    char buf[24];
-    char* q = buf + sizeof buf;
+    int n = 1;
+    for (uint64_t t = 10; n < 20 && v >= t; t *= 10) ++n;
+    char* const e = p + n;
+    char* q = e;
     while (v >= 100) {
         const unsigned r = (unsigned)(v % 100);
         v /= 100;
@@ -50,9 +54,7 @@ static inline char* put_uint(char* p, uint64_t v) {
     }
     if (v >= 10) { q -= 2; memcpy(q, kDigitPairs + 2 * v, 2); }
     else *--q = (char)('0' + v);
-    const size_t n = (size_t)(buf + sizeof buf - q);
-    memcpy(p, q, n);
-    return p + n;
+    return e;
 }
 
 static inline char* put_int(char* p, int64_t v) {
@@ -60,9 +62,26 @@ static inline char* put_int(char* p, int64_t v) {
     return put_uint(p, (uint64_t)v);
 }
 
+// short fields (names, contig names, tags) by overlapping fixed-size moves that
+// stay inside [0, n) of the source; SEQ / QUAL and longer go through memcpy
 static inline char* put_str(char* p, std::string_view s) {
-    memcpy(p, s.data(), s.size());
-    return p + s.size();
+    const char* src = s.data();
+    const size_t n = s.size();
+    if (n >= 16 && n <= 32) {
+        memcpy(p, src, 16);
+        memcpy(p + n - 16, src + n - 16, 16);
+    } else if (n >= 8 && n < 16) {
+        memcpy(p, src, 8);
+        memcpy(p + n - 8, src + n - 8, 8);
+    } else if (n >= 4 && n < 8) {
+        memcpy(p, src, 4);
+        memcpy(p + n - 4, src + n - 4, 4);
+    } else if (n < 4) {
+        for (size_t i = 0; i < n; ++i) p[i] = src[i];
+    } else {
+        memcpy(p, src, n);
+    }
+    return p + n;
 }
 
 static inline void append_uint(std::string& out, uint64_t v) {
