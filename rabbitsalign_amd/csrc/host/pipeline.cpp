@@ -125,20 +125,30 @@ struct OrderedSink {
         s.clear();
         sp.v.push_back(std::move(s));
     }
-    // `made`: the chunk's digest, folded in while its text was written (Sam::digest_into)
+    bool writing = false;     // a worker is in the sink: it writes every chunk that becomes next
+    // `made`: the chunk's digest, folded in while its text was written (Sam::digest_into).
+    // One writer at a time keeps the sink calls in chunk order, and it calls the sink
+    // outside the lock: the other workers file their chunks and go back to mapping
+    // instead of waiting for a file write
     void put(size_t idx, SamText&& s, const SamDigest* made = nullptr) {
         SamDigest d;
         if (digest) d = made ? *made : SamDigest::of(s.data(), s.size());   // in the calling worker
-        std::lock_guard<std::mutex> g(m);
+        std::unique_lock<std::mutex> g(m);
         pending.emplace(idx, std::make_pair(std::move(s), d));
+        if (writing) return;
+        writing = true;
         for (auto it = pending.find(next); it != pending.end(); it = pending.find(next)) {
-            bytes += it->second.first.size();
+            SamText text = std::move(it->second.first);
+            bytes += text.size();
             total.append(it->second.second);
-            if (sink) sink(user, it->second.first.data(), it->second.first.size());
-            give_back(it->second.first);
             pending.erase(it);
             next++;
+            g.unlock();
+            if (sink) sink(user, text.data(), text.size());
+            give_back(text);
+            g.lock();
         }
+        writing = false;
     }
 };
 
