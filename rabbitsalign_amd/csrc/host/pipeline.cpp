@@ -887,6 +887,29 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
     return result;
 }
 
+// seeding outputs of the single-end workers, kept across mapping calls: the GPU
+// engine gives them page-locked storage, which is expensive to allocate (a fresh
+// one per worker per call put page locking into every call)
+struct SeedOutPool {
+    std::mutex m;
+    std::vector<std::unique_ptr<SeedBatchOut>> v;
+    static SeedOutPool& get() {
+        static SeedOutPool* p = new SeedOutPool();   // never destroyed: no exit-time teardown
+        return *p;
+    }
+    std::unique_ptr<SeedBatchOut> take() {
+        std::lock_guard<std::mutex> g(m);
+        if (v.empty()) return std::make_unique<SeedBatchOut>();
+        auto x = std::move(v.back());
+        v.pop_back();
+        return x;
+    }
+    void put(std::unique_ptr<SeedBatchOut> x) {
+        std::lock_guard<std::mutex> g(m);
+        if (v.size() < 64) v.push_back(std::move(x));
+    }
+};
+
 // Single-end: perform_task_async_se (pc.cpp:814-1096).  No insert-size state;
 // records are NOT upper-cased on this path; chunks are independent from the start.
 PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, const MapContext& mc,
@@ -911,7 +934,8 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
         std::vector<SwJob>& jobs = scratch.s->jobs;
         std::vector<AlignmentInfo>& infos = scratch.s->infos;
         AlignmentStatistics local;
-        SeedBatchOut so;                             // the worker's, reused chunk after chunk
+        std::unique_ptr<SeedBatchOut> so_own = SeedOutPool::get().take();
+        SeedBatchOut& so = *so_own;                  // the worker's, reused chunk after chunk and across calls
         try {
         for (;;) {
             if (failed.load()) break;
@@ -976,6 +1000,8 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
             failed = true;
         }
         hold.reset();
+        so.clear();
+        SeedOutPool::get().put(std::move(so_own));
         std::lock_guard<std::mutex> g(stat_m);
         result.stats.add(local);
     };
