@@ -887,24 +887,31 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
     return result;
 }
 
-// seeding outputs of the single-end workers, kept across mapping calls: the GPU
-// engine gives them page-locked storage, which is expensive to allocate (a fresh
-// one per worker per call put page locking into every call)
-struct SeedOutPool {
+// a single-end worker's storage, kept across chunks and mapping calls: the seeding
+// output (page-locked under the GPU engine, expensive to allocate: a fresh one per
+// worker per call put page locking into every call) and the per-read results,
+// reverse complements and NAM list, which keep their capacity
+struct SeScratch {
+    SeedBatchOut so;
+    std::vector<AlignTmpRes> res;
+    std::vector<std::string> rcs;
+    std::vector<Nam> nams;
+};
+struct SeScratchPool {
     std::mutex m;
-    std::vector<std::unique_ptr<SeedBatchOut>> v;
-    static SeedOutPool& get() {
-        static SeedOutPool* p = new SeedOutPool();   // never destroyed: no exit-time teardown
+    std::vector<std::unique_ptr<SeScratch>> v;
+    static SeScratchPool& get() {
+        static SeScratchPool* p = new SeScratchPool();   // never destroyed: no exit-time teardown
         return *p;
     }
-    std::unique_ptr<SeedBatchOut> take() {
+    std::unique_ptr<SeScratch> take() {
         std::lock_guard<std::mutex> g(m);
-        if (v.empty()) return std::make_unique<SeedBatchOut>();
+        if (v.empty()) return std::make_unique<SeScratch>();
         auto x = std::move(v.back());
         v.pop_back();
         return x;
     }
-    void put(std::unique_ptr<SeedBatchOut> x) {
+    void put(std::unique_ptr<SeScratch> x) {
         std::lock_guard<std::mutex> g(m);
         if (v.size() < 64) v.push_back(std::move(x));
     }
@@ -934,8 +941,11 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
         std::vector<SwJob>& jobs = scratch.s->jobs;
         std::vector<AlignmentInfo>& infos = scratch.s->infos;
         AlignmentStatistics local;
-        std::unique_ptr<SeedBatchOut> so_own = SeedOutPool::get().take();
-        SeedBatchOut& so = *so_own;                  // the worker's, reused chunk after chunk and across calls
+        std::unique_ptr<SeScratch> se = SeScratchPool::get().take();
+        SeedBatchOut& so = se->so;                   // the worker's, reused chunk after chunk and across calls
+        std::vector<AlignTmpRes>& res = se->res;
+        std::vector<std::string>& rcs = se->rcs;
+        std::vector<Nam>& nams = se->nams;
         try {
         for (;;) {
             if (failed.load()) break;
@@ -952,12 +962,18 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
                 Unslot u(slots, offl);
                 eng.seed(reads, mc.mparams.rescue_level, (unsigned)mc.mparams.rescue_cutoff, so);
             }
-            std::vector<AlignTmpRes> res(e - b);
-            std::vector<std::string> rcs(e - b);
-            for (size_t i = b; i < e; ++i) rcs[i - b] = reverse_complement(recs[i].seq);
+            if (res.size() > e - b) res.resize(e - b);
+            for (auto& x : res) x.reset();
+            res.resize(e - b);
+            rcs.resize(e - b);
+            for (size_t i = b; i < e; ++i) {
+                std::string& rc = rcs[i - b];
+                rc.resize(recs[i].seq.size());
+                reverse_complement_into(recs[i].seq, rc.data());
+            }
             for (size_t i = b; i < e; ++i) {
                 const size_t r = i - b;
-                std::vector<Nam> nams(so.nams.begin() + (long)so.offsets[r], so.nams.begin() + (long)so.offsets[r + 1]);
+                nams.assign(so.nams.begin() + (long)so.offsets[r], so.nams.begin() + (long)so.offsets[r + 1]);
                 Read read(recs[i].seq, rcs[r]);
                 read.site = so.site_view(r);
                 align_SE_read_part(res[r], recs[i], read, nams, so.rescued[r] != 0, st, mc, rng);
@@ -1001,7 +1017,7 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
         }
         hold.reset();
         so.clear();
-        SeedOutPool::get().put(std::move(so_own));
+        SeScratchPool::get().put(std::move(se));
         std::lock_guard<std::mutex> g(stat_m);
         result.stats.add(local);
     };
