@@ -353,6 +353,11 @@ int rsam_map(rsam* m, const rsam_reads* reads, int threads, int chunk_size, cons
         po.chunk_size = chunk_size;
         po.digest = true;
         SamSink sk = st.f ? sink_fn : nullptr;
+        PosSink ps;                                 // a regular file: chunks written in parallel at their offsets
+        if (st.f && pos_sink_open(st.f, ps)) {
+            po.sink_at = pos_sink_write;
+            po.sink_at_user = &ps;
+        }
         PipelineResult res;
         if (!reads->interleaved.empty()) {          // pairs per chunk of 2 * chunk_size records (pc.cpp:38-107)
             std::vector<Record> all(reads->interleaved), r1, r2;
@@ -363,6 +368,7 @@ int rsam_map(rsam* m, const rsam_reads* reads, int threads, int chunk_size, cons
                                 : run_pipeline_se(reads->r1, *m->eng, mc, po, sk, &st);
         }
         if (st.f) fclose(st.f);
+        if (ps.failed) throw std::runtime_error(std::string("write failed: ") + sam_path);
         if (out) {
             out->n_reads = res.stats.n_reads;
             out->sam_bytes = res.sam_bytes;

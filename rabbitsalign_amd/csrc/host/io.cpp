@@ -1,14 +1,15 @@
-#include <unistd.h>
-#include <fcntl.h>
-#include <sys/stat.h>
 // io.cpp -- CIGAR text, SAM records, FASTA, .sti read/write/build, FASTQ input.
 // Restated from src/cigar.cpp, src/sam.cpp, src/refs.cpp, src/index.cpp,
 // src/indexparameters.cpp and the kseq++ record semantics used by src/fastq.cpp.
+#include <fcntl.h>
 #include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <zlib.h>
 
 #include <algorithm>
 #include <atomic>
+#include <cerrno>
 #include <exception>
 #include <cmath>
 #include <cstdio>
@@ -936,6 +937,39 @@ void FastxReader::read_pair(const std::string& p1, const std::string& p2, std::v
     try { r1 = read(p1); } catch (...) { t.join(); throw; }
     t.join();
     if (err) std::rethrow_exception(err);
+}
+
+}  // namespace rsa
+
+namespace rsa {
+
+bool pos_sink_open(FILE* f, PosSink& ps) {
+    if (!f || fflush(f) != 0) return false;
+    const int fd = fileno(f);
+    if (fd < 0) return false;
+    struct stat st;
+    if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode)) return false;    // pipes, terminals: sequential
+    const off_t at = lseek(fd, 0, SEEK_CUR);
+    if (at < 0) return false;
+    ps.fd = fd;
+    ps.base = (uint64_t)at;
+    return true;
+}
+
+void pos_sink_write(void* user, const char* chunk, size_t bytes, uint64_t offset) {
+    PosSink& ps = *(PosSink*)user;
+    uint64_t at = ps.base + offset;
+    while (bytes > 0) {
+        const ssize_t w = pwrite(ps.fd, chunk, bytes, (off_t)at);
+        if (w <= 0) {
+            if (w < 0 && errno == EINTR) continue;
+            ps.failed = true;
+            return;
+        }
+        chunk += w;
+        bytes -= (size_t)w;
+        at += (uint64_t)w;
+    }
 }
 
 }  // namespace rsa

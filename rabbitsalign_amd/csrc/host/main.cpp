@@ -190,12 +190,21 @@ int cli_main(int argc, char** argv, EngineFactory factory, const char* prog) {
         PipelineOptions po;
         po.threads = o.threads; po.chunk_size = o.chunk_size; po.rg_id = o.rg_id;
         po.chunk_starts = std::move(chunk_starts);
+        PosSink ps;                                 // a regular file: chunks written in parallel at their offsets
+        if (pos_sink_open(out, ps)) {
+            po.sink_at = pos_sink_write;
+            po.sink_at_user = &ps;
+        }
         if (o.interleaved && o.verbose)
             fprintf(stderr, "[%s] interleaved input: %zu pairs, %zu unpaired records (not mapped, as in the "
                             "reference's paired-end task)\n", prog, recs1.size(), singletons);
         PipelineResult res = (recs2.empty() && !o.interleaved) ? run_pipeline_se(recs1, *eng, mc, po, write_sink, out)
                                                                : run_pipeline_pe(recs1, recs2, *eng, mc, po, write_sink, out);
+        if (ps.fd >= 0) {                            // the stream's position trails the positional writes
+            if (fseeko(out, 0, SEEK_END) != 0) throw std::runtime_error("cannot seek the output");
+        }
         if (out != stdout) fclose(out); else fflush(out);
+        if (ps.failed) throw std::runtime_error("write failed: " + (o.out_file.empty() ? std::string("stdout") : o.out_file));
         fprintf(stderr,
                 "[%s] engine %s | index %.2f s, upload %.2f s | mapped %lu reads in %.3f s = %.4f Mreads/s | "
                 "SW calls %lu, tried %lu, inconsistent NAMs %lu, NAM rescue %lu, mate rescue %lu\n",

@@ -125,6 +125,9 @@ struct OrderedSink {
         s.clear();
         sp.v.push_back(std::move(s));
     }
+    SamSinkAt sink_at = nullptr;   // positional mode (PipelineOptions::sink_at)
+    void* at_user = nullptr;
+    std::vector<std::pair<uint64_t, SamText>> ready;   // positional mode: offset known, not written yet
     bool writing = false;     // a worker is in the sink: it writes every chunk that becomes next
     // `made`: the chunk's digest, folded in while its text was written (Sam::digest_into).
     // One writer at a time keeps the sink calls in chunk order, and it calls the sink
@@ -135,6 +138,27 @@ struct OrderedSink {
         if (digest) d = made ? *made : SamDigest::of(s.data(), s.size());   // in the calling worker
         std::unique_lock<std::mutex> g(m);
         pending.emplace(idx, std::make_pair(std::move(s), d));
+        if (sink_at) {
+            // offsets in chunk order as chunks become next; the writes themselves run in
+            // parallel, each ready chunk taken by whichever worker is here
+            for (auto it = pending.find(next); it != pending.end(); it = pending.find(next)) {
+                const uint64_t off = bytes;
+                bytes += it->second.first.size();
+                total.append(it->second.second);
+                ready.emplace_back(off, std::move(it->second.first));
+                pending.erase(it);
+                next++;
+            }
+            while (!ready.empty()) {
+                std::pair<uint64_t, SamText> w = std::move(ready.back());
+                ready.pop_back();
+                g.unlock();
+                sink_at(at_user, w.second.data(), w.second.size(), w.first);
+                give_back(w.second);
+                g.lock();
+            }
+            return;
+        }
         if (writing) return;
         writing = true;
         for (auto it = pending.find(next); it != pending.end(); it = pending.find(next)) {
@@ -609,6 +633,8 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
     const auto t0 = Clock::now();
     PipelineResult result;
     OrderedSink os{sink, user, opt.digest};
+    os.sink_at = opt.sink_at;
+    os.at_user = opt.sink_at_user;
     const size_t chunk = (size_t)std::max(1, opt.chunk_size);
     if (!opt.chunk_starts.empty() && (opt.chunk_starts.front() != 0 || opt.chunk_starts.back() != r1.size()))
         throw std::runtime_error("chunk_starts do not cover the pairs");
@@ -924,6 +950,8 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
     auto t0 = std::chrono::steady_clock::now();
     PipelineResult result;
     OrderedSink os{sink, user, opt.digest};
+    os.sink_at = opt.sink_at;
+    os.at_user = opt.sink_at_user;
     const size_t chunk = (size_t)std::max(1, opt.chunk_size);
     const size_t n_chunks = (recs.size() + chunk - 1) / chunk;
     std::atomic<size_t> next{0};

@@ -15,6 +15,7 @@
 #include <stdexcept>
 #include <string>
 #include <string_view>
+#include <atomic>
 #include <vector>
 
 #include "../../../include/rsa_gpu.h"
@@ -559,6 +560,9 @@ private:
 // called at the start of every pipeline worker thread (profiling hooks; null by default)
 extern void (*g_worker_start_hook)();
 
+// positional form: the chunk's bytes belong at `offset` of the SAM body (chunk order
+// fixes the offsets; several chunks may be written at once)
+using SamSinkAt = void (*)(void* user, const char* chunk, size_t bytes, uint64_t offset);
 struct PipelineOptions {
     int threads = 3;
     int chunk_size = 10000;
@@ -573,6 +577,10 @@ struct PipelineOptions {
     // pairs [chunk_starts[i], chunk_starts[i+1]); empty = every chunk_size pairs.
     // Interleaved input sets them (its chunks hold up to chunk_size pairs each)
     std::vector<size_t> chunk_starts;
+    // when set, SAM chunks go here at their body offsets instead of to the sequential
+    // sink, each written by the worker that finds it ready (parallel file writes)
+    SamSinkAt sink_at = nullptr;
+    void* sink_at_user = nullptr;
 };
 
 // --interleaved input (InputBuffer::read_records + distribute_interleaved,
@@ -617,6 +625,16 @@ struct PipelineResult {
 // chunks are processed strictly in the single-worker timeline until the insert
 // size estimate freezes, then chunk-parallel over `threads` host workers.
 using SamSink = void (*)(void* user, const char* chunk, size_t bytes);
+// positional SAM writes into a seekable file after what it already holds (the
+// header): pos_sink_open flushes `f` and returns false when it cannot take them
+// (a pipe, a terminal); failed is set when a write fails
+struct PosSink {
+    int fd = -1;
+    uint64_t base = 0;
+    std::atomic<bool> failed{false};
+};
+bool pos_sink_open(FILE* f, PosSink& ps);
+void pos_sink_write(void* user, const char* chunk, size_t bytes, uint64_t offset);
 PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<Record>& r2, Engine& eng,
                                const MapContext& mc, const PipelineOptions& opt, SamSink sink, void* user);
 PipelineResult run_pipeline_se(const std::vector<Record>& r, Engine& eng, const MapContext& mc,
