@@ -72,6 +72,13 @@ void rsam_reads_free(rsam_reads* r);
 /* Map every read; SAM to `sam_path` (header + body) or kept in memory only when NULL. */
 int rsam_map(rsam* m, const rsam_reads* reads, int threads, int chunk_size, const char* sam_path,
              rsam_stats* out);
+/* Map FASTQ/FASTA files as the CLI does: the reads are streamed (a reader thread per
+ * file parses chunks of chunk_size pairs while the workers map, InputBuffer::read_records,
+ * src/pc.cpp:74-107), so memory does not grow with the input.  fq2 NULL or "": single-end,
+ * or interleaved pairs when `interleaved` != 0.  map_seconds runs from the call to the last
+ * SAM byte written (the reference's consumer cost, src/main.cpp:446,595). */
+int rsam_map_files(rsam* m, const char* fq1, const char* fq2, int interleaved, int threads, int chunk_size,
+                   const char* sam_path, rsam_stats* out);
 
 /* Map on more devices of this node: each listed device gets its own engine with a
  * full replica of the index; rsam_map then sends every seeding / extension call to

@@ -28,7 +28,7 @@ public:
         p_.q = (uint64_t)idx.params.q;
     }
     const char* name() const override { return "cpu-oracle"; }
-    void seed(const std::vector<const std::string*>& reads, int rescue_level, unsigned rescue_cutoff,
+    void seed(const std::vector<std::string_view>& reads, int rescue_level, unsigned rescue_cutoff,
               rsa::SeedBatchOut& out) override {
         const size_t n = reads.size();
         out.nams.clear();
@@ -38,7 +38,7 @@ public:
         std::vector<ora_qrs> q;
         std::vector<ora_nam> nams(1 << 16);
         for (size_t i = 0; i < n; ++i) {
-            const std::string& s = *reads[i];
+            const std::string_view s = reads[i];
             q.resize(2 * s.size() + 8);
             int nq = ora_randstrobes_query(s.data(), (int)s.size(), &p_, q.data(), (int)q.size());
             float nonrep = 1.f;

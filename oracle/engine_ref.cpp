@@ -63,7 +63,7 @@ public:
         index_.randstrobe_start_indices.assign(idx.bucket_starts.begin(), idx.bucket_starts.end());
     }
     const char* name() const override { return "cpu-reference"; }
-    void seed(const std::vector<const std::string*>& reads, int rescue_level, unsigned rescue_cutoff,
+    void seed(const std::vector<std::string_view>& reads, int rescue_level, unsigned rescue_cutoff,
               rsa::SeedBatchOut& out) override {
         const size_t n = reads.size();
         out.nams.clear();
@@ -71,7 +71,7 @@ public:
         out.nonrep.assign(n, 1.f);
         out.rescued.assign(n, 0);
         for (size_t i = 0; i < n; ++i) {
-            auto q = randstrobes_query(*reads[i], params_);
+            auto q = randstrobes_query(reads[i], params_);
             auto [nonrep, nams] = find_nams(q, index_);
             out.nonrep[i] = nonrep;
             if (rescue_level > 1 && (nams.empty() || nonrep < 0.7)) {

@@ -61,7 +61,7 @@ public:
     static void nap(double ms) {
         if (ms > 0) std::this_thread::sleep_for(std::chrono::microseconds((long)(ms * 1000)));
     }
-    void seed(const std::vector<const std::string*>& reads, int rl, unsigned rc, SeedBatchOut& out) override {
+    void seed(const std::vector<std::string_view>& reads, int rl, unsigned rc, SeedBatchOut& out) override {
         const void* key = reads.empty() ? nullptr : (const void*)reads[0];
         if (replay) {
             nap(seed_ms);

@@ -669,7 +669,7 @@ static void align_PE_part(AlignTmpRes& res, const MapContext& mc, std::vector<Na
 }
 
 // align_PE_read_part (aln.cpp:1927-1981); the find_nams/rescue results come from the engine
-void align_PE_read_part(AlignTmpRes& res, const Record&, const Record&, const Read& read1, const Read& read2,
+void align_PE_read_part(AlignTmpRes& res, const RecView&, const RecView&, const Read& read1, const Read& read2,
                         std::vector<Nam> nams[2],
                         const bool rescued[2], AlignmentStatistics& stats, InsertSizeDistribution& isize,
                         const MapContext& mc, std::minstd_rand& rng, bool sorted) {
@@ -686,7 +686,7 @@ void align_PE_read_part(AlignTmpRes& res, const Record&, const Record&, const Re
 }
 
 // align_SE_part (aln.cpp:95-124)
-void align_SE_read_part(AlignTmpRes& res, const Record&, const Read& read, std::vector<Nam>& nams, bool rescued,
+void align_SE_read_part(AlignTmpRes& res, const RecView&, const Read& read, std::vector<Nam>& nams, bool rescued,
                         AlignmentStatistics& stats, const MapContext& mc, std::minstd_rand& rng) {
     Details det;
     if (mc.mparams.rescue_level > 1 && rescued) det.nam_rescue = true;
@@ -739,7 +739,7 @@ static void rescue_job(const Nam& nam, const Read& read, const References& refs,
     jobs.push_back(SwJob{r_tmp, nam.ref_id, (uint32_t)start, (uint32_t)len});
 }
 
-void collect_jobs_pe(AlignTmpRes& res, const Record&, const Record&, const Read& read1, const Read& read2,
+void collect_jobs_pe(AlignTmpRes& res, const RecView&, const RecView&, const Read& read1, const Read& read2,
                      const MapContext& mc, float mu, float sigma, std::vector<SwJob>& jobs) {
     const size_t n = res.todo_nams.size();
     auto rd = [&](size_t j) -> const Read& { return res.is_read1[j] ? read1 : read2; };
@@ -905,7 +905,7 @@ static void pick_random_top_pair(std::vector<ScoredAlignmentPair>& hs, std::mins
 
 // rescue_read_last (aln.cpp:1983-2081)
 static void rescue_read_last(AlignTmpRes& res, const Read& read2, const Read& read1, const MapContext& mc,
-                             Details det[2], float mu, float sigma, Sam& sam, const Record& rec1, const Record& rec2,
+                             Details det[2], float mu, float sigma, Sam& sam, const RecView& rec1, const RecView& rec2,
                              bool swap_r1r2, std::minstd_rand& rng) {
     RSA_TLS std::vector<Alignment> al1, al2;
     al1.clear();
@@ -952,7 +952,7 @@ static void rescue_read_last(AlignTmpRes& res, const Read& read2, const Read& re
 }
 
 // align_PE_read_last (aln.cpp:2083-2306)
-void align_PE_read_last(AlignTmpRes& res, const Record& rec1, const Record& rec2, const Read& read1, const Read& read2,
+void align_PE_read_last(AlignTmpRes& res, const RecView& rec1, const RecView& rec2, const Read& read1, const Read& read2,
                         Sam& sam,
                         AlignmentStatistics& stats, const InsertSizeDistribution& isize, const MapContext& mc,
                         std::minstd_rand& rng) {
@@ -1054,7 +1054,7 @@ void align_PE_read_last(AlignTmpRes& res, const Record& rec1, const Record& rec2
 }
 
 // align_SE_read_last (aln.cpp:126-238)
-void align_SE_read_last(AlignTmpRes& res, const Record& rec, const Read& read, Sam& sam, AlignmentStatistics& stats,
+void align_SE_read_last(AlignTmpRes& res, const RecView& rec, const Read& read, Sam& sam, AlignmentStatistics& stats,
                         const MapContext& mc, std::minstd_rand& rng) {
     Details det;
     if (res.type == 0) {

@@ -328,6 +328,7 @@ void rsam_reads_free(rsam_reads* r) { delete r; }
 
 struct SinkState {
     FILE* f = nullptr;
+    ~SinkState() { if (f) fclose(f); }   // an error path; the normal one closes and checks
 };
 
 static void sink_fn(void* user, const char* chunk, size_t bytes) {
@@ -335,58 +336,88 @@ static void sink_fn(void* user, const char* chunk, size_t bytes) {
     if (s->f) fwrite(chunk, 1, bytes, s->f);
 }
 
+static void fill_stats(const PipelineResult& res, rsam_stats* out) {
+    if (!out) return;
+    out->n_reads = res.stats.n_reads;
+    out->sam_bytes = res.sam_bytes;
+    out->sam_hash = res.sam_digest.h;
+    out->sw_calls = res.stats.tot_aligner_calls;
+    out->tried = res.stats.tot_all_tried;
+    out->nam_rescue = res.stats.nam_rescue;
+    out->mate_rescue = res.stats.tot_rescued;
+    out->inconsistent = res.stats.inconsistent_nams;
+    out->map_seconds = res.map_seconds;
+    out->t_seed = res.phases.seed;
+    out->t_extend = res.phases.extend;
+    out->t_part = res.phases.part;
+    out->t_collect = res.phases.collect;
+    out->t_last = res.phases.last;
+    out->t_sequential = res.phases.sequential;
+}
+
+// the pipeline over `src` with the SAM (header + body) to sam_path, or kept in memory
+// only when sam_path is empty; map_seconds covers opening the output to the last byte
+static int map_source(rsam* m, ReadSource& src, int threads, int chunk_size, const char* sam_path, rsam_stats* out,
+                      std::chrono::steady_clock::time_point t0) {
+    PcSampler sampler;
+    SinkState st;
+    if (sam_path && *sam_path) {
+        st.f = fopen(sam_path, "wb");
+        if (!st.f) throw std::runtime_error(std::string("cannot open ") + sam_path);
+        std::string hdr = sam_header(m->refs, "", {}, "rsalign (library)");
+        fwrite(hdr.data(), 1, hdr.size(), st.f);
+    }
+    MapContext mc{m->refs, m->idx.params, m->ap, m->mp};
+    PipelineOptions po;
+    po.threads = threads;
+    po.chunk_size = chunk_size;
+    po.digest = true;
+    SamSink sk = st.f ? sink_fn : nullptr;
+    PosSink ps;                                 // a regular file: chunks written in parallel at their offsets
+    if (st.f && pos_sink_open(st.f, ps)) {
+        po.sink_at = pos_sink_write;
+        po.sink_at_user = &ps;
+    }
+    PipelineResult res = src.paired() ? run_pipeline_pe(src, *m->eng, mc, po, sk, &st)
+                                      : run_pipeline_se(src, *m->eng, mc, po, sk, &st);
+    if (st.f) {
+        FILE* f = st.f;
+        st.f = nullptr;
+        if (fclose(f) != 0) throw std::runtime_error(std::string("write failed: ") + sam_path);
+    }
+    if (ps.failed) throw std::runtime_error(std::string("write failed: ") + sam_path);
+    res.map_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    fill_stats(res, out);
+    return 0;
+}
+
 int rsam_map(rsam* m, const rsam_reads* reads, int threads, int chunk_size, const char* sam_path, rsam_stats* out) {
     tune_malloc();
     if (!m || !reads) return -1;
-    PcSampler sampler;
     try {
-        SinkState st;
-        if (sam_path && *sam_path) {
-            st.f = fopen(sam_path, "wb");
-            if (!st.f) throw std::runtime_error(std::string("cannot open ") + sam_path);
-            std::string hdr = sam_header(m->refs, "", {}, "rsalign (library)");
-            fwrite(hdr.data(), 1, hdr.size(), st.f);
-        }
-        MapContext mc{m->refs, m->idx.params, m->ap, m->mp};
-        PipelineOptions po;
-        po.threads = threads;
-        po.chunk_size = chunk_size;
-        po.digest = true;
-        SamSink sk = st.f ? sink_fn : nullptr;
-        PosSink ps;                                 // a regular file: chunks written in parallel at their offsets
-        if (st.f && pos_sink_open(st.f, ps)) {
-            po.sink_at = pos_sink_write;
-            po.sink_at_user = &ps;
-        }
-        PipelineResult res;
-        if (!reads->interleaved.empty()) {          // pairs per chunk of 2 * chunk_size records (pc.cpp:38-107)
-            std::vector<Record> all(reads->interleaved), r1, r2;
-            distribute_interleaved(std::move(all), (size_t)std::max(1, chunk_size), r1, r2, po.chunk_starts);
-            res = run_pipeline_pe(r1, r2, *m->eng, mc, po, sk, &st);
-        } else {
-            res = reads->paired ? run_pipeline_pe(reads->r1, reads->r2, *m->eng, mc, po, sk, &st)
-                                : run_pipeline_se(reads->r1, *m->eng, mc, po, sk, &st);
-        }
-        if (st.f) fclose(st.f);
-        if (ps.failed) throw std::runtime_error(std::string("write failed: ") + sam_path);
-        if (out) {
-            out->n_reads = res.stats.n_reads;
-            out->sam_bytes = res.sam_bytes;
-            out->sam_hash = res.sam_digest.h;
-            out->sw_calls = res.stats.tot_aligner_calls;
-            out->tried = res.stats.tot_all_tried;
-            out->nam_rescue = res.stats.nam_rescue;
-            out->mate_rescue = res.stats.tot_rescued;
-            out->inconsistent = res.stats.inconsistent_nams;
-            out->map_seconds = res.map_seconds;
-            out->t_seed = res.phases.seed;
-            out->t_extend = res.phases.extend;
-            out->t_part = res.phases.part;
-            out->t_collect = res.phases.collect;
-            out->t_last = res.phases.last;
-            out->t_sequential = res.phases.sequential;
-        }
-        return 0;
+        const auto t0 = std::chrono::steady_clock::now();
+        const size_t chunk = (size_t)std::max(1, chunk_size);
+        // views into the read set: interleaved records are paired per chunk of
+        // 2 x chunk_size records (pc.cpp:38-107) as each chunk is taken, no copy
+        std::unique_ptr<ReadSource> src =
+            !reads->interleaved.empty() ? make_interleaved_vector_source(&reads->interleaved, chunk)
+                                        : make_vector_source(&reads->r1, reads->paired ? &reads->r2 : nullptr, chunk);
+        return map_source(m, *src, threads, chunk_size, sam_path, out, t0);
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+int rsam_map_files(rsam* m, const char* fq1, const char* fq2, int interleaved, int threads, int chunk_size,
+                   const char* sam_path, rsam_stats* out) {
+    tune_malloc();
+    if (!m || !fq1) return -1;
+    try {
+        const auto t0 = std::chrono::steady_clock::now();
+        std::unique_ptr<ReadSource> src = open_fastq_source(fq1, fq2 ? fq2 : "", interleaved != 0,
+                                                            (size_t)std::max(1, chunk_size));
+        return map_source(m, *src, threads, chunk_size, sam_path, out, t0);
     } catch (const std::exception& e) {
         g_err = e.what();
         return -1;

@@ -91,26 +91,26 @@ public:
         seed_batch(rb, rescue_level, rescue_cutoff, out);
     }
 
-    void seed(const std::vector<const std::string*>& reads, int rescue_level, unsigned rescue_cutoff,
+    void seed(const std::vector<std::string_view>& reads, int rescue_level, unsigned rescue_cutoff,
               SeedBatchOut& out) override {
         const size_t n = reads.size();
         const Lease ls = lease();
         Staging& sg = *ls.s;
         size_t tot = 0;
-        for (auto* r : reads) tot += r->size();
+        for (auto r : reads) tot += r.size();
         char* blob = sg.get<char>(Staging::READS, tot + 16);
         uint64_t* offs = sg.get<uint64_t>(Staging::ROFF, n);
         uint32_t* lens = sg.get<uint32_t>(Staging::RLEN, n);
         size_t pos = 0;
         for (size_t i = 0; i < n; ++i) {
             if (i + 8 < n) {                       // scattered heap strings: request them ahead
-                const char* a = reads[i + 8]->data();
-                for (size_t o = 0; o < reads[i + 8]->size(); o += 64) __builtin_prefetch(a + o);
+                const char* a = reads[i + 8].data();
+                for (size_t o = 0; o < reads[i + 8].size(); o += 64) __builtin_prefetch(a + o);
             }
             offs[i] = pos;
-            lens[i] = (uint32_t)reads[i]->size();
-            memcpy(blob + pos, reads[i]->data(), reads[i]->size());
-            pos += reads[i]->size();
+            lens[i] = (uint32_t)reads[i].size();
+            memcpy(blob + pos, reads[i].data(), reads[i].size());
+            pos += reads[i].size();
         }
         rsa_read_batch rb{blob, offs, lens, (uint32_t)n};
         seed_batch(rb, rescue_level, rescue_cutoff, out);

@@ -1,0 +1,381 @@
+// input.cpp -- read sources of the pipeline: records streamed from FASTQ/FASTA
+// files while mapping runs, or records already in memory.
+//
+// The reference's workers pull chunks of 10000 pairs from one InputBuffer under
+// a mutex (src/pc.cpp:74-107, called at pc.cpp:1574) while the other workers
+// map.  Here each input file has a reader thread that parses blocks of records
+// ahead of the pipeline (bounded: a few blocks past the last chunk asked for),
+// so resident memory is set by the pipeline's window, not by the input size.
+//
+// Uncompressed files in the plain 4-line layout (header / one sequence line /
+// '+' line / one quality line of the same length) are mapped and split in place:
+// a record is four views into the mapping, no byte is copied, and the mapping's
+// pages are dropped again when the chunk's SAM is written (ReadSource::release).
+// The first record that is not in that layout switches the file to FastxReader
+// (kseq++ semantics, io.cpp) from that record on: the plain records before it
+// are exactly what kseq returns for them, and kseq restarts cleanly at a record
+// header.  gzip input, pipes and FASTA go through FastxReader from the start.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <exception>
+#include <map>
+#include <mutex>
+#include <stdexcept>
+#include <thread>
+
+#include "rsa_host.hpp"
+
+namespace rsa {
+
+bool same_name(std::string_view n1, std::string_view n2) {      // pc.cpp:23-35
+    if (n1.length() != n2.length()) return false;
+    if (n1.length() <= 2) return n1 == n2;
+    size_t i = 0;
+    for (; i < n1.length() - 1; ++i)
+        if (n1[i] != n2[i]) return false;
+    if (n1[i - 1] == '/' && n1[i] == '1' && n2[i] == '2') return true;
+    return n1[i] == n2[i];
+}
+
+// distribute_interleaved (pc.cpp:38-72) on one block; lookahead1 is never set there
+size_t distribute_interleaved(const RecView* block, size_t n, std::vector<RecView>& r1, std::vector<RecView>& r2) {
+    size_t singles = 0;
+    for (size_t i = 0; i < n; ++i) {
+        if (i + 1 < n && same_name(block[i].name, block[i + 1].name)) {
+            r1.push_back(block[i]);
+            r2.push_back(block[i + 1]);
+            ++i;
+        } else {
+            singles++;
+        }
+    }
+    return singles;
+}
+
+namespace {
+
+// ------------------------------------------------------- records in memory --
+class VectorSource final : public ReadSource {
+public:
+    VectorSource(const std::vector<Record>* r1, const std::vector<Record>* r2, size_t chunk)
+        : r1_(r1), r2_(r2), chunk_(std::max<size_t>(1, chunk)) {
+        if (r2_ && r2_->size() != r1_->size()) throw std::runtime_error("read files have different record counts");
+    }
+    bool paired() const override { return r2_ != nullptr; }
+    bool get(size_t idx, InputChunk& out) override {
+        out.clear();
+        out.index = idx;
+        const size_t b = idx * chunk_;
+        if (b >= r1_->size()) return false;
+        const size_t e = std::min(r1_->size(), b + chunk_);
+        out.r1.assign(r1_->begin() + (long)b, r1_->begin() + (long)e);
+        if (r2_) out.r2.assign(r2_->begin() + (long)b, r2_->begin() + (long)e);
+        return true;
+    }
+private:
+    const std::vector<Record>* r1_;
+    const std::vector<Record>* r2_;
+    size_t chunk_;
+};
+
+class InterleavedVectorSource final : public ReadSource {
+public:
+    InterleavedVectorSource(const std::vector<Record>* recs, size_t chunk)
+        : recs_(recs), block_(2 * std::max<size_t>(1, chunk)) {}
+    bool paired() const override { return true; }
+    bool get(size_t idx, InputChunk& out) override {
+        out.clear();
+        out.index = idx;
+        const size_t b = idx * block_;
+        if (b >= recs_->size()) return false;
+        const size_t e = std::min(recs_->size(), b + block_);
+        std::vector<RecView>& tmp = scratch();
+        tmp.assign(recs_->begin() + (long)b, recs_->begin() + (long)e);
+        out.singletons = distribute_interleaved(tmp.data(), tmp.size(), out.r1, out.r2);
+        return true;
+    }
+private:
+    static std::vector<RecView>& scratch() {
+        static thread_local std::vector<RecView> v;
+        return v;
+    }
+    const std::vector<Record>* recs_;
+    size_t block_;
+};
+
+// ------------------------------------------------------------ FASTQ files --
+struct MappedFile {
+    const char* p = nullptr;
+    size_t n = 0;
+    int fd = -1;
+    ~MappedFile() { reset(); }
+    void reset() {
+        if (p && n) munmap((void*)p, n);
+        if (fd >= 0) close(fd);
+        p = nullptr;
+        n = 0;
+        fd = -1;
+    }
+    // a regular, uncompressed, non-empty file; false leaves the caller on the sequential reader
+    bool open_map(const std::string& path) {
+        if (path == "-") return false;
+        fd = ::open(path.c_str(), O_RDONLY);
+        if (fd < 0) return false;
+        struct stat st;
+        if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode) || st.st_size < 2) return false;
+        void* q = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (q == MAP_FAILED) return false;
+        p = (const char*)q;
+        n = (size_t)st.st_size;
+        if ((unsigned char)p[0] == 0x1f && (unsigned char)p[1] == 0x8b) return false;   // gzip
+        return true;
+    }
+};
+
+inline std::string_view strip_cr(std::string_view l) {
+    if (!l.empty() && l.back() == '\r') l.remove_suffix(1);
+    return l;
+}
+
+// One record of the plain layout at p, as views; false (p unchanged) when the
+// bytes at p are anything else.  The conditions are those under which kseq's
+// record (FastxReader::next) is exactly header / sequence line / quality line:
+//  - the record starts with '@' and has four lines;
+//  - the third line starts with '+';
+//  - the sequence line is not empty and does not start with '>', '@', '+' or '\r'
+//    (kseq would end the sequence there); kseq strips one '\r' from the line after
+//    its first byte, then trailing blanks;
+//  - the quality line (one '\r' stripped) is as long as the sequence, so kseq
+//    stops reading quality after it.
+bool plain_record(const char*& p, const char* end, RecView& r) {
+    if (p >= end || *p != '@') return false;
+    const char* q = p;
+    std::string_view line[4];
+    for (int k = 0; k < 4; ++k) {
+        if (q >= end) return false;
+        const char* nl = (const char*)memchr(q, '\n', (size_t)(end - q));
+        const char* le = nl ? nl : end;
+        line[k] = std::string_view(q, (size_t)(le - q));
+        q = nl ? nl + 1 : end;
+    }
+    if (line[2].empty() || line[2][0] != '+') return false;
+    std::string_view sq = line[1];
+    if (sq.empty()) return false;
+    if (sq.size() >= 2 && sq.back() == '\r') sq.remove_suffix(1);
+    const char c0 = sq[0];
+    if (c0 == '>' || c0 == '@' || c0 == '+' || c0 == '\r') return false;
+    while (!sq.empty() && (sq.back() == ' ' || sq.back() == '\t')) sq.remove_suffix(1);
+    const std::string_view ql = strip_cr(line[3]);
+    if (sq.empty() || ql.size() != sq.size()) return false;
+    std::string_view h = strip_cr(line[0].substr(1));
+    size_t ws = 0;
+    while (ws < h.size() && h[ws] != ' ' && h[ws] != '\t' && h[ws] != '\v' && h[ws] != '\f' && h[ws] != '\r') ++ws;
+    r.name = h.substr(0, ws);
+    size_t cs = ws;
+    while (cs < h.size() && (h[cs] == ' ' || h[cs] == '\t' || h[cs] == '\v' || h[cs] == '\f' || h[cs] == '\r')) ++cs;
+    r.comment = h.substr(cs);
+    r.seq = sq;
+    r.qual = ql;
+    p = q;
+    return true;
+}
+
+struct Block {
+    std::vector<RecView> recs;
+    std::vector<Record> owned;                  // records of the sequential reader (recs view them)
+    const char* map_begin = nullptr;            // mapped bytes the views use
+    size_t map_len = 0;
+};
+
+// The blocks of `per_block` records of one file, read by a thread of its own at
+// most `ahead` blocks past the highest block asked for.
+class FileBlocks {
+public:
+    FileBlocks(const std::string& path, size_t per_block, size_t ahead)
+        : path_(path), per_block_(std::max<size_t>(1, per_block)), ahead_(std::max<size_t>(1, ahead)) {
+        if (!mf_.open_map(path_)) {
+            mf_.reset();
+            seq_.reset(new FastxReader(path_));   // throws when the file cannot be opened
+        }
+        th_ = std::thread([this] { run(); });
+    }
+    ~FileBlocks() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        th_.join();
+    }
+    // block idx, waiting for the reader; false past the end of the file
+    bool take(size_t idx, Block& out) {
+        std::unique_lock<std::mutex> g(m_);
+        if (idx + 1 > horizon_) {
+            horizon_ = idx + 1;
+            cv_.notify_all();
+        }
+        cv_.wait(g, [&] { return err_ || blocks_.count(idx) || (finished_ && idx >= produced_); });
+        if (err_) std::rethrow_exception(err_);
+        auto it = blocks_.find(idx);
+        if (it == blocks_.end()) return false;
+        out = std::move(it->second);
+        blocks_.erase(it);
+        return true;
+    }
+    // the pages of a released block's bytes leave this process (the file stays
+    // mapped; a page a neighbouring block still reads is faulted in again)
+    static void drop(const char* p, size_t n) {
+        if (!p || !n) return;
+        const uintptr_t pg = 4096;
+        const uintptr_t a = (uintptr_t)p & ~(pg - 1), b = ((uintptr_t)p + n) & ~(pg - 1);
+        if (b > a) madvise((void*)a, b - a, MADV_DONTNEED);
+    }
+
+private:
+    void run() {
+        try {
+            for (;;) {
+                {
+                    std::unique_lock<std::mutex> g(m_);
+                    cv_.wait(g, [&] { return stop_ || produced_ < horizon_ + ahead_; });
+                    if (stop_) return;
+                }
+                Block b;
+                read_block(b);
+                std::lock_guard<std::mutex> g(m_);
+                if (b.recs.empty()) {
+                    finished_ = true;
+                    cv_.notify_all();
+                    return;
+                }
+                blocks_.emplace(produced_++, std::move(b));
+                cv_.notify_all();
+            }
+        } catch (...) {
+            std::lock_guard<std::mutex> g(m_);
+            err_ = std::current_exception();
+            cv_.notify_all();
+        }
+    }
+    void read_block(Block& b) {
+        b.recs.reserve(per_block_);
+        if (!seq_) {
+            const char* end = mf_.p + mf_.n;
+            const char* p = mf_.p + pos_;
+            b.map_begin = p;
+            RecView r;
+            while (b.recs.size() < per_block_ && p < end && plain_record(p, end, r)) b.recs.push_back(r);
+            b.map_len = (size_t)(p - b.map_begin);
+            pos_ = (size_t)(p - mf_.p);
+            if (b.recs.size() == per_block_ || p >= end) return;
+            // not the plain layout from here on: kseq over the rest of the mapped bytes
+            seq_.reset(new FastxReader(p, (size_t)(end - p)));
+        }
+        const size_t want = per_block_ - b.recs.size();
+        b.owned.reserve(want);
+        Record r;
+        while (b.owned.size() < want && seq_->next(r)) {
+            b.owned.push_back(std::move(r));
+            r = Record();
+        }
+        for (const Record& x : b.owned) b.recs.push_back(RecView(x));
+    }
+
+    std::string path_;
+    size_t per_block_, ahead_;
+    MappedFile mf_;
+    size_t pos_ = 0;                            // mapped mode: next record's offset
+    std::unique_ptr<FastxReader> seq_;          // sequential mode
+    std::thread th_;
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::map<size_t, Block> blocks_;
+    size_t produced_ = 0, horizon_ = 0;
+    bool finished_ = false, stop_ = false;
+    std::exception_ptr err_;
+};
+
+class FastqSource final : public ReadSource {
+public:
+    FastqSource(const std::string& p1, const std::string& p2, bool interleaved, size_t chunk)
+        : interleaved_(interleaved && p2.empty()) {
+        const size_t per = (interleaved_ ? 2 : 1) * std::max<size_t>(1, chunk);
+        constexpr size_t kAhead = 4;
+        f1_.reset(new FileBlocks(p1, per, kAhead));
+        if (!p2.empty()) f2_.reset(new FileBlocks(p2, per, kAhead));
+    }
+    bool paired() const override { return f2_ != nullptr || interleaved_; }
+    bool get(size_t idx, InputChunk& out) override {
+        out.clear();
+        out.index = idx;
+        Block b1, b2;
+        const bool h1 = f1_->take(idx, b1);
+        if (f2_) {
+            const bool h2 = f2_->take(idx, b2);
+            if (h1 != h2 || b1.recs.size() != b2.recs.size())
+                throw std::runtime_error("read files have different record counts");
+            if (!h1) return false;
+            out.r1 = std::move(b1.recs);
+            out.r2 = std::move(b2.recs);
+            keep(b1, out.owned1, out);
+            keep(b2, out.owned2, out);
+            return true;
+        }
+        if (!h1) return false;
+        if (interleaved_) {
+            out.singletons = distribute_interleaved(b1.recs.data(), b1.recs.size(), out.r1, out.r2);
+        } else {
+            out.r1 = std::move(b1.recs);
+        }
+        keep(b1, out.owned1, out);
+        return true;
+    }
+    void release(InputChunk& c) override {
+        for (auto& m : c.mapped) FileBlocks::drop(m.first, m.second);
+        c.clear();
+    }
+
+private:
+    static void keep(Block& b, std::vector<Record>& owned, InputChunk& out) {
+        owned = std::move(b.owned);             // the vector's buffer moves, the records stay put
+        if (b.map_len) out.mapped.emplace_back(b.map_begin, b.map_len);
+    }
+    bool interleaved_;
+    std::unique_ptr<FileBlocks> f1_, f2_;
+};
+
+}  // namespace
+
+std::unique_ptr<ReadSource> make_vector_source(const std::vector<Record>* r1, const std::vector<Record>* r2,
+                                               size_t chunk_size) {
+    return std::unique_ptr<ReadSource>(new VectorSource(r1, r2, chunk_size));
+}
+
+std::unique_ptr<ReadSource> make_interleaved_vector_source(const std::vector<Record>* recs, size_t chunk_size) {
+    return std::unique_ptr<ReadSource>(new InterleavedVectorSource(recs, chunk_size));
+}
+
+std::unique_ptr<ReadSource> open_fastq_source(const std::string& path1, const std::string& path2, bool interleaved,
+                                              size_t chunk_size) {
+    return std::unique_ptr<ReadSource>(new FastqSource(path1, path2, interleaved, chunk_size));
+}
+
+int estimate_read_length(const std::string& path1, const std::string& path2, bool interleaved) {
+    if (path1 == "-" || path2 == "-") return 150;   // a stream cannot be read twice: the default profile
+    uint64_t tot = 0, num = 0;
+    auto scan = [&](const std::string& p, size_t want) {
+        FastxReader in(p);
+        Record r;
+        for (size_t i = 0; i < want && in.next(r); ++i) { tot += r.seq.size(); num++; }
+    };
+    scan(path1, interleaved ? 1000 : 500);
+    if (!path2.empty()) scan(path2, 500);
+    return num ? (int)(tot / num) : 150;
+}
+
+}  // namespace rsa

@@ -2,6 +2,7 @@
 // Restated from src/cigar.cpp, src/sam.cpp, src/refs.cpp, src/index.cpp,
 // src/indexparameters.cpp and the kseq++ record semantics used by src/fastq.cpp.
 #include <fcntl.h>
+#include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -119,10 +120,10 @@ void Cigar::to_m_string(std::string& out) const {
 }
 
 // ------------------------------------------------------------------- SAM --
-static std::string_view strip_suffix(const std::string& name) {   // sam.cpp:29-40
+static std::string_view strip_suffix(std::string_view name) {   // sam.cpp:29-40
     size_t len = name.size();
     if (len >= 2 && name[len - 2] == '/' && (name[len - 1] == '1' || name[len - 1] == '2'))
-        return std::string_view(name).substr(0, len - 2);
+        return name.substr(0, len - 2);
     return name;
 }
 
@@ -150,7 +151,7 @@ static char* put_details(char* p, const Details& d, bool paired) {   // sam.cpp:
 }
 static const size_t kDetailsBound = 5 * (6 + 20);
 
-void Sam::add_unmapped(const Record& r, uint16_t flags) {   // sam.cpp:77-92
+void Sam::add_unmapped(const RecView& r, uint16_t flags) {   // sam.cpp:77-92
     if (!output_unmapped_) return;
     const std::string_view name = strip_suffix(r.name);
     size_t at;
@@ -167,7 +168,7 @@ void Sam::add_unmapped(const Record& r, uint16_t flags) {   // sam.cpp:77-92
     sam_trim(out_, at, p0, p);
 }
 
-void Sam::add_unmapped_mate(const Record& r, uint16_t flags, std::string_view mate_ref, uint32_t mate_pos) {
+void Sam::add_unmapped_mate(const RecView& r, uint16_t flags, std::string_view mate_ref, uint32_t mate_pos) {
     const std::string_view name = strip_suffix(r.name);      // sam.cpp:94-116
     size_t at;
     char* const p0 =
@@ -190,12 +191,12 @@ void Sam::add_unmapped_mate(const Record& r, uint16_t flags, std::string_view ma
     sam_trim(out_, at, p0, p);
 }
 
-void Sam::add_unmapped_pair(const Record& r1, const Record& r2) {
+void Sam::add_unmapped_pair(const RecView& r1, const RecView& r2) {
     add_unmapped(r1, 1 | 4 | 8 | 0x40);
     add_unmapped(r2, 1 | 4 | 8 | 0x80);
 }
 
-void Sam::add(const Alignment& a, const Record& r, std::string_view rc, uint8_t mapq, bool primary,
+void Sam::add(const Alignment& a, const RecView& r, std::string_view rc, uint8_t mapq, bool primary,
               const Details& d) {                               // sam.cpp:124-139
     int flags = 0;
     if (!a.is_unaligned && a.is_rc) flags |= 0x10;
@@ -224,9 +225,9 @@ static char* put_cigar(char* p, const Cigar& c, bool eqx) {
     return p;
 }
 
-void Sam::add_record(const std::string& qname, uint16_t flags, std::string_view rname, uint32_t pos, uint8_t mapq,
+void Sam::add_record(std::string_view qname, uint16_t flags, std::string_view rname, uint32_t pos, uint8_t mapq,
                      const Cigar& cigar, std::string_view mate_rname, uint32_t mate_pos, int32_t tlen,
-                     std::string_view seq, std::string_view seq_rc, const std::string& qual, int ed, int score,
+                     std::string_view seq, std::string_view seq_rc, std::string_view qual, int ed, int score,
                      const Details& d) {                        // sam.cpp:141-213
     const std::string_view name = strip_suffix(qname);
     // upper bound of the record: fixed fields + numbers + CIGAR (<= 11 chars an op) + SEQ/QUAL + tags
@@ -277,7 +278,7 @@ void Sam::add_record(const std::string& qname, uint16_t flags, std::string_view 
     sam_trim(out_, at, p0, p);
 }
 
-void Sam::add_pair(const Alignment& a1, const Alignment& a2, const Record& r1, const Record& r2, std::string_view rc1,
+void Sam::add_pair(const Alignment& a1, const Alignment& a2, const RecView& r1, const RecView& r2, std::string_view rc1,
                    std::string_view rc2, uint8_t mapq1, uint8_t mapq2, bool proper, bool primary,
                    const Details d[2]) {                        // sam.cpp:215-313
     int f1 = 1 | 0x40, f2 = 1 | 0x80;
@@ -670,6 +671,8 @@ struct FastxReader::Impl {
     // block reader: 4 MB gzread()s, lines found with memchr; a line is a view
     // into the buffer, valid until the next refill
     gzFile f = nullptr;
+    const char* mem = nullptr;            // memory mode: bytes [mem_pos, mem_len) still to read
+    size_t mem_len = 0, mem_pos = 0;
     std::vector<char> buf;
     size_t pos = 0, len = 0;
     bool eof = false;
@@ -682,9 +685,17 @@ struct FastxReader::Impl {
             pos = 0;
         }
         if (len == buf.size()) buf.resize(buf.size() * 2);
-        const int n = gzread(f, buf.data() + len, (unsigned)(buf.size() - len));
-        if (n <= 0) { eof = true; return false; }
-        len += (size_t)n;
+        size_t n = 0;
+        if (f) {
+            const int r = gzread(f, buf.data() + len, (unsigned)(buf.size() - len));
+            n = r > 0 ? (size_t)r : 0;
+        } else {
+            n = std::min(buf.size() - len, mem_len - mem_pos);
+            memcpy(buf.data() + len, mem + mem_pos, n);
+            mem_pos += n;
+        }
+        if (n == 0) { eof = true; return false; }
+        len += n;
         return true;
     }
     int getc() {
@@ -723,6 +734,12 @@ FastxReader::FastxReader(const std::string& path) : impl_(new Impl) {
     if (!impl_->f) throw std::runtime_error("Could not open FASTQ file: " + path);
     impl_->buf.resize(4 << 20);
     (void)gzbuffer(impl_->f, 1 << 20);
+}
+
+FastxReader::FastxReader(const char* mem, size_t len) : impl_(new Impl) {
+    impl_->mem = mem;
+    impl_->mem_len = len;
+    impl_->buf.resize(1 << 20);
 }
 
 FastxReader::~FastxReader() { if (impl_->f) gzclose(impl_->f); }
@@ -900,9 +917,13 @@ bool parse_parallel(const std::string& path, int threads, std::vector<Record>& o
     return true;
 }
 
+// the CPUs this process may run on (its affinity mask: a rank's share of the node), at most 16
 int reader_threads() {
-    const unsigned hc = std::thread::hardware_concurrency();
-    return (int)std::max(1u, std::min(16u, hc));
+    cpu_set_t cs;
+    int n = 0;
+    if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = CPU_COUNT(&cs);
+    if (n <= 0) n = (int)std::thread::hardware_concurrency();
+    return std::max(1, std::min(16, n));
 }
 
 }  // namespace
@@ -949,6 +970,15 @@ bool pos_sink_open(FILE* f, PosSink& ps) {
     if (fd < 0) return false;
     struct stat st;
     if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode)) return false;    // pipes, terminals: sequential
+    // O_APPEND: pwrite ignores the offset and appends, so chunks would land in the order
+    // they finish (`>> out.sam`); the sequential sink keeps chunk order there
+    const int fl = fcntl(fd, F_GETFL);
+    if (fl < 0 || (fl & O_APPEND)) return false;
+    // stderr on the same file (`> out.sam 2>&1`): pwrite does not move the shared offset,
+    // so a message on stderr would land inside the SAM body; stay sequential
+    struct stat se;
+    if (fd != STDERR_FILENO && fstat(STDERR_FILENO, &se) == 0 && se.st_dev == st.st_dev && se.st_ino == st.st_ino)
+        return false;
     const off_t at = lseek(fd, 0, SEEK_CUR);
     if (at < 0) return false;
     ps.fd = fd;

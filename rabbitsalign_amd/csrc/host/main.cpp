@@ -120,26 +120,7 @@ int cli_main(int argc, char** argv, EngineFactory factory, const char* prog) {
             throw std::runtime_error("Cannot specify both --interleaved and specify two read files");
         // read length (main.cpp:254-258, readlen.cpp:16-29: average over the first read_records(500):
         // 500 records of each file, or the first 1000 records of an interleaved file)
-        std::vector<Record> recs1, recs2;
-        std::vector<size_t> chunk_starts;
-        size_t singletons = 0;
-        if (!o.reads1.empty() && !index_cmd) {
-            if (o.reads2.empty()) recs1 = FastxReader::read_all(o.reads1);
-            else FastxReader::read_pair(o.reads1, o.reads2, recs1, recs2);
-            if (!o.r_set) {
-                uint64_t tot = 0, num = 0;
-                const size_t first = o.interleaved ? 1000 : 500;
-                for (size_t i = 0; i < std::min<size_t>(first, recs1.size()); ++i) { tot += recs1[i].seq.size(); num++; }
-                for (size_t i = 0; i < std::min<size_t>(500, recs2.size()); ++i) { tot += recs2[i].seq.size(); num++; }
-                o.r = num ? (int)(tot / num) : 150;
-            }
-            if (o.interleaved) {
-                std::vector<Record> all;
-                all.swap(recs1);
-                singletons = distribute_interleaved(std::move(all), (size_t)std::max(1, o.chunk_size), recs1, recs2,
-                                                    chunk_starts);
-            }
-        }
+        if (!o.reads1.empty() && !index_cmd && !o.r_set) o.r = estimate_read_length(o.reads1, o.reads2, o.interleaved);
         IndexParameters ip = IndexParameters::from_read_length(o.r, o.k, o.s, o.l, o.u, o.c, o.m);
         auto t0 = std::chrono::steady_clock::now();
         References refs = References::from_fasta(o.ref);
@@ -189,17 +170,23 @@ int cli_main(int argc, char** argv, EngineFactory factory, const char* prog) {
         MapContext mc{refs, idx.params, ap, mp};
         PipelineOptions po;
         po.threads = o.threads; po.chunk_size = o.chunk_size; po.rg_id = o.rg_id;
-        po.chunk_starts = std::move(chunk_starts);
+        if (o.verbose) fprintf(stderr, "[%s] mapping %s%s%s%s\n", prog, o.reads1.c_str(), o.reads2.empty() ? "" : " + ",
+                               o.reads2.c_str(), o.interleaved ? " (interleaved)" : "");
         PosSink ps;                                 // a regular file: chunks written in parallel at their offsets
         if (pos_sink_open(out, ps)) {
             po.sink_at = pos_sink_write;
             po.sink_at_user = &ps;
         }
+        // the reads are streamed: a reader thread per file parses chunks while the
+        // workers map (InputBuffer::read_records, pc.cpp:74-107)
+        std::unique_ptr<ReadSource> src =
+            open_fastq_source(o.reads1, o.reads2, o.interleaved, (size_t)std::max(1, o.chunk_size));
+        PipelineResult res = src->paired() ? run_pipeline_pe(*src, *eng, mc, po, write_sink, out)
+                                           : run_pipeline_se(*src, *eng, mc, po, write_sink, out);
+        src.reset();
         if (o.interleaved && o.verbose)
-            fprintf(stderr, "[%s] interleaved input: %zu pairs, %zu unpaired records (not mapped, as in the "
-                            "reference's paired-end task)\n", prog, recs1.size(), singletons);
-        PipelineResult res = (recs2.empty() && !o.interleaved) ? run_pipeline_se(recs1, *eng, mc, po, write_sink, out)
-                                                               : run_pipeline_pe(recs1, recs2, *eng, mc, po, write_sink, out);
+            fprintf(stderr, "[%s] interleaved input: %lu unpaired records (not mapped, as in the reference's "
+                            "paired-end task)\n", prog, (unsigned long)res.singletons);
         if (ps.fd >= 0) {                            // the stream's position trails the positional writes
             if (fseeko(out, 0, SEEK_END) != 0) throw std::runtime_error("cannot seek the output");
         }

@@ -46,7 +46,7 @@ public:
     }
     const char* name() const override { return name_.c_str(); }
     bool offloads() const override { return e_[0]->offloads(); }
-    void seed(const std::vector<const std::string*>& reads, int rescue_level, unsigned rescue_cutoff,
+    void seed(const std::vector<std::string_view>& reads, int rescue_level, unsigned rescue_cutoff,
               SeedBatchOut& out) override {
         Hold h(*this);
         e_[h.i]->seed(reads, rescue_level, rescue_cutoff, out);

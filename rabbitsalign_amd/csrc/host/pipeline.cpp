@@ -77,8 +77,6 @@ struct Unslot {                   // the slot handed back for a blocking section
 // +0 9.0/8.8, +8 9.4, +16 8.3 Mreads/s; on the r26 code +4 14.4/14.8, +8
 // 15.7/15.5, +12 15.8/16.3; r27: +12 17.2/17.6, +16 15.9/16.1, +20 15.9/15.7
 // -- none for an engine computing in-thread)
-// chunks per extend call (A/B on the box: see DESIGN.md §5)
-constexpr int kDefaultExtGroup = 1;
 
 static int wait_workers(const Engine& eng, int threads) {
     const char* e = getenv("RSA_WAIT_WORKERS");
@@ -177,20 +175,20 @@ struct OrderedSink {
 };
 
 struct PeChunk {
-    size_t index = 0, begin = 0, end = 0;
-    // the chunk's records as upper-cased (pc.cpp:1586-1587): the input record
-    // itself when upper-casing would not change it, else an upper-cased copy
-    std::vector<const Record*> r1, r2;
-    std::deque<Record> owned;
-    // both mates' (upper-cased) sequences back to back, read 2i + m at seqoff[2i + m], in
-    // memory the engine can DMA from (Engine::io_alloc): the seeding call takes them as is
+    InputChunk in;                            // the source's records; in.r1/in.r2[i].seq upper-cased by pe_load
+    const std::vector<RecView>& r1() const { return in.r1; }
+    const std::vector<RecView>& r2() const { return in.r2; }
+    size_t size() const { return in.r1.size(); }
+    // both mates' upper-cased sequences (pc.cpp:1586-1587) back to back, read 2i + m at
+    // seqoff[2i + m]; in memory the engine can DMA from (Engine::io_alloc) when it has one,
+    // and the seeding call then takes them as is
     std::vector<char, HostAlloc<char>> seqbuf;
     std::vector<uint64_t> seqoff;
     std::vector<uint32_t> seqlen;
     SamText rcbuf;                            // reverse complements of both mates, computed once (resize: no fill):
     std::vector<uint64_t> rcoff;              // read i mate m at rcoff[2i+m] (length = read length)
     std::string_view rc(size_t i, int m) const {
-        const Record& r = m ? *r2[i] : *r1[i];
+        const RecView& r = m ? in.r2[i] : in.r1[i];
         return std::string_view(rcbuf.data() + rcoff[2 * i + m], r.seq.size());
     }
     std::vector<AlignTmpRes> res;
@@ -308,33 +306,19 @@ ChunkPool& chunk_pool() {
     return *p;
 }
 
-// to_uppercase (c & ~32) leaves s unchanged iff no byte has bit 5 set
-static bool upper_already(const std::string& s) {
-    uint64_t acc = 0;
-    size_t i = 0;
-    for (; i + 8 <= s.size(); i += 8) {
-        uint64_t w;
-        memcpy(&w, s.data() + i, 8);
-        acc |= w;
-    }
-    for (; i < s.size(); ++i) acc |= (unsigned char)s[i];
-    return (acc & 0x2020202020202020ULL) == 0;
-}
-
-// Each read's name, sequence and qualities are separate heap strings the
-// hardware prefetcher cannot follow: loading a chunk (sequences) and writing its
-// SAM records (all three, last touched at load) request them a few pairs ahead.
+// Each read's name, sequence and qualities may sit anywhere (a caller's heap
+// strings, a mapped file): loading a chunk (sequences) and writing its SAM
+// records (all three) request them a few pairs ahead.
 static size_t rec_ahead() {                 // RSA_PREFETCH_AHEAD, default 4 pairs
     static const size_t d = getenv("RSA_PREFETCH_AHEAD") ? (size_t)std::max(1, atoi(getenv("RSA_PREFETCH_AHEAD"))) : 4;
     return d;
 }
-static inline void prefetch_str(const std::string& s) {
+static inline void prefetch_str(std::string_view s) {
     const char* p = s.data();
     for (size_t o = 0; o < s.size(); o += 64) __builtin_prefetch(p + o);
 }
-static inline void prefetch_record(const Record& r) {
+static inline void prefetch_record(const RecView& r) {
     prefetch_str(r.name);
-    prefetch_str(r.seq);
     prefetch_str(r.qual);
 }
 template <class T>
@@ -350,117 +334,80 @@ static inline void prefetch_res(const AlignTmpRes& r) {
     prefetch_vec(r.type4_nams);
 }
 
-void pe_load(PeChunk& c, const std::vector<Record>& a, const std::vector<Record>& b, size_t idx, size_t chunk,
-             const std::vector<size_t>& starts, const HostAllocFns* io) {
-    c.index = idx;
-    c.owned.clear();
+// to_uppercase (refs.cpp:10-16, c & ~32) of n bytes into dst
+static inline void upper_into(const char* src, size_t n, char* dst) {
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        memcpy(&w, src + i, 8);
+        w &= ~0x2020202020202020ULL;
+        memcpy(dst + i, &w, 8);
+    }
+    for (; i < n; ++i) dst[i] = (char)((unsigned char)src[i] & ~32);
+}
+
+// Chunk idx from the source, with both mates' sequences upper-cased into one
+// buffer (the chunk's record views then point there) and their reverse
+// complements computed once.  False past the end of the input.
+bool pe_load(PeChunk& c, ReadSource& src, size_t idx, const HostAllocFns* io) {
     c.stats = AlignmentStatistics();
     c.times = PhaseTimes();
-    c.begin = starts.empty() ? std::min(a.size(), idx * chunk) : starts[idx];
-    c.end = starts.empty() ? std::min(a.size(), c.begin + chunk) : starts[idx + 1];
-    const size_t n = c.end - c.begin;
-    c.r1.resize(n);
-    c.r2.resize(n);
-    auto take = [&](const Record& r) -> const Record* {
-        if (upper_already(r.seq)) return &r;
-        c.owned.push_back(r);
-        to_uppercase(c.owned.back().seq);
-        return &c.owned.back();
-    };
+    if (!src.get(idx, c.in)) return false;
+    const size_t n = c.size();
     size_t tot = 0;
-    for (size_t i = 0; i < n; ++i) tot += a[c.begin + i].seq.size() + b[c.begin + i].seq.size();
+    for (size_t i = 0; i < n; ++i) tot += c.in.r1[i].seq.size() + c.in.r2[i].seq.size();
     c.rcbuf.resize(tot);
     c.rcoff.resize(2 * n);
-    if (io) {
-        if (c.seqbuf.get_allocator().fns != io) c.seqbuf = decltype(c.seqbuf)(HostAlloc<char>(io));
-        c.seqbuf.resize(tot + 16);
-        c.seqoff.resize(2 * n);
-        c.seqlen.resize(2 * n);
-    }
+    if (c.seqbuf.get_allocator().fns != io) c.seqbuf = decltype(c.seqbuf)(HostAlloc<char>(io));
+    c.seqbuf.resize(tot + 16);
+    c.seqoff.resize(2 * n);
+    c.seqlen.resize(2 * n);
     size_t at = 0;
     const size_t ahead = rec_ahead();
     // one pass: the reverse complement is taken while the sequence is in cache
     for (size_t i = 0; i < n; ++i) {
         if (i + ahead < n) {
-            prefetch_str(a[c.begin + i + ahead].seq);
-            prefetch_str(b[c.begin + i + ahead].seq);
+            prefetch_str(c.in.r1[i + ahead].seq);
+            prefetch_str(c.in.r2[i + ahead].seq);
         }
-        c.r1[i] = take(a[c.begin + i]);
-        c.r2[i] = take(b[c.begin + i]);
         for (int m = 0; m < 2; ++m) {
-            const std::string& sq = m ? c.r2[i]->seq : c.r1[i]->seq;
+            RecView& r = m ? c.in.r2[i] : c.in.r1[i];
+            const size_t len = r.seq.size();
+            char* up = c.seqbuf.data() + at;
+            upper_into(r.seq.data(), len, up);
+            r.seq = std::string_view(up, len);
+            c.seqoff[2 * i + m] = at;
+            c.seqlen[2 * i + m] = (uint32_t)len;
             c.rcoff[2 * i + m] = at;
-            reverse_complement_into(sq, &c.rcbuf[at]);
-            if (io) {
-                memcpy(c.seqbuf.data() + at, sq.data(), sq.size());
-                c.seqoff[2 * i + m] = at;
-                c.seqlen[2 * i + m] = (uint32_t)sq.size();
-            }
-            at += sq.size();
+            reverse_complement_into(r.seq, &c.rcbuf[at]);
+            at += len;
         }
     }
     if (c.res.size() > n) c.res.resize(n);
     for (auto& r : c.res) r.reset();       // recycled chunk: per-pair vectors keep their capacity
     c.res.resize(n);
+    return true;
 }
 
 // Seeding of a loaded chunk (randstrobes + find_nams + rescue on the engine).
 // Independent of the insert-size state, so it can run ahead of part().
 void pe_seed(PeChunk& c, Engine& eng, const MapContext& mc, CpuSlots& slots) {
-    const size_t n = c.r1.size();
-    if (n == 0) return;
-    if (eng.io_alloc() && c.seqoff.size() == 2 * n) {     // packed by pe_load in DMA-able memory
-        const auto t = Clock::now();
+    const size_t n = c.size();
+    if (n == 0) { c.seeds.clear(); return; }
+    const auto t = Clock::now();
+    if (eng.io_alloc()) {                     // packed by pe_load in DMA-able memory
         Unslot u(slots, eng.offloads());
         eng.seed_packed(c.seqbuf.data(), c.seqoff.data(), c.seqlen.data(), 2 * n, mc.mparams.rescue_level,
                         (unsigned)mc.mparams.rescue_cutoff, c.seeds);
         c.times.seed += since(t);
         return;
     }
-    std::vector<const std::string*> reads;
+    std::vector<std::string_view> reads;
     reads.reserve(2 * n);
-    for (size_t i = 0; i < n; ++i) { reads.push_back(&c.r1[i]->seq); reads.push_back(&c.r2[i]->seq); }
-    const auto t = Clock::now();
+    for (size_t i = 0; i < n; ++i) { reads.push_back(c.in.r1[i].seq); reads.push_back(c.in.r2[i].seq); }
     Unslot u(slots, eng.offloads());
     eng.seed(reads, mc.mparams.rescue_level, (unsigned)mc.mparams.rescue_cutoff, c.seeds);
     c.times.seed += since(t);
-}
-
-// Seeding of several loaded chunks in one engine call (larger, fuller kernels,
-// fewer launches); the output is split back per chunk.  Seeding is a pure
-// function of each read, so the batching is invisible in the results.
-void pe_seed_multi(std::vector<PeChunk*>& cs, Engine& eng, const MapContext& mc, CpuSlots& slots) {
-    if (cs.size() == 1) { pe_seed(*cs[0], eng, mc, slots); return; }
-    std::vector<const std::string*> reads;
-    size_t tot = 0;
-    for (PeChunk* c : cs) tot += 2 * c->r1.size();
-    reads.reserve(tot);
-    for (PeChunk* c : cs)
-        for (size_t i = 0; i < c->r1.size(); ++i) { reads.push_back(&c->r1[i]->seq); reads.push_back(&c->r2[i]->seq); }
-    const auto t = Clock::now();
-    SeedBatchOut all;
-    {
-        Unslot u(slots, eng.offloads());
-        eng.seed(reads, mc.mparams.rescue_level, (unsigned)mc.mparams.rescue_cutoff, all);
-    }
-    const double dt = since(t) / (double)cs.size();
-    size_t r0 = 0;
-    for (PeChunk* c : cs) {
-        const size_t n = 2 * c->r1.size();
-        SeedBatchOut& o = c->seeds;
-        const uint64_t a = all.offsets[r0], b = all.offsets[r0 + n];
-        o.nams.assign(all.nams.begin() + (long)a, all.nams.begin() + (long)b);
-        o.offsets.resize(n + 1);
-        for (size_t i = 0; i <= n; ++i) o.offsets[i] = all.offsets[r0 + i] - a;
-        o.nonrep.assign(all.nonrep.begin() + (long)r0, all.nonrep.begin() + (long)(r0 + n));
-        o.rescued.assign(all.rescued.begin() + (long)r0, all.rescued.begin() + (long)(r0 + n));
-        if (!all.sites.empty()) {   // sites follow the NAMs; positions keep their pool offsets
-            o.sites.assign(all.sites.begin() + (long)a, all.sites.begin() + (long)b);
-            o.mm_pool = all.mm_pool;
-        }
-        c->times.seed += dt;
-        r0 += n;
-    }
 }
 
 // part() of every pair in chunk order (pc.cpp:1739-1766) on the seeded chunk
@@ -470,55 +417,23 @@ void pe_seed_multi(std::vector<PeChunk*>& cs, Engine& eng, const MapContext& mc,
 template <class OnFrozen>
 void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize, OnFrozen&& on_frozen) {
     bool was_frozen = isize.frozen();
-    c.rng.seed((unsigned)c.index);
-    const size_t n = c.r1.size();
+    c.rng.seed((unsigned)c.in.index);
+    const size_t n = c.size();
     if (n == 0) return;
     const SeedBatchOut& so = c.seeds;
     const auto t = Clock::now();
     std::vector<Nam> nams[2];                 // reused: assign() keeps the capacity
-    // part() reads reference windows at the best NAMs (consistency k-mers, the
-    // Hamming window); RSA_PREFETCH_REF=1 prefetches them a few pairs ahead.
-    // Off by default: A/B on the 3 Gb bench, 16 cores: 9.37/9.42 off vs 8.50/8.22 on.
-    static const bool pf_ref = getenv("RSA_PREFETCH_REF") && atoi(getenv("RSA_PREFETCH_REF")) != 0;
-    constexpr size_t kAhead = 4;
-    auto prefetch_read = [&](size_t r, size_t len) {
-        const uint64_t a = so.offsets[r], b = so.offsets[r + 1];
-        const Nam* b1 = nullptr;
-        const Nam* b2 = nullptr;
-        for (uint64_t k = a; k < b; ++k) {
-            const Nam& x = so.nams[k];
-            if (!b1 || x.score > b1->score) { b2 = b1; b1 = &x; }
-            else if (!b2 || x.score > b2->score) b2 = &x;
-        }
-        for (const Nam* x : {b1, b2}) {
-            if (!x) continue;
-            const std::string_view ref = mc.refs.seq(x->ref_id);
-            const size_t st = (size_t)std::max(0, x->ref_start - x->query_start);
-            if (st >= ref.size()) continue;
-            const char* p = ref.data() + st;
-            for (size_t o = 0; o < len + 64; o += 64) __builtin_prefetch(p + o);
-        }
-    };
-    if (pf_ref)
-        for (size_t i = 0; i < std::min(n, kAhead); ++i) {
-            prefetch_read(2 * i, c.r1[i]->seq.size());
-            prefetch_read(2 * i + 1, c.r2[i]->seq.size());
-        }
     for (size_t i = 0; i < n; ++i) {
-        if (pf_ref && i + kAhead < n) {
-            prefetch_read(2 * (i + kAhead), c.r1[i + kAhead]->seq.size());
-            prefetch_read(2 * (i + kAhead) + 1, c.r2[i + kAhead]->seq.size());
-        }
         bool rescued[2];
         for (int m = 0; m < 2; ++m) {
             const size_t r = 2 * i + m;
             load_sorted_nams(nams[m], so.nams.data() + so.offsets[r], so.offsets[r + 1] - so.offsets[r]);
             rescued[m] = so.rescued[r] != 0;
         }
-        Read read1(c.r1[i]->seq, c.rc(i, 0)), read2(c.r2[i]->seq, c.rc(i, 1));
+        Read read1(c.in.r1[i].seq, c.rc(i, 0)), read2(c.in.r2[i].seq, c.rc(i, 1));
         read1.site = so.site_view(2 * i);
         read2.site = so.site_view(2 * i + 1);
-        align_PE_read_part(c.res[i], *c.r1[i], *c.r2[i], read1, read2, nams, rescued, c.stats, isize, mc, c.rng,
+        align_PE_read_part(c.res[i], c.in.r1[i], c.in.r2[i], read1, read2, nams, rescued, c.stats, isize, mc, c.rng,
                            true);
         c.stats.n_reads += 2;
         if (!was_frozen && isize.frozen()) {
@@ -537,11 +452,11 @@ void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize) {
 // appends the chunk's SW jobs (pc.cpp:214-242, 333-368) to `jobs`
 void pe_get_str(PeChunk& c, const MapContext& mc, float mu, float sigma, std::vector<SwJob>& jobs) {
     const auto t = Clock::now();
-    const size_t n = c.r1.size(), ahead = rec_ahead();
+    const size_t n = c.size(), ahead = rec_ahead();
     for (size_t i = 0; i < n; ++i) {
         if (i + ahead < n) prefetch_vec(c.res[i + ahead].todo_nams);   // written by part(), cold by now
-        const Read read1(c.r1[i]->seq, c.rc(i, 0)), read2(c.r2[i]->seq, c.rc(i, 1));
-        collect_jobs_pe(c.res[i], *c.r1[i], *c.r2[i], read1, read2, mc, mu, sigma, jobs);
+        const Read read1(c.in.r1[i].seq, c.rc(i, 0)), read2(c.in.r2[i].seq, c.rc(i, 1));
+        collect_jobs_pe(c.res[i], c.in.r1[i], c.in.r2[i], read1, read2, mc, mu, sigma, jobs);
     }
     c.times.collect += since(t);
 }
@@ -551,26 +466,26 @@ void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistributio
                    std::vector<AlignmentInfo>& infos, size_t pos, const std::string& rg_id, SamText& out,
                    SamDigest* digest) {
     const auto t = Clock::now();
-    const size_t n = c.r1.size();
+    const size_t n = c.size();
     static const bool pf = !(getenv("RSA_PREFETCH") && atoi(getenv("RSA_PREFETCH")) == 0);
     const size_t ahead = rec_ahead();
     for (size_t i = 0; i < n; ++i) {
         if (pf && i + ahead < n) prefetch_res(c.res[i + ahead]);
-        const Read read1(c.r1[i]->seq, c.rc(i, 0)), read2(c.r2[i]->seq, c.rc(i, 1));
+        const Read read1(c.in.r1[i].seq, c.rc(i, 0)), read2(c.in.r2[i].seq, c.rc(i, 1));
         pos = store_results_pe(c.res[i], read1, read2, mc, isize.mu, isize.sigma, infos, pos);
     }
     out.clear();
-    out.reserve(7 * (size_t)mc.mparams.r * c.r1.size());
+    out.reserve(7 * (size_t)mc.mparams.r * n);
     Sam sam(out, mc.refs, mc.mparams.cigar_eqx, rg_id, mc.mparams.output_unmapped, mc.mparams.details);
     sam.digest_into(digest);
     for (size_t i = 0; i < n; ++i) {
         if (pf && i + ahead < n) {
-            prefetch_record(*c.r1[i + ahead]);
-            prefetch_record(*c.r2[i + ahead]);
+            prefetch_record(c.in.r1[i + ahead]);
+            prefetch_record(c.in.r2[i + ahead]);
             prefetch_res(c.res[i + ahead]);
         }
-        const Read read1(c.r1[i]->seq, c.rc(i, 0)), read2(c.r2[i]->seq, c.rc(i, 1));
-        align_PE_read_last(c.res[i], *c.r1[i], *c.r2[i], read1, read2, sam, c.stats, isize, mc, c.rng);
+        const Read read1(c.in.r1[i].seq, c.rc(i, 0)), read2(c.in.r2[i].seq, c.rc(i, 1));
+        align_PE_read_last(c.res[i], c.in.r1[i], c.in.r2[i], read1, read2, sam, c.stats, isize, mc, c.rng);
     }
     c.times.last += since(t);
 }
@@ -586,60 +501,23 @@ void tune_malloc() {
     });
 }
 
-bool same_name(const std::string& n1, const std::string& n2) {      // pc.cpp:23-35
-    if (n1.length() != n2.length()) return false;
-    if (n1.length() <= 2) return n1 == n2;
-    size_t i = 0;
-    for (; i < n1.length() - 1; ++i)
-        if (n1[i] != n2[i]) return false;
-    if (n1[i - 1] == '/' && n1[i] == '1' && n2[i] == '2') return true;
-    return n1[i] == n2[i];
-}
-
-size_t distribute_interleaved(std::vector<Record>&& recs, size_t chunk_size, std::vector<Record>& r1,
-                              std::vector<Record>& r2, std::vector<size_t>& chunk_starts) {
-    const size_t block = 2 * std::max<size_t>(1, chunk_size);   // read_records: ks1->stream().read(to_read * 2)
-    r1.clear();
-    r2.clear();
-    chunk_starts.assign(1, 0);
-    size_t singles = 0;
-    for (size_t b = 0; b < recs.size(); b += block) {
-        const size_t e = std::min(recs.size(), b + block);
-        for (size_t i = b; i < e; ++i) {
-            if (i + 1 < e && same_name(recs[i].name, recs[i + 1].name)) {
-                r1.push_back(std::move(recs[i]));
-                r2.push_back(std::move(recs[i + 1]));
-                ++i;
-            } else {
-                singles++;
-            }
-        }
-        chunk_starts.push_back(r1.size());
-    }
-    recs.clear();
-    return singles;
-}
-
 // Chunks flow through three stages:
 //   load + seed   any order, any worker, up to `window` chunks ahead (needs no
 //                 insert-size state, so it also fills the sequential phase)
 //   sequential    the reference's single-worker timeline (part(N) between
 //                 get_str(N-1) and store(N-1)) until the estimate freezes
 //   parallel      part, get_str, extend, store, last per chunk on any worker
-// Every GPU wait sleeps (blocking-sync events), so a worker waiting on the
-// engine leaves its core to the others.
-PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<Record>& r2, Engine& eng,
-                               const MapContext& mc, const PipelineOptions& opt, SamSink sink, void* user) {
+// Chunks are claimed in index order; how many there are is known only once a
+// claim runs past the end of the input (a streamed source reads while mapping).
+// Every GPU wait sleeps, so a worker waiting on the engine leaves its core to the
+// others.
+PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& mc, const PipelineOptions& opt,
+                               SamSink sink, void* user) {
     const auto t0 = Clock::now();
     PipelineResult result;
     OrderedSink os{sink, user, opt.digest};
     os.sink_at = opt.sink_at;
     os.at_user = opt.sink_at_user;
-    const size_t chunk = (size_t)std::max(1, opt.chunk_size);
-    if (!opt.chunk_starts.empty() && (opt.chunk_starts.front() != 0 || opt.chunk_starts.back() != r1.size()))
-        throw std::runtime_error("chunk_starts do not cover the pairs");
-    const size_t n_chunks = opt.chunk_starts.empty() ? (r1.size() + chunk - 1) / chunk : opt.chunk_starts.size() - 1;
-    if (n_chunks == 0) return result;
     const int T = std::max(1, opt.threads);
     const bool offl = eng.offloads();
     const int W = T + wait_workers(eng, T);
@@ -652,7 +530,13 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
     std::mutex m;
     std::condition_variable cv;
     std::map<size_t, std::unique_ptr<PeChunk>> seeded;   // stage 1 done
-    std::vector<uint8_t> claimed(n_chunks, 0);           // stage 1 taken by some worker
+    std::deque<uint8_t> claimed;                         // stage 1 taken by some worker
+    auto is_claimed = [&](size_t i) { return i < claimed.size() && claimed[i]; };
+    auto claim = [&](size_t i) {
+        if (i >= claimed.size()) claimed.resize(i + 1, 0);
+        claimed[i] = 1;
+    };
+    size_t n_chunks = SIZE_MAX;    // chunks of the input, once a claim has run past its end
     size_t next_seed = 0;          // every chunk below is claimed
     size_t consumed = 0;           // chunks handed past stage 1
     bool frozen = false, done = false;
@@ -668,94 +552,79 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
     PhaseTimes phases_all;
 
     // finished chunks are recycled (process-wide, across runs), so the per-pair
-    // result vectors stop allocating and no run ends by freeing them one by one
-    auto recycle = [&](std::unique_ptr<PeChunk> c) { chunk_pool().put(std::move(c)); };
-    // prefetch claims up to this many consecutive chunks per seeding call (RSA_SEED_BATCH,
-    // default 1: A/B on the bench, 1 -> 11.75/11.61, 4 -> 11.00/10.60 Mreads/s; r26 code:
-    // 1 -> 15.5/16.5/13.8, 2 -> 13.8/12.9/15.2, profiles/r01_ab_seed_batch.jsonl)
-    const size_t seed_batch = std::max<size_t>(1, getenv("RSA_SEED_BATCH") ? (size_t)atol(getenv("RSA_SEED_BATCH")) : 1);
-    // chunks per extend call in the parallel stage (PipelineOptions::ext_group, RSA_EXT_GROUP)
-    const size_t ext_group = (size_t)std::max(1, opt.ext_group > 0 ? opt.ext_group
-                                                   : getenv("RSA_EXT_GROUP") ? atoi(getenv("RSA_EXT_GROUP"))
-                                                   : kDefaultExtGroup);
-    auto stage1_multi = [&](const std::vector<size_t>& idxs) {
-        std::vector<std::unique_ptr<PeChunk>> cs;
-        std::vector<PeChunk*> ps;
-        for (size_t idx : idxs) {
-            std::unique_ptr<PeChunk> c = chunk_pool().take();
-            if (!c) c = std::make_unique<PeChunk>();
-            const auto t = Clock::now();
-            pe_load(*c, r1, r2, idx, chunk, opt.chunk_starts, eng.io_alloc());
-            c->times.load += since(t);
-            ps.push_back(c.get());
-            cs.push_back(std::move(c));
-        }
-        pe_seed_multi(ps, eng, mc, slots);
-        return cs;
+    // result vectors stop allocating and no run ends by freeing them one by one;
+    // the source gets the chunk's input storage back first
+    std::atomic<uint64_t> singletons{0};
+    auto recycle = [&](std::unique_ptr<PeChunk> c) {
+        if (!c) return;
+        singletons += c->in.singletons;
+        src.release(c->in);
+        chunk_pool().put(std::move(c));
     };
-    auto stage1 = [&](size_t idx) {
+    // load + seed chunk idx; null when the input ends before it (n_chunks is then known)
+    auto stage1 = [&](size_t idx) -> std::unique_ptr<PeChunk> {
         std::unique_ptr<PeChunk> c = chunk_pool().take();
         if (!c) c = std::make_unique<PeChunk>();
         const auto t = Clock::now();
-        pe_load(*c, r1, r2, idx, chunk, opt.chunk_starts, eng.io_alloc());
+        if (!pe_load(*c, src, idx, eng.io_alloc())) {
+            chunk_pool().put(std::move(c));
+            std::lock_guard<std::mutex> g(m);
+            n_chunks = std::min(n_chunks, idx);
+            cv.notify_all();
+            return nullptr;
+        }
         c->times.load += since(t);
         pe_seed(*c, eng, mc, slots);
         return c;
     };
-    // chunk idx after stage 1: from the prefetch map, or loaded + seeded here
+    // chunk idx after stage 1: from the prefetch map, or loaded + seeded here.
+    // Null past the end of the input or after a failure (`failure` set).
     auto acquire = [&](size_t idx) -> std::unique_ptr<PeChunk> {
         std::unique_lock<std::mutex> g(m);
-        if (!claimed[idx]) {                    // nobody claimed it yet
-            claimed[idx] = 1;
-            while (next_seed < n_chunks && claimed[next_seed]) next_seed++;
+        if (!is_claimed(idx)) {                 // nobody claimed it yet
+            claim(idx);
+            while (is_claimed(next_seed)) next_seed++;
             g.unlock();
             auto c = stage1(idx);
             g.lock();
-            consumed++;
+            if (c) consumed++;
             cv.notify_all();
             return c;
         }
-        if (!(seeded.count(idx) || failure)) {
+        auto ready = [&] { return seeded.count(idx) || failure || idx >= n_chunks; };
+        if (!ready()) {
             g.unlock();
             Unslot u(slots, true);
             g.lock();
-            cv.wait(g, [&] { return seeded.count(idx) || failure; });
+            cv.wait(g, ready);
             g.unlock();          // the slot comes back without the lock held
         }
         if (!g.owns_lock()) g.lock();
-        if (failure) return nullptr;
+        if (failure || !seeded.count(idx)) return nullptr;
         auto c = std::move(seeded[idx]);
         seeded.erase(idx);
         consumed++;
         cv.notify_all();
         return c;
     };
-    // SW jobs of a group of parted chunks in one engine call, then store + last per chunk
-    auto finish = [&](std::vector<std::unique_ptr<PeChunk>>& cs, const InsertSizeDistribution& est,
-                      std::vector<SwJob>& jobs, std::vector<AlignmentInfo>& infos) {
+    // SW jobs of a parted chunk in one engine call, then store + last
+    auto finish = [&](PeChunk& c, const InsertSizeDistribution& est, std::vector<SwJob>& jobs,
+                      std::vector<AlignmentInfo>& infos) {
         jobs.clear();
-        std::vector<size_t> first(cs.size());
-        for (size_t g = 0; g < cs.size(); ++g) {
-            first[g] = jobs.size();
-            pe_get_str(*cs[g], mc, est.mu, est.sigma, jobs);
-            cs[g]->stats.tot_aligner_calls += jobs.size() - first[g];
-        }
+        pe_get_str(c, mc, est.mu, est.sigma, jobs);
+        c.stats.tot_aligner_calls += jobs.size();
         const auto te = Clock::now();
         {
             Unslot u(slots, offl);
             eng.extend(jobs, mc.aparams, infos);
         }
-        const double dt = since(te) / (double)cs.size();
-        for (size_t g = 0; g < cs.size(); ++g) {
-            PeChunk& c = *cs[g];
-            c.times.extend += dt;
-            SamText out = os.take();
-            SamDigest dg;
-            pe_store_last(c, mc, est, infos, first[g], opt.rg_id, out, os.digest ? &dg : nullptr);
-            const auto tp = Clock::now();
-            os.put(c.index, std::move(out), os.digest ? &dg : nullptr);
-            c.times.output += since(tp);
-        }
+        c.times.extend += since(te);
+        SamText out = os.take();
+        SamDigest dg;
+        pe_store_last(c, mc, est, infos, 0, opt.rg_id, out, os.digest ? &dg : nullptr);
+        const auto tp = Clock::now();
+        os.put(c.in.index, std::move(out), os.digest ? &dg : nullptr);
+        c.times.output += since(tp);
     };
 
     auto worker = [&](bool leader) {
@@ -773,31 +642,32 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                 std::lock_guard<std::mutex> g(m);
                 frozen = true;
                 frozen_isize = isize;
-                next_par = std::min(cur_chunk.index + 1, n_chunks);
+                next_par = cur_chunk.in.index + 1;
                 early = true;
                 cv.notify_all();
             };
             if (leader) {
                 // ---- single-worker timeline until the insert-size estimate freezes ----
                 auto pre = acquire(0);
-                if (!pre) return;
+                bool lost = false;
                 {
                     std::lock_guard<std::mutex> g(m);
-                    lead_seeded = true;
+                    lost = failure != nullptr;
+                    lead_seeded = pre != nullptr;
                     cv.notify_all();
                 }
-                pe_part(*pre, mc, isize, early_freeze);
+                if (lost) return;
+                if (pre) pe_part(*pre, mc, isize, early_freeze);
                 size_t next = 1;
-                for (;;) {
-                    if (isize.frozen() || next > n_chunks) break;
+                while (pre && !isize.frozen()) {
                     jobs.clear();
                     pe_get_str(*pre, mc, isize.mu, isize.sigma, jobs);
-                    std::unique_ptr<PeChunk> cur;
-                    if (next < n_chunks) {
-                        cur = acquire(next);
-                        if (!cur) return;
-                        pe_part(*cur, mc, isize, early_freeze);
+                    std::unique_ptr<PeChunk> cur = acquire(next);
+                    if (!cur) {
+                        std::lock_guard<std::mutex> g(m);
+                        if (failure) return;
                     }
+                    if (cur) pe_part(*cur, mc, isize, early_freeze);
                     next++;
                     const auto te = Clock::now();
                     {
@@ -809,10 +679,9 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                     SamText out = os.take();
                     SamDigest dg;
                     pe_store_last(*pre, mc, isize, infos, 0, opt.rg_id, out, os.digest ? &dg : nullptr);
-                    os.put(pre->index, std::move(out), os.digest ? &dg : nullptr);
+                    os.put(pre->in.index, std::move(out), os.digest ? &dg : nullptr);
                     local.add(pre->stats);
                     lt.add(pre->times);
-                    if (!cur) { recycle(std::move(pre)); break; }
                     recycle(std::move(pre));
                     pre = std::move(cur);
                 }
@@ -822,34 +691,24 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                 frozen_isize = isize;
                 handed = std::move(pre);                 // may be null: everything was sequential
                 leader_busy = false;
-                if (!early) next_par = std::min(next, n_chunks);
+                if (!early) next_par = next;
                 if (next_par >= n_chunks && !handed) done = true;
                 cv.notify_all();
             }
             // ---- shared loop: parallel stage first, prefetch when it has nothing ----
             for (;;) {
                 std::unique_ptr<PeChunk> c;
-                size_t idx = SIZE_MAX, pf = SIZE_MAX, cnt = 0;
-                std::vector<size_t> pfs;
+                size_t idx = SIZE_MAX, pf = SIZE_MAX;
                 {
                     std::unique_lock<std::mutex> g(m);
                     for (;;) {
                         if (failure || done) break;
                         if (frozen && handed) { c = std::move(handed); break; }
-                        if (frozen && next_par < n_chunks) {
-                            idx = next_par;
-                            cnt = std::min(ext_group, n_chunks - next_par);
-                            next_par += cnt;
-                            break;
-                        }
+                        if (frozen && next_par < n_chunks) { idx = next_par++; break; }
                         if (lead_seeded && next_seed < n_chunks && next_seed < consumed + window) {
                             pf = next_seed;
-                            // a run of consecutive unclaimed chunks, seeded in one engine call
-                            for (size_t q = next_seed; q < n_chunks && pfs.size() < seed_batch && !claimed[q]; ++q) {
-                                claimed[q] = 1;
-                                pfs.push_back(q);
-                            }
-                            while (next_seed < n_chunks && claimed[next_seed]) next_seed++;
+                            claim(pf);
+                            while (is_claimed(next_seed)) next_seed++;
                             break;
                         }
                         if (frozen && next_par >= n_chunks && !leader_busy) { done = true; cv.notify_all(); break; }
@@ -863,30 +722,27 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
                         g.lock();
                     }
                 }
-                if (c || idx != SIZE_MAX) {
-                    std::vector<std::unique_ptr<PeChunk>> cs;
-                    if (c) cs.push_back(std::move(c));     // part() already done
-                    bool lost = false;
-                    for (size_t q = idx; q != SIZE_MAX && q < idx + cnt; ++q) {
-                        auto x = acquire(q);
-                        if (!x) { lost = true; break; }
-                        InsertSizeDistribution est = frozen_isize;
-                        pe_part(*x, mc, est);
-                        cs.push_back(std::move(x));
+                if (!c && idx != SIZE_MAX) {
+                    c = acquire(idx);
+                    if (!c) {
+                        std::lock_guard<std::mutex> g(m);
+                        if (failure) break;
+                        continue;                        // past the end: n_chunks is known now
                     }
-                    if (lost) break;
-                    finish(cs, frozen_isize, jobs, infos);
-                    for (auto& x : cs) {
-                        local.add(x->stats);
-                        lt.add(x->times);
-                        recycle(std::move(x));
-                    }
+                    InsertSizeDistribution est = frozen_isize;
+                    pe_part(*c, mc, est);
+                }
+                if (c) {
+                    finish(*c, frozen_isize, jobs, infos);
+                    local.add(c->stats);
+                    lt.add(c->times);
+                    recycle(std::move(c));
                     continue;
                 }
                 if (pf != SIZE_MAX) {
-                    auto s1 = stage1_multi(pfs);
+                    auto s1 = stage1(pf);
                     std::lock_guard<std::mutex> g(m);
-                    for (size_t q = 0; q < pfs.size(); ++q) seeded.emplace(pfs[q], std::move(s1[q]));
+                    if (s1) seeded.emplace(pf, std::move(s1));
                     cv.notify_all();
                     continue;
                 }
@@ -904,13 +760,23 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
     };
     std::atomic<bool> lead_taken{false};
     WorkerPool::get().run(W, [&] { worker(!lead_taken.exchange(true)); });
+    // chunks seeded ahead but never mapped (a failure): their input goes back to the source
+    for (auto& kv : seeded) recycle(std::move(kv.second));
+    if (handed) recycle(std::move(handed));
     if (failure) std::rethrow_exception(failure);
     result.stats = stats_all;
     result.phases = phases_all;
+    result.singletons = singletons.load();
     result.map_seconds = since(t0);
     result.sam_bytes = os.bytes;
     result.sam_digest = os.total;
     return result;
+}
+
+PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<Record>& r2, Engine& eng,
+                               const MapContext& mc, const PipelineOptions& opt, SamSink sink, void* user) {
+    auto src = make_vector_source(&r1, &r2, (size_t)std::max(1, opt.chunk_size));
+    return run_pipeline_pe(*src, eng, mc, opt, sink, user);
 }
 
 // a single-end worker's storage, kept across chunks and mapping calls: the seeding
@@ -918,10 +784,12 @@ PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<
 // worker per call put page locking into every call) and the per-read results,
 // reverse complements and NAM list, which keep their capacity
 struct SeScratch {
+    InputChunk in;
     SeedBatchOut so;
     std::vector<AlignTmpRes> res;
     std::vector<std::string> rcs;
     std::vector<Nam> nams;
+    std::vector<std::string_view> reads;
 };
 struct SeScratchPool {
     std::mutex m;
@@ -945,15 +813,13 @@ struct SeScratchPool {
 
 // Single-end: perform_task_async_se (pc.cpp:814-1096).  No insert-size state;
 // records are NOT upper-cased on this path; chunks are independent from the start.
-PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, const MapContext& mc,
-                               const PipelineOptions& opt, SamSink sink, void* user) {
+PipelineResult run_pipeline_se(ReadSource& src, Engine& eng, const MapContext& mc, const PipelineOptions& opt,
+                               SamSink sink, void* user) {
     auto t0 = std::chrono::steady_clock::now();
     PipelineResult result;
     OrderedSink os{sink, user, opt.digest};
     os.sink_at = opt.sink_at;
     os.at_user = opt.sink_at_user;
-    const size_t chunk = (size_t)std::max(1, opt.chunk_size);
-    const size_t n_chunks = (recs.size() + chunk - 1) / chunk;
     std::atomic<size_t> next{0};
     std::mutex stat_m;
     const int T = std::max(1, opt.threads);
@@ -970,47 +836,48 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
         std::vector<AlignmentInfo>& infos = scratch.s->infos;
         AlignmentStatistics local;
         std::unique_ptr<SeScratch> se = SeScratchPool::get().take();
+        InputChunk& in = se->in;
         SeedBatchOut& so = se->so;                   // the worker's, reused chunk after chunk and across calls
         std::vector<AlignTmpRes>& res = se->res;
         std::vector<std::string>& rcs = se->rcs;
         std::vector<Nam>& nams = se->nams;
+        std::vector<std::string_view>& reads = se->reads;
         try {
         for (;;) {
             if (failed.load()) break;
-            size_t idx = next.fetch_add(1);
-            if (idx >= n_chunks) break;
-            const size_t b = idx * chunk, e = std::min(recs.size(), b + chunk);
+            const size_t idx = next.fetch_add(1);
+            if (!src.get(idx, in)) break;
+            const size_t n = in.r1.size();
+            const RecView* recs = in.r1.data();
             AlignmentStatistics st;
             std::minstd_rand rng;
             rng.seed((unsigned)idx);
-            std::vector<const std::string*> reads;
-            for (size_t i = b; i < e; ++i) reads.push_back(&recs[i].seq);
+            reads.clear();
+            for (size_t i = 0; i < n; ++i) reads.push_back(recs[i].seq);
             so.clear();
-            {
+            if (n) {
                 Unslot u(slots, offl);
                 eng.seed(reads, mc.mparams.rescue_level, (unsigned)mc.mparams.rescue_cutoff, so);
             }
-            if (res.size() > e - b) res.resize(e - b);
+            if (res.size() > n) res.resize(n);
             for (auto& x : res) x.reset();
-            res.resize(e - b);
-            rcs.resize(e - b);
-            for (size_t i = b; i < e; ++i) {
-                std::string& rc = rcs[i - b];
-                rc.resize(recs[i].seq.size());
-                reverse_complement_into(recs[i].seq, rc.data());
+            res.resize(n);
+            rcs.resize(n);
+            for (size_t r = 0; r < n; ++r) {
+                rcs[r].resize(recs[r].seq.size());
+                reverse_complement_into(recs[r].seq, rcs[r].data());
             }
-            for (size_t i = b; i < e; ++i) {
-                const size_t r = i - b;
+            for (size_t r = 0; r < n; ++r) {
                 nams.assign(so.nams.begin() + (long)so.offsets[r], so.nams.begin() + (long)so.offsets[r + 1]);
-                Read read(recs[i].seq, rcs[r]);
+                Read read(recs[r].seq, rcs[r]);
                 read.site = so.site_view(r);
-                align_SE_read_part(res[r], recs[i], read, nams, so.rescued[r] != 0, st, mc, rng);
+                align_SE_read_part(res[r], recs[r], read, nams, so.rescued[r] != 0, st, mc, rng);
                 st.n_reads++;
             }
             jobs.clear();
-            for (size_t i = b; i < e; ++i) {
-                const Read read(recs[i].seq, rcs[i - b]);
-                collect_jobs_se(res[i - b], read, mc, jobs);
+            for (size_t r = 0; r < n; ++r) {
+                const Read read(recs[r].seq, rcs[r]);
+                collect_jobs_se(res[r], read, mc, jobs);
             }
             {
                 Unslot u(slots, offl);
@@ -1018,20 +885,21 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
             }
             st.tot_aligner_calls += jobs.size();
             size_t pos = 0;
-            for (size_t i = b; i < e; ++i) {
-                const Read read(recs[i].seq, rcs[i - b]);
-                pos = store_results_se(res[i - b], read, mc, infos, pos);
+            for (size_t r = 0; r < n; ++r) {
+                const Read read(recs[r].seq, rcs[r]);
+                pos = store_results_se(res[r], read, mc, infos, pos);
             }
             SamText out = os.take();
-            out.reserve(7 * (size_t)mc.mparams.r * (e - b));
+            out.reserve(7 * (size_t)mc.mparams.r * n);
             Sam sam(out, mc.refs, mc.mparams.cigar_eqx, opt.rg_id, mc.mparams.output_unmapped, mc.mparams.details);
             SamDigest dg;
             if (os.digest) sam.digest_into(&dg);
-            for (size_t i = b; i < e; ++i) {
-                if (i + rec_ahead() < e) prefetch_record(recs[i + rec_ahead()]);
-                const Read read(recs[i].seq, rcs[i - b]);
-                align_SE_read_last(res[i - b], recs[i], read, sam, st, mc, rng);
+            for (size_t r = 0; r < n; ++r) {
+                if (r + rec_ahead() < n) prefetch_record(recs[r + rec_ahead()]);
+                const Read read(recs[r].seq, rcs[r]);
+                align_SE_read_last(res[r], recs[r], read, sam, st, mc, rng);
             }
+            src.release(in);
             os.put(idx, std::move(out), os.digest ? &dg : nullptr);
             local.add(st);
         }
@@ -1045,6 +913,7 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
         }
         hold.reset();
         so.clear();
+        src.release(in);
         SeScratchPool::get().put(std::move(se));
         std::lock_guard<std::mutex> g(stat_m);
         result.stats.add(local);
@@ -1055,6 +924,12 @@ PipelineResult run_pipeline_se(const std::vector<Record>& recs, Engine& eng, con
     result.sam_bytes = os.bytes;
     result.sam_digest = os.total;
     return result;
+}
+
+PipelineResult run_pipeline_se(const std::vector<Record>& r, Engine& eng, const MapContext& mc,
+                               const PipelineOptions& opt, SamSink sink, void* user) {
+    auto src = make_vector_source(&r, nullptr, (size_t)std::max(1, opt.chunk_size));
+    return run_pipeline_se(*src, eng, mc, opt, sink, user);
 }
 
 }  // namespace rsa

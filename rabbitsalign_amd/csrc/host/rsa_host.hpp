@@ -213,6 +213,15 @@ struct AlignmentStatistics {
 
 struct Record { std::string name, comment, seq, qual; };   // klibpp::KSeq fields used
 
+// A record as the pipeline and the SAM writer read it: views into storage that
+// outlives the chunk (a mapped FASTQ file, a chunk's parsed records, a caller's
+// Record vector).  Chunks of the mapped 4-line layout are never copied.
+struct RecView {
+    std::string_view name, comment, seq, qual;
+    RecView() = default;
+    RecView(const Record& r) : name(r.name), comment(r.comment), seq(r.seq), qual(r.qual) {}   // NOLINT: implicit
+};
+
 std::string reverse_complement(std::string_view s);
 void reverse_complement_into(std::string_view s, char* out);   // out holds s.size() bytes
 void reverse_into(std::string_view s, char* out);              // plain byte reversal
@@ -376,7 +385,7 @@ public:
     virtual ~Engine() = default;
     virtual const char* name() const = 0;
     // NAMs (pre-sort order) for every read, as align_*_read_part computes them (aln.cpp:1946-1962)
-    virtual void seed(const std::vector<const std::string*>& reads, int rescue_level, unsigned rescue_cutoff,
+    virtual void seed(const std::vector<std::string_view>& reads, int rescue_level, unsigned rescue_cutoff,
                       SeedBatchOut& out) = 0;
     // The same for reads already packed back to back (read i at blob[offs[i] ..
     // offs[i] + lens[i])), in memory from io_alloc() -- engines that offer it
@@ -416,23 +425,23 @@ struct MapContext {
 // part / last split of src/aln.cpp:1927-2306 (PE) and 2372-2467 (SE).  `nams`
 // are the pre-sort NAM lists of both mates (already through find_nams/rescue).
 // sorted: nams[m] are already in std::sort(by_score) order (load_sorted_nams)
-void align_PE_read_part(AlignTmpRes& res, const Record& r1, const Record& r2, const Read& read1, const Read& read2,
+void align_PE_read_part(AlignTmpRes& res, const RecView& r1, const RecView& r2, const Read& read1, const Read& read2,
                         std::vector<Nam> nams[2],
                         const bool rescued[2], AlignmentStatistics& stats, InsertSizeDistribution& isize,
                         const MapContext& mc, std::minstd_rand& rng, bool sorted = false);
 // dst = src[0 .. n) in the order std::sort(by_score) gives (aln.cpp:1962-1964), in one gather
 void load_sorted_nams(std::vector<Nam>& dst, const Nam* src, size_t n);
-void align_PE_read_last(AlignTmpRes& res, const Record& r1, const Record& r2, const Read& read1, const Read& read2,
+void align_PE_read_last(AlignTmpRes& res, const RecView& r1, const RecView& r2, const Read& read1, const Read& read2,
                         Sam& sam,
                         AlignmentStatistics& stats, const InsertSizeDistribution& isize, const MapContext& mc,
                         std::minstd_rand& rng);
-void align_SE_read_part(AlignTmpRes& res, const Record& r, const Read& read, std::vector<Nam>& nams, bool rescued,
+void align_SE_read_part(AlignTmpRes& res, const RecView& r, const Read& read, std::vector<Nam>& nams, bool rescued,
                         AlignmentStatistics& stats, const MapContext& mc, std::minstd_rand& rng);
-void align_SE_read_last(AlignTmpRes& res, const Record& r, const Read& read, Sam& sam, AlignmentStatistics& stats,
+void align_SE_read_last(AlignTmpRes& res, const RecView& r, const Read& read, Sam& sam, AlignmentStatistics& stats,
                         const MapContext& mc, std::minstd_rand& rng);
 
 // SW jobs of a finished part() (pc.cpp:1604-1669 get_str) and storing their results (pc.cpp:1789-1844)
-void collect_jobs_pe(AlignTmpRes& res, const Record& r1, const Record& r2, const Read& read1, const Read& read2,
+void collect_jobs_pe(AlignTmpRes& res, const RecView& r1, const RecView& r2, const Read& read1, const Read& read2,
                      const MapContext& mc, float mu, float sigma, std::vector<SwJob>& jobs);
 size_t store_results_pe(AlignTmpRes& res, const Read& read1, const Read& read2, const MapContext& mc, float mu,
                         float sigma, std::vector<AlignmentInfo>& infos, size_t pos);
@@ -509,14 +518,14 @@ class Sam {                                     // src/sam.hpp:69-120
 public:
     Sam(SamText& out, const References& refs, bool eqx, const std::string& rg_id, bool output_unmapped,
         bool details);
-    void add(const Alignment& a, const Record& r, std::string_view rc, uint8_t mapq, bool primary,
+    void add(const Alignment& a, const RecView& r, std::string_view rc, uint8_t mapq, bool primary,
              const Details& d);
-    void add_pair(const Alignment& a1, const Alignment& a2, const Record& r1, const Record& r2,
+    void add_pair(const Alignment& a1, const Alignment& a2, const RecView& r1, const RecView& r2,
                   std::string_view rc1, std::string_view rc2, uint8_t mapq1, uint8_t mapq2, bool proper,
                   bool primary, const Details d[2]);
-    void add_unmapped(const Record& r, uint16_t flags = 4);
-    void add_unmapped_pair(const Record& r1, const Record& r2);
-    void add_unmapped_mate(const Record& r, uint16_t flags, std::string_view mate_ref, uint32_t mate_pos);
+    void add_unmapped(const RecView& r, uint16_t flags = 4);
+    void add_unmapped_pair(const RecView& r1, const RecView& r2);
+    void add_unmapped_mate(const RecView& r, uint16_t flags, std::string_view mate_ref, uint32_t mate_pos);
     // fold every line into *d as it is written (while it is in cache) instead of a
     // second pass over the chunk's text; same value as SamDigest::of on the text
     void digest_into(SamDigest* d) { digest_ = d; }
@@ -528,9 +537,9 @@ private:
             digest_->lines++;
         }
     }
-    void add_record(const std::string& qname, uint16_t flags, std::string_view rname, uint32_t pos, uint8_t mapq,
+    void add_record(std::string_view qname, uint16_t flags, std::string_view rname, uint32_t pos, uint8_t mapq,
                     const Cigar& cigar, std::string_view mate_rname, uint32_t mate_pos, int32_t tlen,
-                    std::string_view seq, std::string_view seq_rc, const std::string& qual, int ed, int score,
+                    std::string_view seq, std::string_view seq_rc, std::string_view qual, int ed, int score,
                     const Details& d);
     SamText& out_;
     const References& refs_;
@@ -551,10 +560,60 @@ public:
     static std::vector<Record> read_all(const std::string& path);
     static void read_pair(const std::string& p1, const std::string& p2, std::vector<Record>& r1,
                           std::vector<Record>& r2);
+    // the same parser over bytes in memory (the rest of a mapped file after its
+    // last record in the plain layout); `mem` must outlive the reader
+    FastxReader(const char* mem, size_t len);
 private:
     struct Impl;
     std::unique_ptr<Impl> impl_;
 };
+
+// ---------------------------------------------------------- read source ---
+// One chunk of input as the reference's InputBuffer::read_records hands it out
+// (src/pc.cpp:74-107): chunk `index`, up to chunk_size pairs (PE), reads (SE) or
+// the pairs of a block of 2 x chunk_size interleaved records.  The views point
+// into storage the chunk (`owned`) or the source keeps alive until release().
+struct InputChunk {
+    size_t index = 0;
+    std::vector<RecView> r1, r2;                // pairs (r2 empty for single-end)
+    uint64_t singletons = 0;                    // interleaved: unpaired records, read and dropped
+    std::vector<Record> owned1, owned2;         // records parsed by the sequential reader
+    std::vector<std::pair<const char*, size_t>> mapped;   // mapped file bytes the views use
+    void clear() {
+        r1.clear(); r2.clear(); singletons = 0; owned1.clear(); owned2.clear(); mapped.clear();
+    }
+};
+
+// Chunks are asked for in increasing index order (the pipeline claims them in
+// order), possibly from different threads; get() blocks until chunk idx is read
+// and returns false past the end of the input.  release() hands a chunk's
+// storage back once its SAM is written (a mapped file's pages are dropped, so
+// resident memory does not grow with the input).
+class ReadSource {
+public:
+    virtual ~ReadSource() = default;
+    virtual bool paired() const = 0;
+    virtual bool get(size_t idx, InputChunk& out) = 0;
+    virtual void release(InputChunk& c) { c.clear(); }
+};
+
+// Records already in memory (rsam_reads, tests): chunks are views into the
+// caller's vectors (r2 null: single-end).
+std::unique_ptr<ReadSource> make_vector_source(const std::vector<Record>* r1, const std::vector<Record>* r2,
+                                               size_t chunk_size);
+// Interleaved records in memory: chunk i pairs records [2ci, 2c(i+1)) by same_name.
+std::unique_ptr<ReadSource> make_interleaved_vector_source(const std::vector<Record>* recs, size_t chunk_size);
+// FASTQ/FASTA files, streamed: one reader thread per file parses blocks of
+// records ahead of the pipeline (a bounded number of chunks ahead of the last
+// one asked for).  Uncompressed files in the plain 4-line layout are mapped and
+// split without copying (records are views into the mapping); gzip, pipes and
+// any other layout go through FastxReader (kseq semantics).  path2 empty:
+// single-end, or interleaved pairs when `interleaved`.
+std::unique_ptr<ReadSource> open_fastq_source(const std::string& path1, const std::string& path2, bool interleaved,
+                                              size_t chunk_size);
+// the read-length estimate of the CLI (main.cpp:254-258, readlen.cpp:16-29): the
+// mean length of the first 500 records of each file (1000 of an interleaved file)
+int estimate_read_length(const std::string& path1, const std::string& path2, bool interleaved);
 
 // ------------------------------------------------------------ pipeline ---
 // called at the start of every pipeline worker thread (profiling hooks; null by default)
@@ -566,17 +625,8 @@ using SamSinkAt = void (*)(void* user, const char* chunk, size_t bytes, uint64_t
 struct PipelineOptions {
     int threads = 3;
     int chunk_size = 10000;
-    bool interleaved = false;
     std::string rg_id;
     bool digest = false;   // compute PipelineResult::sam_digest (in the workers, in parallel)
-    // chunks whose SW jobs go to the engine in one extend call (parallel stage, PE);
-    // 0: RSA_EXT_GROUP or the default.  Bigger calls fill the GPU (one chunk is ~7 k jobs,
-    // < 2 waves per SIMD of the scan kernel); results do not depend on it
-    int ext_group = 0;
-    // explicit chunk boundaries in pairs ([n_chunks + 1], first 0): chunk i holds
-    // pairs [chunk_starts[i], chunk_starts[i+1]); empty = every chunk_size pairs.
-    // Interleaved input sets them (its chunks hold up to chunk_size pairs each)
-    std::vector<size_t> chunk_starts;
     // when set, SAM chunks go here at their body offsets instead of to the sequential
     // sink, each written by the worker that finds it ready (parallel file writes)
     SamSinkAt sink_at = nullptr;
@@ -590,11 +640,10 @@ struct PipelineOptions {
 // every other record is a singleton.  The reference's paired-end task
 // (perform_task_async_pe, pc.cpp:1522-1887) maps only the pairs -- singletons
 // are read and dropped -- and a pair split across two blocks is two singletons
-// (the lookahead of distribute_interleaved is never set).  Returns the number of
-// singletons; r1/r2/chunk_starts receive the pairs and their chunk boundaries.
-size_t distribute_interleaved(std::vector<Record>&& recs, size_t chunk_size, std::vector<Record>& r1,
-                              std::vector<Record>& r2, std::vector<size_t>& chunk_starts);
-bool same_name(const std::string& n1, const std::string& n2);
+// (the lookahead of distribute_interleaved is never set).  Appends the pairs
+// of `block` to r1/r2 and returns the number of singletons.
+size_t distribute_interleaved(const RecView* block, size_t n, std::vector<RecView>& r1, std::vector<RecView>& r2);
+bool same_name(std::string_view n1, std::string_view n2);
 
 // glibc malloc settings for the mapping process (once; library entry points and
 // the CLI call it): free memory stays in the heap instead of being trimmed and
@@ -615,6 +664,7 @@ struct PhaseTimes {
 
 struct PipelineResult {
     AlignmentStatistics stats;
+    uint64_t singletons = 0;                    // interleaved input: unpaired records (not mapped)
     double map_seconds = 0;
     uint64_t sam_bytes = 0;
     SamDigest sam_digest;
@@ -635,6 +685,12 @@ struct PosSink {
 };
 bool pos_sink_open(FILE* f, PosSink& ps);
 void pos_sink_write(void* user, const char* chunk, size_t bytes, uint64_t offset);
+// the pipeline over a read source (ReadSource: streamed files or records in memory)
+PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& mc, const PipelineOptions& opt,
+                               SamSink sink, void* user);
+PipelineResult run_pipeline_se(ReadSource& src, Engine& eng, const MapContext& mc, const PipelineOptions& opt,
+                               SamSink sink, void* user);
+// the same over records in memory
 PipelineResult run_pipeline_pe(const std::vector<Record>& r1, const std::vector<Record>& r2, Engine& eng,
                                const MapContext& mc, const PipelineOptions& opt, SamSink sink, void* user);
 PipelineResult run_pipeline_se(const std::vector<Record>& r, Engine& eng, const MapContext& mc,

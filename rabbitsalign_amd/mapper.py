@@ -39,7 +39,7 @@ class _Info(C.Structure):
 
 EXPORTED_SYMBOLS = [
     "rsam_open_files", "rsam_open_synthetic", "rsam_open_like", "rsam_close", "rsam_get_info",
-    "rsam_reads_load", "rsam_reads_load_interleaved", "rsam_reads_synthetic", "rsam_reads_write_fastq", "rsam_reads_count", "rsam_reads_free", "rsam_map",
+    "rsam_reads_load", "rsam_reads_load_interleaved", "rsam_reads_synthetic", "rsam_reads_write_fastq", "rsam_reads_count", "rsam_reads_free", "rsam_map", "rsam_map_files",
     "rsam_add_devices", "rsam_kernel_stats", "rsam_reset_kernel_stats", "rsam_engine_name", "rsam_last_error",
 ]
 
@@ -73,6 +73,7 @@ def load(path: str = PRODUCT_LIB) -> C.CDLL:
     lib.rsam_reads_count.argtypes = [vp]
     lib.rsam_reads_free.argtypes = [vp]
     lib.rsam_map.argtypes = [vp, vp, i32, i32, cp, C.POINTER(_Stats)]
+    lib.rsam_map_files.argtypes = [vp, cp, cp, i32, i32, i32, cp, C.POINTER(_Stats)]
     lib.rsam_kernel_stats.argtypes = [vp, C.POINTER(KernelStats)]
     lib.rsam_reset_kernel_stats.argtypes = [vp]
     lib.rsam_engine_name.restype = cp
@@ -182,6 +183,17 @@ class Mapper:
                                 str(sam_path).encode() if sam_path else None, C.byref(st))
         if rc != 0:
             raise RuntimeError(f"rsam_map: {self._lib.rsam_last_error().decode()}")
+        return MapStats(**{f: getattr(st, f) for f, _ in _Stats._fields_})
+
+    def map_files(self, fq1, fq2=None, interleaved=False, threads=8, chunk_size=10000, sam_path=None) -> MapStats:
+        """FASTQ files -> SAM, the reads streamed while mapping (the CLI's path);
+        map_seconds = call -> last SAM byte written."""
+        st = _Stats()
+        rc = self._lib.rsam_map_files(self._h, str(fq1).encode(), str(fq2).encode() if fq2 else None,
+                                      1 if interleaved else 0, threads, chunk_size,
+                                      str(sam_path).encode() if sam_path else None, C.byref(st))
+        if rc != 0:
+            raise RuntimeError(f"rsam_map_files: {self._lib.rsam_last_error().decode()}")
         return MapStats(**{f: getattr(st, f) for f, _ in _Stats._fields_})
 
     def add_devices(self, devices):
