@@ -209,13 +209,15 @@ def roofline(ks: dict, elapsed: float) -> dict:
 
 
 def pick_io_dir(requested: str, need_bytes: int) -> str:
-    """The bench's FASTQ/SAM directory: the one asked for, else /dev/shm when it has
-    room for `need_bytes` (memory-backed: the run measures the mapper, not a disk),
-    else the system temp dir."""
+    """The bench's FASTQ/SAM directory: the one asked for, else the system temp dir
+    (a disk file system's page cache) when it has room for `need_bytes`, else
+    /dev/shm.  Writing one SAM file into the page cache runs at the speed of one
+    writer (the file's inode lock); on the box that is ~5.5 GB/s on the disk file
+    system and ~3.7 GB/s on tmpfs (scripts/write_bw.py)."""
     import tempfile
     if requested:
         return requested
-    for d in ("/dev/shm", tempfile.gettempdir()):
+    for d in (tempfile.gettempdir(), "/dev/shm"):
         try:
             st = os.statvfs(d)
             if os.access(d, os.W_OK) and st.f_bavail * st.f_frsize > 1.5 * need_bytes:
@@ -276,8 +278,8 @@ def main():
                     help="cpu_baseline sample (pairs; ~10 s of CPU work on 16 cores at 2x150)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--io-dir", default="",
-                    help="where the FASTQ inputs and the SAM output go (default: /dev/shm when it has room, "
-                         "else the system temp dir)")
+                    help="where the FASTQ inputs and the SAM output go (default: the system temp dir when it "
+                         "has room, else /dev/shm)")
     ap.add_argument("--read-sets", type=int, default=3,
                     help="distinct synthetic read sets (FASTQ file pairs) rotated over the steps")
     ap.add_argument("--ref-len", type=int, default=0, help="override reference length (testing only)")
@@ -344,7 +346,7 @@ def main():
     # The FASTQ files are written once before timing (page cache warm, as a re-run of a
     # mapper over the same files would find them); every step truncates and rewrites its SAM.
     io_dir = pick_io_dir(args.io_dir, n_sets * P * (2 if wl["paired"] else 1) * (2 * wl["read_len"] + 80)
-                         + 2 * P * (2 if wl["paired"] else 1) * (2 * wl["read_len"] + 120))
+                         + max(args.steps, args.warmup) * P * (2 if wl["paired"] else 1) * (2 * wl["read_len"] + 120))
     tag = f"rsa_bench_{os.getpid()}_r{rank}"
     fqs = []
     t = time.time()
@@ -353,18 +355,26 @@ def main():
         f2 = os.path.join(io_dir, f"{tag}_s{s}_2.fq") if wl["paired"] else None
         b.write_fastq(f1, f2)
         fqs.append((f1, f2))
-    sam_path = os.path.join(io_dir, f"{tag}.sam")
+    # every step writes a SAM file of its own (a new file, as a mapping run makes one);
+    # the files are removed after the timed region
+    sam_paths = [os.path.join(io_dir, f"{tag}_step{s}.sam") for s in range(total_steps)]
     fq_bytes = sum(os.path.getsize(f) for pair in fqs for f in pair if f)
     log(rank, f"wrote {n_sets} FASTQ sets ({fq_bytes / 1e9:.2f} GB) to {io_dir} in {time.time()-t:.1f} s")
 
     def map_step(s):
         f1, f2 = fqs[s % n_sets]
-        return m.map_files(f1, f2, threads=threads, chunk_size=args.chunk_size, sam_path=sam_path)
+        return m.map_files(f1, f2, threads=threads, chunk_size=args.chunk_size, sam_path=sam_paths[s])
+
+    def drop_sams(upto):
+        for f in sam_paths[:upto]:
+            if os.path.exists(f):
+                os.remove(f)
 
     try:
         for s in range(args.warmup):
             st = map_step(s)
             log(rank, f"warmup {s}: {st.n_reads} reads in {st.map_seconds:.3f} s")
+        drop_sams(args.warmup)
         m.reset_kernel_stats()
 
         barrier()
@@ -381,7 +391,7 @@ def main():
             for f in shard.STAT_FIELDS:
                 totals[f] += getattr(st, f)
             hashes.append(st.sam_hash)
-            sam_file_bytes = os.path.getsize(sam_path)
+            sam_file_bytes = os.path.getsize(sam_paths[s])
             log(rank, f"step {s - args.warmup}: {st.n_reads} reads in {st.map_seconds:.3f} s "
                       f"({st.n_reads / st.map_seconds / 1e6:.4f} Mreads/s), SW {st.sw_calls}; thread-s: "
                       f"seed {st.t_seed:.2f} extend {st.t_extend:.2f} part {st.t_part:.2f} "
@@ -396,8 +406,7 @@ def main():
             for f in pair:
                 if f and os.path.exists(f):
                     os.remove(f)
-        if os.path.exists(sam_path):
-            os.remove(sam_path)
+        drop_sams(total_steps)
     # host CPU time of this rank's timed steps (all threads, user + system): the
     # host-bound part of the path, steadier than wall-time throughput on a shared box
     host_cpu_s = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)

@@ -373,19 +373,14 @@ static int map_source(rsam* m, ReadSource& src, int threads, int chunk_size, con
     po.chunk_size = chunk_size;
     po.digest = true;
     SamSink sk = st.f ? sink_fn : nullptr;
-    PosSink ps;                                 // a regular file: chunks written in parallel at their offsets
-    if (st.f && pos_sink_open(st.f, ps)) {
-        po.sink_at = pos_sink_write;
-        po.sink_at_user = &ps;
-    }
     PipelineResult res = src.paired() ? run_pipeline_pe(src, *m->eng, mc, po, sk, &st)
                                       : run_pipeline_se(src, *m->eng, mc, po, sk, &st);
     if (st.f) {
         FILE* f = st.f;
         st.f = nullptr;
-        if (fclose(f) != 0) throw std::runtime_error(std::string("write failed: ") + sam_path);
+        const bool bad = ferror(f) != 0;
+        if (fclose(f) != 0 || bad) throw std::runtime_error(std::string("write failed: ") + sam_path);
     }
-    if (ps.failed) throw std::runtime_error(std::string("write failed: ") + sam_path);
     res.map_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     fill_stats(res, out);
     return 0;

@@ -19,6 +19,7 @@
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
+#include <emmintrin.h>
 
 #include <algorithm>
 #include <condition_variable>
@@ -142,9 +143,46 @@ inline std::string_view strip_cr(std::string_view l) {
     return l;
 }
 
-// One record of the plain layout at p, as views; false (p unchanged) when the
-// bytes at p are anything else.  The conditions are those under which kseq's
-// record (FastxReader::next) is exactly header / sequence line / quality line:
+// Newlines of [p, end) in order, 64 bytes at a time: four SSE2 compares give a
+// 64-bit mask of the block's '\n' bytes, the set bits are taken one by one.  A
+// record's four line ends cost a few instructions each instead of a memchr call.
+// The block containing `end` is read with a scalar loop (no read past the mapping).
+struct NlIter {
+    const char* blk;                            // current 64-byte block
+    const char* end;
+    uint64_t mask;                              // newlines of blk not yet taken
+    NlIter(const char* p, const char* e) : blk(p), end(e) { mask = load(blk); }
+    uint64_t load(const char* q) const {
+        if (q + 64 <= end) {
+            const __m128i nl = _mm_set1_epi8('\n');
+            const uint64_t m0 = (uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128((const __m128i*)q), nl));
+            const uint64_t m1 = (uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128((const __m128i*)(q + 16)), nl));
+            const uint64_t m2 = (uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128((const __m128i*)(q + 32)), nl));
+            const uint64_t m3 = (uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128((const __m128i*)(q + 48)), nl));
+            return m0 | m1 << 16 | m2 << 32 | m3 << 48;
+        }
+        uint64_t m = 0;
+        for (const char* x = q; x < end; ++x)
+            if (*x == '\n') m |= 1ull << (x - q);
+        return m;
+    }
+    // the next '\n' at or after the current position, or `end` when there is none
+    const char* next() {
+        while (!mask) {
+            blk += 64;
+            if (blk >= end) { blk = end; return end; }
+            mask = load(blk);
+        }
+        const char* r = blk + __builtin_ctzll(mask);
+        mask &= mask - 1;
+        return r;
+    }
+};
+
+// One record of the plain layout starting at p (`it` positioned at p), as views;
+// false when the bytes at p are anything else (`it` then undefined: the caller
+// keeps a copy).  The conditions are those under which kseq's record
+// (FastxReader::next) is exactly header / sequence line / quality line:
 //  - the record starts with '@' and has four lines;
 //  - the third line starts with '+';
 //  - the sequence line is not empty and does not start with '>', '@', '+' or '\r'
@@ -152,27 +190,26 @@ inline std::string_view strip_cr(std::string_view l) {
 //    its first byte, then trailing blanks;
 //  - the quality line (one '\r' stripped) is as long as the sequence, so kseq
 //    stops reading quality after it.
-bool plain_record(const char*& p, const char* end, RecView& r) {
+inline bool plain_record(const char*& p, const char* end, NlIter& it, RecView& r) {
     if (p >= end || *p != '@') return false;
-    const char* q = p;
-    std::string_view line[4];
-    for (int k = 0; k < 4; ++k) {
-        if (q >= end) return false;
-        const char* nl = (const char*)memchr(q, '\n', (size_t)(end - q));
-        const char* le = nl ? nl : end;
-        line[k] = std::string_view(q, (size_t)(le - q));
-        q = nl ? nl + 1 : end;
-    }
-    if (line[2].empty() || line[2][0] != '+') return false;
-    std::string_view sq = line[1];
+    const char* e0 = it.next();
+    const char* e1 = it.next();
+    const char* e2 = it.next();
+    if (e2 >= end) return false;                // fewer than four lines
+    const char* e3 = it.next();
+    const char* l1 = e0 + 1;
+    const char* l2 = e1 + 1;
+    const char* l3 = e2 + 1;
+    if (l2 >= e2 || *l2 != '+') return false;
+    std::string_view sq(l1, (size_t)(e1 - l1));
     if (sq.empty()) return false;
     if (sq.size() >= 2 && sq.back() == '\r') sq.remove_suffix(1);
     const char c0 = sq[0];
     if (c0 == '>' || c0 == '@' || c0 == '+' || c0 == '\r') return false;
     while (!sq.empty() && (sq.back() == ' ' || sq.back() == '\t')) sq.remove_suffix(1);
-    const std::string_view ql = strip_cr(line[3]);
+    const std::string_view ql = strip_cr(std::string_view(l3, (size_t)(e3 - l3)));
     if (sq.empty() || ql.size() != sq.size()) return false;
-    std::string_view h = strip_cr(line[0].substr(1));
+    std::string_view h = strip_cr(std::string_view(p + 1, (size_t)(e0 - p - 1)));
     size_t ws = 0;
     while (ws < h.size() && h[ws] != ' ' && h[ws] != '\t' && h[ws] != '\v' && h[ws] != '\f' && h[ws] != '\r') ++ws;
     r.name = h.substr(0, ws);
@@ -181,19 +218,20 @@ bool plain_record(const char*& p, const char* end, RecView& r) {
     r.comment = h.substr(cs);
     r.seq = sq;
     r.qual = ql;
-    p = q;
+    p = e3 < end ? e3 + 1 : end;
     return true;
 }
 
 struct Block {
     std::vector<RecView> recs;
     std::vector<Record> owned;                  // records of the sequential reader (recs view them)
-    const char* map_begin = nullptr;            // mapped bytes the views use
-    size_t map_len = 0;
 };
 
 // The blocks of `per_block` records of one file, read by a thread of its own at
-// most `ahead` blocks past the highest block asked for.
+// most `ahead` blocks past the highest block asked for.  Mapped mode: the reader
+// asks the kernel to map the next window of the file in one call
+// (MADV_POPULATE_READ) instead of taking a page fault every few pages, and the
+// pages of blocks whose chunks are done leave the process again in 64 MB steps.
 class FileBlocks {
 public:
     FileBlocks(const std::string& path, size_t per_block, size_t ahead)
@@ -227,13 +265,26 @@ public:
         blocks_.erase(it);
         return true;
     }
-    // the pages of a released block's bytes leave this process (the file stays
-    // mapped; a page a neighbouring block still reads is faulted in again)
-    static void drop(const char* p, size_t n) {
-        if (!p || !n) return;
-        const uintptr_t pg = 4096;
-        const uintptr_t a = (uintptr_t)p & ~(pg - 1), b = ((uintptr_t)p + n) & ~(pg - 1);
-        if (b > a) madvise((void*)a, b - a, MADV_DONTNEED);
+    // block idx is no longer used: once every block before it is done too, the
+    // mapped bytes up to its end are dropped from this process (64 MB at a time;
+    // the file stays mapped, and the page cache keeps the data)
+    void done(size_t idx) {
+        if (!mf_.p) return;
+        static const bool keep = getenv("RSA_INPUT_DROP") && getenv("RSA_INPUT_DROP")[0] == '0';   // A/B
+        size_t from = 0, to = 0;
+        {
+            std::lock_guard<std::mutex> g(m_);
+            if (idx >= released_.size()) return;
+            released_[idx] = 1;
+            while (prefix_ < released_.size() && released_[prefix_]) prefix_++;
+            if (prefix_ == 0 || keep) return;
+            const size_t off = ends_[prefix_ - 1] & ~(size_t)4095;
+            if (off < dropped_ + (64u << 20)) return;
+            from = dropped_;
+            to = off;
+            dropped_ = off;
+        }
+        madvise((void*)(mf_.p + from), to - from, MADV_DONTNEED);
     }
 
 private:
@@ -246,13 +297,15 @@ private:
                     if (stop_) return;
                 }
                 Block b;
-                read_block(b);
+                const size_t end_off = read_block(b);
                 std::lock_guard<std::mutex> g(m_);
                 if (b.recs.empty()) {
                     finished_ = true;
                     cv_.notify_all();
                     return;
                 }
+                released_.push_back(0);
+                ends_.push_back(end_off);
                 blocks_.emplace(produced_++, std::move(b));
                 cv_.notify_all();
             }
@@ -262,17 +315,40 @@ private:
             cv_.notify_all();
         }
     }
-    void read_block(Block& b) {
+    // the mapped bytes from `pos_` on are in this process's page table at least `want` ahead
+    void populate(size_t want) {
+#ifdef MADV_POPULATE_READ
+        constexpr size_t kStep = 32u << 20;
+        if (populated_ >= mf_.n || populated_ >= pos_ + want) return;
+        const size_t from = std::max(populated_, pos_) & ~(size_t)4095;
+        const size_t to = std::min(mf_.n, from + kStep);
+        if (madvise((void*)(mf_.p + from), to - from, MADV_POPULATE_READ) != 0) populated_ = mf_.n;   // not supported
+        else populated_ = to;
+#else
+        (void)want;
+#endif
+    }
+    // returns the mapped offset the block ends at (0 in sequential mode)
+    size_t read_block(Block& b) {
         b.recs.reserve(per_block_);
         if (!seq_) {
+            populate(16u << 20);
             const char* end = mf_.p + mf_.n;
             const char* p = mf_.p + pos_;
-            b.map_begin = p;
+            NlIter it(p, end);
             RecView r;
-            while (b.recs.size() < per_block_ && p < end && plain_record(p, end, r)) b.recs.push_back(r);
-            b.map_len = (size_t)(p - b.map_begin);
+            while (b.recs.size() < per_block_ && p < end) {
+                const NlIter save = it;
+                const char* at = p;
+                if (!plain_record(p, end, it, r)) {
+                    it = save;
+                    p = at;
+                    break;
+                }
+                b.recs.push_back(r);
+            }
             pos_ = (size_t)(p - mf_.p);
-            if (b.recs.size() == per_block_ || p >= end) return;
+            if (b.recs.size() == per_block_ || p >= end) return pos_;
             // not the plain layout from here on: kseq over the rest of the mapped bytes
             seq_.reset(new FastxReader(p, (size_t)(end - p)));
         }
@@ -284,12 +360,14 @@ private:
             r = Record();
         }
         for (const Record& x : b.owned) b.recs.push_back(RecView(x));
+        return pos_;
     }
 
     std::string path_;
     size_t per_block_, ahead_;
     MappedFile mf_;
     size_t pos_ = 0;                            // mapped mode: next record's offset
+    size_t populated_ = 0;                      // mapped bytes already in the page table
     std::unique_ptr<FastxReader> seq_;          // sequential mode
     std::thread th_;
     std::mutex m_;
@@ -298,6 +376,9 @@ private:
     size_t produced_ = 0, horizon_ = 0;
     bool finished_ = false, stop_ = false;
     std::exception_ptr err_;
+    std::vector<uint8_t> released_;             // per produced block: its chunk is done
+    std::vector<size_t> ends_;                  // per produced block: mapped offset it ends at
+    size_t prefix_ = 0, dropped_ = 0;
 };
 
 class FastqSource final : public ReadSource {
@@ -305,7 +386,7 @@ public:
     FastqSource(const std::string& p1, const std::string& p2, bool interleaved, size_t chunk)
         : interleaved_(interleaved && p2.empty()) {
         const size_t per = (interleaved_ ? 2 : 1) * std::max<size_t>(1, chunk);
-        constexpr size_t kAhead = 4;
+        static const size_t kAhead = getenv("RSA_READ_AHEAD") ? (size_t)atol(getenv("RSA_READ_AHEAD")) : 4;
         f1_.reset(new FileBlocks(p1, per, kAhead));
         if (!p2.empty()) f2_.reset(new FileBlocks(p2, per, kAhead));
     }
@@ -322,8 +403,8 @@ public:
             if (!h1) return false;
             out.r1 = std::move(b1.recs);
             out.r2 = std::move(b2.recs);
-            keep(b1, out.owned1, out);
-            keep(b2, out.owned2, out);
+            out.owned1 = std::move(b1.owned);   // the vectors' buffers move, the records stay put
+            out.owned2 = std::move(b2.owned);
             return true;
         }
         if (!h1) return false;
@@ -332,19 +413,16 @@ public:
         } else {
             out.r1 = std::move(b1.recs);
         }
-        keep(b1, out.owned1, out);
+        out.owned1 = std::move(b1.owned);
         return true;
     }
     void release(InputChunk& c) override {
-        for (auto& m : c.mapped) FileBlocks::drop(m.first, m.second);
+        f1_->done(c.index);
+        if (f2_) f2_->done(c.index);
         c.clear();
     }
 
 private:
-    static void keep(Block& b, std::vector<Record>& owned, InputChunk& out) {
-        owned = std::move(b.owned);             // the vector's buffer moves, the records stay put
-        if (b.map_len) out.mapped.emplace_back(b.map_begin, b.map_len);
-    }
     bool interleaved_;
     std::unique_ptr<FileBlocks> f1_, f2_;
 };

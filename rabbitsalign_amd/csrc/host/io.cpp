@@ -964,42 +964,4 @@ void FastxReader::read_pair(const std::string& p1, const std::string& p2, std::v
 
 namespace rsa {
 
-bool pos_sink_open(FILE* f, PosSink& ps) {
-    if (!f || fflush(f) != 0) return false;
-    const int fd = fileno(f);
-    if (fd < 0) return false;
-    struct stat st;
-    if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode)) return false;    // pipes, terminals: sequential
-    // O_APPEND: pwrite ignores the offset and appends, so chunks would land in the order
-    // they finish (`>> out.sam`); the sequential sink keeps chunk order there
-    const int fl = fcntl(fd, F_GETFL);
-    if (fl < 0 || (fl & O_APPEND)) return false;
-    // stderr on the same file (`> out.sam 2>&1`): pwrite does not move the shared offset,
-    // so a message on stderr would land inside the SAM body; stay sequential
-    struct stat se;
-    if (fd != STDERR_FILENO && fstat(STDERR_FILENO, &se) == 0 && se.st_dev == st.st_dev && se.st_ino == st.st_ino)
-        return false;
-    const off_t at = lseek(fd, 0, SEEK_CUR);
-    if (at < 0) return false;
-    ps.fd = fd;
-    ps.base = (uint64_t)at;
-    return true;
-}
-
-void pos_sink_write(void* user, const char* chunk, size_t bytes, uint64_t offset) {
-    PosSink& ps = *(PosSink*)user;
-    uint64_t at = ps.base + offset;
-    while (bytes > 0) {
-        const ssize_t w = pwrite(ps.fd, chunk, bytes, (off_t)at);
-        if (w <= 0) {
-            if (w < 0 && errno == EINTR) continue;
-            ps.failed = true;
-            return;
-        }
-        chunk += w;
-        bytes -= (size_t)w;
-        at += (uint64_t)w;
-    }
-}
-
 }  // namespace rsa

@@ -172,11 +172,6 @@ int cli_main(int argc, char** argv, EngineFactory factory, const char* prog) {
         po.threads = o.threads; po.chunk_size = o.chunk_size; po.rg_id = o.rg_id;
         if (o.verbose) fprintf(stderr, "[%s] mapping %s%s%s%s\n", prog, o.reads1.c_str(), o.reads2.empty() ? "" : " + ",
                                o.reads2.c_str(), o.interleaved ? " (interleaved)" : "");
-        PosSink ps;                                 // a regular file: chunks written in parallel at their offsets
-        if (pos_sink_open(out, ps)) {
-            po.sink_at = pos_sink_write;
-            po.sink_at_user = &ps;
-        }
         // the reads are streamed: a reader thread per file parses chunks while the
         // workers map (InputBuffer::read_records, pc.cpp:74-107)
         std::unique_ptr<ReadSource> src =
@@ -187,11 +182,9 @@ int cli_main(int argc, char** argv, EngineFactory factory, const char* prog) {
         if (o.interleaved && o.verbose)
             fprintf(stderr, "[%s] interleaved input: %lu unpaired records (not mapped, as in the reference's "
                             "paired-end task)\n", prog, (unsigned long)res.singletons);
-        if (ps.fd >= 0) {                            // the stream's position trails the positional writes
-            if (fseeko(out, 0, SEEK_END) != 0) throw std::runtime_error("cannot seek the output");
-        }
-        if (out != stdout) fclose(out); else fflush(out);
-        if (ps.failed) throw std::runtime_error("write failed: " + (o.out_file.empty() ? std::string("stdout") : o.out_file));
+        const bool bad = ferror(out) != 0;
+        if ((out != stdout ? fclose(out) : fflush(out)) != 0 || bad)
+            throw std::runtime_error("write failed: " + (o.out_file.empty() ? std::string("stdout") : o.out_file));
         fprintf(stderr,
                 "[%s] engine %s | index %.2f s, upload %.2f s | mapped %lu reads in %.3f s = %.4f Mreads/s | "
                 "SW calls %lu, tried %lu, inconsistent NAMs %lu, NAM rescue %lu, mate rescue %lu\n",

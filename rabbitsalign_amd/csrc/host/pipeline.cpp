@@ -87,15 +87,40 @@ static int wait_workers(const Engine& eng, int threads) {
     return eng.offloads() ? (3 * threads) / 4 : 0;
 }
 
+// Chunks' SAM text in chunk order (OutputBuffer::output_records, pc.cpp:119-135).
+// One writer thread of its own hands the text to the sink, so no worker ever
+// blocks on the output file and nobody contends for it: the page-cache writes of
+// one file are serialised by the kernel anyway (the inode lock), and parallel
+// pwrite()s only spun on that lock.  Workers wait only when more
+// than kMaxQueued bytes are waiting for the writer.
 struct OrderedSink {
     SamSink sink;
     void* user;
     bool digest = false;
+    static constexpr size_t kMaxQueued = 768u << 20;
     std::mutex m;
+    std::condition_variable cv, room_cv;
     std::map<size_t, std::pair<SamText, SamDigest>> pending;
+    std::deque<SamText> queue;                // in chunk order, for the writer
+    size_t queued_bytes = 0;
     size_t next = 0;
     uint64_t bytes = 0;
     SamDigest total;
+    bool closing = false;
+    std::thread writer;
+    OrderedSink(SamSink s, void* u, bool d) : sink(s), user(u), digest(d) {
+        if (sink) writer = std::thread([this] { write_loop(); });
+    }
+    ~OrderedSink() { close(); }
+    // every chunk written (the writer drained and stopped)
+    void close() {
+        {
+            std::lock_guard<std::mutex> g(m);
+            closing = true;
+        }
+        cv.notify_all();
+        if (writer.joinable()) writer.join();
+    }
     // written chunks' buffers, kept at capacity for the next chunks (and the next
     // mapping calls): a fresh ~10 MB buffer per chunk is memory the first write
     // page-faults in
@@ -123,61 +148,49 @@ struct OrderedSink {
         s.clear();
         sp.v.push_back(std::move(s));
     }
-    SamSinkAt sink_at = nullptr;   // positional mode (PipelineOptions::sink_at)
-    void* at_user = nullptr;
-    std::vector<std::pair<uint64_t, SamText>> ready;   // positional mode: offset known, not written yet
-    bool writing = false;     // a worker is in the sink: it writes every chunk that becomes next
-    // `made`: the chunk's digest, folded in while its text was written (Sam::digest_into).
-    // One writer at a time keeps the sink calls in chunk order, and it calls the sink
-    // outside the lock: the other workers file their chunks and go back to mapping
-    // instead of waiting for a file write
+    // `made`: the chunk's digest, folded in while its text was written (Sam::digest_into)
     void put(size_t idx, SamText&& s, const SamDigest* made = nullptr) {
         SamDigest d;
         if (digest) d = made ? *made : SamDigest::of(s.data(), s.size());   // in the calling worker
         std::unique_lock<std::mutex> g(m);
         pending.emplace(idx, std::make_pair(std::move(s), d));
-        if (sink_at) {
-            // offsets in chunk order as chunks become next; the writes themselves run in
-            // parallel, each ready chunk taken by whichever worker is here
-            for (auto it = pending.find(next); it != pending.end(); it = pending.find(next)) {
-                const uint64_t off = bytes;
-                bytes += it->second.first.size();
-                total.append(it->second.second);
-                ready.emplace_back(off, std::move(it->second.first));
-                pending.erase(it);
-                next++;
-            }
-            while (!ready.empty()) {
-                std::pair<uint64_t, SamText> w = std::move(ready.back());
-                ready.pop_back();
-                g.unlock();
-                sink_at(at_user, w.second.data(), w.second.size(), w.first);
-                give_back(w.second);
-                g.lock();
-            }
-            return;
-        }
-        if (writing) return;
-        writing = true;
+        bool moved = false;
         for (auto it = pending.find(next); it != pending.end(); it = pending.find(next)) {
-            SamText text = std::move(it->second.first);
-            bytes += text.size();
+            bytes += it->second.first.size();
             total.append(it->second.second);
+            if (sink) {
+                queued_bytes += it->second.first.size();
+                queue.push_back(std::move(it->second.first));
+                moved = true;
+            } else {
+                give_back(it->second.first);
+            }
             pending.erase(it);
             next++;
-            g.unlock();
-            if (sink) sink(user, text.data(), text.size());
-            give_back(text);
-            g.lock();
         }
-        writing = false;
+        if (moved) cv.notify_one();
+        room_cv.wait(g, [&] { return queued_bytes <= kMaxQueued; });
+    }
+    void write_loop() {
+        std::unique_lock<std::mutex> g(m);
+        for (;;) {
+            cv.wait(g, [&] { return closing || !queue.empty(); });
+            if (queue.empty()) return;          // closing and drained
+            SamText t = std::move(queue.front());
+            queue.pop_front();
+            g.unlock();
+            sink(user, t.data(), t.size());
+            const size_t n = t.size();
+            give_back(t);
+            g.lock();
+            queued_bytes -= n;
+            room_cv.notify_all();
+        }
     }
 };
 
 struct PeChunk {
     InputChunk in;                            // the source's records; in.r1/in.r2[i].seq upper-cased by pe_load
-    const std::vector<RecView>& r1() const { return in.r1; }
-    const std::vector<RecView>& r2() const { return in.r2; }
     size_t size() const { return in.r1.size(); }
     // both mates' upper-cased sequences (pc.cpp:1586-1587) back to back, read 2i + m at
     // seqoff[2i + m]; in memory the engine can DMA from (Engine::io_alloc) when it has one,
@@ -515,9 +528,7 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
                                SamSink sink, void* user) {
     const auto t0 = Clock::now();
     PipelineResult result;
-    OrderedSink os{sink, user, opt.digest};
-    os.sink_at = opt.sink_at;
-    os.at_user = opt.sink_at_user;
+    OrderedSink os(sink, user, opt.digest);
     const int T = std::max(1, opt.threads);
     const bool offl = eng.offloads();
     const int W = T + wait_workers(eng, T);
@@ -763,6 +774,7 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
     // chunks seeded ahead but never mapped (a failure): their input goes back to the source
     for (auto& kv : seeded) recycle(std::move(kv.second));
     if (handed) recycle(std::move(handed));
+    os.close();                                  // the last SAM byte is with the sink
     if (failure) std::rethrow_exception(failure);
     result.stats = stats_all;
     result.phases = phases_all;
@@ -817,9 +829,7 @@ PipelineResult run_pipeline_se(ReadSource& src, Engine& eng, const MapContext& m
                                SamSink sink, void* user) {
     auto t0 = std::chrono::steady_clock::now();
     PipelineResult result;
-    OrderedSink os{sink, user, opt.digest};
-    os.sink_at = opt.sink_at;
-    os.at_user = opt.sink_at_user;
+    OrderedSink os(sink, user, opt.digest);
     std::atomic<size_t> next{0};
     std::mutex stat_m;
     const int T = std::max(1, opt.threads);
@@ -919,6 +929,7 @@ PipelineResult run_pipeline_se(ReadSource& src, Engine& eng, const MapContext& m
         result.stats.add(local);
     };
     WorkerPool::get().run(T + wait_workers(eng, T), worker);
+    os.close();                                  // the last SAM byte is with the sink
     if (failure) std::rethrow_exception(failure);
     result.map_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     result.sam_bytes = os.bytes;

@@ -578,9 +578,8 @@ struct InputChunk {
     std::vector<RecView> r1, r2;                // pairs (r2 empty for single-end)
     uint64_t singletons = 0;                    // interleaved: unpaired records, read and dropped
     std::vector<Record> owned1, owned2;         // records parsed by the sequential reader
-    std::vector<std::pair<const char*, size_t>> mapped;   // mapped file bytes the views use
     void clear() {
-        r1.clear(); r2.clear(); singletons = 0; owned1.clear(); owned2.clear(); mapped.clear();
+        r1.clear(); r2.clear(); singletons = 0; owned1.clear(); owned2.clear();
     }
 };
 
@@ -619,18 +618,11 @@ int estimate_read_length(const std::string& path1, const std::string& path2, boo
 // called at the start of every pipeline worker thread (profiling hooks; null by default)
 extern void (*g_worker_start_hook)();
 
-// positional form: the chunk's bytes belong at `offset` of the SAM body (chunk order
-// fixes the offsets; several chunks may be written at once)
-using SamSinkAt = void (*)(void* user, const char* chunk, size_t bytes, uint64_t offset);
 struct PipelineOptions {
     int threads = 3;
     int chunk_size = 10000;
     std::string rg_id;
     bool digest = false;   // compute PipelineResult::sam_digest (in the workers, in parallel)
-    // when set, SAM chunks go here at their body offsets instead of to the sequential
-    // sink, each written by the worker that finds it ready (parallel file writes)
-    SamSinkAt sink_at = nullptr;
-    void* sink_at_user = nullptr;
 };
 
 // --interleaved input (InputBuffer::read_records + distribute_interleaved,
@@ -675,16 +667,6 @@ struct PipelineResult {
 // chunks are processed strictly in the single-worker timeline until the insert
 // size estimate freezes, then chunk-parallel over `threads` host workers.
 using SamSink = void (*)(void* user, const char* chunk, size_t bytes);
-// positional SAM writes into a seekable file after what it already holds (the
-// header): pos_sink_open flushes `f` and returns false when it cannot take them
-// (a pipe, a terminal); failed is set when a write fails
-struct PosSink {
-    int fd = -1;
-    uint64_t base = 0;
-    std::atomic<bool> failed{false};
-};
-bool pos_sink_open(FILE* f, PosSink& ps);
-void pos_sink_write(void* user, const char* chunk, size_t bytes, uint64_t offset);
 // the pipeline over a read source (ReadSource: streamed files or records in memory)
 PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& mc, const PipelineOptions& opt,
                                SamSink sink, void* user);

@@ -7,8 +7,8 @@ src/pc.cpp:74-107) and the SAM sinks.
 - resident memory does not grow with the input: mapping twice the reads raises
   the peak RSS by far less than the extra FASTQ bytes (the old CLI loaded the
   whole file before mapping);
-- SAM through `>> out.sam` (O_APPEND) and through `> out.sam 2>&1` is the same
-  body as `-o` (the positional sink steps aside for both);
+- SAM through `>> out.sam`, `> out.sam 2>&1`, `> out.sam` and a pipe is the
+  same body as `-o` (one writer thread writes the chunks in order);
 - rsam_map_files (files streamed) == rsam_map (records in memory) == CLI.
 """
 import os
@@ -183,3 +183,18 @@ def test_unequal_mate_files_fail(data):
     r = subprocess.run([CPU_PORT, "--use-index", "-t", "2", "-o", str(d / "uneq.sam"), fa, str(p1), str(p2)],
                        capture_output=True, text=True)
     assert r.returncode == 1 and "different record counts" in r.stderr
+
+
+@pytest.mark.parametrize("mode", ["stdout_file", "stdout_pipe"])
+def test_sam_to_stdout(data, mode):
+    """stdout redirected to a file or read through a pipe carries the -o bytes."""
+    d, fa, f1, f2, want = data
+    out = d / f"sink_{mode}.sam"
+    args = [CPU_PORT, "--use-index", "-t", "4", "--chunk-size", "256", fa, f1, f2]
+    if mode == "stdout_file":
+        with open(out, "w") as fo:
+            subprocess.run(args, stdout=fo, stderr=subprocess.DEVNULL, check=True)
+    else:
+        r = subprocess.run(args, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, check=True)
+        out.write_bytes(r.stdout)
+    assert sam_body(out) == want
