@@ -282,7 +282,7 @@ enum {
     RSA_K_EXT_SCAN = 5,    /* SSW forward/reverse score scans (ssw.c:121-620) */
     RSA_K_EXT_BAND = 6,    /* banded_sw + traceback + Aligner::align, 16 lanes/job (ssw.c:622-790, aligner.cpp:114-210) */
     RSA_K_EXT_BAND_WIDE = 7, /* the same, 64 lanes/job, for the jobs the 16-lane kernel queues */
-    RSA_K_EXT_BAND_LANE = 8, /* the same, one lane per job with global scratch (bands > 64 cells) */
+    RSA_K_EXT_BAND_PANEL = 8, /* the same, one wave per job sweeping 64-cell panels (bands > 64 cells) */
     RSA_K_SITES = 9,       /* per-NAM orientation + Hamming site checks (aln.cpp:60-93, 374-431) */
     RSA_K_COUNT = 10
 };

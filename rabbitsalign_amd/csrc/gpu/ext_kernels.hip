@@ -15,10 +15,11 @@
 //              striping artefact (cross-stripe F never feeds E, ssw.c:275-289)
 //              is reproduced with the byte (16 stripes) / word (8 stripes)
 //              layout of the reference.  Query/reference codes sit in LDS.
-//  k_ext_band  one lane per job: banded_sw (ssw.c:590-774) restated literally
-//              (its array-index quirks are observable), traceback, =/X CIGAR
-//              (ssw_cpp.cpp:126-210) and the end-bonus extension
-//              (aligner.cpp:147-207).
+//  k_ext_band16 / k_ext_band64 / k_ext_band_panel  banded_sw (ssw.c:590-774)
+//              with 16 or 64 lanes per job, one band cell per lane, or 64-lane
+//              panels swept along each band row for the widest bands; then the
+//              traceback, =/X CIGAR (ssw_cpp.cpp:126-210) and the end-bonus
+//              extension (aligner.cpp:147-207).
 //
 // Integer DP, no MFMA.  Roofline: VALU-bound (cells/s), see DESIGN.md.
 #include <hip/hip_runtime.h>
@@ -350,114 +351,7 @@ k_ext_scan(const ExtJobDev* __restrict__ jobs, int n_jobs, const int* __restrict
     if (lane == 0) out[j] = res;
 }
 
-// ---------------------------------------------------------------------------
-// banded_sw + traceback + CIGAR post-processing, one lane per job
-// ---------------------------------------------------------------------------
-#define SET_U(w, i, j) ((j) - max((i) - (w), 0) + 1)
-#define SET_D(w, i, j, p) (((j) - max((i) - (w), 0)) * 3 + (p))
-
 __device__ __forceinline__ uint32_t cig(uint32_t len, uint32_t op) { return (len << 4) | op; }
-
-struct BandScratch {
-    int* hb; int* eb; int* hc;   // arr_cap ints each
-    int8_t* dir;                 // dir_cap bytes
-    int arr_cap;
-    int64_t dir_cap;
-};
-
-// Returns #ops written to `out` (reversed order fixed), -1 traceback error, -2 scratch overflow.
-__device__ int banded_sw_dev(const char* __restrict__ refw, int ref_begin, int rlen_total, const char* __restrict__ qry,
-                             int ref_len, int read_len, int score, int gO, int gE, int band_width, int match,
-                             int mismatch, BandScratch sc, uint32_t* out) {
-    const int len = ref_len > read_len ? ref_len : read_len;
-    int s1 = 8;
-    int64_t s2 = 1024;
-    if (s1 > sc.arr_cap || s2 > sc.dir_cap) return -2;
-    for (int z = 0; z < s1; ++z) sc.hb[z] = sc.eb[z] = sc.hc[z] = 0;
-    for (int64_t z = 0; z < s2; ++z) sc.dir[z] = 0;
-    int* h_b = sc.hb; int* e_b = sc.eb; int* h_c = sc.hc;
-    int8_t* direction = sc.dir;
-    int8_t* direction_line = direction;
-    int max_v = 0, width, width_d;
-    do {
-        width = band_width * 2 + 3;
-        width_d = band_width * 2 + 1;
-        while (width >= s1) {
-            int ns = s1 + 1;
-            ns--; ns |= ns >> 1; ns |= ns >> 2; ns |= ns >> 4; ns |= ns >> 8; ns |= ns >> 16; ns++;
-            if (ns > sc.arr_cap) return -2;
-            for (int z = s1; z < ns; ++z) h_b[z] = e_b[z] = h_c[z] = 0;
-            s1 = ns;
-        }
-        while ((int64_t)width_d * read_len * 3 >= s2) {
-            int64_t ns = s2 + 1;
-            ns--; ns |= ns >> 1; ns |= ns >> 2; ns |= ns >> 4; ns |= ns >> 8; ns |= ns >> 16; ns |= ns >> 32; ns++;
-            if (ns > sc.dir_cap) return -2;
-            for (int64_t z = s2; z < ns; ++z) direction[z] = 0;
-            s2 = ns;
-        }
-        direction_line = direction;
-        for (int j = 1; j < width - 1; j++) h_b[j] = 0;
-        for (int i = 0; i < read_len; i++) {
-            int beg = max(0, i - band_width), end = min(ref_len - 1, i + band_width), u = 0;
-            const int edge = end + 1 < width - 1 ? end + 1 : width - 1;
-            int f = 0;
-            h_b[0] = e_b[0] = h_b[edge] = e_b[edge] = h_c[0] = 0;
-            direction_line = direction + (int64_t)width_d * i * 3;
-            const int rcode_i = ssw_code((unsigned char)qry[i]);
-            for (int j = beg; j <= end; j++) {
-                u = SET_U(band_width, i, j);
-                const int e = SET_U(band_width, i - 1, j);
-                const int b = SET_U(band_width, i, j - 1);
-                const int d = SET_U(band_width, i - 1, j - 1);
-                const int de = SET_D(band_width, i, j, 0), df = SET_D(band_width, i, j, 1), dh = SET_D(band_width, i, j, 2);
-                int temp1 = i == 0 ? -gO : h_b[e] - gO;
-                int temp2 = i == 0 ? -gE : e_b[e] - gE;
-                e_b[u] = temp1 > temp2 ? temp1 : temp2;
-                direction_line[de] = temp1 > temp2 ? 3 : 2;
-                temp1 = h_c[b] - gO;
-                temp2 = f - gE;
-                f = temp1 > temp2 ? temp1 : temp2;
-                direction_line[df] = temp1 > temp2 ? 5 : 4;
-                const int e1 = e_b[u] > 0 ? e_b[u] : 0;
-                const int f1 = f > 0 ? f : 0;
-                temp1 = e1 > f1 ? e1 : f1;
-                const int gj = ref_begin + j;
-                const int rcj = (gj >= 0 && gj < rlen_total) ? ssw_code((unsigned char)refw[gj]) : 4;
-                temp2 = h_b[d] + subst(rcj, rcode_i, match, mismatch);
-                h_c[u] = temp1 > temp2 ? temp1 : temp2;
-                if (h_c[u] > max_v) max_v = h_c[u];
-                if (temp1 <= temp2) direction_line[dh] = 1;
-                else direction_line[dh] = e1 > f1 ? direction_line[de] : direction_line[df];
-            }
-            for (int j = 1; j <= u; j++) h_b[j] = h_c[j];
-        }
-        band_width *= 2;
-    } while (max_v < score && band_width <= len);
-    band_width /= 2;
-
-    int i = read_len - 1, j = ref_len - 1, e = 0, l = 0, temp2 = 2;
-    uint32_t op = 0, prev_op = 0;   // 0 = M, 1 = I, 2 = D (SSW encoded_ops)
-    while (i >= 0 && j > 0) {
-        const int temp1 = SET_D(band_width, i, j, temp2);
-        const int64_t at = (direction_line - direction) + temp1;
-        if (at < 0 || at >= s2) return -1;
-        switch (direction_line[temp1]) {
-            case 1: --i; --j; temp2 = 2; direction_line -= width_d * 3; op = 0; break;
-            case 2: --i; temp2 = 0; direction_line -= width_d * 3; op = 1; break;
-            case 3: --i; temp2 = 2; direction_line -= width_d * 3; op = 1; break;
-            case 4: --j; temp2 = 1; op = 2; break;
-            case 5: --j; temp2 = 2; op = 2; break;
-            default: return -1;
-        }
-        if (op == prev_op) ++e;
-        else { ++l; out[l - 1] = cig((uint32_t)e, prev_op); prev_op = op; e = 1; }
-    }
-    if (op == 0) { ++l; out[l - 1] = cig((uint32_t)e + 1, op); }
-    else { l += 2; out[l - 2] = cig((uint32_t)e, op); out[l - 1] = cig(1, 0); }
-    for (int s = 0, t = l - 1; s < t; ++s, --t) { const uint32_t x = out[s]; out[s] = out[t]; out[t] = x; }
-    return l;
-}
 
 // Cigar::push merge rule (src/cigar.hpp:52-59)
 __device__ __forceinline__ void cpush(uint32_t* c, int& n, uint32_t op, uint32_t len) {
@@ -607,58 +501,6 @@ __device__ __forceinline__ void w2_check(const ScanRes& sr, int pscore, int mism
     }
 }
 
-__global__ void __launch_bounds__(64)
-k_ext_band(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan, int n_jobs,
-           const int* __restrict__ idx_list, int job_base,
-           const char* __restrict__ qbuf, const char* __restrict__ ref, uint32_t* __restrict__ cig_pool,
-           rsa_aln* __restrict__ out, uint8_t* __restrict__ scratch, int64_t scr_stride, int arr_cap,
-           int64_t dir_cap, int match, int mismatch, int gO, int gE, int bonus, int* __restrict__ overflow,
-           int over_code) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n_jobs) return;
-    const int j = idx_list ? idx_list[t] : job_base + t;
-    const ExtJobDev jb = jobs[j];
-    const ScanRes sr = scan[j];
-    rsa_aln a;
-    a.sw_score = 0; a.edit_distance = 0; a.ref_start = a.ref_end = a.query_start = a.query_end = 0;
-    a.cigar_offset = jb.cig_off; a.cigar_len = 0; a.pad_ = 0;
-    if (sr.status != 0) {                       // ref > 2000 (aligner.cpp:119-125)
-        a.edit_distance = 100000; a.sw_score = -1000000;
-        out[j] = a;
-        return;
-    }
-    const char* q = qbuf + jb.q_off;
-    const char* r = ref + jb.r_off;
-    const int qlen = (int)jb.qlen, rlen = (int)jb.rlen;
-    uint32_t* c = cig_pool + jb.cig_off;
-    if (sr.flag != 0) {                         // aligner.cpp:131-136
-        a.edit_distance = 100000; a.sw_score = -100000;
-        out[j] = a;
-        return;
-    }
-    // banded_sw over ref[ref_begin1..ref_end1] x read[read_begin1..read_end1] (ssw.c:899-918)
-    const int ref_l = sr.ref_end1 - sr.ref_begin1 + 1;
-    const int read_l = sr.read_end1 - sr.read_begin1 + 1;
-    const int bw = abs(ref_l - read_l) + 1;
-    uint8_t* my = scratch + (int64_t)t * scr_stride;
-    BandScratch bs;
-    bs.hb = (int*)my; bs.eb = bs.hb + arr_cap; bs.hc = bs.eb + arr_cap;
-    bs.dir = (int8_t*)(bs.hc + arr_cap);
-    bs.arr_cap = arr_cap; bs.dir_cap = dir_cap;
-    // raw banded ops live in the job's scratch, the final CIGAR is built in its slot
-    uint32_t* raw = (uint32_t*)(bs.dir + dir_cap);
-    const int nraw = banded_sw_dev(r, sr.ref_begin1, rlen, q + sr.read_begin1, ref_l, read_l, sr.score1, gO, gE, bw,
-                                   match, mismatch, bs, raw);
-    if (nraw == -2) { overflow[j] = over_code; return; }
-    if (nraw < 0) {                             // banded_sw failed -> flag 1
-        a.edit_distance = 100000; a.sw_score = -100000;
-        out[j] = a;
-        return;
-    }
-    (void)ext_finish(jb, sr, q, r, raw, nraw, c, a, match, mismatch, bonus, gO, gE);
-    out[j] = a;
-}
-
 // ---------------------------------------------------------------------------
 // Group-parallel banded_sw: G lanes per job (G = 16: 4 jobs per wave; G = 64:
 // one job per wave).
@@ -678,7 +520,7 @@ k_ext_band(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan,
 //                appended to a device queue (no host round trip).
 //  k_ext_band64  drains that queue, one wave per job, 32 KB direction matrix
 //                in LDS.  Whatever still does not fit is flagged in `overflow`
-//                for the one-lane kernel with global scratch (k_ext_band).
+//                for the panel kernel with global scratch (k_ext_band_panel).
 // ---------------------------------------------------------------------------
 #define BG_NEG (-0x20000000)
 
@@ -964,6 +806,175 @@ k_ext_band64(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
         if (!done && z == 0) { overflow[j] = 1; atomicAdd(ocount, 1); }
         WSYNC();
     }
+}
+
+// ---------------------------------------------------------------------------
+// k_ext_band_panel: bands too wide for one wave (band rows longer than 64 cells,
+// up to the 2 x 2000 + 1 cells a 2 kb window can need) or direction matrices
+// larger than LDS.  One wave per job.  Each band row is swept in panels of 64
+// cells: lane z computes cell 64p + z + 1 of panel p, E and the diagonal from
+// the previous row's h_b / e_b, and F as the same max-plus prefix scan as the
+// 16/64-lane kernels, entered with the F and H' of the panel before it (a
+// scalar carry read from lane 63).  h_b / e_b live in LDS with the reference's
+// index layout (SET_U, ssw.c:600-601), so every out-of-band read and the
+// values a band doubling leaves behind are the reference's; the current row's
+// H reaches h_b one panel late (after the next panel has read the previous
+// row), which is the reference's end-of-row copy h_b[1..u] = h_c[1..u].  The
+// direction matrix (SET_D layout, zero-filled as it grows) is in global
+// scratch; lane 0 walks the traceback over it once the band passes are done.
+// ---------------------------------------------------------------------------
+#define BP_KW 4104        // h_b / e_b entries: width = 2 * bw + 3 <= 2 * 2000 + 3
+#define BP_QCAP 1024      // query segment (rsa_extend refuses longer queries)
+#define BP_RCAP 2048      // reference segment (windows > 2000 are sentinels)
+
+__global__ void __launch_bounds__(64)
+k_ext_band_panel(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan, int n_jobs,
+                 const int* __restrict__ idx_list, const char* __restrict__ qbuf, const char* __restrict__ ref,
+                 uint32_t* __restrict__ cig_pool, rsa_aln* __restrict__ out, uint8_t* __restrict__ scratch,
+                 int64_t scr_stride, int64_t dir_cap, int match, int mismatch, int gO, int gE, int bonus,
+                 int* __restrict__ overflow, int over_code) {
+    __shared__ int s_hb[BP_KW];
+    __shared__ int s_eb[BP_KW];
+    __shared__ uint8_t s_qc[BP_QCAP];
+    __shared__ uint8_t s_rc[BP_RCAP];
+    const int z = threadIdx.x & 63;
+    const int t = blockIdx.x;
+    if (t >= n_jobs) return;
+    const int j = idx_list[t];
+    const ExtJobDev jb = jobs[j];
+    const ScanRes sr = scan[j];
+    if (sr.status != 0) {                            // ref > 2000 (aligner.cpp:119-125)
+        if (z == 0) aln_sentinel(out, j, jb, -1000000);
+        return;
+    }
+    if (sr.flag != 0) {                              // aligner.cpp:131-136
+        if (z == 0) aln_sentinel(out, j, jb, -100000);
+        return;
+    }
+    const char* q = qbuf + jb.q_off;
+    const char* r = ref + jb.r_off;
+    const int rlen = (int)jb.rlen;
+    const int ref_begin = sr.ref_begin1;
+    const int ref_l = sr.ref_end1 - sr.ref_begin1 + 1;
+    const int read_l = sr.read_end1 - sr.read_begin1 + 1;
+    const int len = ref_l > read_l ? ref_l : read_l;
+    if (read_l <= 0 || ref_l <= 0 || read_l > BP_QCAP || ref_l > BP_RCAP || gO < gE || 2 * len + 3 > BP_KW) {
+        if (z == 0) overflow[j] = over_code;
+        return;
+    }
+    int8_t* dir = (int8_t*)(scratch + (int64_t)t * scr_stride);
+    uint32_t* raw = (uint32_t*)(scratch + (int64_t)t * scr_stride + dir_cap);
+    for (int x = z; x < read_l; x += 64) s_qc[x] = (uint8_t)ssw_code((unsigned char)q[sr.read_begin1 + x]);
+    for (int x = z; x < ref_l; x += 64) {
+        const int gj = ref_begin + x;
+        s_rc[x] = (uint8_t)((gj >= 0 && gj < rlen) ? ssw_code((unsigned char)r[gj]) : 4);
+    }
+    for (int x = z; x < BP_KW; x += 64) { s_hb[x] = 0; s_eb[x] = 0; }
+    int64_t s2 = 0;                                  // direction bytes zeroed so far
+    int64_t s2_ref = 1024;                           // the reference's direction size (traceback bound)
+    int bw = abs(ref_l - read_l) + 1, max_v = 0, width_d = 0;
+    WSYNC();
+    do {
+        const int width = bw * 2 + 3;
+        width_d = bw * 2 + 1;
+        while ((int64_t)width_d * read_l * 3 >= s2_ref) s2_ref *= 2;
+        if (s2_ref > dir_cap) {
+            if (z == 0) overflow[j] = over_code;
+            return;
+        }
+        // the direction matrix grows zero-filled (only its first s2_ref bytes are ever read)
+        for (int64_t x = s2 + 4 * z; x < s2_ref; x += 256) *(int*)(dir + x) = 0;
+        s2 = s2_ref;
+        for (int x = 1 + z; x <= width - 2; x += 64) s_hb[x] = 0;
+        __threadfence();                             // zeroes before the band's own stores, from any lane
+        WSYNC();
+        int lmax = 0;
+        for (int i = 0; i < read_l; ++i) {
+            const int beg = max(0, i - bw), end = min(ref_l - 1, i + bw);
+            const int edge = end + 1 < width - 1 ? end + 1 : width - 1;
+            const int ncell = end - beg + 1;         // u = 1 .. ncell
+            const int sh = i - bw >= 1 ? 1 : 0;       // SET_U(i-1, j) - SET_U(i, j)
+            if (z == 0) { s_hb[0] = 0; s_eb[0] = 0; s_hb[edge] = 0; s_eb[edge] = 0; }
+            WSYNC();
+            const int qv = s_qc[i];
+            int8_t* dline = dir + (int64_t)width_d * 3 * i;
+            int Fc = 0, HPc = 0;                     // f and h_c[u-1]'s H' entering the panel
+            int H_prev = 0, u_prev = 0;
+            bool on_prev = false;
+            for (int base = 0; base < ncell; base += 64) {
+                const int u = base + z + 1;
+                const bool on = u <= ncell;
+                const int ue = min(u + sh, BP_KW - 1), ud = u - 1 + sh;
+                const int hb_e = s_hb[ue], eb_e = s_eb[ue], hb_d = s_hb[ud];
+                WSYNC();                             // the previous row's values are read: update them
+                if (on_prev) s_hb[u_prev] = H_prev;
+                const int t1 = i == 0 ? -gO : hb_e - gO;
+                const int t2 = i == 0 ? -gE : eb_e - gE;
+                const int E = t1 > t2 ? t1 : t2;
+                const int de = t1 > t2 ? 3 : 2;
+                if (on) s_eb[u] = E;
+                const int rv = on ? s_rc[beg + u - 1] : 4;
+                const int diag = hb_d + ((rv == qv && rv < 4) ? match : -mismatch);
+                const int e1 = E > 0 ? E : 0;
+                const int hp = e1 > diag ? e1 : diag;
+                const int left_hp = __builtin_amdgcn_update_dpp(0, hp, 0x138, 0xf, 0xf, false);   // lane z-1
+                const int A = (z == 0 ? HPc : left_hp) - gO;
+                const int F = max(gscan_f<64>(A, gE), Fc - (z + 1) * gE);
+                const int left_f = __builtin_amdgcn_update_dpp(0, F, 0x138, 0xf, 0xf, false);
+                const int f_prev = z == 0 ? Fc : left_f;
+                const int df = A > f_prev - gE ? 5 : 4;
+                const int f1 = F > 0 ? F : 0;
+                const int m = e1 > f1 ? e1 : f1;
+                const int H = m > diag ? m : diag;
+                const int dh = m <= diag ? 1 : (e1 > f1 ? de : df);
+                if (on) {
+                    int8_t* dl = dline + 3 * (u - 1);
+                    dl[0] = (int8_t)de; dl[1] = (int8_t)df; dl[2] = (int8_t)dh;
+                    lmax = H > lmax ? H : lmax;
+                }
+                Fc = __builtin_amdgcn_readlane(F, 63);
+                HPc = __builtin_amdgcn_readlane(hp, 63);
+                H_prev = H;
+                u_prev = u;
+                on_prev = on;
+            }
+            if (on_prev) s_hb[u_prev] = H_prev;      // the row's last panel: h_b[1..u] = h_c[1..u]
+            WSYNC();
+        }
+        lmax = gmax<64>(lmax);
+        if (lmax > max_v) max_v = lmax;
+        bw *= 2;
+    } while (max_v < sr.score1 && bw <= len);
+    __threadfence();                                 // direction bytes of every lane visible to lane 0
+    WSYNC();
+    if (z != 0) return;
+    bw /= 2;
+
+    // traceback (ssw.c:748-776)
+    rsa_aln a;
+    a.sw_score = 0; a.edit_distance = 0; a.ref_start = a.ref_end = a.query_start = a.query_end = 0;
+    a.cigar_offset = jb.cig_off; a.cigar_len = 0; a.pad_ = 0;
+    int i = read_l - 1, jx = ref_l - 1, ecount = 0, l = 0, temp2 = 2;
+    int64_t line = (int64_t)width_d * 3 * (read_l - 1);
+    uint32_t op = 0, prev_op = 0;
+    while (i >= 0 && jx > 0) {
+        const int64_t at = line + (int64_t)(jx - max(i - bw, 0)) * 3 + temp2;
+        if (at < 0 || at >= s2_ref) { aln_sentinel(out, j, jb, -100000); return; }
+        const int dv = dir[at];
+        if (dv == 1) { --i; --jx; temp2 = 2; line -= width_d * 3; op = 0; }
+        else if (dv == 2) { --i; temp2 = 0; line -= width_d * 3; op = 1; }
+        else if (dv == 3) { --i; temp2 = 2; line -= width_d * 3; op = 1; }
+        else if (dv == 4) { --jx; temp2 = 1; op = 2; }
+        else if (dv == 5) { --jx; temp2 = 2; op = 2; }
+        else { aln_sentinel(out, j, jb, -100000); return; }   // banded_sw failed -> flag 1
+        if (op == prev_op) ++ecount;
+        else { ++l; raw[l - 1] = cig((uint32_t)ecount, prev_op); prev_op = op; ecount = 1; }
+    }
+    if (op == 0) { ++l; raw[l - 1] = cig((uint32_t)ecount + 1, op); }
+    else { l += 2; raw[l - 2] = cig((uint32_t)ecount, op); raw[l - 1] = cig(1, 0); }
+    for (int s = 0, e = l - 1; s < e; ++s, --e) { const uint32_t x = raw[s]; raw[s] = raw[e]; raw[e] = x; }
+    (void)ext_finish(jb, sr, q, r, raw, l, cig_pool + jb.cig_off, a, match, mismatch, bonus, gO, gE, s_qc, s_rc);
+    out[j] = a;
 }
 
 // ---------------------------------------------------------------------------

@@ -32,10 +32,10 @@ bool scan_g_params_ok(int match, int mismatch, int gO, int gE);
 void launch_ext_scan_w2(int rows, int n, hipStream_t st, const ExtJobDev* jobs, const int* order, const char* q,
                         const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE);
 bool scan_w2_params_ok(int match, int mismatch, int gO, int gE);
-__global__ void k_ext_band(const ExtJobDev* jobs, const ScanRes* scan, int n_jobs, const int* idx_list, int job_base,
-                           const char* qbuf, const char* ref, uint32_t* cig_pool, rsa_aln* out, uint8_t* scratch,
-                           int64_t scr_stride, int arr_cap, int64_t dir_cap, int match, int mismatch, int gO,
-                           int gE, int bonus, int* overflow, int over_code);
+__global__ void k_ext_band_panel(const ExtJobDev* jobs, const ScanRes* scan, int n_jobs, const int* idx_list,
+                                 const char* qbuf, const char* ref, uint32_t* cig_pool, rsa_aln* out,
+                                 uint8_t* scratch, int64_t scr_stride, int64_t dir_cap, int match, int mismatch,
+                                 int gO, int gE, int bonus, int* overflow, int over_code);
 void launch_ext_band16(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n, const char* q,
                        const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match, int mismatch, int gO,
                        int gE, int bonus, int* queue, int* qcount, int* overflow, int* rcount);
@@ -333,15 +333,16 @@ uint64_t rsa_extend_cigar_bound(const rsa_job_batch* jb) {
     return t;
 }
 
-// band kernel scratch geometry of the one-lane fallback (per in-flight job)
-static const int BIG_ARR_CAP = 1 << 16;
-static const int64_t BIG_DIR_CAP = 64ll << 20;
-static const int BIG_CHUNK = 8;
+// band scratch of k_ext_band_panel (per in-flight job): the direction matrix of the
+// widest band a job can need (2 x 2000 + 1 cells x 1024 rows x 3 bytes < 16 MB) and
+// the raw traceback ops
+static const int64_t BIG_DIR_CAP = 16ll << 20;
+static const int BIG_CHUNK = 32;
 static const int BAND64_GRID = 512;        // waves draining the band16 deferral queue
 static const uint64_t DENSE_GUESS = 24;    // CIGAR ops per job copied before the total is known
 
-static int64_t band_stride(int arr_cap, int64_t dir_cap) {
-    int64_t s = (int64_t)arr_cap * 3 * 4 + dir_cap + (int64_t)RSA_RAW_CAP * 4;
+static int64_t band_stride(int64_t dir_cap) {
+    int64_t s = dir_cap + (int64_t)RSA_RAW_CAP * 4;
     return (s + 255) & ~(int64_t)255;
 }
 
@@ -553,8 +554,8 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
     return ext_compact_copy(P);
 }
 
-// second half: wait, the rare one-lane pass for bands the 64-lane kernel could
-// not hold, the CIGAR entries past the first guess, statistics
+// second half: wait, the rare panel pass for bands the 64-lane kernel could not
+// hold, the CIGAR entries past the first guess, statistics
 static int ext_finish(rsa_pending& P) {
     rsa_ctx* ctx = P.ctx;
     Lane* L = P.L;
@@ -568,8 +569,8 @@ static int ext_finish(rsa_pending& P) {
     if (hs.ocount > 0 || hs.rcount > 0) {
         // rare: bands the 64-lane kernel cannot hold (flag 1) and pair-scan results whose
         // alignment did not prove the byte layout saturated (flag 3) -> the exact
-        // one-job-per-wave scan again (the same result for a flag-1 job), then one lane
-        // per job with large global scratch
+        // one-job-per-wave scan again (the same result for a flag-1 job), then one wave
+        // per job sweeping each band row in 64-cell panels (direction matrix in global scratch)
         HIPCHK(L->h_over.ensure(sizeof(int) * n));
         HIPCHK(hipMemcpyAsync(L->h_over.p, L->d_over.p, sizeof(int) * n, hipMemcpyDeviceToHost, st));
         HIPCHK(stream_wait(st, L->sb.done));
@@ -581,7 +582,7 @@ static int ext_finish(rsa_pending& P) {
                 big.push_back((int)i);
                 rmax = std::max(rmax, (int)((hj[i].qlen + 63) / 64));
             }
-        const int64_t bstride = band_stride(BIG_ARR_CAP, BIG_DIR_CAP);
+        const int64_t bstride = band_stride(BIG_DIR_CAP);
         HIPCHK(L->d_scratch.ensure((size_t)bstride * BIG_CHUNK));
         HIPCHK(L->d_idx.ensure(sizeof(int) * big.size()));
         HIPCHK(hipMemcpyAsync(L->d_idx.p, big.data(), sizeof(int) * big.size(), hipMemcpyHostToDevice, st));
@@ -596,11 +597,11 @@ static int ext_finish(rsa_pending& P) {
         }
         for (size_t b = 0; b < big.size(); b += BIG_CHUNK) {
             const int cnt = (int)std::min<size_t>(BIG_CHUNK, big.size() - b);
-            L->kt.begin(st, RSA_K_EXT_BAND_LANE);
-            hipLaunchKernelGGL(k_ext_band, dim3(1), dim3(64), 0, st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(),
-                               cnt, L->d_idx.as<int>() + b, 0, L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(),
-                               L->d_alns.as<rsa_aln>(), L->d_scratch.as<uint8_t>(), bstride, BIG_ARR_CAP, BIG_DIR_CAP,
-                               P.match, P.mismatch, P.gap_open, P.gap_extend, P.end_bonus,
+            L->kt.begin(st, RSA_K_EXT_BAND_PANEL);
+            hipLaunchKernelGGL(k_ext_band_panel, dim3(cnt), dim3(64), 0, st, L->d_jobs.as<ExtJobDev>(),
+                               L->d_scan.as<ScanRes>(), cnt, L->d_idx.as<int>() + b, L->d_q.as<char>(), ctx->d_ref,
+                               L->d_cig.as<uint32_t>(), L->d_alns.as<rsa_aln>(), L->d_scratch.as<uint8_t>(), bstride,
+                               BIG_DIR_CAP, P.match, P.mismatch, P.gap_open, P.gap_extend, P.end_bonus,
                                L->d_over.as<int>(), 2);
             HIPCHK(hipGetLastError());
             L->kt.end(st);

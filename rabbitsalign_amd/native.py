@@ -81,10 +81,10 @@ class AlnBatch(C.Structure):
 
 
 KERNELS = ["randstrobes", "lookup", "find_nams", "rescue", "compact", "ext_scan", "ext_band", "ext_band_wide",
-           "ext_band_lane", "sites"]
+           "ext_band_panel", "sites"]
 KERNEL_SYMBOLS = {"randstrobes": "k_rs_wave", "lookup": "k_lookup", "find_nams": "k_find_nams_w2",
                   "rescue": "k_rescue_w", "compact": "k_compact", "ext_scan": "k_ext_scan_g", "ext_band": "k_ext_band16",
-                  "ext_band_wide": "k_ext_band64", "ext_band_lane": "k_ext_band",
+                  "ext_band_wide": "k_ext_band64", "ext_band_panel": "k_ext_band_panel",
                   "sites": "k_sites"}
 NK = len(KERNELS)
 

@@ -68,7 +68,7 @@ def test_extend_order_independent(ctx):
 @pytest.mark.gpu
 def test_extend_band_paths_exercised(ctx):
     """Jobs whose bands the 16-lane kernel cannot hold go through the 64-lane
-    queue kernel, and bands wider than 64 cells through the one-lane kernel;
+    queue kernel, and bands wider than 64 cells through the panel kernel;
     all three must agree with the oracle."""
     c, ref, offs = ctx
     c.reset_stats()
@@ -78,7 +78,63 @@ def test_extend_band_paths_exercised(ctx):
     assert st["band_deferred"] > 0, st
     assert st["band_overflow"] > 0, st
     k = st["kernels"]
-    assert k["ext_band_wide"]["launches"] > 0 and k["ext_band_lane"]["launches"] > 0
+    assert k["ext_band_wide"]["launches"] > 0 and k["ext_band_panel"]["launches"] > 0
+
+
+def _wide_band_jobs(rng, ref, offs, n):
+    """Queries that bridge a long deletion (or carry a long insertion) of the
+    window: |ref span - query span| of 65-1200 bp, so banded_sw needs bands far
+    wider than one wave (2 x 1200 + 1 cells at most): k_ext_band_panel's panels."""
+    from jobgen import JOB_DTYPE, ACGT, mutate
+    queries = bytearray()
+    jobs = np.zeros(n, dtype=JOB_DTYPE)
+    pairs = []
+    for i in range(n):
+        c = int(rng.integers(0, len(offs) - 1))
+        clen = int(offs[c + 1] - offs[c])
+        gap = int(rng.choice([65, 100, 180, 300, 500, 800, 1200]))
+        flank = int(rng.integers(160, 420))
+        deletion = rng.random() < 0.7
+        span = 2 * flank + (gap if deletion else 0) + 60
+        rs = int(rng.integers(0, clen - span - 1))
+        win = ref[int(offs[c]) + rs:int(offs[c]) + rs + span]
+        left, right = win[30:30 + flank], win[30 + flank + (gap if deletion else 0):30 + 2 * flank + (gap if deletion else 0)]
+        mid = np.zeros(0, np.uint8) if deletion else ACGT[rng.integers(0, 4, min(gap, 1000 - 2 * flank))]
+        q = mutate(rng, np.concatenate([left, mid, right]), sub=float(rng.choice([0.0, 0.01, 0.03])), ind=0.005)[:1000]
+        if rng.random() < 0.3 and span > 2000:
+            win = win[:2000]
+        qb = bytes(q)
+        jobs[i] = (len(queries), len(qb), c, rs, len(win))
+        queries += qb
+        pairs.append((qb, bytes(win)))
+    return bytes(queries), jobs, pairs
+
+
+@pytest.mark.gpu
+def test_extend_wide_bands_panel_kernel(ctx):
+    """Bands 65-2401 cells wide: every job through k_ext_band_panel, == the oracle."""
+    c, ref, offs = ctx
+    rng = np.random.default_rng(23)
+    queries, jobs, pairs = _wide_band_jobs(rng, ref, offs, 120)
+    c.reset_stats()
+    alns, pool = c.extend(queries, jobs)
+    bad = []
+    for i, (q, r) in enumerate(pairs):
+        o = oracle_lib.align(q, r)
+        a = alns[i]
+        cig = [int(x) for x in pool[int(a["cigar_offset"]):int(a["cigar_offset"]) + int(a["cigar_len"])]]
+        got = dict(sw_score=int(a["sw_score"]), edit_distance=int(a["edit_distance"]), ref_start=int(a["ref_start"]),
+                   ref_end=int(a["ref_end"]), query_start=int(a["query_start"]), query_end=int(a["query_end"]),
+                   cigar=cig)
+        if got["sw_score"] < -1000:
+            for k in ("ref_end", "query_start", "query_end"):
+                got[k] = o[k]
+        if got != o:
+            bad.append((i, len(q), len(r), o, got))
+    assert not bad, f"{len(bad)} mismatches, first: {bad[0]}"
+    st = c.stats()
+    assert st["band_overflow"] >= 60, st
+    assert st["kernels"]["ext_band_panel"]["launches"] > 0
 
 
 @pytest.mark.gpu
