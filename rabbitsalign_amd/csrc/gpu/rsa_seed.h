@@ -21,11 +21,14 @@ struct SeedIndexParams {
     const uint64_t* coff;       // [n_contigs + 1] contig offsets in ref (device)
 };
 
+#define SEED_NBUF 40
+#define SEED_NHBUF 8
 struct SeedBufs {
-    void* p[32] = {nullptr};
-    size_t cap[32] = {0};
-    void* h[12] = {nullptr};
-    size_t hcap[12] = {0};
+    void* p[SEED_NBUF] = {nullptr};
+    size_t cap[SEED_NBUF] = {0};
+    void* h[SEED_NHBUF] = {nullptr};
+    size_t hcap[SEED_NHBUF] = {0};
+    uint64_t pool_n = 0;         // entries of the global-map / rescue pool (grows when a call runs out)
     hipEvent_t done = nullptr;   // blocking-sync event (RSA_WAIT=event)
 };
 

@@ -54,6 +54,40 @@ struct HitD {
     int32_t pad;
 };
 
+// Device-side state of one rsa_seed call.  The host uploads it zeroed with the
+// read offsets and downloads it with the results, once: every count that used to
+// come back between the kernels (hits per read, big-map reads, rescued reads, the
+// final NAM offsets) is a device counter, scan or list now.
+#define SEED_E_POOL 1u      // the call's pool ran out: the host grows it and runs again
+#define SEED_E_FIND 2u      // robin_hood emulation overflow in the global-map pass
+#define SEED_E_RESCUE 4u    // the same in the rescue pass
+struct SeedHdr {
+    unsigned long long pool_used;   // pool entries handed out
+    unsigned long long total;       // final NAMs of the batch
+    unsigned long long mm_used;     // mismatch positions of the site checks
+    uint32_t big_count;             // reads listed for k_find_nams_big
+    uint32_t rbig_count;            // rescued reads listed for k_rescue_big
+    uint32_t errors;                // SEED_E_*
+    uint32_t pad_;
+    // statistics (DESIGN.md "Kernels": algorithmic bytes and per-read counts)
+    unsigned long long qrs, found, good, hits_find, hits_all, scan_find, scan_all, n1, n2, resc_reads, resc_q,
+        resc_scan, resc_hits;
+};
+
+// The call's pool: per entry one hit, one open NAM, one NAM, one group hit and
+// one added flag (the global-map and rescue passes take one run of entries per
+// read, as many as the read has hits).  The NAMs sit at arena_base + entry in
+// the NAM arena, after the n x FN2_HCAP fixed slots of k_find_nams_w2.
+struct SeedPool {
+    HitD* hits;
+    rsa_nam* open;
+    rsa_nam* nams;
+    HitD* grp;
+    uint8_t* added;
+    uint64_t n;             // entries
+    uint64_t arena_base;    // index of nams[0] in the NAM arena
+};
+
 // ---------------------------------------------------------------------------
 // k_randstrobes
 // ---------------------------------------------------------------------------
@@ -432,7 +466,7 @@ __device__ __forceinline__ int wave_excl_scan_lk(int v, int lane, int& total) {
 __global__ void __launch_bounds__(256)
 k_lookup(const rsa_query_randstrobe* __restrict__ qrs, const uint32_t* __restrict__ qcnt,
          const uint64_t* __restrict__ qbase, int n_reads, SeedIndexParams p, QrsInfo* __restrict__ qi,
-         ReadStat* __restrict__ st, HitD* __restrict__ hit_slots) {
+         ReadStat* __restrict__ st, HitD* __restrict__ hit_slots, SeedHdr* __restrict__ hdr) {
     const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (wave >= n_reads) return;
@@ -523,6 +557,13 @@ k_lookup(const rsa_query_randstrobe* __restrict__ qrs, const uint32_t* __restric
         ReadStat s;
         s.found = found; s.good = good; s.hits_find = hfind; s.hits_all = hall; s.scan_find = sfind; s.scan_all = sall;
         st[r] = s;
+        atomicAdd(&hdr->qrs, (unsigned long long)nq);
+        if (found) atomicAdd(&hdr->found, (unsigned long long)found);
+        if (good) atomicAdd(&hdr->good, (unsigned long long)good);
+        if (hfind) atomicAdd(&hdr->hits_find, (unsigned long long)hfind);
+        if (hall) atomicAdd(&hdr->hits_all, (unsigned long long)hall);
+        if (sfind) atomicAdd(&hdr->scan_find, (unsigned long long)sfind);
+        if (sall) atomicAdd(&hdr->scan_all, (unsigned long long)sall);
     }
 }
 
@@ -896,13 +937,13 @@ __device__ void merge_fast(const M& m, int orient, HitD* hits, int n_hits, int k
 
 // ---------------------------------------------------------------------------
 // find_nams of one read (nam.cpp:771-926) given k_lookup's per-randstrobe
-// results.  `ms` holds the read's two robin_hood maps (map_stride(map_cap)).
+// results.  `ms` holds the read's two robin_hood maps (map_stride(map_cap));
+// hits / open / out have room for the read's hits_find entries.
 // ---------------------------------------------------------------------------
 __device__ void find_nams_read(int r, const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi,
                                const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase,
-                               const ReadStat* __restrict__ st, const uint64_t* __restrict__ hoff,
-                               const SeedIndexParams& p, HitD* __restrict__ hits_buf, rsa_nam* __restrict__ open_buf,
-                               rsa_nam* __restrict__ nam_buf, uint8_t* ms, uint32_t map_cap,
+                               const ReadStat* __restrict__ st, const SeedIndexParams& p, HitD* __restrict__ hits,
+                               rsa_nam* __restrict__ open, rsa_nam* __restrict__ out, uint8_t* ms, uint32_t map_cap,
                                uint32_t* __restrict__ ncnt, float* __restrict__ nonrep, uint32_t* __restrict__ flags) {
     const int nq = (int)qcnt[r];
     const uint64_t base = qbase[r];
@@ -914,7 +955,6 @@ __device__ void find_nams_read(int r, const rsa_query_randstrobe* __restrict__ q
     map_bind(m[1], ms, map_cap, 1);
     rh_new_reserved(m[0]);
     rh_new_reserved(m[1]);
-    HitD* hits = hits_buf + hoff[r];
     int n_hits = 0, n_lists = 0;
     for (int i = 0; i < nq; ++i) {
         const QrsInfo o = qi[base + i];
@@ -924,31 +964,11 @@ __device__ void find_nams_read(int r, const rsa_query_randstrobe* __restrict__ q
         add_hits(m[orient], orient, (int)q.start, (int)q.end, p, o.pos, o.count, hits, n_hits, n_lists);
     }
     if (m[0].overflow || m[1].overflow) { flags[r] = 2; ncnt[r] = 0; return; }
-    rsa_nam* out = nam_buf + hoff[r];
-    rsa_nam* open = open_buf + hoff[r];
     int n_out = 0;
     merge_slow(m[0], 0, hits, n_hits, p.k, open, out, n_out);
     merge_slow(m[1], 1, hits, n_hits, p.k, open, out, n_out);
     ncnt[r] = (uint32_t)n_out;
     flags[r] = 0;
-}
-
-// one lane per read, maps in global scratch (the large-map pass for the rare
-// reads whose maps rehash past the LDS tables)
-__global__ void __launch_bounds__(64)
-k_find_nams(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi, const uint32_t* __restrict__ qcnt,
-            const uint64_t* __restrict__ qbase, const ReadStat* __restrict__ st, const uint64_t* __restrict__ hoff,
-            int n_reads, const int* __restrict__ list, SeedIndexParams p, HitD* __restrict__ hits_buf,
-            rsa_nam* __restrict__ open_buf, rsa_nam* __restrict__ nam_buf, uint8_t* __restrict__ map_scratch,
-            uint32_t map_cap, uint32_t* __restrict__ ncnt, float* __restrict__ nonrep, uint32_t* __restrict__ flags,
-            int rpw) {
-    const int lane = threadIdx.x & 63;
-    if (lane >= rpw) return;
-    const int t = blockIdx.x * rpw + lane;
-    if (t >= n_reads) return;
-    const int r = list ? list[t] : t;
-    find_nams_read(r, qrs, qi, qcnt, qbase, st, hoff, p, hits_buf, open_buf, nam_buf,
-                   map_scratch + (size_t)t * map_stride(map_cap), map_cap, ncnt, nonrep, flags);
 }
 
 #define FN_WAVES 4
@@ -1056,9 +1076,10 @@ __device__ __forceinline__ void map_insert_hits(LMap& m, int orient, LHit* hits,
 }
 
 __global__ void __launch_bounds__(64 * FN2_WAVES)
-k_find_nams_w2(const ReadStat* __restrict__ st, const HitD* __restrict__ hit_slots,
-               const uint64_t* __restrict__ hoff, int n_reads, SeedIndexParams p, rsa_nam* __restrict__ nam_buf,
-               uint32_t* __restrict__ ncnt, float* __restrict__ nonrep, uint32_t* __restrict__ flags) {
+k_find_nams_w2(const ReadStat* __restrict__ st, const HitD* __restrict__ hit_slots, int n_reads, SeedIndexParams p,
+               rsa_nam* __restrict__ nam_buf, uint32_t* __restrict__ ncnt, float* __restrict__ nonrep,
+               uint32_t* __restrict__ flags, uint64_t* __restrict__ nsrc, SeedHdr* __restrict__ hdr,
+               uint32_t* __restrict__ big_list) {
     __shared__ __attribute__((aligned(16))) uint8_t s_map[FN2_WAVES][FN2_MAPB];   // maps, then NAMs
     __shared__ HitD s_hits[FN2_WAVES][FN2_HCAP];
     __shared__ int2 s_order[FN2_WAVES][FN2_HCAP];
@@ -1068,7 +1089,11 @@ k_find_nams_w2(const ReadStat* __restrict__ st, const HitD* __restrict__ hit_slo
     if (r >= n_reads) return;                           // whole wave
     const ReadStat rs = st[r];
     if (rs.hits_find > FN2_HCAP || rs.hits_find > LK_HCAP) {
-        if (lane == 0) { nonrep[r] = rs.found > 0 ? (float)rs.good / (float)rs.found : 1.0f; flags[r] = 2; ncnt[r] = 0; }
+        if (lane == 0) {
+            nonrep[r] = rs.found > 0 ? (float)rs.good / (float)rs.found : 1.0f;
+            flags[r] = 2; ncnt[r] = 0;
+            big_list[atomicAdd(&hdr->big_count, 1u)] = (uint32_t)r;   // the global-map pass
+        }
         return;
     }
     LHit* hits = LDS_PTR(HitD, s_hits[w]);
@@ -1102,7 +1127,10 @@ k_find_nams_w2(const ReadStat* __restrict__ st, const HitD* __restrict__ hit_slo
     }
     WSYNC_SEED();
     if (s_ctl[w][0]) {
-        if (lane == 0) { flags[r] = 2; ncnt[r] = 0; }
+        if (lane == 0) {
+            flags[r] = 2; ncnt[r] = 0;
+            big_list[atomicAdd(&hdr->big_count, 1u)] = (uint32_t)r;
+        }
         return;
     }
     // list order = occupied slots of the fwd map, then of the rc map (robin_hood iteration order);
@@ -1141,7 +1169,7 @@ k_find_nams_w2(const ReadStat* __restrict__ st, const HitD* __restrict__ hit_slo
     }
     WSYNC_SEED();                                        // maps dead from here: their LDS holds NAMs
     LSeq* store = LDS_PTR(SeqNam, s_map[w]);
-    rsa_nam* out = nam_buf + hoff[r];
+    rsa_nam* out = nam_buf + (size_t)r * FN2_HCAP;          // a read's fixed NAM slot (NAMs <= hits)
     // 3. one lane per list, 64 lists a round
     int hbase = 0, obase = 0;
     for (int l0 = 0; l0 < nl; l0 += 64) {
@@ -1173,7 +1201,36 @@ k_find_nams_w2(const ReadStat* __restrict__ st, const HitD* __restrict__ hit_slo
             out[x.nam_id] = x;
         }
     }
-    if (lane == 0) { ncnt[r] = (uint32_t)obase; flags[r] = 0; }
+    if (lane == 0) { ncnt[r] = (uint32_t)obase; flags[r] = 0; nsrc[r] = (uint64_t)r * FN2_HCAP; }
+}
+
+// ---------------------------------------------------------------------------
+// The rare reads k_find_nams_w2 lists (more hits than its LDS holds, or maps
+// that would rehash past the LDS tables): one lane per read, maps in global
+// scratch, hits / open NAMs / NAMs from the call's pool (one bump allocation a
+// read).  A single block works through the device list, so the host never
+// waits for the list to know what to launch.
+// ---------------------------------------------------------------------------
+#define BIG_LANES 32
+__global__ void __launch_bounds__(64)
+k_find_nams_big(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi,
+                const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, const ReadStat* __restrict__ st,
+                SeedIndexParams p, SeedPool pool, uint8_t* __restrict__ map_scratch, uint32_t map_cap,
+                uint32_t* __restrict__ ncnt, float* __restrict__ nonrep, uint32_t* __restrict__ flags,
+                uint64_t* __restrict__ nsrc, SeedHdr* __restrict__ hdr, const uint32_t* __restrict__ big_list) {
+    const int lane = threadIdx.x;
+    if (lane >= BIG_LANES) return;
+    const uint32_t nb = hdr->big_count;
+    for (uint32_t t = lane; t < nb; t += BIG_LANES) {
+        const int r = (int)big_list[t];
+        const uint32_t hf = st[r].hits_find;
+        const unsigned long long e = atomicAdd(&hdr->pool_used, (unsigned long long)hf);
+        if (e + hf > pool.n) { atomicOr(&hdr->errors, SEED_E_POOL); ncnt[r] = 0; continue; }
+        nsrc[r] = pool.arena_base + e;
+        find_nams_read(r, qrs, qi, qcnt, qbase, st, p, pool.hits + e, pool.open + e, pool.nams + e,
+                       map_scratch + (size_t)lane * map_stride(map_cap), map_cap, ncnt, nonrep, flags);
+        if (flags[r] & 2u) atomicOr(&hdr->errors, SEED_E_FIND);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1276,52 +1333,112 @@ __device__ void rescue_read(int r, const rsa_query_randstrobe* __restrict__ qrs,
     flags[r] = (flags[r] & ~4u) | 8u;   // bit3: rescued result present
 }
 
-// one lane per listed read, maps in global scratch (large-map pass)
-__global__ void __launch_bounds__(64)
-k_rescue(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi, const uint32_t* __restrict__ qcnt,
-         const uint64_t* __restrict__ qbase, const uint64_t* __restrict__ roff, int n_list, const int* __restrict__ list,
-         SeedIndexParams p, uint32_t rescue_cutoff, RescueD* __restrict__ rbuf, HitD* __restrict__ hits_buf,
-         rsa_nam* __restrict__ open_buf, rsa_nam* __restrict__ nam_buf, HitD* __restrict__ grp_buf,
-         uint8_t* __restrict__ added_buf, uint8_t* __restrict__ map_scratch, uint32_t map_cap,
-         uint32_t* __restrict__ ncnt, uint32_t* __restrict__ flags) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n_list) return;
-    rescue_read(list[t], qrs, qi, qcnt, qbase, roff, p, rescue_cutoff, rbuf, hits_buf, open_buf, nam_buf, grp_buf,
-                added_buf, map_scratch + (size_t)t * map_stride(map_cap), map_cap, ncnt, flags);
-}
-
-// one wavefront per listed read, maps in LDS, lane 0 (the LDS map layout of k_find_nams_w2)
+// find_nams_rescue for every read that needs it (aln.cpp:1954-1962: rescue_level
+// > 1 and no NAMs or nonrepetitive_fraction < 0.7), decided here from
+// k_find_nams' results: one wave per read, lane 0, maps in LDS.  Most waves
+// leave at once.  Each rescued read takes hits_all pool entries.
 __global__ void __launch_bounds__(64 * FN_WAVES)
-k_rescue_w(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi,
-           const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, const uint64_t* __restrict__ roff,
-           int n_list, const int* __restrict__ list, SeedIndexParams p, uint32_t rescue_cutoff,
-           RescueD* __restrict__ rbuf, HitD* __restrict__ hits_buf, rsa_nam* __restrict__ open_buf,
-           rsa_nam* __restrict__ nam_buf, HitD* __restrict__ grp_buf, uint8_t* __restrict__ added_buf,
-           uint32_t* __restrict__ ncnt, uint32_t* __restrict__ flags) {
+k_rescue_all(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi,
+             const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, const ReadStat* __restrict__ st,
+             int n_reads, SeedIndexParams p, int32_t rescue_level, uint32_t rescue_cutoff, RescueD* __restrict__ rbuf,
+             SeedPool pool, const uint32_t* __restrict__ ncnt1, const float* __restrict__ nonrep,
+             uint32_t* __restrict__ ncnt2, uint32_t* __restrict__ flags, uint64_t* __restrict__ rbase,
+             uint8_t* __restrict__ rescued, SeedHdr* __restrict__ hdr, uint32_t* __restrict__ rbig_list) {
     __shared__ __attribute__((aligned(16))) uint8_t s_map[FN_WAVES][FN_MAP_CAP * 9 * 4];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int t = blockIdx.x * FN_WAVES + w;
-    if (t >= n_list || lane != 0) return;
-    rescue_read(list[t], qrs, qi, qcnt, qbase, roff, p, rescue_cutoff, rbuf, hits_buf, open_buf, nam_buf, grp_buf,
-                added_buf, s_map[w], FN_MAP_CAP, ncnt, flags);
+    const int r = blockIdx.x * FN_WAVES + w;
+    if (r >= n_reads || lane != 0) return;
+    const bool need = rescue_level > 1 && (ncnt1[r] == 0 || nonrep[r] < 0.7f);
+    rescued[r] = need ? 1 : 0;
+    ncnt2[r] = 0;
+    if (!need) return;
+    const ReadStat rs = st[r];
+    const uint32_t ha = rs.hits_all;
+    atomicAdd(&hdr->resc_reads, 1ull);
+    atomicAdd(&hdr->resc_q, (unsigned long long)qcnt[r]);
+    atomicAdd(&hdr->resc_scan, (unsigned long long)rs.scan_all);
+    atomicAdd(&hdr->resc_hits, (unsigned long long)ha);
+    const unsigned long long e = atomicAdd(&hdr->pool_used, (unsigned long long)ha);
+    if (e + ha > pool.n) { atomicOr(&hdr->errors, SEED_E_POOL); return; }
+    rbase[r] = e;
+    rescue_read(r, qrs, qi, qcnt, qbase, rbase, p, rescue_cutoff, rbuf, pool.hits, pool.open, pool.nams, pool.grp,
+                pool.added, s_map[w], FN_MAP_CAP, ncnt2, flags);
+    if (flags[r] & 4u) rbig_list[atomicAdd(&hdr->rbig_count, 1u)] = (uint32_t)r;
+}
+
+// the rescued reads whose maps outgrow LDS: one lane per read, global map scratch,
+// the read's pool entries again
+__global__ void __launch_bounds__(64)
+k_rescue_big(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi,
+             const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, SeedIndexParams p,
+             uint32_t rescue_cutoff, RescueD* __restrict__ rbuf, SeedPool pool, uint8_t* __restrict__ map_scratch,
+             uint32_t map_cap, uint32_t* __restrict__ ncnt2, uint32_t* __restrict__ flags,
+             const uint64_t* __restrict__ rbase, SeedHdr* __restrict__ hdr, const uint32_t* __restrict__ rbig_list) {
+    const int lane = threadIdx.x;
+    if (lane >= BIG_LANES) return;
+    const uint32_t nb = hdr->rbig_count;
+    for (uint32_t t = lane; t < nb; t += BIG_LANES) {
+        const int r = (int)rbig_list[t];
+        rescue_read(r, qrs, qi, qcnt, qbase, rbase, p, rescue_cutoff, rbuf, pool.hits, pool.open, pool.nams, pool.grp,
+                    pool.added, map_scratch + (size_t)lane * map_stride(map_cap), map_cap, ncnt2, flags);
+        if (flags[r] & 4u) atomicOr(&hdr->errors, SEED_E_RESCUE);
+    }
+}
+
+// final NAM offsets: count[r] = rescued ? rescue NAMs : find NAMs, exclusive scan
+// into ooff[0..n] (one workgroup, each thread a run of reads), total into the header
+__global__ void __launch_bounds__(1024)
+k_seed_scan(int n_reads, const uint8_t* __restrict__ rescued, const uint32_t* __restrict__ ncnt1,
+            const uint32_t* __restrict__ ncnt2, uint64_t* __restrict__ ooff, SeedHdr* __restrict__ hdr) {
+    __shared__ uint64_t s[1024];
+    const int t = threadIdx.x;
+    const int per = (n_reads + 1023) / 1024;
+    const int a = min(n_reads, t * per), b = min(n_reads, a + per);
+    uint64_t mine = 0, n1 = 0, n2 = 0;
+    for (int r = a; r < b; ++r) {
+        const uint64_t c1 = ncnt1[r], c2 = rescued[r] ? ncnt2[r] : 0;
+        mine += rescued[r] ? c2 : c1;
+        n1 += c1;
+        n2 += c2;
+    }
+    s[t] = mine;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const uint64_t x = t >= o ? s[t - o] : 0;
+        __syncthreads();
+        s[t] += x;
+        __syncthreads();
+    }
+    uint64_t off = s[t] - mine;
+    for (int r = a; r < b; ++r) {
+        ooff[r] = off;
+        off += rescued[r] ? ncnt2[r] : ncnt1[r];
+    }
+    if (n1) atomicAdd(&hdr->n1, (unsigned long long)n1);
+    if (n2) atomicAdd(&hdr->n2, (unsigned long long)n2);
+    if (t == 1023) { ooff[n_reads] = s[t]; hdr->total = s[t]; }
 }
 
 // ---------------------------------------------------------------------------
-// k_compact: final list per read = rescue list if rescued else find_nams list
+// k_compact: final list per read = rescue list if rescued else find_nams list,
+// from the NAM arena to the batch's output (at most `cap` NAMs: a batch with
+// more is reported to the host, which asks again with room for them)
 // ---------------------------------------------------------------------------
-__global__ void k_compact(int n_reads, const uint64_t* __restrict__ hoff, const uint64_t* __restrict__ roff,
-                          const uint32_t* __restrict__ ncnt1, const uint32_t* __restrict__ ncnt2,
-                          const uint32_t* __restrict__ flags, const rsa_nam* __restrict__ nam1,
-                          const rsa_nam* __restrict__ nam2, const uint64_t* __restrict__ ooff, rsa_nam* __restrict__ out,
+__global__ void k_compact(int n_reads, const uint64_t* __restrict__ nsrc, const uint64_t* __restrict__ rbase,
+                          uint64_t arena_base, const uint32_t* __restrict__ ncnt1, const uint32_t* __restrict__ ncnt2,
+                          const uint8_t* __restrict__ rescued, const rsa_nam* __restrict__ arena,
+                          const uint64_t* __restrict__ ooff, uint64_t cap, rsa_nam* __restrict__ out,
                           uint32_t* __restrict__ nam_read) {
     const int r = blockIdx.x;
     if (r >= n_reads) return;
-    const bool resc = flags[r] & 8u;
-    const rsa_nam* src = resc ? nam2 + roff[r] : nam1 + hoff[r];
+    const bool resc = rescued[r] != 0;
+    const rsa_nam* src = arena + (resc ? arena_base + rbase[r] : nsrc[r]);
     const uint32_t n = resc ? ncnt2[r] : ncnt1[r];
+    const uint64_t o = ooff[r];
+    if (o + n > cap) return;
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        out[ooff[r] + i] = src[i];
-        if (nam_read) nam_read[ooff[r] + i] = (uint32_t)r;
+        out[o + i] = src[i];
+        if (nam_read) nam_read[o + i] = (uint32_t)r;
     }
 }
 
@@ -1375,14 +1492,17 @@ __device__ bool site_kmer_eq(const char* ref, int64_t rlen, int64_t rpos, const 
 }
 
 __global__ void __launch_bounds__(256)
-k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read, uint64_t total,
-        const char* __restrict__ seq, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
+k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read, const SeedHdr* __restrict__ hdr,
+        uint64_t cap, const char* __restrict__ seq, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
         SeedIndexParams p, rsa_nam_site* __restrict__ sites, uint16_t* __restrict__ pool, uint64_t pool_cap,
         unsigned long long* __restrict__ pool_used) {
     __shared__ uint32_t s_need[16], s_base[16];
     __shared__ unsigned long long s_at;
+    const uint64_t total = min((uint64_t)hdr->total, cap);
     const int l16 = threadIdx.x & 15, grp = threadIdx.x >> 4;
-    const uint64_t g0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+    // a fixed grid walks the batch's NAMs, 16 a block per round (the count is known on the device only)
+    for (uint64_t blk = blockIdx.x; blk * 16 < total; blk += gridDim.x) {
+    const uint64_t g0 = blk * 16 + grp;
     const bool valid = g0 < total;
     const uint64_t g = valid ? g0 : total - 1;             // idle groups shadow the last NAM (ballots stay uniform)
     const uint32_t r = nam_read[g];
@@ -1462,24 +1582,26 @@ k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read,
         out.mm_offset = mm_off;
         sites[g] = out;
     }
+    __syncthreads();                             // s_need / s_base / s_at are reused next round
+    }
 }
 
 // ---------------------------------------------------------------------------
 // host orchestration
 // ---------------------------------------------------------------------------
 enum {
-    B_SEQ, B_ROFF, B_RLEN, B_QBASE, B_QRS, B_QCNT, B_SYNC, B_QI, B_ST, B_HOFF, B_HITS, B_OPEN, B_NAM1, B_NCNT1,
-    B_NONREP, B_FLAGS, B_MAP, B_ROFF2, B_NAM2, B_NCNT2, B_LIST, B_RBUF, B_OUT, B_OOFF, B_SLOTS, B_SITES, B_POOL,
-    B_PUSED, B_NREAD, B_RSLIST
+    B_SEQ, B_ROFF, B_RLEN, B_QBASE, B_QRS, B_QCNT, B_SYNC, B_QI, B_ST, B_X, B_ARENA, B_PHIT, B_POPEN, B_PGRP, B_PADD,
+    B_NCNT1, B_FLAGS, B_MAP, B_NCNT2, B_NSRC, B_RBASE, B_BIGL, B_RBIGL, B_RBUF, B_OUT, B_SLOTS, B_SITES, B_POOL,
+    B_NREAD, B_RSLIST
 };
 // every host side of a transfer is page-locked: a pageable one would make the copy synchronous
-enum { H_ST, H_HOFF, H_FLAGS, H_CNT, H_ROFF, H_LIST, H_OOFF, H_CNT2, H_QBASE, H_NONREP, H_PUSED, H_RSLIST };
+enum { H_X, H_QBASE, H_RSLIST };
 
 void seed_bufs_release(SeedBufs& b) {
-    for (int i = 0; i < 32; ++i) if (b.p[i]) (void)hipFree(b.p[i]);
-    for (int i = 0; i < 12; ++i) if (b.h[i]) (void)hipHostFree(b.h[i]);
-    for (int i = 0; i < 32; ++i) { b.p[i] = nullptr; b.cap[i] = 0; }
-    for (int i = 0; i < 12; ++i) { b.h[i] = nullptr; b.hcap[i] = 0; }
+    for (int i = 0; i < SEED_NBUF; ++i) if (b.p[i]) (void)hipFree(b.p[i]);
+    for (int i = 0; i < SEED_NHBUF; ++i) if (b.h[i]) (void)hipHostFree(b.h[i]);
+    for (int i = 0; i < SEED_NBUF; ++i) { b.p[i] = nullptr; b.cap[i] = 0; }
+    for (int i = 0; i < SEED_NHBUF; ++i) { b.h[i] = nullptr; b.hcap[i] = 0; }
     if (b.done) (void)hipEventDestroy(b.done);
     b.done = nullptr;
 }
@@ -1597,237 +1719,233 @@ int seed_randstrobes_run(SeedBufs& b, hipStream_t st, const SeedIndexParams& p, 
     return RSA_OK;
 }
 
+// Byte layout of the call's packed device/host block B_X / H_X: the header and the
+// read table go up in one copy, the header and the per-read results come down in one.
+struct XLayout {
+    size_t roff, rlen, qbase, rsl, up, ooff, nonrep, resc, down;
+    XLayout(uint32_t n, uint32_t n_long) {
+        auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+        roff = al(sizeof(SeedHdr));
+        rlen = al(roff + 8ull * n);
+        qbase = al(rlen + 4ull * n);
+        rsl = al(qbase + 8ull * (n + 1));
+        up = rsl + 4ull * n_long;
+        ooff = al(up);
+        nonrep = al(ooff + 8ull * (n + 1));
+        resc = al(nonrep + 4ull * n);
+        down = resc + n;
+    }
+};
+
+static const uint32_t MAP_BIG_LANES = BIG_LANES;
+
+// rsa_seed: every kernel of the call is queued before the host waits once.  The
+// per-read counts the kernels need from each other stay on the device (fixed NAM
+// slots for k_find_nams_w2, device lists for the global-map passes, a pool for
+// their variable-size scratch, a device scan for the final offsets); the host gets
+// the header, offsets, NAMs, site checks and mismatch positions back in one round
+// trip.  A second round trip is needed only when a guessed download size was too
+// small; a pool that ran out is grown and the call runs again.
 int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, const rsa_read_batch* rb,
              int32_t rescue_level, uint32_t rescue_cutoff, rsa_nam_batch* out, std::string& err, SeedCounters& c) {
     const uint32_t n = rb->n_reads;
-    std::vector<uint64_t> qbase;
-    int rc = seed_stage_randstrobes(b, st, p, rb, qbase, err, &kt);
-    if (rc) return rc;
-    SCHK(dens(b, B_QI, sizeof(QrsInfo) * (qbase[n] + 1)));
-    SCHK(dens(b, B_ST, sizeof(ReadStat) * n));
-    kt.begin(st, RSA_K_LOOKUP);
-    SCHK(dens(b, B_SLOTS, sizeof(HitD) * LK_HCAP * (size_t)n));
-    hipLaunchKernelGGL(k_lookup, dim3((n + 3) / 4), dim3(256), 0, st, DP(B_QRS, rsa_query_randstrobe),
-                       DP(B_QCNT, uint32_t), DP(B_QBASE, uint64_t), (int)n, p, DP(B_QI, QrsInfo), DP(B_ST, ReadStat),
-                       DP(B_SLOTS, HitD));
-    SCHK(hipGetLastError());
-    kt.end(st);
-    SCHK(hens(b, H_ST, sizeof(ReadStat) * n));
-    SCHK(hipMemcpyAsync(b.h[H_ST], b.p[B_ST], sizeof(ReadStat) * n, hipMemcpyDeviceToHost, st));
-    SCHK(hens(b, H_CNT, 4ull * n));
-    SCHK(hipMemcpyAsync(b.h[H_CNT], b.p[B_QCNT], 4ull * n, hipMemcpyDeviceToHost, st));
-    SCHK(stream_wait(st, b.done));
-    const ReadStat* hs = HP(H_ST, ReadStat);
-    SCHK(hens(b, H_HOFF, 8ull * (n + 1)));
-    uint64_t* hoff = HP(H_HOFF, uint64_t);
-    hoff[0] = 0;
-    uint64_t n_qrs = 0, n_found = 0, n_good = 0, scan_find = 0, scan_all = 0, bases = 0;
-    std::vector<uint32_t> qcnt(HP(H_CNT, uint32_t), HP(H_CNT, uint32_t) + n);
+    // reads longer than RW_MAXLEN (and parameters k_rs_wave cannot take) go one lane per read
+    const bool wave_ok = p.k <= 32 && p.s <= 32 && p.s >= 1 && p.k - p.s + 1 <= RW_WMAX && p.k - p.s + 1 >= 1;
+    uint32_t n_long = 0;
+    uint64_t total_len = 0, bases = 0;
     for (uint32_t i = 0; i < n; ++i) {
-        hoff[i + 1] = hoff[i] + hs[i].hits_find;
-        n_qrs += qcnt[i];
-        n_found += hs[i].found;
-        n_good += hs[i].good;
-        scan_find += hs[i].scan_find;
-        scan_all += hs[i].scan_all;
+        n_long += rb->lengths[i] > RW_MAXLEN ? 1 : 0;
+        total_len = std::max<uint64_t>(total_len, rb->offsets[i] + rb->lengths[i]);
         bases += rb->lengths[i];
     }
-    const uint64_t H = hoff[n];
-    SCHK(dens(b, B_HOFF, 8ull * (n + 1)));
-    SCHK(dens(b, B_HITS, sizeof(HitD) * (H + 1)));
-    SCHK(dens(b, B_OPEN, sizeof(rsa_nam) * (H + 1)));
-    SCHK(dens(b, B_NAM1, sizeof(rsa_nam) * (H + 1)));
+    const uint32_t n_lane = wave_ok ? n_long : n;
+    const XLayout X(n, wave_ok ? n_long : 0);
+    SCHK(hens(b, H_X, X.down));
+    char* hx = (char*)b.h[H_X];
+    memcpy(hx + X.roff, rb->offsets, 8ull * n);
+    memcpy(hx + X.rlen, rb->lengths, 4ull * n);
+    uint64_t* hq = (uint64_t*)(hx + X.qbase);
+    hq[0] = 0;
+    for (uint32_t i = 0; i < n; ++i) hq[i + 1] = hq[i] + 2ull * rb->lengths[i];
+    const uint64_t nq_cap = hq[n];
+    if (wave_ok && n_long) {
+        int* hl = (int*)(hx + X.rsl);
+        uint32_t at = 0;
+        for (uint32_t i = 0; i < n; ++i) if (rb->lengths[i] > RW_MAXLEN) hl[at++] = (int)i;
+    }
+    if (b.pool_n < 4ull * n + 65536) b.pool_n = 4ull * n + 65536;
+    const uint64_t slots = (uint64_t)n * FN2_HCAP;
+    const uint64_t cap = out->capacity;
+    SCHK(dens(b, B_SEQ, total_len + 16));
+    SCHK(dens(b, B_X, X.down));
+    SCHK(dens(b, B_QRS, sizeof(rsa_query_randstrobe) * (nq_cap + 1)));
+    SCHK(dens(b, B_QCNT, 4ull * n));
+    SCHK(dens(b, B_QI, sizeof(QrsInfo) * (nq_cap + 1)));
+    SCHK(dens(b, B_ST, sizeof(ReadStat) * n));
+    SCHK(dens(b, B_SLOTS, sizeof(HitD) * LK_HCAP * (size_t)n));
     SCHK(dens(b, B_NCNT1, 4ull * n));
-    SCHK(dens(b, B_NONREP, 4ull * n));
+    SCHK(dens(b, B_NCNT2, 4ull * n));
     SCHK(dens(b, B_FLAGS, 4ull * n));
-    const uint32_t chunk = 65536;
-    SCHK(hipMemcpyAsync(b.p[B_HOFF], hoff, 8ull * (n + 1), hipMemcpyHostToDevice, st));
-    kt.begin(st, RSA_K_FIND_NAMS);
-    hipLaunchKernelGGL(k_find_nams_w2, dim3((n + FN2_WAVES - 1) / FN2_WAVES), dim3(64 * FN2_WAVES), 0, st,
-                       DP(B_ST, ReadStat), DP(B_SLOTS, HitD), DP(B_HOFF, uint64_t), (int)n, p, DP(B_NAM1, rsa_nam),
-                       DP(B_NCNT1, uint32_t), DP(B_NONREP, float), DP(B_FLAGS, uint32_t));
-    SCHK(hipGetLastError());
-    kt.end(st);
-    SCHK(hens(b, H_FLAGS, 4ull * n));
-    SCHK(hens(b, H_NONREP, 4ull * n));
-    SCHK(hipMemcpyAsync(b.h[H_FLAGS], b.p[B_FLAGS], 4ull * n, hipMemcpyDeviceToHost, st));
-    SCHK(hipMemcpyAsync(b.h[H_CNT], b.p[B_NCNT1], 4ull * n, hipMemcpyDeviceToHost, st));
-    SCHK(hipMemcpyAsync(b.h[H_NONREP], b.p[B_NONREP], 4ull * n, hipMemcpyDeviceToHost, st));
-    SCHK(stream_wait(st, b.done));
-    // rare: reads whose maps rehash past the small table -> big-map pass
-    std::vector<int> big;
-    for (uint32_t i = 0; i < n; ++i) if (HP(H_FLAGS, uint32_t)[i] & 2u) big.push_back((int)i);
-    if (!big.empty()) {
-        const size_t big_stride = (size_t)MAP_BIG * 9 * 4;
-        const uint32_t bchunk = 32;
-        SCHK(dens(b, B_MAP, big_stride * bchunk));
-        SCHK(dens(b, B_LIST, 4ull * big.size()));
-        SCHK(hipMemcpyAsync(b.p[B_LIST], big.data(), 4ull * big.size(), hipMemcpyHostToDevice, st));
-        for (size_t a = 0; a < big.size(); a += bchunk) {
-            const int cnt = (int)std::min<size_t>(bchunk, big.size() - a);
-            kt.begin(st, RSA_K_FIND_NAMS);
-            hipLaunchKernelGGL(k_find_nams, dim3(1), dim3(64), 0, st, DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo),
-                               DP(B_QCNT, uint32_t), DP(B_QBASE, uint64_t), DP(B_ST, ReadStat), DP(B_HOFF, uint64_t), cnt,
-                               DP(B_LIST, int) + a, p, DP(B_HITS, HitD), DP(B_OPEN, rsa_nam), DP(B_NAM1, rsa_nam),
-                               DP(B_MAP, uint8_t), MAP_BIG, DP(B_NCNT1, uint32_t), DP(B_NONREP, float),
-                               DP(B_FLAGS, uint32_t), 64);
-            SCHK(hipGetLastError());
-            kt.end(st);
-        }
-        SCHK(hipMemcpyAsync(b.h[H_FLAGS], b.p[B_FLAGS], 4ull * n, hipMemcpyDeviceToHost, st));
-        SCHK(hipMemcpyAsync(b.h[H_CNT], b.p[B_NCNT1], 4ull * n, hipMemcpyDeviceToHost, st));
-        SCHK(hipMemcpyAsync(b.h[H_NONREP], b.p[B_NONREP], 4ull * n, hipMemcpyDeviceToHost, st));
-        SCHK(stream_wait(st, b.done));
-        for (int i : big) if (HP(H_FLAGS, uint32_t)[i] & 2u) { err = "rsa_seed: robin_hood emulation overflow"; return RSA_ERR_NOMEM; }
-    }
-    // nonrepetitive fraction (copied with the flags above)
-    memcpy(out->nonrepetitive_fraction, b.h[H_NONREP], 4ull * n);
-    // rescue decision (aln.cpp:1954-1962)
-    std::vector<int> resc;
-    std::vector<uint32_t> n1(HP(H_CNT, uint32_t), HP(H_CNT, uint32_t) + n);
-    SCHK(hens(b, H_ROFF, 8ull * (n + 1)));
-    uint64_t* roff = HP(H_ROFF, uint64_t);
-    roff[0] = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        const bool need = rescue_level > 1 && (n1[i] == 0 || out->nonrepetitive_fraction[i] < 0.7f);
-        roff[i + 1] = roff[i] + (need ? hs[i].hits_all : 0);
-        if (need) resc.push_back((int)i);
-        out->rescued[i] = need ? 1 : 0;
-    }
-    std::vector<uint32_t> n2(n, 0);
-    if (!resc.empty()) {
-        const uint64_t R = roff[n];
-        SCHK(dens(b, B_ROFF2, 8ull * (n + 1)));
-        SCHK(dens(b, B_NAM2, sizeof(rsa_nam) * (R + 1)));
-        SCHK(dens(b, B_NCNT2, 4ull * n));
-        SCHK(dens(b, B_RBUF, sizeof(RescueD) * (qbase[n] + 1)));
-        // rescue reuses the hits/open buffers sized for max(H, R), plus group + added scratch
-        SCHK(dens(b, B_HITS, sizeof(HitD) * (std::max(H, R) + 1)));
-        SCHK(dens(b, B_OPEN, sizeof(rsa_nam) * (std::max(H, R) + 1)));
-        SCHK(dens(b, B_OUT, (sizeof(HitD) + 1) * (R + 1)));
-        SCHK(dens(b, B_LIST, 4ull * resc.size()));
-        SCHK(hipMemcpyAsync(b.p[B_ROFF2], roff, 8ull * (n + 1), hipMemcpyHostToDevice, st));
-        SCHK(hens(b, H_LIST, 4ull * resc.size()));
-        memcpy(b.h[H_LIST], resc.data(), 4ull * resc.size());
-        SCHK(hipMemcpyAsync(b.p[B_LIST], b.h[H_LIST], 4ull * resc.size(), hipMemcpyHostToDevice, st));
-        HitD* grp = DP(B_OUT, HitD);
-        uint8_t* added = (uint8_t*)(grp + (R + 1));
-        for (size_t a = 0; a < resc.size(); a += chunk) {
-            const int cnt = (int)std::min<size_t>(chunk, resc.size() - a);
-            kt.begin(st, RSA_K_RESCUE);
-            hipLaunchKernelGGL(k_rescue_w, dim3((cnt + FN_WAVES - 1) / FN_WAVES), dim3(64 * FN_WAVES), 0, st,
-                               DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t),
-                               DP(B_QBASE, uint64_t), DP(B_ROFF2, uint64_t), cnt, DP(B_LIST, int) + a, p, rescue_cutoff,
-                               DP(B_RBUF, RescueD), DP(B_HITS, HitD), DP(B_OPEN, rsa_nam), DP(B_NAM2, rsa_nam), grp,
-                               added, DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t));
-            SCHK(hipGetLastError());
-            kt.end(st);
-        }
-        SCHK(hens(b, H_CNT2, 4ull * n));
-        SCHK(hipMemcpyAsync(b.h[H_FLAGS], b.p[B_FLAGS], 4ull * n, hipMemcpyDeviceToHost, st));
-        SCHK(hipMemcpyAsync(b.h[H_CNT2], b.p[B_NCNT2], 4ull * n, hipMemcpyDeviceToHost, st));
-        SCHK(stream_wait(st, b.done));
-        std::vector<int> bigr;
-        for (int i : resc) if (HP(H_FLAGS, uint32_t)[i] & 4u) bigr.push_back(i);
-        if (!bigr.empty()) {
-            const size_t big_stride = (size_t)MAP_BIG * 9 * 4;
-            const uint32_t bchunk = 32;
-            SCHK(dens(b, B_MAP, std::max(big_stride * bchunk, b.cap[B_MAP])));
-            SCHK(dens(b, B_LIST, 4ull * std::max(bigr.size(), resc.size())));
-            SCHK(hipMemcpyAsync(b.p[B_LIST], bigr.data(), 4ull * bigr.size(), hipMemcpyHostToDevice, st));
-            for (size_t a = 0; a < bigr.size(); a += bchunk) {
-                const int cnt = (int)std::min<size_t>(bchunk, bigr.size() - a);
-                kt.begin(st, RSA_K_RESCUE);
-                hipLaunchKernelGGL(k_rescue, dim3(1), dim3(64), 0, st, DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo),
-                                   DP(B_QCNT, uint32_t), DP(B_QBASE, uint64_t), DP(B_ROFF2, uint64_t), cnt,
-                                   DP(B_LIST, int) + a, p, rescue_cutoff, DP(B_RBUF, RescueD), DP(B_HITS, HitD),
-                                   DP(B_OPEN, rsa_nam), DP(B_NAM2, rsa_nam), grp, added, DP(B_MAP, uint8_t), MAP_BIG,
-                                   DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t));
-                SCHK(hipGetLastError());
-                kt.end(st);
-            }
-            SCHK(hipMemcpyAsync(b.h[H_FLAGS], b.p[B_FLAGS], 4ull * n, hipMemcpyDeviceToHost, st));
-            SCHK(hipMemcpyAsync(b.h[H_CNT2], b.p[B_NCNT2], 4ull * n, hipMemcpyDeviceToHost, st));
-            SCHK(stream_wait(st, b.done));
-            for (int i : bigr) if (HP(H_FLAGS, uint32_t)[i] & 4u) { err = "rsa_seed: rescue map overflow"; return RSA_ERR_NOMEM; }
-        }
-        for (int i : resc) n2[i] = HP(H_CNT2, uint32_t)[i];
-    } else {
-        SCHK(dens(b, B_ROFF2, 8ull * (n + 1)));
-        SCHK(dens(b, B_NAM2, sizeof(rsa_nam)));
-        SCHK(dens(b, B_NCNT2, 4ull * n));
-        SCHK(hipMemcpyAsync(b.p[B_ROFF2], roff, 8ull * (n + 1), hipMemcpyHostToDevice, st));
-    }
-    // final offsets + compaction
-    SCHK(hens(b, H_OOFF, 8ull * (n + 1)));
-    uint64_t* ooff = HP(H_OOFF, uint64_t);
-    ooff[0] = 0;
-    for (uint32_t i = 0; i < n; ++i) ooff[i + 1] = ooff[i] + (out->rescued[i] ? n2[i] : n1[i]);
-    const uint64_t total = ooff[n];
-    for (uint32_t i = 0; i <= n; ++i) out->offsets[i] = ooff[i];
-    out->needed = total;
-    if (total > out->capacity) { err = "rsa_seed: NAM output too small"; return RSA_ERR_CAPACITY; }
-    // resc flag bit3 must be visible to k_compact for rescued reads with bit3 set on device already
-    SCHK(dens(b, B_OOFF, 8ull * (n + 1)));
-    SCHK(dens(b, B_OUT, std::max(b.cap[B_OUT], sizeof(rsa_nam) * (total + 1))));
-    SCHK(hipMemcpyAsync(b.p[B_OOFF], ooff, 8ull * (n + 1), hipMemcpyHostToDevice, st));
-    if (out->sites) SCHK(dens(b, B_NREAD, 4ull * (total + 1)));
-    kt.begin(st, RSA_K_COMPACT);
-    hipLaunchKernelGGL(k_compact, dim3(n), dim3(64), 0, st, (int)n, DP(B_HOFF, uint64_t), DP(B_ROFF2, uint64_t),
-                       DP(B_NCNT1, uint32_t), DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t), DP(B_NAM1, rsa_nam),
-                       DP(B_NAM2, rsa_nam), DP(B_OOFF, uint64_t), DP(B_OUT, rsa_nam),
-                       out->sites ? DP(B_NREAD, uint32_t) : nullptr);
-    SCHK(hipGetLastError());
-    kt.end(st);
-    if (total) SCHK(hipMemcpyAsync(out->nams, b.p[B_OUT], sizeof(rsa_nam) * total, hipMemcpyDeviceToHost, st));
-    // site checks (optional output)
-    double site_bytes = 0;
-    if (out->sites && total) {
-        SCHK(dens(b, B_SITES, sizeof(rsa_nam_site) * total));
+    SCHK(dens(b, B_NSRC, 8ull * n));
+    SCHK(dens(b, B_RBASE, 8ull * n));
+    SCHK(dens(b, B_BIGL, 4ull * n));
+    SCHK(dens(b, B_RBIGL, 4ull * n));
+    SCHK(dens(b, B_RBUF, sizeof(RescueD) * (nq_cap + 1)));
+    SCHK(dens(b, B_MAP, (size_t)MAP_BIG * 9 * 4 * MAP_BIG_LANES));
+    SCHK(dens(b, B_OUT, sizeof(rsa_nam) * (cap + 1)));
+    if (out->sites) {
+        SCHK(dens(b, B_NREAD, 4ull * (cap + 1)));
+        SCHK(dens(b, B_SITES, sizeof(rsa_nam_site) * (cap + 1)));
         SCHK(dens(b, B_POOL, 2 * std::max<uint64_t>(1, out->mm_capacity)));
-        SCHK(dens(b, B_PUSED, 8));
-        SCHK(hipMemsetAsync(b.p[B_PUSED], 0, 8, st));
-        kt.begin(st, RSA_K_SITES);
-        hipLaunchKernelGGL(k_sites, dim3((unsigned)((16 * total + 255) / 256)), dim3(256), 0, st, DP(B_OUT, rsa_nam),
-                           DP(B_NREAD, uint32_t), total, DP(B_SEQ, char), DP(B_ROFF, uint64_t),
-                           DP(B_RLEN, uint32_t), p, DP(B_SITES, rsa_nam_site), DP(B_POOL, uint16_t), out->mm_capacity,
-                           DP(B_PUSED, unsigned long long));
+    }
+    char* dx = (char*)b.p[B_X];
+    SeedHdr* dhdr = (SeedHdr*)dx;
+    const uint64_t* d_roff = (const uint64_t*)(dx + X.roff);
+    const uint32_t* d_rlen = (const uint32_t*)(dx + X.rlen);
+    const uint64_t* d_qbase = (const uint64_t*)(dx + X.qbase);
+    uint64_t* d_ooff = (uint64_t*)(dx + X.ooff);
+    float* d_nonrep = (float*)(dx + X.nonrep);
+    uint8_t* d_resc = (uint8_t*)(dx + X.resc);
+    SCHK(hipMemcpyAsync(b.p[B_SEQ], rb->seq, total_len, hipMemcpyHostToDevice, st));
+    SeedHdr hh;
+    for (int attempt = 0;; ++attempt) {
+        SCHK(dens(b, B_ARENA, sizeof(rsa_nam) * (slots + b.pool_n)));
+        SCHK(dens(b, B_PHIT, sizeof(HitD) * b.pool_n));
+        SCHK(dens(b, B_POPEN, sizeof(rsa_nam) * b.pool_n));
+        SCHK(dens(b, B_PGRP, sizeof(HitD) * b.pool_n));
+        SCHK(dens(b, B_PADD, b.pool_n));
+        const SeedPool pool{DP(B_PHIT, HitD), DP(B_POPEN, rsa_nam), DP(B_ARENA, rsa_nam) + slots, DP(B_PGRP, HitD),
+                            DP(B_PADD, uint8_t), b.pool_n, slots};
+        memset(hx, 0, sizeof(SeedHdr));             // counters start at zero (a retry re-zeroes them)
+        SCHK(hipMemcpyAsync(dx, hx, X.up, hipMemcpyHostToDevice, st));
+        // 1. randstrobes (randstrobes.cpp:207-253)
+        kt.begin(st, RSA_K_RANDSTROBES);
+        if (wave_ok)
+            hipLaunchKernelGGL(k_rs_wave, dim3((n + RW_WAVES - 1) / RW_WAVES), dim3(64 * RW_WAVES), 0, st,
+                               DP(B_SEQ, char), d_roff, d_rlen, d_qbase, (int)n, p, DP(B_QRS, rsa_query_randstrobe),
+                               DP(B_QCNT, uint32_t));
+        if (n_lane) {
+            SCHK(dens(b, B_SYNC, sizeof(SyncD) * (nq_cap / 2 + 1)));
+            const int* lane_list = wave_ok ? (const int*)(dx + X.rsl) : nullptr;
+            if (p.k - p.s + 1 == 5)
+                hipLaunchKernelGGL(k_randstrobes<5>, dim3((n_lane + 63) / 64), dim3(64), 0, st, DP(B_SEQ, char), d_roff,
+                                   d_rlen, d_qbase, (int)n_lane, lane_list, p, DP(B_SYNC, SyncD),
+                                   DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
+            else
+                hipLaunchKernelGGL(k_randstrobes<0>, dim3((n_lane + 63) / 64), dim3(64), 0, st, DP(B_SEQ, char), d_roff,
+                                   d_rlen, d_qbase, (int)n_lane, lane_list, p, DP(B_SYNC, SyncD),
+                                   DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
+        }
         SCHK(hipGetLastError());
         kt.end(st);
-        SCHK(hipMemcpyAsync(out->sites, b.p[B_SITES], sizeof(rsa_nam_site) * total, hipMemcpyDeviceToHost, st));
-        SCHK(hens(b, H_PUSED, 8));
-        SCHK(hipMemcpyAsync(b.h[H_PUSED], b.p[B_PUSED], 8, hipMemcpyDeviceToHost, st));
-        // positions: one per NAM comes back with the rest (synthetic 2x150: ~0.5 a NAM); more
-        // only in a second copy after the wait
-        const uint64_t guess = std::min<uint64_t>(out->mm_capacity, total);
-        if (guess) SCHK(hipMemcpyAsync(out->mm_pool, b.p[B_POOL], 2 * guess, hipMemcpyDeviceToHost, st));
+        // 2. lookups + the min_diff hits (index.hpp:57-93, nam.cpp:68-85)
+        kt.begin(st, RSA_K_LOOKUP);
+        hipLaunchKernelGGL(k_lookup, dim3((n + 3) / 4), dim3(256), 0, st, DP(B_QRS, rsa_query_randstrobe),
+                           DP(B_QCNT, uint32_t), d_qbase, (int)n, p, DP(B_QI, QrsInfo), DP(B_ST, ReadStat),
+                           DP(B_SLOTS, HitD), dhdr);
+        SCHK(hipGetLastError());
+        kt.end(st);
+        // 3. find_nams (nam.cpp:771-926): LDS maps, then the listed reads with global maps
+        kt.begin(st, RSA_K_FIND_NAMS);
+        hipLaunchKernelGGL(k_find_nams_w2, dim3((n + FN2_WAVES - 1) / FN2_WAVES), dim3(64 * FN2_WAVES), 0, st,
+                           DP(B_ST, ReadStat), DP(B_SLOTS, HitD), (int)n, p, DP(B_ARENA, rsa_nam),
+                           DP(B_NCNT1, uint32_t), d_nonrep, DP(B_FLAGS, uint32_t), DP(B_NSRC, uint64_t), dhdr,
+                           DP(B_BIGL, uint32_t));
+        hipLaunchKernelGGL(k_find_nams_big, dim3(1), dim3(64), 0, st, DP(B_QRS, rsa_query_randstrobe),
+                           DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t), d_qbase, DP(B_ST, ReadStat), p, pool,
+                           DP(B_MAP, uint8_t), MAP_BIG, DP(B_NCNT1, uint32_t), d_nonrep, DP(B_FLAGS, uint32_t),
+                           DP(B_NSRC, uint64_t), dhdr, DP(B_BIGL, uint32_t));
+        SCHK(hipGetLastError());
+        kt.end(st);
+        // 4. rescue (aln.cpp:1954-1962, nam.cpp:955-1012)
+        kt.begin(st, RSA_K_RESCUE);
+        hipLaunchKernelGGL(k_rescue_all, dim3((n + FN_WAVES - 1) / FN_WAVES), dim3(64 * FN_WAVES), 0, st,
+                           DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t), d_qbase,
+                           DP(B_ST, ReadStat), (int)n, p, rescue_level, rescue_cutoff, DP(B_RBUF, RescueD), pool,
+                           DP(B_NCNT1, uint32_t), d_nonrep, DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t),
+                           DP(B_RBASE, uint64_t), d_resc, dhdr, DP(B_RBIGL, uint32_t));
+        hipLaunchKernelGGL(k_rescue_big, dim3(1), dim3(64), 0, st, DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo),
+                           DP(B_QCNT, uint32_t), d_qbase, p, rescue_cutoff, DP(B_RBUF, RescueD), pool,
+                           DP(B_MAP, uint8_t), MAP_BIG, DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t),
+                           DP(B_RBASE, uint64_t), dhdr, DP(B_RBIGL, uint32_t));
+        SCHK(hipGetLastError());
+        kt.end(st);
+        // 5. final offsets and the NAM lists back to back
+        kt.begin(st, RSA_K_COMPACT);
+        hipLaunchKernelGGL(k_seed_scan, dim3(1), dim3(1024), 0, st, (int)n, d_resc, DP(B_NCNT1, uint32_t),
+                           DP(B_NCNT2, uint32_t), d_ooff, dhdr);
+        hipLaunchKernelGGL(k_compact, dim3(n), dim3(64), 0, st, (int)n, DP(B_NSRC, uint64_t), DP(B_RBASE, uint64_t),
+                           slots, DP(B_NCNT1, uint32_t), DP(B_NCNT2, uint32_t), d_resc, DP(B_ARENA, rsa_nam), d_ooff,
+                           cap, DP(B_OUT, rsa_nam), out->sites ? DP(B_NREAD, uint32_t) : nullptr);
+        SCHK(hipGetLastError());
+        kt.end(st);
+        // 6. site checks (aln.cpp:60-93, 374-431)
+        if (out->sites) {
+            kt.begin(st, RSA_K_SITES);
+            const uint32_t grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1, (cap + 15) / 16), 4096);
+            hipLaunchKernelGGL(k_sites, dim3(grid), dim3(256), 0, st, DP(B_OUT, rsa_nam), DP(B_NREAD, uint32_t), dhdr,
+                               cap, DP(B_SEQ, char), d_roff, d_rlen, p, DP(B_SITES, rsa_nam_site), DP(B_POOL, uint16_t),
+                               out->mm_capacity, &dhdr->mm_used);
+            SCHK(hipGetLastError());
+            kt.end(st);
+        }
+        // 7. one download of the header + per-read results, and the outputs up to a guessed size
+        SCHK(hipMemcpyAsync(hx, dx, X.down, hipMemcpyDeviceToHost, st));
+        const uint64_t guess = std::min<uint64_t>(cap, 8ull * n + 1024);
+        SCHK(hipMemcpyAsync(out->nams, b.p[B_OUT], sizeof(rsa_nam) * guess, hipMemcpyDeviceToHost, st));
+        const uint64_t mm_guess = out->sites ? std::min<uint64_t>(out->mm_capacity, guess) : 0;
+        if (out->sites) {
+            SCHK(hipMemcpyAsync(out->sites, b.p[B_SITES], sizeof(rsa_nam_site) * guess, hipMemcpyDeviceToHost, st));
+            if (mm_guess) SCHK(hipMemcpyAsync(out->mm_pool, b.p[B_POOL], 2 * mm_guess, hipMemcpyDeviceToHost, st));
+        }
         SCHK(stream_wait(st, b.done));
-        const uint64_t used = std::min<uint64_t>(*HP(H_PUSED, uint64_t), out->mm_capacity);
-        out->mm_used = used;
-        if (used > guess) {
-            SCHK(hipMemcpyAsync(out->mm_pool + guess, DP(B_POOL, uint16_t) + guess, 2 * (used - guess),
-                                hipMemcpyDeviceToHost, st));
+        memcpy(&hh, hx, sizeof hh);
+        if (hh.errors & SEED_E_FIND) { err = "rsa_seed: robin_hood emulation overflow"; return RSA_ERR_NOMEM; }
+        if (hh.errors & SEED_E_RESCUE) { err = "rsa_seed: rescue map overflow"; return RSA_ERR_NOMEM; }
+        if (hh.errors & SEED_E_POOL) {          // grow the pool and run the call again
+            if (attempt >= 8) { err = "rsa_seed: seeding pool exhausted"; return RSA_ERR_NOMEM; }
+            b.pool_n = std::max<uint64_t>(2 * b.pool_n, hh.pool_used + 1024);
+            kt.reset();
+            continue;
+        }
+        const uint64_t total = hh.total;
+        out->needed = total;
+        memcpy(out->offsets, hx + X.ooff, 8ull * (n + 1));
+        memcpy(out->nonrepetitive_fraction, hx + X.nonrep, 4ull * n);
+        memcpy(out->rescued, hx + X.resc, n);
+        if (total > cap) { err = "rsa_seed: NAM output too small"; return RSA_ERR_CAPACITY; }
+        const uint64_t mm_used = out->sites ? std::min<uint64_t>(hh.mm_used, out->mm_capacity) : 0;
+        if (out->sites) out->mm_used = mm_used;
+        else out->mm_used = 0;
+        if (total > guess || mm_used > mm_guess) {   // rare: a second round trip for the rest
+            if (total > guess) {
+                SCHK(hipMemcpyAsync(out->nams + guess, DP(B_OUT, rsa_nam) + guess, sizeof(rsa_nam) * (total - guess),
+                                    hipMemcpyDeviceToHost, st));
+                if (out->sites)
+                    SCHK(hipMemcpyAsync(out->sites + guess, DP(B_SITES, rsa_nam_site) + guess,
+                                        sizeof(rsa_nam_site) * (total - guess), hipMemcpyDeviceToHost, st));
+            }
+            if (mm_used > mm_guess)
+                SCHK(hipMemcpyAsync(out->mm_pool + mm_guess, DP(B_POOL, uint16_t) + mm_guess, 2 * (mm_used - mm_guess),
+                                    hipMemcpyDeviceToHost, st));
             SCHK(stream_wait(st, b.done));
         }
-        // NAM + read bytes read, window bytes compared, site + positions written
-        site_bytes = (double)total * (sizeof(rsa_nam) + sizeof(rsa_nam_site) + 2.0 * 20 + 150) + 2.0 * used;
-    } else {
-        if (out->sites == nullptr) out->mm_used = 0;
-        SCHK(stream_wait(st, b.done));
+        break;
     }
     // counters and algorithmic bytes (DESIGN.md "Kernels")
-    uint64_t n1_tot = 0, n2_tot = 0, resc_q = 0, resc_scan = 0, resc_hits = 0;
-    for (uint32_t i = 0; i < n; ++i) n1_tot += n1[i];
-    for (int i : resc) { n2_tot += n2[i]; resc_q += qcnt[i]; resc_scan += hs[i].scan_all; resc_hits += hs[i].hits_all; }
+    const uint64_t total = hh.total;
     const double QRS = sizeof(rsa_query_randstrobe), QI = sizeof(QrsInfo), RS = sizeof(rsa_ref_randstrobe),
                  NAM = sizeof(rsa_nam), HIT = sizeof(HitD);
-    c.reads = n; c.read_bases = bases; c.qrs = n_qrs; c.found = n_found; c.filtered = n_found - n_good;
-    c.hits = H; c.nams = total; c.rescued = resc.size();
-    c.alg_bytes[RSA_K_RANDSTROBES] = (double)bases + QRS * n_qrs + 24.0 * n;
-    c.alg_bytes[RSA_K_LOOKUP] = (QRS + 16 + QI) * n_qrs + 8.0 * n_found + RS * scan_all + sizeof(ReadStat) * (double)n;
-    c.alg_bytes[RSA_K_FIND_NAMS] = (QRS + QI) * n_qrs + RS * scan_find + 2 * HIT * H + NAM * n1_tot + 16.0 * n;
-    c.alg_bytes[RSA_K_RESCUE] = (QRS + QI) * resc_q + RS * resc_scan + 2 * HIT * resc_hits + NAM * n2_tot;
+    c.reads = n; c.read_bases = bases; c.qrs = hh.qrs; c.found = hh.found; c.filtered = hh.found - hh.good;
+    c.hits = hh.hits_find; c.nams = total; c.rescued = hh.resc_reads;
+    c.alg_bytes[RSA_K_RANDSTROBES] = (double)bases + QRS * hh.qrs + 24.0 * n;
+    c.alg_bytes[RSA_K_LOOKUP] = (QRS + 16 + QI) * hh.qrs + 8.0 * hh.found + RS * hh.scan_all + sizeof(ReadStat) * (double)n;
+    c.alg_bytes[RSA_K_FIND_NAMS] = (QRS + QI) * hh.qrs + RS * hh.scan_find + 2 * HIT * hh.hits_find + NAM * hh.n1 + 16.0 * n;
+    c.alg_bytes[RSA_K_RESCUE] = (QRS + QI) * hh.resc_q + RS * hh.resc_scan + 2 * HIT * hh.resc_hits + NAM * hh.n2;
     c.alg_bytes[RSA_K_COMPACT] = 2 * NAM * total + 28.0 * n;
-    c.alg_bytes[RSA_K_SITES] = (double)site_bytes;
+    // NAM + read bytes read, window bytes compared, site + positions written
+    if (out->sites)
+        c.alg_bytes[RSA_K_SITES] = (double)total * (sizeof(rsa_nam) + sizeof(rsa_nam_site) + 2.0 * 20 + 150) +
+                                   2.0 * (double)out->mm_used;
     return RSA_OK;
 }

@@ -289,6 +289,7 @@ public:
 
 private:
     void run() {
+        if (g_worker_start_hook) g_worker_start_hook();
         try {
             for (;;) {
                 {

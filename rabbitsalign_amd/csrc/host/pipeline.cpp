@@ -172,6 +172,7 @@ struct OrderedSink {
         room_cv.wait(g, [&] { return queued_bytes <= kMaxQueued; });
     }
     void write_loop() {
+        if (g_worker_start_hook) g_worker_start_hook();
         std::unique_lock<std::mutex> g(m);
         for (;;) {
             cv.wait(g, [&] { return closing || !queue.empty(); });
