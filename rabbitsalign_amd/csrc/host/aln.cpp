@@ -713,30 +713,43 @@ void align_SE_read_part(AlignTmpRes& res, const RecView&, const Read& read, std:
 }
 
 // ------------------------------------------------------ SW job strings ---
-// part2_extend_seed_get_str (pc.cpp:214-242)
-static void extend_job(const Nam& nam, const Read& read, const References& refs, std::vector<SwJob>& jobs) {
-    std::string_view query = nam.is_rc ? std::string_view(read.rc) : std::string_view(read.seq);
-    const std::string_view ref = refs.seq(nam.ref_id);
+// part2_extend_seed_get_str (pc.cpp:214-242): the window is the NAM's projection
+// onto the reference widened by |ref span - query span| and up to 50 bases on
+// each side (size_t arithmetic; std::string::substr clamps at the contig's end)
+void extension_window(const Nam& nam, size_t read_len, size_t contig_len, uint32_t& start, uint32_t& len) {
     const auto projected_ref_start = std::max(0, nam.ref_start - nam.query_start);
     const int diff = std::abs((nam.ref_end - nam.ref_start) - (nam.query_end - nam.query_start));
     const int ext_left = std::min(50, projected_ref_start);
     const int ref_start = projected_ref_start - ext_left;
-    const int ext_right = (int)std::min(std::size_t(50), ref.size() - nam.ref_end);
-    const size_t ref_segm_size = read.size() + diff + ext_left + ext_right;
-    const size_t len = std::min(ref_segm_size, ref.size() - (size_t)ref_start);
-    jobs.push_back(SwJob{query, nam.ref_id, (uint32_t)ref_start, (uint32_t)len});
+    const int ext_right = (int)std::min(std::size_t(50), contig_len - nam.ref_end);
+    const size_t ref_segm_size = read_len + diff + ext_left + ext_right;
+    start = (uint32_t)ref_start;
+    len = (uint32_t)std::min(ref_segm_size, contig_len - (size_t)ref_start);
+}
+
+static void extend_job(const Nam& nam, const Read& read, const References& refs, std::vector<SwJob>& jobs) {
+    std::string_view query = nam.is_rc ? std::string_view(read.rc) : std::string_view(read.seq);
+    uint32_t start, len;
+    extension_window(nam, read.size(), refs.seq(nam.ref_id).size(), start, len);
+    jobs.push_back(SwJob{query, nam.ref_id, start, len});
 }
 
 // part2_rescue_mate_get_str (pc.cpp:333-368)
+void rescue_mate_window(const Nam& nam, size_t read_len, float mu, float sigma, size_t contig_len, uint32_t& start,
+                        uint32_t& len) {
+    int ref_start, ref_end;
+    rescue_window(nam, read_len, mu, sigma, (int)contig_len, ref_start, ref_end);
+    const size_t s0 = std::min((size_t)ref_start, contig_len);
+    start = (uint32_t)s0;
+    len = (uint32_t)std::min((size_t)(ref_end - ref_start), contig_len - s0);
+}
+
 static void rescue_job(const Nam& nam, const Read& read, const References& refs, float mu, float sigma,
                        std::vector<SwJob>& jobs) {
     std::string_view r_tmp = nam.is_rc ? std::string_view(read.seq) : std::string_view(read.rc);
-    int ref_start, ref_end;
-    rescue_window(nam, read.size(), mu, sigma, (int)refs.seq(nam.ref_id).size(), ref_start, ref_end);
-    const size_t clen = refs.seq(nam.ref_id).size();
-    size_t start = std::min((size_t)ref_start, clen);
-    size_t len = std::min((size_t)(ref_end - ref_start), clen - start);
-    jobs.push_back(SwJob{r_tmp, nam.ref_id, (uint32_t)start, (uint32_t)len});
+    uint32_t start, len;
+    rescue_mate_window(nam, read.size(), mu, sigma, refs.seq(nam.ref_id).size(), start, len);
+    jobs.push_back(SwJob{r_tmp, nam.ref_id, start, len});
 }
 
 void collect_jobs_pe(AlignTmpRes& res, const RecView&, const RecView&, const Read& read1, const Read& read2,
@@ -760,19 +773,14 @@ void collect_jobs_pe(AlignTmpRes& res, const RecView&, const RecView&, const Rea
     }
 }
 
-// part2_extend_seed_store_res (pc.cpp:177-212)
-static void store_extend(AlignTmpRes& res, size_t j, const Read& read, const References& refs,
-                         AlignmentInfo& info) {
-    const Nam& nam = res.todo_nams[j];
-    const std::string_view ref = refs.seq(nam.ref_id);
-    const size_t qsize = read.size();
+// part2_extend_seed_store_res (pc.cpp:177-212): the alignment's reference start is
+// the window start plus the aligner's; global_ed adds both soft clips
+void extension_alignment(const Nam& nam, size_t read_len, AlignmentInfo& info, Alignment& a) {
     const auto projected_ref_start = std::max(0, nam.ref_start - nam.query_start);
     const int ext_left = std::min(50, projected_ref_start);
     const int ref_start = projected_ref_start - ext_left;
-    (void)ref;
     int result_ref_start = ref_start + (int)info.ref_start;
-    int softclipped = (int)info.query_start + ((int)qsize - (int)info.query_end);
-    Alignment& a = res.align_res[j];
+    int softclipped = (int)info.query_start + ((int)read_len - (int)info.query_end);
     a.cigar = std::move(info.cigar);               // each result is stored exactly once
     a.edit_distance = (int)info.edit_distance;
     a.global_ed = (int)info.edit_distance + softclipped;
@@ -785,13 +793,17 @@ static void store_extend(AlignTmpRes& res, size_t j, const Read& read, const Ref
     a.gapped = true;
 }
 
-// part2_rescue_mate_store_res (pc.cpp:291-331)
-static void store_rescue(AlignTmpRes& res, size_t j, const Read& read, const References& refs, float mu, float sigma,
-                         AlignmentInfo& info) {
-    const Nam& nam = res.todo_nams[j];
+static void store_extend(AlignTmpRes& res, size_t j, const Read& read, AlignmentInfo& info) {
+    extension_alignment(res.todo_nams[j], read.size(), info, res.align_res[j]);
+}
+
+// part2_rescue_mate_store_res (pc.cpp:291-331): the mate lands on the other strand;
+// an empty CIGAR (the aligner's sentinels) leaves it unaligned.  global_ed and
+// gapped keep what part() left in the slot
+void rescue_alignment(const Nam& nam, size_t read_len, float mu, float sigma, size_t contig_len, AlignmentInfo& info,
+                      Alignment& a) {
     int ref_start, ref_end;
-    rescue_window(nam, read.size(), mu, sigma, (int)refs.seq(nam.ref_id).size(), ref_start, ref_end);
-    Alignment& a = res.align_res[j];
+    rescue_window(nam, read_len, mu, sigma, (int)contig_len, ref_start, ref_end);
     a.is_unaligned = info.cigar.empty();
     a.cigar = std::move(info.cigar);               // each result is stored exactly once
     a.edit_distance = (int)info.edit_distance;
@@ -802,22 +814,28 @@ static void store_rescue(AlignTmpRes& res, size_t j, const Read& read, const Ref
     a.length = info.ref_span();
 }
 
+static void store_rescue(AlignTmpRes& res, size_t j, const Read& read, const References& refs, float mu, float sigma,
+                         AlignmentInfo& info) {
+    const Nam& nam = res.todo_nams[j];
+    rescue_alignment(nam, read.size(), mu, sigma, refs.seq(nam.ref_id).size(), info, res.align_res[j]);
+}
+
 size_t store_results_pe(AlignTmpRes& res, const Read& read1, const Read& read2, const MapContext& mc, float mu,
                         float sigma, std::vector<AlignmentInfo>& infos, size_t pos) {
     const size_t n = res.todo_nams.size();
     auto rd = [&](size_t j) -> const Read& { return res.is_read1[j] ? read1 : read2; };
     if (res.type == 1 || res.type == 2) {
         for (size_t j = 0; j < n; j += 2) {
-            if (!res.done_align[j]) store_extend(res, j, rd(j), mc.refs, infos[pos++]);
+            if (!res.done_align[j]) store_extend(res, j, rd(j), infos[pos++]);
             if (!res.done_align[j + 1]) store_rescue(res, j + 1, rd(j + 1), mc.refs, mu, sigma, infos[pos++]);
         }
     } else if (res.type == 3) {
-        if (!res.done_align[0]) store_extend(res, 0, rd(0), mc.refs, infos[pos++]);
-        if (!res.done_align[1]) store_extend(res, 1, rd(1), mc.refs, infos[pos++]);
+        if (!res.done_align[0]) store_extend(res, 0, rd(0), infos[pos++]);
+        if (!res.done_align[1]) store_extend(res, 1, rd(1), infos[pos++]);
     } else if (res.type == 4) {
         for (size_t j = 0; j < n; ++j) {
             if (res.done_align[j]) continue;
-            if (res.is_extend_seed[j]) store_extend(res, j, rd(j), mc.refs, infos[pos++]);
+            if (res.is_extend_seed[j]) store_extend(res, j, rd(j), infos[pos++]);
             else store_rescue(res, j, rd(j), mc.refs, mu, sigma, infos[pos++]);
         }
     }
@@ -834,7 +852,7 @@ size_t store_results_se(AlignTmpRes& res, const Read& read, const MapContext& mc
                         std::vector<AlignmentInfo>& infos, size_t pos) {
     if (res.type != 4) return pos;
     for (size_t j = 0; j < res.todo_nams.size(); ++j)
-        if (!res.done_align[j] && res.is_extend_seed[j]) store_extend(res, j, read, mc.refs, infos[pos++]);
+        if (!res.done_align[j] && res.is_extend_seed[j]) store_extend(res, j, read, infos[pos++]);
     return pos;
 }
 

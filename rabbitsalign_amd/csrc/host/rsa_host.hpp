@@ -449,6 +449,19 @@ void collect_jobs_se(AlignTmpRes& res, const Read& read, const MapContext& mc, s
 size_t store_results_se(AlignTmpRes& res, const Read& read, const MapContext& mc,
                         std::vector<AlignmentInfo>& infos, size_t pos);
 
+// The pieces of those two that are pure arithmetic on one job, also used by the
+// hand-derived host cases (tests/host_cases.py through bin/rsa_host_cases):
+// extension_window: the reference window [start, start + len) of an extension job
+// (pc.cpp:214-242); rescue_mate_window: of a mate rescue job (pc.cpp:333-368, with
+// its int / size_t / float arithmetic); extension_alignment / rescue_alignment:
+// the Alignment stored from the aligner's result (pc.cpp:177-212, 291-331).
+void extension_window(const Nam& nam, size_t read_len, size_t contig_len, uint32_t& start, uint32_t& len);
+void rescue_mate_window(const Nam& nam, size_t read_len, float mu, float sigma, size_t contig_len, uint32_t& start,
+                        uint32_t& len);
+void extension_alignment(const Nam& nam, size_t read_len, AlignmentInfo& info, Alignment& a);
+void rescue_alignment(const Nam& nam, size_t read_len, float mu, float sigma, size_t contig_len, AlignmentInfo& info,
+                      Alignment& a);
+
 // Order-sensitive digest of a SAM body, independent of how it is chunked:
 // D = sum_k line_hash(line_k) * P^(N-1-k) mod 2^64 over the N lines (without '\n').
 // line_hash runs four independent 64-bit multiply-rotate lanes over 32-byte

@@ -4,7 +4,7 @@ out from the source text in the comment next to it; test_oracle_golden checks th
 oracle's restatement against them and test_extend_gpu the GPU path."""
 import random
 
-EQ, X, S = 7, 8, 4
+EQ, X, S, I, D = 7, 8, 4, 1, 2
 
 
 def op(n, o):
@@ -61,7 +61,30 @@ def cases():
             q6[i] = _flip(q6[i])
     out.append(("ref_start_clip", bytes(q6), bytes(R), dict(sw_score=104, edit_distance=0, ref_start=0, ref_end=47,
                                                            query_start=3, query_end=50, cigar=[op(3, S), op(47, EQ)])))
-    # 7. window longer than 2000: the sentinel (aligner.cpp:119-125)
+    # 7. both ends clipped: five flipped bases on each side of an exact 40-mer.  SSW's local
+    #    maximum is the 40-mer (80; a flank base costs 8, a gap to reach a match 12 > the 10
+    #    five matches could bring); the front extension scores 80 - 5 * 8 = 40 and 40 + 10 is
+    #    not > 80, the back extension likewise: 5S40=5S, no edits (S is not counted)
+    q7 = bytearray(R[10:60])
+    for i in list(range(0, 5)) + list(range(45, 50)):
+        q7[i] = _flip(q7[i])
+    out.append(("both_clipped", bytes(q7), bytes(R), dict(sw_score=80, edit_distance=0, ref_start=15, ref_end=55,
+                                                         query_start=5, query_end=45,
+                                                         cigar=[op(5, S), op(40, EQ), op(5, S)])))
+    # 8. one reference base (R[40] = 'C', between 'T' and 'A': no equal neighbour, so the
+    #    gap has one place) missing from the query: 59 matches - gap_open 12 = 106; both
+    #    ends reached -> +10 +10 = 126; D counts as an edit (ssw_cpp.cpp:126-210)
+    q8 = bytes(R[10:40] + R[41:70])
+    out.append(("deletion", q8, bytes(R), dict(sw_score=126, edit_distance=1, ref_start=10, ref_end=70,
+                                               query_start=0, query_end=59,
+                                               cigar=[op(30, EQ), op(1, D), op(29, EQ)])))
+    # 9. a 'G' inserted between R[39] = 'T' and R[40] = 'C' (equal to neither): 60 matches -
+    #    12 = 108, +20 -> 128, one I edit, the query end is 61
+    q9 = bytes(R[10:40] + b"G" + R[40:70])
+    out.append(("insertion", q9, bytes(R), dict(sw_score=128, edit_distance=1, ref_start=10, ref_end=70,
+                                                query_start=0, query_end=61,
+                                                cigar=[op(30, EQ), op(1, I), op(30, EQ)])))
+    # 10. window longer than 2000: the sentinel (aligner.cpp:119-125)
     out.append(("ref_gt_2000", bytes(R[10:60]), bytes(_ref(3, 2001)), dict(sw_score=-1000000, edit_distance=100000,
                                                                            ref_start=0)))
     return out
