@@ -66,9 +66,9 @@ struct SeedHdr {
     unsigned long long total;       // final NAMs of the batch
     unsigned long long mm_used;     // mismatch positions of the site checks
     uint32_t big_count;             // reads listed for k_find_nams_big
+    uint32_t rcount;                // reads listed for find_nams_rescue
     uint32_t rbig_count;            // rescued reads listed for k_rescue_big
     uint32_t errors;                // SEED_E_*
-    uint32_t pad_;
     // statistics (DESIGN.md "Kernels": algorithmic bytes and per-read counts)
     unsigned long long qrs, found, good, hits_find, hits_all, scan_find, scan_all, n1, n2, resc_reads, resc_q,
         resc_scan, resc_hits;
@@ -466,7 +466,7 @@ __device__ __forceinline__ int wave_excl_scan_lk(int v, int lane, int& total) {
 __global__ void __launch_bounds__(256)
 k_lookup(const rsa_query_randstrobe* __restrict__ qrs, const uint32_t* __restrict__ qcnt,
          const uint64_t* __restrict__ qbase, int n_reads, SeedIndexParams p, QrsInfo* __restrict__ qi,
-         ReadStat* __restrict__ st, HitD* __restrict__ hit_slots, SeedHdr* __restrict__ hdr) {
+         ReadStat* __restrict__ st, HitD* __restrict__ hit_slots) {
     const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (wave >= n_reads) return;
@@ -557,13 +557,6 @@ k_lookup(const rsa_query_randstrobe* __restrict__ qrs, const uint32_t* __restric
         ReadStat s;
         s.found = found; s.good = good; s.hits_find = hfind; s.hits_all = hall; s.scan_find = sfind; s.scan_all = sall;
         st[r] = s;
-        atomicAdd(&hdr->qrs, (unsigned long long)nq);
-        if (found) atomicAdd(&hdr->found, (unsigned long long)found);
-        if (good) atomicAdd(&hdr->good, (unsigned long long)good);
-        if (hfind) atomicAdd(&hdr->hits_find, (unsigned long long)hfind);
-        if (hall) atomicAdd(&hdr->hits_all, (unsigned long long)hall);
-        if (sfind) atomicAdd(&hdr->scan_find, (unsigned long long)sfind);
-        if (sall) atomicAdd(&hdr->scan_all, (unsigned long long)sall);
     }
 }
 
@@ -1333,37 +1326,47 @@ __device__ void rescue_read(int r, const rsa_query_randstrobe* __restrict__ qrs,
     flags[r] = (flags[r] & ~4u) | 8u;   // bit3: rescued result present
 }
 
-// find_nams_rescue for every read that needs it (aln.cpp:1954-1962: rescue_level
-// > 1 and no NAMs or nonrepetitive_fraction < 0.7), decided here from
-// k_find_nams' results: one wave per read, lane 0, maps in LDS.  Most waves
-// leave at once.  Each rescued read takes hits_all pool entries.
-__global__ void __launch_bounds__(64 * FN_WAVES)
-k_rescue_all(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi,
-             const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, const ReadStat* __restrict__ st,
-             int n_reads, SeedIndexParams p, int32_t rescue_level, uint32_t rescue_cutoff, RescueD* __restrict__ rbuf,
-             SeedPool pool, const uint32_t* __restrict__ ncnt1, const float* __restrict__ nonrep,
-             uint32_t* __restrict__ ncnt2, uint32_t* __restrict__ flags, uint64_t* __restrict__ rbase,
-             uint8_t* __restrict__ rescued, SeedHdr* __restrict__ hdr, uint32_t* __restrict__ rbig_list) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_map[FN_WAVES][FN_MAP_CAP * 9 * 4];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int r = blockIdx.x * FN_WAVES + w;
-    if (r >= n_reads || lane != 0) return;
+// The rescue decision (aln.cpp:1954-1962: rescue_level > 1 and no NAMs or
+// nonrepetitive_fraction < 0.7) from k_find_nams' results, one thread a read:
+// the reads that need find_nams_rescue are listed and take hits_all pool
+// entries each (one atomic per rescued read; most reads take none).
+__global__ void __launch_bounds__(256)
+k_rescue_select(int n_reads, int32_t rescue_level, const ReadStat* __restrict__ st, const uint32_t* __restrict__ ncnt1,
+                const float* __restrict__ nonrep, uint32_t* __restrict__ ncnt2, uint64_t* __restrict__ rbase,
+                uint8_t* __restrict__ rescued, uint64_t pool_n, SeedHdr* __restrict__ hdr,
+                uint32_t* __restrict__ rlist) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_reads) return;
     const bool need = rescue_level > 1 && (ncnt1[r] == 0 || nonrep[r] < 0.7f);
     rescued[r] = need ? 1 : 0;
     ncnt2[r] = 0;
     if (!need) return;
-    const ReadStat rs = st[r];
-    const uint32_t ha = rs.hits_all;
-    atomicAdd(&hdr->resc_reads, 1ull);
-    atomicAdd(&hdr->resc_q, (unsigned long long)qcnt[r]);
-    atomicAdd(&hdr->resc_scan, (unsigned long long)rs.scan_all);
-    atomicAdd(&hdr->resc_hits, (unsigned long long)ha);
+    const uint32_t ha = st[r].hits_all;
     const unsigned long long e = atomicAdd(&hdr->pool_used, (unsigned long long)ha);
-    if (e + ha > pool.n) { atomicOr(&hdr->errors, SEED_E_POOL); return; }
+    if (e + ha > pool_n) { atomicOr(&hdr->errors, SEED_E_POOL); return; }
     rbase[r] = e;
-    rescue_read(r, qrs, qi, qcnt, qbase, rbase, p, rescue_cutoff, rbuf, pool.hits, pool.open, pool.nams, pool.grp,
-                pool.added, s_map[w], FN_MAP_CAP, ncnt2, flags);
-    if (flags[r] & 4u) rbig_list[atomicAdd(&hdr->rbig_count, 1u)] = (uint32_t)r;
+    rlist[atomicAdd(&hdr->rcount, 1u)] = (uint32_t)r;
+}
+
+// find_nams_rescue (nam.cpp:955-1012) of the listed reads: one wave per read,
+// lane 0, maps in LDS; a fixed grid walks the device list
+#define RESCUE_GRID 256
+__global__ void __launch_bounds__(64 * FN_WAVES)
+k_rescue_w(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi,
+           const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, SeedIndexParams p,
+           uint32_t rescue_cutoff, RescueD* __restrict__ rbuf, SeedPool pool, uint32_t* __restrict__ ncnt2,
+           uint32_t* __restrict__ flags, const uint64_t* __restrict__ rbase, SeedHdr* __restrict__ hdr,
+           const uint32_t* __restrict__ rlist, uint32_t* __restrict__ rbig_list) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_map[FN_WAVES][FN_MAP_CAP * 9 * 4];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane != 0) return;
+    const uint32_t nr = hdr->rcount;
+    for (uint32_t t = blockIdx.x * FN_WAVES + w; t < nr; t += gridDim.x * FN_WAVES) {
+        const int r = (int)rlist[t];
+        rescue_read(r, qrs, qi, qcnt, qbase, rbase, p, rescue_cutoff, rbuf, pool.hits, pool.open, pool.nams, pool.grp,
+                    pool.added, s_map[w], FN_MAP_CAP, ncnt2, flags);
+        if (flags[r] & 4u) rbig_list[atomicAdd(&hdr->rbig_count, 1u)] = (uint32_t)r;
+    }
 }
 
 // the rescued reads whose maps outgrow LDS: one lane per read, global map scratch,
@@ -1386,23 +1389,35 @@ k_rescue_big(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __rest
 }
 
 // final NAM offsets: count[r] = rescued ? rescue NAMs : find NAMs, exclusive scan
-// into ooff[0..n] (one workgroup, each thread a run of reads), total into the header
+// into ooff[0..n] (one workgroup, each thread a run of reads), total into the
+// header, and the call's statistics summed over the reads (LDS atomics, one
+// global write each: k_lookup's 20 k waves adding to one address serialised)
+#define SEED_NSTAT 13
 __global__ void __launch_bounds__(1024)
 k_seed_scan(int n_reads, const uint8_t* __restrict__ rescued, const uint32_t* __restrict__ ncnt1,
-            const uint32_t* __restrict__ ncnt2, uint64_t* __restrict__ ooff, SeedHdr* __restrict__ hdr) {
+            const uint32_t* __restrict__ ncnt2, const uint32_t* __restrict__ qcnt, const ReadStat* __restrict__ st,
+            uint64_t* __restrict__ ooff, SeedHdr* __restrict__ hdr) {
     __shared__ uint64_t s[1024];
+    __shared__ unsigned long long s_stat[SEED_NSTAT];
     const int t = threadIdx.x;
+    if (t < SEED_NSTAT) s_stat[t] = 0;
     const int per = (n_reads + 1023) / 1024;
     const int a = min(n_reads, t * per), b = min(n_reads, a + per);
-    uint64_t mine = 0, n1 = 0, n2 = 0;
+    uint64_t mine = 0;
+    uint64_t v[SEED_NSTAT] = {0};    // qrs found good hits_find hits_all scan_find scan_all n1 n2 rr rq rscan rhits
     for (int r = a; r < b; ++r) {
-        const uint64_t c1 = ncnt1[r], c2 = rescued[r] ? ncnt2[r] : 0;
-        mine += rescued[r] ? c2 : c1;
-        n1 += c1;
-        n2 += c2;
+        const bool rs = rescued[r] != 0;
+        const uint64_t c1 = ncnt1[r], c2 = rs ? ncnt2[r] : 0;
+        mine += rs ? c2 : c1;
+        const ReadStat x = st[r];
+        v[0] += qcnt[r]; v[1] += x.found; v[2] += x.good; v[3] += x.hits_find; v[4] += x.hits_all;
+        v[5] += x.scan_find; v[6] += x.scan_all; v[7] += c1; v[8] += c2;
+        if (rs) { v[9] += 1; v[10] += qcnt[r]; v[11] += x.scan_all; v[12] += x.hits_all; }
     }
     s[t] = mine;
     __syncthreads();
+    for (int k = 0; k < SEED_NSTAT; ++k)
+        if (v[k]) atomicAdd(&s_stat[k], (unsigned long long)v[k]);
     for (int o = 1; o < 1024; o <<= 1) {
         const uint64_t x = t >= o ? s[t - o] : 0;
         __syncthreads();
@@ -1414,9 +1429,13 @@ k_seed_scan(int n_reads, const uint8_t* __restrict__ rescued, const uint32_t* __
         ooff[r] = off;
         off += rescued[r] ? ncnt2[r] : ncnt1[r];
     }
-    if (n1) atomicAdd(&hdr->n1, (unsigned long long)n1);
-    if (n2) atomicAdd(&hdr->n2, (unsigned long long)n2);
     if (t == 1023) { ooff[n_reads] = s[t]; hdr->total = s[t]; }
+    if (t == 0) {
+        hdr->qrs = s_stat[0]; hdr->found = s_stat[1]; hdr->good = s_stat[2]; hdr->hits_find = s_stat[3];
+        hdr->hits_all = s_stat[4]; hdr->scan_find = s_stat[5]; hdr->scan_all = s_stat[6]; hdr->n1 = s_stat[7];
+        hdr->n2 = s_stat[8]; hdr->resc_reads = s_stat[9]; hdr->resc_q = s_stat[10]; hdr->resc_scan = s_stat[11];
+        hdr->resc_hits = s_stat[12];
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1592,7 +1611,7 @@ k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read,
 enum {
     B_SEQ, B_ROFF, B_RLEN, B_QBASE, B_QRS, B_QCNT, B_SYNC, B_QI, B_ST, B_X, B_ARENA, B_PHIT, B_POPEN, B_PGRP, B_PADD,
     B_NCNT1, B_FLAGS, B_MAP, B_NCNT2, B_NSRC, B_RBASE, B_BIGL, B_RBIGL, B_RBUF, B_OUT, B_SLOTS, B_SITES, B_POOL,
-    B_NREAD, B_RSLIST
+    B_NREAD, B_RSLIST, B_RLIST
 };
 // every host side of a transfer is page-locked: a pageable one would make the copy synchronous
 enum { H_X, H_QBASE, H_RSLIST };
@@ -1790,6 +1809,7 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
     SCHK(dens(b, B_RBASE, 8ull * n));
     SCHK(dens(b, B_BIGL, 4ull * n));
     SCHK(dens(b, B_RBIGL, 4ull * n));
+    SCHK(dens(b, B_RLIST, 4ull * n));
     SCHK(dens(b, B_RBUF, sizeof(RescueD) * (nq_cap + 1)));
     SCHK(dens(b, B_MAP, (size_t)MAP_BIG * 9 * 4 * MAP_BIG_LANES));
     SCHK(dens(b, B_OUT, sizeof(rsa_nam) * (cap + 1)));
@@ -1842,7 +1862,7 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
         kt.begin(st, RSA_K_LOOKUP);
         hipLaunchKernelGGL(k_lookup, dim3((n + 3) / 4), dim3(256), 0, st, DP(B_QRS, rsa_query_randstrobe),
                            DP(B_QCNT, uint32_t), d_qbase, (int)n, p, DP(B_QI, QrsInfo), DP(B_ST, ReadStat),
-                           DP(B_SLOTS, HitD), dhdr);
+                           DP(B_SLOTS, HitD));
         SCHK(hipGetLastError());
         kt.end(st);
         // 3. find_nams (nam.cpp:771-926): LDS maps, then the listed reads with global maps
@@ -1859,11 +1879,13 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
         kt.end(st);
         // 4. rescue (aln.cpp:1954-1962, nam.cpp:955-1012)
         kt.begin(st, RSA_K_RESCUE);
-        hipLaunchKernelGGL(k_rescue_all, dim3((n + FN_WAVES - 1) / FN_WAVES), dim3(64 * FN_WAVES), 0, st,
-                           DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t), d_qbase,
-                           DP(B_ST, ReadStat), (int)n, p, rescue_level, rescue_cutoff, DP(B_RBUF, RescueD), pool,
-                           DP(B_NCNT1, uint32_t), d_nonrep, DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t),
-                           DP(B_RBASE, uint64_t), d_resc, dhdr, DP(B_RBIGL, uint32_t));
+        hipLaunchKernelGGL(k_rescue_select, dim3((n + 255) / 256), dim3(256), 0, st, (int)n, rescue_level,
+                           DP(B_ST, ReadStat), DP(B_NCNT1, uint32_t), d_nonrep, DP(B_NCNT2, uint32_t),
+                           DP(B_RBASE, uint64_t), d_resc, b.pool_n, dhdr, DP(B_RLIST, uint32_t));
+        hipLaunchKernelGGL(k_rescue_w, dim3(RESCUE_GRID), dim3(64 * FN_WAVES), 0, st, DP(B_QRS, rsa_query_randstrobe),
+                           DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t), d_qbase, p, rescue_cutoff, DP(B_RBUF, RescueD),
+                           pool, DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t), DP(B_RBASE, uint64_t), dhdr,
+                           DP(B_RLIST, uint32_t), DP(B_RBIGL, uint32_t));
         hipLaunchKernelGGL(k_rescue_big, dim3(1), dim3(64), 0, st, DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo),
                            DP(B_QCNT, uint32_t), d_qbase, p, rescue_cutoff, DP(B_RBUF, RescueD), pool,
                            DP(B_MAP, uint8_t), MAP_BIG, DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t),
@@ -1873,7 +1895,7 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
         // 5. final offsets and the NAM lists back to back
         kt.begin(st, RSA_K_COMPACT);
         hipLaunchKernelGGL(k_seed_scan, dim3(1), dim3(1024), 0, st, (int)n, d_resc, DP(B_NCNT1, uint32_t),
-                           DP(B_NCNT2, uint32_t), d_ooff, dhdr);
+                           DP(B_NCNT2, uint32_t), DP(B_QCNT, uint32_t), DP(B_ST, ReadStat), d_ooff, dhdr);
         hipLaunchKernelGGL(k_compact, dim3(n), dim3(64), 0, st, (int)n, DP(B_NSRC, uint64_t), DP(B_RBASE, uint64_t),
                            slots, DP(B_NCNT1, uint32_t), DP(B_NCNT2, uint32_t), d_resc, DP(B_ARENA, rsa_nam), d_ooff,
                            cap, DP(B_OUT, rsa_nam), out->sites ? DP(B_NREAD, uint32_t) : nullptr);
