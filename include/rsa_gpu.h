@@ -294,10 +294,7 @@ typedef struct rsa_kernel_stats {
     uint64_t seed_calls, ext_calls;
     uint64_t reads, read_bases, query_randstrobes, lookups_found, filtered, hits, nams, rescued_reads;
     uint64_t jobs, dp_cells;         /* dp_cells: sum query_len * ref_len of the forward scan */
-    uint64_t band_deferred, band_overflow;   /* jobs handed to the 64-lane / one-lane band kernels */
-    uint64_t scan_pair_jobs;         /* jobs through the word-layout pair scan (k_ext_scan_w2) */
-    uint64_t scan_rescans;           /* of those, jobs whose alignment did not prove the byte layout
-                                        saturated: rescanned exactly (one-job-per-wave scan) */
+    uint64_t band_deferred, band_overflow;   /* jobs handed to the 64-lane / panel band kernels */
     /* wall time of the calls ([0] rsa_seed, [1] rsa_extend), ms summed over calls: whole call,
      * waiting for a free stream lane, blocked on the device (event waits); the rest is host work */
     double call_ms[2], lane_wait_ms[2], device_wait_ms[2];

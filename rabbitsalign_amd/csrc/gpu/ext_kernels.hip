@@ -365,11 +365,7 @@ __device__ __forceinline__ void cpush(uint32_t* c, int& n, uint32_t op, uint32_t
 // ref_begin1.. (the band kernels hold them in LDS); without them the =/X split
 // translates the bytes from global memory.
 //
-// Returns the SSW score of the raw path itself (match / -mismatch per aligned
-// column, N never matching; gap_open + (len - 1) gap_extend per gap), or INT_MIN
-// when the path leaves the window or has an insertion next to a deletion: the
-// pair scan's check (k_ext_scan_w2) that the byte layout would have saturated.
-__device__ int ext_finish(const ExtJobDev& jb, const ScanRes& sr, const char* __restrict__ q,
+__device__ void ext_finish(const ExtJobDev& jb, const ScanRes& sr, const char* __restrict__ q,
                           const char* __restrict__ r, const uint32_t* __restrict__ raw, int nraw,
                           uint32_t* __restrict__ c, rsa_aln& a, int match, int mismatch, int bonus, int gO, int gE,
                           const uint8_t* qcs = nullptr, const uint8_t* rcs = nullptr) {
@@ -385,18 +381,9 @@ __device__ int ext_finish(const ExtJobDev& jb, const ScanRes& sr, const char* __
     int rp = sr.ref_begin1, qp = qs0;
     int in_m = 0, in_x = 0;
     uint32_t len_m = 0, len_x = 0;
-    int pscore = 0;             // the path's own score
-    bool pbad = false;          // out of the window, or I next to D
-    uint32_t pgap = 0;          // type of the last non-empty op when it was a gap (1 = I, 2 = D)
     for (int k = 0; k < nraw; ++k) {
         const uint32_t opk = raw[k] & 0xf, lenk = raw[k] >> 4;
-        if (lenk != 0) {
-            if ((opk == 1 && pgap == 2) || (opk == 2 && pgap == 1)) pbad = true;
-            pgap = (opk == 1 || opk == 2) ? opk : 0;
-            if (opk == 1 || opk == 2) pscore -= gO + (int)(lenk - 1) * gE;
-        }
         if (opk == 0) {
-            if (rp < 0 || rp + (int)lenk > rlen || qp + (int)lenk > qlen) pbad = true;
             for (uint32_t z = 0; z < lenk; ++z) {
                 int rcode, qcode;
                 const int qo = qp - qs0, ro = rp - sr.ref_begin1;
@@ -407,7 +394,6 @@ __device__ int ext_finish(const ExtJobDev& jb, const ScanRes& sr, const char* __
                     rcode = (rp >= 0 && rp < rlen) ? ssw_code((unsigned char)r[rp]) : 4;
                     qcode = ssw_code((unsigned char)q[qp]);
                 }
-                pscore += (rcode == qcode && qcode < 4) ? match : -mismatch;
                 if (rcode != qcode) {
                     ++mism;
                     if (in_m) core[n++] = cig(len_m, 7);
@@ -488,17 +474,6 @@ __device__ int ext_finish(const ExtJobDev& jb, const ScanRes& sr, const char* __
     }
     a.sw_score = sw; a.edit_distance = ed; a.ref_start = rs; a.ref_end = re; a.query_start = qs; a.query_end = qe;
     a.cigar_len = (uint32_t)final_n;
-    return pbad ? INT_MIN : pscore;
-}
-
-// a pair-scan result (word == 3) whose alignment does not prove the byte layout
-// saturated: flag it for the exact rescan (rsa_ctx.hip's one-lane pass)
-__device__ __forceinline__ void w2_check(const ScanRes& sr, int pscore, int mismatch, int j, int* __restrict__ overflow,
-                                         int* __restrict__ rcount) {
-    if (sr.word == 3 && !(pscore != INT_MIN && pscore + mismatch >= 255)) {
-        overflow[j] = 3;
-        atomicAdd(rcount, 1);
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -617,8 +592,7 @@ template <int G, int DIRCAP, int QCAP, int RCAP>
 __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr, const char* __restrict__ qbuf,
                            const char* __restrict__ ref, uint32_t* __restrict__ cig_pool,
                            uint32_t* __restrict__ raw_pool, rsa_aln* __restrict__ out, int match, int mismatch,
-                           int gO, int gE, int bonus, int8_t* dir, uint8_t* qc, uint8_t* rc, int* __restrict__ overflow,
-                           int* __restrict__ rcount) {
+                           int gO, int gE, int bonus, int8_t* dir, uint8_t* qc, uint8_t* rc) {
     const char* q = qbuf + jb.q_off;
     const char* r = ref + jb.r_off;
     const int rlen = (int)jb.rlen;
@@ -725,15 +699,13 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
     }
     if (fail) {                                     // banded_sw failed -> flag 1 sentinel
         aln_sentinel(out, j, jb, -100000);
-        w2_check(sr, INT_MIN, mismatch, j, overflow, rcount);
         return true;
     }
     if (op == 0) { ++l; raw[l - 1] = cig((uint32_t)ecount + 1, op); }
     else { l += 2; raw[l - 2] = cig((uint32_t)ecount, op); raw[l - 1] = cig(1, 0); }
     for (int s = 0, t = l - 1; s < t; ++s, --t) { const uint32_t x = raw[s]; raw[s] = raw[t]; raw[t] = x; }
-    const int ps = ext_finish(jb, sr, q, r, raw, l, cig_pool + jb.cig_off, a, match, mismatch, bonus, gO, gE, qc, rc);
+    ext_finish(jb, sr, q, r, raw, l, cig_pool + jb.cig_off, a, match, mismatch, bonus, gO, gE, qc, rc);
     out[j] = a;
-    w2_check(sr, ps, mismatch, j, overflow, rcount);
     return true;
 }
 
@@ -745,8 +717,7 @@ __global__ void __launch_bounds__(64)
 k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan, int n_jobs,
              const char* __restrict__ qbuf, const char* __restrict__ ref, uint32_t* __restrict__ cig_pool,
              uint32_t* __restrict__ raw_pool, rsa_aln* __restrict__ out, int match, int mismatch, int gO, int gE,
-             int bonus, int* __restrict__ queue, int* __restrict__ qcount, int* __restrict__ overflow,
-             int* __restrict__ rcount) {
+             int bonus, int* __restrict__ queue, int* __restrict__ qcount, int* __restrict__ overflow) {
     __shared__ __attribute__((aligned(16))) int8_t s_dir[B16_GROUPS][B16_DIRCAP];
     __shared__ uint8_t s_qc[B16_GROUPS][B16_SEGCAP];
     __shared__ uint8_t s_rc[B16_GROUPS][B16_SEGCAP];
@@ -761,15 +732,11 @@ k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
         return;
     }
     if (sr.flag != 0) {                            // aligner.cpp:131-136
-        if (z == 0) {
-            aln_sentinel(out, j, jb, -100000);
-            w2_check(sr, INT_MIN, mismatch, j, overflow, rcount);
-        }
+        if (z == 0) aln_sentinel(out, j, jb, -100000);
         return;
     }
     const bool done = band_group<16, B16_DIRCAP, B16_SEGCAP, B16_SEGCAP>(
-        j, z, jb, sr, qbuf, ref, cig_pool, raw_pool, out, match, mismatch, gO, gE, bonus, s_dir[g], s_qc[g], s_rc[g],
-        overflow, rcount);
+        j, z, jb, sr, qbuf, ref, cig_pool, raw_pool, out, match, mismatch, gO, gE, bonus, s_dir[g], s_qc[g], s_rc[g]);
     if (!done && z == 0) {
         // an empty result until a wider kernel writes it: the CIGAR compaction reads
         // every job, including one the 64-lane kernel leaves to the one-lane pass
@@ -790,7 +757,7 @@ k_ext_band64(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
              const char* __restrict__ ref, uint32_t* __restrict__ cig_pool, uint32_t* __restrict__ raw_pool,
              rsa_aln* __restrict__ out, int match, int mismatch, int gO, int gE, int bonus,
              const int* __restrict__ queue, const int* __restrict__ qcount, int* __restrict__ overflow,
-             int* __restrict__ ocount, int* __restrict__ rcount) {
+             int* __restrict__ ocount) {
     __shared__ __attribute__((aligned(16))) int8_t s_dir[B64_DIRCAP];
     __shared__ uint8_t s_qc[B64_QCAP];
     __shared__ uint8_t s_rc[B64_RCAP];
@@ -801,8 +768,7 @@ k_ext_band64(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
         const ExtJobDev jb = jobs[j];
         const ScanRes sr = scan[j];
         const bool done = band_group<64, B64_DIRCAP, B64_QCAP, B64_RCAP>(
-            j, z, jb, sr, qbuf, ref, cig_pool, raw_pool, out, match, mismatch, gO, gE, bonus, s_dir, s_qc, s_rc,
-            overflow, rcount);
+            j, z, jb, sr, qbuf, ref, cig_pool, raw_pool, out, match, mismatch, gO, gE, bonus, s_dir, s_qc, s_rc);
         if (!done && z == 0) { overflow[j] = 1; atomicAdd(ocount, 1); }
         WSYNC();
     }
@@ -973,7 +939,7 @@ k_ext_band_panel(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__
     if (op == 0) { ++l; raw[l - 1] = cig((uint32_t)ecount + 1, op); }
     else { l += 2; raw[l - 2] = cig((uint32_t)ecount, op); raw[l - 1] = cig(1, 0); }
     for (int s = 0, e = l - 1; s < e; ++s, --e) { const uint32_t x = raw[s]; raw[s] = raw[e]; raw[e] = x; }
-    (void)ext_finish(jb, sr, q, r, raw, l, cig_pool + jb.cig_off, a, match, mismatch, bonus, gO, gE, s_qc, s_rc);
+    ext_finish(jb, sr, q, r, raw, l, cig_pool + jb.cig_off, a, match, mismatch, bonus, gO, gE, s_qc, s_rc);
     out[j] = a;
 }
 
@@ -1077,31 +1043,16 @@ void launch_ext_scan(int rmax, dim3 grid, dim3 block, hipStream_t st, const ExtJ
 #undef RSA_L
 }
 
-// test switch (RSA_W2_FORCE_RESCAN=1): every pair-scan result goes through the
-// exact rescan, as if its alignment had not proven the byte layout saturated
-__global__ void k_w2_force(const ScanRes* __restrict__ scan, int n, int* __restrict__ overflow, int* __restrict__ rcount) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < n && scan[j].word == 3 && overflow[j] == 0) {
-        overflow[j] = 3;
-        atomicAdd(rcount, 1);
-    }
-}
-
-void launch_w2_force(hipStream_t st, const ScanRes* scan, int n, int* overflow, int* rcount) {
-    hipLaunchKernelGGL(k_w2_force, dim3((n + 255) / 256), dim3(256), 0, st, scan, n, overflow, rcount);
-}
-
 void launch_ext_band16(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n, const char* q,
                        const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match, int mismatch, int gO,
-                       int gE, int bonus, int* queue, int* qcount, int* overflow, int* rcount) {
+                       int gE, int bonus, int* queue, int* qcount, int* overflow) {
     hipLaunchKernelGGL(k_ext_band16, grid, dim3(64), 0, st, jobs, scan, n, q, ref, cig, raw, out, match, mismatch, gO,
-                       gE, bonus, queue, qcount, overflow, rcount);
+                       gE, bonus, queue, qcount, overflow);
 }
 
 void launch_ext_band64(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, const char* q,
                        const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match, int mismatch, int gO,
-                       int gE, int bonus, const int* queue, const int* qcount, int* overflow, int* ocount,
-                       int* rcount) {
+                       int gE, int bonus, const int* queue, const int* qcount, int* overflow, int* ocount) {
     hipLaunchKernelGGL(k_ext_band64, grid, dim3(64), 0, st, jobs, scan, q, ref, cig, raw, out, match, mismatch, gO, gE,
-                       bonus, queue, qcount, overflow, ocount, rcount);
+                       bonus, queue, qcount, overflow, ocount);
 }

@@ -49,8 +49,6 @@
 #define GS_G 16                  // lanes per job: a DPP row (32, half a wave, measured slower at chunk size)
 #define GS_JOBS (GS_WAVES * (64 / GS_G))   // jobs per workgroup
 #define GS_MAXR 1024             // reference window bytes staged in LDS per job
-#define W2_WAVES 2
-#define W2_JOBS (W2_WAVES * (64 / GS_G) * 2)   // jobs per workgroup of the pair scan
 #define GS_RPAD 32               // code-4 bytes staged on both sides of a window: the scans read
                                  // a column's code ahead of time without a range check
 
@@ -413,141 +411,6 @@ __device__ __forceinline__ void stage_rev_prof(uint16_t* __restrict__ lane_prof,
     __builtin_amdgcn_wave_barrier();
 }
 
-// ---------------------------------------------------------------------------
-// Word-layout pair scan.  SSW runs the byte layout first and keeps its answer
-// unless it saturates (score + bias >= 255, ssw.c:838-850); on the headline
-// workload ~98 % of jobs saturate, so the byte half of k_ext_scan_g's packed
-// registers is almost always thrown away.  fwd_w2 instead runs the word layout
-// of TWO jobs, A in the low half and B in the high half of every packed f16
-// register (their profiles merged per row with one v_perm_b32), so a 16-lane
-// group does two jobs' useful cells per instruction.
-//
-// Why the byte answer can be skipped: the byte and word layouts differ only in
-// which vertical-gap runs cross a stripe start (such a run feeds H but never E,
-// ssw.c's lazy-F loop), i.e. in paths with an insertion followed directly by a
-// deletion.  A path without adjacent I/D scores the same in every layout, so
-// if the final alignment of the word answer is such a path and scores
-// S >= 255 - bias, the byte layout reaches S too and saturates: SSW would have
-// used the word answer.  The kernel keeps jobs whose word maximum is below
-// 255 - bias for the exact two-layout pass (fwd_g) in the same launch; the band
-// kernels check the path of every other job (ext_finish) and flag the ones the
-// argument does not cover for an exact rescan (rsa_ctx.hip) -- results are
-// SSW's either way.
-//
-// Columns past a job's window (the pair's other job is longer) read code 4 and
-// only ever produce values strictly below the job's maximum (mismatch > 0,
-// gap_open > 0: the host checks), so they never move the best column or row.
-// ---------------------------------------------------------------------------
-struct FwdW2 {
-    int best[2], col[2], row[2];     // [0] job A (low half), [1] job B (high half); best as f16 bits
-};
-
-template <int R>
-__device__ __forceinline__ FwdW2 fwd_w2(const uint16_t* __restrict__ profA, const uint16_t* __restrict__ profB,
-                                        int nrowA, int nrowB, const uint8_t* __restrict__ rcA,
-                                        const uint8_t* __restrict__ rcB, int ncolA, int ncolB, int S, bool on,
-                                        int gO, int gE, int gl) {
-    constexpr int RP = ProfDim<R>::RP;
-    const int segA = max(1, (nrowA + 7) / 8), segB = max(1, (nrowB + 7) / 8);
-    const int ncol = max(ncolA, ncolB);
-    hh2 E[R], HA[R], HB[R];
-    uint32_t ssm[R], B0[R], B1[R];
-    const hh2 zero = h2_from(0u);
-    const hh2 GO2 = h2_from(h2_pair(gO)), GE2 = h2_from(h2_pair(gE));
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        E[r] = zero;
-        HA[r] = zero;
-        HB[r] = zero;
-        B0[r] = 0;
-        B1[r] = 0;
-        const int p = gl * R + r;
-        ssm[r] = ((p % segA) == 0 ? 0u : 0x0000FFFFu) | ((p % segB) == 0 ? 0u : 0xFFFF0000u);
-    }
-    uint32_t F_out = 0, Fw_out = 0, H_last = 0, diag_top = 0;
-    FwdW2 o;
-    o.best[0] = o.best[1] = 0;
-    o.col[0] = o.col[1] = INT_MAX;
-    o.row[0] = o.row[1] = INT_MAX;
-    // code(x) of a job: its window code, code 4 (the pad at rc[ncol]) past the window
-    auto codeA = [&](int x) -> int { return (int)rcA[min(x, ncolA)]; };
-    auto codeB = [&](int x) -> int { return (int)rcB[min(x, ncolB)]; };
-    uint32_t PA[RP / 2], PAn[RP / 2], PB[RP / 2], PBn[RP / 2];
-    prof_load<R>(profA, codeA(-gl), PA);
-    prof_load<R>(profB, codeB(-gl), PB);
-    int cA1 = codeA(1 - gl), cB1 = codeB(1 - gl);
-    auto step = [&](int s, const uint32_t (&PA)[RP / 2], uint32_t (&PAn)[RP / 2], const uint32_t (&PB)[RP / 2],
-                    uint32_t (&PBn)[RP / 2], const hh2 (&Hin)[R], hh2 (&Hout)[R]) {
-        const uint32_t F_in = row_shr1(F_out);
-        const uint32_t Fw_in = row_shr1(Fw_out);
-        const uint32_t Hl_in = row_shr1(H_last);
-        const int c = s - gl;
-        prof_load<R>(profA, cA1, PAn);
-        prof_load<R>(profB, cB1, PBn);
-        const int cA2 = codeA(c + 2), cB2 = codeB(c + 2);
-        if (on && c >= 0 && c < ncol) {
-            hh2 dg = h2_from(diag_top), F = h2_from(F_in), Fw = h2_from(Fw_in), cm = zero;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                Fw = h2_from(h2_bits(Fw) & ssm[r]);
-                // row r's scores of both jobs: A's 16 bits low, B's high
-                const uint32_t a = PA[r >> 1], b = PB[r >> 1];
-                const hh2 sc = h2_from((r & 1) ? __builtin_amdgcn_perm(b, a, 0x07060302u)
-                                               : __builtin_amdgcn_perm(b, a, 0x05040100u));
-                const hh2 diag = dg + sc;
-                const hh2 hm = hmax3(diag, E[r], Fw);
-                const hh2 h = hmax(hm, F);
-                dg = Hin[r];
-                Hout[r] = h;
-                const hh2 t = hm - GO2;
-                E[r] = hmax3(E[r] - GE2, t, zero);
-                Fw = hmax3(Fw - GE2, t, zero);
-                F = hmax3(F - GE2, t, zero);
-                cm = hmax(cm, h);
-            }
-            F_out = h2_bits(F);
-            Fw_out = h2_bits(Fw);
-            H_last = h2_bits(Hout[R - 1]);
-            const uint32_t cmb = h2_bits(cm);
-            const int v0 = (int)(cmb & 0xFFFFu), v1 = (int)(cmb >> 16);
-            if (v0 > o.best[0]) {
-                o.best[0] = v0;
-                o.col[0] = c;
-#pragma unroll
-                for (int r = 0; r < R; ++r) B0[r] = h2_bits(Hout[r]);
-            }
-            if (v1 > o.best[1]) {
-                o.best[1] = v1;
-                o.col[1] = c;
-#pragma unroll
-                for (int r = 0; r < R; ++r) B1[r] = h2_bits(Hout[r]);
-            }
-        }
-        diag_top = Hl_in;
-        cA1 = cA2;
-        cB1 = cB2;
-    };
-    int s = 0;
-    for (; s + 1 < S; s += 2) {
-        step(s, PA, PAn, PB, PBn, HA, HB);
-        step(s + 1, PAn, PA, PBn, PB, HB, HA);
-    }
-    if (s < S) step(s, PA, PAn, PB, PBn, HA, HB);
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-        if (o.col[hf] == INT_MAX) continue;
-        const int nrow = hf ? nrowB : nrowA;
-        int row = INT_MAX;
-#pragma unroll
-        for (int r = R - 1; r >= 0; --r) {
-            const uint32_t b = hf ? B1[r] : B0[r];
-            if (gl * R + r < nrow && (int)((b >> (16 * hf)) & 0xFFFFu) == o.best[hf]) row = gl * R + r;
-        }
-        o.row[hf] = row;
-    }
-    return o;
-}
-
 // SSW's choice between the layouts (ssw.c:838-850) from the two-layout forward
 // pass: byte unless it saturates; score, ref end (first best column) and read
 // end (smallest row of that column reaching the score).  Group-collective.
@@ -570,12 +433,12 @@ __device__ __forceinline__ void pick_g(const FwdG& fo, int mismatch, int& word, 
 }
 
 // reverse pass (ssw.c:877-893) on read[0..read_end1] x ref[0..ref_end1],
-// reversed, and the job's ScanRes (lane 0 of the group writes it; word_out is
-// what the result's word field carries).  Wave-collective: every lane calls it.
+// reversed, and the job's ScanRes (lane 0 of the group writes it).
+// Wave-collective: every lane calls it.
 template <int R>
 __device__ __forceinline__ void rev_write(uint16_t* __restrict__ lane_prof, const ExtJobDev& jb, int j, bool on,
                                           int gl, const char* __restrict__ qbuf, const uint8_t* __restrict__ rc,
-                                          int word, int word_out, int score1, int ref_end1, int read_end1,
+                                          int word, int score1, int ref_end1, int read_end1,
                                           int match, int mismatch, int gO, int gE, ScanRes* __restrict__ out) {
     const bool ron = on && score1 > 0;
     const int nrow = ron ? read_end1 + 1 : 0, ncol = ron ? ref_end1 + 1 : 0;
@@ -591,7 +454,7 @@ __device__ __forceinline__ void rev_write(uint16_t* __restrict__ lane_prof, cons
     const int trow = grp_min(tc == tcol ? tr : INT_MAX);
     if (!on || gl != 0) return;
     ScanRes res;
-    res.score1 = score1; res.ref_end1 = ref_end1; res.read_end1 = read_end1; res.word = word_out;
+    res.score1 = score1; res.ref_end1 = ref_end1; res.read_end1 = read_end1; res.word = word;
     res.flag = 0; res.status = 0;
     if (score1 > 0) {
         if (tcol == INT_MAX) {
@@ -641,77 +504,7 @@ k_ext_scan_g(const ExtJobDev* __restrict__ jobs, const int* __restrict__ order, 
     const FwdG fo = fwd_g<R>(lane_prof, qlen, rc, rlen, S, on && gl < lanes_used, gO, gE, gl);
     int word, score1, ref_end1, read_end1;
     pick_g(fo, mismatch, word, score1, ref_end1, read_end1);
-    rev_write<R>(lane_prof, jb, j, on, gl, qbuf, rc, word, word, score1, ref_end1, read_end1, match, mismatch, gO, gE,
-                 out);
-}
-
-// Word-layout pair scan (see fwd_w2): 16 lanes per pair of jobs, jobs[order[k]]
-// and jobs[order[k + 1]] of the window-length order side by side; the same job
-// limits as k_ext_scan_g.  Jobs whose word maximum stays below 255 - bias get
-// the exact two-layout pass (fwd_g) in their own lanes afterwards; every other
-// result carries word = 3 (word layout, chosen without the byte pass).
-template <int R>
-__global__ void __launch_bounds__(64 * W2_WAVES)
-k_ext_scan_w2(const ExtJobDev* __restrict__ jobs, const int* __restrict__ order, int n,
-              const char* __restrict__ qbuf, const char* __restrict__ ref, ScanRes* __restrict__ out,
-              int match, int mismatch, int gO, int gE) {
-    __shared__ uint8_t s_r[W2_JOBS][GS_RPAD + GS_MAXR + GS_RPAD];
-    __shared__ __attribute__((aligned(16))) uint16_t s_prof[W2_JOBS][ProfDim<R>::JOB];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int grp = wave * (64 / GS_G) + lane / GS_G, gl = lane & (GS_G - 1);
-    bool on[2];
-    int j[2], qlen[2], rlen[2], lu[2];
-    ExtJobDev jb[2];
-    uint8_t* rc[2];
-    uint16_t* prof[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int k = blockIdx.x * W2_JOBS + 2 * grp + h;
-        on[h] = k < n;
-        j[h] = on[h] ? order[k] : 0;
-        jb[h].q_off = 0; jb[h].r_off = 0; jb[h].qlen = 0; jb[h].rlen = 0; jb[h].cig_off = 0;
-        if (on[h]) jb[h] = jobs[j[h]];
-        qlen[h] = (int)jb[h].qlen;
-        rlen[h] = (int)jb[h].rlen;
-        lu[h] = (qlen[h] + R - 1) / R;
-        rc[h] = s_r[2 * grp + h] + GS_RPAD;
-        prof[h] = s_prof[2 * grp + h] + gl * ProfDim<R>::RP;
-        stage_job<R>(rc[h], prof[h], jb[h], gl, qbuf, ref, match, mismatch);
-    }
-    __syncthreads();
-
-    // word layout of both jobs at once
-    const int S = wave_max_i32(max(on[0] ? rlen[0] + lu[0] - 1 : 0, on[1] ? rlen[1] + lu[1] - 1 : 0));
-    const bool lon = (on[0] && gl < lu[0]) || (on[1] && gl < lu[1]);
-    const FwdW2 fo = fwd_w2<R>(prof[0], prof[1], qlen[0], qlen[1], rc[0], rc[1], on[0] ? rlen[0] : 0,
-                               on[1] ? rlen[1] : 0, S, lon, gO, gE, gl);
-    int word[2], score1[2], ref_end1[2], read_end1[2];
-    bool redo[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int bw = grp_max(fo.best[h]);
-        score1[h] = h_bits_to_int((uint32_t)bw);
-        redo[h] = on[h] && score1[h] + mismatch < 255;
-        word[h] = 1;
-        ref_end1[h] = grp_min(fo.best[h] == bw ? fo.col[h] : INT_MAX);
-        read_end1[h] = grp_min((fo.best[h] == bw && fo.col[h] == ref_end1[h]) ? fo.row[h] : INT_MAX);
-    }
-    // below saturation the byte layout may hold the answer: the exact pass, both layouts
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        if (!wave_max_i32(redo[h] ? 1 : 0)) continue;
-        const int S1 = wave_max_i32(redo[h] ? rlen[h] + lu[h] - 1 : 0);
-        const FwdG g = fwd_g<R>(prof[h], qlen[h], rc[h], rlen[h], S1, redo[h] && gl < lu[h], gO, gE, gl);
-        int w, sc, re, qe;
-        pick_g(g, mismatch, w, sc, re, qe);
-        if (redo[h]) {
-            word[h] = w; score1[h] = sc; ref_end1[h] = re; read_end1[h] = qe;
-        }
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-        rev_write<R>(prof[h], jb[h], j[h], on[h], gl, qbuf, rc[h], word[h], redo[h] ? word[h] : 3, score1[h],
-                     ref_end1[h], read_end1[h], match, mismatch, gO, gE, out);
+    rev_write<R>(lane_prof, jb, j, on, gl, qbuf, rc, word, score1, ref_end1, read_end1, match, mismatch, gO, gE, out);
 }
 
 // rows per lane of the grouped scan for a query length (0: not handled here)
@@ -756,28 +549,7 @@ void launch_ext_scan_g(int rows, int n, hipStream_t st, const ExtJobDev* jobs, c
 #undef RSA_G
 }
 
-void launch_ext_scan_w2(int rows, int n, hipStream_t st, const ExtJobDev* jobs, const int* order, const char* q,
-                        const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE) {
-    if (n <= 0) return;
-    const dim3 grid((n + W2_JOBS - 1) / W2_JOBS), block(64 * W2_WAVES);
-#define RSA_W(RR)                                                                                                \
-    if (rows == RR) {                                                                                            \
-        hipLaunchKernelGGL((k_ext_scan_w2<RR>), grid, block, 0, st, jobs, order, n, q, ref, out, match, mismatch, \
-                           gO, gE);                                                                              \
-        return;                                                                                                  \
-    }
-    if constexpr (GS_G == 16) { RSA_W(4) RSA_W(7) RSA_W(10) RSA_W(13) RSA_W(16) }
-    else { RSA_W(2) RSA_W(4) RSA_W(5) RSA_W(7) RSA_W(8) }
-#undef RSA_W
-}
-
 bool scan_g_params_ok(int match, int mismatch, int gO, int gE);
-
-// the pair scan's extra conditions: columns past a job's window must stay below
-// its maximum (mismatch > 0, gap_open > 0), see fwd_w2
-bool scan_w2_params_ok(int match, int mismatch, int gO, int gE) {
-    return scan_g_params_ok(match, mismatch, gO, gE) && mismatch > 0 && gO > 0;
-}
 
 // parameters the grouped scan computes exactly: half-precision integers stay
 // below 2048 in magnitude (scores up to match * 256, penalties), and F's

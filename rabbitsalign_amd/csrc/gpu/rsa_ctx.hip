@@ -29,21 +29,16 @@ int scan_g_max_ref();
 void launch_ext_scan_g(int rows, int n, hipStream_t st, const ExtJobDev* jobs, const int* order, const char* q,
                        const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE);
 bool scan_g_params_ok(int match, int mismatch, int gO, int gE);
-void launch_ext_scan_w2(int rows, int n, hipStream_t st, const ExtJobDev* jobs, const int* order, const char* q,
-                        const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE);
-bool scan_w2_params_ok(int match, int mismatch, int gO, int gE);
 __global__ void k_ext_band_panel(const ExtJobDev* jobs, const ScanRes* scan, int n_jobs, const int* idx_list,
                                  const char* qbuf, const char* ref, uint32_t* cig_pool, rsa_aln* out,
                                  uint8_t* scratch, int64_t scr_stride, int64_t dir_cap, int match, int mismatch,
                                  int gO, int gE, int bonus, int* overflow, int over_code);
 void launch_ext_band16(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n, const char* q,
                        const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match, int mismatch, int gO,
-                       int gE, int bonus, int* queue, int* qcount, int* overflow, int* rcount);
+                       int gE, int bonus, int* queue, int* qcount, int* overflow);
 void launch_ext_band64(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, const char* q,
                        const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match, int mismatch, int gO,
-                       int gE, int bonus, const int* queue, const int* qcount, int* overflow, int* ocount,
-                       int* rcount);
-void launch_w2_force(hipStream_t st, const ScanRes* scan, int n, int* overflow, int* rcount);
+                       int gE, int bonus, const int* queue, const int* qcount, int* overflow, int* ocount);
 void launch_cigar_compact(hipStream_t st, const rsa_aln* alns, rsa_aln* alns_out, int n_jobs, const uint32_t* slots,
                           uint32_t* dense, uint64_t* bsum, uint64_t* total);
 
@@ -350,8 +345,6 @@ struct ExtStatus {            // device-side counters of one rsa_extend call
     int qcount;               // jobs deferred by k_ext_band16
     int ocount;               // jobs k_ext_band64 could not hold
     uint64_t total;           // dense CIGAR ops (k_cigar_compact)
-    int rcount;               // pair-scan results the band kernels sent back for an exact rescan
-    int pad_;
 };
 
 // byte offsets of the scan order and the status in the staged job upload of n jobs
@@ -369,7 +362,7 @@ struct rsa_pending {
     rsa_aln_batch* out = nullptr;
     uint32_t n = 0;
     int32_t match = 0, mismatch = 0, gap_open = 0, gap_extend = 0, end_bonus = 0;
-    uint64_t guess = 0, cells = 0, qr_bytes = 0, pair_jobs = 0;
+    uint64_t guess = 0, cells = 0, qr_bytes = 0;
     ExtStatus* d_status = nullptr;     // in the lane's staged upload
 };
 
@@ -455,14 +448,6 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
     // length (longest first) so the four jobs of a wave run about as long; the
     // rest -- and sentinels -- to the one-job-per-wave kernel via an index list.
     const bool grouped = scan_g_params_ok(jb->match, jb->mismatch, jb->gap_open, jb->gap_extend);
-    // RSA_SCAN_W2=1: the word-layout pair scan (k_ext_scan_w2) for the grouped classes
-    // instead of the two-layout k_ext_scan_g.  Both give SSW's results (tests run both);
-    // the pair scan does half the VALU work per job but each wave runs two reverse
-    // passes and, for any of its 8 jobs below saturation, the two-layout pass as well,
-    // so at chunk size (latency-bound) it is slower: off by default
-    const char* w2_env = getenv("RSA_SCAN_W2");
-    const bool pairs = grouped && scan_w2_params_ok(jb->match, jb->mismatch, jb->gap_open, jb->gap_extend) &&
-                       w2_env && w2_env[0] == '1';
     constexpr int NCLS = 5;
     int cls_rows[NCLS];
     scan_g_classes(cls_rows);
@@ -510,11 +495,9 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
         uint32_t off = 0;
         for (int c = 0; c < NCLS; ++c) {
             if (!cls_n[c]) continue;
-            (pairs ? launch_ext_scan_w2 : launch_ext_scan_g)(cls_rows[c], (int)cls_n[c], st, L->d_jobs.as<ExtJobDev>(),
-                                                             d_ord + off, L->d_q.as<char>(), ctx->d_ref,
-                                                             L->d_scan.as<ScanRes>(), jb->match, jb->mismatch,
-                                                             jb->gap_open, jb->gap_extend);
-            if (pairs) P.pair_jobs += cls_n[c];
+            launch_ext_scan_g(cls_rows[c], (int)cls_n[c], st, L->d_jobs.as<ExtJobDev>(), d_ord + off,
+                              L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(), jb->match, jb->mismatch,
+                              jb->gap_open, jb->gap_extend);
             HIPCHK(hipGetLastError());
             off += cls_n[c];
         }
@@ -534,7 +517,7 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
     launch_ext_band16(dim3((n + 3) / 4), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(), (int)n,
                       L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(),
                       L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open, jb->gap_extend, jb->end_bonus,
-                      L->d_queue.as<int>(), &dst->qcount, L->d_over.as<int>(), &dst->rcount);
+                      L->d_queue.as<int>(), &dst->qcount, L->d_over.as<int>());
     HIPCHK(hipGetLastError());
     L->kt.end(st);
     L->kt.begin(st, RSA_K_EXT_BAND_WIDE);
@@ -542,14 +525,9 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
                       L->d_scan.as<ScanRes>(), L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(),
                       L->d_raw.as<uint32_t>(), L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open,
                       jb->gap_extend, jb->end_bonus, L->d_queue.as<int>(), &dst->qcount, L->d_over.as<int>(),
-                      &dst->ocount, &dst->rcount);
+                      &dst->ocount);
     HIPCHK(hipGetLastError());
     L->kt.end(st);
-    const char* force = getenv("RSA_W2_FORCE_RESCAN");
-    if (pairs && force && force[0] == '1') {
-        launch_w2_force(st, L->d_scan.as<ScanRes>(), (int)n, L->d_over.as<int>(), &dst->rcount);
-        HIPCHK(hipGetLastError());
-    }
     P.guess = std::min<uint64_t>(bound, DENSE_GUESS * n);
     return ext_compact_copy(P);
 }
@@ -565,36 +543,20 @@ static int ext_finish(rsa_pending& P) {
     const uint64_t guess = P.guess;
     HIPCHK(stream_wait(st, L->sb.done));
     ExtStatus hs = *L->h_status.as<ExtStatus>();
-    const int rescans = hs.rcount;
-    if (hs.ocount > 0 || hs.rcount > 0) {
-        // rare: bands the 64-lane kernel cannot hold (flag 1) and pair-scan results whose
-        // alignment did not prove the byte layout saturated (flag 3) -> the exact
-        // one-job-per-wave scan again (the same result for a flag-1 job), then one wave
-        // per job sweeping each band row in 64-cell panels (direction matrix in global scratch)
+    if (hs.ocount > 0) {
+        // rare: bands the 64-lane kernel cannot hold (flag 1) -> one wave per job sweeping
+        // each band row in 64-cell panels (direction matrix in global scratch)
         HIPCHK(L->h_over.ensure(sizeof(int) * n));
         HIPCHK(hipMemcpyAsync(L->h_over.p, L->d_over.p, sizeof(int) * n, hipMemcpyDeviceToHost, st));
         HIPCHK(stream_wait(st, L->sb.done));
         std::vector<int> big;
-        int rmax = 1;
-        const ExtJobDev* hj = L->h_jobs.as<ExtJobDev>();      // the staged descriptors of this call
         for (uint32_t i = 0; i < n; ++i)
-            if (L->h_over.as<int>()[i]) {
-                big.push_back((int)i);
-                rmax = std::max(rmax, (int)((hj[i].qlen + 63) / 64));
-            }
+            if (L->h_over.as<int>()[i]) big.push_back((int)i);
         const int64_t bstride = band_stride(BIG_DIR_CAP);
         HIPCHK(L->d_scratch.ensure((size_t)bstride * BIG_CHUNK));
         HIPCHK(L->d_idx.ensure(sizeof(int) * big.size()));
         HIPCHK(hipMemcpyAsync(L->d_idx.p, big.data(), sizeof(int) * big.size(), hipMemcpyHostToDevice, st));
         HIPCHK(hipMemsetAsync(L->d_over.p, 0, sizeof(int) * n, st));
-        if (hs.rcount > 0) {
-            L->kt.begin(st, RSA_K_EXT_SCAN);
-            launch_ext_scan(rmax, dim3(((uint32_t)big.size() + 3) / 4), dim3(256), st, L->d_jobs.as<ExtJobDev>(),
-                            (int)big.size(), L->d_idx.as<int>(), L->d_q.as<char>(), ctx->d_ref,
-                            L->d_scan.as<ScanRes>(), P.match, P.mismatch, P.gap_open, P.gap_extend);
-            HIPCHK(hipGetLastError());
-            L->kt.end(st);
-        }
         for (size_t b = 0; b < big.size(); b += BIG_CHUNK) {
             const int cnt = (int)std::min<size_t>(BIG_CHUNK, big.size() - b);
             L->kt.begin(st, RSA_K_EXT_BAND_PANEL);
@@ -632,8 +594,6 @@ static int ext_finish(rsa_pending& P) {
         ctx->stats.dp_cells += P.cells;
         ctx->stats.band_deferred += (uint64_t)hs.qcount;
         ctx->stats.band_overflow += (uint64_t)hs.ocount;
-        ctx->stats.scan_pair_jobs += P.pair_jobs;
-        ctx->stats.scan_rescans += (uint64_t)rescans;
     }
     return RSA_OK;
 }

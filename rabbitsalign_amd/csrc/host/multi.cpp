@@ -27,7 +27,7 @@ void add_stats(rsa_kernel_stats& a, const rsa_kernel_stats& b) {
     }
     uint64_t* au = &a.seed_calls;
     const uint64_t* bu = &b.seed_calls;
-    const size_t nu = (size_t)(&a.scan_rescans - &a.seed_calls) + 1;       // seed_calls .. scan_rescans
+    const size_t nu = (size_t)(&a.band_overflow - &a.seed_calls) + 1;      // seed_calls .. band_overflow
     for (size_t i = 0; i < nu; ++i) au[i] += bu[i];
     for (int i = 0; i < 2; ++i) {
         a.call_ms[i] += b.call_ms[i];

@@ -97,7 +97,6 @@ class KernelStats(C.Structure):
                 ("nams", C.c_uint64), ("rescued_reads", C.c_uint64),
                 ("jobs", C.c_uint64), ("dp_cells", C.c_uint64),
                 ("band_deferred", C.c_uint64), ("band_overflow", C.c_uint64),
-                ("scan_pair_jobs", C.c_uint64), ("scan_rescans", C.c_uint64),
                 ("call_ms", C.c_double * 2), ("lane_wait_ms", C.c_double * 2), ("device_wait_ms", C.c_double * 2)]
 
 

@@ -1,8 +1,7 @@
 # A/B of host tuning switches on the default bench, alternating settings, REPS rounds.
 # Usage: [REPS=2] [STEPS=10] bash scripts/gpu_ab_env.sh TAG "RSA_PREFETCH=1" "RSA_PREFETCH=0" ...
 # (each argument is one setting: space-separated VAR=value pairs, "" for the defaults)
-# Earlier one-off scripts this replaces produced profiles/r01_ab_*.jsonl and
-# profiles/r02/ab_ext_group.jsonl, e.g. gpu_ab_env.sh abg "RSA_EXT_GROUP=1" "RSA_EXT_GROUP=2".
+# e.g. gpu_ab_env.sh abw "RSA_WAIT_WORKERS=12" "RSA_WAIT_WORKERS=4"
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp

@@ -206,24 +206,9 @@ def test_extend_async_equals_sync(ctx):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["pairs", "two_layout", "forced_rescan"])
-def test_extend_scan_modes(ctx, monkeypatch, mode):
-    """The two-layout grouped scan (k_ext_scan_g, default), the word-layout pair scan
-    (RSA_SCAN_W2=1, k_ext_scan_w2) and the pair scan with every result sent through the
-    exact rescan (+ RSA_W2_FORCE_RESCAN=1, the path the band kernels take when an
-    alignment does not prove the byte layout saturated) all give Aligner::align's results."""
+def test_extend_grouped_and_wave_scans(ctx):
+    """The grouped scan (k_ext_scan_g, queries <= 256 bp and windows <= 1 KB) and the
+    one-job-per-wave scan (k_ext_scan, the rest) on one mixed batch: Aligner::align's results."""
     c, ref, offs = ctx
-    if mode != "two_layout":
-        monkeypatch.setenv("RSA_SCAN_W2", "1")
-    if mode == "forced_rescan":
-        monkeypatch.setenv("RSA_W2_FORCE_RESCAN", "1")
-    c.reset_stats()
     bad = _compare(c, ref, offs, 11, 3000, qlens=(150, 100, 250, 64, 129, 300))
     assert not bad, f"{len(bad)} mismatches, first: {bad[0]}"
-    st = c.stats()
-    if mode == "two_layout":
-        assert st["scan_pair_jobs"] == 0, st
-    else:
-        assert st["scan_pair_jobs"] > 0, st
-    if mode == "forced_rescan":
-        assert st["scan_rescans"] > 0, st
