@@ -172,7 +172,8 @@ KERNEL_LIMITER = {
     "ext_band_wide": "latency of the few (~3 a call) 64-lane jobs, one wave each",
     "find_nams": "LDS latency and divergence of the robin_hood map emulation, one wave per read",
     "sites": "latency of random reference windows (one read per NAM)",
-    "lookup": "random HBM lines: two per query randstrobe (bucket bounds + entries)",
+    "lookup": "random HBM lines: one 128-B bucket line per query randstrobe (bounds + up to 7 entries; "
+              "larger buckets add their entries' line)",
     "randstrobes": "xxh64 and the syncmer window in LDS, one wave per read",
     "rescue": "latency, rescued reads only",
 }

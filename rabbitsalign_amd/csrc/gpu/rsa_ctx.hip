@@ -46,6 +46,8 @@ void index_build_peek(const rsa_index_build* b, int* device, int* bits);
 void index_build_release(rsa_index_build* b, int* device, char** ref, rsa_ref_randstrobe** rs, uint64_t** starts,
                          uint64_t* n, int* bits);
 
+hipError_t bucket_lines_build(const uint64_t* starts, const rsa_ref_randstrobe* rs, int bits, BucketLine* lines,
+                              hipStream_t st);
 int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, const rsa_read_batch* rb,
              int32_t rescue_level, uint32_t rescue_cutoff, rsa_nam_batch* out, std::string& err, SeedCounters& c);
 int seed_randstrobes_run(SeedBufs& b, hipStream_t st, const SeedIndexParams& p, const rsa_read_batch* rb,
@@ -121,6 +123,7 @@ struct rsa_ctx {
     uint64_t* d_coff = nullptr;        // contig offsets (device copy)
     uint64_t n_rs = 0;
     uint64_t* d_starts = nullptr;
+    BucketLine* d_lines = nullptr;     // k_lookup's copy of the bucket table (rsa_seed.h)
     SeedIndexParams ip{};
     uint64_t resident = 0;
     // lanes
@@ -197,6 +200,26 @@ struct LaneGuard {
     ~LaneGuard() { if (l) release_lane(ctx, l); }
 };
 
+// The BucketLine table (one 128-byte line a bucket, 32 GiB at bits = 28) unless
+// RSA_BUCKET_LINES=0 or it would take more than half of the free HBM; without it
+// k_lookup reads the .sti bucket table and entries (two random lines a lookup).
+static void open_bucket_lines(rsa_ctx* ctx) {
+    const char* v = getenv("RSA_BUCKET_LINES");
+    if ((v && v[0] == '0') || !ctx->d_starts || !ctx->d_rs) return;
+    const size_t bytes = sizeof(BucketLine) << ctx->ip.bits;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || bytes > free_b / 2) return;
+    if (hipMalloc(&ctx->d_lines, bytes) != hipSuccess) { ctx->d_lines = nullptr; (void)hipGetLastError(); return; }
+    if (bucket_lines_build(ctx->d_starts, ctx->d_rs, ctx->ip.bits, ctx->d_lines, nullptr) != hipSuccess) {
+        (void)hipFree(ctx->d_lines);
+        ctx->d_lines = nullptr;
+        (void)hipGetLastError();
+        return;
+    }
+    ctx->ip.lines = ctx->d_lines;
+    ctx->resident += bytes;
+}
+
 extern "C" {
 
 rsa_ctx* rsa_open(int device, const rsa_index_view* v, char* errbuf, size_t err_len) {
@@ -244,6 +267,7 @@ rsa_ctx* rsa_open(int device, const rsa_index_view* v, char* errbuf, size_t err_
     ctx->ip.ref = ctx->d_ref;
     ctx->ip.coff = ctx->d_coff;
     ctx->resident = ctx->ref_bytes + sizeof(rsa_ref_randstrobe) * ctx->n_rs + sizeof(uint64_t) * n_starts;
+    open_bucket_lines(ctx);
     return ctx;
 }
 
@@ -283,6 +307,7 @@ rsa_ctx* rsa_open_built(rsa_index_build* b, const rsa_index_view* v, char* errbu
     ctx->ip.ref = ctx->d_ref;
     ctx->ip.coff = ctx->d_coff;
     ctx->resident = ctx->ref_bytes + sizeof(rsa_ref_randstrobe) * ctx->n_rs + sizeof(uint64_t) * (((size_t)1 << v->bits) + 1);
+    open_bucket_lines(ctx);
     return ctx;
 }
 
@@ -314,6 +339,7 @@ void rsa_close(rsa_ctx* ctx) {
     if (ctx->d_ref) (void)hipFree(ctx->d_ref);
     if (ctx->d_rs) (void)hipFree(ctx->d_rs);
     if (ctx->d_starts) (void)hipFree(ctx->d_starts);
+    if (ctx->d_lines) (void)hipFree(ctx->d_lines);
     if (ctx->d_coff) (void)hipFree(ctx->d_coff);
     delete ctx;
 }

@@ -9,9 +9,23 @@
 #include <stdlib.h>
 #include "../../../include/rsa_gpu.h"
 
+// Bucket lines: a device-side copy of the bucket table with each bucket's first
+// entries beside its bounds, one 128-byte line per bucket -- 16 bytes {start,
+// end} then up to BL_CAP RefRandstrobes (zero past the bucket's end; none when
+// the bucket holds more).  A lookup in a bucket of at most BL_CAP entries reads
+// one random line instead of two (bounds, then entries).  Built at rsa_open from
+// the .sti arrays, which stay the index of record.
+#define BL_CAP 7
+struct __attribute__((aligned(128))) BucketLine {
+    uint64_t start, end;
+    rsa_ref_randstrobe e[BL_CAP];
+};
+static_assert(sizeof(BucketLine) == 128, "one bucket, one 128-byte line");
+
 struct SeedIndexParams {
     const rsa_ref_randstrobe* rs;
     const uint64_t* starts;
+    const BucketLine* lines;    // null: k_lookup reads starts + rs
     uint64_t n;
     int bits;
     uint32_t filter_cutoff;

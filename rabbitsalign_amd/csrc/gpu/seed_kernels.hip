@@ -481,42 +481,79 @@ k_lookup(const rsa_query_randstrobe* __restrict__ qrs, const uint32_t* __restric
         QrsInfo o;
         o.pos = END64; o.count = 0; o.hits = 0; o.flags = 0; o.pad = 0;
         rsa_query_randstrobe q;
+        // the bucket's entries are eb[0, b - a) (in its line or in p.rs); lo/ub index eb
         uint64_t lo = 0, ub = 0;
+        const rsa_ref_randstrobe* eb = p.rs;
         if (i < nq) {
             q = qrs[base + i];
             const uint64_t top = q.hash >> (64 - p.bits);
-            const uint64_t a = p.starts[top], b = p.starts[top + 1];
-            if (a != b) {
-                lo = lower_bound_hash(p.rs, a, b, q.hash);
-                if (lo < b && p.rs[lo].hash == q.hash) {
-                    o.pos = lo;
-                    o.flags = 1;
-                    ub = upper_bound_hash(p.rs, lo, b, q.hash);
-                    // is_filtered (index.hpp:91-93) probes rs[lo + filter_cutoff].hash == hash;
-                    // equal hashes are contiguous from lo to ub (one bucket), so that is
-                    // ub - lo > filter_cutoff, and the probe's random line is not fetched
-                    if (ub - lo > (uint64_t)p.filter_cutoff) o.flags |= 2;
-                    o.count = (uint32_t)min<uint64_t>(ub - lo, 0xFFFFFFFFull);
-                    if (o.count <= 1000) {
-                        // add_to_hits_per_ref min_diff filter (nam.cpp:68-85)
-                        int min_diff = INT_MAX;
-                        uint32_t h = 0;
-                        const int qspan = (int)q.end - (int)q.start;
-                        for (uint64_t e = lo; e < ub; ++e) {
-                            const rsa_ref_randstrobe x = p.rs[e];
-                            const int rspan = (int)(x.packed & 0xFF) + p.k;
-                            int d = qspan - rspan;
-                            d = d < 0 ? -d : d;
-                            if (d <= min_diff) { h++; min_diff = d; }
+            uint64_t a, b;
+            bool hit = false;
+            if (p.lines) {
+                // the whole line in one go (eight independent 16-byte loads, one
+                // miss): bounds and up to BL_CAP entries, searched in registers
+                const BucketLine* L = p.lines + top;
+                const uint4* lv = (const uint4*)L;
+                uint4 w[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) w[t] = lv[t];
+                a = (uint64_t)w[0].x | (uint64_t)w[0].y << 32;
+                b = (uint64_t)w[0].z | (uint64_t)w[0].w << 32;
+                if (b - a <= BL_CAP) {
+                    eb = L->e;
+                    const uint64_t c = b - a;
+                    lo = c; ub = c;            // first entry >= / > the key (entries sorted)
+#pragma unroll
+                    for (int t = BL_CAP - 1; t >= 0; --t) {
+                        const uint64_t h = (uint64_t)w[1 + t].x | (uint64_t)w[1 + t].y << 32;
+                        if ((uint64_t)t < c) {
+                            if (h >= q.hash) lo = t;
+                            if (h > q.hash) ub = t;
                         }
-                        o.hits = h;
                     }
-                    found++;
-                    const uint32_t scanned = o.count <= 1000 ? o.count : 0;
-                    if (!(o.flags & 2)) { good++; hfind += o.hits; sfind += scanned; }
-                    if (o.count <= 1000) hall += o.hits;
-                    sall += scanned;
+                    hit = ub > lo;
+                } else {
+                    eb = p.rs + a;
+                    lo = lower_bound_hash(eb, 0, b - a, q.hash);
+                    hit = lo < b - a && eb[lo].hash == q.hash;
+                    if (hit) ub = upper_bound_hash(eb, lo, b - a, q.hash);
                 }
+            } else {
+                a = p.starts[top]; b = p.starts[top + 1];
+                eb = p.rs + a;
+                if (a != b) {
+                    lo = lower_bound_hash(eb, 0, b - a, q.hash);
+                    hit = lo < b - a && eb[lo].hash == q.hash;
+                    if (hit) ub = upper_bound_hash(eb, lo, b - a, q.hash);
+                }
+            }
+            if (hit) {
+                o.pos = a + lo;
+                o.flags = 1;
+                // is_filtered (index.hpp:91-93) probes rs[lo + filter_cutoff].hash == hash;
+                // equal hashes are contiguous from lo to ub (one bucket), so that is
+                // ub - lo > filter_cutoff, and the probe's random line is not fetched
+                if (ub - lo > (uint64_t)p.filter_cutoff) o.flags |= 2;
+                o.count = (uint32_t)min<uint64_t>(ub - lo, 0xFFFFFFFFull);
+                if (o.count <= 1000) {
+                    // add_to_hits_per_ref min_diff filter (nam.cpp:68-85)
+                    int min_diff = INT_MAX;
+                    uint32_t h = 0;
+                    const int qspan = (int)q.end - (int)q.start;
+                    for (uint64_t e = lo; e < ub; ++e) {
+                        const rsa_ref_randstrobe x = eb[e];
+                        const int rspan = (int)(x.packed & 0xFF) + p.k;
+                        int d = qspan - rspan;
+                        d = d < 0 ? -d : d;
+                        if (d <= min_diff) { h++; min_diff = d; }
+                    }
+                    o.hits = h;
+                }
+                found++;
+                const uint32_t scanned = o.count <= 1000 ? o.count : 0;
+                if (!(o.flags & 2)) { good++; hfind += o.hits; sfind += scanned; }
+                if (o.count <= 1000) hall += o.hits;
+                sall += scanned;
             }
             qi[base + i] = o;
         }
@@ -528,7 +565,7 @@ k_lookup(const rsa_query_randstrobe* __restrict__ qrs, const uint32_t* __restric
             const int qs = (int)q.start, qe = (int)q.end;
             int min_diff = INT_MAX, h = at;
             for (uint64_t e = lo; e < ub; ++e) {
-                const rsa_ref_randstrobe x = p.rs[e];
+                const rsa_ref_randstrobe x = eb[e];
                 const int rs0 = (int)x.position;
                 const int re0 = rs0 + (int)(x.packed & 0xFF) + p.k;
                 int d = (qe - qs) - (re0 - rs0);
@@ -1517,7 +1554,10 @@ k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read,
         unsigned long long* __restrict__ pool_used) {
     __shared__ uint32_t s_need[16], s_base[16];
     __shared__ unsigned long long s_at;
-    const uint64_t total = min((uint64_t)hdr->total, cap);
+    // a batch whose NAMs overflow the output was not compacted whole (k_compact skips
+    // the reads past `cap`, so their nam_read entries were never written): no site
+    // checks then -- the host reports RSA_ERR_CAPACITY and the caller asks again
+    const uint64_t total = (uint64_t)hdr->total <= cap ? (uint64_t)hdr->total : 0;
     const int l16 = threadIdx.x & 15, grp = threadIdx.x >> 4;
     // a fixed grid walks the batch's NAMs, 16 a block per round (the count is known on the device only)
     for (uint64_t blk = blockIdx.x; blk * 16 < total; blk += gridDim.x) {
@@ -1603,6 +1643,37 @@ k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read,
     }
     __syncthreads();                             // s_need / s_base / s_at are reused next round
     }
+}
+
+// ---------------------------------------------------------------------------
+// k_bucket_lines: the BucketLine copy of the bucket table (rsa_seed.h), eight
+// lanes a line, each writing 16 contiguous bytes (bounds, then entry slot - 1)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+k_bucket_lines(const uint64_t* __restrict__ starts, const rsa_ref_randstrobe* __restrict__ rs, uint64_t n_buckets,
+               uint4* __restrict__ lines) {
+    const uint64_t total = n_buckets * 8;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t bk = t >> 3;
+        const uint32_t s = (uint32_t)(t & 7);
+        const uint64_t a = starts[bk], e = starts[bk + 1];
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (s == 0) v = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)e, (uint32_t)(e >> 32));
+        else if (e - a <= BL_CAP && s - 1 < e - a) v = ((const uint4*)rs)[a + s - 1];
+        lines[t] = v;
+    }
+}
+
+hipError_t bucket_lines_build(const uint64_t* starts, const rsa_ref_randstrobe* rs, int bits, BucketLine* lines,
+                              hipStream_t st) {
+    const uint64_t nb = (uint64_t)1 << bits;
+    const uint64_t threads = nb * 8;
+    const unsigned grid = (unsigned)std::min<uint64_t>((threads + 255) / 256, 8192);
+    k_bucket_lines<<<grid, 256, 0, st>>>(starts, rs, nb, (uint4*)lines);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    return e;
 }
 
 // ---------------------------------------------------------------------------
@@ -1961,8 +2032,11 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
     c.reads = n; c.read_bases = bases; c.qrs = hh.qrs; c.found = hh.found; c.filtered = hh.found - hh.good;
     c.hits = hh.hits_find; c.nams = total; c.rescued = hh.resc_reads;
     c.alg_bytes[RSA_K_RANDSTROBES] = (double)bases + QRS * hh.qrs + 24.0 * n;
-    c.alg_bytes[RSA_K_LOOKUP] = (QRS + 16 + QI) * hh.qrs + 8.0 * hh.found + RS * hh.scan_all + sizeof(ReadStat) * (double)n;
-    c.alg_bytes[RSA_K_FIND_NAMS] = (QRS + QI) * hh.qrs + RS * hh.scan_find + 2 * HIT * hh.hits_find + NAM * hh.n1 + 16.0 * n;
+    // query randstrobe, bucket bounds, QrsInfo; the found entries; the hits into the slots
+    c.alg_bytes[RSA_K_LOOKUP] = (QRS + 16 + QI) * hh.qrs + 8.0 * hh.found + RS * hh.scan_all + HIT * hh.hits_find +
+                                sizeof(ReadStat) * (double)n;
+    // the hits from the read's slot (k_lookup wrote them), the NAMs, the per-read results
+    c.alg_bytes[RSA_K_FIND_NAMS] = HIT * hh.hits_find + NAM * hh.n1 + (16.0 + sizeof(ReadStat)) * n;
     c.alg_bytes[RSA_K_RESCUE] = (QRS + QI) * hh.resc_q + RS * hh.resc_scan + 2 * HIT * hh.resc_hits + NAM * hh.n2;
     c.alg_bytes[RSA_K_COMPACT] = 2 * NAM * total + 28.0 * n;
     // NAM + read bytes read, window bytes compared, site + positions written

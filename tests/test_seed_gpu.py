@@ -62,6 +62,34 @@ def test_seed(setup, rescue_level):
 
 
 @pytest.mark.gpu
+def test_seed_bucket_lines_equal_table(setup, monkeypatch):
+    """k_lookup through the bucket lines (bounds and up to 7 entries in one 128-byte
+    line; the default) and through the .sti bucket table + entries (RSA_BUCKET_LINES=0)
+    give the same NAMs.  The "rep" index holds buckets past the line's capacity, so
+    both of the line path's branches run there."""
+    from rabbitsalign_amd import native
+    name, idx, ctx, ora = setup
+    reads = _reads(name)
+    sizes = np.diff(idx.bucket_starts.astype(np.int64))
+    assert (sizes <= 7).any()
+    if name == "rep":
+        assert (sizes > 7).any()
+    bits = int(idx.bits)
+    monkeypatch.setenv("RSA_BUCKET_LINES", "0")
+    plain = native.GpuContext(idx)
+    try:
+        assert ctx.resident_bytes() - plain.resident_bytes() == 128 << bits
+        for level in (2, 1):
+            a, an, ar = ctx.seed(reads, rescue_level=level)
+            b, bn, br = plain.seed(reads, rescue_level=level)
+            assert all(_nam_equal(x, y) for x, y in zip(a, b))
+            assert np.array_equal(np.asarray(an, np.float32).view(np.uint32), np.asarray(bn, np.float32).view(np.uint32))
+            assert list(ar) == list(br)
+    finally:
+        plain.close()
+
+
+@pytest.mark.gpu
 def test_seed_batch_independent(setup):
     name, idx, ctx, ora = setup
     reads = _reads(name)
