@@ -92,15 +92,13 @@ struct SyncState {
     // push; true when the window was full (its oldest value dropped)
     __device__ __forceinline__ bool push(uint64_t h, int W) {
         if constexpr (WC > 0) {
-            if (qn < WC) {
-#pragma unroll
-                for (int x = 0; x < WC; ++x) if (x == qn) win[x] = h;
-                qn++;
-                return false;
-            }
+            // always shift in at the end (no store at a variable index, which
+            // would move the window out of registers); while filling, the
+            // window is read only once it is full, when the order is right
 #pragma unroll
             for (int x = 0; x + 1 < WC; ++x) win[x] = win[x + 1];
             win[WC - 1] = h;
+            if (qn < WC) { qn++; return false; }
             return true;
         } else {
             win[(qh + qn) & 31] = h;
@@ -126,14 +124,17 @@ struct SyncState {
         const bool popped = push(hs, W);
         if (!popped) {
             if (qn < W) return 0;
-            for (int j = 0; j < W; ++j) {               // first fill: leftmost minimum
+            // WC > 0: constant trip counts, so the window stays in registers
+#pragma unroll
+            for (int j = 0; j < (WC > 0 ? WC : W); ++j) {   // first fill: leftmost minimum
                 const uint64_t v = at(j);
                 if (v < min_val) { min_val = v; min_pos = i - p.k + j + 1; }
             }
         } else if (min_pos == i - p.k) {                 // the minimum left: rescan, rightmost wins
             min_val = END64;
             min_pos = i - p.s + 1;
-            for (int j = W - 1; j >= 0; --j) {
+#pragma unroll
+            for (int j = (WC > 0 ? WC : W) - 1; j >= 0; --j) {
                 const uint64_t v = at(j);
                 if (v < min_val) { min_val = v; min_pos = i - p.k + j + 1; }
             }
@@ -152,10 +153,17 @@ struct SyncState {
     __device__ __forceinline__ bool converged(int W) const {
         if (qn < W) return false;
         int eq = 0;
-        for (int j = 0; j < W; ++j) eq += at(j) == min_val;
+#pragma unroll
+        for (int j = 0; j < (WC > 0 ? WC : W); ++j) eq += at(j) == min_val;
         return eq == 1;
     }
 };
+
+// base o (0..15) of a 16-byte word held as two values
+__device__ __forceinline__ int pick_base(uint64_t wlo, uint64_t whi, unsigned o) {
+    const uint64_t x = o < 8 ? wlo : whi;
+    return nt4_code((unsigned char)(x >> ((o & 7) * 8)));
+}
 
 struct SegTable {
     const uint32_t* contig;     // [n_seg] contig of the segment
@@ -193,34 +201,34 @@ k_seg_syncmers(const char* __restrict__ ref, SegTable st, BuildParams p, int mod
     // bases come from aligned 16-B loads kept in registers: one load per 16 steps
     // instead of one byte load per step (a wave's lanes walk 64 segments 4 KB apart)
     const uint64_t c0 = (uint64_t)(cs - ref);
-    uint64_t wbase = ~0ull;
-    uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-    auto base_at = [&](uint64_t i) -> int {
-        const uint64_t g = c0 + i, a = g & ~15ull;
-        if (a != wbase) {
-            const uint4 v = *reinterpret_cast<const uint4*>(ref + a);
-            w0 = v.x; w1 = v.y; w2 = v.z; w3 = v.w;
-            wbase = a;
-        }
-        const unsigned o = (unsigned)(g & 15);
-        const uint32_t x = o < 8 ? (o < 4 ? w0 : w1) : (o < 12 ? w2 : w3);
-        return nt4_code((unsigned char)(x >> ((o & 3) * 8)));
-    };
+    uint64_t wbase = ~0ull, wlo = 0, whi = 0;
+    // (no lambda over the words: one captured by reference let the compiler
+    // pick between their addresses and keep them in scratch)
+#define SEG_BASE_AT(i_)                                                               \
+    ({                                                                                \
+        const uint64_t g_ = c0 + (i_), a_ = g_ & ~15ull;                              \
+        if (a_ != wbase) {                                                            \
+            const ulonglong2 v_ = *reinterpret_cast<const ulonglong2*>(ref + a_);     \
+            wlo = v_.x; whi = v_.y; wbase = a_;                                       \
+        }                                                                             \
+        pick_base(wlo, whi, (unsigned)(g_ & 15));                                     \
+    })
     uint64_t i = from;
     for (; i < b; ++i) {                                   // replay, no output
-        const int r = S.step(base_at(i), (long long)i, p, W, kmask, smask, kshift, sshift, sm);
+        const int r = S.step(SEG_BASE_AT(i), (long long)i, p, W, kmask, smask, kshift, sshift, sm);
         if (mode == 0 && !ok) ok = r < 0 || S.converged(W);
     }
     uint32_t n = 0;
     SyncmerOut* o = mode == 2 ? out + off[sg] : nullptr;
     for (; i < e; ++i) {
-        if (S.step(base_at(i), (long long)i, p, W, kmask, smask, kshift, sshift, sm) == 1) {
+        if (S.step(SEG_BASE_AT(i), (long long)i, p, W, kmask, smask, kshift, sshift, sm) == 1) {
             if (mode == 2) o[n] = sm;
             n++;
         }
     }
     if (mode != 2) count[sg] = n;
     if (mode == 0) conv[sg] = ok ? 1 : 0;
+#undef SEG_BASE_AT
 }
 
 // RandstrobeGenerator::next (randstrobes.cpp:173-202) + assign_randstrobes'
