@@ -145,8 +145,8 @@ def kernel_roofline(name: str, k: dict, ks: dict) -> dict:
     traffic, src = pmc_traffic(sym)
     out = {"kernel": sym, "launches": k["launches"], "avg_launch_us": round(avg_s * 1e6, 3),
            "alg_bytes_per_launch": round(per_launch_bytes, 1), "traffic": traffic, "traffic_source": src}
-    if name == "ext_scan" and ks.get("dp_cells"):
-        cells = ks["dp_cells"] / k["launches"]
+    if name == "ext_scan" and ks.get("dp_cells_timed"):
+        cells = ks["dp_cells_timed"] / k["launches"]
         achieved = cells / avg_s / 1e9
         out.update({"bound": "valu", "achieved": round(achieved, 2), "peak": round(DP_PEAK_GCELLS, 1),
                     "unit": "Gcells/s", "frac": round(achieved / DP_PEAK_GCELLS, 5),
@@ -190,7 +190,12 @@ def roofline(ks: dict, elapsed: float) -> dict:
     out["top_kernels"] = [kernel_roofline(n, kern[n], ks) for n in top[:3]]
     # whole path: the algorithmic bytes of every kernel of the timed steps / wall time
     reads = max(1, ks.get("reads", 0))
-    alg = sum(k["alg_bytes"] for k in kern.values())
+    # alg_bytes cover the timed calls (one in RSA_KTIMER_EVERY): scale each kernel's to all calls
+    from rabbitsalign_amd.native import EXT_KERNELS
+    def scale(n):
+        calls, timed = (("ext_calls", "ext_calls_timed") if n in EXT_KERNELS else ("seed_calls", "seed_calls_timed"))
+        return ks.get(calls, 0) / max(1, ks.get(timed, 0))
+    alg = sum(k["alg_bytes"] * scale(n) for n, k in kern.items())
     path = {"alg_bytes_per_read": round(alg / reads, 1), "achieved": round(alg / elapsed / 1e9, 3),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(alg / elapsed / 1e9 / HBM_PEAK_GBS, 6)}
     # SURVEY.md §8d's B_alg with this run's counters: 32 n_q + 24 n_hit + L n_site + n_sw (L + t + 16)

@@ -288,9 +288,13 @@ enum {
 };
 
 typedef struct rsa_kernel_stats {
+    /* kernel_ms / launches / alg_bytes / dp_cells_timed: over the timed calls only
+     * (one call in RSA_KTIMER_EVERY per lane, default 4) */
     double kernel_ms[RSA_K_COUNT];   /* sum of per-launch HIP-event durations (launch stream) */
     uint64_t launches[RSA_K_COUNT];
     double alg_bytes[RSA_K_COUNT];   /* algorithmic HBM bytes (DESIGN.md "Kernels") */
+    uint64_t dp_cells_timed;         /* dp_cells of the timed rsa_extend calls */
+    uint64_t seed_calls_timed, ext_calls_timed;
     uint64_t seed_calls, ext_calls;
     uint64_t reads, read_bases, query_randstrobes, lookups_found, filtered, hits, nams, rescued_reads;
     uint64_t jobs, dp_cells;         /* dp_cells: sum query_len * ref_len of the forward scan */

@@ -514,7 +514,7 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
     }
     // jobs, scan order and the zeroed status in one copy
     HIPCHK(hipMemcpyAsync(L->d_jobs.p, L->h_jobs.p, stage_bytes(n), hipMemcpyHostToDevice, st));
-    L->kt.reset();
+    L->kt.arm();
     L->kt.begin(st, RSA_K_EXT_SCAN);
     {
         const int* d_ord = reinterpret_cast<const int*>(L->d_jobs.as<char>() + stage_order_off(n));
@@ -610,11 +610,15 @@ static int ext_finish(rsa_pending& P) {
     out->cigar_used = hs.total;
     {
         std::lock_guard<std::mutex> g(ctx->stat_m);
-        L->kt.collect(ctx->stats.kernel_ms, ctx->stats.launches);
-        // scan: query + window in, ScanRes out; band: the segment bytes again, ScanRes in, rsa_aln + CIGAR out
-        ctx->stats.alg_bytes[RSA_K_EXT_SCAN] += (double)P.qr_bytes + (double)(sizeof(ExtJobDev) + sizeof(ScanRes)) * n;
-        ctx->stats.alg_bytes[RSA_K_EXT_BAND] += (double)P.qr_bytes + (double)(sizeof(ExtJobDev) + sizeof(ScanRes) +
-                                                                            sizeof(rsa_aln)) * n + 4.0 * hs.total;
+        if (L->kt.on) {
+            L->kt.collect(ctx->stats.kernel_ms, ctx->stats.launches);
+            // scan: query + window in, ScanRes out; band: the segment bytes again, ScanRes in, rsa_aln + CIGAR out
+            ctx->stats.alg_bytes[RSA_K_EXT_SCAN] += (double)P.qr_bytes + (double)(sizeof(ExtJobDev) + sizeof(ScanRes)) * n;
+            ctx->stats.alg_bytes[RSA_K_EXT_BAND] += (double)P.qr_bytes + (double)(sizeof(ExtJobDev) + sizeof(ScanRes) +
+                                                                                sizeof(rsa_aln)) * n + 4.0 * hs.total;
+            ctx->stats.dp_cells_timed += P.cells;
+            ctx->stats.ext_calls_timed++;
+        }
         ctx->stats.ext_calls++;
         ctx->stats.jobs += n;
         ctx->stats.dp_cells += P.cells;
@@ -758,12 +762,15 @@ int rsa_seed(rsa_ctx* ctx, const rsa_read_batch* rb, int32_t rescue_level, uint3
     LaneGuard guard{ctx, L};
     std::string err;
     SeedCounters c;
-    L->kt.reset();
+    L->kt.arm();
     rc = seed_run(L->sb, L->stream, L->kt, ctx->ip, rb, rescue_level, rescue_cutoff, out, err, c);
     if (rc) { set_err(ctx, err); return rc; }
     std::lock_guard<std::mutex> g(ctx->stat_m);
-    L->kt.collect(ctx->stats.kernel_ms, ctx->stats.launches);
-    for (int k = 0; k < RSA_K_COUNT; ++k) ctx->stats.alg_bytes[k] += c.alg_bytes[k];
+    if (L->kt.on) {
+        L->kt.collect(ctx->stats.kernel_ms, ctx->stats.launches);
+        for (int k = 0; k < RSA_K_COUNT; ++k) ctx->stats.alg_bytes[k] += c.alg_bytes[k];
+        ctx->stats.seed_calls_timed++;
+    }
     ctx->stats.seed_calls++;
     ctx->stats.reads += c.reads;
     ctx->stats.read_bases += c.read_bases;

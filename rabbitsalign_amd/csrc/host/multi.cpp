@@ -25,9 +25,9 @@ void add_stats(rsa_kernel_stats& a, const rsa_kernel_stats& b) {
         a.launches[k] += b.launches[k];
         a.alg_bytes[k] += b.alg_bytes[k];
     }
-    uint64_t* au = &a.seed_calls;
-    const uint64_t* bu = &b.seed_calls;
-    const size_t nu = (size_t)(&a.band_overflow - &a.seed_calls) + 1;      // seed_calls .. band_overflow
+    uint64_t* au = &a.dp_cells_timed;
+    const uint64_t* bu = &b.dp_cells_timed;
+    const size_t nu = (size_t)(&a.band_overflow - &a.dp_cells_timed) + 1;  // dp_cells_timed .. band_overflow
     for (size_t i = 0; i < nu; ++i) au[i] += bu[i];
     for (int i = 0; i < 2; ++i) {
         a.call_ms[i] += b.call_ms[i];

@@ -87,11 +87,13 @@ KERNEL_SYMBOLS = {"randstrobes": "k_rs_wave", "lookup": "k_lookup", "find_nams":
                   "ext_band_wide": "k_ext_band64", "ext_band_panel": "k_ext_band_panel",
                   "sites": "k_sites"}
 NK = len(KERNELS)
+EXT_KERNELS = ("ext_scan", "ext_band", "ext_band_wide", "ext_band_panel")   # launched by rsa_extend
 
 
 class KernelStats(C.Structure):
     _fields_ = [("kernel_ms", C.c_double * NK), ("launches", C.c_uint64 * NK), ("alg_bytes", C.c_double * NK),
-                ("seed_calls", C.c_uint64), ("ext_calls", C.c_uint64),
+                ("dp_cells_timed", C.c_uint64), ("seed_calls_timed", C.c_uint64),
+                ("ext_calls_timed", C.c_uint64), ("seed_calls", C.c_uint64), ("ext_calls", C.c_uint64),
                 ("reads", C.c_uint64), ("read_bases", C.c_uint64), ("query_randstrobes", C.c_uint64),
                 ("lookups_found", C.c_uint64), ("filtered", C.c_uint64), ("hits", C.c_uint64),
                 ("nams", C.c_uint64), ("rescued_reads", C.c_uint64),
