@@ -214,6 +214,18 @@ def roofline(ks: dict, elapsed: float) -> dict:
     return out
 
 
+def file_xxh64(path: str) -> str:
+    import xxhash
+    h = xxhash.xxh64()
+    with open(path, "rb") as f:
+        while True:
+            b = f.read(1 << 24)
+            if not b:
+                break
+            h.update(b)
+    return h.hexdigest()
+
+
 def pick_io_dir(requested: str, need_bytes: int) -> str:
     """The bench's FASTQ/SAM directory: the one asked for, else the system temp dir
     (a disk file system's page cache) when it has room for `need_bytes`, else
@@ -371,17 +383,25 @@ def main():
         f1, f2 = fqs[s % n_sets]
         return m.map_files(f1, f2, threads=threads, chunk_size=args.chunk_size, sam_path=sam_paths[s])
 
-    def drop_sams(upto):
+    def drop_sams(upto, keep=()):
         for f in sam_paths[:upto]:
-            if os.path.exists(f):
+            if f not in keep and os.path.exists(f):
                 os.remove(f)
 
     try:
+        # warm-up steps with the SAM digest (the in-memory leg and the CPU path are compared
+        # with it); the timed steps without it, as a mapping run has no use for one -- their
+        # SAM files are checked against the warm-up files of the same read set after timing
+        set_hash, set_file = {}, {}
         for s in range(args.warmup):
             st = map_step(s)
             log(rank, f"warmup {s}: {st.n_reads} reads in {st.map_seconds:.3f} s")
-        drop_sams(args.warmup)
+            if s % n_sets not in set_hash:
+                set_hash[s % n_sets] = st.sam_hash
+                set_file[s % n_sets] = sam_paths[s]
+        drop_sams(args.warmup, keep=set(set_file.values()))
         m.reset_kernel_stats()
+        m.set_sam_digest(False)
 
         barrier()
         torch.cuda.synchronize()
@@ -396,7 +416,6 @@ def main():
             n_reads += st.n_reads
             for f in shard.STAT_FIELDS:
                 totals[f] += getattr(st, f)
-            hashes.append(st.sam_hash)
             sam_file_bytes = os.path.getsize(sam_paths[s])
             log(rank, f"step {s - args.warmup}: {st.n_reads} reads in {st.map_seconds:.3f} s "
                       f"({st.n_reads / st.map_seconds / 1e6:.4f} Mreads/s), SW {st.sw_calls}; thread-s: "
@@ -407,6 +426,17 @@ def main():
         elapsed = time.perf_counter() - t0
         ru1 = resource.getrusage(resource.RUSAGE_SELF)
         ks = m.kernel_stats()
+        m.set_sam_digest(True)
+        # untimed: every timed step's SAM file == the warm-up file of its read set
+        file_hash = {}
+        def fhash(path):
+            if path not in file_hash:
+                file_hash[path] = file_xxh64(path)
+            return file_hash[path]
+        checked = [s for s in range(args.warmup, total_steps) if s % n_sets in set_file]
+        timed_files_identical = all(fhash(sam_paths[s]) == fhash(set_file[s % n_sets])
+                                    for s in checked) if checked else None
+        hashes = [set_hash.get(s % n_sets, 0) for s in range(args.warmup, total_steps)]
     finally:
         for pair in fqs:
             for f in pair:
@@ -529,6 +559,11 @@ def main():
                                  "the host CPUs each rank's pipeline may use (affinity / cgroup share)"},
             "mapping_stats_all_ranks": totals_all,
             "sam_hashes": [f"{h:016x}" for h in hashes],
+            "sam_check": {"timed_files_identical_to_warmup": timed_files_identical,
+                          "note": "timed steps run without the SAM digest (rsam_set_sam_digest 0: a mapping run "
+                                  "computes none); each timed step's SAM file is compared (xxh64 of the file, "
+                                  "untimed) with the warm-up file of the same read set, whose digest is the one "
+                                  "sam_hashes, in_memory and parity compare"},
         }
         if args.stats_out:
             with open(args.stats_out, "w") as f:

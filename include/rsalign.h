@@ -80,6 +80,11 @@ int rsam_map(rsam* m, const rsam_reads* reads, int threads, int chunk_size, cons
 int rsam_map_files(rsam* m, const char* fq1, const char* fq2, int interleaved, int threads, int chunk_size,
                    const char* sam_path, rsam_stats* out);
 
+/* SAM digest (rsam_stats.sam_hash): an order-sensitive hash of the SAM body, folded in
+ * by the workers as they format the records; on by default.  Off, sam_hash is 0 and the
+ * hashing (about 5 % of the host pipeline's CPU time) is skipped. */
+int rsam_set_sam_digest(rsam* m, int on);
+
 /* Map on more devices of this node: each listed device gets its own engine with a
  * full replica of the index; rsam_map then sends every seeding / extension call to
  * the least busy device.  The SAM is the same for any number of devices (one chunk

@@ -118,6 +118,7 @@ struct rsam {
     MappingParameters mp;
     double index_seconds = 0, upload_seconds = 0;
     int read_len = 150;
+    bool digest = true;                // rsam_set_sam_digest
 };
 
 struct rsam_reads {
@@ -371,7 +372,7 @@ static int map_source(rsam* m, ReadSource& src, int threads, int chunk_size, con
     PipelineOptions po;
     po.threads = threads;
     po.chunk_size = chunk_size;
-    po.digest = true;
+    po.digest = m->digest;
     SamSink sk = st.f ? sink_fn : nullptr;
     PipelineResult res = src.paired() ? run_pipeline_pe(src, *m->eng, mc, po, sk, &st)
                                       : run_pipeline_se(src, *m->eng, mc, po, sk, &st);
@@ -417,6 +418,12 @@ int rsam_map_files(rsam* m, const char* fq1, const char* fq2, int interleaved, i
         g_err = e.what();
         return -1;
     }
+}
+
+int rsam_set_sam_digest(rsam* m, int on) {
+    if (!m) return -1;
+    m->digest = on != 0;
+    return 0;
 }
 
 int rsam_add_devices(rsam* m, const int* devices, int n) {

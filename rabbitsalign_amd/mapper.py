@@ -40,7 +40,7 @@ class _Info(C.Structure):
 EXPORTED_SYMBOLS = [
     "rsam_open_files", "rsam_open_synthetic", "rsam_open_like", "rsam_close", "rsam_get_info",
     "rsam_reads_load", "rsam_reads_load_interleaved", "rsam_reads_synthetic", "rsam_reads_write_fastq", "rsam_reads_count", "rsam_reads_free", "rsam_map", "rsam_map_files",
-    "rsam_add_devices", "rsam_kernel_stats", "rsam_reset_kernel_stats", "rsam_engine_name", "rsam_last_error",
+    "rsam_set_sam_digest", "rsam_add_devices", "rsam_kernel_stats", "rsam_reset_kernel_stats", "rsam_engine_name", "rsam_last_error",
 ]
 
 _LIBS: dict = {}
@@ -74,6 +74,7 @@ def load(path: str = PRODUCT_LIB) -> C.CDLL:
     lib.rsam_reads_free.argtypes = [vp]
     lib.rsam_map.argtypes = [vp, vp, i32, i32, cp, C.POINTER(_Stats)]
     lib.rsam_map_files.argtypes = [vp, cp, cp, i32, i32, i32, cp, C.POINTER(_Stats)]
+    lib.rsam_set_sam_digest.argtypes = [vp, i32]
     lib.rsam_kernel_stats.argtypes = [vp, C.POINTER(KernelStats)]
     lib.rsam_reset_kernel_stats.argtypes = [vp]
     lib.rsam_engine_name.restype = cp
@@ -195,6 +196,10 @@ class Mapper:
         if rc != 0:
             raise RuntimeError(f"rsam_map_files: {self._lib.rsam_last_error().decode()}")
         return MapStats(**{f: getattr(st, f) for f, _ in _Stats._fields_})
+
+    def set_sam_digest(self, on: bool):
+        """MapStats.sam_hash computed while mapping (default) or not (sam_hash 0, less host CPU)."""
+        self._lib.rsam_set_sam_digest(self._h, 1 if on else 0)
 
     def add_devices(self, devices):
         """Replicate the index on more devices and spread the mapping calls over them."""

@@ -170,6 +170,13 @@ def test_map_files_equals_map_in_memory(data):
         s_se_mem = m.map(r1, threads=2, chunk_size=300)
         r1.close()
         assert (s_se.sam_hash, s_se.n_reads) == (s_se_mem.sam_hash, s_se_mem.n_reads)
+        # without the digest (rsam_set_sam_digest 0): sam_hash 0, the same SAM file
+        m.set_sam_digest(False)
+        out2 = d / "lib_files_nodigest.sam"
+        s_nd = m.map_files(f1, f2, threads=3, chunk_size=256, sam_path=out2)
+        m.set_sam_digest(True)
+        assert s_nd.sam_hash == 0 and s_nd.sam_bytes == s_files.sam_bytes
+        assert open(out2, "rb").read() == open(out, "rb").read()
     finally:
         m.close()
 
