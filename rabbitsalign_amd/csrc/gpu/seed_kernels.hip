@@ -1426,48 +1426,72 @@ k_rescue_big(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __rest
 }
 
 // final NAM offsets: count[r] = rescued ? rescue NAMs : find NAMs, exclusive scan
-// into ooff[0..n] (one workgroup, each thread a run of reads), total into the
-// header, and the call's statistics summed over the reads (LDS atomics, one
-// global write each: k_lookup's 20 k waves adding to one address serialised)
+// into ooff[0..n] and the total into the header, plus the call's statistics
+// summed over the reads (LDS atomics, one global write each: k_lookup's 20 k
+// waves adding to one address serialised).  One workgroup walks the reads in
+// tiles of 4096, each thread 4 consecutive reads whose loads all issue before
+// the tile's scan (a thread walking a private run of reads waited on one
+// dependent load per read: 142 us a call).
 #define SEED_NSTAT 13
+#define SS_PER 4
 __global__ void __launch_bounds__(1024)
 k_seed_scan(int n_reads, const uint8_t* __restrict__ rescued, const uint32_t* __restrict__ ncnt1,
             const uint32_t* __restrict__ ncnt2, const uint32_t* __restrict__ qcnt, const ReadStat* __restrict__ st,
             uint64_t* __restrict__ ooff, SeedHdr* __restrict__ hdr) {
-    __shared__ uint64_t s[1024];
+    __shared__ uint64_t s_w[16];
     __shared__ unsigned long long s_stat[SEED_NSTAT];
-    const int t = threadIdx.x;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     if (t < SEED_NSTAT) s_stat[t] = 0;
-    const int per = (n_reads + 1023) / 1024;
-    const int a = min(n_reads, t * per), b = min(n_reads, a + per);
-    uint64_t mine = 0;
     uint64_t v[SEED_NSTAT] = {0};    // qrs found good hits_find hits_all scan_find scan_all n1 n2 rr rq rscan rhits
-    for (int r = a; r < b; ++r) {
-        const bool rs = rescued[r] != 0;
-        const uint64_t c1 = ncnt1[r], c2 = rs ? ncnt2[r] : 0;
-        mine += rs ? c2 : c1;
-        const ReadStat x = st[r];
-        v[0] += qcnt[r]; v[1] += x.found; v[2] += x.good; v[3] += x.hits_find; v[4] += x.hits_all;
-        v[5] += x.scan_find; v[6] += x.scan_all; v[7] += c1; v[8] += c2;
-        if (rs) { v[9] += 1; v[10] += qcnt[r]; v[11] += x.scan_all; v[12] += x.hits_all; }
+    uint64_t carry = 0;
+    for (int base = 0; base < n_reads; base += 1024 * SS_PER) {
+        const int r0 = base + t * SS_PER;
+        uint32_t cnt[SS_PER];
+        uint64_t mine = 0;
+#pragma unroll
+        for (int j = 0; j < SS_PER; ++j) {
+            const int r = r0 + j;
+            cnt[j] = 0;
+            if (r < n_reads) {
+                const bool rs = rescued[r] != 0;
+                const uint32_t c1 = ncnt1[r], c2 = rs ? ncnt2[r] : 0, q = qcnt[r];
+                const ReadStat x = st[r];
+                cnt[j] = rs ? c2 : c1;
+                v[0] += q; v[1] += x.found; v[2] += x.good; v[3] += x.hits_find; v[4] += x.hits_all;
+                v[5] += x.scan_find; v[6] += x.scan_all; v[7] += c1; v[8] += c2;
+                if (rs) { v[9] += 1; v[10] += q; v[11] += x.scan_all; v[12] += x.hits_all; }
+            }
+            mine += cnt[j];
+        }
+        uint64_t x = mine;                       // wave inclusive scan of the threads' sums
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) s_w[w] = x;
+        __syncthreads();
+        uint64_t wpre = 0, tot = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint64_t sj = s_w[j];
+            wpre += j < w ? sj : 0;
+            tot += sj;
+        }
+        uint64_t off = carry + wpre + x - mine;
+#pragma unroll
+        for (int j = 0; j < SS_PER; ++j) {
+            if (r0 + j < n_reads) ooff[r0 + j] = off;
+            off += cnt[j];
+        }
+        carry += tot;
+        __syncthreads();                         // s_w is rewritten by the next tile
     }
-    s[t] = mine;
-    __syncthreads();
     for (int k = 0; k < SEED_NSTAT; ++k)
         if (v[k]) atomicAdd(&s_stat[k], (unsigned long long)v[k]);
-    for (int o = 1; o < 1024; o <<= 1) {
-        const uint64_t x = t >= o ? s[t - o] : 0;
-        __syncthreads();
-        s[t] += x;
-        __syncthreads();
-    }
-    uint64_t off = s[t] - mine;
-    for (int r = a; r < b; ++r) {
-        ooff[r] = off;
-        off += rescued[r] ? ncnt2[r] : ncnt1[r];
-    }
-    if (t == 1023) { ooff[n_reads] = s[t]; hdr->total = s[t]; }
+    __syncthreads();
     if (t == 0) {
+        ooff[n_reads] = carry;
+        hdr->total = carry;
         hdr->qrs = s_stat[0]; hdr->found = s_stat[1]; hdr->good = s_stat[2]; hdr->hits_find = s_stat[3];
         hdr->hits_all = s_stat[4]; hdr->scan_find = s_stat[5]; hdr->scan_all = s_stat[6]; hdr->n1 = s_stat[7];
         hdr->n2 = s_stat[8]; hdr->resc_reads = s_stat[9]; hdr->resc_q = s_stat[10]; hdr->resc_scan = s_stat[11];

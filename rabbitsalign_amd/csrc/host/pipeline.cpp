@@ -323,6 +323,10 @@ ChunkPool& chunk_pool() {
 // Each read's name, sequence and qualities may sit anywhere (a caller's heap
 // strings, a mapped file): loading a chunk (sequences) and writing its SAM
 // records (all three) request them a few pairs ahead.
+static bool prefetch_on() {                // RSA_PREFETCH=0 turns the software prefetches off (A/B)
+    static const bool on = !(getenv("RSA_PREFETCH") && atoi(getenv("RSA_PREFETCH")) == 0);
+    return on;
+}
 static size_t rec_ahead() {                 // RSA_PREFETCH_AHEAD, default 4 pairs
     static const size_t d = getenv("RSA_PREFETCH_AHEAD") ? (size_t)std::max(1, atoi(getenv("RSA_PREFETCH_AHEAD"))) : 4;
     return d;
@@ -334,6 +338,11 @@ static inline void prefetch_str(std::string_view s) {
 static inline void prefetch_record(const RecView& r) {
     prefetch_str(r.name);
     prefetch_str(r.qual);
+}
+static inline void prefetch_bytes(const void* p, size_t bytes) {
+    const char* c = (const char*)p;
+    bytes = std::min<size_t>(bytes, 2048);
+    for (size_t o = 0; o < bytes; o += 64) __builtin_prefetch(c + o);
 }
 template <class T>
 static inline void prefetch_vec(const std::vector<T>& v) {
@@ -437,7 +446,13 @@ void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize, On
     const SeedBatchOut& so = c.seeds;
     const auto t = Clock::now();
     std::vector<Nam> nams[2];                 // reused: assign() keeps the capacity
+    const size_t ahead = rec_ahead();
     for (size_t i = 0; i < n; ++i) {
+        if (prefetch_on() && i + ahead < n) {   // the NAMs and site checks came by DMA: not in any cache
+            const size_t a = so.offsets[2 * (i + ahead)], b = so.offsets[2 * (i + ahead) + 2];
+            prefetch_bytes(so.nams.data() + a, (b - a) * sizeof(Nam));
+            if (!so.sites.empty()) prefetch_bytes(so.sites.data() + a, (b - a) * sizeof(rsa_nam_site));
+        }
         bool rescued[2];
         for (int m = 0; m < 2; ++m) {
             const size_t r = 2 * i + m;
@@ -481,7 +496,7 @@ void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistributio
                    SamDigest* digest) {
     const auto t = Clock::now();
     const size_t n = c.size();
-    static const bool pf = !(getenv("RSA_PREFETCH") && atoi(getenv("RSA_PREFETCH")) == 0);
+    const bool pf = prefetch_on();
     const size_t ahead = rec_ahead();
     for (size_t i = 0; i < n; ++i) {
         if (pf && i + ahead < n) prefetch_res(c.res[i + ahead]);
