@@ -512,6 +512,12 @@ void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistributio
             prefetch_record(c.in.r1[i + ahead]);
             prefetch_record(c.in.r2[i + ahead]);
             prefetch_res(c.res[i + ahead]);
+            // SEQ comes from the chunk's upper-cased copy or its reverse complement,
+            // both written at load time and long out of cache
+            prefetch_str(c.in.r1[i + ahead].seq);
+            prefetch_str(c.in.r2[i + ahead].seq);
+            prefetch_str(c.rc(i + ahead, 0));
+            prefetch_str(c.rc(i + ahead, 1));
         }
         const Read read1(c.in.r1[i].seq, c.rc(i, 0)), read2(c.in.r2[i].seq, c.rc(i, 1));
         align_PE_read_last(c.res[i], c.in.r1[i], c.in.r2[i], read1, read2, sam, c.stats, isize, mc, c.rng);
