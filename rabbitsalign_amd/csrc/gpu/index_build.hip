@@ -159,12 +159,6 @@ struct SyncState {
     }
 };
 
-// base o (0..15) of a 16-byte word held as two values
-__device__ __forceinline__ int pick_base(uint64_t wlo, uint64_t whi, unsigned o) {
-    const uint64_t x = o < 8 ? wlo : whi;
-    return nt4_code((unsigned char)(x >> ((o & 7) * 8)));
-}
-
 struct SegTable {
     const uint32_t* contig;     // [n_seg] contig of the segment
     const uint64_t* begin;      // [n_seg] first base (contig coordinates)
@@ -175,12 +169,21 @@ struct SegTable {
 
 // mode 0: warm-up probe (converged flag + syncmer count); 1: count from the
 // replay start; 2: write the syncmers at out[off[seg]..].  The reference
-// buffer is 16-B aligned with 64 bytes of slack past its end (aligned loads
+// buffer is 256-B aligned with 64 bytes of slack past its end (aligned loads
 // never leave the allocation).
+//
+// Memory shape: a wave's lanes walk 64 segments 4 KB apart, so every load and
+// store instruction touches 64 lines.  The bases come from aligned 64-byte
+// blocks held in eight registers (one block per 64 steps: a line is fetched
+// once instead of once per 16-byte load when it drops out of L2 between two),
+// and the records are staged in LDS and stored in runs that end on 128-byte
+// boundaries (whole lines, instead of one 16-byte partial-line store per record).
+constexpr int SEG_STAGE = 8;      // records staged per lane (one 128-B line)
 template <int WC>
 __global__ void __launch_bounds__(TPB)
 k_seg_syncmers(const char* __restrict__ ref, SegTable st, BuildParams p, int mode, uint32_t* __restrict__ count,
                uint8_t* __restrict__ conv, const uint64_t* __restrict__ off, SyncmerOut* __restrict__ out) {
+    __shared__ SyncmerOut s_stage[SEG_STAGE * TPB];        // [slot][lane]: consecutive lanes, consecutive banks
     const uint64_t sg = (uint64_t)blockIdx.x * TPB + threadIdx.x;
     if (sg >= st.n_seg) return;
     const uint32_t c = st.contig[sg];
@@ -198,37 +201,78 @@ k_seg_syncmers(const char* __restrict__ ref, SegTable st, BuildParams p, int mod
     const int kshift = (p.k - 1) * 2, sshift = (p.s - 1) * 2;
     SyncState<WC> S;
     SyncmerOut sm;
-    // bases come from aligned 16-B loads kept in registers: one load per 16 steps
-    // instead of one byte load per step (a wave's lanes walk 64 segments 4 KB apart)
-    const uint64_t c0 = (uint64_t)(cs - ref);
-    uint64_t wbase = ~0ull, wlo = 0, whi = 0;
-    // (no lambda over the words: one captured by reference let the compiler
-    // pick between their addresses and keep them in scratch)
-#define SEG_BASE_AT(i_)                                                               \
+    // the base stream: words w0..w7 of the current 64-B block (w0 next), `cur` the
+    // word being consumed with `nb` bases left in it.  Plain locals rotated with
+    // constant indices: an array picked by a run-time index, or a lambda capturing
+    // them by reference, put the state in scratch.
+    uint64_t w0, w1, w2, w3, w4, w5, w6, w7, cur;
+    int nb, nw;
+    uint64_t nexta;
+#define SEG_LOAD(a_)                                                                  \
+    do {                                                                              \
+        const ulonglong2* q_ = reinterpret_cast<const ulonglong2*>(ref + (a_));       \
+        const ulonglong2 v0_ = q_[0], v1_ = q_[1], v2_ = q_[2], v3_ = q_[3];          \
+        w0 = v0_.x; w1 = v0_.y; w2 = v1_.x; w3 = v1_.y;                                \
+        w4 = v2_.x; w5 = v2_.y; w6 = v3_.x; w7 = v3_.y;                                \
+    } while (0)
+#define SEG_ROT() do { w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6; w6 = w7; } while (0)
+    {
+        const uint64_t g = (uint64_t)(cs - ref) + from, a = g & ~63ull;
+        SEG_LOAD(a);
+        nexta = a + 64;
+        nw = 8;
+        for (unsigned k = (unsigned)((g - a) >> 3); k > 0; --k) { SEG_ROT(); --nw; }
+        cur = w0;
+        SEG_ROT();
+        --nw;
+        cur >>= (g & 7) * 8;
+        nb = 8 - (int)(g & 7);
+    }
+#define SEG_NEXT()                                                                    \
     ({                                                                                \
-        const uint64_t g_ = c0 + (i_), a_ = g_ & ~15ull;                              \
-        if (a_ != wbase) {                                                            \
-            const ulonglong2 v_ = *reinterpret_cast<const ulonglong2*>(ref + a_);     \
-            wlo = v_.x; whi = v_.y; wbase = a_;                                       \
+        if (nb == 0) {                                                                \
+            if (nw == 0) { SEG_LOAD(nexta); nexta += 64; nw = 8; }                    \
+            cur = w0;                                                                 \
+            SEG_ROT();                                                                \
+            --nw;                                                                     \
+            nb = 8;                                                                   \
         }                                                                             \
-        pick_base(wlo, whi, (unsigned)(g_ & 15));                                     \
+        const int c_ = nt4_code((unsigned char)(cur & 0xFF));                         \
+        cur >>= 8;                                                                    \
+        --nb;                                                                         \
+        c_;                                                                           \
     })
     uint64_t i = from;
     for (; i < b; ++i) {                                   // replay, no output
-        const int r = S.step(SEG_BASE_AT(i), (long long)i, p, W, kmask, smask, kshift, sshift, sm);
+        const int r = S.step(SEG_NEXT(), (long long)i, p, W, kmask, smask, kshift, sshift, sm);
         if (mode == 0 && !ok) ok = r < 0 || S.converged(W);
     }
     uint32_t n = 0;
-    SyncmerOut* o = mode == 2 ? out + off[sg] : nullptr;
-    for (; i < e; ++i) {
-        if (S.step(SEG_BASE_AT(i), (long long)i, p, W, kmask, smask, kshift, sshift, sm) == 1) {
-            if (mode == 2) o[n] = sm;
-            n++;
+    if (mode == 2) {
+        SyncmerOut* o = out + off[sg];
+        const uint64_t g0 = off[sg];                       // record index of o[0] in `out`
+        int k = 0;                                         // records staged
+        for (; i < e; ++i) {
+            if (S.step(SEG_NEXT(), (long long)i, p, W, kmask, smask, kshift, sshift, sm) == 1) {
+                s_stage[k * TPB + threadIdx.x] = sm;
+                ++k;
+                ++n;
+                if (((g0 + n) & (SEG_STAGE - 1)) == 0) {     // a 128-B line of `out` is complete
+                    for (int j = 0; j < k; ++j) o[n - k + j] = s_stage[j * TPB + threadIdx.x];
+                    k = 0;
+                }
+            }
         }
+        for (int j = 0; j < k; ++j) o[n - k + j] = s_stage[j * TPB + threadIdx.x];
+    } else {
+        for (; i < e; ++i)
+            if (S.step(SEG_NEXT(), (long long)i, p, W, kmask, smask, kshift, sshift, sm) == 1) n++;
+        count[sg] = n;
+        if (mode == 0) conv[sg] = ok ? 1 : 0;
     }
-    if (mode != 2) count[sg] = n;
-    if (mode == 0) conv[sg] = ok ? 1 : 0;
-#undef SEG_BASE_AT
+#undef SEG_NEXT
+#undef SEG_ROT
+#undef SEG_LOAD
 }
 
 // RandstrobeGenerator::next (randstrobes.cpp:173-202) + assign_randstrobes'
