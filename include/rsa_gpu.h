@@ -123,12 +123,25 @@ enum {
     RSA_SITE_POSITIONS = 8,      /* n_mm / read length < 0.05 and mm_pool[mm_offset .. + n_mm) holds the positions */
     RSA_SITE_POOL_FULL = 16      /* as 8, but the pool was too small: the positions were not stored */
 };
+/* One per NAM, at the NAM's nam_id within its read's list (sites + offsets[i] +
+ * nam_id: the index the NAM had in find_nams' / find_nams_rescue's list, whatever
+ * order the NAMs are returned in).  orig_*: the NAM as found, before any reversal
+ * (reverse_nam_if_needed reverses from these, aln.cpp:78-90). */
 typedef struct rsa_nam_site {
     uint8_t flags;
-    uint8_t pad_;
+    uint8_t orig_is_rc;
     uint16_t n_mm;               /* mismatches of the read-length window (RSA_SITE_HAMMING), capped at 65535 */
     uint32_t mm_offset;          /* into mm_pool (RSA_SITE_POSITIONS) */
+    int32_t orig_query_start, orig_query_end;
 } rsa_nam_site;
+
+/* rsa_nam_batch.order */
+enum {
+    RSA_NAMS_FOUND = 0,          /* each read's NAMs in the order find_nams / find_nams_rescue made them */
+    RSA_NAMS_BY_SCORE = 1        /* lists of at most 16 NAMs in std::sort(by_score) order (aln.cpp:1962-1964:
+                                  * libstdc++ sorts such lists by insertion, i.e. stable by descending score);
+                                  * longer lists as found (the caller sorts them) */
+};
 
 typedef struct rsa_nam_batch {
     rsa_nam* nams;               /* caller-owned, NAMs of read i at [offsets[i], offsets[i+1]) */
@@ -143,12 +156,16 @@ typedef struct rsa_nam_batch {
     uint16_t* mm_pool;
     uint64_t mm_capacity;
     uint64_t mm_used;            /* out */
+    uint32_t order;              /* RSA_NAMS_FOUND (0) or RSA_NAMS_BY_SCORE */
+    uint32_t pad_;
 } rsa_nam_batch;
 
 /* For every read: NAMs = find_nams(randstrobes_query(read)); if rescue_level > 1
  * and (NAMs empty or nonrepetitive_fraction < 0.7) then NAMs =
- * find_nams_rescue(..., rescue_cutoff)  (src/aln.cpp:1946-1962).  NAMs come in
- * the reference's exact pre-sort order (robin_hood slot order per orientation). */
+ * find_nams_rescue(..., rescue_cutoff)  (src/aln.cpp:1946-1962).  With
+ * order = RSA_NAMS_FOUND the NAMs come in the reference's exact pre-sort order
+ * (robin_hood slot order per orientation); RSA_NAMS_BY_SCORE hands lists of up
+ * to 16 over already sorted, as the caller's std::sort would leave them. */
 int rsa_seed(rsa_ctx* ctx, const rsa_read_batch* reads, int32_t rescue_level, uint32_t rescue_cutoff,
              rsa_nam_batch* out);
 

@@ -1502,13 +1502,19 @@ k_seed_scan(int n_reads, const uint8_t* __restrict__ rescued, const uint32_t* __
 // ---------------------------------------------------------------------------
 // k_compact: final list per read = rescue list if rescued else find_nams list,
 // from the NAM arena to the batch's output (at most `cap` NAMs: a batch with
-// more is reported to the host, which asks again with room for them)
+// more is reported to the host, which asks again with room for them).
+// by_score (RSA_NAMS_BY_SCORE): a list of 2..16 NAMs lands in the order the
+// caller's std::sort(by_score) gives it (aln.cpp:1962-1964).  libstdc++ sorts
+// such a list by insertion (no introsort pass at <= 16 elements), which is
+// stable by descending score, so NAM i goes to its rank: the NAMs scoring
+// higher, plus the equal ones before it.  One wave a read, scores by shuffle.
 // ---------------------------------------------------------------------------
-__global__ void k_compact(int n_reads, const uint64_t* __restrict__ nsrc, const uint64_t* __restrict__ rbase,
-                          uint64_t arena_base, const uint32_t* __restrict__ ncnt1, const uint32_t* __restrict__ ncnt2,
-                          const uint8_t* __restrict__ rescued, const rsa_nam* __restrict__ arena,
-                          const uint64_t* __restrict__ ooff, uint64_t cap, rsa_nam* __restrict__ out,
-                          uint32_t* __restrict__ nam_read) {
+__global__ void __launch_bounds__(64)
+k_compact(int n_reads, const uint64_t* __restrict__ nsrc, const uint64_t* __restrict__ rbase,
+          uint64_t arena_base, const uint32_t* __restrict__ ncnt1, const uint32_t* __restrict__ ncnt2,
+          const uint8_t* __restrict__ rescued, const rsa_nam* __restrict__ arena,
+          const uint64_t* __restrict__ ooff, uint64_t cap, rsa_nam* __restrict__ out,
+          uint32_t* __restrict__ nam_read, int by_score) {
     const int r = blockIdx.x;
     if (r >= n_reads) return;
     const bool resc = rescued[r] != 0;
@@ -1516,6 +1522,20 @@ __global__ void k_compact(int n_reads, const uint64_t* __restrict__ nsrc, const 
     const uint32_t n = resc ? ncnt2[r] : ncnt1[r];
     const uint64_t o = ooff[r];
     if (o + n > cap) return;
+    if (by_score && n >= 2 && n <= 16) {
+        const int i = threadIdx.x;
+        const float si = i < (int)n ? src[i].score : 0.0f;
+        int rank = 0;
+        for (int j = 0; j < (int)n; ++j) {
+            const float sj = __shfl(si, j, 64);
+            rank += (sj > si || (sj == si && j < i)) ? 1 : 0;
+        }
+        if (i < (int)n) {
+            out[o + rank] = src[i];
+            if (nam_read) nam_read[o + rank] = (uint32_t)r;
+        }
+        return;
+    }
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
         out[o + i] = src[i];
         if (nam_read) nam_read[o + i] = (uint32_t)r;
@@ -1573,9 +1593,9 @@ __device__ bool site_kmer_eq(const char* ref, int64_t rlen, int64_t rpos, const 
 
 __global__ void __launch_bounds__(256)
 k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read, const SeedHdr* __restrict__ hdr,
-        uint64_t cap, const char* __restrict__ seq, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
-        SeedIndexParams p, rsa_nam_site* __restrict__ sites, uint16_t* __restrict__ pool, uint64_t pool_cap,
-        unsigned long long* __restrict__ pool_used) {
+        uint64_t cap, const uint64_t* __restrict__ ooff, const char* __restrict__ seq, const uint64_t* __restrict__ roff,
+        const uint32_t* __restrict__ rlen, SeedIndexParams p, rsa_nam_site* __restrict__ sites,
+        uint16_t* __restrict__ pool, uint64_t pool_cap, unsigned long long* __restrict__ pool_used) {
     __shared__ uint32_t s_need[16], s_base[16];
     __shared__ unsigned long long s_at;
     // a batch whose NAMs overflow the output was not compacted whole (k_compact skips
@@ -1660,10 +1680,14 @@ k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read,
     if (valid && l16 == 0) {
         rsa_nam_site out;
         out.flags = (uint8_t)flags;
-        out.pad_ = 0;
+        out.orig_is_rc = (uint8_t)(nam.is_rc != 0);
         out.n_mm = (uint16_t)min(hd, 65535u);
         out.mm_offset = mm_off;
-        sites[g] = out;
+        out.orig_query_start = nam.query_start;
+        out.orig_query_end = nam.query_end;
+        // at the NAM's index in its read's list as found (nam_id; the NAMs may come sorted)
+        const uint64_t ro = ooff[r], rn = ooff[r + 1] - ro;
+        sites[(nam.nam_id >= 0 && (uint64_t)nam.nam_id < rn) ? ro + (uint64_t)nam.nam_id : g] = out;
     }
     __syncthreads();                             // s_need / s_base / s_at are reused next round
     }
@@ -1993,7 +2017,8 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
                            DP(B_NCNT2, uint32_t), DP(B_QCNT, uint32_t), DP(B_ST, ReadStat), d_ooff, dhdr);
         hipLaunchKernelGGL(k_compact, dim3(n), dim3(64), 0, st, (int)n, DP(B_NSRC, uint64_t), DP(B_RBASE, uint64_t),
                            slots, DP(B_NCNT1, uint32_t), DP(B_NCNT2, uint32_t), d_resc, DP(B_ARENA, rsa_nam), d_ooff,
-                           cap, DP(B_OUT, rsa_nam), out->sites ? DP(B_NREAD, uint32_t) : nullptr);
+                           cap, DP(B_OUT, rsa_nam), out->sites ? DP(B_NREAD, uint32_t) : nullptr,
+                           out->order == RSA_NAMS_BY_SCORE ? 1 : 0);
         SCHK(hipGetLastError());
         kt.end(st);
         // 6. site checks (aln.cpp:60-93, 374-431)
@@ -2001,7 +2026,7 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
             kt.begin(st, RSA_K_SITES);
             const uint32_t grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1, (cap + 15) / 16), 4096);
             hipLaunchKernelGGL(k_sites, dim3(grid), dim3(256), 0, st, DP(B_OUT, rsa_nam), DP(B_NREAD, uint32_t), dhdr,
-                               cap, DP(B_SEQ, char), d_roff, d_rlen, p, DP(B_SITES, rsa_nam_site), DP(B_POOL, uint16_t),
+                               cap, d_ooff, DP(B_SEQ, char), d_roff, d_rlen, p, DP(B_SITES, rsa_nam_site), DP(B_POOL, uint16_t),
                                out->mm_capacity, &dhdr->mm_used);
             SCHK(hipGetLastError());
             kt.end(st);

@@ -143,13 +143,28 @@ void load_sorted_nams(std::vector<Nam>& dst, const Nam* src, size_t n) {
     for (size_t i = 0; i < n; ++i) dst[i] = src[ix[i]];
 }
 
-static void sort_nams_by_score(std::vector<Nam>& v) {
+void sort_nams_by_score(NamSpan v) {
     const size_t n = v.size();
     if (n > 16) { std::sort(v.begin(), v.end(), by_score<Nam>); return; }
     if (n < 2) return;
+    float sc[16];
+    uint8_t ix[16];
+    for (size_t i = 0; i < n; ++i) { sc[i] = v[i].score; ix[i] = (uint8_t)i; }
+    bool moved = false;
+    for (size_t i = 1; i < n; ++i) {
+        if (!(sc[i] > sc[i - 1])) continue;
+        moved = true;
+        const float xs = sc[i];
+        const uint8_t xi = ix[i];
+        size_t j = i;
+        do { sc[j] = sc[j - 1]; ix[j] = ix[j - 1]; --j; } while (j > 0 && xs > sc[j - 1]);
+        sc[j] = xs;
+        ix[j] = xi;
+    }
+    if (!moved) return;                    // already in order (the engine sorted it)
     Nam tmp[16];
     std::copy(v.begin(), v.end(), tmp);
-    load_sorted_nams(v, tmp, n);
+    for (size_t i = 0; i < n; ++i) v[i] = tmp[ix[i]];
 }
 
 // ------------------------------------------------------------- NAM ops ---
@@ -159,11 +174,10 @@ static bool reverse_nam_if_needed(Nam& nam, const Read& read, const References& 
     if (const rsa_nam_site* st = read.site.find(nam)) {   // checked on the GPU (k_sites)
         const int o = st->flags & RSA_SITE_ORIENT_MASK;
         if (o != 1) return o == 0;
-        const Nam& orig = read.site.orig[nam.nam_id];
-        if (nam.is_rc == orig.is_rc) {                      // not reversed yet (a second call keeps it)
-            nam.is_rc = !orig.is_rc;
-            nam.query_start = (int)read_len - orig.query_end;
-            nam.query_end = (int)read_len - orig.query_start;
+        if (nam.is_rc == st->orig_is_rc) {                  // not reversed yet (a second call keeps it)
+            nam.is_rc = !st->orig_is_rc;
+            nam.query_start = (int)read_len - st->orig_query_end;
+            nam.query_end = (int)read_len - st->orig_query_start;
         }
         return true;
     }
@@ -189,21 +203,21 @@ static bool reverse_nam_if_needed(Nam& nam, const Read& read, const References& 
     return false;
 }
 
-static void shuffle_top_nams(std::vector<Nam>& nams, std::minstd_rand& rng) {   // aln.cpp:1910-1925
+static void shuffle_top_nams(NamSpan nams, std::minstd_rand& rng) {   // aln.cpp:1910-1925
     if (nams.empty()) return;
     const float best = nams[0].score;
     auto it = std::find_if(nams.begin(), nams.end(), [&](const Nam& n) { return n.score != best; });
     if (it != nams.end()) std::shuffle(nams.begin(), it, rng);
 }
 
-static float top_dropoff(const std::vector<Nam>& nams) {   // aln.cpp:1349-1360
+static float top_dropoff(const NamSpan& nams) {   // aln.cpp:1349-1360
     const Nam& n_max = nams[0];
     if (n_max.n_hits <= 2) return 1.0;
     if (nams.size() > 1) return (float)nams[1].n_hits / n_max.n_hits;
     return 0.0;
 }
 
-static uint8_t get_mapq(const std::vector<Nam>& nams, const Nam& n_max) {   // aln.cpp:493-503
+static uint8_t get_mapq(const NamSpan& nams, const Nam& n_max) {   // aln.cpp:493-503
     if (nams.size() <= 1) return 60;
     const float s1 = n_max.score;
     const float s2 = nams[1].score;
@@ -227,14 +241,14 @@ struct NamPair { int score; Nam nam1; Nam nam2; };
 
 // aln.cpp:583-918 (use_fast_loop3 variant)
 // into `joint` (cleared first; the caller's per-thread vector, so no allocation per pair)
-static void get_best_scoring_nam_pairs(std::vector<NamPair>& joint, const std::vector<Nam>& nams1,
-                                       const std::vector<Nam>& nams2, float mu, float sigma) {
+static void get_best_scoring_nam_pairs(std::vector<NamPair>& joint, const NamSpan& nams1,
+                                       const NamSpan& nams2, float mu, float sigma) {
     joint.clear();
     if (nams1.empty() && nams2.empty()) return;
     joint.reserve(nams1.size() + nams2.size());
     // membership by nam_id (the NAM's index in its read's list) instead of a hash set
     RSA_TLS std::vector<uint8_t> added_n1, added_n2;
-    auto reset_ids = [](std::vector<uint8_t>& v, const std::vector<Nam>& ns) {
+    auto reset_ids = [](std::vector<uint8_t>& v, const NamSpan& ns) {
         int mx = -1;
         for (const Nam& n : ns) mx = std::max(mx, n.nam_id);
         v.assign((size_t)(mx + 1), 0);
@@ -530,7 +544,7 @@ static bool rescue_mate_part(AlignTmpRes& res, const Nam& nam, const References&
 
 // rescue_read_part (aln.cpp:1135-1176)
 static void rescue_read_part(int flag, AlignTmpRes& res, const Read& read2, const Read& read1, const MapContext& mc,
-                             std::vector<Nam>& nams1, Details det[2], int k, float mu, float sigma) {
+                             NamSpan nams1, Details det[2], int k, float mu, float sigma) {
     res.type = flag;
     const Nam n_max1 = nams1[0];
     int tries = 0;
@@ -550,7 +564,7 @@ static void rescue_read_part(int flag, AlignTmpRes& res, const Read& read2, cons
 }
 
 // align_PE_part (aln.cpp:1372-1580)
-static void align_PE_part(AlignTmpRes& res, const MapContext& mc, std::vector<Nam>& nams1, std::vector<Nam>& nams2,
+static void align_PE_part(AlignTmpRes& res, const MapContext& mc, NamSpan nams1, NamSpan nams2,
                           const Read& read1, const Read& read2, int k, Details det[2], InsertSizeDistribution& isize) {
     const float mu = isize.mu, sigma = isize.sigma;
     const float dropoff = mc.mparams.dropoff_threshold;
@@ -596,7 +610,7 @@ static void align_PE_part(AlignTmpRes& res, const MapContext& mc, std::vector<Na
     get_best_scoring_nam_pairs(joint, nams1, nams2, mu, sigma);
     // nam_id flags (the id is the NAM's index in its read's list) instead of hash sets
     RSA_TLS std::vector<uint8_t> aligned1, aligned2;
-    auto reset_ids = [](std::vector<uint8_t>& v, const std::vector<Nam>& ns) {
+    auto reset_ids = [](std::vector<uint8_t>& v, const NamSpan& ns) {
         int mx = -1;
         for (const Nam& x : ns) mx = std::max(mx, x.nam_id);
         v.assign((size_t)(mx + 1), 0);
@@ -670,7 +684,7 @@ static void align_PE_part(AlignTmpRes& res, const MapContext& mc, std::vector<Na
 
 // align_PE_read_part (aln.cpp:1927-1981); the find_nams/rescue results come from the engine
 void align_PE_read_part(AlignTmpRes& res, const RecView&, const RecView&, const Read& read1, const Read& read2,
-                        std::vector<Nam> nams[2],
+                        NamSpan nams[2],
                         const bool rescued[2], AlignmentStatistics& stats, InsertSizeDistribution& isize,
                         const MapContext& mc, std::minstd_rand& rng, bool sorted) {
     Details det[2];

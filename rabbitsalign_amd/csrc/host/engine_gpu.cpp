@@ -136,12 +136,15 @@ public:
             out.nams.resize(cap);
             out.sites.resize(want_sites ? cap : 0);
             out.mm_pool.resize(mm_cap);
+            // lists of <= 16 NAMs come sorted (RSA_NAMS_BY_SCORE): part() works on them in place
             rsa_nam_batch nb{out.nams.data(), cap, out.offsets.data(), out.nonrep.data(), out.rescued.data(), 0,
-                             want_sites ? out.sites.data() : nullptr, out.mm_pool.data(), mm_cap, 0};
+                             want_sites ? out.sites.data() : nullptr, out.mm_pool.data(), mm_cap, 0,
+                             RSA_NAMS_BY_SCORE, 0};
             int rc = rsa_seed(ctx_, &rb, rescue_level, rescue_cutoff, &nb);
             if (rc == RSA_ERR_CAPACITY) { cap = nb.needed + 16; continue; }
             if (rc != RSA_OK) throw std::runtime_error(std::string("rsa_seed: ") + rsa_last_error(ctx_));
             out.nams.resize(nb.needed);
+            out.by_score = true;
             if (want_sites) {
                 out.sites.resize(nb.needed);
                 out.mm_pool.resize(nb.mm_used);

@@ -443,9 +443,12 @@ void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize, On
     c.rng.seed((unsigned)c.in.index);
     const size_t n = c.size();
     if (n == 0) return;
-    const SeedBatchOut& so = c.seeds;
+    SeedBatchOut& so = c.seeds;
     const auto t = Clock::now();
-    std::vector<Nam> nams[2];                 // reused: assign() keeps the capacity
+    // an engine that sorted the lists (RSA_NAMS_BY_SCORE) leaves only those over 16
+    // NAMs to sort, and part() works on its download in place; otherwise each list
+    // is gathered into a reused vector in std::sort order
+    std::vector<Nam> copies[2];
     const size_t ahead = rec_ahead();
     for (size_t i = 0; i < n; ++i) {
         if (prefetch_on() && i + ahead < n) {   // the NAMs and site checks came by DMA: not in any cache
@@ -454,14 +457,23 @@ void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize, On
             if (!so.sites.empty()) prefetch_bytes(so.sites.data() + a, (b - a) * sizeof(rsa_nam_site));
         }
         bool rescued[2];
+        NamSpan nams[2];
         for (int m = 0; m < 2; ++m) {
             const size_t r = 2 * i + m;
-            load_sorted_nams(nams[m], so.nams.data() + so.offsets[r], so.offsets[r + 1] - so.offsets[r]);
+            Nam* src = so.nams.data() + so.offsets[r];
+            const size_t cnt = so.offsets[r + 1] - so.offsets[r];
+            if (so.by_score) {
+                nams[m] = NamSpan(src, cnt);
+                if (cnt > 16) sort_nams_by_score(nams[m]);
+            } else {
+                load_sorted_nams(copies[m], src, cnt);
+                nams[m] = NamSpan(copies[m]);
+            }
             rescued[m] = so.rescued[r] != 0;
         }
         Read read1(c.in.r1[i].seq, c.rc(i, 0)), read2(c.in.r2[i].seq, c.rc(i, 1));
-        read1.site = so.site_view(2 * i);
-        read2.site = so.site_view(2 * i + 1);
+        read1.site = so.site_view(2 * i, c.in.r1[i].seq.size());
+        read2.site = so.site_view(2 * i + 1, c.in.r2[i].seq.size());
         align_PE_read_part(c.res[i], c.in.r1[i], c.in.r2[i], read1, read2, nams, rescued, c.stats, isize, mc, c.rng,
                            true);
         c.stats.n_reads += 2;
@@ -902,7 +914,7 @@ PipelineResult run_pipeline_se(ReadSource& src, Engine& eng, const MapContext& m
             for (size_t r = 0; r < n; ++r) {
                 nams.assign(so.nams.begin() + (long)so.offsets[r], so.nams.begin() + (long)so.offsets[r + 1]);
                 Read read(recs[r].seq, rcs[r]);
-                read.site = so.site_view(r);
+                read.site = so.site_view(r, recs[r].seq.size());
                 align_SE_read_part(res[r], recs[r], read, nams, so.rescued[r] != 0, st, mc, rng);
                 st.n_reads++;
             }

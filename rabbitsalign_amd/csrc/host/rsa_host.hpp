@@ -231,16 +231,34 @@ void reverse_into(std::string_view s, char* out);              // plain byte rev
 // GPU site checks of one read's NAM list (rsa_nam_site, include/rsa_gpu.h),
 // indexed by nam_id; empty for the CPU engines (the host computes them)
 struct SiteView {
-    const rsa_nam_site* sites = nullptr;
-    const rsa_nam* orig = nullptr;              // the read's NAMs as the engine returned them
+    const rsa_nam_site* sites = nullptr;        // at each NAM's nam_id
     size_t n = 0;
+    int64_t read_len = 0;
     const uint16_t* pool = nullptr;             // mismatch positions
+    // the check of the NAM the host holds: its id, and its query span as found or reversed
     const rsa_nam_site* find(const rsa_nam& nam) const {
         if (!sites || nam.nam_id < 0 || (size_t)nam.nam_id >= n) return nullptr;
-        const rsa_nam& o = orig[nam.nam_id];
-        if (o.ref_id != nam.ref_id || o.ref_start != nam.ref_start || o.ref_end != nam.ref_end) return nullptr;
-        return &sites[nam.nam_id];
+        const rsa_nam_site& s = sites[nam.nam_id];
+        const bool as_found = nam.query_start == s.orig_query_start && nam.query_end == s.orig_query_end;
+        const bool reversed = nam.query_start == read_len - s.orig_query_end &&
+                              nam.query_end == read_len - s.orig_query_start;
+        return (as_found || reversed) ? &s : nullptr;
     }
+};
+
+// A read's NAM list as part() works on it: the engine's download sorted in place
+// (RSA_NAMS_BY_SCORE) or a vector; shuffled and reversed in place.
+struct NamSpan {
+    Nam* p = nullptr;
+    size_t n = 0;
+    NamSpan() = default;
+    NamSpan(Nam* p_, size_t n_) : p(p_), n(n_) {}
+    NamSpan(std::vector<Nam>& v) : p(v.data()), n(v.size()) {}
+    Nam* begin() const { return p; }
+    Nam* end() const { return p + n; }
+    size_t size() const { return n; }
+    bool empty() const { return n == 0; }
+    Nam& operator[](size_t i) const { return p[i]; }
 };
 
 struct Read {
@@ -363,15 +381,17 @@ struct SeedBatchOut {
         nams.clear(); offsets.clear(); nonrep.clear(); rescued.clear(); sites.clear(); mm_pool.clear();
     }
     // site view of read r's NAM list (empty without site checks)
-    SiteView site_view(size_t r) const {
+    SiteView site_view(size_t r, size_t read_len) const {
         SiteView v;
         if (sites.empty()) return v;
         v.sites = sites.data() + offsets[r];
-        v.orig = nams.data() + offsets[r];
         v.n = offsets[r + 1] - offsets[r];
+        v.read_len = (int64_t)read_len;
         v.pool = mm_pool.data();
         return v;
     }
+    // the engine returned lists of <= 16 NAMs already in std::sort(by_score) order
+    bool by_score = false;
 };
 
 struct SwJob {                                  // query host bytes vs reference window
@@ -426,11 +446,13 @@ struct MapContext {
 // are the pre-sort NAM lists of both mates (already through find_nams/rescue).
 // sorted: nams[m] are already in std::sort(by_score) order (load_sorted_nams)
 void align_PE_read_part(AlignTmpRes& res, const RecView& r1, const RecView& r2, const Read& read1, const Read& read2,
-                        std::vector<Nam> nams[2],
+                        NamSpan nams[2],
                         const bool rescued[2], AlignmentStatistics& stats, InsertSizeDistribution& isize,
                         const MapContext& mc, std::minstd_rand& rng, bool sorted = false);
 // dst = src[0 .. n) in the order std::sort(by_score) gives (aln.cpp:1962-1964), in one gather
 void load_sorted_nams(std::vector<Nam>& dst, const Nam* src, size_t n);
+// the same order in place: <= 16 NAMs by the insertion sort's rule, longer lists by std::sort
+void sort_nams_by_score(NamSpan v);
 void align_PE_read_last(AlignTmpRes& res, const RecView& r1, const RecView& r2, const Read& read1, const Read& read2,
                         Sam& sam,
                         AlignmentStatistics& stats, const InsertSizeDistribution& isize, const MapContext& mc,

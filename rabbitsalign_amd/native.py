@@ -63,10 +63,13 @@ ALN_DTYPE = np.dtype([("sw_score", "<i4"), ("edit_distance", "<u4"), ("ref_start
 class NamBatch(C.Structure):
     _fields_ = [("nams", C.c_void_p), ("capacity", C.c_uint64), ("offsets", C.c_void_p),
                 ("nonrepetitive_fraction", C.c_void_p), ("rescued", C.c_void_p), ("needed", C.c_uint64),
-                ("sites", C.c_void_p), ("mm_pool", C.c_void_p), ("mm_capacity", C.c_uint64), ("mm_used", C.c_uint64)]
+                ("sites", C.c_void_p), ("mm_pool", C.c_void_p), ("mm_capacity", C.c_uint64), ("mm_used", C.c_uint64),
+                ("order", C.c_uint32), ("pad_", C.c_uint32)]
 
 
-SITE_DTYPE = np.dtype([("flags", "u1"), ("pad_", "u1"), ("n_mm", "<u2"), ("mm_offset", "<u4")])
+SITE_DTYPE = np.dtype([("flags", "u1"), ("orig_is_rc", "u1"), ("n_mm", "<u2"), ("mm_offset", "<u4"),
+                       ("orig_query_start", "<i4"), ("orig_query_end", "<i4")])
+NAMS_FOUND, NAMS_BY_SCORE = 0, 1
 
 
 class JobBatch(C.Structure):
@@ -360,9 +363,10 @@ class GpuContext:
         self._check(self.lib.rsa_randstrobes(self.ctx, C.byref(rb), C.byref(b)), "rsa_randstrobes")
         return [out[int(offs[i]):int(offs[i + 1])] for i in range(len(seqs))]
 
-    def seed(self, seqs, rescue_level=2, rescue_cutoff=None, sites=False, mm_capacity=None):
+    def seed(self, seqs, rescue_level=2, rescue_cutoff=None, sites=False, mm_capacity=None, order=NAMS_FOUND):
         """NAM lists per read (+ nonrepetitive fraction, rescued flags); with sites=True
-        also the per-NAM site checks and the mismatch-position pool (rsa_nam_site)."""
+        also the per-NAM site checks (indexed by nam_id) and the mismatch-position pool
+        (rsa_nam_site); order=NAMS_BY_SCORE returns lists of <= 16 NAMs sorted."""
         if rescue_cutoff is None:
             rescue_cutoff = rescue_level * self.index.filter_cutoff if rescue_level < 100 else 1000
         rb, keep = self._reads(seqs)
@@ -376,7 +380,7 @@ class GpuContext:
             mcap = (4 * cap if mm_capacity is None else mm_capacity) if sites else 0
             pool = np.zeros(max(1, mcap), dtype=np.uint16)
             b = NamBatch(_ptr(nams), cap, _ptr(offs), _ptr(nonrep), _ptr(resc), 0,
-                         _ptr(st) if sites else 0, _ptr(pool) if sites else 0, mcap, 0)
+                         _ptr(st) if sites else 0, _ptr(pool) if sites else 0, mcap, 0, order, 0)
             rc = self.lib.rsa_seed(self.ctx, C.byref(rb), rescue_level, rescue_cutoff, C.byref(b))
             if rc == -3:
                 cap = int(b.needed) + 1

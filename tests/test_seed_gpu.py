@@ -90,6 +90,40 @@ def test_seed_bucket_lines_equal_table(setup, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_seed_by_score_order(setup):
+    """order=RSA_NAMS_BY_SCORE: each list of 2..16 NAMs comes as libstdc++'s
+    std::sort(by_score) leaves it (insertion sort: stable, descending score), longer
+    lists as found; the site checks stay at each NAM's nam_id and carry its query span
+    and strand as found (what the host reverses from)."""
+    from rabbitsalign_amd import native
+    name, idx, ctx, ora = setup
+    reads = _reads(name)
+    found, _, _, s_found, p_found = ctx.seed(reads, sites=True)
+    srt, _, _, s_srt, p_srt = ctx.seed(reads, sites=True, order=native.NAMS_BY_SCORE)
+    n_sorted = 0
+    for f, s, sf, ss in zip(found, srt, s_found, s_srt):
+        if 2 <= len(f) <= 16:
+            perm = sorted(range(len(f)), key=lambda i: (-float(f["score"][i]), i))
+            want = f[perm]
+            n_sorted += int(perm != list(range(len(f))))
+        else:
+            want = f
+        assert _nam_equal(s, want)
+        assert list(f["nam_id"]) == list(range(len(f)))
+        for fld in ("flags", "n_mm"):
+            assert np.array_equal(sf[fld], ss[fld])
+        assert np.array_equal(ss["orig_query_start"], f["query_start"])
+        assert np.array_equal(ss["orig_query_end"], f["query_end"])
+        assert np.array_equal(ss["orig_is_rc"], f["is_rc"].astype(np.uint8))
+        for a, b in zip(sf, ss):                 # the same mismatch positions wherever they were pooled
+            if a["flags"] & 8:
+                assert list(p_found[a["mm_offset"]:a["mm_offset"] + a["n_mm"]]) == \
+                    list(p_srt[b["mm_offset"]:b["mm_offset"] + b["n_mm"]])
+    if name == "small":                          # (the repetitive reads' short lists happen to come in order)
+        assert n_sorted > 0
+
+
+@pytest.mark.gpu
 def test_seed_batch_independent(setup):
     name, idx, ctx, ora = setup
     reads = _reads(name)
