@@ -2,6 +2,8 @@
 // HIP C-ABI (include/rsa_gpu.h, librsa_gpu.so).  There is no CPU fallback;
 // a failed GPU call aborts the run with the library's error message.
 #include <algorithm>
+#include <condition_variable>
+#include <exception>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -156,53 +158,142 @@ public:
         }
     }
 
+    // Extension calls from the pipeline's workers are combined: a caller that finds
+    // fewer than ext_leaders() calls on the device takes every pending request (its
+    // own and those that queued meanwhile, up to ext_batch_jobs() jobs) into one
+    // rsa_extend; the others sleep until a leader has stored their results.  While
+    // calls are in flight requests pile up, so the launches grow with the load
+    // (k_ext_scan_g runs far below its throughput at one chunk's 7300 jobs, DESIGN.md
+    // §3) and the results do not change: every job is aligned on its own.
     void extend(const std::vector<SwJob>& jobs, const AlignmentParameters& p,
                 std::vector<AlignmentInfo>& out) override {
-        const size_t n = jobs.size();
-        out.assign(n, AlignmentInfo());
-        if (n == 0) return;
-        const Lease ls = lease();
-        Staging& sg = *ls.s;
-        size_t qtot = 0;
-        for (const auto& j : jobs) qtot += j.query.size();
-        char* q = sg.get<char>(Staging::QUERIES, qtot + 16);
-        rsa_job* js = sg.get<rsa_job>(Staging::JOBS, n);
-        size_t pos = 0;
-        for (size_t i = 0; i < n; ++i) {
-            if (i + 8 < n) {
-                const char* a = jobs[i + 8].query.data();
-                for (size_t o = 0; o < jobs[i + 8].query.size(); o += 64) __builtin_prefetch(a + o);
+        out.assign(jobs.size(), AlignmentInfo());
+        if (jobs.empty()) return;
+        if (ext_leaders() <= 0) {
+            ExtReq me{&jobs, &p, &out};
+            ExtReq* one[1] = {&me};
+            run_batch(one, 1);
+            if (me.err) std::rethrow_exception(me.err);
+            return;
+        }
+        ExtReq me{&jobs, &p, &out};
+        std::unique_lock<std::mutex> l(ext_m_);
+        ext_pending_.push_back(&me);
+        while (!me.done) {
+            if (ext_active_ < ext_leaders() && !ext_pending_.empty()) {
+                ++ext_active_;
+                std::vector<ExtReq*> batch;
+                size_t n_jobs = 0;
+                const AlignmentParameters& bp = *ext_pending_.front()->p;
+                for (auto it = ext_pending_.begin(); it != ext_pending_.end();) {
+                    ExtReq* r = *it;
+                    const bool same = r->p->match == bp.match && r->p->mismatch == bp.mismatch &&
+                                      r->p->gap_open == bp.gap_open && r->p->gap_extend == bp.gap_extend &&
+                                      r->p->end_bonus == bp.end_bonus;
+                    if (same && (batch.empty() || n_jobs + r->jobs->size() <= ext_batch_jobs())) {
+                        batch.push_back(r);
+                        n_jobs += r->jobs->size();
+                        it = ext_pending_.erase(it);
+                    } else {
+                        ++it;
+                    }
+                }
+                l.unlock();
+                run_batch(batch.data(), batch.size());
+                l.lock();
+                for (ExtReq* r : batch) r->done = true;
+                --ext_active_;
+                ext_cv_.notify_all();
+                continue;
             }
-            js[i].query_offset = pos;
-            js[i].query_len = (uint32_t)jobs[i].query.size();
-            js[i].ref_id = jobs[i].ref_id;
-            js[i].ref_start = jobs[i].ref_start;
-            js[i].ref_len = jobs[i].ref_len;
-            memcpy(q + pos, jobs[i].query.data(), jobs[i].query.size());
-            pos += jobs[i].query.size();
+            ext_cv_.wait(l);
         }
-        rsa_job_batch jb{q, qtot, js, (uint32_t)n, p.match, p.mismatch, p.gap_open, p.gap_extend, p.end_bonus};
-        const uint64_t bound = rsa_extend_cigar_bound(&jb) + 1;
-        rsa_aln* alns = sg.get<rsa_aln>(Staging::ALNS, n);
-        uint32_t* pool = sg.get<uint32_t>(Staging::POOL, bound);
-        rsa_aln_batch ab{alns, pool, bound, 0};
-        int rc = rsa_extend(ctx_, &jb, &ab);
-        if (rc != RSA_OK) throw std::runtime_error(std::string("rsa_extend: ") + rsa_last_error(ctx_));
-        for (size_t i = 0; i < n; ++i) {
-            const rsa_aln& a = alns[i];
-            AlignmentInfo& o = out[i];
-            o.sw_score = a.sw_score;
-            o.edit_distance = a.edit_distance;
-            o.ref_start = a.ref_start; o.ref_end = a.ref_end;
-            o.query_start = a.query_start; o.query_end = a.query_end;
-            o.cigar.ops.assign(pool + a.cigar_offset, pool + a.cigar_offset + a.cigar_len);
-        }
+        l.unlock();
+        if (me.err) std::rethrow_exception(me.err);
     }
 
     bool kernel_stats(rsa_kernel_stats* out) override { return rsa_get_stats(ctx_, out) == RSA_OK; }
     void reset_kernel_stats() override { rsa_reset_stats(ctx_); }
 
 private:
+    struct ExtReq {
+        const std::vector<SwJob>* jobs;
+        const AlignmentParameters* p;
+        std::vector<AlignmentInfo>* out;
+        bool done = false;
+        std::exception_ptr err;
+    };
+    // RSA_EXT_LEADERS: combined extension calls in flight at once (0 = every worker
+    // calls rsa_extend for its own chunk); RSA_EXT_BATCH_JOBS: jobs a combined call takes
+    static int ext_leaders() {
+        static const int n = getenv("RSA_EXT_LEADERS") ? atoi(getenv("RSA_EXT_LEADERS")) : 2;
+        return n;
+    }
+    static size_t ext_batch_jobs() {
+        static const size_t n = getenv("RSA_EXT_BATCH_JOBS") ? (size_t)std::max(1, atoi(getenv("RSA_EXT_BATCH_JOBS")))
+                                                             : 32768;
+        return n;
+    }
+    // one rsa_extend over the jobs of several requests, results scattered back;
+    // a failure is handed to every request of the batch
+    void run_batch(ExtReq* const* reqs, size_t nr) {
+        try {
+            size_t n = 0, qtot = 0;
+            for (size_t k = 0; k < nr; ++k) {
+                n += reqs[k]->jobs->size();
+                for (const auto& j : *reqs[k]->jobs) qtot += j.query.size();
+            }
+            const AlignmentParameters& p = *reqs[0]->p;
+            const Lease ls = lease();
+            Staging& sg = *ls.s;
+            char* q = sg.get<char>(Staging::QUERIES, qtot + 16);
+            rsa_job* js = sg.get<rsa_job>(Staging::JOBS, n);
+            size_t pos = 0, i = 0;
+            for (size_t k = 0; k < nr; ++k) {
+                const std::vector<SwJob>& jobs = *reqs[k]->jobs;
+                for (size_t t = 0; t < jobs.size(); ++t, ++i) {
+                    if (t + 8 < jobs.size()) {
+                        const char* a = jobs[t + 8].query.data();
+                        for (size_t o = 0; o < jobs[t + 8].query.size(); o += 64) __builtin_prefetch(a + o);
+                    }
+                    js[i].query_offset = pos;
+                    js[i].query_len = (uint32_t)jobs[t].query.size();
+                    js[i].ref_id = jobs[t].ref_id;
+                    js[i].ref_start = jobs[t].ref_start;
+                    js[i].ref_len = jobs[t].ref_len;
+                    memcpy(q + pos, jobs[t].query.data(), jobs[t].query.size());
+                    pos += jobs[t].query.size();
+                }
+            }
+            rsa_job_batch jb{q, qtot, js, (uint32_t)n, p.match, p.mismatch, p.gap_open, p.gap_extend, p.end_bonus};
+            const uint64_t bound = rsa_extend_cigar_bound(&jb) + 1;
+            rsa_aln* alns = sg.get<rsa_aln>(Staging::ALNS, n);
+            uint32_t* pool = sg.get<uint32_t>(Staging::POOL, bound);
+            rsa_aln_batch ab{alns, pool, bound, 0};
+            int rc = rsa_extend(ctx_, &jb, &ab);
+            if (rc != RSA_OK) throw std::runtime_error(std::string("rsa_extend: ") + rsa_last_error(ctx_));
+            i = 0;
+            for (size_t k = 0; k < nr; ++k) {
+                std::vector<AlignmentInfo>& out = *reqs[k]->out;
+                for (size_t t = 0; t < out.size(); ++t, ++i) {
+                    const rsa_aln& a = alns[i];
+                    AlignmentInfo& o = out[t];
+                    o.sw_score = a.sw_score;
+                    o.edit_distance = a.edit_distance;
+                    o.ref_start = a.ref_start; o.ref_end = a.ref_end;
+                    o.query_start = a.query_start; o.query_end = a.query_end;
+                    o.cigar.ops.assign(pool + a.cigar_offset, pool + a.cigar_offset + a.cigar_len);
+                }
+            }
+        } catch (...) {
+            for (size_t k = 0; k < nr; ++k) reqs[k]->err = std::current_exception();
+        }
+    }
+    std::mutex ext_m_;
+    std::condition_variable ext_cv_;
+    std::vector<ExtReq*> ext_pending_;
+    int ext_active_ = 0;
+
     // staging sets are checked out per call (at most one per concurrent caller)
     struct Lease {
         GpuEngine* e;
