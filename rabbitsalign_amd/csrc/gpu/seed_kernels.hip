@@ -1144,19 +1144,25 @@ k_find_nams_w2(const ReadStat* __restrict__ st, const HitD* __restrict__ hit_slo
         m1.info = LDS_PTR(uint8_t, b1 + (size_t)FN_MAP_CAP * 8);
         m0.info2 = m1.info2 = nullptr; m0.keys2 = m1.keys2 = nullptr; m0.vals2 = m1.vals2 = nullptr;  // rehash -> fallback
     }
-    if (lane == 0) {
-        nonrep[r] = rs.found > 0 ? (float)rs.good / (float)rs.found : 1.0f;   // nam.cpp:920
+    if (lane == 0) nonrep[r] = rs.found > 0 ? (float)rs.good / (float)rs.found : 1.0f;   // nam.cpp:920
+    if (lane < 2) {
         // each map sees its own keys in hit order, which fixes its slot layout; list
-        // ids only have to be distinct, so each map numbers its lists itself and one
-        // pass per orientation keeps the map state in registers
-        map_insert_hits(m0, 0, hits, n_hits);
-        map_insert_hits(m1, 1, hits, n_hits);
-        s_ctl[w][0] = (m0.overflow || m1.overflow) ? 1 : 0;
-        s_ctl[w][1] = (int)m0.nwb;
-        s_ctl[w][2] = (int)m1.nwb;
+        // ids only have to be distinct, so each map numbers its lists itself: lane 0
+        // fills the fwd map while lane 1 fills the rc map (each writes only its own
+        // orientation's hits).  The map is built by value per lane: picking m0 or m1
+        // by reference would take their addresses (scratch).
+        LMap m;
+        uint8_t* bm = s_map[w] + (size_t)lane * FN_MAP_CAP * 9;
+        m.cap = FN_MAP_CAP;
+        m.keys = LDS_PTR(uint32_t, bm); m.vals = LDS_PTR(int32_t, bm + (size_t)FN_MAP_CAP * 4);
+        m.info = LDS_PTR(uint8_t, bm + (size_t)FN_MAP_CAP * 8);
+        m.info2 = nullptr; m.keys2 = nullptr; m.vals2 = nullptr;   // rehash -> fallback
+        map_insert_hits(m, lane, hits, n_hits);
+        s_ctl[w][1 + lane] = (int)m.nwb;
+        s_ctl[w][3 - lane * 3] = m.overflow ? 1 : 0;         // lane 0 -> [3], lane 1 -> [0]
     }
     WSYNC_SEED();
-    if (s_ctl[w][0]) {
+    if (s_ctl[w][0] | s_ctl[w][3]) {
         if (lane == 0) {
             flags[r] = 2; ncnt[r] = 0;
             big_list[atomicAdd(&hdr->big_count, 1u)] = (uint32_t)r;
