@@ -350,6 +350,17 @@ static inline void prefetch_vec(const std::vector<T>& v) {
     const size_t n = std::min<size_t>(v.size() * sizeof(T), 1024);
     for (size_t o = 0; o < n; o += 64) __builtin_prefetch(p + o);
 }
+template <class T>
+static inline void prefetch_vec_w(const std::vector<T>& v) {   // the storage past size() too: it is about to be written
+    const char* p = (const char*)v.data();
+    const size_t n = std::min<size_t>(std::max(v.size(), (size_t)4) * sizeof(T), std::min<size_t>(v.capacity() * sizeof(T), 1024));
+    for (size_t o = 0; o < n; o += 64) __builtin_prefetch(p + o, 1);
+}
+static inline void prefetch_res_w(const AlignTmpRes& r) {
+    prefetch_vec_w(r.align_res);
+    prefetch_vec_w(r.todo_nams);
+    __builtin_prefetch(&r, 1);
+}
 // a pair's alignments and NAM lists, written by part() and extend, read back when stored
 static inline void prefetch_res(const AlignTmpRes& r) {
     prefetch_vec(r.align_res);
@@ -406,8 +417,9 @@ bool pe_load(PeChunk& c, ReadSource& src, size_t idx, const HostAllocFns* io) {
             at += len;
         }
     }
+    // recycled chunk: per-pair vectors keep their capacity; part() empties each pair's
+    // results as it reaches it (a pass over every cold pair here cost its own misses)
     if (c.res.size() > n) c.res.resize(n);
-    for (auto& r : c.res) r.reset();       // recycled chunk: per-pair vectors keep their capacity
     c.res.resize(n);
     return true;
 }
@@ -455,6 +467,7 @@ void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize, On
             const size_t a = so.offsets[2 * (i + ahead)], b = so.offsets[2 * (i + ahead) + 2];
             prefetch_bytes(so.nams.data() + a, (b - a) * sizeof(Nam));
             if (!so.sites.empty()) prefetch_bytes(so.sites.data() + a, (b - a) * sizeof(rsa_nam_site));
+            prefetch_res_w(c.res[i + ahead]);   // part() appends to the pair's lists (storage kept from the last chunk)
         }
         bool rescued[2];
         NamSpan nams[2];
@@ -474,6 +487,7 @@ void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize, On
         Read read1(c.in.r1[i].seq, c.rc(i, 0)), read2(c.in.r2[i].seq, c.rc(i, 1));
         read1.site = so.site_view(2 * i, c.in.r1[i].seq.size());
         read2.site = so.site_view(2 * i + 1, c.in.r2[i].seq.size());
+        c.res[i].reset();
         align_PE_read_part(c.res[i], c.in.r1[i], c.in.r2[i], read1, read2, nams, rescued, c.stats, isize, mc, c.rng,
                            true);
         c.stats.n_reads += 2;
