@@ -420,7 +420,9 @@ def main():
             log(rank, f"step {s - args.warmup}: {st.n_reads} reads in {st.map_seconds:.3f} s "
                       f"({st.n_reads / st.map_seconds / 1e6:.4f} Mreads/s), SW {st.sw_calls}; thread-s: "
                       f"seed {st.t_seed:.2f} extend {st.t_extend:.2f} part {st.t_part:.2f} "
-                      f"collect {st.t_collect:.2f} last {st.t_last:.2f}; sequential phase {st.t_sequential:.3f} s")
+                      f"collect {st.t_collect:.2f} last {st.t_last:.2f}; sequential phase {st.t_sequential:.3f} s "
+                      f"(chunk 0 seeded at {st.t_first_seeded:.3f} s), last chunk: finish {st.t_last_start:.3f} s, "
+                      f"SAM out {st.t_last_put:.3f} s; workers done {st.t_workers_done:.3f} s")
         torch.cuda.synchronize()
         barrier()
         elapsed = time.perf_counter() - t0

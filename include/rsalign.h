@@ -30,6 +30,9 @@ typedef struct rsam_stats {
     double map_seconds;       /* first chunk read -> last SAM byte (consumer cost, main.cpp:446,595) */
     /* host pipeline phases, seconds summed over worker threads (PE path) */
     double t_seed, t_extend, t_part, t_collect, t_last, t_sequential;
+    /* s from the call: chunk 0 seeded; the last chunk's extension + store began; the last
+     * chunk's SAM text went to the sink; all workers done (map_seconds: the sink closed) */
+    double t_first_seeded, t_last_start, t_last_put, t_workers_done;
 } rsam_stats;
 
 /* Open from files: FASTA + optional .sti (NULL: build the index in memory). */

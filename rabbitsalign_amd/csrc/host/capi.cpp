@@ -354,6 +354,10 @@ static void fill_stats(const PipelineResult& res, rsam_stats* out) {
     out->t_collect = res.phases.collect;
     out->t_last = res.phases.last;
     out->t_sequential = res.phases.sequential;
+    out->t_first_seeded = res.phases.first_seeded;
+    out->t_last_start = res.phases.last_start;
+    out->t_last_put = res.phases.last_put;
+    out->t_workers_done = res.phases.workers_done;
 }
 
 // the pipeline over `src` with the SAM (header + body) to sam_path, or kept in memory

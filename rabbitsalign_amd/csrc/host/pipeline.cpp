@@ -173,20 +173,29 @@ struct OrderedSink {
     }
     void write_loop() {
         if (g_worker_start_hook) g_worker_start_hook();
+        // RSA_SINK_TRACE=<file>: one line a write (instrumentation): seconds since the
+        // writer started at the call and at the return, bytes, bytes still queued
+        static const char* trace_path = getenv("RSA_SINK_TRACE");
+        FILE* trace = trace_path ? fopen(trace_path, "a") : nullptr;
+        const auto t0 = Clock::now();
         std::unique_lock<std::mutex> g(m);
         for (;;) {
             cv.wait(g, [&] { return closing || !queue.empty(); });
-            if (queue.empty()) return;          // closing and drained
+            if (queue.empty()) break;           // closing and drained
             SamText t = std::move(queue.front());
             queue.pop_front();
+            const size_t behind = queued_bytes;
             g.unlock();
+            const double ta = since(t0);
             sink(user, t.data(), t.size());
+            if (trace) fprintf(trace, "%.4f %.4f %zu %zu\n", ta, since(t0), t.size(), behind);
             const size_t n = t.size();
             give_back(t);
             g.lock();
             queued_bytes -= n;
             room_cv.notify_all();
         }
+        if (trace) { fprintf(trace, "end %.4f\n", since(t0)); fclose(trace); }
     }
 };
 
@@ -323,6 +332,14 @@ ChunkPool& chunk_pool() {
 // Each read's name, sequence and qualities may sit anywhere (a caller's heap
 // strings, a mapped file): loading a chunk (sequences) and writing its SAM
 // records (all three) request them a few pairs ahead.
+// Cores the mapping workers leave to the SAM writer and the FASTQ readers when the
+// output goes to a sink (RSA_IO_CORES).  The writer is the streamed path's critical
+// path at the end of a call: it must copy every chunk into the page cache in chunk
+// order, and with all cores' worth of workers runnable it got a share of a core.
+static int io_cores(bool has_sink, int threads) {
+    static const int n = getenv("RSA_IO_CORES") ? atoi(getenv("RSA_IO_CORES")) : 1;
+    return has_sink && threads > 2 ? std::max(0, n) : 0;
+}
 static bool prefetch_on() {                // RSA_PREFETCH=0 turns the software prefetches off (A/B)
     static const bool on = !(getenv("RSA_PREFETCH") && atoi(getenv("RSA_PREFETCH")) == 0);
     return on;
@@ -581,7 +598,7 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
     const bool offl = eng.offloads();
     const int W = T + wait_workers(eng, T);
     CpuSlots slots;
-    slots.free = T;
+    slots.free = std::max(1, T - io_cores(sink != nullptr, T));
     // prefetch depth (RSA_PREFETCH chunks, default 2W+2; 0 = every worker seeds its own chunk)
     const char* pf_env = getenv("RSA_PREFETCH");
     const size_t window = pf_env ? (size_t)atol(pf_env) : 2 * (size_t)W + 2;
@@ -708,6 +725,7 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
             if (leader) {
                 // ---- single-worker timeline until the insert-size estimate freezes ----
                 auto pre = acquire(0);
+                lt.first_seeded = since(t0);
                 bool lost = false;
                 {
                     std::lock_guard<std::mutex> g(m);
@@ -792,7 +810,9 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
                     pe_part(*c, mc, est);
                 }
                 if (c) {
+                    lt.last_start = std::max(lt.last_start, since(t0));
                     finish(*c, frozen_isize, jobs, infos);
+                    lt.last_put = std::max(lt.last_put, since(t0));
                     local.add(c->stats);
                     lt.add(c->times);
                     recycle(std::move(c));
@@ -819,6 +839,7 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
     };
     std::atomic<bool> lead_taken{false};
     WorkerPool::get().run(W, [&] { worker(!lead_taken.exchange(true)); });
+    phases_all.workers_done = since(t0);
     // chunks seeded ahead but never mapped (a failure): their input goes back to the source
     for (auto& kv : seeded) recycle(std::move(kv.second));
     if (handed) recycle(std::move(handed));

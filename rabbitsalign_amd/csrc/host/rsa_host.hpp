@@ -683,9 +683,16 @@ void tune_malloc();
 // thread-summed seconds per phase (instrumentation of the host pipeline)
 struct PhaseTimes {
     double seed = 0, extend = 0, part = 0, collect = 0, last = 0, sequential = 0, load = 0, output = 0;
+    // since the call started: chunk 0 loaded and seeded; the last chunk's finish began
+    // ... its SAM text went to the sink; every worker was done (the sink may still be writing)
+    double first_seeded = 0, last_start = 0, last_put = 0, workers_done = 0;
     void add(const PhaseTimes& o) {
         seed += o.seed; extend += o.extend; part += o.part; collect += o.collect; last += o.last;
         sequential += o.sequential; load += o.load; output += o.output;
+        first_seeded = std::max(first_seeded, o.first_seeded);
+        last_start = std::max(last_start, o.last_start);
+        last_put = std::max(last_put, o.last_put);
+        workers_done = std::max(workers_done, o.workers_done);
     }
 };
 

@@ -25,7 +25,9 @@ class _Stats(C.Structure):
                 ("sw_calls", C.c_uint64), ("tried", C.c_uint64), ("nam_rescue", C.c_uint64),
                 ("mate_rescue", C.c_uint64), ("inconsistent", C.c_uint64), ("map_seconds", C.c_double),
                 ("t_seed", C.c_double), ("t_extend", C.c_double), ("t_part", C.c_double),
-                ("t_collect", C.c_double), ("t_last", C.c_double), ("t_sequential", C.c_double)]
+                ("t_collect", C.c_double), ("t_last", C.c_double), ("t_sequential", C.c_double),
+                ("t_first_seeded", C.c_double), ("t_last_start", C.c_double), ("t_last_put", C.c_double),
+                ("t_workers_done", C.c_double)]
 
 
 class _Info(C.Structure):
@@ -101,6 +103,10 @@ class MapStats:
     t_collect: float = 0.0
     t_last: float = 0.0
     t_sequential: float = 0.0
+    t_first_seeded: float = 0.0
+    t_last_start: float = 0.0
+    t_last_put: float = 0.0
+    t_workers_done: float = 0.0
 
 
 class Reads:
