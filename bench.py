@@ -180,21 +180,26 @@ KERNEL_LIMITER = {
 
 
 def roofline(ks: dict, elapsed: float) -> dict:
-    """Roofline object: the kernel with the largest total device time (k_ext_scan_g on
-    the headline workload), plus the top three kernels and the whole path's HBM view."""
+    """Roofline object: the kernel with the largest total device time over all calls
+    (k_ext_scan_g on the headline workload), plus the top three kernels and the whole
+    path's HBM view."""
     kern = {n: k for n, k in ks["kernels"].items() if k["launches"] and k["ms"] > 0}
     if not kern:
         return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None}
-    top = sorted(kern, key=lambda n: -kern[n]["ms"])
-    out = kernel_roofline(top[0], kern[top[0]], ks)
-    out["top_kernels"] = [kernel_roofline(n, kern[n], ks) for n in top[:3]]
-    # whole path: the algorithmic bytes of every kernel of the timed steps / wall time
-    reads = max(1, ks.get("reads", 0))
-    # alg_bytes cover the timed calls (one in RSA_KTIMER_EVERY): scale each kernel's to all calls
+    # kernel times and alg_bytes cover the timed calls (one in RSA_KTIMER_EVERY per lane), and
+    # the timed share differs between seeding and (combined) extension calls: scale each
+    # kernel's to all calls before ranking
     from rabbitsalign_amd.native import EXT_KERNELS
     def scale(n):
         calls, timed = (("ext_calls", "ext_calls_timed") if n in EXT_KERNELS else ("seed_calls", "seed_calls_timed"))
         return ks.get(calls, 0) / max(1, ks.get(timed, 0))
+    top = sorted(kern, key=lambda n: -kern[n]["ms"] * scale(n))
+    out = kernel_roofline(top[0], kern[top[0]], ks)
+    out["device_ms_all_calls"] = round(kern[top[0]]["ms"] * scale(top[0]), 3)
+    out["top_kernels"] = [dict(kernel_roofline(n, kern[n], ks), device_ms_all_calls=round(kern[n]["ms"] * scale(n), 3))
+                          for n in top[:3]]
+    # whole path: the algorithmic bytes of every kernel of the timed steps / wall time
+    reads = max(1, ks.get("reads", 0))
     alg = sum(k["alg_bytes"] * scale(n) for n, k in kern.items())
     path = {"alg_bytes_per_read": round(alg / reads, 1), "achieved": round(alg / elapsed / 1e9, 3),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(alg / elapsed / 1e9 / HBM_PEAK_GBS, 6)}

@@ -28,6 +28,37 @@ def kernel_times(db):
                           "max_us": r[5] / 1e3} for r in rows}
 
 
+def busy(db):
+    """GPU busy time over the mapping span (first to last seeding kernel): the union
+    of all kernel intervals, their summed durations (concurrency = sum / union), and
+    the union per 100 ms window."""
+    c = sqlite3.connect(db)
+    try:
+        rows = c.execute("select name, start, \"end\" from kernels order by start").fetchall()
+    except sqlite3.Error:
+        return None
+    seed = [r for r in rows if short(r[0]) == "k_lookup"]
+    if not seed:
+        return None
+    lo, hi = seed[0][1], max(r[2] for r in seed)
+    iv = [(max(s, lo), min(e, hi)) for _, s, e in rows if e > lo and s < hi]
+    union, cur_s, cur_e, tot = 0, None, None, 0
+    win = {}
+    for s, e in iv:
+        tot += e - s
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                union += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    if cur_e is not None:
+        union += cur_e - cur_s
+    span = hi - lo
+    return {"span_ms": span / 1e6, "busy_union_ms": union / 1e6, "busy_frac": union / span if span else None,
+            "kernel_sum_ms": tot / 1e6, "mean_concurrency": tot / union if union else None}
+
+
 def counter(db, cname):
     c = sqlite3.connect(db)
     rows = c.execute("select kernel_name, count(*), avg(value), sum(value) from counters_collection "
@@ -61,10 +92,16 @@ def main():
         lines.append(f"| {k} | {v['calls']} | {v['total_ms']:.2f} | {100 * v['total_ms'] / total:.1f} | "
                      f"{v['avg_us']:.1f} | {v['min_us']:.1f} | {v['max_us']:.1f} | "
                      f"{'' if rd is None else f'{rd:.0f}'} | {'' if wr is None else f'{wr:.0f}'} |")
+    b = busy(os.path.join(src, "trace", "run_results.db"))
+    if b:
+        lines += ["", f"GPU busy over the mapping span (first to last `k_lookup`, warm-up included): "
+                      f"{b['busy_union_ms']:.1f} ms of {b['span_ms']:.1f} ms = {100 * b['busy_frac']:.1f} % "
+                      f"(union of kernel intervals); summed kernel time {b['kernel_sum_ms']:.1f} ms, mean "
+                      f"concurrency while busy {b['mean_concurrency']:.2f}."]
     with open(out + "_rocprof.md", "w") as f:
         f.write("\n".join(lines) + "\n")
     with open(out + "_traffic.json", "w") as f:
-        json.dump({"source": src, "kernels": kt, "traffic_per_launch": traffic}, f, indent=1)
+        json.dump({"source": src, "kernels": kt, "traffic_per_launch": traffic, "busy": b}, f, indent=1)
     print("\n".join(lines))
 
 
