@@ -100,6 +100,7 @@ struct Lane {
     hipStream_t stream = nullptr;
     KTimer kt;
     bool busy = false;
+    int kind = 0;                      // LANE_SEED or LANE_EXT (the pool it belongs to)
     // extension
     // d_jobs / h_jobs: one staged upload per call, [ExtJobDev x n | scan order x n | ExtStatus (zeroed)];
     // d_alns holds results with CIGAR slot offsets, d_alns_out the copy with packed offsets
@@ -147,16 +148,41 @@ static void set_err(rsa_ctx* ctx, const std::string& s) {
     ctx->err = s;
 }
 
-static const int RSA_MAX_LANES = 16;
+static const int RSA_MAX_LANES = 16;   // per pool
+enum { LANE_SEED = 0, LANE_EXT = 1 };
 
-static Lane* acquire_lane(rsa_ctx* ctx) {
+// Extension calls have lanes of their own, on high-priority streams: an extension
+// call finishes chunks whose SAM the ordered output waits for, while the seeding
+// calls mostly run chunks ahead of it, so the command processor dispatches the
+// extension kernels' workgroups first when both wait for compute units
+// (RSA_EXT_PRIORITY=0: one pool at normal priority for both kinds).
+static bool ext_priority() {
+    static const bool on = !(getenv("RSA_EXT_PRIORITY") && getenv("RSA_EXT_PRIORITY")[0] == '0');
+    return on;
+}
+
+static Lane* acquire_lane(rsa_ctx* ctx, int kind) {
+    if (!ext_priority()) kind = LANE_SEED;
     std::unique_lock<std::mutex> g(ctx->lane_m);
     for (;;) {
-        for (Lane* l : ctx->lanes)
+        int mine = 0;
+        for (Lane* l : ctx->lanes) {
+            if (l->kind != kind) continue;
+            mine++;
             if (!l->busy) { l->busy = true; return l; }
-        if (ctx->lanes.size() < (size_t)RSA_MAX_LANES) {
+        }
+        if (mine < RSA_MAX_LANES) {
             Lane* l = new Lane();
-            if (hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking) != hipSuccess) { delete l; return nullptr; }
+            l->kind = kind;
+            hipError_t e;
+            if (kind == LANE_EXT) {
+                int least = 0, greatest = 0;
+                (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+                e = hipStreamCreateWithPriority(&l->stream, hipStreamNonBlocking, greatest);
+            } else {
+                e = hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking);
+            }
+            if (e != hipSuccess) { delete l; return nullptr; }
             l->busy = true;
             ctx->lanes.push_back(l);
             return l;
@@ -170,7 +196,7 @@ static void release_lane(rsa_ctx* ctx, Lane* l) {
         std::lock_guard<std::mutex> g(ctx->lane_m);
         l->busy = false;
     }
-    ctx->lane_cv.notify_one();
+    ctx->lane_cv.notify_all();
 }
 
 // wall-time breakdown of one entry-point call into ctx->stats (call_ms / lane_wait_ms / device_wait_ms)
@@ -180,9 +206,9 @@ struct CallTimer {
     std::chrono::steady_clock::time_point t0;
     double lane_ms = 0;
     CallTimer(rsa_ctx* c, int w) : ctx(c), which(w), t0(std::chrono::steady_clock::now()) { device_wait_ms() = 0; }
-    Lane* lane() {
+    Lane* lane(int kind) {
         const auto t = std::chrono::steady_clock::now();
-        Lane* l = acquire_lane(ctx);
+        Lane* l = acquire_lane(ctx, kind);
         lane_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
         return l;
     }
@@ -643,7 +669,7 @@ int rsa_extend(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out) {
     CallTimer ct(ctx, 1);
     rsa_pending P;
     P.ctx = ctx;
-    P.L = ct.lane();
+    P.L = ct.lane(LANE_EXT);
     if (!P.L) { set_err(ctx, "rsa_extend: cannot create HIP stream"); return RSA_ERR_HIP; }
     LaneGuard guard{ctx, P.L};
     if (int rc = ext_enqueue(ctx, jb, out, P)) return rc;
@@ -676,7 +702,7 @@ int rsa_extend_async(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out, 
     P->ctx = ctx;
     P->out = out;
     if (jb->n_jobs == 0) { *pending = P; return RSA_OK; }   // nothing enqueued: rsa_wait returns at once
-    P->L = acquire_lane(ctx);
+    P->L = acquire_lane(ctx, LANE_EXT);
     if (!P->L) {
         delete P;
         unpend();
@@ -740,7 +766,7 @@ int rsa_randstrobes(rsa_ctx* ctx, const rsa_read_batch* rb, rsa_randstrobe_batch
     if (rc) return rc;
     if (rb->n_reads == 0) { out->needed = 0; if (out->offsets) out->offsets[0] = 0; return RSA_OK; }
     HIPCHK(hipSetDevice(ctx->device));
-    Lane* L = acquire_lane(ctx);
+    Lane* L = acquire_lane(ctx, LANE_SEED);
     if (!L) { set_err(ctx, "cannot create HIP stream"); return RSA_ERR_HIP; }
     LaneGuard guard{ctx, L};
     std::string err;
@@ -757,7 +783,7 @@ int rsa_seed(rsa_ctx* ctx, const rsa_read_batch* rb, int32_t rescue_level, uint3
     if (!ctx->d_rs || !ctx->d_starts) { set_err(ctx, "rsa_seed: context opened without an index"); return RSA_ERR_ARG; }
     HIPCHK(hipSetDevice(ctx->device));
     CallTimer ct(ctx, 0);
-    Lane* L = ct.lane();
+    Lane* L = ct.lane(LANE_SEED);
     if (!L) { set_err(ctx, "cannot create HIP stream"); return RSA_ERR_HIP; }
     LaneGuard guard{ctx, L};
     std::string err;

@@ -22,6 +22,7 @@
 #include <cstring>
 #include <deque>
 #include <map>
+#include <set>
 #include <mutex>
 #include <stdexcept>
 #include <thread>
@@ -42,22 +43,46 @@ inline double since(Clock::time_point t) { return std::chrono::duration<double>(
 // CPU slots: at most `threads` workers compute at once.  With an offloading
 // engine the pipeline runs extra workers, and a worker gives its slot back
 // while it sleeps on the GPU (or on another chunk), so the host cores stay busy
-// while seeding/extension run on the device.
+// while seeding/extension run on the device.  A freed slot goes to the waiting
+// worker with the lowest chunk index: the SAM writer takes chunks in order, so
+// the oldest chunk in flight is the one it may be waiting for, while the newest
+// are only being seeded ahead (RSA_SLOT_ORDER=0: first come, first served).
 struct CpuSlots {
+    static constexpr uint64_t kIdle = UINT64_MAX;   // a worker with no chunk yet
     std::mutex m;
-    std::condition_variable cv;
     int free = 0;
-    void acquire() {
+    struct Waiter {
+        uint64_t prio, seq;
+        std::condition_variable cv;
+        bool granted = false;
+    };
+    struct ByPrio {
+        bool operator()(const Waiter* a, const Waiter* b) const {
+            return a->prio != b->prio ? a->prio < b->prio : a->seq < b->seq;
+        }
+    };
+    std::set<Waiter*, ByPrio> waiters;
+    uint64_t seq = 0;
+    static bool ordered() {
+        static const bool on = !(getenv("RSA_SLOT_ORDER") && getenv("RSA_SLOT_ORDER")[0] == '0');
+        return on;
+    }
+    void acquire(uint64_t prio = kIdle) {
         std::unique_lock<std::mutex> g(m);
-        cv.wait(g, [&] { return free > 0; });
-        --free;
+        if (free > 0 && waiters.empty()) { --free; return; }
+        Waiter w;
+        w.prio = ordered() ? prio : 0;
+        w.seq = seq++;
+        waiters.insert(&w);
+        w.cv.wait(g, [&] { return w.granted; });       // release() handed its slot over
     }
     void release() {
-        {
-            std::lock_guard<std::mutex> g(m);
-            ++free;
-        }
-        cv.notify_one();
+        std::lock_guard<std::mutex> g(m);
+        if (waiters.empty()) { ++free; return; }
+        Waiter* w = *waiters.begin();
+        waiters.erase(waiters.begin());
+        w->granted = true;
+        w->cv.notify_one();                              // under the lock: w lives on its waiter's stack
     }
 };
 struct SlotHold {                 // a slot for the lifetime of a worker
@@ -65,11 +90,14 @@ struct SlotHold {                 // a slot for the lifetime of a worker
     explicit SlotHold(CpuSlots& s_) : s(s_) { s.acquire(); }
     ~SlotHold() { s.release(); }
 };
-struct Unslot {                   // the slot handed back for a blocking section
+struct Unslot {                   // the slot handed back for a blocking section (chunk `prio` waits)
     CpuSlots& s;
     bool on;
-    Unslot(CpuSlots& s_, bool on_) : s(s_), on(on_) { if (on) s.release(); }
-    ~Unslot() { if (on) s.acquire(); }
+    uint64_t prio;
+    Unslot(CpuSlots& s_, bool on_, uint64_t prio_ = CpuSlots::kIdle) : s(s_), on(on_), prio(prio_) {
+        if (on) s.release();
+    }
+    ~Unslot() { if (on) s.acquire(prio); }
 };
 
 // extra workers beyond the compute slots (RSA_WAIT_WORKERS; default: three
@@ -448,7 +476,7 @@ void pe_seed(PeChunk& c, Engine& eng, const MapContext& mc, CpuSlots& slots) {
     if (n == 0) { c.seeds.clear(); return; }
     const auto t = Clock::now();
     if (eng.io_alloc()) {                     // packed by pe_load in DMA-able memory
-        Unslot u(slots, eng.offloads());
+        Unslot u(slots, eng.offloads(), c.in.index);
         eng.seed_packed(c.seqbuf.data(), c.seqoff.data(), c.seqlen.data(), 2 * n, mc.mparams.rescue_level,
                         (unsigned)mc.mparams.rescue_cutoff, c.seeds);
         c.times.seed += since(t);
@@ -457,7 +485,7 @@ void pe_seed(PeChunk& c, Engine& eng, const MapContext& mc, CpuSlots& slots) {
     std::vector<std::string_view> reads;
     reads.reserve(2 * n);
     for (size_t i = 0; i < n; ++i) { reads.push_back(c.in.r1[i].seq); reads.push_back(c.in.r2[i].seq); }
-    Unslot u(slots, eng.offloads());
+    Unslot u(slots, eng.offloads(), c.in.index);
     eng.seed(reads, mc.mparams.rescue_level, (unsigned)mc.mparams.rescue_cutoff, c.seeds);
     c.times.seed += since(t);
 }
@@ -670,7 +698,7 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
         auto ready = [&] { return seeded.count(idx) || failure || idx >= n_chunks; };
         if (!ready()) {
             g.unlock();
-            Unslot u(slots, true);
+            Unslot u(slots, true, idx);
             g.lock();
             cv.wait(g, ready);
             g.unlock();          // the slot comes back without the lock held
@@ -691,7 +719,7 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
         c.stats.tot_aligner_calls += jobs.size();
         const auto te = Clock::now();
         {
-            Unslot u(slots, offl);
+            Unslot u(slots, offl, c.in.index);
             eng.extend(jobs, mc.aparams, infos);
         }
         c.times.extend += since(te);
@@ -748,7 +776,7 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
                     next++;
                     const auto te = Clock::now();
                     {
-                        Unslot u(slots, offl);
+                        Unslot u(slots, offl, pre->in.index);
                         eng.extend(jobs, mc.aparams, infos);
                     }
                     pre->times.extend += since(te);
@@ -935,7 +963,7 @@ PipelineResult run_pipeline_se(ReadSource& src, Engine& eng, const MapContext& m
             for (size_t i = 0; i < n; ++i) reads.push_back(recs[i].seq);
             so.clear();
             if (n) {
-                Unslot u(slots, offl);
+                Unslot u(slots, offl, idx);
                 eng.seed(reads, mc.mparams.rescue_level, (unsigned)mc.mparams.rescue_cutoff, so);
             }
             if (res.size() > n) res.resize(n);
@@ -959,7 +987,7 @@ PipelineResult run_pipeline_se(ReadSource& src, Engine& eng, const MapContext& m
                 collect_jobs_se(res[r], read, mc, jobs);
             }
             {
-                Unslot u(slots, offl);
+                Unslot u(slots, offl, idx);
                 eng.extend(jobs, mc.aparams, infos);
             }
             st.tot_aligner_calls += jobs.size();

@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Summarise an RSA_SINK_TRACE file (one line a SAM write: seconds since the writer
+started at the call and at the return, bytes, bytes queued; "end T" a mapping call).
+
+    python scripts/sink_report.py sink.txt [bench.json]
+
+Per mapping call: the first write, the writer's idle time between writes (and the
+largest gaps, by chunk), its busy time and rate, and the call's end; the timed steps
+are the last ones.  With the bench line, its value and host core-us a read."""
+import json
+import sys
+
+
+def calls(path):
+    out, cur = [], []
+    for line in open(path):
+        f = line.split()
+        if not f:
+            continue
+        if f[0] == "end":
+            out.append((cur, float(f[1])))
+            cur = []
+        else:
+            cur.append((float(f[0]), float(f[1]), int(f[2]), int(f[3])))
+    return out
+
+
+def main():
+    segs = calls(sys.argv[1])
+    for cur, end in segs:
+        if not cur:
+            continue
+        gaps = [(cur[i][0] - cur[i - 1][1]) * 1e3 for i in range(1, len(cur))]
+        busy = sum(b - a for a, b, _, _ in cur)
+        nbytes = sum(n for _, _, n, _ in cur)
+        big = [(i, round(g, 1)) for i, g in enumerate(gaps, 1) if g > 2.0]
+        print(f"  first {cur[0][0] * 1e3:5.1f} ms  idle {sum(g for g in gaps if g > 0):5.1f} ms  busy {busy * 1e3:5.1f} ms "
+              f"({nbytes / busy / 1e9:.2f} GB/s)  end {end * 1e3:5.1f} ms  gaps>2ms {big}")
+    if len(sys.argv) > 2:
+        try:
+            d = json.load(open(sys.argv[2]))
+            print(f"  value {d['value']:.3f} Mreads/s, {d['host_cpu']['core_us_per_read']} core-us a read, "
+                  f"in memory {d['in_memory']['value']:.3f}")
+        except (OSError, ValueError, KeyError):
+            pass
+
+
+if __name__ == "__main__":
+    main()
