@@ -233,7 +233,8 @@ int rsa_wait(rsa_pending* pending);
 uint64_t rsa_extend_cigar_bound(const rsa_job_batch* jobs);
 
 /* Page-locked host memory for batch buffers (DMA-speed H2D/D2H); any caller
- * buffer works, these are only faster.  NULL on failure. */
+ * buffer works, these are only faster.  Portable: usable with every device's
+ * context.  NULL on failure. */
 void* rsa_host_alloc(size_t bytes);
 void rsa_host_free(void* p);
 

@@ -292,20 +292,27 @@ __device__ __forceinline__ void rev_g(const uint16_t* __restrict__ lane_prof, in
                 E[r] = max3i(E[r] - gE, t, 0);
                 Fw = max3i(Fw - gE, t, 0);
                 F = max3i(F - gE, t, 0);
-                cm = max(cm, valid[r] ? h : 0);
+                cm = max(cm, h);                   // padding rows included: cm >= the valid rows' maximum
             }
             F_out = F;
             Fw_out = Fw;
             H_last = Hout[R - 1];
-            const bool hit = cm == terminate && tcol == INT_MAX;
-            if (__builtin_amdgcn_ballot_w64(hit)) {        // at most once a job: skip the row search otherwise
-                if (hit) {
-                    tcol = c;
+            // a column whose maximum over every row reaches terminate may hold a valid row
+            // that equals it: only such columns (at most a few a job) look at the valid rows
+            const bool cand = cm >= terminate && tcol == INT_MAX;
+            if (__builtin_amdgcn_ballot_w64(cand)) {
+                if (cand) {
                     int row = INT_MAX;
 #pragma unroll
                     for (int r = R - 1; r >= 0; --r)
                         if (valid[r] && Hout[r] == terminate) row = gl * R + r;
-                    trow = row;
+                    int cmv = 0;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) cmv = max(cmv, valid[r] ? Hout[r] : 0);
+                    if (cmv == terminate) {
+                        tcol = c;
+                        trow = row;
+                    }
                 }
             }
         }

@@ -744,8 +744,10 @@ int rsa_wait(rsa_pending* p) {
 }
 
 void* rsa_host_alloc(size_t bytes) {
+    // portable: the product's multi-device engine (csrc/host/multi.cpp) hands one page-locked
+    // buffer to whichever device's context serves the call
     void* p = nullptr;
-    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable) != hipSuccess) return nullptr;
     return p;
 }
 

@@ -56,7 +56,8 @@ public:
         Hold h(*this);
         e_[h.i]->seed_packed(blob, offs, lens, n, rescue_level, rescue_cutoff, out);
     }
-    // every device's engine shares the process's page-locked allocator (or none)
+    // every device's engine shares the process's page-locked allocator (or none): rsa_host_alloc
+    // buffers are portable (hipHostMallocPortable), usable by any device's context
     const HostAllocFns* io_alloc() const override { return e_[0]->io_alloc(); }
     void extend(const std::vector<SwJob>& jobs, const AlignmentParameters& p,
                 std::vector<AlignmentInfo>& out) override {

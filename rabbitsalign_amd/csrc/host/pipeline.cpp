@@ -28,6 +28,9 @@
 #include <thread>
 
 #include <malloc.h>
+#include <sys/resource.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include "rsa_host.hpp"
 
@@ -367,6 +370,16 @@ ChunkPool& chunk_pool() {
 static int io_cores(bool has_sink, int threads) {
     static const int n = getenv("RSA_IO_CORES") ? atoi(getenv("RSA_IO_CORES")) : 1;
     return has_sink && threads > 2 ? std::max(0, n) : 0;
+}
+// RSA_WORKER_NICE=n: mapping workers run at nice n (default 0), so the SAM writer and the
+// FASTQ readers -- the streamed path's serial stages -- win the host cores they compete for
+static void worker_priority() {
+    static const int n = getenv("RSA_WORKER_NICE") ? atoi(getenv("RSA_WORKER_NICE")) : 0;
+    thread_local int set = 0;
+    if (n > 0 && set != n) {
+        (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), n);
+        set = n;
+    }
 }
 static bool prefetch_on() {                // RSA_PREFETCH=0 turns the software prefetches off (A/B)
     static const bool on = !(getenv("RSA_PREFETCH") && atoi(getenv("RSA_PREFETCH")) == 0);
@@ -733,6 +746,7 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
 
     auto worker = [&](bool leader) {
         if (g_worker_start_hook) g_worker_start_hook();
+        worker_priority();
         ScratchLease scratch;
         std::vector<SwJob>& jobs = scratch.s->jobs;
         std::vector<AlignmentInfo>& infos = scratch.s->infos;
@@ -937,6 +951,7 @@ PipelineResult run_pipeline_se(ReadSource& src, Engine& eng, const MapContext& m
     std::atomic<bool> failed{false};
     auto worker = [&]() {
         if (g_worker_start_hook) g_worker_start_hook();
+        worker_priority();
         std::unique_ptr<SlotHold> hold(new SlotHold(slots));
         ScratchLease scratch;
         std::vector<SwJob>& jobs = scratch.s->jobs;

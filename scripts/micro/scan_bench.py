@@ -37,6 +37,8 @@ def make(rng, ref, n, L=150, W=257):
 def main():
     import torch  # noqa: F401
     from rabbitsalign_amd import native
+    if os.environ.get("SCAN_BENCH_LIB"):          # A/B against another build of librsa_gpu.so
+        native.load(os.environ["SCAN_BENCH_LIB"])
     sizes = [int(x) for x in sys.argv[1:]] or [16, 256, 1024, 4096, 7300, 16384, 65536]
     rng = np.random.default_rng(1)
     ref = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, 4_000_000)].copy()
