@@ -5,27 +5,32 @@
 
 #define RSA_WAVE 64
 
+// Base codes as selects on the case-folded byte, no branches: a switch compiles to
+// a tree of divergent branches, and every kernel that translates bases (staging
+// loops over a window, per-row lookups) paid its exec-mask bookkeeping per byte.
+// c | 0x20 equals 'a'/'c'/'g'/'t'/'u' only for that letter in either case.
+
 // SSW base translation (ext/ssw/ssw_cpp.cpp:12-25, kBaseTranslation):
 // A/a/U/u -> 0, C/c -> 1, G/g -> 2, T/t -> 3, everything else -> 4.
 __device__ __forceinline__ int ssw_code(unsigned char c) {
-    switch (c) {
-        case 'A': case 'a': case 'U': case 'u': return 0;
-        case 'C': case 'c': return 1;
-        case 'G': case 'g': return 2;
-        case 'T': case 't': return 3;
-        default: return 4;
-    }
+    const uint32_t u = (uint32_t)c | 0x20u;
+    int r = 4;
+    r = u == 't' ? 3 : r;
+    r = u == 'g' ? 2 : r;
+    r = u == 'c' ? 1 : r;
+    r = (u == 'a' || u == 'u') ? 0 : r;
+    return r;
 }
 
 // seq_nt4_table (src/randstrobes.cpp:14-31): U/u -> 3 (unlike SSW)
 __device__ __forceinline__ int nt4_code(unsigned char c) {
-    switch (c) {
-        case 'A': case 'a': return 0;
-        case 'C': case 'c': return 1;
-        case 'G': case 'g': return 2;
-        case 'T': case 't': case 'U': case 'u': return 3;
-        default: return 4;
-    }
+    const uint32_t u = (uint32_t)c | 0x20u;
+    int r = 4;
+    r = (u == 't' || u == 'u') ? 3 : r;
+    r = u == 'g' ? 2 : r;
+    r = u == 'c' ? 1 : r;
+    r = u == 'a' ? 0 : r;
+    return r;
 }
 
 // lane l receives lane l-1's value; lane 0 receives 0 (DPP wave_shr:1)
