@@ -659,7 +659,10 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
     bool frozen = false, done = false;
     bool early = false;            // the parallel stage opened from inside part() (early_freeze)
     bool leader_busy = true;       // the leader may still hand a chunk over: nobody ends the run before
-    bool lead_seeded = false;      // prefetch waits until chunk 0 is seeded: it would only queue
+    // chunks 1..RSA_EARLY_SEEDS (default 2) are seeded alongside chunk 0: the writer needs them
+    // right after it, and a few calls do not crowd chunk 0's seeding out of the GPU
+    static const size_t early_seeds = getenv("RSA_EARLY_SEEDS") ? (size_t)atoi(getenv("RSA_EARLY_SEEDS")) : 2;
+    bool lead_seeded = false;      // other prefetch waits until chunk 0 is seeded: it would only queue
                                    // other chunks' seeding ahead of the single-worker timeline
     size_t next_par = 0;           // next chunk for the parallel stage (valid once frozen)
     std::unique_ptr<PeChunk> handed;                     // part() done in the sequential phase
@@ -824,7 +827,8 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
                         if (failure || done) break;
                         if (frozen && handed) { c = std::move(handed); break; }
                         if (frozen && next_par < n_chunks) { idx = next_par++; break; }
-                        if (lead_seeded && next_seed < n_chunks && next_seed < consumed + window) {
+                        if ((lead_seeded || next_seed <= early_seeds) && next_seed < n_chunks &&
+                            next_seed < consumed + window) {
                             pf = next_seed;
                             claim(pf);
                             while (is_claimed(next_seed)) next_seed++;

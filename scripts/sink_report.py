@@ -36,6 +36,16 @@ def main():
         big = [(i, round(g, 1)) for i, g in enumerate(gaps, 1) if g > 2.0]
         print(f"  first {cur[0][0] * 1e3:5.1f} ms  idle {sum(g for g in gaps if g > 0):5.1f} ms  busy {busy * 1e3:5.1f} ms "
               f"({nbytes / busy / 1e9:.2f} GB/s)  end {end * 1e3:5.1f} ms  gaps>2ms {big}")
+    tail = [c for c in segs if c[0]][-5:]          # the bench's timed steps (5 by default)
+    if tail:
+        def mean(f):
+            return sum(f(c) for c in tail) / len(tail)
+        first = mean(lambda c: c[0][0][0] * 1e3)
+        head = mean(lambda c: sum(max(0.0, c[0][i][0] - c[0][i - 1][1]) for i in range(1, min(5, len(c[0])))) * 1e3)
+        idle = mean(lambda c: sum(max(0.0, c[0][i][0] - c[0][i - 1][1]) for i in range(1, len(c[0]))) * 1e3)
+        end = mean(lambda c: c[1] * 1e3)
+        print(f"  last {len(tail)} calls: first write {first:.1f} ms, idle at chunks 1-4 {head:.1f} ms, idle {idle:.1f} ms, "
+              f"end {end:.1f} ms")
     if len(sys.argv) > 2:
         try:
             d = json.load(open(sys.argv[2]))
