@@ -112,6 +112,17 @@ def host_cores(pinned: bool = False) -> int:
 
 
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "latest_traffic.json")
+EXT_PMC_JSON = os.path.join(ROOT, "profiles", "r03", "ext_pmc.json")
+
+
+def scan_instr_per_cell():
+    """wave64 VALU instructions per DP cell of k_ext_scan_g, from the committed PMC pass
+    (scripts/gpu_ext_pmc.sh: SQ_INSTS_VALU / cells of an isolated 22000-job launch), or None."""
+    try:
+        with open(EXT_PMC_JSON) as f:
+            return float(json.load(f)["k_ext_scan_g"]["wave_instr_per_cell"])
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def pmc_traffic(symbol: str):
@@ -155,6 +166,16 @@ def kernel_roofline(name: str, k: dict, ks: dict) -> dict:
                                    "frac": round(achieved / DP_SPEC_GCELLS, 5)},
                     "cells_per_launch": round(cells, 1),
                     "hbm_GBps": round(per_launch_bytes / avg_s / 1e9, 3)})
+        ipc = scan_instr_per_cell()
+        if ipc:
+            # what the kernel as written issues: its VALU instructions per cell (PMC) times the
+            # live cell rate, against the chip's VALU issue ceiling -- the bound it runs into
+            issued = achieved * ipc
+            out["valu_issue"] = {"wave_instr_per_cell": ipc, "achieved": round(issued, 2),
+                                 "peak": VALU_WAVE_INSTR_PER_S / 1e9, "unit": "G wave64 VALU instr/s",
+                                 "frac": round(issued * 1e9 / VALU_WAVE_INSTR_PER_S, 4),
+                                 "cells_ceiling_Gcells": round(VALU_WAVE_INSTR_PER_S / 1e9 / ipc, 1),
+                                 "source": "profiles/r03/ext_pmc.json"}
     else:
         achieved = per_launch_bytes / avg_s / 1e9
         out.update({"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
