@@ -12,8 +12,10 @@ for r in $(seq 1 ${ROUNDS:-1}); do
   k=0
   for setting in "$@"; do
     k=$((k + 1))
+    T0=$(grep -E "nr_throttled|throttled_usec" /sys/fs/cgroup/cpu.stat 2>/dev/null | awk '{print $2}' | tr '\n' ' ')
     env $setting RSA_SINK_TRACE=$O/sink_${k}_$r.txt timeout -k 10 300 python bench.py --no-cpu-baseline --steps ${STEPS:-5} --warmup 2 > $O/b_${k}_$r.json 2> $O/b_${k}_$r.err || exit $?
-    echo "== [$k/$r] ${setting}"
+    T1=$(grep -E "nr_throttled|throttled_usec" /sys/fs/cgroup/cpu.stat 2>/dev/null | awk '{print $2}' | tr '\n' ' ')
+    echo "== [$k/$r] ${setting}   cgroup cpu.stat nr_throttled/throttled_usec before: $T0 after: $T1"
     python3 scripts/sink_report.py $O/sink_${k}_$r.txt $O/b_${k}_$r.json
   done
 done
