@@ -384,25 +384,44 @@ __device__ void ext_finish(const ExtJobDev& jb, const ScanRes& sr, const char* _
     for (int k = 0; k < nraw; ++k) {
         const uint32_t opk = raw[k] & 0xf, lenk = raw[k] >> 4;
         if (opk == 0) {
-            for (uint32_t z = 0; z < lenk; ++z) {
-                int rcode, qcode;
+            // the =/X split 32 bases at a time: a branch-free pass builds the chunk's mismatch
+            // mask (its LDS loads issue back to back), then its runs are emitted from the mask
+            // -- the same ops as comparing base by base
+            for (uint32_t z = 0; z < lenk; z += 32) {
+                const uint32_t cnt = lenk - z < 32 ? lenk - z : 32;
                 const int qo = qp - qs0, ro = rp - sr.ref_begin1;
-                if (qcs && qo >= 0 && qo <= sr.read_end1 - qs0 && ro >= 0 && ro <= sr.ref_end1 - sr.ref_begin1) {
-                    rcode = rcs[ro];
-                    qcode = qcs[qo];
+                uint32_t mm = 0;
+                if (qcs && qo >= 0 && qo + (int)cnt - 1 <= sr.read_end1 - qs0 && ro >= 0 &&
+                    ro + (int)cnt - 1 <= sr.ref_end1 - sr.ref_begin1) {
+#pragma unroll 8
+                    for (uint32_t b = 0; b < cnt; ++b) mm |= (uint32_t)(rcs[ro + b] != qcs[qo + b]) << b;
                 } else {
-                    rcode = (rp >= 0 && rp < rlen) ? ssw_code((unsigned char)r[rp]) : 4;
-                    qcode = ssw_code((unsigned char)q[qp]);
+                    for (uint32_t b = 0; b < cnt; ++b) {
+                        const int rr = rp + (int)b;
+                        const int rcode = (rr >= 0 && rr < rlen) ? ssw_code((unsigned char)r[rr]) : 4;
+                        const int qcode = ssw_code((unsigned char)q[qp + (int)b]);
+                        mm |= (uint32_t)(rcode != qcode) << b;
+                    }
                 }
-                if (rcode != qcode) {
-                    ++mism;
-                    if (in_m) core[n++] = cig(len_m, 7);
-                    len_m = 0; ++len_x; in_m = 0; in_x = 1;
-                } else {
-                    if (in_x) core[n++] = cig(len_x, 8);
-                    ++len_m; len_x = 0; in_m = 1; in_x = 0;
+                uint64_t m = mm;                            // 64-bit: a shift by 32 stays defined
+                uint32_t rem = cnt;
+                while (rem) {
+                    if (m & 1) {                            // a run of mismatches
+                        uint32_t run = (uint32_t)__builtin_ctzll(~m);
+                        run = run < rem ? run : rem;
+                        if (in_m) core[n++] = cig(len_m, 7);
+                        mism += (int)run;
+                        len_m = 0; len_x += run; in_m = 0; in_x = 1;
+                        m >>= run; rem -= run;
+                    } else {                                // a run of matches
+                        uint32_t run = m ? (uint32_t)__builtin_ctzll(m) : rem;
+                        run = run < rem ? run : rem;
+                        if (in_x) core[n++] = cig(len_x, 8);
+                        len_m += run; len_x = 0; in_m = 1; in_x = 0;
+                        m >>= run; rem -= run;
+                    }
                 }
-                ++rp; ++qp;
+                rp += (int)cnt; qp += (int)cnt;
             }
         } else if (opk == 1 || opk == 2) {
             const uint32_t rawk = raw[k];
