@@ -438,29 +438,51 @@ __device__ void ext_finish(const ExtJobDev& jb, const ScanRes& sr, const char* _
     const int tail = qlen - sr.read_end1 - 1;
     if (tail > 0) core[n++] = cig((uint32_t)tail, 4);
 
-    // Aligner::align end bonus (aligner.cpp:138-207)
+    // Aligner::align end bonus (aligner.cpp:138-207).  The scans over the clipped ends are
+    // sums (no early exit), so they run branch-free with their loads issued ahead, and the
+    // =/X ops of a taken end are pushed run by run from 32-base match masks.
+    auto end_scan = [&](const char* qa, const char* rb, uint32_t len, int& score, uint32_t& edits) {
+#pragma unroll 8
+        for (uint32_t i = 0; i < len; ++i) {
+            const bool eq = qa[i] == rb[i];
+            score += eq ? match : -mismatch;
+            edits += eq ? 0u : 1u;
+        }
+    };
+    auto push_eq_runs = [&](int& fn, const char* qa, const char* rb, uint32_t len) {
+        for (uint32_t z = 0; z < len; z += 32) {
+            const uint32_t cnt = len - z < 32 ? len - z : 32;
+            uint32_t eqm = 0;
+#pragma unroll 8
+            for (uint32_t b = 0; b < cnt; ++b) eqm |= (uint32_t)(qa[z + b] == rb[z + b]) << b;
+            uint64_t m = eqm;
+            uint32_t rem = cnt;
+            while (rem) {
+                const bool eq = m & 1;
+                uint32_t run = eq ? (uint32_t)__builtin_ctzll(~m) : (m ? (uint32_t)__builtin_ctzll(m) : rem);
+                run = run < rem ? run : rem;
+                cpush(c, fn, eq ? 7u : 8u, run);
+                m >>= run;
+                rem -= run;
+            }
+        }
+    };
     uint32_t ed = (uint32_t)mism;
     int sw = sr.score1;
     uint32_t rs = (uint32_t)sr.ref_begin1, re = (uint32_t)sr.ref_end1 + 1;
     uint32_t qs = (uint32_t)qs0, qe = (uint32_t)sr.read_end1 + 1;
     int final_n;
     {
-        uint32_t q0 = qs, r0 = rs;
+        const uint32_t steps = qs < rs ? qs : rs;      // while (q0 > 0 && r0 > 0)
+        const uint32_t q0 = qs - steps, r0 = rs - steps;
         int score = sw;
         uint32_t edits = ed;
-        while (q0 > 0 && r0 > 0) {
-            q0--; r0--;
-            if (q[q0] == r[r0]) score += match;
-            else { score -= mismatch; edits++; }
-        }
+        end_scan(q + q0, r + r0, steps, score, edits);
         if (q0 == 0 && score + bonus > sw) {
             if (qs > 0) {
                 // front ops in left-to-right order, then core without its leading S
                 int fn = 0;
-                for (uint32_t z = 0; z < qs; ++z) {
-                    const uint32_t qq = z, rr = rs - qs + z;
-                    cpush(c, fn, q[qq] == r[rr] ? 7u : 8u, 1);
-                }
+                push_eq_runs(fn, q, r + (rs - qs), qs);
                 for (int k = 1; k < n; ++k) cpush(c, fn, core[k] & 0xf, core[k] >> 4);
                 final_n = fn;
             } else {
@@ -474,19 +496,16 @@ __device__ void ext_finish(const ExtJobDev& jb, const ScanRes& sr, const char* _
         }
     }
     {
-        uint32_t q1 = qe, r1 = re;
+        const uint32_t qrem = (uint32_t)qlen - qe, rrem = (uint32_t)rlen - re;
+        const uint32_t steps = qrem < rrem ? qrem : rrem;   // while (q1 < qlen && r1 < rlen)
+        const uint32_t q1 = qe + steps, r1 = re + steps;
         int score = sw;
         uint32_t edits = ed;
-        while (q1 < (uint32_t)qlen && r1 < (uint32_t)rlen) {
-            if (q[q1] == r[r1]) score += match;
-            else { score -= mismatch; edits++; }
-            q1++; r1++;
-        }
+        end_scan(q + qe, r + re, steps, score, edits);
         if (q1 == (uint32_t)qlen && score + bonus > sw) {
             if (qe < (uint32_t)qlen) {
                 final_n--;   // drop trailing soft clip
-                for (uint32_t z = 0; z < (uint32_t)qlen - qe; ++z)
-                    cpush(c, final_n, q[qe + z] == r[re + z] ? 7u : 8u, 1);
+                push_eq_runs(final_n, q + qe, r + re, (uint32_t)qlen - qe);
             }
             qe = (uint32_t)qlen; re = r1; sw = score + bonus; ed = edits;
         }
