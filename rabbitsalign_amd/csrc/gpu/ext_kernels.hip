@@ -722,18 +722,49 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
     int line = width_d * 3 * (read_l - 1);
     uint32_t op = 0, prev_op = 0;
     bool fail = false;
-    while (i >= 0 && jx > 0) {
-        const int at = line + (jx - max(i - bw, 0)) * 3 + temp2;
-        if (at < 0 || at >= s2) { fail = true; break; }
-        const int dv = dir[at];
-        if (dv == 1) { --i; --jx; temp2 = 2; line -= width_d * 3; op = 0; }
-        else if (dv == 2) { --i; temp2 = 0; line -= width_d * 3; op = 1; }
-        else if (dv == 3) { --i; temp2 = 2; line -= width_d * 3; op = 1; }
+    const int W3 = width_d * 3;
+    // one traceback step from the direction byte dv at the current cell; false = failure
+    auto step = [&](int dv) -> bool {
+        if (dv == 1) { --i; --jx; temp2 = 2; line -= W3; op = 0; }
+        else if (dv == 2) { --i; temp2 = 0; line -= W3; op = 1; }
+        else if (dv == 3) { --i; temp2 = 2; line -= W3; op = 1; }
         else if (dv == 4) { --jx; temp2 = 1; op = 2; }
         else if (dv == 5) { --jx; temp2 = 2; op = 2; }
-        else { fail = true; break; }
+        else return false;
         if (op == prev_op) ++ecount;
         else { ++l; raw[l - 1] = cig((uint32_t)ecount, prev_op); prev_op = op; ecount = 1; }
+        return true;
+    };
+    // Each step's byte address depends on the byte before it, so the walk is a chain of LDS
+    // latencies.  From a cell entered with temp2 = 2, the next 8 cells along the diagonal
+    // are loaded together (the addresses a run of diagonal moves would visit) and consumed
+    // while the moves are diagonal; the first other move is taken from its byte as usual.
+    // The same cells and bytes as the one-step walk (ssw.c:748-776).
+    constexpr int TB_AHEAD = 8;
+    while (i >= 0 && jx > 0) {
+        if (temp2 == 2) {
+            int dvs[TB_AHEAD];
+#pragma unroll
+            for (int k = 0; k < TB_AHEAD; ++k) {
+                const int ik = i - k, jk = jx - k;
+                const int atk = line - k * W3 + (jk - max(ik - bw, 0)) * 3 + 2;
+                dvs[k] = (ik >= 0 && jk > 0 && atk >= 0 && atk < s2) ? (int)dir[atk] : 0;
+            }
+            bool more = true;
+#pragma unroll
+            for (int k = 0; k < TB_AHEAD; ++k) {
+                if (!more || !(i >= 0 && jx > 0)) { more = false; continue; }
+                const int at = line + (jx - max(i - bw, 0)) * 3 + 2;
+                if (at < 0 || at >= s2) { fail = true; more = false; continue; }
+                if (!step(dvs[k])) { fail = true; more = false; continue; }
+                if (dvs[k] != 1) more = false;             // left the diagonal: back to single steps
+            }
+            if (fail) break;
+            continue;
+        }
+        const int at = line + (jx - max(i - bw, 0)) * 3 + temp2;
+        if (at < 0 || at >= s2) { fail = true; break; }
+        if (!step(dir[at])) { fail = true; break; }
     }
     if (fail) {                                     // banded_sw failed -> flag 1 sentinel
         aln_sentinel(out, j, jb, -100000);
