@@ -620,6 +620,26 @@ __device__ __forceinline__ void aln_sentinel(rsa_aln* out, int j, const ExtJobDe
     out[j] = a;
 }
 
+// The direction matrix keeps the reference's byte layout for addressing (cell c of
+// band row i at byte 3 (width_d i + c), bytes [de, df, dh], SET_D in ssw.c), but LDS holds
+// one byte per cell: the band fill always writes a cell's three bytes together, so a
+// packed cell decodes to exactly the bytes the reference layout would hold there (an
+// unwritten cell, 0, to three zeros).  A third of the LDS lets k_ext_band16 keep three
+// times as many jobs resident.  Packed byte: bit 0 de - 2, bit 1 df - 4, bits 2-3 dh as
+// 1 (1), de (2), df (3).
+__device__ __forceinline__ int8_t dir_pack(int de, int df, int dh) {
+    const int dhc = dh == 1 ? 1 : (dh == de ? 2 : 3);
+    return (int8_t)((de - 2) | ((df - 4) << 1) | (dhc << 2));
+}
+// byte `sub` (0..2) of cell `cell`, i.e. reference byte 3 cell + sub
+__device__ __forceinline__ int dir_byte(const int8_t* dirp, int cell, int sub) {
+    const int v = (int)(uint8_t)dirp[cell];
+    if (v == 0) return 0;
+    const int de = 2 + (v & 1), df = 4 + ((v >> 1) & 1), dhc = (v >> 2) & 3;
+    return sub == 0 ? de : (sub == 1 ? df : (dhc == 1 ? 1 : (dhc == 2 ? de : df)));
+}
+template <int DIRCAP> struct DirCells { static constexpr int BYTES = ((DIRCAP + 2) / 3 + 15) & ~15; };
+
 // banded_sw + traceback + ext_finish of job j by a group of G lanes (z = lane in
 // group).  LDS: dir[DIRCAP], qc[QCAP], rc[RCAP].  Returns false when the job does
 // not fit the group (nothing written).  Lane z keeps the reference's h_b[z+1] and
@@ -649,7 +669,7 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
         const int gj = ref_begin + x;
         rc[x] = (uint8_t)((gj >= 0 && gj < rlen) ? ssw_code((unsigned char)r[gj]) : 4);
     }
-    for (int x = z * 16; x < DIRCAP; x += G * 16) *(int4*)(dir + x) = make_int4(0, 0, 0, 0);
+    for (int x = z * 16; x < DirCells<DIRCAP>::BYTES; x += G * 16) *(int4*)(dir + x) = make_int4(0, 0, 0, 0);
     WSYNC();
 
     const int len = ref_l > read_l ? ref_l : read_l;
@@ -697,8 +717,7 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
             const int H = m > diag ? m : diag;
             const int dh = m <= diag ? 1 : (e1 > f1 ? de : df);
             if (on) {
-                int8_t* dl = dir + width_d * 3 * i + 3 * z;
-                dl[0] = (int8_t)de; dl[1] = (int8_t)df; dl[2] = (int8_t)dh;
+                dir[width_d * i + z] = dir_pack(de, df, dh);
             }
             lmax = (on && H > lmax) ? H : lmax;
             EB = on ? E : EB;                            // h_b[1..u] = h_c[1..u]
@@ -720,14 +739,15 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
     uint32_t* raw = raw_pool + jb.cig_off;
     int i = read_l - 1, jx = ref_l - 1, ecount = 0, l = 0, temp2 = 2;
     int line = width_d * 3 * (read_l - 1);
+    int lineC = width_d * (read_l - 1);           // line / 3: the row's first cell
     uint32_t op = 0, prev_op = 0;
     bool fail = false;
     const int W3 = width_d * 3;
     // one traceback step from the direction byte dv at the current cell; false = failure
     auto step = [&](int dv) -> bool {
-        if (dv == 1) { --i; --jx; temp2 = 2; line -= W3; op = 0; }
-        else if (dv == 2) { --i; temp2 = 0; line -= W3; op = 1; }
-        else if (dv == 3) { --i; temp2 = 2; line -= W3; op = 1; }
+        if (dv == 1) { --i; --jx; temp2 = 2; line -= W3; lineC -= width_d; op = 0; }
+        else if (dv == 2) { --i; temp2 = 0; line -= W3; lineC -= width_d; op = 1; }
+        else if (dv == 3) { --i; temp2 = 2; line -= W3; lineC -= width_d; op = 1; }
         else if (dv == 4) { --jx; temp2 = 1; op = 2; }
         else if (dv == 5) { --jx; temp2 = 2; op = 2; }
         else return false;
@@ -747,8 +767,9 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
 #pragma unroll
             for (int k = 0; k < TB_AHEAD; ++k) {
                 const int ik = i - k, jk = jx - k;
-                const int atk = line - k * W3 + (jk - max(ik - bw, 0)) * 3 + 2;
-                dvs[k] = (ik >= 0 && jk > 0 && atk >= 0 && atk < s2) ? (int)dir[atk] : 0;
+                const int ck = lineC - k * width_d + (jk - max(ik - bw, 0));
+                const int atk = 3 * ck + 2;
+                dvs[k] = (ik >= 0 && jk > 0 && atk >= 0 && atk < s2) ? dir_byte(dir, ck, 2) : 0;
             }
             bool more = true;
 #pragma unroll
@@ -762,9 +783,10 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
             if (fail) break;
             continue;
         }
-        const int at = line + (jx - max(i - bw, 0)) * 3 + temp2;
+        const int cell = lineC + (jx - max(i - bw, 0));
+        const int at = 3 * cell + temp2;                   // = line + (jx - max(i - bw, 0)) * 3 + temp2
         if (at < 0 || at >= s2) { fail = true; break; }
-        if (!step(dir[at])) { fail = true; break; }
+        if (!step(dir_byte(dir, cell, temp2))) { fail = true; break; }
     }
     if (fail) {                                     // banded_sw failed -> flag 1 sentinel
         aln_sentinel(out, j, jb, -100000);
@@ -787,7 +809,7 @@ k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
              const char* __restrict__ qbuf, const char* __restrict__ ref, uint32_t* __restrict__ cig_pool,
              uint32_t* __restrict__ raw_pool, rsa_aln* __restrict__ out, int match, int mismatch, int gO, int gE,
              int bonus, int* __restrict__ queue, int* __restrict__ qcount, int* __restrict__ overflow) {
-    __shared__ __attribute__((aligned(16))) int8_t s_dir[B16_GROUPS][B16_DIRCAP];
+    __shared__ __attribute__((aligned(16))) int8_t s_dir[B16_GROUPS][DirCells<B16_DIRCAP>::BYTES];
     __shared__ uint8_t s_qc[B16_GROUPS][B16_SEGCAP];
     __shared__ uint8_t s_rc[B16_GROUPS][B16_SEGCAP];
     const int lane = threadIdx.x & 63, g = lane >> 4, z = lane & 15;
@@ -827,7 +849,7 @@ k_ext_band64(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
              rsa_aln* __restrict__ out, int match, int mismatch, int gO, int gE, int bonus,
              const int* __restrict__ queue, const int* __restrict__ qcount, int* __restrict__ overflow,
              int* __restrict__ ocount) {
-    __shared__ __attribute__((aligned(16))) int8_t s_dir[B64_DIRCAP];
+    __shared__ __attribute__((aligned(16))) int8_t s_dir[DirCells<B64_DIRCAP>::BYTES];
     __shared__ uint8_t s_qc[B64_QCAP];
     __shared__ uint8_t s_rc[B64_RCAP];
     const int z = threadIdx.x & 63;
