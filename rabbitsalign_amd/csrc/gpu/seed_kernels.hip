@@ -1435,22 +1435,24 @@ k_rescue_big(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __rest
 // into ooff[0..n] and the total into the header, plus the call's statistics
 // summed over the reads (LDS atomics, one global write each: k_lookup's 20 k
 // waves adding to one address serialised).  One workgroup walks the reads in
-// tiles of 4096, each thread 4 consecutive reads whose loads all issue before
+// tiles of 4096, each thread 16 consecutive reads whose loads all issue before
 // the tile's scan (a thread walking a private run of reads waited on one
 // dependent load per read: 142 us a call).
 #define SEED_NSTAT 13
-#define SS_PER 4
-__global__ void __launch_bounds__(1024)
+#define SS_TPB 256           // one workgroup of 4 waves: it finds a CU sooner on a busy GPU than 16 waves did
+#define SS_PER 16            // reads a thread takes per tile (tiles of SS_TPB * SS_PER = 4096 reads)
+#define SS_WAVES (SS_TPB / 64)
+__global__ void __launch_bounds__(SS_TPB)
 k_seed_scan(int n_reads, const uint8_t* __restrict__ rescued, const uint32_t* __restrict__ ncnt1,
             const uint32_t* __restrict__ ncnt2, const uint32_t* __restrict__ qcnt, const ReadStat* __restrict__ st,
             uint64_t* __restrict__ ooff, SeedHdr* __restrict__ hdr) {
-    __shared__ uint64_t s_w[16];
+    __shared__ uint64_t s_w[SS_WAVES];
     __shared__ unsigned long long s_stat[SEED_NSTAT];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     if (t < SEED_NSTAT) s_stat[t] = 0;
     uint64_t v[SEED_NSTAT] = {0};    // qrs found good hits_find hits_all scan_find scan_all n1 n2 rr rq rscan rhits
     uint64_t carry = 0;
-    for (int base = 0; base < n_reads; base += 1024 * SS_PER) {
+    for (int base = 0; base < n_reads; base += SS_TPB * SS_PER) {
         const int r0 = base + t * SS_PER;
         uint32_t cnt[SS_PER];
         uint64_t mine = 0;
@@ -1478,7 +1480,7 @@ k_seed_scan(int n_reads, const uint8_t* __restrict__ rescued, const uint32_t* __
         __syncthreads();
         uint64_t wpre = 0, tot = 0;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
+        for (int j = 0; j < SS_WAVES; ++j) {
             const uint64_t sj = s_w[j];
             wpre += j < w ? sj : 0;
             tot += sj;
@@ -2019,7 +2021,7 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
         kt.end(st);
         // 5. final offsets and the NAM lists back to back
         kt.begin(st, RSA_K_COMPACT);
-        hipLaunchKernelGGL(k_seed_scan, dim3(1), dim3(1024), 0, st, (int)n, d_resc, DP(B_NCNT1, uint32_t),
+        hipLaunchKernelGGL(k_seed_scan, dim3(1), dim3(SS_TPB), 0, st, (int)n, d_resc, DP(B_NCNT1, uint32_t),
                            DP(B_NCNT2, uint32_t), DP(B_QCNT, uint32_t), DP(B_ST, ReadStat), d_ooff, dhdr);
         hipLaunchKernelGGL(k_compact, dim3(n), dim3(64), 0, st, (int)n, DP(B_NSRC, uint64_t), DP(B_RBASE, uint64_t),
                            slots, DP(B_NCNT1, uint32_t), DP(B_NCNT2, uint32_t), d_resc, DP(B_ARENA, rsa_nam), d_ooff,
