@@ -15,10 +15,13 @@
 
 #include "rsa_host.hpp"
 
-// per-thread pairing scratch: initial-exec TLS (one %fs-relative access instead of
-// a __tls_get_addr call per use; the whole block is a few hundred bytes of the
-// static TLS surplus glibc keeps for dlopen'ed libraries)
-#define RSA_TLS thread_local __attribute__((tls_model("initial-exec")))
+// per-thread pairing scratch.  Dynamic TLS, never initial-exec: librsalign.so is
+// dlopen'ed by FFI hosts (ctypes, torch processes) whose static-TLS surplus may
+// already be spent, and initial-exec TLS in a dlopen'ed object fails to load then
+// ("cannot allocate memory in static TLS block").  The library is built with TLS
+// descriptors (-mtls-dialect=gnu2), so an access after the first is a short
+// call that reads the thread's DTV, not a __tls_get_addr lookup.
+#define RSA_TLS thread_local
 
 namespace rsa {
 
