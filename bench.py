@@ -16,7 +16,10 @@ reported beside it.
 N>1: one process per GPU under torch.distributed.run; every rank holds the
 replicated index and maps its own shard of pairs (no data-path collective);
 the wall time is the max over ranks and the read count the sum ("weak").
-rank 0 prints one JSON line.  The cpu_baseline leg (rank 0, N=1) maps a
+rank 0 prints one JSON line.  `python3 bench.py --gpus N` without WORLD_SIZE
+starts the N ranks itself (rabbitsalign_amd/launch.py; the launcher never
+touches the GPU), then runs the product's one-process multi-device path
+(rsam_add_devices, one SAM file) and adds it to the line as `multi_device`.  The cpu_baseline leg (rank 0, N=1) maps a
 bounded sample of the same workload with oracle/_ref/librsalign_ref.so (the
 reference's own seeding + SSW code inside the same host pipeline) and checks
 that its SAM hash equals the GPU path's on that sample.
@@ -311,6 +314,114 @@ def kernel_table(ks: dict) -> dict:
     return out
 
 
+def self_launch(args) -> int:
+    """--gpus N > 1 without WORLD_SIZE: start N ranks (torch.distributed.run, one process
+    per GPU), relay rank 0's line, then run the product's one-process multi-device leg
+    and report it beside the per-rank weak-scaling value."""
+    from rabbitsalign_amd import launch
+    me = os.path.abspath(__file__)
+    n_vis = launch.visible_gpus()
+    if n_vis < args.gpus:
+        log(0, f"error: {args.gpus} GPUs requested, {n_vis} visible; nothing was run")
+        return 2
+    log(0, f"launching {args.gpus} ranks (torch.distributed.run, one process per GPU)")
+    argv = sys.argv[1:]
+    rc, line = launch.run_ranks(me, argv, args.gpus)
+    if rc != 0 or line is None:
+        log(0, f"error: the ranks exited with {rc}" + ("" if line else " and printed no result line"))
+        return rc or 1
+    if not args.no_multi_device:
+        log(0, f"multi-device leg: one process, rsam_add_devices over {args.gpus} GPUs, one SAM file")
+        rc2, md = launch.run_child([sys.executable, me, "--multi-device-leg", *argv])
+        line["multi_device"] = (md or {}).get("multi_device") if rc2 == 0 and md else \
+            {"error": f"multi-device leg exited with {rc2}"}
+    print(json.dumps(line), flush=True)
+    return 0
+
+
+def multi_device_leg(args) -> int:
+    """The product's own multi-GPU path (rsalign --devices 0..N-1 / rsam_add_devices): one
+    process, one chunk queue, one engine per GPU (index replica each), ONE ordered SAM
+    file.  Each step maps N x --pairs pairs (the same per-GPU work as the rank leg) from
+    FASTQ files to one SAM file.  Prints {"multi_device": {...}}."""
+    wl = dict(WORKLOADS[args.workload])
+    if args.ref_len:
+        wl["ref_len"] = args.ref_len
+    env_dev = os.environ.get("RSA_BENCH_DEVICES")           # e.g. "0,0": rehearse on one GPU
+    devices = [int(x) for x in env_dev.split(",")] if env_dev else list(range(args.gpus))
+    cores = host_cores(False)
+    threads = args.threads or min(16 * len(devices), cores)
+    import torch
+    from rabbitsalign_amd import mapper as M
+    M.load()
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU (the product path has no CPU fallback)")
+    t = time.time()
+    m = M.Mapper.synthetic(args.ref_seed, wl["ref_len"], wl["n_contigs"], wl["read_len"], device=devices[0],
+                           threads=threads)
+    t_idx = time.time() - t
+    t = time.time()
+    m.add_devices(devices[1:])
+    t_add = time.time() - t
+    log(0, f"multi-device: index on device {devices[0]} in {t_idx:.1f} s, replicated to {devices[1:]} in "
+           f"{t_add:.1f} s; engine {m.engine}; {threads} pipeline threads of {cores} cores")
+    P = args.pairs * len(devices)
+    reads = m.synthetic_reads(args.read_seed, 0, P, wl["read_len"], wl["mu"], wl["sigma"], wl["paired"])
+    per_pair = (2 if wl["paired"] else 1)
+    io_dir = pick_io_dir(args.io_dir, P * per_pair * (2 * wl["read_len"] + 80) * 2
+                         + 2 * P * per_pair * (2 * wl["read_len"] + 120))
+    tag = f"rsa_bench_md_{os.getpid()}"
+    f1 = os.path.join(io_dir, f"{tag}_1.fq")
+    f2 = os.path.join(io_dir, f"{tag}_2.fq") if wl["paired"] else None
+    reads.write_fastq(f1, f2)
+    reads.close()
+    steps = max(1, args.md_steps)
+    warm = os.path.join(io_dir, f"{tag}_warm.sam")
+    sam = os.path.join(io_dir, f"{tag}_step.sam")
+    out = {}
+    try:
+        w = m.map_files(f1, f2, threads=threads, chunk_size=args.chunk_size, sam_path=warm)
+        log(0, f"multi-device warmup: {w.n_reads} reads in {w.map_seconds:.3f} s")
+        warm_hash = file_xxh64(warm)
+        m.set_sam_digest(False)
+        m.reset_kernel_stats()
+        walls, n_reads, identical = [], 0, True
+        ru0 = resource.getrusage(resource.RUSAGE_SELF)
+        for s in range(steps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            st = m.map_files(f1, f2, threads=threads, chunk_size=args.chunk_size, sam_path=sam)
+            walls.append(time.perf_counter() - t0)
+            n_reads += st.n_reads
+            log(0, f"multi-device step {s}: {st.n_reads} reads in {walls[-1]:.3f} s "
+                   f"({st.n_reads / walls[-1] / 1e6:.3f} Mreads/s)")
+            identical = identical and file_xxh64(sam) == warm_hash      # untimed
+            os.remove(sam)
+        ru1 = resource.getrusage(resource.RUSAGE_SELF)
+        ks = m.kernel_stats()
+        elapsed = sum(walls)
+        cpu_s = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+        out = {"value": round(n_reads / elapsed / 1e6, 6), "unit": "Mreads/s", "devices": devices,
+               "steps": steps, "ms_per_step": round(1e3 * elapsed / steps, 3), "pairs_per_step": P,
+               "sam_file_bytes_per_step": w.sam_bytes,
+               "sam_write_GBps": round(w.sam_bytes * steps / elapsed / 1e9, 3),
+               "host_threads": threads, "host_cores": cores,
+               "core_us_per_read": round(1e6 * cpu_s / max(1, n_reads), 4),
+               "timed_files_identical_to_warmup": identical,
+               "engine": m.engine, "index_replicate_seconds": round(t_add, 3),
+               "calls": {"seed": ks.get("seed_calls"), "extend": ks.get("ext_calls")},
+               "note": "product path: one process, rsam_add_devices (csrc/host/multi.cpp), one chunk queue, "
+                       "one ordered SAM file; FASTQ files -> SAM file, timed per step from the call to the "
+                       "last SAM byte (steps run back to back; each step's SAM file checked untimed)"}
+    finally:
+        for f in (f1, f2, warm, sam):
+            if f and os.path.exists(f):
+                os.remove(f)
+        m.close()
+    print(json.dumps({"multi_device": out}), flush=True)
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -334,7 +445,18 @@ def main():
                     help="distinct synthetic read sets (FASTQ file pairs) rotated over the steps")
     ap.add_argument("--ref-len", type=int, default=0, help="override reference length (testing only)")
     ap.add_argument("--stats-out", default="", help="write per-kernel stats JSON here")
+    ap.add_argument("--no-multi-device", action="store_true",
+                    help="N>1: skip the product's one-process multi-device leg (one SAM file over N GPUs)")
+    ap.add_argument("--md-steps", type=int, default=3, help="timed steps of the multi-device leg")
+    ap.add_argument("--multi-device-leg", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+
+    if args.multi_device_leg:
+        return multi_device_leg(args)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python3 bench.py --gpus N` (the driver's form): this process is the launcher,
+        # not a rank, and never initialises the GPU
+        raise SystemExit(self_launch(args))
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -382,7 +504,9 @@ def main():
     P = args.pairs
     total_steps = args.warmup + args.steps
     # distinct read sets, rotated over the steps (each step maps one whole set)
-    n_sets = max(1, min(total_steps, args.read_sets))
+    # at most one read set per warm-up step, so every set has a warm-up SAM digest the timed
+    # steps and the in-memory leg are compared with
+    n_sets = max(1, min(total_steps, args.read_sets, args.warmup))
     batches = []
     t = time.time()
     for s in range(n_sets):
@@ -504,8 +628,11 @@ def main():
     in_memory = {"value": round(mem_tot["n_reads"] / mem_elapsed_max / 1e6, 6), "unit": "Mreads/s",
                  "ms_per_step": round(1e3 * mem_elapsed_max / args.steps, 3),
                  "core_us_per_read": round(1e6 * mem_cpu_s / max(1, mem_reads), 4),
-                 # steps whose read set had a warm-up step (its digest is the headline's reference)
-                 "sam_identical_to_headline": all(mh == h for mh, h in zip(mem_hashes, hashes) if h),
+                 # steps whose read set had a warm-up step (its digest is the headline's reference);
+                 # None when no step could be compared
+                 "sam_identical_to_headline": (all(mh == h for mh, h in zip(mem_hashes, hashes) if h)
+                                               if any(hashes) else None),
+                 "sam_compared_steps": sum(1 for h in hashes if h),
                  "note": "the same read sets held in host RAM (rsam_map), SAM text kept in memory"}
     log(rank, f"in-memory leg: {in_memory['value']} Mreads/s, {in_memory['core_us_per_read']} core-us a read")
     for b in batches:
@@ -564,7 +691,10 @@ def main():
             else f"Mreads/s aligned ({args.workload})",
             "value": round(value, 6), "unit": "Mreads/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed_max / args.steps, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            # the DP's arithmetic: exact small integers in packed f16 (forward scan) and int32
+            # (reverse pass, band traceback); hashing and lookups in 64-bit integers
+            "dtype": "int32+f16x2(exact int)",
             "data": "synthetic (seeded reference + reads, SURVEY.md Appendix D)",
             "config": {"workload": wl["desc"], "reference_bp": wl["ref_len"], "contigs": wl["n_contigs"],
                        "read_len": wl["read_len"], "paired": wl["paired"], "pairs_per_step_per_gpu": P,
@@ -595,6 +725,7 @@ def main():
             "mapping_stats_all_ranks": totals_all,
             "sam_hashes": [f"{h:016x}" for h in hashes],
             "sam_check": {"timed_files_identical_to_warmup": timed_files_identical,
+                          "compared_steps": len(checked),
                           "note": "timed steps run without the SAM digest (rsam_set_sam_digest 0: a mapping run "
                                   "computes none); each timed step's SAM file is compared (xxh64 of the file, "
                                   "untimed) with the warm-up file of the same read set, whose digest is the one "
@@ -610,4 +741,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)
