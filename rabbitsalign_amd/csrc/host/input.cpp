@@ -22,6 +22,7 @@
 #include <emmintrin.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <exception>
 #include <map>
@@ -232,154 +233,213 @@ struct Block {
 // asks the kernel to map the next window of the file in one call
 // (MADV_POPULATE_READ) instead of taking a page fault every few pages, and the
 // pages of blocks whose chunks are done leave the process again in 64 MB steps.
+//
+// The reader's state is shared with its thread: a FileBlocks given up before the
+// end of its input (a mapping error) stops the reader, and a reader that does not
+// stop within kStopWait -- blocked in a read of a pipe or a terminal whose writer
+// has stalled -- is detached with the state it holds, so the error path never
+// waits on a slow producer.
 class FileBlocks {
-public:
-    FileBlocks(const std::string& path, size_t per_block, size_t ahead)
-        : path_(path), per_block_(std::max<size_t>(1, per_block)), ahead_(std::max<size_t>(1, ahead)) {
-        if (!mf_.open_map(path_)) {
-            mf_.reset();
-            seq_.reset(new FastxReader(path_));   // throws when the file cannot be opened
+    struct State {
+        std::string path;
+        size_t per_block, ahead;
+        MappedFile mf;
+        size_t pos = 0;                             // mapped mode: next record's offset
+        size_t populated = 0;                       // mapped bytes already in the page table
+        std::unique_ptr<FastxReader> seq;           // sequential mode
+        std::mutex m;
+        std::condition_variable cv;
+        std::map<size_t, Block> blocks;
+        size_t produced = 0, horizon = 0;
+        bool finished = false, stop = false, exited = false, cancelled = false;
+        std::exception_ptr err;
+        std::vector<uint8_t> released;              // per produced block: its chunk is done
+        std::vector<size_t> ends;                   // per produced block: mapped offset it ends at
+        size_t prefix = 0, dropped = 0;
+
+        void run() {
+            if (g_worker_start_hook) g_worker_start_hook();
+            try {
+                for (;;) {
+                    {
+                        std::unique_lock<std::mutex> g(m);
+                        cv.wait(g, [&] { return stop || produced < horizon + ahead; });
+                        if (stop) break;
+                    }
+                    Block b;
+                    const size_t end_off = read_block(b);
+                    std::lock_guard<std::mutex> g(m);
+                    if (b.recs.empty()) {
+                        finished = true;
+                        break;
+                    }
+                    released.push_back(0);
+                    ends.push_back(end_off);
+                    blocks.emplace(produced++, std::move(b));
+                    cv.notify_all();
+                }
+            } catch (...) {
+                std::lock_guard<std::mutex> g(m);
+                err = std::current_exception();
+            }
+            std::lock_guard<std::mutex> g(m);
+            exited = true;
+            cv.notify_all();
         }
-        th_ = std::thread([this] { run(); });
+        // the mapped bytes from `pos` on are in this process's page table at least `want` ahead
+        void populate(size_t want) {
+#ifdef MADV_POPULATE_READ
+            constexpr size_t kStep = 32u << 20;
+            if (populated >= mf.n || populated >= pos + want) return;
+            const size_t from = std::max(populated, pos) & ~(size_t)4095;
+            const size_t to = std::min(mf.n, from + kStep);
+            if (madvise((void*)(mf.p + from), to - from, MADV_POPULATE_READ) != 0) populated = mf.n;   // not supported
+            else populated = to;
+#else
+            (void)want;
+#endif
+        }
+        // returns the mapped offset the block ends at (0 in sequential mode)
+        size_t read_block(Block& b) {
+            b.recs.reserve(per_block);
+            if (!seq) {
+                populate(16u << 20);
+                const char* end = mf.p + mf.n;
+                const char* p = mf.p + pos;
+                NlIter it(p, end);
+                RecView r;
+                while (b.recs.size() < per_block && p < end) {
+                    const NlIter save = it;
+                    const char* at = p;
+                    if (!plain_record(p, end, it, r)) {
+                        it = save;
+                        p = at;
+                        break;
+                    }
+                    b.recs.push_back(r);
+                }
+                pos = (size_t)(p - mf.p);
+                if (b.recs.size() == per_block || p >= end) return pos;
+                // not the plain layout from here on: kseq over the rest of the mapped bytes
+                seq.reset(new FastxReader(p, (size_t)(end - p)));
+            }
+            const size_t want = per_block - b.recs.size();
+            b.owned.reserve(want);
+            Record r;
+            while (b.owned.size() < want && seq->next(r)) {
+                b.owned.push_back(std::move(r));
+                r = Record();
+            }
+            for (const Record& x : b.owned) b.recs.push_back(RecView(x));
+            return pos;
+        }
+    };
+
+public:
+    FileBlocks(const std::string& path, size_t per_block, size_t ahead) : st_(std::make_shared<State>()) {
+        State& s = *st_;
+        s.path = path;
+        s.per_block = std::max<size_t>(1, per_block);
+        s.ahead = std::max<size_t>(1, ahead);
+        if (!s.mf.open_map(s.path)) {
+            s.mf.reset();
+            s.seq.reset(new FastxReader(s.path));   // throws when the file cannot be opened
+        }
+        std::shared_ptr<State> keep = st_;
+        th_ = std::thread([keep] { keep->run(); });
     }
     ~FileBlocks() {
-        {
-            std::lock_guard<std::mutex> g(m_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        th_.join();
+        static constexpr auto kStopWait = std::chrono::seconds(2);
+        State& s = *st_;
+        std::unique_lock<std::mutex> g(s.m);
+        s.stop = true;
+        s.cv.notify_all();
+        const bool out = s.cv.wait_for(g, kStopWait, [&] { return s.exited; });
+        g.unlock();
+        if (out) th_.join();
+        else th_.detach();                       // the thread keeps the state alive
     }
     // block idx, waiting for the reader; false past the end of the file
     bool take(size_t idx, Block& out) {
-        std::unique_lock<std::mutex> g(m_);
-        if (idx + 1 > horizon_) {
-            horizon_ = idx + 1;
-            cv_.notify_all();
+        State& s = *st_;
+        std::unique_lock<std::mutex> g(s.m);
+        if (idx + 1 > s.horizon) {
+            s.horizon = idx + 1;
+            s.cv.notify_all();
         }
-        cv_.wait(g, [&] { return err_ || blocks_.count(idx) || (finished_ && idx >= produced_); });
-        if (err_) std::rethrow_exception(err_);
-        auto it = blocks_.find(idx);
-        if (it == blocks_.end()) return false;
+        s.cv.wait(g, [&] {
+            return s.err || s.cancelled || s.blocks.count(idx) || (s.finished && idx >= s.produced);
+        });
+        if (s.err) std::rethrow_exception(s.err);
+        auto it = s.blocks.find(idx);
+        if (it == s.blocks.end()) {
+            if (s.finished) return false;
+            throw std::runtime_error("input of " + s.path + " abandoned after an earlier failure");
+        }
         out = std::move(it->second);
-        blocks_.erase(it);
+        s.blocks.erase(it);
         return true;
+    }
+    // the summed sequence length of the file's first `n` records (fewer at the end of
+    // the file) and their count, before any block is taken: the records stay queued
+    // for the pipeline, so a stream is read once (readlen.cpp:16-29 over the same
+    // records the first chunk maps, as the reference's RewindableFile replays them)
+    void peek_lengths(size_t n, uint64_t& tot, uint64_t& num) {
+        State& s = *st_;
+        std::unique_lock<std::mutex> g(s.m);
+        for (;;) {
+            tot = num = 0;
+            for (size_t b = 0; b < s.produced && num < n; ++b) {
+                auto it = s.blocks.find(b);
+                if (it == s.blocks.end()) throw std::logic_error("read-length estimate after mapping started");
+                for (const RecView& r : it->second.recs) {
+                    if (num == n) break;
+                    tot += r.seq.size();
+                    num++;
+                }
+            }
+            if (num >= n) return;
+            if (s.err) std::rethrow_exception(s.err);
+            if (s.finished) return;
+            if (s.produced + 1 > s.horizon) {             // let the reader go past its lookahead
+                s.horizon = s.produced + 1;
+                s.cv.notify_all();
+            }
+            const size_t seen = s.produced;
+            s.cv.wait(g, [&] { return s.err || s.finished || s.produced > seen; });
+        }
+    }
+    void cancel() {
+        std::lock_guard<std::mutex> g(st_->m);
+        st_->cancelled = true;
+        st_->cv.notify_all();
     }
     // block idx is no longer used: once every block before it is done too, the
     // mapped bytes up to its end are dropped from this process (64 MB at a time;
     // the file stays mapped, and the page cache keeps the data)
     void done(size_t idx) {
-        if (!mf_.p) return;
+        State& s = *st_;
+        if (!s.mf.p) return;
         static const bool keep = getenv("RSA_INPUT_DROP") && getenv("RSA_INPUT_DROP")[0] == '0';   // A/B
         size_t from = 0, to = 0;
         {
-            std::lock_guard<std::mutex> g(m_);
-            if (idx >= released_.size()) return;
-            released_[idx] = 1;
-            while (prefix_ < released_.size() && released_[prefix_]) prefix_++;
-            if (prefix_ == 0 || keep) return;
-            const size_t off = ends_[prefix_ - 1] & ~(size_t)4095;
-            if (off < dropped_ + (64u << 20)) return;
-            from = dropped_;
+            std::lock_guard<std::mutex> g(s.m);
+            if (idx >= s.released.size()) return;
+            s.released[idx] = 1;
+            while (s.prefix < s.released.size() && s.released[s.prefix]) s.prefix++;
+            if (s.prefix == 0 || keep) return;
+            const size_t off = s.ends[s.prefix - 1] & ~(size_t)4095;
+            if (off < s.dropped + (64u << 20)) return;
+            from = s.dropped;
             to = off;
-            dropped_ = off;
+            s.dropped = off;
         }
-        madvise((void*)(mf_.p + from), to - from, MADV_DONTNEED);
+        madvise((void*)(s.mf.p + from), to - from, MADV_DONTNEED);
     }
 
 private:
-    void run() {
-        if (g_worker_start_hook) g_worker_start_hook();
-        try {
-            for (;;) {
-                {
-                    std::unique_lock<std::mutex> g(m_);
-                    cv_.wait(g, [&] { return stop_ || produced_ < horizon_ + ahead_; });
-                    if (stop_) return;
-                }
-                Block b;
-                const size_t end_off = read_block(b);
-                std::lock_guard<std::mutex> g(m_);
-                if (b.recs.empty()) {
-                    finished_ = true;
-                    cv_.notify_all();
-                    return;
-                }
-                released_.push_back(0);
-                ends_.push_back(end_off);
-                blocks_.emplace(produced_++, std::move(b));
-                cv_.notify_all();
-            }
-        } catch (...) {
-            std::lock_guard<std::mutex> g(m_);
-            err_ = std::current_exception();
-            cv_.notify_all();
-        }
-    }
-    // the mapped bytes from `pos_` on are in this process's page table at least `want` ahead
-    void populate(size_t want) {
-#ifdef MADV_POPULATE_READ
-        constexpr size_t kStep = 32u << 20;
-        if (populated_ >= mf_.n || populated_ >= pos_ + want) return;
-        const size_t from = std::max(populated_, pos_) & ~(size_t)4095;
-        const size_t to = std::min(mf_.n, from + kStep);
-        if (madvise((void*)(mf_.p + from), to - from, MADV_POPULATE_READ) != 0) populated_ = mf_.n;   // not supported
-        else populated_ = to;
-#else
-        (void)want;
-#endif
-    }
-    // returns the mapped offset the block ends at (0 in sequential mode)
-    size_t read_block(Block& b) {
-        b.recs.reserve(per_block_);
-        if (!seq_) {
-            populate(16u << 20);
-            const char* end = mf_.p + mf_.n;
-            const char* p = mf_.p + pos_;
-            NlIter it(p, end);
-            RecView r;
-            while (b.recs.size() < per_block_ && p < end) {
-                const NlIter save = it;
-                const char* at = p;
-                if (!plain_record(p, end, it, r)) {
-                    it = save;
-                    p = at;
-                    break;
-                }
-                b.recs.push_back(r);
-            }
-            pos_ = (size_t)(p - mf_.p);
-            if (b.recs.size() == per_block_ || p >= end) return pos_;
-            // not the plain layout from here on: kseq over the rest of the mapped bytes
-            seq_.reset(new FastxReader(p, (size_t)(end - p)));
-        }
-        const size_t want = per_block_ - b.recs.size();
-        b.owned.reserve(want);
-        Record r;
-        while (b.owned.size() < want && seq_->next(r)) {
-            b.owned.push_back(std::move(r));
-            r = Record();
-        }
-        for (const Record& x : b.owned) b.recs.push_back(RecView(x));
-        return pos_;
-    }
-
-    std::string path_;
-    size_t per_block_, ahead_;
-    MappedFile mf_;
-    size_t pos_ = 0;                            // mapped mode: next record's offset
-    size_t populated_ = 0;                      // mapped bytes already in the page table
-    std::unique_ptr<FastxReader> seq_;          // sequential mode
+    std::shared_ptr<State> st_;
     std::thread th_;
-    std::mutex m_;
-    std::condition_variable cv_;
-    std::map<size_t, Block> blocks_;
-    size_t produced_ = 0, horizon_ = 0;
-    bool finished_ = false, stop_ = false;
-    std::exception_ptr err_;
-    std::vector<uint8_t> released_;             // per produced block: its chunk is done
-    std::vector<size_t> ends_;                  // per produced block: mapped offset it ends at
-    size_t prefix_ = 0, dropped_ = 0;
 };
 
 class FastqSource final : public ReadSource {
@@ -422,6 +482,20 @@ public:
         if (f2_) f2_->done(c.index);
         c.clear();
     }
+    // readlen.cpp:16-29 over InputBuffer::read_records(.., 500) (pc.cpp:74-107): the
+    // first 500 records of each file, or the first 1000 records of an interleaved
+    // file; 150 when the first file has none
+    void cancel() override {
+        f1_->cancel();
+        if (f2_) f2_->cancel();
+    }
+    int estimate_read_length() override {
+        uint64_t tot1 = 0, n1 = 0, tot2 = 0, n2 = 0;
+        f1_->peek_lengths(interleaved_ ? 1000 : 500, tot1, n1);
+        if (n1 == 0) return 150;
+        if (f2_) f2_->peek_lengths(500, tot2, n2);
+        return (int)((tot1 + tot2) / (n1 + n2));
+    }
 
 private:
     bool interleaved_;
@@ -442,19 +516,6 @@ std::unique_ptr<ReadSource> make_interleaved_vector_source(const std::vector<Rec
 std::unique_ptr<ReadSource> open_fastq_source(const std::string& path1, const std::string& path2, bool interleaved,
                                               size_t chunk_size) {
     return std::unique_ptr<ReadSource>(new FastqSource(path1, path2, interleaved, chunk_size));
-}
-
-int estimate_read_length(const std::string& path1, const std::string& path2, bool interleaved) {
-    if (path1 == "-" || path2 == "-") return 150;   // a stream cannot be read twice: the default profile
-    uint64_t tot = 0, num = 0;
-    auto scan = [&](const std::string& p, size_t want) {
-        FastxReader in(p);
-        Record r;
-        for (size_t i = 0; i < want && in.next(r); ++i) { tot += r.seq.size(); num++; }
-    };
-    scan(path1, interleaved ? 1000 : 500);
-    if (!path2.empty()) scan(path2, 500);
-    return num ? (int)(tot / num) : 150;
 }
 
 }  // namespace rsa

@@ -118,9 +118,17 @@ int cli_main(int argc, char** argv, EngineFactory factory, const char* prog) {
         if (o.c != INT32_MIN && (o.c >= 64 || o.c <= 0)) throw std::runtime_error("c must be greater than 0 and less than 64");
         if (o.interleaved && !o.reads2.empty())        // main.cpp:136-139
             throw std::runtime_error("Cannot specify both --interleaved and specify two read files");
-        // read length (main.cpp:254-258, readlen.cpp:16-29: average over the first read_records(500):
-        // 500 records of each file, or the first 1000 records of an interleaved file)
-        if (!o.reads1.empty() && !index_cmd && !o.r_set) o.r = estimate_read_length(o.reads1, o.reads2, o.interleaved);
+        // the reads are streamed: a reader thread per file parses chunks while the
+        // workers map (InputBuffer::read_records, pc.cpp:74-107).  The source opens
+        // first: the read-length estimate (main.cpp:254-258, readlen.cpp:16-29: the
+        // first read_records(500), i.e. 500 records of each file or 1000 of an
+        // interleaved file) is taken from the records it has parsed, which stay queued
+        // for mapping -- a pipe or stdin is read once, as the reference's
+        // RewindableFile replays what the estimate read (fastq.cpp:1-65)
+        std::unique_ptr<ReadSource> src;
+        if (!o.reads1.empty() && !index_cmd)
+            src = open_fastq_source(o.reads1, o.reads2, o.interleaved, (size_t)std::max(1, o.chunk_size));
+        if (src && !o.r_set) o.r = src->estimate_read_length();
         IndexParameters ip = IndexParameters::from_read_length(o.r, o.k, o.s, o.l, o.u, o.c, o.m);
         auto t0 = std::chrono::steady_clock::now();
         References refs = References::from_fasta(o.ref);
@@ -172,10 +180,6 @@ int cli_main(int argc, char** argv, EngineFactory factory, const char* prog) {
         po.threads = o.threads; po.chunk_size = o.chunk_size; po.rg_id = o.rg_id;
         if (o.verbose) fprintf(stderr, "[%s] mapping %s%s%s%s\n", prog, o.reads1.c_str(), o.reads2.empty() ? "" : " + ",
                                o.reads2.c_str(), o.interleaved ? " (interleaved)" : "");
-        // the reads are streamed: a reader thread per file parses chunks while the
-        // workers map (InputBuffer::read_records, pc.cpp:74-107)
-        std::unique_ptr<ReadSource> src =
-            open_fastq_source(o.reads1, o.reads2, o.interleaved, (size_t)std::max(1, o.chunk_size));
         PipelineResult res = src->paired() ? run_pipeline_pe(*src, *eng, mc, po, write_sink, out)
                                            : run_pipeline_se(*src, *eng, mc, po, write_sink, out);
         src.reset();

@@ -874,9 +874,12 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
                 break;
             }
         } catch (...) {
-            std::lock_guard<std::mutex> g(m);
-            if (!failure) failure = std::current_exception();
-            cv.notify_all();
+            {
+                std::lock_guard<std::mutex> g(m);
+                if (!failure) failure = std::current_exception();
+                cv.notify_all();
+            }
+            src.cancel();        // workers waiting on input (a stalled pipe) give up too
         }
         hold.reset();
         std::lock_guard<std::mutex> g(m);
@@ -1033,9 +1036,12 @@ PipelineResult run_pipeline_se(ReadSource& src, Engine& eng, const MapContext& m
             // an engine error on any worker ends the run: the others stop at their next
             // chunk and rsam_map / the CLI report it (an exception escaping a std::thread
             // would terminate the process)
-            std::lock_guard<std::mutex> g(stat_m);
-            if (!failure) failure = std::current_exception();
-            failed = true;
+            {
+                std::lock_guard<std::mutex> g(stat_m);
+                if (!failure) failure = std::current_exception();
+                failed = true;
+            }
+            src.cancel();        // workers waiting on input (a stalled pipe) give up too
         }
         hold.reset();
         so.clear();

@@ -629,6 +629,13 @@ public:
     virtual bool paired() const = 0;
     virtual bool get(size_t idx, InputChunk& out) = 0;
     virtual void release(InputChunk& c) { c.clear(); }
+    // the CLI's read-length estimate (main.cpp:254-258, readlen.cpp:16-29) from the
+    // source's own first records, before any chunk is taken; sources that are not
+    // files have none and give the default profile's 150
+    virtual int estimate_read_length() { return 150; }
+    // the run failed: get() calls waiting on input return with an error instead of
+    // waiting for a producer that may never write again
+    virtual void cancel() {}
 };
 
 // Records already in memory (rsam_reads, tests): chunks are views into the
@@ -645,9 +652,6 @@ std::unique_ptr<ReadSource> make_interleaved_vector_source(const std::vector<Rec
 // single-end, or interleaved pairs when `interleaved`.
 std::unique_ptr<ReadSource> open_fastq_source(const std::string& path1, const std::string& path2, bool interleaved,
                                               size_t chunk_size);
-// the read-length estimate of the CLI (main.cpp:254-258, readlen.cpp:16-29): the
-// mean length of the first 500 records of each file (1000 of an interleaved file)
-int estimate_read_length(const std::string& path1, const std::string& path2, bool interleaved);
 
 // ------------------------------------------------------------ pipeline ---
 // called at the start of every pipeline worker thread (profiling hooks; null by default)
