@@ -76,3 +76,26 @@ def test_aligner_wrapper_hand_derived():
             continue
         for k, v in want.items():
             assert got[k] == v, (name, k, got[k], v)
+
+
+@pytest.mark.skipif(not os.path.exists(oracle_lib.REFGEN), reason="reference build (oracle/_ref/refgen) absent")
+def test_wrapper_cases_ssw_core_live(tmp_path):
+    """The SSW part of each hand derivation in tests/wrapper_cases.py (score1, begins,
+    ends, the M/I/D CIGAR) against the reference's own ssw.c (oracle/_ref/refgen ssw),
+    so only the Aligner::align wrapper above it stays restated-only."""
+    from wrapper_cases import cases, ssw_core
+    core = ssw_core()
+    sel = [(n, q, r) for n, q, r, _ in cases() if n in core]
+    assert len(sel) == len(core)
+    jobs = tmp_path / "jobs.txt"
+    jobs.write_text("".join(f"{q.decode()} {r.decode()}\n" for _, q, r in sel))
+    out = tmp_path / "out.txt"
+    subprocess.run([oracle_lib.REFGEN, "ssw", str(jobs), str(out)], check=True)
+    lines = out.read_text().splitlines()
+    assert len(lines) == len(sel)
+    for (name, _, _), line in zip(sel, lines):
+        f = line.split()[2:]
+        score1, rb, re_, qb, qe, flag, n = (int(x) for x in f[:7])
+        cig = [int(x) for x in f[7:7 + n]]
+        assert flag == 0, name
+        assert (score1, rb, re_, qb, qe, cig) == core[name], (name, (score1, rb, re_, qb, qe, cig), core[name])

@@ -20,6 +20,17 @@ def _flip(b):
     return ord("A") if b != ord("A") else ord("C")
 
 
+def _other(*avoid):
+    """A base equal to none of `avoid`."""
+    return next(c for c in b"ACGT" if c not in avoid)
+
+
+def cigar_m(*ops):
+    """SSW's own CIGAR words (ssw.c to_cigar_int: len << 4 | index in "MIDNSHP=X")."""
+    code = {"M": 0, "I": 1, "D": 2}
+    return [(n << 4) | code[o] for n, o in ops]
+
+
 def cases():
     R = _ref()
     out = []
@@ -87,4 +98,107 @@ def cases():
     # 10. window longer than 2000: the sentinel (aligner.cpp:119-125)
     out.append(("ref_gt_2000", bytes(R[10:60]), bytes(_ref(3, 2001)), dict(sw_score=-1000000, edit_distance=100000,
                                                                            ref_start=0)))
+    out += cases_r04(R)
     return out
+
+
+def cases_r04(R):
+    """Round-4 cases (VERDICT r03 "next" item 8).  SSW's part of each derivation (score1,
+    begins/ends, the M/I/D CIGAR) is also checked against the reference's own ssw.c run
+    here (ssw_core(), tests/test_oracle_golden.py::test_wrapper_cases_ssw_core_live)."""
+    out = []
+    # 11. a gap seven bases after a clip that the front extension replaces.  banded_sw's
+    #     traceback appends a final M after its last move (ssw.c:756-770), so the CIGAR of
+    #     an SSW alignment always begins with M: a clip cannot be followed by I or D
+    #     directly; the closest case is a short = run, then the gap.
+    #     query = R[18] (=), flip(R[19]) (X), R[20:27] (7 bases), b, R[27:67] (40 bases), with
+    #     b equal to neither R[26] nor R[27] (the insertion has one place; asserted).
+    #     SSW: 7 x 2 - 12 + 40 x 2 = 82 beats the 40-base run alone (80); the two leading
+    #     bases add -8 + 2 < 0, so read_begin1 = 2, ref_begin1 = 20, read_end1 = 49, ref_end1 =
+    #     66; banded_sw (refLen 47, readLen 48, band 2) keeps 82 and traces 7M1I40M.
+    #     ConvertAlignment/CalculateNumberMismatch: 2S7=1I40=, mismatches 1 (the I).
+    #     Aligner::align: front loop q1 vs R19 X (74), q0 vs R18 = (76); q reaches 0 and 76 + 10 >
+    #     82: the 2S goes, front_cigar reversed (= X) is followed by 7=1I40= (no merge: X then
+    #     =) -> 1=1X7=1I40=, ref_start 18, score 86, edits 2; back: query end reached, 86 + 10
+    #     > 86 -> 96
+    assert R[26] != R[27]
+    b = _other(R[26], R[27])
+    q11 = bytes([R[18], _flip(R[19])]) + bytes(R[20:27]) + bytes([b]) + bytes(R[27:67])
+    out.append(("front_ext_then_ins", q11, bytes(R),
+                dict(sw_score=96, edit_distance=2, ref_start=18, ref_end=67, query_start=0, query_end=50,
+                     cigar=[op(1, EQ), op(1, X), op(7, EQ), op(1, I), op(40, EQ)])))
+    # 12. the same with a deletion: R[27] is skipped (R[27] differs from R[26] and R[28], so
+    #     the deletion has one place; asserted).  SSW 82 (7M1D40M, refLen 48, readLen 47);
+    #     front extension as in 11 -> 1=1X7=1D40=, ref_start 18, ref_end 68, 86 + 10 = 96
+    assert R[27] != R[26] and R[27] != R[28]
+    q12 = bytes([R[18], _flip(R[19])]) + bytes(R[20:27]) + bytes(R[28:68])
+    out.append(("front_ext_then_del", q12, bytes(R),
+                dict(sw_score=96, edit_distance=2, ref_start=18, ref_end=68, query_start=0, query_end=49,
+                     cigar=[op(1, EQ), op(1, X), op(7, EQ), op(1, D), op(40, EQ)])))
+    # 13. end-bonus ties at both ends: query = R[10:60] with q3, q4, q45, q46 flipped.  Read
+    #     outward from the 40-base core (q5..q44 = R15..R54, SSW 80, 40M), each flank is
+    #     X X = = = (-16 + 6 = -10, every partial flank negative, so SSW clips both).  Front
+    #     extension 80 - 10 = 70, 70 + 10 > 80 fails (equal); the back likewise: 5S40=5S, 80
+    q13 = bytearray(R[10:60])
+    for i in (3, 4, 45, 46):
+        q13[i] = _flip(q13[i])
+    out.append(("both_ends_tie", bytes(q13), bytes(R),
+                dict(sw_score=80, edit_distance=0, ref_start=15, ref_end=55, query_start=5, query_end=45,
+                     cigar=[op(5, S), op(40, EQ), op(5, S)])))
+    # 14. N on both sides of a mismatch: ref N at 28 and 30, query = that ref[10:60] with q19
+    #     (ref 29) changed to a base that matches neither its own nor a neighbouring ref base
+    #     (no shifted diagonal scores; asserted).  SSW scores N-N -8: 47 matches - 3 x 8 = 70
+    #     beats the right part alone (29 x 2 = 58) and any gap pair around the three bases
+    #     (I3 + D3 costs 2 x (12 + 2) = 28 > 24), so the whole 50 bases align, 50M
+    #     (refLen = readLen: band 1).  (With four bases N X X N a 4I4D pair, 30, beats four
+    #     mismatches, 32: the live ssw.c check caught that in a first draft of this case.)
+    #     The =/X split compares translated codes, N (4) == N (4): 19= (q0..q18) 1X 30=
+    #     (q20..q49), mismatches 1.  Both ends reached: 70 + 10 + 10 = 90
+    rn = bytearray(R)
+    rn[28] = rn[30] = ord("N")
+    q14 = bytearray(rn[10:60])
+    q14[19] = _other(R[29], R[28], R[30])
+    out.append(("n_around_mismatch", bytes(q14), bytes(rn),
+                dict(sw_score=90, edit_distance=1, ref_start=10, ref_end=60, query_start=0, query_end=50,
+                     cigar=[op(19, EQ), op(1, X), op(30, EQ)])))
+    # 15. N inside the front extension: ref N at 12, query = that ref[10:60] with q3 flipped
+    #     (q2 = N).  SSW: the prefix q0..q3 scores 2 + 2 - 8 - 8 < 0 (N-N is -8), every part
+    #     of it too, so 4S46M (92, core q4..q49 = ref 14..59).  The front loop compares raw
+    #     bytes (aligner.cpp:152-163): q3 X (84), q2 N == N '=' (86), q1, q0 = (90); 90 + 10 >
+    #     92 -> X = = = reversed -> 3=1X, then 46= -> 3=1X46=, ref_start 10, 100, edits 1;
+    #     back +10 -> 110
+    rn2 = bytearray(R)
+    rn2[12] = ord("N")
+    q15 = bytearray(rn2[10:60])
+    q15[3] = _flip(q15[3])
+    out.append(("n_in_front_extension", bytes(q15), bytes(rn2),
+                dict(sw_score=110, edit_distance=1, ref_start=10, ref_end=60, query_start=0, query_end=50,
+                     cigar=[op(3, EQ), op(1, X), op(46, EQ)])))
+    # 16. a window of exactly 2000 bases is aligned (the sentinel is for > 2000,
+    #     aligner.cpp:119): an exact 50-mer at 1000 -> 100 + 10 + 10, 50=
+    W = _ref(5, 2000)
+    out.append(("ref_eq_2000", bytes(W[1000:1050]), bytes(W),
+                dict(sw_score=120, edit_distance=0, ref_start=1000, ref_end=1050, query_start=0, query_end=50,
+                     cigar=[op(50, EQ)])))
+    # 17. one base more, the same exact 50-mer: the sentinel, no CIGAR
+    W1 = _ref(5, 2001)
+    out.append(("ref_eq_2001", bytes(W1[1000:1050]), bytes(W1),
+                dict(sw_score=-1000000, edit_distance=100000, ref_start=0, cigar=[])))
+    return out
+
+
+def ssw_core():
+    """SSW's own results for the cases whose derivation above states them:
+    (score1, ref_begin1, ref_end1, read_begin1, read_end1, SSW CIGAR words)."""
+    return {
+        "exact": (100, 10, 59, 0, 49, cigar_m((50, "M"))),
+        "deletion": (106, 10, 69, 0, 58, cigar_m((30, "M"), (1, "D"), (29, "M"))),
+        "insertion": (108, 10, 69, 0, 60, cigar_m((30, "M"), (1, "I"), (30, "M"))),
+        "both_clipped": (80, 15, 54, 5, 44, cigar_m((40, "M"))),
+        "front_ext_then_ins": (82, 20, 66, 2, 49, cigar_m((7, "M"), (1, "I"), (40, "M"))),
+        "front_ext_then_del": (82, 20, 67, 2, 48, cigar_m((7, "M"), (1, "D"), (40, "M"))),
+        "both_ends_tie": (80, 15, 54, 5, 44, cigar_m((40, "M"))),
+        "n_around_mismatch": (70, 10, 59, 0, 49, cigar_m((50, "M"))),
+        "n_in_front_extension": (92, 14, 59, 4, 49, cigar_m((46, "M"))),
+        "ref_eq_2000": (100, 1000, 1049, 0, 49, cigar_m((50, "M"))),
+    }
