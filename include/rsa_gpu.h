@@ -40,6 +40,7 @@ extern "C" {
 #define RSA_ERR_CAPACITY (-3)   /* an output buffer is too small; *_needed fields say how much */
 #define RSA_ERR_NOMEM (-4)
 #define RSA_ERR_BUSY (-5)       /* rsa_extend_async: RSA_MAX_PENDING calls not yet waited for */
+#define RSA_ERR_INTERNAL (-6)   /* a device-side consistency check failed (a defect, not an input error) */
 
 /* RefRandstrobe exactly as stored in a .sti file (src/randstrobes.hpp:20-49) */
 typedef struct rsa_ref_randstrobe {
@@ -317,6 +318,8 @@ typedef struct rsa_kernel_stats {
     uint64_t reads, read_bases, query_randstrobes, lookups_found, filtered, hits, nams, rescued_reads;
     uint64_t jobs, dp_cells;         /* dp_cells: sum query_len * ref_len of the forward scan */
     uint64_t band_deferred, band_overflow;   /* jobs handed to the 64-lane / panel band kernels */
+    uint64_t scan_certified, scan_redo;      /* word results taken without the byte pass (certified by the
+                                              * band path), and those re-run through the two-layout scan */
     /* wall time of the calls ([0] rsa_seed, [1] rsa_extend), ms summed over calls: whole call,
      * waiting for a free stream lane, blocked on the device (event waits); the rest is host work */
     double call_ms[2], lane_wait_ms[2], device_wait_ms[2];

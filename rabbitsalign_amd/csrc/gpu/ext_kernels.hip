@@ -638,6 +638,21 @@ __device__ __forceinline__ int dir_byte(const int8_t* dirp, int cell, int sub) {
     const int de = 2 + (v & 1), df = 4 + ((v >> 1) & 1), dhc = (v >> 2) & 3;
     return sub == 0 ? de : (sub == 1 ? df : (dhc == 1 ? 1 : (dhc == 2 ? de : df)));
 }
+// Certificate of a word-layout result taken without the byte pass (k_ext_scan_v,
+// ScanRes.word bit 1): the job's banded path must have no insertion next to a
+// deletion, or the job is listed for the exact two-layout scan (rsa_ctx.hip).
+// raw: the path's ops in order (0 M, 1 I, 2 D); ok = false lists the job as is.
+__device__ __forceinline__ void cert_check(const ScanRes& sr, int j, const uint32_t* raw, int nraw, bool ok,
+                                           int* redo, int* redo_count) {
+    if (!(sr.word & 2) || !redo) return;
+    bool bad = !ok;
+    for (int k = 1; k < nraw && !bad; ++k) {
+        const uint32_t a = raw[k - 1] & 0xf, b = raw[k] & 0xf;
+        bad = (a == 1 && b == 2) || (a == 2 && b == 1);
+    }
+    if (bad) redo[atomicAdd(redo_count, 1)] = j;
+}
+
 template <int DIRCAP> struct DirCells { static constexpr int BYTES = ((DIRCAP + 2) / 3 + 15) & ~15; };
 
 // banded_sw + traceback + ext_finish of job j by a group of G lanes (z = lane in
@@ -650,7 +665,8 @@ template <int G, int DIRCAP, int QCAP, int RCAP>
 __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr, const char* __restrict__ qbuf,
                            const char* __restrict__ ref, uint32_t* __restrict__ cig_pool,
                            uint32_t* __restrict__ raw_pool, rsa_aln* __restrict__ out, int match, int mismatch,
-                           int gO, int gE, int bonus, int8_t* dir, uint8_t* qc, uint8_t* rc) {
+                           int gO, int gE, int bonus, int8_t* dir, uint8_t* qc, uint8_t* rc, int* redo,
+                           int* redo_count) {
     const char* q = qbuf + jb.q_off;
     const char* r = ref + jb.r_off;
     const int rlen = (int)jb.rlen;
@@ -790,11 +806,13 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
     }
     if (fail) {                                     // banded_sw failed -> flag 1 sentinel
         aln_sentinel(out, j, jb, -100000);
+        cert_check(sr, j, raw, 0, false, redo, redo_count);
         return true;
     }
     if (op == 0) { ++l; raw[l - 1] = cig((uint32_t)ecount + 1, op); }
     else { l += 2; raw[l - 2] = cig((uint32_t)ecount, op); raw[l - 1] = cig(1, 0); }
     for (int s = 0, t = l - 1; s < t; ++s, --t) { const uint32_t x = raw[s]; raw[s] = raw[t]; raw[t] = x; }
+    cert_check(sr, j, raw, l, true, redo, redo_count);
     ext_finish(jb, sr, q, r, raw, l, cig_pool + jb.cig_off, a, match, mismatch, bonus, gO, gE, qc, rc);
     out[j] = a;
     return true;
@@ -806,15 +824,17 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
 
 __global__ void __launch_bounds__(64)
 k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan, int n_jobs,
-             const char* __restrict__ qbuf, const char* __restrict__ ref, uint32_t* __restrict__ cig_pool,
-             uint32_t* __restrict__ raw_pool, rsa_aln* __restrict__ out, int match, int mismatch, int gO, int gE,
-             int bonus, int* __restrict__ queue, int* __restrict__ qcount, int* __restrict__ overflow) {
+             const int* __restrict__ idx, const char* __restrict__ qbuf, const char* __restrict__ ref,
+             uint32_t* __restrict__ cig_pool, uint32_t* __restrict__ raw_pool, rsa_aln* __restrict__ out, int match,
+             int mismatch, int gO, int gE, int bonus, int* __restrict__ queue, int* __restrict__ qcount,
+             int* __restrict__ overflow, int* __restrict__ redo, int* __restrict__ redo_count) {
     __shared__ __attribute__((aligned(16))) int8_t s_dir[B16_GROUPS][DirCells<B16_DIRCAP>::BYTES];
     __shared__ uint8_t s_qc[B16_GROUPS][B16_SEGCAP];
     __shared__ uint8_t s_rc[B16_GROUPS][B16_SEGCAP];
     const int lane = threadIdx.x & 63, g = lane >> 4, z = lane & 15;
-    const int j = blockIdx.x * B16_GROUPS + g;
-    if (j >= n_jobs) return;                       // whole group leaves together
+    const int t = blockIdx.x * B16_GROUPS + g;
+    if (t >= n_jobs) return;                       // whole group leaves together
+    const int j = idx ? idx[t] : t;
     const ExtJobDev jb = jobs[j];
     const ScanRes sr = scan[j];
     if (z == 0) overflow[j] = 0;                   // k_ext_band64 sets the jobs it cannot hold
@@ -823,11 +843,15 @@ k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
         return;
     }
     if (sr.flag != 0) {                            // aligner.cpp:131-136
-        if (z == 0) aln_sentinel(out, j, jb, -100000);
+        if (z == 0) {
+            aln_sentinel(out, j, jb, -100000);
+            cert_check(sr, j, nullptr, 0, false, redo, redo_count);
+        }
         return;
     }
     const bool done = band_group<16, B16_DIRCAP, B16_SEGCAP, B16_SEGCAP>(
-        j, z, jb, sr, qbuf, ref, cig_pool, raw_pool, out, match, mismatch, gO, gE, bonus, s_dir[g], s_qc[g], s_rc[g]);
+        j, z, jb, sr, qbuf, ref, cig_pool, raw_pool, out, match, mismatch, gO, gE, bonus, s_dir[g], s_qc[g], s_rc[g],
+        redo, redo_count);
     if (!done && z == 0) {
         // an empty result until a wider kernel writes it: the CIGAR compaction reads
         // every job, including one the 64-lane kernel leaves to the one-lane pass
@@ -848,7 +872,7 @@ k_ext_band64(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
              const char* __restrict__ ref, uint32_t* __restrict__ cig_pool, uint32_t* __restrict__ raw_pool,
              rsa_aln* __restrict__ out, int match, int mismatch, int gO, int gE, int bonus,
              const int* __restrict__ queue, const int* __restrict__ qcount, int* __restrict__ overflow,
-             int* __restrict__ ocount) {
+             int* __restrict__ ocount, int* __restrict__ redo, int* __restrict__ redo_count) {
     __shared__ __attribute__((aligned(16))) int8_t s_dir[DirCells<B64_DIRCAP>::BYTES];
     __shared__ uint8_t s_qc[B64_QCAP];
     __shared__ uint8_t s_rc[B64_RCAP];
@@ -859,7 +883,8 @@ k_ext_band64(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
         const ExtJobDev jb = jobs[j];
         const ScanRes sr = scan[j];
         const bool done = band_group<64, B64_DIRCAP, B64_QCAP, B64_RCAP>(
-            j, z, jb, sr, qbuf, ref, cig_pool, raw_pool, out, match, mismatch, gO, gE, bonus, s_dir, s_qc, s_rc);
+            j, z, jb, sr, qbuf, ref, cig_pool, raw_pool, out, match, mismatch, gO, gE, bonus, s_dir, s_qc, s_rc,
+            redo, redo_count);
         if (!done && z == 0) { overflow[j] = 1; atomicAdd(ocount, 1); }
         WSYNC();
     }
@@ -889,7 +914,7 @@ k_ext_band_panel(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__
                  const int* __restrict__ idx_list, const char* __restrict__ qbuf, const char* __restrict__ ref,
                  uint32_t* __restrict__ cig_pool, rsa_aln* __restrict__ out, uint8_t* __restrict__ scratch,
                  int64_t scr_stride, int64_t dir_cap, int match, int mismatch, int gO, int gE, int bonus,
-                 int* __restrict__ overflow, int over_code) {
+                 int* __restrict__ overflow, int over_code, int* __restrict__ redo, int* __restrict__ redo_count) {
     __shared__ int s_hb[BP_KW];
     __shared__ int s_eb[BP_KW];
     __shared__ uint8_t s_qc[BP_QCAP];
@@ -1016,20 +1041,29 @@ k_ext_band_panel(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__
     uint32_t op = 0, prev_op = 0;
     while (i >= 0 && jx > 0) {
         const int64_t at = line + (int64_t)(jx - max(i - bw, 0)) * 3 + temp2;
-        if (at < 0 || at >= s2_ref) { aln_sentinel(out, j, jb, -100000); return; }
+        if (at < 0 || at >= s2_ref) {
+            aln_sentinel(out, j, jb, -100000);
+            cert_check(sr, j, raw, 0, false, redo, redo_count);
+            return;
+        }
         const int dv = dir[at];
         if (dv == 1) { --i; --jx; temp2 = 2; line -= width_d * 3; op = 0; }
         else if (dv == 2) { --i; temp2 = 0; line -= width_d * 3; op = 1; }
         else if (dv == 3) { --i; temp2 = 2; line -= width_d * 3; op = 1; }
         else if (dv == 4) { --jx; temp2 = 1; op = 2; }
         else if (dv == 5) { --jx; temp2 = 2; op = 2; }
-        else { aln_sentinel(out, j, jb, -100000); return; }   // banded_sw failed -> flag 1
+        else {                                               // banded_sw failed -> flag 1
+            aln_sentinel(out, j, jb, -100000);
+            cert_check(sr, j, raw, 0, false, redo, redo_count);
+            return;
+        }
         if (op == prev_op) ++ecount;
         else { ++l; raw[l - 1] = cig((uint32_t)ecount, prev_op); prev_op = op; ecount = 1; }
     }
     if (op == 0) { ++l; raw[l - 1] = cig((uint32_t)ecount + 1, op); }
     else { l += 2; raw[l - 2] = cig((uint32_t)ecount, op); raw[l - 1] = cig(1, 0); }
     for (int s = 0, e = l - 1; s < e; ++s, --e) { const uint32_t x = raw[s]; raw[s] = raw[e]; raw[e] = x; }
+    cert_check(sr, j, raw, l, true, redo, redo_count);
     ext_finish(jb, sr, q, r, raw, l, cig_pool + jb.cig_off, a, match, mismatch, bonus, gO, gE, s_qc, s_rc);
     out[j] = a;
 }
@@ -1134,16 +1168,18 @@ void launch_ext_scan(int rmax, dim3 grid, dim3 block, hipStream_t st, const ExtJ
 #undef RSA_L
 }
 
-void launch_ext_band16(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n, const char* q,
-                       const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match, int mismatch, int gO,
-                       int gE, int bonus, int* queue, int* qcount, int* overflow) {
-    hipLaunchKernelGGL(k_ext_band16, grid, dim3(64), 0, st, jobs, scan, n, q, ref, cig, raw, out, match, mismatch, gO,
-                       gE, bonus, queue, qcount, overflow);
+void launch_ext_band16(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n, const int* idx,
+                       const char* q, const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match,
+                       int mismatch, int gO, int gE, int bonus, int* queue, int* qcount, int* overflow, int* redo,
+                       int* redo_count) {
+    hipLaunchKernelGGL(k_ext_band16, grid, dim3(64), 0, st, jobs, scan, n, idx, q, ref, cig, raw, out, match, mismatch,
+                       gO, gE, bonus, queue, qcount, overflow, redo, redo_count);
 }
 
 void launch_ext_band64(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, const char* q,
                        const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match, int mismatch, int gO,
-                       int gE, int bonus, const int* queue, const int* qcount, int* overflow, int* ocount) {
+                       int gE, int bonus, const int* queue, const int* qcount, int* overflow, int* ocount, int* redo,
+                       int* redo_count) {
     hipLaunchKernelGGL(k_ext_band64, grid, dim3(64), 0, st, jobs, scan, q, ref, cig, raw, out, match, mismatch, gO, gE,
-                       bonus, queue, qcount, overflow, ocount);
+                       bonus, queue, qcount, overflow, ocount, redo, redo_count);
 }

@@ -32,13 +32,20 @@ bool scan_g_params_ok(int match, int mismatch, int gO, int gE);
 __global__ void k_ext_band_panel(const ExtJobDev* jobs, const ScanRes* scan, int n_jobs, const int* idx_list,
                                  const char* qbuf, const char* ref, uint32_t* cig_pool, rsa_aln* out,
                                  uint8_t* scratch, int64_t scr_stride, int64_t dir_cap, int match, int mismatch,
-                                 int gO, int gE, int bonus, int* overflow, int over_code);
-void launch_ext_band16(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n, const char* q,
-                       const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match, int mismatch, int gO,
-                       int gE, int bonus, int* queue, int* qcount, int* overflow);
+                                 int gO, int gE, int bonus, int* overflow, int over_code, int* redo,
+                                 int* redo_count);
+void launch_ext_band16(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n, const int* idx,
+                       const char* q, const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match,
+                       int mismatch, int gO, int gE, int bonus, int* queue, int* qcount, int* overflow, int* redo,
+                       int* redo_count);
 void launch_ext_band64(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, const char* q,
                        const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match, int mismatch, int gO,
-                       int gE, int bonus, const int* queue, const int* qcount, int* overflow, int* ocount);
+                       int gE, int bonus, const int* queue, const int* qcount, int* overflow, int* ocount, int* redo,
+                       int* redo_count);
+int scan_v_rows(uint32_t qlen);
+int scan_v_wcap(uint32_t rlen);
+void launch_ext_scan_v(int rv, int wcap, int n, hipStream_t st, const ExtJobDev* jobs, const int* order, const char* q,
+                       const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE, int* err);
 void launch_cigar_compact(hipStream_t st, const rsa_aln* alns, rsa_aln* alns_out, int n_jobs, const uint32_t* slots,
                           uint32_t* dense, uint64_t* bsum, uint64_t* total);
 
@@ -104,7 +111,9 @@ struct Lane {
     // extension
     // d_jobs / h_jobs: one staged upload per call, [ExtJobDev x n | scan order x n | ExtStatus (zeroed)];
     // d_alns holds results with CIGAR slot offsets, d_alns_out the copy with packed offsets
-    DevBuf d_q, d_jobs, d_scan, d_alns, d_alns_out, d_cig, d_dense, d_raw, d_scratch, d_over, d_queue, d_idx, d_bsum;
+    // d_redo: jobs whose certified word result the band path could not confirm (k_ext_scan_v)
+    DevBuf d_q, d_jobs, d_scan, d_alns, d_alns_out, d_cig, d_dense, d_raw, d_scratch, d_over, d_queue, d_idx, d_bsum,
+        d_redo;
     HostBuf h_jobs, h_over, h_status;
     // seeding
     SeedBufs sb;
@@ -112,8 +121,16 @@ struct Lane {
 
 }  // namespace
 
+// k_ext_scan_v (one layout per pass, certified) unless RSA_SCAN_V=0 (k_ext_scan_g,
+// both layouts in every pass); read when a context opens
+static bool scan_v_env() {
+    const char* v = getenv("RSA_SCAN_V");
+    return !(v && v[0] == '0');
+}
+
 struct rsa_ctx {
     int device = 0;
+    bool scan_v = scan_v_env();
     std::string err;
     std::mutex err_m;
     // resident data
@@ -397,6 +414,8 @@ struct ExtStatus {            // device-side counters of one rsa_extend call
     int qcount;               // jobs deferred by k_ext_band16
     int ocount;               // jobs k_ext_band64 could not hold
     uint64_t total;           // dense CIGAR ops (k_cigar_compact)
+    int rcount;               // jobs listed in d_redo (certificate not met)
+    int err;                  // k_ext_scan_v found an alignment end outside its job (a defect)
 };
 
 // byte offsets of the scan order and the status in the staged job upload of n jobs
@@ -415,6 +434,8 @@ struct rsa_pending {
     uint32_t n = 0;
     int32_t match = 0, mismatch = 0, gap_open = 0, gap_extend = 0, end_bonus = 0;
     uint64_t guess = 0, cells = 0, qr_bytes = 0;
+    uint64_t certified = 0;            // jobs k_ext_scan_v took on the word score alone
+    int rmax = 1;                      // k_ext_scan's rows-per-lane bound for this call's jobs
     ExtStatus* d_status = nullptr;     // in the lane's staged upload
 };
 
@@ -488,6 +509,7 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
     HIPCHK(L->d_raw.ensure(sizeof(uint32_t) * (bound + 16)));
     HIPCHK(L->d_over.ensure(sizeof(int) * n));
     HIPCHK(L->d_queue.ensure(sizeof(int) * n));
+    HIPCHK(L->d_redo.ensure(sizeof(int) * n));
     HIPCHK(L->d_bsum.ensure(sizeof(uint64_t) * ((n + 255) / 256 + 1)));
     HIPCHK(L->h_status.ensure(sizeof(ExtStatus)));
     hipStream_t st = L->stream;
@@ -495,23 +517,38 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
     P.d_status = dst;
     memset(L->h_jobs.as<char>() + stage_status_off(n), 0, sizeof(ExtStatus));
     HIPCHK(hipMemcpyAsync(L->d_q.p, jb->queries, jb->queries_len, hipMemcpyHostToDevice, st));
-    // Scan routing: jobs the grouped kernel takes (query <= 256 bp, window <= 1 KB,
-    // parameters it computes exactly) go to it per rows-per-lane class, sorted by window
-    // length (longest first) so the four jobs of a wave run about as long; the
-    // rest -- and sentinels -- to the one-job-per-wave kernel via an index list.
+    // Scan routing: jobs a grouped kernel takes (query <= 256 bp, window <= 1 KB,
+    // parameters it computes exactly) go to it per class, sorted by window length
+    // (longest first) so the jobs of a wave run about as long; the rest -- and
+    // sentinels -- to the one-job-per-wave kernel via an index list.  Classes:
+    // k_ext_scan_v (default): rows per virtual lane 2..8 x window capacity 512 / 1024;
+    // k_ext_scan_g (RSA_SCAN_V=0): rows per lane 4/7/10/13/16.
     const bool grouped = scan_g_params_ok(jb->match, jb->mismatch, jb->gap_open, jb->gap_extend);
-    constexpr int NCLS = 5;
-    int cls_rows[NCLS];
-    scan_g_classes(cls_rows);
-    uint32_t cls_n[NCLS] = {0}, rest_n = 0;
+    const bool use_v = ctx->scan_v;
+    constexpr int NCLS_MAX = 14;
+    const int ncls = use_v ? 14 : 5;
+    int cls_rows[NCLS_MAX], cls_wcap[NCLS_MAX];
+    if (use_v) {
+        for (int c = 0; c < 14; ++c) { cls_rows[c] = 2 + c / 2; cls_wcap[c] = (c & 1) ? 1024 : 512; }
+    } else {
+        scan_g_classes(cls_rows);
+        for (int c = 0; c < 5; ++c) cls_wcap[c] = scan_g_max_ref();
+    }
+    uint32_t cls_n[NCLS_MAX] = {0}, rest_n = 0;
     int* ord = reinterpret_cast<int*>(L->h_jobs.as<char>() + stage_order_off(n));
     if (grouped) {
-        const uint32_t maxr = (uint32_t)scan_g_max_ref();
-        std::vector<uint32_t> cnt((size_t)NCLS * (maxr + 1), 0);
+        const uint32_t maxr = 1024;
+        std::vector<uint32_t> cnt((size_t)ncls * (maxr + 1), 0);
         auto cls_of = [&](const ExtJobDev& j) -> int {
-            if (j.rlen > 2000 || j.qlen == 0 || j.qlen > 1024 || j.rlen > maxr) return -1;
+            if (j.rlen > 2000 || j.qlen == 0 || j.qlen > 1024) return -1;
+            if (use_v) {
+                const int r = scan_v_rows(j.qlen), w = scan_v_wcap(j.rlen);
+                if (r == 0 || w == 0) return -1;
+                return (r - 2) * 2 + (w == 1024 ? 1 : 0);
+            }
+            if (j.rlen > (uint32_t)scan_g_max_ref()) return -1;
             const int r = scan_g_rows(j.qlen);
-            for (int c = 0; c < NCLS; ++c) if (cls_rows[c] == r) return c;
+            for (int c = 0; c < 5; ++c) if (cls_rows[c] == r) return c;
             return -1;
         };
         std::vector<int8_t> cls(n);
@@ -522,7 +559,7 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
         }
         // counting sort: class-major, then window length descending; the rest after
         uint64_t at = 0;
-        for (int c = 0; c < NCLS; ++c)
+        for (int c = 0; c < ncls; ++c)
             for (uint32_t b = 0; b <= maxr; ++b) {
                 uint32_t& x = cnt[(size_t)c * (maxr + 1) + b];
                 const uint32_t k = x;
@@ -534,10 +571,12 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
             if (cls[i] < 0) ord[rest_at++] = (int)i;
             else ord[cnt[(size_t)cls[i] * (maxr + 1) + (maxr - hj[i].rlen)]++] = (int)i;
         }
+        if (use_v) for (int c = 0; c < ncls; ++c) P.certified += cls_n[c];
     } else {
         rest_n = n;
         for (uint32_t i = 0; i < n; ++i) ord[i] = (int)i;
     }
+    P.rmax = rmax;
     // jobs, scan order and the zeroed status in one copy
     HIPCHK(hipMemcpyAsync(L->d_jobs.p, L->h_jobs.p, stage_bytes(n), hipMemcpyHostToDevice, st));
     L->kt.arm();
@@ -545,11 +584,16 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
     {
         const int* d_ord = reinterpret_cast<const int*>(L->d_jobs.as<char>() + stage_order_off(n));
         uint32_t off = 0;
-        for (int c = 0; c < NCLS; ++c) {
+        for (int c = 0; c < ncls; ++c) {
             if (!cls_n[c]) continue;
-            launch_ext_scan_g(cls_rows[c], (int)cls_n[c], st, L->d_jobs.as<ExtJobDev>(), d_ord + off,
-                              L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(), jb->match, jb->mismatch,
-                              jb->gap_open, jb->gap_extend);
+            if (use_v)
+                launch_ext_scan_v(cls_rows[c], cls_wcap[c], (int)cls_n[c], st, L->d_jobs.as<ExtJobDev>(), d_ord + off,
+                                  L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(), jb->match, jb->mismatch,
+                                  jb->gap_open, jb->gap_extend, &dst->err);
+            else
+                launch_ext_scan_g(cls_rows[c], (int)cls_n[c], st, L->d_jobs.as<ExtJobDev>(), d_ord + off,
+                                  L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(), jb->match, jb->mismatch,
+                                  jb->gap_open, jb->gap_extend);
             HIPCHK(hipGetLastError());
             off += cls_n[c];
         }
@@ -566,10 +610,10 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
     // the compaction below never reads an unwritten result) and clears every job's
     // overflow flag, which k_ext_band64 sets for the bands it cannot hold
     L->kt.begin(st, RSA_K_EXT_BAND);
-    launch_ext_band16(dim3((n + 3) / 4), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(), (int)n,
+    launch_ext_band16(dim3((n + 3) / 4), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(), (int)n, nullptr,
                       L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(),
                       L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open, jb->gap_extend, jb->end_bonus,
-                      L->d_queue.as<int>(), &dst->qcount, L->d_over.as<int>());
+                      L->d_queue.as<int>(), &dst->qcount, L->d_over.as<int>(), L->d_redo.as<int>(), &dst->rcount);
     HIPCHK(hipGetLastError());
     L->kt.end(st);
     L->kt.begin(st, RSA_K_EXT_BAND_WIDE);
@@ -577,7 +621,7 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
                       L->d_scan.as<ScanRes>(), L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(),
                       L->d_raw.as<uint32_t>(), L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open,
                       jb->gap_extend, jb->end_bonus, L->d_queue.as<int>(), &dst->qcount, L->d_over.as<int>(),
-                      &dst->ocount);
+                      &dst->ocount, L->d_redo.as<int>(), &dst->rcount);
     HIPCHK(hipGetLastError());
     L->kt.end(st);
     P.guess = std::min<uint64_t>(bound, DENSE_GUESS * n);
@@ -586,6 +630,49 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
 
 // second half: wait, the rare panel pass for bands the 64-lane kernel could not
 // hold, the CIGAR entries past the first guess, statistics
+// the rare panel pass: bands the 64-lane kernel could not hold (overflow flag 1) ->
+// one wave per job sweeping each band row in 64-cell panels (direction matrix in
+// global scratch); then the CIGAR compaction and copies again
+static int ext_panel(rsa_pending& P, ExtStatus& hs) {
+    rsa_ctx* ctx = P.ctx;
+    Lane* L = P.L;
+    const uint32_t n = P.n;
+    hipStream_t st = L->stream;
+    HIPCHK(L->h_over.ensure(sizeof(int) * n));
+    HIPCHK(hipMemcpyAsync(L->h_over.p, L->d_over.p, sizeof(int) * n, hipMemcpyDeviceToHost, st));
+    HIPCHK(stream_wait(st, L->sb.done));
+    std::vector<int> big;
+    for (uint32_t i = 0; i < n; ++i)
+        if (L->h_over.as<int>()[i]) big.push_back((int)i);
+    const int64_t bstride = band_stride(BIG_DIR_CAP);
+    HIPCHK(L->d_scratch.ensure((size_t)bstride * BIG_CHUNK));
+    HIPCHK(L->d_idx.ensure(sizeof(int) * big.size()));
+    HIPCHK(hipMemcpyAsync(L->d_idx.p, big.data(), sizeof(int) * big.size(), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(L->d_over.p, 0, sizeof(int) * n, st));
+    for (size_t b = 0; b < big.size(); b += BIG_CHUNK) {
+        const int cnt = (int)std::min<size_t>(BIG_CHUNK, big.size() - b);
+        L->kt.begin(st, RSA_K_EXT_BAND_PANEL);
+        hipLaunchKernelGGL(k_ext_band_panel, dim3(cnt), dim3(64), 0, st, L->d_jobs.as<ExtJobDev>(),
+                           L->d_scan.as<ScanRes>(), cnt, L->d_idx.as<int>() + b, L->d_q.as<char>(), ctx->d_ref,
+                           L->d_cig.as<uint32_t>(), L->d_alns.as<rsa_aln>(), L->d_scratch.as<uint8_t>(), bstride,
+                           BIG_DIR_CAP, P.match, P.mismatch, P.gap_open, P.gap_extend, P.end_bonus,
+                           L->d_over.as<int>(), 2, L->d_redo.as<int>(), &P.d_status->rcount);
+        HIPCHK(hipGetLastError());
+        L->kt.end(st);
+    }
+    HIPCHK(hipMemcpyAsync(L->h_over.p, L->d_over.p, sizeof(int) * n, hipMemcpyDeviceToHost, st));
+    HIPCHK(stream_wait(st, L->sb.done));
+    for (int i : big)
+        if (L->h_over.as<int>()[i] > 1) { set_err(ctx, "rsa_extend: band scratch exhausted"); return RSA_ERR_NOMEM; }
+    if (int rc = ext_compact_copy(P)) return rc;
+    HIPCHK(stream_wait(st, L->sb.done));
+    hs = *L->h_status.as<ExtStatus>();
+    return RSA_OK;
+}
+
+// second half: wait, the rare panel pass, the rare re-run of jobs whose word
+// result k_ext_scan_v could not certify, the CIGAR entries past the first guess,
+// statistics
 static int ext_finish(rsa_pending& P) {
     rsa_ctx* ctx = P.ctx;
     Lane* L = P.L;
@@ -595,38 +682,46 @@ static int ext_finish(rsa_pending& P) {
     const uint64_t guess = P.guess;
     HIPCHK(stream_wait(st, L->sb.done));
     ExtStatus hs = *L->h_status.as<ExtStatus>();
-    if (hs.ocount > 0) {
-        // rare: bands the 64-lane kernel cannot hold (flag 1) -> one wave per job sweeping
-        // each band row in 64-cell panels (direction matrix in global scratch)
-        HIPCHK(L->h_over.ensure(sizeof(int) * n));
-        HIPCHK(hipMemcpyAsync(L->h_over.p, L->d_over.p, sizeof(int) * n, hipMemcpyDeviceToHost, st));
-        HIPCHK(stream_wait(st, L->sb.done));
-        std::vector<int> big;
-        for (uint32_t i = 0; i < n; ++i)
-            if (L->h_over.as<int>()[i]) big.push_back((int)i);
-        const int64_t bstride = band_stride(BIG_DIR_CAP);
-        HIPCHK(L->d_scratch.ensure((size_t)bstride * BIG_CHUNK));
-        HIPCHK(L->d_idx.ensure(sizeof(int) * big.size()));
-        HIPCHK(hipMemcpyAsync(L->d_idx.p, big.data(), sizeof(int) * big.size(), hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemsetAsync(L->d_over.p, 0, sizeof(int) * n, st));
-        for (size_t b = 0; b < big.size(); b += BIG_CHUNK) {
-            const int cnt = (int)std::min<size_t>(BIG_CHUNK, big.size() - b);
-            L->kt.begin(st, RSA_K_EXT_BAND_PANEL);
-            hipLaunchKernelGGL(k_ext_band_panel, dim3(cnt), dim3(64), 0, st, L->d_jobs.as<ExtJobDev>(),
-                               L->d_scan.as<ScanRes>(), cnt, L->d_idx.as<int>() + b, L->d_q.as<char>(), ctx->d_ref,
-                               L->d_cig.as<uint32_t>(), L->d_alns.as<rsa_aln>(), L->d_scratch.as<uint8_t>(), bstride,
-                               BIG_DIR_CAP, P.match, P.mismatch, P.gap_open, P.gap_extend, P.end_bonus,
-                               L->d_over.as<int>(), 2);
-            HIPCHK(hipGetLastError());
-            L->kt.end(st);
-        }
-        HIPCHK(hipMemcpyAsync(L->h_over.p, L->d_over.p, sizeof(int) * n, hipMemcpyDeviceToHost, st));
-        HIPCHK(stream_wait(st, L->sb.done));
-        for (int i : big)
-            if (L->h_over.as<int>()[i] > 1) { set_err(ctx, "rsa_extend: band scratch exhausted"); return RSA_ERR_NOMEM; }
+    if (hs.err) { set_err(ctx, "rsa_extend: k_ext_scan_v produced an alignment end outside its job"); return RSA_ERR_INTERNAL; }
+    if (hs.ocount > 0)
+        if (int rc = ext_panel(P, hs)) return rc;
+    const int redo = hs.rcount;
+    uint64_t deferred = (uint64_t)hs.qcount, overflowed = (uint64_t)hs.ocount;
+    if (redo > 0) {
+        // the listed jobs' path had an insertion next to a deletion (or no path): the
+        // byte layout may score them differently, so they take the exact two-layout
+        // scan (k_ext_scan: SSW's byte-then-word decision) and the band kernels again
+        if (redo > (int)n) { set_err(ctx, "rsa_extend: redo list overflow"); return RSA_ERR_INTERNAL; }
+        const int* d_redo = L->d_redo.as<int>();
+        L->kt.begin(st, RSA_K_EXT_SCAN);
+        launch_ext_scan(P.rmax, dim3((redo + 3) / 4), dim3(256), st, L->d_jobs.as<ExtJobDev>(), redo, d_redo,
+                        L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(), P.match, P.mismatch, P.gap_open,
+                        P.gap_extend);
+        HIPCHK(hipGetLastError());
+        L->kt.end(st);
+        HIPCHK(hipMemsetAsync(&P.d_status->qcount, 0, 2 * sizeof(int), st));    // qcount, ocount
+        L->kt.begin(st, RSA_K_EXT_BAND);
+        launch_ext_band16(dim3((redo + 3) / 4), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(), redo, d_redo,
+                          L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(),
+                          L->d_alns.as<rsa_aln>(), P.match, P.mismatch, P.gap_open, P.gap_extend, P.end_bonus,
+                          L->d_queue.as<int>(), &P.d_status->qcount, L->d_over.as<int>(), nullptr, nullptr);
+        HIPCHK(hipGetLastError());
+        L->kt.end(st);
+        L->kt.begin(st, RSA_K_EXT_BAND_WIDE);
+        launch_ext_band64(dim3(std::min(redo, BAND64_GRID)), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(),
+                          L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(),
+                          L->d_alns.as<rsa_aln>(), P.match, P.mismatch, P.gap_open, P.gap_extend, P.end_bonus,
+                          L->d_queue.as<int>(), &P.d_status->qcount, L->d_over.as<int>(), &P.d_status->ocount,
+                          nullptr, nullptr);
+        HIPCHK(hipGetLastError());
+        L->kt.end(st);
         if (int rc = ext_compact_copy(P)) return rc;
         HIPCHK(stream_wait(st, L->sb.done));
         hs = *L->h_status.as<ExtStatus>();
+        deferred += (uint64_t)hs.qcount;
+        overflowed += (uint64_t)hs.ocount;
+        if (hs.ocount > 0)
+            if (int rc = ext_panel(P, hs)) return rc;
     }
     if (hs.total > guess) {
         HIPCHK(hipMemcpyAsync(out->cigar_pool + guess, L->d_dense.as<uint32_t>() + guess,
@@ -648,8 +743,10 @@ static int ext_finish(rsa_pending& P) {
         ctx->stats.ext_calls++;
         ctx->stats.jobs += n;
         ctx->stats.dp_cells += P.cells;
-        ctx->stats.band_deferred += (uint64_t)hs.qcount;
-        ctx->stats.band_overflow += (uint64_t)hs.ocount;
+        ctx->stats.band_deferred += deferred;
+        ctx->stats.band_overflow += overflowed;
+        ctx->stats.scan_certified += P.certified - (uint64_t)redo;
+        ctx->stats.scan_redo += (uint64_t)redo;
     }
     return RSA_OK;
 }

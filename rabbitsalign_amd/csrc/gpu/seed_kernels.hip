@@ -61,6 +61,7 @@ struct HitD {
 #define SEED_E_POOL 1u      // the call's pool ran out: the host grows it and runs again
 #define SEED_E_FIND 2u      // robin_hood emulation overflow in the global-map pass
 #define SEED_E_RESCUE 4u    // the same in the rescue pass
+#define SEED_E_SITE 8u      // k_sites met a NAM whose nam_id is outside its read's list (a broken permutation)
 struct SeedHdr {
     unsigned long long pool_used;   // pool entries handed out
     unsigned long long total;       // final NAMs of the batch
@@ -1600,7 +1601,7 @@ __device__ bool site_kmer_eq(const char* ref, int64_t rlen, int64_t rpos, const 
 }
 
 __global__ void __launch_bounds__(256)
-k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read, const SeedHdr* __restrict__ hdr,
+k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read, SeedHdr* __restrict__ err_hdr,
         uint64_t cap, const uint64_t* __restrict__ ooff, const char* __restrict__ seq, const uint64_t* __restrict__ roff,
         const uint32_t* __restrict__ rlen, SeedIndexParams p, rsa_nam_site* __restrict__ sites,
         uint16_t* __restrict__ pool, uint64_t pool_cap, unsigned long long* __restrict__ pool_used) {
@@ -1609,7 +1610,7 @@ k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read,
     // a batch whose NAMs overflow the output was not compacted whole (k_compact skips
     // the reads past `cap`, so their nam_read entries were never written): no site
     // checks then -- the host reports RSA_ERR_CAPACITY and the caller asks again
-    const uint64_t total = (uint64_t)hdr->total <= cap ? (uint64_t)hdr->total : 0;
+    const uint64_t total = (uint64_t)err_hdr->total <= cap ? (uint64_t)err_hdr->total : 0;
     const int l16 = threadIdx.x & 15, grp = threadIdx.x >> 4;
     // a fixed grid walks the batch's NAMs, 16 a block per round (the count is known on the device only)
     for (uint64_t blk = blockIdx.x; blk * 16 < total; blk += gridDim.x) {
@@ -1694,8 +1695,10 @@ k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read,
         out.orig_query_start = nam.query_start;
         out.orig_query_end = nam.query_end;
         // at the NAM's index in its read's list as found (nam_id; the NAMs may come sorted)
+        // a nam_id outside the list would alias another NAM's slot: no write, the call fails
         const uint64_t ro = ooff[r], rn = ooff[r + 1] - ro;
-        sites[(nam.nam_id >= 0 && (uint64_t)nam.nam_id < rn) ? ro + (uint64_t)nam.nam_id : g] = out;
+        if (nam.nam_id >= 0 && (uint64_t)nam.nam_id < rn) sites[ro + (uint64_t)nam.nam_id] = out;
+        else atomicOr(&err_hdr->errors, SEED_E_SITE);
     }
     __syncthreads();                             // s_need / s_base / s_at are reused next round
     }
@@ -2052,6 +2055,7 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
         memcpy(&hh, hx, sizeof hh);
         if (hh.errors & SEED_E_FIND) { err = "rsa_seed: robin_hood emulation overflow"; return RSA_ERR_NOMEM; }
         if (hh.errors & SEED_E_RESCUE) { err = "rsa_seed: rescue map overflow"; return RSA_ERR_NOMEM; }
+        if (hh.errors & SEED_E_SITE) { err = "rsa_seed: site check for a NAM outside its read's list"; return RSA_ERR_INTERNAL; }
         if (hh.errors & SEED_E_POOL) {          // grow the pool and run the call again
             if (attempt >= 8) { err = "rsa_seed: seeding pool exhausted"; return RSA_ERR_NOMEM; }
             b.pool_n = std::max<uint64_t>(2 * b.pool_n, hh.pool_used + 1024);

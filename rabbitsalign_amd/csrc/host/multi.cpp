@@ -27,7 +27,7 @@ void add_stats(rsa_kernel_stats& a, const rsa_kernel_stats& b) {
     }
     uint64_t* au = &a.dp_cells_timed;
     const uint64_t* bu = &b.dp_cells_timed;
-    const size_t nu = (size_t)(&a.band_overflow - &a.dp_cells_timed) + 1;  // dp_cells_timed .. band_overflow
+    const size_t nu = (size_t)(&a.scan_redo - &a.dp_cells_timed) + 1;  // dp_cells_timed .. scan_redo
     for (size_t i = 0; i < nu; ++i) au[i] += bu[i];
     for (int i = 0; i < 2; ++i) {
         a.call_ms[i] += b.call_ms[i];

@@ -102,6 +102,7 @@ class KernelStats(C.Structure):
                 ("nams", C.c_uint64), ("rescued_reads", C.c_uint64),
                 ("jobs", C.c_uint64), ("dp_cells", C.c_uint64),
                 ("band_deferred", C.c_uint64), ("band_overflow", C.c_uint64),
+                ("scan_certified", C.c_uint64), ("scan_redo", C.c_uint64),
                 ("call_ms", C.c_double * 2), ("lane_wait_ms", C.c_double * 2), ("device_wait_ms", C.c_double * 2)]
 
 

@@ -212,3 +212,88 @@ def test_extend_grouped_and_wave_scans(ctx):
     c, ref, offs = ctx
     bad = _compare(c, ref, offs, 11, 3000, qlens=(150, 100, 250, 64, 129, 300))
     assert not bad, f"{len(bad)} mismatches, first: {bad[0]}"
+
+
+def _block_replacement_jobs(rng, ref, offs, n, L=250):
+    """Queries copied from their window with one block replaced (d bases deleted, e
+    random bases inserted at the same place, 1-25 each) and light substitutions:
+    the best path often has an insertion next to a deletion, which is where the
+    byte and word layouts of SSW may differ (k_ext_scan_v's certificate fails and
+    the job takes the two-layout re-run)."""
+    from jobgen import JOB_DTYPE, ACGT
+    queries = bytearray()
+    jobs = np.zeros(n, dtype=JOB_DTYPE)
+    pairs = []
+    for i in range(n):
+        c = int(rng.integers(0, len(offs) - 1))
+        clen = int(offs[c + 1] - offs[c])
+        rl = L + int(rng.integers(20, 150))
+        rs = int(rng.integers(0, clen - rl - 1))
+        win = ref[int(offs[c]) + rs:int(offs[c]) + rs + rl].copy()
+        a = int(rng.integers(0, 30))
+        cut = int(rng.integers(L // 4, 3 * L // 4))
+        d, e = int(rng.integers(1, 26)), int(rng.integers(1, 26))
+        q = np.concatenate([win[a:a + cut], ACGT[rng.integers(0, 4, e)], win[a + cut + d:]])[:L].copy()
+        subs = rng.random(len(q)) < 0.005
+        q[subs] = ACGT[rng.integers(0, 4, int(subs.sum()))]
+        if len(q) < L:
+            q = np.concatenate([q, ACGT[rng.integers(0, 4, L - len(q))]])
+        qb = bytes(q)
+        jobs[i] = (len(queries), len(qb), c, rs, rl)
+        queries += qb
+        pairs.append((qb, bytes(win)))
+    return bytes(queries), jobs, pairs
+
+
+@pytest.mark.gpu
+def test_extend_scan_certificate_and_redo(ctx):
+    """k_ext_scan_v takes the word layout on the word score alone and the band path
+    certifies it; jobs whose path puts an insertion next to a deletion are re-run
+    through the two-layout scan.  Both outcomes occur here and every result is
+    Aligner::align's."""
+    c, ref, offs = ctx
+    rng = np.random.default_rng(31)
+    queries, jobs, pairs = _block_replacement_jobs(rng, ref, offs, 1500)
+    c.reset_stats()
+    alns, pool = c.extend(queries, jobs)
+    bad = []
+    for i, (q, r) in enumerate(pairs):
+        o = oracle_lib.align(q, r)
+        a = alns[i]
+        got = dict(sw_score=int(a["sw_score"]), edit_distance=int(a["edit_distance"]), ref_start=int(a["ref_start"]),
+                   ref_end=int(a["ref_end"]), query_start=int(a["query_start"]), query_end=int(a["query_end"]),
+                   cigar=[int(x) for x in pool[int(a["cigar_offset"]):int(a["cigar_offset"]) + int(a["cigar_len"])]])
+        if got["sw_score"] < -1000:
+            for k in ("ref_end", "query_start", "query_end"):
+                got[k] = o[k]
+        if got != o:
+            bad.append((i, o, got))
+    assert not bad, f"{len(bad)} mismatches, first: {bad[0]}"
+    st = c.stats()
+    assert st["scan_certified"] > 1000 and st["scan_redo"] > 0, st
+
+
+@pytest.mark.gpu
+def test_extend_scan_v_equals_scan_g(ctx, monkeypatch):
+    """The virtual-lane scan (default) and the two-layout grouped scan (RSA_SCAN_V=0,
+    read when a context opens) give identical results on one mixed batch."""
+    from rabbitsalign_amd import native
+    c, ref, offs = ctx
+    rng = np.random.default_rng(41)
+    queries, jobs, _ = make_jobs(rng, ref, offs, 3000, (150, 100, 250, 64, 33, 129, 200))
+    q2, j2, _ = _block_replacement_jobs(rng, ref, offs, 300)
+    j2 = j2.copy()
+    j2["query_offset"] += len(queries)
+    queries, jobs = queries + q2, np.concatenate([jobs, j2])
+    a1, p1 = c.extend(queries, jobs)
+    monkeypatch.setenv("RSA_SCAN_V", "0")
+    c2 = native.GpuContext(native.empty_index(ref, offs))
+    try:
+        a2, p2 = c2.extend(queries, jobs)
+    finally:
+        c2.close()
+    assert (a1[["sw_score", "edit_distance", "ref_start", "ref_end", "query_start", "query_end", "cigar_len"]] ==
+            a2[["sw_score", "edit_distance", "ref_start", "ref_end", "query_start", "query_end", "cigar_len"]]).all()
+    for x, y in zip(a1, a2):
+        assert list(p1[x["cigar_offset"]:x["cigar_offset"] + x["cigar_len"]]) == \
+            list(p2[y["cigar_offset"]:y["cigar_offset"] + y["cigar_len"]])
