@@ -49,14 +49,18 @@ WORKLOADS = {
 }
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md "Chip-level parameters")
-# VALU ceilings of the DP scan (DESIGN.md §3 "Roofline reporting"), in cell updates/s with
-# SURVEY.md §8d's model of 12 ops per cell and 2 cells per packed op:
-#  - measured: 600 G wave64 VALU instructions/s chip-wide, the issue ceiling of independent
-#    packed-f16 / int32 streams at 4-8 waves per SIMD (scripts/micro/valu_lat.hip,
-#    profiles/r02_valu_ceiling.txt) -> 600e9 x 64 lanes x 2 / 12 = 6.4 T cells/s (the roofline peak);
-#  - spec model: 256 CUs x 128 lane-ops/clk x 2.4 GHz x 2 / 12 = 13.1 T cells/s (reported beside it)
-VALU_WAVE_INSTR_PER_S = 600e9
-DP_PEAK_GCELLS = VALU_WAVE_INSTR_PER_S * 64 * 2 / 12 / 1e9
+# VALU ceilings of the DP scan (DESIGN.md §3 "Roofline reporting"), in cell updates/s.
+# Measured issue cost on gfx950 (scripts/micro/valu_issue.hip, profiles/r04/valu_issue.txt,
+# 4 waves per SIMD): a wave64 VOP3/VOP3P instruction (v_pk_maximum3_f16, v_pk_add_f16,
+# v_max3_i32) 4.4 cycles, a VOP1/VOP2 one (v_add_u32, v_and_b32, v_add_f32) 2.35 cycles.
+#  - peak: SSW's recurrence is 11.5 packed-f16 instructions per row of two cells (diag add,
+#    three max3 for H/E/F, three gap decays, the gap-open term, the column max), i.e. 5.75
+#    VOP3P per cell: 1024 SIMDs x 2.4 GHz / 4.4 cycles x 64 lanes / 5.75 = 6.2 T cells/s;
+#  - spec model: 256 CUs x 128 lane-ops/clk x 2.4 GHz x 2 / 12 = 13.1 T
+#    cells/s -- it assumes packed instructions issue at the VOP2 rate, which gfx950 does not
+VOP3P_CYCLES, VOP2_CYCLES = 4.4, 2.35
+VALU_SIMDS, VALU_CLOCK = 1024, 2.4e9
+DP_PEAK_GCELLS = VALU_SIMDS * VALU_CLOCK / VOP3P_CYCLES * 64 / 5.75 / 1e9
 DP_SPEC_GCELLS = 256 * 128 * 2.4 * 2 / 12
 REF_CPU_LIB = os.path.join(ROOT, "oracle", "_ref", "librsalign_ref.so")
 
@@ -115,15 +119,17 @@ def host_cores(pinned: bool = False) -> int:
 
 
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "latest_traffic.json")
-EXT_PMC_JSON = os.path.join(ROOT, "profiles", "r03", "ext_pmc.json")
+EXT_PMC_JSON = os.path.join(ROOT, "profiles", "r04", "ext_pmc.json")
 
 
-def scan_instr_per_cell():
-    """wave64 VALU instructions per DP cell of k_ext_scan_g, from the committed PMC pass
-    (scripts/gpu_ext_pmc.sh: SQ_INSTS_VALU / cells of an isolated 22000-job launch), or None."""
+def scan_pmc(symbol: str):
+    """(wave64 VALU instructions per DP cell, VOP3P share) of the scan kernel from the
+    committed PMC pass (scripts/gpu_ext_pmc.sh: SQ_INSTS_VALU / cells of an isolated
+    22000-job launch), or None."""
     try:
         with open(EXT_PMC_JSON) as f:
-            return float(json.load(f)["k_ext_scan_g"]["wave_instr_per_cell"])
+            d = json.load(f)[symbol]
+        return float(d["wave_instr_per_cell"]), float(d.get("vop3p_share", 1.0))
     except (OSError, ValueError, KeyError):
         return None
 
@@ -164,21 +170,25 @@ def kernel_roofline(name: str, k: dict, ks: dict) -> dict:
         achieved = cells / avg_s / 1e9
         out.update({"bound": "valu", "achieved": round(achieved, 2), "peak": round(DP_PEAK_GCELLS, 1),
                     "unit": "Gcells/s", "frac": round(achieved / DP_PEAK_GCELLS, 5),
-                    "peak_source": "measured VALU issue ceiling, profiles/r02_valu_ceiling.txt",
+                    "peak_source": "measured VALU issue cost (4.4 cycles a wave64 VOP3P instruction, "
+                                   "profiles/r04/valu_issue.txt) x 5.75 packed instructions a cell",
                     "spec_model": {"peak": round(DP_SPEC_GCELLS, 1),
                                    "frac": round(achieved / DP_SPEC_GCELLS, 5)},
                     "cells_per_launch": round(cells, 1),
                     "hbm_GBps": round(per_launch_bytes / avg_s / 1e9, 3)})
-        ipc = scan_instr_per_cell()
-        if ipc:
+        pm = scan_pmc(sym)
+        if pm:
             # what the kernel as written issues: its VALU instructions per cell (PMC) times the
-            # live cell rate, against the chip's VALU issue ceiling -- the bound it runs into
-            issued = achieved * ipc
-            out["valu_issue"] = {"wave_instr_per_cell": ipc, "achieved": round(issued, 2),
-                                 "peak": VALU_WAVE_INSTR_PER_S / 1e9, "unit": "G wave64 VALU instr/s",
-                                 "frac": round(issued * 1e9 / VALU_WAVE_INSTR_PER_S, 4),
-                                 "cells_ceiling_Gcells": round(VALU_WAVE_INSTR_PER_S / 1e9 / ipc, 1),
-                                 "source": "profiles/r03/ext_pmc.json"}
+            # live cell rate, against the issue ceiling of its VOP3P / VOP2 instruction mix
+            ipc, share = pm
+            cyc = share * VOP3P_CYCLES + (1 - share) * VOP2_CYCLES
+            ceiling = VALU_SIMDS * VALU_CLOCK / cyc
+            issued = achieved * 1e9 * ipc
+            out["valu_issue"] = {"wave_instr_per_cell": ipc, "vop3p_share": share,
+                                 "achieved": round(issued / 1e9, 2), "peak": round(ceiling / 1e9, 1),
+                                 "unit": "G wave64 VALU instr/s", "frac": round(issued / ceiling, 4),
+                                 "cells_ceiling_Gcells": round(ceiling / ipc / 1e9, 1),
+                                 "source": "profiles/r04/ext_pmc.json"}
     else:
         achieved = per_launch_bytes / avg_s / 1e9
         out.update({"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -204,7 +214,7 @@ KERNEL_LIMITER = {
 
 
 def roofline(ks: dict, elapsed: float) -> dict:
-    """Roofline object: the extension scan k_ext_scan_g (the path's compute kernel), plus
+    """Roofline object: the extension scan (k_ext_scan_v by default: the path's compute kernel), plus
     the three kernels with the largest device time over all calls and the whole path's
     HBM view."""
     kern = {n: k for n, k in ks["kernels"].items() if k["launches"] and k["ms"] > 0}
@@ -218,7 +228,7 @@ def roofline(ks: dict, elapsed: float) -> dict:
         calls, timed = (("ext_calls", "ext_calls_timed") if n in EXT_KERNELS else ("seed_calls", "seed_calls_timed"))
         return ks.get(calls, 0) / max(1, ks.get(timed, 0))
     top = sorted(kern, key=lambda n: -kern[n]["ms"] * scale(n))
-    # the headline kernel is the extension scan (k_ext_scan_g: the path's compute kernel and
+    # the headline kernel is the extension scan (k_ext_scan_v: the path's compute kernel and
     # the largest in the isolated kernel trace, profiles/r03m_rocprof.md).  In the bench its
     # in-bench device time ties with the seeding kernels', whose launches are inflated by
     # waiting behind the high-priority extension streams, so the in-bench
@@ -321,7 +331,13 @@ def self_launch(args) -> int:
     from rabbitsalign_amd import launch
     me = os.path.abspath(__file__)
     n_vis = launch.visible_gpus()
-    if n_vis < args.gpus:
+    # RSA_BENCH_REHEARSE=1: rehearse the N-rank path on fewer GPUs (every rank on GPU 0, a
+    # gloo process group since RCCL refuses two ranks on one device); the line says so
+    rehearse = os.environ.get("RSA_BENCH_REHEARSE") == "1"
+    if rehearse and n_vis >= 1:
+        log(0, f"rehearsal: {args.gpus} ranks share GPU 0 (gloo process group); not a scaling measurement")
+        os.environ.setdefault("RSA_BENCH_DEVICES", ",".join("0" * args.gpus))
+    elif n_vis < args.gpus:
         log(0, f"error: {args.gpus} GPUs requested, {n_vis} visible; nothing was run")
         return 2
     log(0, f"launching {args.gpus} ranks (torch.distributed.run, one process per GPU)")
@@ -483,9 +499,14 @@ def main():
     has_gpu = torch.cuda.is_available()
     if not has_gpu:
         raise SystemExit("bench.py needs a GPU (the product path has no CPU fallback)")
-    torch.cuda.set_device(local_rank)
+    rehearse = os.environ.get("RSA_BENCH_REHEARSE") == "1"
+    device = 0 if rehearse else local_rank
+    torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     def barrier():
         if world > 1:
@@ -494,7 +515,7 @@ def main():
     t = time.time()
     log(rank, f"building {wl['ref_len']/1e9:.3f} Gb reference ({wl['n_contigs']} contigs) + index; "
               f"host cores for this rank {cores}, pipeline threads {threads}")
-    m = M.Mapper.synthetic(args.ref_seed, wl["ref_len"], wl["n_contigs"], wl["read_len"], device=local_rank,
+    m = M.Mapper.synthetic(args.ref_seed, wl["ref_len"], wl["n_contigs"], wl["read_len"], device=device,
                            threads=threads)
     info = m.info()
     log(rank, f"index ready in {time.time()-t:.1f} s: {info['n_randstrobes']} randstrobes, bits {info['bits']}, "
@@ -694,7 +715,7 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             # the DP's arithmetic: exact small integers in packed f16 (forward scan) and int32
             # (reverse pass, band traceback); hashing and lookups in 64-bit integers
-            "dtype": "int32+f16x2(exact int)",
+            "dtype": "int: exact integers in packed f16x2 (SSW scan) and int32 (bands, seeding)",
             "data": "synthetic (seeded reference + reads, SURVEY.md Appendix D)",
             "config": {"workload": wl["desc"], "reference_bp": wl["ref_len"], "contigs": wl["n_contigs"],
                        "read_len": wl["read_len"], "paired": wl["paired"], "pairs_per_step_per_gpu": P,
@@ -707,6 +728,8 @@ def main():
                             "note": "StrobemerIndex::populate (index.cpp:141-309) via rsa_index_build_run; the "
                                     "index stays in HBM and the engine adopts it (rsa_open_built)"},
             "roofline": rl,
+            **({"rehearsal": "RSA_BENCH_REHEARSE=1: every rank on GPU 0 with a gloo process group -- "
+                             "exercises the N-rank path, not a scaling measurement"} if rehearse else {}),
             "cpu_baseline": cpu,
             "in_memory": in_memory,
             "io": {"dir": io_dir, "fastq_bytes_per_set": fq_bytes // n_sets, "read_sets": n_sets,

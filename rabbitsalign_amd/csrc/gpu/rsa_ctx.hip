@@ -402,7 +402,10 @@ uint64_t rsa_extend_cigar_bound(const rsa_job_batch* jb) {
 // the raw traceback ops
 static const int64_t BIG_DIR_CAP = 16ll << 20;
 static const int BIG_CHUNK = 32;
-static const int BAND64_GRID = 512;        // waves draining the band16 deferral queue
+// waves draining the band16 deferral queue: k_ext_band64 holds 35 KB of LDS, so a CU
+// keeps 4 of them (one a SIMD) and 1024 cover the chip; a wave past the queue's end exits
+// at once (PE 2x250 defers ~15 % of its jobs: 512 waves left half the SIMDs idle)
+static const int BAND64_GRID = 1024;
 static const uint64_t DENSE_GUESS = 24;    // CIGAR ops per job copied before the total is known
 
 static int64_t band_stride(int64_t dir_cap) {
@@ -571,7 +574,11 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
             if (cls[i] < 0) ord[rest_at++] = (int)i;
             else ord[cnt[(size_t)cls[i] * (maxr + 1) + (maxr - hj[i].rlen)]++] = (int)i;
         }
-        if (use_v) for (int c = 0; c < ncls; ++c) P.certified += cls_n[c];
+        // certified: word results k_ext_scan_v may take on the word score alone (queries that can
+        // reach the byte bound; shorter ones run the byte layout only)
+        if (use_v)
+            for (uint32_t i = 0; i < n; ++i)
+                if (cls[i] >= 0 && (int64_t)jb->match * hj[i].qlen + jb->mismatch >= 255) P.certified++;
     } else {
         rest_n = n;
         for (uint32_t i = 0; i < n; ++i) ord[i] = (int)i;

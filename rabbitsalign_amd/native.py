@@ -85,8 +85,10 @@ class AlnBatch(C.Structure):
 
 KERNELS = ["randstrobes", "lookup", "find_nams", "rescue", "compact", "ext_scan", "ext_band", "ext_band_wide",
            "ext_band_panel", "sites"]
+# the extension scan is k_ext_scan_v unless RSA_SCAN_V=0 selects the two-layout k_ext_scan_g (rsa_ctx.hip)
+SCAN_SYMBOL = "k_ext_scan_g" if os.environ.get("RSA_SCAN_V", "1")[:1] == "0" else "k_ext_scan_v"
 KERNEL_SYMBOLS = {"randstrobes": "k_rs_wave", "lookup": "k_lookup", "find_nams": "k_find_nams_w2",
-                  "rescue": "k_rescue_w", "compact": "k_compact", "ext_scan": "k_ext_scan_g", "ext_band": "k_ext_band16",
+                  "rescue": "k_rescue_w", "compact": "k_compact", "ext_scan": SCAN_SYMBOL, "ext_band": "k_ext_band16",
                   "ext_band_wide": "k_ext_band64", "ext_band_panel": "k_ext_band_panel",
                   "sites": "k_sites"}
 NK = len(KERNELS)

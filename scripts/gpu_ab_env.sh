@@ -13,7 +13,7 @@ for i in $(seq 1 ${REPS:-2}); do
   for setting in "$@"; do
     k=$((k + 1))
     env $setting timeout -k 10 300 python bench.py --no-cpu-baseline --steps ${STEPS:-10} > $O/b_${k}_$i.json 2> $O/b_${k}_$i.err || exit $?
-    python -c "import json;d=json.load(open('$O/b_${k}_$i.json'));print(json.dumps({'setting':'$setting','rep':$i,'value':d['value'],'in_memory':d.get('in_memory',{}).get('value'),'ms_per_step':d['ms_per_step'],'host_cpu':d.get('host_cpu')}))" | tee -a $O/ab.jsonl
+    python -c "import json;d=json.load(open('$O/b_${k}_$i.json'));print(json.dumps({'setting':'$setting','rep':$i,'value':d['value'],'in_memory':d.get('in_memory',{}).get('value'),'ms_per_step':d['ms_per_step'],'scan_Gcells':d['roofline'].get('achieved'),'scan_us':d['roofline'].get('avg_launch_us'),'core_us':d.get('host_cpu',{}).get('core_us_per_read')}))" | tee -a $O/ab.jsonl
   done
 done
 echo "exit 0"

@@ -7,6 +7,9 @@
 //   cold   : write() of 200 distinct chunks filled beforehand (source out of cache, as the
 //            writer thread finds the chunks other workers formatted)
 //   coldB  : the same while B background threads copy memory (a busy host)
+//   --direct: T threads pwrite() 8 MiB blocks at disjoint offsets of one file, with O_DIRECT
+//            (aligned source blocks, no page cache, no inode lock held across the copy) and
+//            buffered (for comparison); the file is fsync'ed in neither mode's timing
 // Build: g++ -O2 -pthread sam_sink_bw.cpp -o /tmp/sam_sink_bw ; run: sam_sink_bw DIR...
 #include <fcntl.h>
 #include <sys/mman.h>
@@ -101,7 +104,50 @@ static double by_write_cold(const std::string& path, const std::vector<std::vect
     return kTotal / dt / 1e9;
 }
 
+static double by_pwrite(const std::string& path, int threads, bool direct, size_t blk, size_t nblk, char* src) {
+    int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC | (direct ? O_DIRECT : 0), 0644);
+    if (fd < 0) { perror("open"); return 0; }
+    const double t = now();
+    std::vector<std::thread> ws;
+    std::vector<int> bad(threads, 0);
+    for (int w = 0; w < threads; ++w)
+        ws.emplace_back([&, w] {
+            for (size_t i = (size_t)w; i < nblk; i += (size_t)threads) {
+                size_t off = 0;
+                while (off < blk) {
+                    ssize_t r = pwrite(fd, src + (i % 16) * blk + off, blk - off, (off_t)(i * blk + off));
+                    if (r <= 0) { bad[w] = 1; return; }
+                    off += (size_t)r;
+                }
+            }
+        });
+    for (auto& x : ws) x.join();
+    const double dt = now() - t;
+    close(fd);
+    unlink(path.c_str());
+    for (int b : bad) if (b) { perror("pwrite"); return 0; }
+    return (double)blk * nblk / dt / 1e9;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && std::string(argv[1]) == "--direct") {
+        const size_t blk = 8u << 20, nblk = 96;   // 768 MiB, the size of a bench step's SAM
+        char* src = nullptr;
+        if (posix_memalign((void**)&src, 4096, 16 * blk) != 0) return 1;
+        for (size_t i = 0; i < 16 * blk; ++i) src[i] = (char)('A' + (i * 7919) % 26);
+        for (int a = 2; a < argc; ++a) {
+            const std::string p = std::string(argv[a]) + "/ssbw_" + std::to_string(getpid());
+            for (int rep = 0; rep < 2; ++rep) {
+                printf("%s:", argv[a]);
+                for (int t : {1, 2, 4, 8, 16}) printf(" direct%d %.2f", t, by_pwrite(p, t, true, blk, nblk, src));
+                for (int t : {1, 4, 16}) printf(" buffered%d %.2f", t, by_pwrite(p, t, false, blk, nblk, src));
+                printf(" GB/s\n");
+                fflush(stdout);
+            }
+        }
+        free(src);
+        return 0;
+    }
     if (argc > 1 && std::string(argv[1]) == "--cold") {
         std::vector<std::vector<char>> bufs(kN, std::vector<char>(kChunk));
         for (auto& b : bufs) for (size_t i = 0; i < kChunk; i += 64) b[i] = 'A';
