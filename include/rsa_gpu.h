@@ -122,7 +122,12 @@ enum {
     RSA_SITE_ORIENT_MASK = 3,    /* 0 consistent as is, 1 consistent once reversed, 2 inconsistent */
     RSA_SITE_HAMMING = 4,        /* (reversed if 1) projection is read-length and consistent: n_mm = Hamming distance */
     RSA_SITE_POSITIONS = 8,      /* n_mm / read length < 0.05 and mm_pool[mm_offset .. + n_mm) holds the positions */
-    RSA_SITE_POOL_FULL = 16      /* as 8, but the pool was too small: the positions were not stored */
+    RSA_SITE_POOL_FULL = 16,     /* as 8, but the pool was too small: the positions were not stored */
+    RSA_SITE_ALIGNED = 32        /* with 8 (rsa_nam_batch.hamming_align set): mm_pool[mm_offset ..] holds
+                                  * hamming_align's result (aligner.cpp:219-302) instead of the positions:
+                                  * u16 words [score lo, score hi, segment start, segment end, mismatches in
+                                  * the segment, n_ops], then n_ops CIGAR ops (len<<4|op) as (lo, hi) pairs;
+                                  * 12 + 4 n_mm words at most */
 };
 /* One per NAM, at the NAM's nam_id within its read's list (sites + offsets[i] +
  * nam_id: the index the NAM had in find_nams' / find_nams_rescue's list, whatever
@@ -158,6 +163,9 @@ typedef struct rsa_nam_batch {
     uint64_t mm_capacity;
     uint64_t mm_used;            /* out */
     uint32_t order;              /* RSA_NAMS_FOUND (0) or RSA_NAMS_BY_SCORE */
+    uint32_t hamming_align;      /* 1: sites accepted by the Hamming test get hamming_align's result
+                                  * (RSA_SITE_ALIGNED) with the scores below, not their positions */
+    int32_t match, mismatch, end_bonus;   /* -A -B -L, for hamming_align */
     uint32_t pad_;
 } rsa_nam_batch;
 

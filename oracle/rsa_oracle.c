@@ -1107,3 +1107,44 @@ int ora_nam_site(const ora_nam* nam, const char* read, const char* read_rc, int 
     }
     return flags;
 }
+
+/* hamming_align (src/aligner.cpp:254-302) with highest_scoring_segment
+ * (aligner.cpp:219-252), restated per position as the reference runs them:
+ * query and ref of equal length n.  Writes the CIGAR ops (len<<4|op, Cigar::push
+ * merging) to cigar and returns their count; *score, *start, *end (the segment,
+ * half-open) and *mismatches (inside it) as AlignmentInfo holds them. */
+int ora_hamming_align(const char* query, const char* ref, int n, int match, int mismatch, int end_bonus,
+                      int* score_out, int* start_out, int* end_out, int* mismatches_out, uint32_t* cigar) {
+    int start = 0, score = end_bonus, best_start = 0, best_end = 0, best_score = 0;
+    for (int i = 0; i < n; ++i) {
+        if (query[i] == ref[i]) score += match;
+        else score -= mismatch;
+        if (score < 0) { start = i + 1; score = 0; }
+        if (score > best_score) { best_start = start; best_score = score; best_end = i + 1; }
+    }
+    if (score + end_bonus > best_score) { best_score = score + end_bonus; best_end = n; best_start = start; }
+    int nc = 0;
+#define ORA_PUSH(op, len) do { uint32_t o_ = (op), l_ = (uint32_t)(len); \
+        if (nc == 0 || (cigar[nc - 1] & 0xf) != o_) cigar[nc++] = (l_ << 4) | o_; else cigar[nc - 1] += l_ << 4; } while (0)
+    if (best_start > 0) ORA_PUSH(4, best_start);
+    int counter = 0, prev_is_match = 0, mismatches = 0, first = 1;
+    for (int i = best_start; i < best_end; i++) {
+        const int is_match = query[i] == ref[i];
+        mismatches += is_match ? 0 : 1;
+        if (!first && is_match != prev_is_match) {
+            ORA_PUSH(prev_is_match ? 7 : 8, counter);
+            counter = 0;
+        }
+        counter++;
+        prev_is_match = is_match;
+        first = 0;
+    }
+    if (!first) ORA_PUSH(prev_is_match ? 7 : 8, counter);
+    if (n - best_end > 0) ORA_PUSH(4, n - best_end);
+#undef ORA_PUSH
+    *score_out = best_score;
+    *start_out = best_start;
+    *end_out = best_end;
+    *mismatches_out = mismatches;
+    return nc;
+}

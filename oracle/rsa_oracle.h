@@ -106,6 +106,11 @@ typedef struct ora_aln_info {   /* AlignmentInfo (aligner.hpp:20-30) */
 void ora_aligner_align(const char* query, int qlen, const char* ref, int rlen, int match, int mismatch,
                        int gap_open, int gap_extend, int end_bonus, ora_aln_info* out, uint32_t* cigar);
 
+/* hamming_align (aligner.cpp:219-302) on equal-length query/ref: CIGAR ops in cigar
+ * (>= 2n + 3 entries), their count returned */
+int ora_hamming_align(const char* query, const char* ref, int n, int match, int mismatch, int end_bonus,
+                      int* score, int* start, int* end, int* mismatches, uint32_t* cigar);
+
 #ifdef __cplusplus
 }
 #endif

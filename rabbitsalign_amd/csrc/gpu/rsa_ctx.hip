@@ -405,7 +405,11 @@ static const int BIG_CHUNK = 32;
 // waves draining the band16 deferral queue: k_ext_band64 holds 35 KB of LDS, so a CU
 // keeps 4 of them (one a SIMD) and 1024 cover the chip; a wave past the queue's end exits
 // at once (PE 2x250 defers ~15 % of its jobs: 512 waves left half the SIMDs idle)
-static const int BAND64_GRID = 1024;
+static const int BAND64_GRID_DEFAULT = 1024;
+static int band64_grid() {                          // RSA_BAND64_GRID overrides (A/B)
+    static const int g = getenv("RSA_BAND64_GRID") ? std::max(1, atoi(getenv("RSA_BAND64_GRID"))) : BAND64_GRID_DEFAULT;
+    return g;
+}
 static const uint64_t DENSE_GUESS = 24;    // CIGAR ops per job copied before the total is known
 
 static int64_t band_stride(int64_t dir_cap) {
@@ -624,7 +628,7 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
     HIPCHK(hipGetLastError());
     L->kt.end(st);
     L->kt.begin(st, RSA_K_EXT_BAND_WIDE);
-    launch_ext_band64(dim3(std::min<uint32_t>(n, BAND64_GRID)), st, L->d_jobs.as<ExtJobDev>(),
+    launch_ext_band64(dim3(std::min<uint32_t>(n, (uint32_t)band64_grid())), st, L->d_jobs.as<ExtJobDev>(),
                       L->d_scan.as<ScanRes>(), L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(),
                       L->d_raw.as<uint32_t>(), L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open,
                       jb->gap_extend, jb->end_bonus, L->d_queue.as<int>(), &dst->qcount, L->d_over.as<int>(),
@@ -715,7 +719,7 @@ static int ext_finish(rsa_pending& P) {
         HIPCHK(hipGetLastError());
         L->kt.end(st);
         L->kt.begin(st, RSA_K_EXT_BAND_WIDE);
-        launch_ext_band64(dim3(std::min(redo, BAND64_GRID)), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(),
+        launch_ext_band64(dim3(std::min(redo, band64_grid())), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(),
                           L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(),
                           L->d_alns.as<rsa_aln>(), P.match, P.mismatch, P.gap_open, P.gap_extend, P.end_bonus,
                           L->d_queue.as<int>(), &P.d_status->qcount, L->d_over.as<int>(), &P.d_status->ocount,

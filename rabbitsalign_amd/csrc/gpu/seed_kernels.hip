@@ -1604,7 +1604,8 @@ __global__ void __launch_bounds__(256)
 k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read, SeedHdr* __restrict__ err_hdr,
         uint64_t cap, const uint64_t* __restrict__ ooff, const char* __restrict__ seq, const uint64_t* __restrict__ roff,
         const uint32_t* __restrict__ rlen, SeedIndexParams p, rsa_nam_site* __restrict__ sites,
-        uint16_t* __restrict__ pool, uint64_t pool_cap, unsigned long long* __restrict__ pool_used) {
+        uint16_t* __restrict__ pool, uint64_t pool_cap, unsigned long long* __restrict__ pool_used, int ham,
+        int h_match, int h_mismatch, int h_bonus) {
     __shared__ uint32_t s_need[16], s_base[16];
     __shared__ unsigned long long s_at;
     // a batch whose NAMs overflow the output was not compacted whole (k_compact skips
@@ -1660,8 +1661,10 @@ k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read,
             want = (double)((float)hd / (float)rd.len) < 0.05;
         }
     }
-    // pool space: a block-wide prefix over its 16 NAMs and one atomic per block
-    if (l16 == 0) s_need[grp] = (want && valid) ? hd : 0;
+    // pool space: a block-wide prefix over its 16 NAMs and one atomic per block (positions:
+    // n_mm words; hamming_align's result: a 6-word header and at most 2 n_mm + 3 ops of 2 words)
+    const uint32_t need = ham ? 12u + 4u * hd : hd;
+    if (l16 == 0) s_need[grp] = (want && valid) ? need : 0;
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t acc = 0;
@@ -1671,7 +1674,7 @@ k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read,
     __syncthreads();
     if (want) {
         const unsigned long long at = s_at + s_base[grp];
-        if (at + hd <= pool_cap) {
+        if (at + need <= pool_cap && !ham) {
             flags |= RSA_SITE_POSITIONS;
             mm_off = (uint32_t)at;
             uint32_t m = 0;
@@ -1681,6 +1684,82 @@ k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read,
                 const uint32_t bits = grp_ballot(mis);
                 if (mis && valid) pool[at + m + __popc(bits & ((1u << l16) - 1))] = (uint16_t)i;
                 m += __popc(bits);
+            }
+        } else if (at + need <= pool_cap) {
+            // hamming_align (aligner.cpp:219-302) over the window just tested: the group walks
+            // the mismatch positions in order (16-base ballots) twice, every lane computing the
+            // same values; lane 0 writes the result
+            flags |= RSA_SITE_POSITIONS | RSA_SITE_ALIGNED;
+            mm_off = (uint32_t)at;
+            const int64_t n = rd.len;
+            // 1. highest_scoring_segment (aligner.cpp:219-252), run by run: between mismatches
+            //    the score only grows, so each run of matches needs one check at its end
+            int64_t start = 0, best_start = 0, best_end = 0, i = 0;
+            int score = h_bonus, best = 0;
+            for (int64_t i0 = 0; i0 < n; i0 += 16) {
+                const int64_t x = i0 + l16;
+                uint32_t bits = grp_ballot(x < n && (unsigned char)ref[ps + x] != rd.at(is_rc, x));
+                while (bits) {
+                    const int64_t m = i0 + __builtin_ctz(bits);
+                    bits &= bits - 1;
+                    if (m > i) {
+                        score += h_match * (int)(m - i);
+                        if (score > best) { best_start = start; best = score; best_end = m; }
+                    }
+                    score -= h_mismatch;
+                    if (score < 0) { start = m + 1; score = 0; }
+                    if (score > best) { best_start = start; best = score; best_end = m + 1; }
+                    i = m + 1;
+                }
+            }
+            if (n > i) {
+                score += h_match * (int)(n - i);
+                if (score > best) { best_start = start; best = score; best_end = n; }
+            }
+            if (score + h_bonus > best) { best = score + h_bonus; best_end = n; best_start = start; }
+            // 2. the CIGAR (S, =/X runs of the segment, S) with Cigar::push's merging, and the
+            //    mismatches inside the segment
+            uint32_t n_ops = 0, last = 0, ed = 0;
+            bool have = false;
+            auto push = [&](uint32_t op, uint32_t len) {
+                if (have && (last & 0xf) == op) { last += len << 4; return; }
+                if (have && l16 == 0 && valid) {
+                    pool[at + 6 + 2 * n_ops] = (uint16_t)(last & 0xFFFF);
+                    pool[at + 7 + 2 * n_ops] = (uint16_t)(last >> 16);
+                }
+                n_ops += have ? 1 : 0;
+                last = (len << 4) | op;
+                have = true;
+            };
+            if (best_start > 0) push(4, (uint32_t)best_start);
+            int64_t cur = best_start;
+            for (int64_t i0 = 0; i0 < best_end; i0 += 16) {
+                const int64_t x = i0 + l16;
+                uint32_t bits = grp_ballot(x < best_end && x >= best_start &&
+                                           (unsigned char)ref[ps + x] != rd.at(is_rc, x));
+                while (bits) {
+                    const int64_t m = i0 + __builtin_ctz(bits);
+                    bits &= bits - 1;
+                    if (m > cur) push(7, (uint32_t)(m - cur));
+                    push(8, 1);
+                    ed++;
+                    cur = m + 1;
+                }
+            }
+            if (best_end > cur) push(7, (uint32_t)(best_end - cur));
+            if (n - best_end > 0) push(4, (uint32_t)(n - best_end));
+            if (have && l16 == 0 && valid) {
+                pool[at + 6 + 2 * n_ops] = (uint16_t)(last & 0xFFFF);
+                pool[at + 7 + 2 * n_ops] = (uint16_t)(last >> 16);
+            }
+            n_ops += have ? 1 : 0;
+            if (l16 == 0 && valid) {
+                pool[at + 0] = (uint16_t)((uint32_t)best & 0xFFFF);
+                pool[at + 1] = (uint16_t)((uint32_t)best >> 16);
+                pool[at + 2] = (uint16_t)best_start;
+                pool[at + 3] = (uint16_t)best_end;
+                pool[at + 4] = (uint16_t)ed;
+                pool[at + 5] = (uint16_t)n_ops;
             }
         } else {
             flags |= RSA_SITE_POOL_FULL;
@@ -2038,7 +2117,8 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
             const uint32_t grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1, (cap + 15) / 16), 4096);
             hipLaunchKernelGGL(k_sites, dim3(grid), dim3(256), 0, st, DP(B_OUT, rsa_nam), DP(B_NREAD, uint32_t), dhdr,
                                cap, d_ooff, DP(B_SEQ, char), d_roff, d_rlen, p, DP(B_SITES, rsa_nam_site), DP(B_POOL, uint16_t),
-                               out->mm_capacity, &dhdr->mm_used);
+                               out->mm_capacity, &dhdr->mm_used, out->hamming_align ? 1 : 0, out->match, out->mismatch,
+                               out->end_bonus);
             SCHK(hipGetLastError());
             kt.end(st);
         }
@@ -2046,7 +2126,9 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
         SCHK(hipMemcpyAsync(hx, dx, X.down, hipMemcpyDeviceToHost, st));
         const uint64_t guess = std::min<uint64_t>(cap, 8ull * n + 1024);
         SCHK(hipMemcpyAsync(out->nams, b.p[B_OUT], sizeof(rsa_nam) * guess, hipMemcpyDeviceToHost, st));
-        const uint64_t mm_guess = out->sites ? std::min<uint64_t>(out->mm_capacity, guess) : 0;
+        // pool words copied before the total is known: ~1 accepted site a read, n_mm words each,
+        // or 12 + 4 n_mm with hamming_align's results
+        const uint64_t mm_guess = out->sites ? std::min<uint64_t>(out->mm_capacity, (out->hamming_align ? 3 : 1) * guess) : 0;
         if (out->sites) {
             SCHK(hipMemcpyAsync(out->sites, b.p[B_SITES], sizeof(rsa_nam_site) * guess, hipMemcpyDeviceToHost, st));
             if (mm_guess) SCHK(hipMemcpyAsync(out->mm_pool, b.p[B_POOL], 2 * mm_guess, hipMemcpyDeviceToHost, st));

@@ -438,7 +438,18 @@ static bool extend_seed_part(AlignTmpRes& res, const AlignmentParameters& ap, co
     bool gapped = true;
     const rsa_nam_site* st = consistent_nam ? read.site.find(nam) : nullptr;
     if (st && !(st->flags & RSA_SITE_POOL_FULL)) {         // the GPU checked this window (k_sites)
-        if (st->flags & RSA_SITE_POSITIONS) {
+        if (st->flags & RSA_SITE_ALIGNED) {                   // ... and ran hamming_align on it
+            const uint16_t* w = read.site.pool + st->mm_offset;
+            info.sw_score = (int)((uint32_t)w[0] | ((uint32_t)w[1] << 16));
+            info.ref_start = info.query_start = w[2];
+            info.ref_end = info.query_end = w[3];
+            info.edit_distance = w[4];
+            const uint32_t n_ops = w[5];
+            for (uint32_t k = 0; k < n_ops; ++k)
+                info.cigar.ops.push_back((uint32_t)w[6 + 2 * k] | ((uint32_t)w[7 + 2 * k] << 16));
+            result_ref_start = projected_ref_start + (int)info.ref_start;
+            gapped = false;
+        } else if (st->flags & RSA_SITE_POSITIONS) {
             int mm[64];
             std::vector<int> big;
             int* pos = mm;

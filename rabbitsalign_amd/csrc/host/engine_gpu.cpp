@@ -2,6 +2,7 @@
 // HIP C-ABI (include/rsa_gpu.h, librsa_gpu.so).  There is no CPU fallback;
 // a failed GPU call aborts the run with the library's error message.
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <exception>
 #include <cstdlib>
@@ -73,6 +74,11 @@ public:
         idx.bucket_starts.swap(st);
         return true;
     }
+    void set_alignment_params(const AlignmentParameters& p) override {
+        ap_ = p;
+        ap_set_.store(true, std::memory_order_release);
+    }
+
     ~GpuEngine() override {
         free_.clear();
         staging_.clear();                  // pinned buffers go before the context
@@ -132,16 +138,21 @@ public:
         // site checks on the device (k_sites): the host's NAM orientation and
         // Hamming windows then never read the reference
         static const bool want_sites = !(getenv("RSA_SITES") && getenv("RSA_SITES")[0] == '0');   // A/B switch
+        // hamming_align on the device too (RSA_SITE_ALIGNED, RSA_SITE_ALIGN=0: positions only)
+        static const bool align_env = !(getenv("RSA_SITE_ALIGN") && getenv("RSA_SITE_ALIGN")[0] == '0');
+        const bool hamming_on = align_env && ap_set_.load(std::memory_order_acquire);
         size_t cap = std::max<size_t>(1024, 12 * n);
         for (;;) {
-            const size_t mm_cap = 4 * cap;           // overflow is flagged per NAM and handled on the host
+            // 12 + 4 n_mm words an accepted site at most (n_mm < 5 % of the read): overflow is
+            // flagged per NAM and handled on the host
+            const size_t mm_cap = (hamming_on ? 16 : 4) * cap;
             out.nams.resize(cap);
             out.sites.resize(want_sites ? cap : 0);
             out.mm_pool.resize(mm_cap);
             // lists of <= 16 NAMs come sorted (RSA_NAMS_BY_SCORE): part() works on them in place
             rsa_nam_batch nb{out.nams.data(), cap, out.offsets.data(), out.nonrep.data(), out.rescued.data(), 0,
                              want_sites ? out.sites.data() : nullptr, out.mm_pool.data(), mm_cap, 0,
-                             RSA_NAMS_BY_SCORE, 0};
+                             RSA_NAMS_BY_SCORE, hamming_on ? 1u : 0u, ap_.match, ap_.mismatch, ap_.end_bonus, 0};
             int rc = rsa_seed(ctx_, &rb, rescue_level, rescue_cutoff, &nb);
             if (rc == RSA_ERR_CAPACITY) { cap = nb.needed + 16; continue; }
             if (rc != RSA_OK) throw std::runtime_error(std::string("rsa_seed: ") + rsa_last_error(ctx_));
@@ -315,6 +326,8 @@ private:
     rsa_ctx* ctx_ = nullptr;
     std::mutex staging_m_;
     std::vector<std::unique_ptr<Staging>> staging_;
+    AlignmentParameters ap_;                    // hamming_align's scores (set_alignment_params)
+    std::atomic<bool> ap_set_{false};
     std::vector<Staging*> free_;
 };
 

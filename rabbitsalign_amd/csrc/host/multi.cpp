@@ -75,6 +75,9 @@ public:
     }
     void reset_kernel_stats() override { for (auto& e : e_) e->reset_kernel_stats(); }
     bool download_index(StiIndex& idx) override { return e_[0]->download_index(idx); }
+    void set_alignment_params(const AlignmentParameters& p) override {
+        for (auto& e : e_) e->set_alignment_params(p);
+    }
 
 private:
     struct Hold {                       // the least busy engine, counted busy for the call

@@ -634,6 +634,7 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
                                SamSink sink, void* user) {
     const auto t0 = Clock::now();
     PipelineResult result;
+    eng.set_alignment_params(mc.aparams);     // hamming_align with the site checks (GPU engine)
     OrderedSink os(sink, user, opt.digest);
     const int T = std::max(1, opt.threads);
     const bool offl = eng.offloads();
@@ -947,6 +948,7 @@ PipelineResult run_pipeline_se(ReadSource& src, Engine& eng, const MapContext& m
                                SamSink sink, void* user) {
     auto t0 = std::chrono::steady_clock::now();
     PipelineResult result;
+    eng.set_alignment_params(mc.aparams);
     OrderedSink os(sink, user, opt.digest);
     std::atomic<size_t> next{0};
     std::mutex stat_m;

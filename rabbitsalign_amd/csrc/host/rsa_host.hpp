@@ -427,6 +427,9 @@ public:
     virtual void reset_kernel_stats() {}
     // the host copy of an index the engine holds on its device (GPU engine only)
     virtual bool download_index(StiIndex&) { return false; }
+    // the scores hamming_align runs with, for an engine that computes it with the site
+    // checks (GPU engine: RSA_SITE_ALIGNED); set before the first seeding call
+    virtual void set_alignment_params(const AlignmentParameters&) {}
 };
 
 // GPU engine over the C-ABI (engine_gpu.cpp)

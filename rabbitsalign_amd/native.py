@@ -64,7 +64,8 @@ class NamBatch(C.Structure):
     _fields_ = [("nams", C.c_void_p), ("capacity", C.c_uint64), ("offsets", C.c_void_p),
                 ("nonrepetitive_fraction", C.c_void_p), ("rescued", C.c_void_p), ("needed", C.c_uint64),
                 ("sites", C.c_void_p), ("mm_pool", C.c_void_p), ("mm_capacity", C.c_uint64), ("mm_used", C.c_uint64),
-                ("order", C.c_uint32), ("pad_", C.c_uint32)]
+                ("order", C.c_uint32), ("hamming_align", C.c_uint32), ("match", C.c_int32),
+                ("mismatch", C.c_int32), ("end_bonus", C.c_int32), ("pad_", C.c_uint32)]
 
 
 SITE_DTYPE = np.dtype([("flags", "u1"), ("orig_is_rc", "u1"), ("n_mm", "<u2"), ("mm_offset", "<u4"),
@@ -366,10 +367,13 @@ class GpuContext:
         self._check(self.lib.rsa_randstrobes(self.ctx, C.byref(rb), C.byref(b)), "rsa_randstrobes")
         return [out[int(offs[i]):int(offs[i + 1])] for i in range(len(seqs))]
 
-    def seed(self, seqs, rescue_level=2, rescue_cutoff=None, sites=False, mm_capacity=None, order=NAMS_FOUND):
+    def seed(self, seqs, rescue_level=2, rescue_cutoff=None, sites=False, mm_capacity=None, order=NAMS_FOUND,
+             hamming=None):
         """NAM lists per read (+ nonrepetitive fraction, rescued flags); with sites=True
         also the per-NAM site checks (indexed by nam_id) and the mismatch-position pool
-        (rsa_nam_site); order=NAMS_BY_SCORE returns lists of <= 16 NAMs sorted."""
+        (rsa_nam_site); order=NAMS_BY_SCORE returns lists of <= 16 NAMs sorted.
+        hamming=(match, mismatch, end_bonus): accepted sites carry hamming_align's result
+        in the pool instead of their positions (RSA_SITE_ALIGNED, decode_hamming)."""
         if rescue_cutoff is None:
             rescue_cutoff = rescue_level * self.index.filter_cutoff if rescue_level < 100 else 1000
         rb, keep = self._reads(seqs)
@@ -380,10 +384,12 @@ class GpuContext:
             nonrep = np.zeros(len(seqs), dtype=np.float32)
             resc = np.zeros(len(seqs), dtype=np.uint8)
             st = np.zeros(cap if sites else 0, dtype=SITE_DTYPE)
-            mcap = (4 * cap if mm_capacity is None else mm_capacity) if sites else 0
+            mcap = (16 * cap if mm_capacity is None else mm_capacity) if sites else 0
             pool = np.zeros(max(1, mcap), dtype=np.uint16)
+            hm = hamming or (0, 0, 0)
             b = NamBatch(_ptr(nams), cap, _ptr(offs), _ptr(nonrep), _ptr(resc), 0,
-                         _ptr(st) if sites else 0, _ptr(pool) if sites else 0, mcap, 0, order, 0)
+                         _ptr(st) if sites else 0, _ptr(pool) if sites else 0, mcap, 0, order,
+                         1 if hamming else 0, hm[0], hm[1], hm[2], 0)
             rc = self.lib.rsa_seed(self.ctx, C.byref(rb), rescue_level, rescue_cutoff, C.byref(b))
             if rc == -3:
                 cap = int(b.needed) + 1
@@ -394,6 +400,16 @@ class GpuContext:
                 return lists, nonrep, resc, [st[int(offs[i]):int(offs[i + 1])] for i in range(len(seqs))], \
                     pool[:int(b.mm_used)]
             return lists, nonrep, resc
+
+    @staticmethod
+    def decode_hamming(pool, offset):
+        """hamming_align's result of an RSA_SITE_ALIGNED site: (score, start, end, mismatches, cigar ops)."""
+        w = [int(x) for x in pool[offset:offset + 6]]
+        score = w[0] | (w[1] << 16)
+        if score >= 1 << 31:
+            score -= 1 << 32
+        ops = [int(pool[offset + 6 + 2 * i]) | (int(pool[offset + 7 + 2 * i]) << 16) for i in range(w[5])]
+        return score, w[2], w[3], w[4], ops
 
     @staticmethod
     def _ext_batches(queries, jobs, match, mismatch, gap_open, gap_extend, end_bonus, lib):

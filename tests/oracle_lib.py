@@ -58,6 +58,9 @@ def lib():
                                     C.POINTER(C.c_float)]
         L.ora_find_nams_rescue.argtypes = [C.POINTER(Index), C.c_void_p, C.c_int, C.c_uint, C.c_void_p, C.c_int]
         L.ora_reverse_complement.argtypes = [C.c_char_p, C.c_int, C.c_char_p]
+        L.ora_hamming_align.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                        C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                        C.POINTER(C.c_int), C.c_void_p]
         L.ora_nam_site.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int, C.c_char_p, C.c_int64, C.c_int,
                                    C.c_void_p, C.POINTER(C.c_int)]
         _lib = L
@@ -146,3 +149,13 @@ def nam_site(nam, read: bytes, contig: bytes, k: int):
     f = lib().ora_nam_site(n.ctypes.data, read, reverse_complement(read), len(read), contig, len(contig), k,
                            pos.ctypes.data, C.byref(n_mm))
     return int(f), int(n_mm.value), [int(x) for x in pos[:n_mm.value]] if f & 8 else []
+
+
+def hamming_align(query: bytes, ref: bytes, match=2, mismatch=8, end_bonus=10):
+    """hamming_align (aligner.cpp:219-302): (score, segment start, end, mismatches, CIGAR ops)."""
+    n = len(query)
+    cig = np.zeros(2 * n + 4, dtype=np.uint32)
+    sc, st, en, mm = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    k = lib().ora_hamming_align(query, ref, n, match, mismatch, end_bonus, C.byref(sc), C.byref(st), C.byref(en),
+                                C.byref(mm), cig.ctypes.data)
+    return int(sc.value), int(st.value), int(en.value), int(mm.value), [int(x) for x in cig[:k]]

@@ -26,10 +26,28 @@ CONFIGS = {
 }
 
 
+def _first_differences(gpu_sam, cpu_sam, name, limit=8):
+    """The first differing SAM records (kept under gpurun_out/ on the GPU box)."""
+    out = []
+    with open(gpu_sam) as fg, open(cpu_sam) as fc:
+        for i, (a, b) in enumerate(zip(fg, fc)):
+            if a != b:
+                out.append(f"line {i}\n  gpu {a.rstrip()}\n  cpu {b.rstrip()}")
+                if len(out) == limit:
+                    break
+    text = "\n".join(out)
+    keep = os.environ.get("GRAFT_REPO_ROOT")
+    if keep:
+        os.makedirs(os.path.join(keep, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(keep, "gpurun_out", f"samdiff_{name}.txt"), "a") as f:
+            f.write(text + "\n\n")
+    return text
+
+
 @pytest.mark.gpu
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("name", sorted(CONFIGS))
-def test_baseline_config_sam_identical(name):
+def test_baseline_config_sam_identical(name, tmp_path):
     import torch  # noqa: F401  (HIP runtime of the process first, see bench.py)
     from rabbitsalign_amd import mapper as M
     if not os.path.exists(REF_CPU_LIB):
@@ -41,17 +59,19 @@ def test_baseline_config_sam_identical(name):
         info = m.info()
         assert info["bits"] == bits and info["n_contigs"] == contigs and info["index_on_device"] == 1
         reads = m.synthetic_reads(7, 0, n, L, mu, sigma, paired)
-        g = m.map(reads, threads=threads)
+        g = m.map(reads, threads=threads, sam_path=tmp_path / "gpu.sam")
         ks = m.kernel_stats()
         assert ks["kernels"]["ext_scan"]["launches"] > 0 and ks["kernels"]["lookup"]["launches"] > 0
         cm = m.like(device=0, threads=threads, lib_path=REF_CPU_LIB)
         try:
-            c = cm.map(reads, threads=threads)
+            c = cm.map(reads, threads=threads, sam_path=tmp_path / "cpu.sam")
         finally:
             cm.close()
         assert g.n_reads == c.n_reads == (2 * n if paired else n)
-        assert (g.sam_hash, g.sam_bytes) == (c.sam_hash, c.sam_bytes), \
-            f"{name}: gpu {g.sam_hash:016x}/{g.sam_bytes} cpu {c.sam_hash:016x}/{c.sam_bytes}"
+        if (g.sam_hash, g.sam_bytes) != (c.sam_hash, c.sam_bytes):
+            diff = _first_differences(tmp_path / "gpu.sam", tmp_path / "cpu.sam", name)
+            raise AssertionError(f"{name}: gpu {g.sam_hash:016x}/{g.sam_bytes} "
+                                 f"cpu {c.sam_hash:016x}/{c.sam_bytes}\n{diff}")
         assert g.sw_calls == c.sw_calls and g.mate_rescue == c.mate_rescue
         reads.close()
     finally:

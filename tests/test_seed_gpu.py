@@ -165,6 +165,45 @@ def test_sites(setup, mm_capacity):
     assert n_checked > 0 and (n_pos > 0 or mm_capacity is not None)
 
 
+@pytest.mark.gpu
+def test_sites_hamming_align(setup):
+    """k_sites with hamming_align on (rsa_nam_batch.hamming_align, RSA_SITE_ALIGNED): every
+    accepted site's score, segment, mismatch count and CIGAR equal the oracle's literal
+    restatement of aligner.cpp:219-302 on the same oriented read and projected window;
+    everything else equals the positions mode."""
+    from rabbitsalign_amd.native import GpuContext
+    name, idx, ctx, ora = setup
+    reads = _reads(name)
+    ref = idx.ref_seq.tobytes()
+    coff = idx.contig_offsets
+    # a pool large enough for every result (the pool-full flag is covered by the positions test)
+    nams, _, _, sites, pool = ctx.seed(reads, sites=True, hamming=(2, 8, 10), mm_capacity=1 << 24)
+    n_aln = 0
+    for r, ns, ss in zip(reads, nams, sites):
+        rc = oracle_lib.reverse_complement(r)
+        for nam, st in zip(ns, ss):
+            c = int(nam["ref_id"])
+            contig = ref[int(coff[c]):int(coff[c + 1])]
+            flags, n_mm, pos = oracle_lib.nam_site(nam, r, contig, idx.k)
+            got = int(st["flags"])
+            assert not got & 16, "pool full at 2^24 words"
+            assert (got & ~32) == flags, (r, nam, got, flags)
+            if not flags & 8:
+                assert not got & 32
+                continue
+            assert got & 32
+            # the oriented read and its projected window (aln.cpp:374-395)
+            rev = (flags & 3) == 1
+            is_rc = bool(nam["is_rc"]) != rev
+            qs = len(r) - int(nam["query_end"]) if rev else int(nam["query_start"])
+            q = rc if is_rc else r
+            ps = max(0, int(nam["ref_start"]) - qs)
+            want = oracle_lib.hamming_align(q, contig[ps:ps + len(r)])
+            assert GpuContext.decode_hamming(pool, int(st["mm_offset"])) == want, (r, nam)
+            n_aln += 1
+    assert n_aln > 0
+
+
 def _adversarial_reads(rng):
     acgt = np.frombuffer(b"ACGT", np.uint8)
 
