@@ -445,6 +445,7 @@ static bool extend_seed_part(AlignTmpRes& res, const AlignmentParameters& ap, co
             info.ref_end = info.query_end = w[3];
             info.edit_distance = w[4];
             const uint32_t n_ops = w[5];
+            info.cigar.ops.reserve(n_ops);
             for (uint32_t k = 0; k < n_ops; ++k)
                 info.cigar.ops.push_back((uint32_t)w[6 + 2 * k] | ((uint32_t)w[7 + 2 * k] << 16));
             result_ref_start = projected_ref_start + (int)info.ref_start;

@@ -414,6 +414,18 @@ static inline void prefetch_vec_w(const std::vector<T>& v) {   // the storage pa
     const size_t n = std::min<size_t>(std::max(v.size(), (size_t)4) * sizeof(T), std::min<size_t>(v.capacity() * sizeof(T), 1024));
     for (size_t o = 0; o < n; o += 64) __builtin_prefetch(p + o, 1);
 }
+// the pool entries (mismatch positions / hamming_align results) of read r's first site
+// checks; the sites themselves must be in cache by now (prefetched further ahead)
+static inline void prefetch_site_pool(const SeedBatchOut& so, size_t r) {
+    if (so.sites.empty()) return;
+    const size_t a = so.offsets[r], b = std::min<size_t>(so.offsets[r + 1], so.offsets[r] + 8);
+    for (size_t k = a; k < b; ++k) {
+        const rsa_nam_site& st = so.sites[k];
+        if (!(st.flags & RSA_SITE_POSITIONS) || (st.flags & RSA_SITE_POOL_FULL)) continue;
+        const size_t words = (st.flags & RSA_SITE_ALIGNED) ? 12 + 4 * (size_t)st.n_mm : (size_t)st.n_mm;
+        prefetch_bytes(so.mm_pool.data() + st.mm_offset, 2 * words);
+    }
+}
 static inline void prefetch_res_w(const AlignTmpRes& r) {
     prefetch_vec_w(r.align_res);
     prefetch_vec_w(r.todo_nams);
@@ -521,11 +533,17 @@ void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize, On
     std::vector<Nam> copies[2];
     const size_t ahead = rec_ahead();
     for (size_t i = 0; i < n; ++i) {
-        if (prefetch_on() && i + ahead < n) {   // the NAMs and site checks came by DMA: not in any cache
-            const size_t a = so.offsets[2 * (i + ahead)], b = so.offsets[2 * (i + ahead) + 2];
-            prefetch_bytes(so.nams.data() + a, (b - a) * sizeof(Nam));
-            if (!so.sites.empty()) prefetch_bytes(so.sites.data() + a, (b - a) * sizeof(rsa_nam_site));
-            prefetch_res_w(c.res[i + ahead]);   // part() appends to the pair's lists (storage kept from the last chunk)
+        if (prefetch_on()) {   // the NAMs, site checks and pool came by DMA: not in any cache
+            if (i + 2 * ahead < n) {
+                const size_t a = so.offsets[2 * (i + 2 * ahead)], b = so.offsets[2 * (i + 2 * ahead) + 2];
+                prefetch_bytes(so.nams.data() + a, (b - a) * sizeof(Nam));
+                if (!so.sites.empty()) prefetch_bytes(so.sites.data() + a, (b - a) * sizeof(rsa_nam_site));
+            }
+            if (i + ahead < n) {
+                prefetch_site_pool(so, 2 * (i + ahead));       // sites read here came in `ahead` pairs ago
+                prefetch_site_pool(so, 2 * (i + ahead) + 1);
+                prefetch_res_w(c.res[i + ahead]);   // part() appends to the pair's lists (storage kept from the last chunk)
+            }
         }
         bool rescued[2];
         NamSpan nams[2];
@@ -998,7 +1016,15 @@ PipelineResult run_pipeline_se(ReadSource& src, Engine& eng, const MapContext& m
                 rcs[r].resize(recs[r].seq.size());
                 reverse_complement_into(recs[r].seq, rcs[r].data());
             }
+            const size_t ahead = rec_ahead();
             for (size_t r = 0; r < n; ++r) {
+                if (prefetch_on()) {
+                    if (r + 2 * ahead < n && !so.sites.empty()) {
+                        const size_t a = so.offsets[r + 2 * ahead], b = so.offsets[r + 2 * ahead + 1];
+                        prefetch_bytes(so.sites.data() + a, (b - a) * sizeof(rsa_nam_site));
+                    }
+                    if (r + ahead < n) prefetch_site_pool(so, r + ahead);
+                }
                 nams.assign(so.nams.begin() + (long)so.offsets[r], so.nams.begin() + (long)so.offsets[r + 1]);
                 Read read(recs[r].seq, rcs[r]);
                 read.site = so.site_view(r, recs[r].seq.size());
