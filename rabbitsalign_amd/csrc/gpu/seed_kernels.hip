@@ -1600,6 +1600,78 @@ __device__ bool site_kmer_eq(const char* ref, int64_t rlen, int64_t rpos, const 
     return grp_ballot(bad) == 0;
 }
 
+// Mismatch mask of one lane's 16 window positions x0 .. x0 + 15 (bit b: x0 + b < n and the
+// reference byte differs from the oriented read byte).  The group's 16 lanes cover 256
+// positions, so a read of <= 256 bp takes one round of loads instead of one per 16
+// positions.  Both sides come by five aligned dword loads: the window lies inside its
+// contig and the reference buffer has 64 bytes of padding past the last one; the read
+// buffer has SEQ_PAD bytes of padding before the first read and after the last.
+__device__ __forceinline__ uint32_t rc_byte4(uint32_t w) {     // rc_base on each byte
+    uint32_t o = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const uint32_t u = (w >> (8 * b)) & 0xDFu;             // upper case (only letters reach A/C/G/T/U)
+        const uint32_t c = u == 'A' ? 'T' : u == 'C' ? 'G' : u == 'G' ? 'C' : (u == 'T' || u == 'U') ? 'A' : 'N';
+        o |= c << (8 * b);
+    }
+    return o;
+}
+__device__ __forceinline__ void load16(const char* p, uint32_t out[4]) {   // bytes p[0 .. 16), any alignment
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    uint32_t d[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) d[k] = w[k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) out[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+}
+__device__ __forceinline__ uint32_t window_mask(const char* ref_win, const SiteRead& rd, bool rc, int64_t x0,
+                                                int64_t n) {
+    if (x0 >= n) return 0u;
+    uint32_t r[4], q[4];
+    load16(ref_win + x0, r);
+    if (!rc) {
+        load16(rd.s + x0, q);
+    } else {                                   // q byte b = rc_base(s[n - 1 - (x0 + b)])
+        uint32_t t[4];
+        load16(rd.s + (n - x0 - 16), t);       // s[n - x0 - 16 .. n - x0), reversed below
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[k] = rc_byte4(__builtin_bswap32(t[3 - k]));
+    }
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t x = r[k] ^ q[k];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) m |= ((x >> (8 * b)) & 0xFFu) ? (1u << (4 * k + b)) : 0u;
+    }
+    const int64_t left = n - x0;               // positions past the read end do not count
+    return left >= 16 ? m : m & ((1u << left) - 1u);
+}
+
+// reads over 1024 bp: masks past the four kept in registers, out of line
+__device__ __attribute__((noinline)) uint32_t window_mask_far(const char* ref_win, const char* s, int64_t len, bool rc,
+                                                              int64_t x0) {
+    return window_mask(ref_win, SiteRead{s, len}, rc, x0, len);
+}
+
+// sums / exclusive prefix sums over a 16-lane group
+__device__ __forceinline__ uint32_t grp_sum(uint32_t v) {
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 16);
+    return v;
+}
+__device__ __forceinline__ uint32_t grp_excl_scan(uint32_t v, int l16) {
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o, 16);
+        if (l16 >= o) x += y;
+    }
+    return x - v;
+}
+
 __global__ void __launch_bounds__(256)
 k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read, SeedHdr* __restrict__ err_hdr,
         uint64_t cap, const uint64_t* __restrict__ ooff, const char* __restrict__ seq, const uint64_t* __restrict__ roff,
@@ -1645,8 +1717,14 @@ k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read,
         }
     }
     uint32_t hd = 0, mm_off = 0;
+    uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;      // this lane's mismatch masks, positions c * 256 + 16 * l16 + b
     bool want = false;
     int64_t ps = 0;
+    // the mask of chunk c (256 positions): registers for the first four, loads again beyond
+    auto mask_of = [&](int64_t c) -> uint32_t {
+        if (c < 4) return c == 0 ? m0 : c == 1 ? m1 : c == 2 ? m2 : m3;
+        return window_mask_far(ref + ps, rd.s, rd.len, is_rc, 256 * c + 16 * l16);
+    };
     if (flags != 2) {
         // projected_ref_start = max(0, ref_start - query_start); projected_ref_end =
         // min(ref_end + |read| - query_end, |contig|) (size_t arithmetic)
@@ -1654,10 +1732,17 @@ k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read,
         const uint64_t pe = min((uint64_t)((int64_t)nam.ref_end + rd.len - qe), (uint64_t)ref_len);
         if (pe - (uint64_t)ps == (uint64_t)rd.len) {
             flags |= RSA_SITE_HAMMING;
-            for (int64_t i0 = 0; i0 < rd.len; i0 += 16) {
-                const int64_t i = i0 + l16;
-                hd += __popc(grp_ballot(i < rd.len && (unsigned char)ref[ps + i] != rd.at(is_rc, i)));
+            // masks of the first 1024 positions stay in registers for the passes below
+#pragma nounroll
+            for (int64_t c = 0; 256 * c < rd.len; ++c) {
+                const uint32_t mc = window_mask(ref + ps, rd, is_rc, 256 * c + 16 * l16, rd.len);
+                m0 = c == 0 ? mc : m0;
+                m1 = c == 1 ? mc : m1;
+                m2 = c == 2 ? mc : m2;
+                m3 = c == 3 ? mc : m3;
+                hd += __popc(mc);
             }
+            hd = grp_sum(hd);
             want = (double)((float)hd / (float)rd.len) < 0.05;
         }
     }
@@ -1678,12 +1763,17 @@ k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read,
             flags |= RSA_SITE_POSITIONS;
             mm_off = (uint32_t)at;
             uint32_t m = 0;
-            for (int64_t i0 = 0; i0 < rd.len && m < hd; i0 += 16) {
-                const int64_t i = i0 + l16;
-                const bool mis = i < rd.len && (unsigned char)ref[ps + i] != rd.at(is_rc, i);
-                const uint32_t bits = grp_ballot(mis);
-                if (mis && valid) pool[at + m + __popc(bits & ((1u << l16) - 1))] = (uint16_t)i;
-                m += __popc(bits);
+            for (int64_t c = 0; 256 * c < rd.len && m < hd; ++c) {
+                uint32_t bits = mask_of(c);
+                const uint32_t cnt = __popc(bits);
+                uint32_t o = m + grp_excl_scan(cnt, l16);
+                while (bits) {
+                    const int b = __builtin_ctz(bits);
+                    bits &= bits - 1;
+                    if (valid) pool[at + o] = (uint16_t)(256 * c + 16 * l16 + b);
+                    ++o;
+                }
+                m += grp_sum(cnt);
             }
         } else if (at + need <= pool_cap) {
             // hamming_align (aligner.cpp:219-302) over the window just tested: the group walks
@@ -1697,8 +1787,8 @@ k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read,
             int64_t start = 0, best_start = 0, best_end = 0, i = 0;
             int score = h_bonus, best = 0;
             for (int64_t i0 = 0; i0 < n; i0 += 16) {
-                const int64_t x = i0 + l16;
-                uint32_t bits = grp_ballot(x < n && (unsigned char)ref[ps + x] != rd.at(is_rc, x));
+                // lane (i0 / 16) % 16 of the group holds positions i0 .. i0 + 15
+                uint32_t bits = (uint32_t)__shfl((int)mask_of(i0 >> 8), (int)((i0 >> 4) & 15), 16);
                 while (bits) {
                     const int64_t m = i0 + __builtin_ctz(bits);
                     bits &= bits - 1;
@@ -1733,10 +1823,12 @@ k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read,
             };
             if (best_start > 0) push(4, (uint32_t)best_start);
             int64_t cur = best_start;
-            for (int64_t i0 = 0; i0 < best_end; i0 += 16) {
-                const int64_t x = i0 + l16;
-                uint32_t bits = grp_ballot(x < best_end && x >= best_start &&
-                                           (unsigned char)ref[ps + x] != rd.at(is_rc, x));
+            for (int64_t i0 = best_start & ~(int64_t)15; i0 < best_end; i0 += 16) {
+                uint32_t bits = (uint32_t)__shfl((int)mask_of(i0 >> 8), (int)((i0 >> 4) & 15), 16);
+                // positions in [best_start, best_end) only
+                const int64_t lo = best_start - i0, hi = best_end - i0;
+                if (lo > 0) bits &= ~((1u << lo) - 1u);
+                if (hi < 16) bits &= (1u << hi) - 1u;
                 while (bits) {
                     const int64_t m = i0 + __builtin_ctz(bits);
                     bits &= bits - 1;
@@ -1862,6 +1954,10 @@ static hipError_t hens(SeedBufs& b, int i, size_t bytes) {
         if (e_ != hipSuccess) { err = std::string(#x) + ": " + hipGetErrorString(e_); return RSA_ERR_HIP; } \
     } while (0)
 #define DP(i, T) ((T*)b.p[i])
+// the reads sit SEQ_PAD bytes into B_SEQ, with as many after them: k_sites reads 16-byte
+// windows by aligned dwords that may start or end up to 19 bytes outside a read
+#define SEQ_PAD 64
+#define D_SEQ ((char*)b.p[B_SEQ] + SEQ_PAD)
 #define HP(i, T) ((T*)b.h[i])
 
 static const uint32_t MAP_BIG = 65536 + 512;
@@ -1876,13 +1972,13 @@ int seed_stage_randstrobes(SeedBufs& b, hipStream_t st, const SeedIndexParams& p
         qbase[i + 1] = qbase[i] + 2ull * rb->lengths[i];
         total_len = std::max<uint64_t>(total_len, rb->offsets[i] + rb->lengths[i]);
     }
-    SCHK(dens(b, B_SEQ, total_len + 16));
+    SCHK(dens(b, B_SEQ, total_len + 2 * SEQ_PAD));
     SCHK(dens(b, B_ROFF, 8ull * n));
     SCHK(dens(b, B_RLEN, 4ull * n));
     SCHK(dens(b, B_QBASE, 8ull * (n + 1)));
     SCHK(dens(b, B_QRS, sizeof(rsa_query_randstrobe) * (qbase[n] + 1)));
     SCHK(dens(b, B_QCNT, 4ull * n));
-    SCHK(hipMemcpyAsync(b.p[B_SEQ], rb->seq, total_len, hipMemcpyHostToDevice, st));
+    SCHK(hipMemcpyAsync(D_SEQ, rb->seq, total_len, hipMemcpyHostToDevice, st));
     SCHK(hipMemcpyAsync(b.p[B_ROFF], rb->offsets, 8ull * n, hipMemcpyHostToDevice, st));
     SCHK(hipMemcpyAsync(b.p[B_RLEN], rb->lengths, 4ull * n, hipMemcpyHostToDevice, st));
     SCHK(hens(b, H_QBASE, 8ull * (n + 1)));
@@ -1906,17 +2002,17 @@ int seed_stage_randstrobes(SeedBufs& b, hipStream_t st, const SeedIndexParams& p
     }
     if (kt) kt->begin(st, RSA_K_RANDSTROBES);
     if (wave_ok)
-        hipLaunchKernelGGL(k_rs_wave, dim3((n + RW_WAVES - 1) / RW_WAVES), dim3(64 * RW_WAVES), 0, st, DP(B_SEQ, char),
+        hipLaunchKernelGGL(k_rs_wave, dim3((n + RW_WAVES - 1) / RW_WAVES), dim3(64 * RW_WAVES), 0, st, D_SEQ,
                            DP(B_ROFF, uint64_t), DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n, p,
                            DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
     if (n_lane) {
         SCHK(dens(b, B_SYNC, sizeof(SyncD) * (qbase[n] / 2 + 1)));
         if (p.k - p.s + 1 == 5)
-            hipLaunchKernelGGL(k_randstrobes<5>, dim3((n_lane + 63) / 64), dim3(64), 0, st, DP(B_SEQ, char),
+            hipLaunchKernelGGL(k_randstrobes<5>, dim3((n_lane + 63) / 64), dim3(64), 0, st, D_SEQ,
                                DP(B_ROFF, uint64_t), DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n_lane,
                                lane_list, p, DP(B_SYNC, SyncD), DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
         else
-            hipLaunchKernelGGL(k_randstrobes<0>, dim3((n_lane + 63) / 64), dim3(64), 0, st, DP(B_SEQ, char),
+            hipLaunchKernelGGL(k_randstrobes<0>, dim3((n_lane + 63) / 64), dim3(64), 0, st, D_SEQ,
                                DP(B_ROFF, uint64_t), DP(B_RLEN, uint32_t), DP(B_QBASE, uint64_t), (int)n_lane,
                                lane_list, p, DP(B_SYNC, SyncD), DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
     }
@@ -2004,7 +2100,7 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
     if (b.pool_n < 4ull * n + 65536) b.pool_n = 4ull * n + 65536;
     const uint64_t slots = (uint64_t)n * FN2_HCAP;
     const uint64_t cap = out->capacity;
-    SCHK(dens(b, B_SEQ, total_len + 16));
+    SCHK(dens(b, B_SEQ, total_len + 2 * SEQ_PAD));
     SCHK(dens(b, B_X, X.down));
     SCHK(dens(b, B_QRS, sizeof(rsa_query_randstrobe) * (nq_cap + 1)));
     SCHK(dens(b, B_QCNT, 4ull * n));
@@ -2035,7 +2131,7 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
     uint64_t* d_ooff = (uint64_t*)(dx + X.ooff);
     float* d_nonrep = (float*)(dx + X.nonrep);
     uint8_t* d_resc = (uint8_t*)(dx + X.resc);
-    SCHK(hipMemcpyAsync(b.p[B_SEQ], rb->seq, total_len, hipMemcpyHostToDevice, st));
+    SCHK(hipMemcpyAsync(D_SEQ, rb->seq, total_len, hipMemcpyHostToDevice, st));
     SeedHdr hh;
     for (int attempt = 0;; ++attempt) {
         SCHK(dens(b, B_ARENA, sizeof(rsa_nam) * (slots + b.pool_n)));
@@ -2051,17 +2147,17 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
         kt.begin(st, RSA_K_RANDSTROBES);
         if (wave_ok)
             hipLaunchKernelGGL(k_rs_wave, dim3((n + RW_WAVES - 1) / RW_WAVES), dim3(64 * RW_WAVES), 0, st,
-                               DP(B_SEQ, char), d_roff, d_rlen, d_qbase, (int)n, p, DP(B_QRS, rsa_query_randstrobe),
+                               D_SEQ, d_roff, d_rlen, d_qbase, (int)n, p, DP(B_QRS, rsa_query_randstrobe),
                                DP(B_QCNT, uint32_t));
         if (n_lane) {
             SCHK(dens(b, B_SYNC, sizeof(SyncD) * (nq_cap / 2 + 1)));
             const int* lane_list = wave_ok ? (const int*)(dx + X.rsl) : nullptr;
             if (p.k - p.s + 1 == 5)
-                hipLaunchKernelGGL(k_randstrobes<5>, dim3((n_lane + 63) / 64), dim3(64), 0, st, DP(B_SEQ, char), d_roff,
+                hipLaunchKernelGGL(k_randstrobes<5>, dim3((n_lane + 63) / 64), dim3(64), 0, st, D_SEQ, d_roff,
                                    d_rlen, d_qbase, (int)n_lane, lane_list, p, DP(B_SYNC, SyncD),
                                    DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
             else
-                hipLaunchKernelGGL(k_randstrobes<0>, dim3((n_lane + 63) / 64), dim3(64), 0, st, DP(B_SEQ, char), d_roff,
+                hipLaunchKernelGGL(k_randstrobes<0>, dim3((n_lane + 63) / 64), dim3(64), 0, st, D_SEQ, d_roff,
                                    d_rlen, d_qbase, (int)n_lane, lane_list, p, DP(B_SYNC, SyncD),
                                    DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
         }
@@ -2116,7 +2212,7 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
             kt.begin(st, RSA_K_SITES);
             const uint32_t grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1, (cap + 15) / 16), 4096);
             hipLaunchKernelGGL(k_sites, dim3(grid), dim3(256), 0, st, DP(B_OUT, rsa_nam), DP(B_NREAD, uint32_t), dhdr,
-                               cap, d_ooff, DP(B_SEQ, char), d_roff, d_rlen, p, DP(B_SITES, rsa_nam_site), DP(B_POOL, uint16_t),
+                               cap, d_ooff, D_SEQ, d_roff, d_rlen, p, DP(B_SITES, rsa_nam_site), DP(B_POOL, uint16_t),
                                out->mm_capacity, &dhdr->mm_used, out->hamming_align ? 1 : 0, out->match, out->mismatch,
                                out->end_bonus);
             SCHK(hipGetLastError());

@@ -426,6 +426,14 @@ static inline void prefetch_site_pool(const SeedBatchOut& so, size_t r) {
         prefetch_bytes(so.mm_pool.data() + st.mm_offset, 2 * words);
     }
 }
+// the object itself (a pair's AlignTmpRes): its vector headers must be in cache before
+// prefetch_res / prefetch_res_w read them, so this goes one distance further ahead
+template <class T>
+static inline void prefetch_obj(const T& x, int rw = 0) {
+    const char* p = (const char*)&x;
+    for (size_t o = 0; o < sizeof(T); o += 64) rw ? __builtin_prefetch(p + o, 1) : __builtin_prefetch(p + o);
+    __builtin_prefetch(p + sizeof(T) - 1);
+}
 static inline void prefetch_res_w(const AlignTmpRes& r) {
     prefetch_vec_w(r.align_res);
     prefetch_vec_w(r.todo_nams);
@@ -538,6 +546,8 @@ void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize, On
                 const size_t a = so.offsets[2 * (i + 2 * ahead)], b = so.offsets[2 * (i + 2 * ahead) + 2];
                 prefetch_bytes(so.nams.data() + a, (b - a) * sizeof(Nam));
                 if (!so.sites.empty()) prefetch_bytes(so.sites.data() + a, (b - a) * sizeof(rsa_nam_site));
+                prefetch_obj(c.res[i + 2 * ahead], 1);
+                if (i + 4 * ahead < n) __builtin_prefetch(&so.offsets[2 * (i + 4 * ahead)]);
             }
             if (i + ahead < n) {
                 prefetch_site_pool(so, 2 * (i + ahead));       // sites read here came in `ahead` pairs ago
@@ -585,6 +595,7 @@ void pe_get_str(PeChunk& c, const MapContext& mc, float mu, float sigma, std::ve
     const auto t = Clock::now();
     const size_t n = c.size(), ahead = rec_ahead();
     for (size_t i = 0; i < n; ++i) {
+        if (i + 2 * ahead < n) prefetch_obj(c.res[i + 2 * ahead]);
         if (i + ahead < n) prefetch_vec(c.res[i + ahead].todo_nams);   // written by part(), cold by now
         const Read read1(c.in.r1[i].seq, c.rc(i, 0)), read2(c.in.r2[i].seq, c.rc(i, 1));
         collect_jobs_pe(c.res[i], c.in.r1[i], c.in.r2[i], read1, read2, mc, mu, sigma, jobs);
@@ -601,6 +612,7 @@ void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistributio
     const bool pf = prefetch_on();
     const size_t ahead = rec_ahead();
     for (size_t i = 0; i < n; ++i) {
+        if (pf && i + 2 * ahead < n) prefetch_obj(c.res[i + 2 * ahead]);
         if (pf && i + ahead < n) prefetch_res(c.res[i + ahead]);
         const Read read1(c.in.r1[i].seq, c.rc(i, 0)), read2(c.in.r2[i].seq, c.rc(i, 1));
         pos = store_results_pe(c.res[i], read1, read2, mc, isize.mu, isize.sigma, infos, pos);
@@ -610,6 +622,11 @@ void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistributio
     Sam sam(out, mc.refs, mc.mparams.cigar_eqx, rg_id, mc.mparams.output_unmapped, mc.mparams.details);
     sam.digest_into(digest);
     for (size_t i = 0; i < n; ++i) {
+        if (pf && i + 2 * ahead < n) {
+            prefetch_obj(c.res[i + 2 * ahead]);
+            prefetch_obj(c.in.r1[i + 2 * ahead]);
+            prefetch_obj(c.in.r2[i + 2 * ahead]);
+        }
         if (pf && i + ahead < n) {
             prefetch_record(c.in.r1[i + ahead]);
             prefetch_record(c.in.r2[i + ahead]);

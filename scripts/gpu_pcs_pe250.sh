@@ -1,4 +1,4 @@
-# Host PC samples of the default bench, then a kernel trace of the PE 2x250 workload
+# Host PC samples of the default bench (NO_PCS=1: skipped), then a kernel trace of the PE 2x250 workload
 # (trace + stats only; summary with the GPU busy union via scripts/prof_summary.py)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -6,8 +6,10 @@ export TMPDIR=/tmp
 TAG=${1:-pcs_pe250}
 O=gpurun_out/$TAG
 mkdir -p $O
-RSA_PC_SAMPLE=$O/pcs.txt timeout -k 10 300 python bench.py --no-cpu-baseline --no-multi-device --steps 5 > $O/bench.json 2> $O/bench.err || exit $?
-echo "pcs done"
+if [ -z "$NO_PCS" ]; then
+  RSA_PC_SAMPLE=$O/pcs.txt timeout -k 10 300 python bench.py --no-cpu-baseline --no-multi-device --steps 5 > $O/bench.json 2> $O/bench.err || exit $?
+  echo "pcs done"
+fi
 P=$O/prof_pe250
 mkdir -p $P
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $P/trace -o run -- python3 bench.py --workload pe250_3g --no-cpu-baseline --no-multi-device --steps 4 --warmup 2 > $P/bench_trace.json 2> $P/bench_trace.err || exit $?
