@@ -46,6 +46,8 @@ struct QrsInfo {            // per query randstrobe, filled by k_lookup
 struct ReadStat {
     uint32_t found, good, hits_find, hits_all;
     uint32_t scan_find, scan_all;   // index entries read by the min_diff pass (instrumentation)
+    uint32_t qw;                    // the read's query randstrobes and QrsInfo are in qrs / qi
+    uint32_t pad;
 };
 
 struct HitD {
@@ -72,7 +74,7 @@ struct SeedHdr {
     uint32_t errors;                // SEED_E_*
     // statistics (DESIGN.md "Kernels": algorithmic bytes and per-read counts)
     unsigned long long qrs, found, good, hits_find, hits_all, scan_find, scan_all, n1, n2, resc_reads, resc_q,
-        resc_scan, resc_hits;
+        resc_scan, resc_hits, qw_q;   // qw_q: query randstrobes written out (reads with ReadStat::qw)
 };
 
 // The call's pool: per entry one hit, one open NAM, one NAM, one group hit and
@@ -93,6 +95,13 @@ struct SeedPool {
 // k_randstrobes
 // ---------------------------------------------------------------------------
 struct SyncD { uint64_t hash; uint32_t pos; uint32_t pad; };
+struct RescueD { uint64_t pos; uint32_t count, qs, qe, pad; };
+// query_lane's syncmer scratch for read r inside the rescue buffer: RescueD room for
+// 2 len entries at qbase[r] holds len SyncD (the rescue pass overwrites it afterwards)
+struct RescueScratch {
+    RescueD* rbuf;
+    __device__ __forceinline__ SyncD* sync(uint64_t qb) const { return (SyncD*)(rbuf + qb); }
+};
 
 __device__ void rs_get(const SyncD* sm, int n, int i, const SeedIndexParams& p, uint64_t& h, uint32_t& a,
                        uint32_t& b) {
@@ -317,26 +326,11 @@ __device__ __forceinline__ void rs_pick(const uint64_t* __restrict__ sh, const u
     b = pos(best);
 }
 
-__global__ void __launch_bounds__(64 * RW_WAVES)
-k_rs_wave(const char* __restrict__ seq, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
-          const uint64_t* __restrict__ qbase, int n_reads, SeedIndexParams p, rsa_query_randstrobe* __restrict__ qrs,
-          uint32_t* __restrict__ qcnt) {
-    __shared__ uint32_t s_code[RW_WAVES][RW_MAXLEN / 16 + 4];
-    __shared__ uint32_t s_nm[RW_WAVES][RW_MAXLEN / 32 + 4];
-    __shared__ uint64_t s_h[RW_WAVES][RW_MAXLEN];       // s-mer hash by end position, then syncmer k-mer hashes
-    __shared__ uint32_t s_sp[RW_WAVES][RW_MAXLEN];      // syncmer positions
-    __shared__ int s_n[RW_WAVES];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int r = blockIdx.x * RW_WAVES + w;
-    if (r >= n_reads) return;                           // the whole wave leaves together
-    const int len = (int)rlen[r];
-    if (len > RW_MAXLEN) return;                        // k_randstrobes takes it
-    if (len < p.w_max) { if (lane == 0) qcnt[r] = 0; return; }   // randstrobes.cpp:209
-    const char* sq = seq + roff[r];
-    uint32_t* cw = s_code[w];
-    uint32_t* nm = s_nm[w];
-    uint64_t* hs = s_h[w];
-    uint32_t* sp = s_sp[w];
+// Steps 1-4a for one read on one wave (len <= RW_MAXLEN, len >= p.w_max): returns the
+// syncmer count n, with their canonical k-mer hashes in hs[0, n) and positions in sp[0, n).
+// s_nw is a wave-private LDS int (the tie walk's count).
+__device__ __forceinline__ int rw_syncmers(const char* __restrict__ sq, int len, const SeedIndexParams& p, int lane,
+                                           uint32_t* cw, uint32_t* nm, uint64_t* hs, uint32_t* sp, int* s_nw) {
     const int k = p.k, sl = p.s, W = k - sl + 1;
     // 1. codes and N mask
     for (int i = lane; i < RW_MAXLEN / 16 + 4; i += 64) cw[i] = 0;
@@ -405,15 +399,41 @@ k_rs_wave(const char* __restrict__ seq, const uint64_t* __restrict__ roff, const
                 }
                 if (min_pos == i - k + p.t) sp[nn++] = (uint32_t)(i - k + 1);
             }
-            s_n[w] = nn;
+            *s_nw = nn;
         }
         WSYNC_SEED();
-        n = s_n[w];
+        n = *s_nw;
     }
     WSYNC_SEED();                                       // every read of the s-mer hashes is done
     // 4a. syncmer k-mer hashes (into the s-mer hash array)
     for (int x = lane; x < n; x += 64) hs[x] = xxh64_u64(rw_canon(rw_bases(cw, (int)sp[x], k), k));
     WSYNC_SEED();
+    return n;
+}
+
+// the wave kernel's LDS, per wave
+#define RW_LDS_DECL                                                                          \
+    __shared__ uint32_t s_code[RW_WAVES][RW_MAXLEN / 16 + 4];                                \
+    __shared__ uint32_t s_nm[RW_WAVES][RW_MAXLEN / 32 + 4];                                  \
+    __shared__ uint64_t s_h[RW_WAVES][RW_MAXLEN];   /* s-mer hash by end, then k-mer hashes */ \
+    __shared__ uint32_t s_sp[RW_WAVES][RW_MAXLEN];  /* syncmer positions */                  \
+    __shared__ int s_n[RW_WAVES]
+
+// rsa_randstrobes (the randstrobe API): every query randstrobe written out
+__global__ void __launch_bounds__(64 * RW_WAVES)
+k_rs_wave(const char* __restrict__ seq, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
+          const uint64_t* __restrict__ qbase, int n_reads, SeedIndexParams p, rsa_query_randstrobe* __restrict__ qrs,
+          uint32_t* __restrict__ qcnt) {
+    RW_LDS_DECL;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = blockIdx.x * RW_WAVES + w;
+    if (r >= n_reads) return;                           // the whole wave leaves together
+    const int len = (int)rlen[r];
+    if (len > RW_MAXLEN) return;                        // k_randstrobes takes it
+    if (len < p.w_max) { if (lane == 0) qcnt[r] = 0; return; }   // randstrobes.cpp:209
+    uint64_t* hs = s_h[w];
+    uint32_t* sp = s_sp[w];
+    const int n = rw_syncmers(seq + roff[r], len, p, lane, s_code[w], s_nm[w], hs, sp, &s_n[w]);
     // 4b. randstrobes, forward then reverse complement
     const int m = n > p.w_min ? n - p.w_min : 0;
     rsa_query_randstrobe* out = qrs + qbase[r];
@@ -422,7 +442,7 @@ k_rs_wave(const char* __restrict__ seq, const uint64_t* __restrict__ roff, const
         uint64_t h; uint32_t a, b;
         rs_pick(hs, sp, n, rcx ? x - m : x, rcx, len, p, h, a, b);
         rsa_query_randstrobe o;
-        o.hash = h; o.start = a; o.end = b + (uint32_t)k; o.is_reverse = rcx ? 1 : 0; o.pad_ = 0;
+        o.hash = h; o.start = a; o.end = b + (uint32_t)p.k; o.is_reverse = rcx ? 1 : 0; o.pad_ = 0;
         out[x] = o;
     }
     if (lane == 0) qcnt[r] = (uint32_t)(2 * m);
@@ -464,138 +484,285 @@ __device__ __forceinline__ int wave_excl_scan_lk(int v, int lane, int& total) {
     return x - v;
 }
 
+// One query randstrobe against the index (index.hpp:57-93, nam.cpp:68-85): its
+// QrsInfo, and the run of equal hashes as eb[lo, ub)
+__device__ __forceinline__ QrsInfo lookup_one(const rsa_query_randstrobe& q, const SeedIndexParams& p, uint64_t& lo,
+                                              uint64_t& ub, const rsa_ref_randstrobe*& eb) {
+    QrsInfo o;
+    o.pos = END64; o.count = 0; o.hits = 0; o.flags = 0; o.pad = 0;
+    // the bucket's entries are eb[0, b - a) (in its line or in p.rs); lo/ub index eb
+    lo = 0; ub = 0;
+    eb = p.rs;
+    const uint64_t top = q.hash >> (64 - p.bits);
+    uint64_t a, b;
+    bool hit = false;
+    if (p.lines) {
+        // the whole line in one go (eight independent 16-byte loads, one
+        // miss): bounds and up to BL_CAP entries, searched in registers
+        const BucketLine* L = p.lines + top;
+        const uint4* lv = (const uint4*)L;
+        uint4 w[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) w[t] = lv[t];
+        a = (uint64_t)w[0].x | (uint64_t)w[0].y << 32;
+        b = (uint64_t)w[0].z | (uint64_t)w[0].w << 32;
+        if (b - a <= BL_CAP) {
+            eb = L->e;
+            const uint64_t c = b - a;
+            lo = c; ub = c;            // first entry >= / > the key (entries sorted)
+#pragma unroll
+            for (int t = BL_CAP - 1; t >= 0; --t) {
+                const uint64_t h = (uint64_t)w[1 + t].x | (uint64_t)w[1 + t].y << 32;
+                if ((uint64_t)t < c) {
+                    if (h >= q.hash) lo = t;
+                    if (h > q.hash) ub = t;
+                }
+            }
+            hit = ub > lo;
+        } else {
+            eb = p.rs + a;
+            lo = lower_bound_hash(eb, 0, b - a, q.hash);
+            hit = lo < b - a && eb[lo].hash == q.hash;
+            if (hit) ub = upper_bound_hash(eb, lo, b - a, q.hash);
+        }
+    } else {
+        a = p.starts[top]; b = p.starts[top + 1];
+        eb = p.rs + a;
+        if (a != b) {
+            lo = lower_bound_hash(eb, 0, b - a, q.hash);
+            hit = lo < b - a && eb[lo].hash == q.hash;
+            if (hit) ub = upper_bound_hash(eb, lo, b - a, q.hash);
+        }
+    }
+    if (hit) {
+        o.pos = a + lo;
+        o.flags = 1;
+        // is_filtered (index.hpp:91-93) probes rs[lo + filter_cutoff].hash == hash;
+        // equal hashes are contiguous from lo to ub (one bucket), so that is
+        // ub - lo > filter_cutoff, and the probe's random line is not fetched
+        if (ub - lo > (uint64_t)p.filter_cutoff) o.flags |= 2;
+        o.count = (uint32_t)min<uint64_t>(ub - lo, 0xFFFFFFFFull);
+        if (o.count <= 1000) {
+            // add_to_hits_per_ref min_diff filter (nam.cpp:68-85)
+            int min_diff = INT_MAX;
+            uint32_t h = 0;
+            const int qspan = (int)q.end - (int)q.start;
+            for (uint64_t e = lo; e < ub; ++e) {
+                const rsa_ref_randstrobe x = eb[e];
+                const int rspan = (int)(x.packed & 0xFF) + p.k;
+                int d = qspan - rspan;
+                d = d < 0 ? -d : d;
+                if (d <= min_diff) { h++; min_diff = d; }
+            }
+            o.hits = h;
+        }
+    }
+    return o;
+}
+
+// a read's lookup statistics (ReadStat fields)
+struct LkStat {
+    uint32_t found = 0, good = 0, hfind = 0, hall = 0, sfind = 0, sall = 0;
+    __device__ __forceinline__ void add(const QrsInfo& o) {
+        if (!(o.flags & 1)) return;
+        found++;
+        const uint32_t scanned = o.count <= 1000 ? o.count : 0;
+        if (!(o.flags & 2)) { good++; hfind += o.hits; sfind += scanned; }
+        if (o.count <= 1000) hall += o.hits;
+        sall += scanned;
+    }
+    __device__ __forceinline__ void wave_sum() {
+        for (int off = 32; off > 0; off >>= 1) {
+            found += __shfl_xor(found, off, 64);
+            good += __shfl_xor(good, off, 64);
+            hfind += __shfl_xor(hfind, off, 64);
+            hall += __shfl_xor(hall, off, 64);
+            sfind += __shfl_xor(sfind, off, 64);
+            sall += __shfl_xor(sall, off, 64);
+        }
+    }
+    __device__ __forceinline__ ReadStat to_stat(uint32_t qw) const {
+        ReadStat s;
+        s.found = found; s.good = good; s.hits_find = hfind; s.hits_all = hall; s.scan_find = sfind; s.scan_all = sall;
+        s.qw = qw; s.pad = 0;
+        return s;
+    }
+};
+
+// the hits of one non-filtered randstrobe (add_to_hits_per_ref order) into slot[at, ...)
+__device__ __forceinline__ void lk_emit(const rsa_query_randstrobe& q, uint64_t lo, uint64_t ub,
+                                        const rsa_ref_randstrobe* eb, const SeedIndexParams& p, HitD* slot, int at) {
+    const int qs = (int)q.start, qe = (int)q.end;
+    int min_diff = INT_MAX, h = at;
+    for (uint64_t e = lo; e < ub; ++e) {
+        const rsa_ref_randstrobe x = eb[e];
+        const int rs0 = (int)x.position;
+        const int re0 = rs0 + (int)(x.packed & 0xFF) + p.k;
+        int d = (qe - qs) - (re0 - rs0);
+        d = d < 0 ? -d : d;
+        if (d <= min_diff) {
+            HitD hd;
+            hd.qs = qs; hd.qe = qe; hd.rs = rs0; hd.re = re0;
+            hd.list = (int32_t)(x.packed >> 8);
+            hd.pad = q.is_reverse ? 1 : 0;
+            slot[h++] = hd;
+            min_diff = d;
+        }
+    }
+}
+
+// k_lookup: the reads k_randstrobes took (list; NULL = every read), one wave a read
 __global__ void __launch_bounds__(256)
 k_lookup(const rsa_query_randstrobe* __restrict__ qrs, const uint32_t* __restrict__ qcnt,
-         const uint64_t* __restrict__ qbase, int n_reads, SeedIndexParams p, QrsInfo* __restrict__ qi,
-         ReadStat* __restrict__ st, HitD* __restrict__ hit_slots) {
+         const uint64_t* __restrict__ qbase, int n_list, const int* __restrict__ list, SeedIndexParams p,
+         QrsInfo* __restrict__ qi, ReadStat* __restrict__ st, HitD* __restrict__ hit_slots) {
     const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
-    if (wave >= n_reads) return;
-    const int r = wave;
+    if (wave >= n_list) return;
+    const int r = list ? list[wave] : wave;
     const int nq = (int)qcnt[r];
     const uint64_t base = qbase[r];
     HitD* slot = hit_slots + (size_t)r * LK_HCAP;
-    uint32_t found = 0, good = 0, hfind = 0, hall = 0, sfind = 0, sall = 0;
+    LkStat ls;
     int hoff = 0;                                      // hits of the read written so far
     for (int i0 = 0; i0 < nq; i0 += 64) {
         const int i = i0 + lane;
         QrsInfo o;
-        o.pos = END64; o.count = 0; o.hits = 0; o.flags = 0; o.pad = 0;
+        o.flags = 0; o.hits = 0;
         rsa_query_randstrobe q;
-        // the bucket's entries are eb[0, b - a) (in its line or in p.rs); lo/ub index eb
         uint64_t lo = 0, ub = 0;
         const rsa_ref_randstrobe* eb = p.rs;
         if (i < nq) {
             q = qrs[base + i];
-            const uint64_t top = q.hash >> (64 - p.bits);
-            uint64_t a, b;
-            bool hit = false;
-            if (p.lines) {
-                // the whole line in one go (eight independent 16-byte loads, one
-                // miss): bounds and up to BL_CAP entries, searched in registers
-                const BucketLine* L = p.lines + top;
-                const uint4* lv = (const uint4*)L;
-                uint4 w[8];
-#pragma unroll
-                for (int t = 0; t < 8; ++t) w[t] = lv[t];
-                a = (uint64_t)w[0].x | (uint64_t)w[0].y << 32;
-                b = (uint64_t)w[0].z | (uint64_t)w[0].w << 32;
-                if (b - a <= BL_CAP) {
-                    eb = L->e;
-                    const uint64_t c = b - a;
-                    lo = c; ub = c;            // first entry >= / > the key (entries sorted)
-#pragma unroll
-                    for (int t = BL_CAP - 1; t >= 0; --t) {
-                        const uint64_t h = (uint64_t)w[1 + t].x | (uint64_t)w[1 + t].y << 32;
-                        if ((uint64_t)t < c) {
-                            if (h >= q.hash) lo = t;
-                            if (h > q.hash) ub = t;
-                        }
-                    }
-                    hit = ub > lo;
-                } else {
-                    eb = p.rs + a;
-                    lo = lower_bound_hash(eb, 0, b - a, q.hash);
-                    hit = lo < b - a && eb[lo].hash == q.hash;
-                    if (hit) ub = upper_bound_hash(eb, lo, b - a, q.hash);
-                }
-            } else {
-                a = p.starts[top]; b = p.starts[top + 1];
-                eb = p.rs + a;
-                if (a != b) {
-                    lo = lower_bound_hash(eb, 0, b - a, q.hash);
-                    hit = lo < b - a && eb[lo].hash == q.hash;
-                    if (hit) ub = upper_bound_hash(eb, lo, b - a, q.hash);
-                }
-            }
-            if (hit) {
-                o.pos = a + lo;
-                o.flags = 1;
-                // is_filtered (index.hpp:91-93) probes rs[lo + filter_cutoff].hash == hash;
-                // equal hashes are contiguous from lo to ub (one bucket), so that is
-                // ub - lo > filter_cutoff, and the probe's random line is not fetched
-                if (ub - lo > (uint64_t)p.filter_cutoff) o.flags |= 2;
-                o.count = (uint32_t)min<uint64_t>(ub - lo, 0xFFFFFFFFull);
-                if (o.count <= 1000) {
-                    // add_to_hits_per_ref min_diff filter (nam.cpp:68-85)
-                    int min_diff = INT_MAX;
-                    uint32_t h = 0;
-                    const int qspan = (int)q.end - (int)q.start;
-                    for (uint64_t e = lo; e < ub; ++e) {
-                        const rsa_ref_randstrobe x = eb[e];
-                        const int rspan = (int)(x.packed & 0xFF) + p.k;
-                        int d = qspan - rspan;
-                        d = d < 0 ? -d : d;
-                        if (d <= min_diff) { h++; min_diff = d; }
-                    }
-                    o.hits = h;
-                }
-                found++;
-                const uint32_t scanned = o.count <= 1000 ? o.count : 0;
-                if (!(o.flags & 2)) { good++; hfind += o.hits; sfind += scanned; }
-                if (o.count <= 1000) hall += o.hits;
-                sall += scanned;
-            }
+            o = lookup_one(q, p, lo, ub, eb);
+            ls.add(o);
             qi[base + i] = o;
         }
         // the non-filtered randstrobes' hits, in randstrobe order, into the read's slot
         const bool emit = (o.flags & 1) && !(o.flags & 2) && o.hits > 0;
         int tot;
         const int at = hoff + wave_excl_scan_lk(emit ? (int)o.hits : 0, lane, tot);
-        if (emit && at + (int)o.hits <= LK_HCAP) {
-            const int qs = (int)q.start, qe = (int)q.end;
-            int min_diff = INT_MAX, h = at;
-            for (uint64_t e = lo; e < ub; ++e) {
-                const rsa_ref_randstrobe x = eb[e];
-                const int rs0 = (int)x.position;
-                const int re0 = rs0 + (int)(x.packed & 0xFF) + p.k;
-                int d = (qe - qs) - (re0 - rs0);
-                d = d < 0 ? -d : d;
-                if (d <= min_diff) {
-                    HitD hd;
-                    hd.qs = qs; hd.qe = qe; hd.rs = rs0; hd.re = re0;
-                    hd.list = (int32_t)(x.packed >> 8);
-                    hd.pad = q.is_reverse ? 1 : 0;
-                    slot[h++] = hd;
-                    min_diff = d;
-                }
-            }
-        }
+        if (emit && at + (int)o.hits <= LK_HCAP) lk_emit(q, lo, ub, eb, p, slot, at);
         hoff += tot;
     }
-    for (int off = 32; off > 0; off >>= 1) {
-        found += __shfl_xor(found, off, 64);
-        good += __shfl_xor(good, off, 64);
-        hfind += __shfl_xor(hfind, off, 64);
-        hall += __shfl_xor(hall, off, 64);
-        sfind += __shfl_xor(sfind, off, 64);
-        sall += __shfl_xor(sall, off, 64);
+    ls.wave_sum();
+    if (lane == 0) st[r] = ls.to_stat(1);
+}
+
+// Reads the fused kernel predicts to need their query randstrobes and QrsInfo
+// written out: the global-map pass (k_find_nams_w2 lists reads with more than
+// FN2_HCAP hits, or whose LDS maps would rehash at ~102 lists an orientation)
+// and find_nams_rescue (the rescue decision of k_rescue_select: no NAMs, which
+// is no hits, since every hit opens or extends a NAM, or nonrepetitive fraction
+// < 0.7).  A read the prediction misses is recomputed by query_lane.
+#define SQ_BIG_HITS 96
+
+// RSA_SEED_QW (qw_mode) overrides the prediction in the tests: 0 = never, 2 = always.
+// k_seed_query: k_rs_wave + k_lookup fused, one wave a read (len <= RW_MAXLEN).
+// Randstrobe x of the read is made on lane x % 64 (rs_pick from the LDS syncmers)
+// and looked up straight from registers; only its hits leave the kernel (the
+// read's fixed slot), and the per-read statistics.  The randstrobes and their
+// QrsInfo are written only for the reads predicted above (a second, rare pass
+// that repeats the picks and lookups: their lines are in L2 by then).
+__global__ void __launch_bounds__(64 * RW_WAVES)
+k_seed_query(const char* __restrict__ seq, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
+             const uint64_t* __restrict__ qbase, int n_reads, SeedIndexParams p, int32_t rescue_level, int qw_mode,
+             rsa_query_randstrobe* __restrict__ qrs, uint32_t* __restrict__ qcnt, QrsInfo* __restrict__ qi,
+             ReadStat* __restrict__ st, HitD* __restrict__ hit_slots) {
+    RW_LDS_DECL;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = blockIdx.x * RW_WAVES + w;
+    if (r >= n_reads) return;                           // the whole wave leaves together
+    const int len = (int)rlen[r];
+    if (len > RW_MAXLEN) return;                        // k_randstrobes + k_lookup take it
+    if (len < p.w_max) {                                // randstrobes.cpp:209: no randstrobes
+        if (lane == 0) { qcnt[r] = 0; st[r] = LkStat().to_stat(1); }
+        return;
     }
-    if (lane == 0) {
-        ReadStat s;
-        s.found = found; s.good = good; s.hits_find = hfind; s.hits_all = hall; s.scan_find = sfind; s.scan_all = sall;
-        st[r] = s;
+    uint64_t* hs = s_h[w];
+    uint32_t* sp = s_sp[w];
+    const int n = rw_syncmers(seq + roff[r], len, p, lane, s_code[w], s_nm[w], hs, sp, &s_n[w]);
+    const int m = n > p.w_min ? n - p.w_min : 0;
+    const int nq = 2 * m;
+    HitD* slot = hit_slots + (size_t)r * LK_HCAP;
+    LkStat ls;
+    int hoff = 0;
+    for (int i0 = 0; i0 < nq; i0 += 64) {
+        const int x = i0 + lane;
+        QrsInfo o;
+        o.flags = 0; o.hits = 0;
+        rsa_query_randstrobe q;
+        uint64_t lo = 0, ub = 0;
+        const rsa_ref_randstrobe* eb = p.rs;
+        if (x < nq) {
+            const bool rcx = x >= m;
+            uint64_t h; uint32_t a, b;
+            rs_pick(hs, sp, n, rcx ? x - m : x, rcx, len, p, h, a, b);
+            q.hash = h; q.start = a; q.end = b + (uint32_t)p.k; q.is_reverse = rcx ? 1 : 0; q.pad_ = 0;
+            o = lookup_one(q, p, lo, ub, eb);
+            ls.add(o);
+        }
+        const bool emit = (o.flags & 1) && !(o.flags & 2) && o.hits > 0;
+        int tot;
+        const int at = hoff + wave_excl_scan_lk(emit ? (int)o.hits : 0, lane, tot);
+        if (emit && at + (int)o.hits <= LK_HCAP) lk_emit(q, lo, ub, eb, p, slot, at);
+        hoff += tot;
     }
+    ls.wave_sum();                                      // every lane holds the read's totals
+    const float nonrep = ls.found > 0 ? (float)ls.good / (float)ls.found : 1.0f;   // nam.cpp:920
+    const bool need = qw_mode == 2 ||
+                      (qw_mode == 1 && (ls.hfind > SQ_BIG_HITS || (rescue_level > 1 && (ls.hfind == 0 || nonrep < 0.7f))));
+    if (need) {                                         // wave-uniform
+        const uint64_t base = qbase[r];
+        for (int x = lane; x < nq; x += 64) {
+            const bool rcx = x >= m;
+            uint64_t h; uint32_t a, b;
+            rs_pick(hs, sp, n, rcx ? x - m : x, rcx, len, p, h, a, b);
+            rsa_query_randstrobe q;
+            q.hash = h; q.start = a; q.end = b + (uint32_t)p.k; q.is_reverse = rcx ? 1 : 0; q.pad_ = 0;
+            uint64_t lo, ub;
+            const rsa_ref_randstrobe* eb;
+            qrs[base + x] = q;
+            qi[base + x] = lookup_one(q, p, lo, ub, eb);
+        }
+    }
+    if (lane == 0) { qcnt[r] = (uint32_t)nq; st[r] = ls.to_stat(need ? 1u : 0u); }
+}
+
+// The query randstrobes and QrsInfo of read r on one lane, for a read the fused
+// kernel did not write them for (a global-map or rescue read it did not predict):
+// k_randstrobes' lane walk and lookup_one.  `sync` is scratch for the read's
+// syncmers (len entries).  Marks the read written.
+__device__ __noinline__ void query_lane(int r, const char* __restrict__ seq, const uint64_t* __restrict__ roff,
+                                        const uint32_t* __restrict__ rlen, const uint64_t* __restrict__ qbase,
+                                        const SeedIndexParams& p, SyncD* __restrict__ sm,
+                                        rsa_query_randstrobe* __restrict__ qrs, QrsInfo* __restrict__ qi,
+                                        ReadStat* __restrict__ st) {
+    const int len = (int)rlen[r];
+    const uint64_t base = qbase[r];
+    const int k = p.k;
+    int cnt = 0;
+    if (len >= p.w_max) {
+        const int n = syncmers_lane<0>(seq + roff[r], len, p, sm);
+        for (int o = 0; o < 2 && n > 0; ++o) {
+            if (o == 1) {                                // the reverse complement's syncmers
+                for (int i = 0, j = n - 1; i < j; ++i, --j) { const SyncD x = sm[i]; sm[i] = sm[j]; sm[j] = x; }
+                for (int i = 0; i < n; ++i) sm[i].pos = (uint32_t)(len - (int)sm[i].pos - k);
+            }
+            for (int i = 0; i + p.w_min < n; ++i) {
+                uint64_t h; uint32_t a, b;
+                rs_get(sm, n, i, p, h, a, b);
+                rsa_query_randstrobe q;
+                q.hash = h; q.start = a; q.end = b + (uint32_t)k; q.is_reverse = (uint32_t)o; q.pad_ = 0;
+                uint64_t lo, ub;
+                const rsa_ref_randstrobe* eb;
+                qrs[base + cnt] = q;
+                qi[base + cnt] = lookup_one(q, p, lo, ub, eb);
+                cnt++;
+            }
+        }
+    }
+    st[r].qw = 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -1250,9 +1417,10 @@ k_find_nams_w2(const ReadStat* __restrict__ st, const HitD* __restrict__ hit_slo
 // ---------------------------------------------------------------------------
 #define BIG_LANES 32
 __global__ void __launch_bounds__(64)
-k_find_nams_big(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi,
-                const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, const ReadStat* __restrict__ st,
-                SeedIndexParams p, SeedPool pool, uint8_t* __restrict__ map_scratch, uint32_t map_cap,
+k_find_nams_big(rsa_query_randstrobe* __restrict__ qrs, QrsInfo* __restrict__ qi,
+                const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, ReadStat* __restrict__ st,
+                const char* __restrict__ seq, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
+                RescueScratch scr, SeedIndexParams p, SeedPool pool, uint8_t* __restrict__ map_scratch, uint32_t map_cap,
                 uint32_t* __restrict__ ncnt, float* __restrict__ nonrep, uint32_t* __restrict__ flags,
                 uint64_t* __restrict__ nsrc, SeedHdr* __restrict__ hdr, const uint32_t* __restrict__ big_list) {
     const int lane = threadIdx.x;
@@ -1264,6 +1432,7 @@ k_find_nams_big(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __r
         const unsigned long long e = atomicAdd(&hdr->pool_used, (unsigned long long)hf);
         if (e + hf > pool.n) { atomicOr(&hdr->errors, SEED_E_POOL); ncnt[r] = 0; continue; }
         nsrc[r] = pool.arena_base + e;
+        if (!st[r].qw) query_lane(r, seq, roff, rlen, qbase, p, scr.sync(qbase[r]), qrs, qi, st);
         find_nams_read(r, qrs, qi, qcnt, qbase, st, p, pool.hits + e, pool.open + e, pool.nams + e,
                        map_scratch + (size_t)lane * map_stride(map_cap), map_cap, ncnt, nonrep, flags);
         if (flags[r] & 2u) atomicOr(&hdr->errors, SEED_E_FIND);
@@ -1273,7 +1442,6 @@ k_find_nams_big(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __r
 // ---------------------------------------------------------------------------
 // k_rescue: find_nams_rescue for listed reads (one lane per read)
 // ---------------------------------------------------------------------------
-struct RescueD { uint64_t pos; uint32_t count, qs, qe, pad; };
 
 __device__ __forceinline__ bool rcmp1(const RescueD& a, const RescueD& b) {   // nam.cpp:943-946
     if (a.count != b.count) return a.count < b.count;
@@ -1396,8 +1564,10 @@ k_rescue_select(int n_reads, int32_t rescue_level, const ReadStat* __restrict__ 
 // lane 0, maps in LDS; a fixed grid walks the device list
 #define RESCUE_GRID 256
 __global__ void __launch_bounds__(64 * FN_WAVES)
-k_rescue_w(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi,
-           const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, SeedIndexParams p,
+k_rescue_w(rsa_query_randstrobe* __restrict__ qrs, QrsInfo* __restrict__ qi,
+           const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, ReadStat* __restrict__ st,
+           const char* __restrict__ seq, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
+           SeedIndexParams p,
            uint32_t rescue_cutoff, RescueD* __restrict__ rbuf, SeedPool pool, uint32_t* __restrict__ ncnt2,
            uint32_t* __restrict__ flags, const uint64_t* __restrict__ rbase, SeedHdr* __restrict__ hdr,
            const uint32_t* __restrict__ rlist, uint32_t* __restrict__ rbig_list) {
@@ -1407,6 +1577,7 @@ k_rescue_w(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restri
     const uint32_t nr = hdr->rcount;
     for (uint32_t t = blockIdx.x * FN_WAVES + w; t < nr; t += gridDim.x * FN_WAVES) {
         const int r = (int)rlist[t];
+        if (!st[r].qw) query_lane(r, seq, roff, rlen, qbase, p, RescueScratch{rbuf}.sync(qbase[r]), qrs, qi, st);
         rescue_read(r, qrs, qi, qcnt, qbase, rbase, p, rescue_cutoff, rbuf, pool.hits, pool.open, pool.nams, pool.grp,
                     pool.added, s_map[w], FN_MAP_CAP, ncnt2, flags);
         if (flags[r] & 4u) rbig_list[atomicAdd(&hdr->rbig_count, 1u)] = (uint32_t)r;
@@ -1416,8 +1587,10 @@ k_rescue_w(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restri
 // the rescued reads whose maps outgrow LDS: one lane per read, global map scratch,
 // the read's pool entries again
 __global__ void __launch_bounds__(64)
-k_rescue_big(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi,
-             const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, SeedIndexParams p,
+k_rescue_big(rsa_query_randstrobe* __restrict__ qrs, QrsInfo* __restrict__ qi,
+             const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, ReadStat* __restrict__ st,
+             const char* __restrict__ seq, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
+             SeedIndexParams p,
              uint32_t rescue_cutoff, RescueD* __restrict__ rbuf, SeedPool pool, uint8_t* __restrict__ map_scratch,
              uint32_t map_cap, uint32_t* __restrict__ ncnt2, uint32_t* __restrict__ flags,
              const uint64_t* __restrict__ rbase, SeedHdr* __restrict__ hdr, const uint32_t* __restrict__ rbig_list) {
@@ -1426,6 +1599,7 @@ k_rescue_big(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __rest
     const uint32_t nb = hdr->rbig_count;
     for (uint32_t t = lane; t < nb; t += BIG_LANES) {
         const int r = (int)rbig_list[t];
+        if (!st[r].qw) query_lane(r, seq, roff, rlen, qbase, p, RescueScratch{rbuf}.sync(qbase[r]), qrs, qi, st);
         rescue_read(r, qrs, qi, qcnt, qbase, rbase, p, rescue_cutoff, rbuf, pool.hits, pool.open, pool.nams, pool.grp,
                     pool.added, map_scratch + (size_t)lane * map_stride(map_cap), map_cap, ncnt2, flags);
         if (flags[r] & 4u) atomicOr(&hdr->errors, SEED_E_RESCUE);
@@ -1439,7 +1613,7 @@ k_rescue_big(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __rest
 // tiles of 4096, each thread 16 consecutive reads whose loads all issue before
 // the tile's scan (a thread walking a private run of reads waited on one
 // dependent load per read: 142 us a call).
-#define SEED_NSTAT 13
+#define SEED_NSTAT 14
 #define SS_TPB 256           // one workgroup of 4 waves: it finds a CU sooner on a busy GPU than 16 waves did
 #define SS_PER 16            // reads a thread takes per tile (tiles of SS_TPB * SS_PER = 4096 reads)
 #define SS_WAVES (SS_TPB / 64)
@@ -1451,7 +1625,7 @@ k_seed_scan(int n_reads, const uint8_t* __restrict__ rescued, const uint32_t* __
     __shared__ unsigned long long s_stat[SEED_NSTAT];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     if (t < SEED_NSTAT) s_stat[t] = 0;
-    uint64_t v[SEED_NSTAT] = {0};    // qrs found good hits_find hits_all scan_find scan_all n1 n2 rr rq rscan rhits
+    uint64_t v[SEED_NSTAT] = {0};    // qrs found good hits_find hits_all scan_find scan_all n1 n2 rr rq rscan rhits qw_q
     uint64_t carry = 0;
     for (int base = 0; base < n_reads; base += SS_TPB * SS_PER) {
         const int r0 = base + t * SS_PER;
@@ -1469,6 +1643,7 @@ k_seed_scan(int n_reads, const uint8_t* __restrict__ rescued, const uint32_t* __
                 v[0] += q; v[1] += x.found; v[2] += x.good; v[3] += x.hits_find; v[4] += x.hits_all;
                 v[5] += x.scan_find; v[6] += x.scan_all; v[7] += c1; v[8] += c2;
                 if (rs) { v[9] += 1; v[10] += q; v[11] += x.scan_all; v[12] += x.hits_all; }
+                if (x.qw) v[13] += q;
             }
             mine += cnt[j];
         }
@@ -1504,7 +1679,7 @@ k_seed_scan(int n_reads, const uint8_t* __restrict__ rescued, const uint32_t* __
         hdr->qrs = s_stat[0]; hdr->found = s_stat[1]; hdr->good = s_stat[2]; hdr->hits_find = s_stat[3];
         hdr->hits_all = s_stat[4]; hdr->scan_find = s_stat[5]; hdr->scan_all = s_stat[6]; hdr->n1 = s_stat[7];
         hdr->n2 = s_stat[8]; hdr->resc_reads = s_stat[9]; hdr->resc_q = s_stat[10]; hdr->resc_scan = s_stat[11];
-        hdr->resc_hits = s_stat[12];
+        hdr->resc_hits = s_stat[12]; hdr->qw_q = s_stat[13];
     }
 }
 
@@ -2084,6 +2259,10 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
     }
     const uint32_t n_lane = wave_ok ? n_long : n;
     const XLayout X(n, wave_ok ? n_long : 0);
+    // RSA_SEED_QW (tests): 1 = k_seed_query writes the randstrobes of the reads it predicts
+    // the global-map / rescue passes need, 0 = of none (query_lane makes them), 2 = of all
+    const char* qwv = getenv("RSA_SEED_QW");
+    const int qw_mode = qwv ? atoi(qwv) : 1;
     SCHK(hens(b, H_X, X.down));
     char* hx = (char*)b.h[H_X];
     memcpy(hx + X.roff, rb->offsets, 8ull * n);
@@ -2143,15 +2322,12 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
                             DP(B_PADD, uint8_t), b.pool_n, slots};
         memset(hx, 0, sizeof(SeedHdr));             // counters start at zero (a retry re-zeroes them)
         SCHK(hipMemcpyAsync(dx, hx, X.up, hipMemcpyHostToDevice, st));
-        // 1. randstrobes (randstrobes.cpp:207-253)
-        kt.begin(st, RSA_K_RANDSTROBES);
-        if (wave_ok)
-            hipLaunchKernelGGL(k_rs_wave, dim3((n + RW_WAVES - 1) / RW_WAVES), dim3(64 * RW_WAVES), 0, st,
-                               D_SEQ, d_roff, d_rlen, d_qbase, (int)n, p, DP(B_QRS, rsa_query_randstrobe),
-                               DP(B_QCNT, uint32_t));
+        // 1. reads the fused kernel does not take (longer than RW_MAXLEN, or parameters
+        //    outside its limits): randstrobes one lane per read (randstrobes.cpp:207-253)
+        const int* lane_list = wave_ok ? (const int*)(dx + X.rsl) : nullptr;
         if (n_lane) {
+            kt.begin(st, RSA_K_RANDSTROBES);
             SCHK(dens(b, B_SYNC, sizeof(SyncD) * (nq_cap / 2 + 1)));
-            const int* lane_list = wave_ok ? (const int*)(dx + X.rsl) : nullptr;
             if (p.k - p.s + 1 == 5)
                 hipLaunchKernelGGL(k_randstrobes<5>, dim3((n_lane + 63) / 64), dim3(64), 0, st, D_SEQ, d_roff,
                                    d_rlen, d_qbase, (int)n_lane, lane_list, p, DP(B_SYNC, SyncD),
@@ -2160,14 +2336,21 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
                 hipLaunchKernelGGL(k_randstrobes<0>, dim3((n_lane + 63) / 64), dim3(64), 0, st, D_SEQ, d_roff,
                                    d_rlen, d_qbase, (int)n_lane, lane_list, p, DP(B_SYNC, SyncD),
                                    DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t));
+            SCHK(hipGetLastError());
+            kt.end(st);
         }
-        SCHK(hipGetLastError());
-        kt.end(st);
-        // 2. lookups + the min_diff hits (index.hpp:57-93, nam.cpp:68-85)
+        // 2. randstrobes + lookups + the min_diff hits (randstrobes.cpp:207-253, index.hpp:57-93,
+        //    nam.cpp:68-85): fused, one wave a read; the lane-walked reads through k_lookup
         kt.begin(st, RSA_K_LOOKUP);
-        hipLaunchKernelGGL(k_lookup, dim3((n + 3) / 4), dim3(256), 0, st, DP(B_QRS, rsa_query_randstrobe),
-                           DP(B_QCNT, uint32_t), d_qbase, (int)n, p, DP(B_QI, QrsInfo), DP(B_ST, ReadStat),
-                           DP(B_SLOTS, HitD));
+        if (wave_ok)
+            hipLaunchKernelGGL(k_seed_query, dim3((n + RW_WAVES - 1) / RW_WAVES), dim3(64 * RW_WAVES), 0, st,
+                               D_SEQ, d_roff, d_rlen, d_qbase, (int)n, p, rescue_level, qw_mode,
+                               DP(B_QRS, rsa_query_randstrobe), DP(B_QCNT, uint32_t), DP(B_QI, QrsInfo),
+                               DP(B_ST, ReadStat), DP(B_SLOTS, HitD));
+        if (n_lane)
+            hipLaunchKernelGGL(k_lookup, dim3((n_lane + 3) / 4), dim3(256), 0, st, DP(B_QRS, rsa_query_randstrobe),
+                               DP(B_QCNT, uint32_t), d_qbase, (int)n_lane, lane_list, p, DP(B_QI, QrsInfo),
+                               DP(B_ST, ReadStat), DP(B_SLOTS, HitD));
         SCHK(hipGetLastError());
         kt.end(st);
         // 3. find_nams (nam.cpp:771-926): LDS maps, then the listed reads with global maps
@@ -2177,7 +2360,8 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
                            DP(B_NCNT1, uint32_t), d_nonrep, DP(B_FLAGS, uint32_t), DP(B_NSRC, uint64_t), dhdr,
                            DP(B_BIGL, uint32_t));
         hipLaunchKernelGGL(k_find_nams_big, dim3(1), dim3(64), 0, st, DP(B_QRS, rsa_query_randstrobe),
-                           DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t), d_qbase, DP(B_ST, ReadStat), p, pool,
+                           DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t), d_qbase, DP(B_ST, ReadStat), D_SEQ, d_roff,
+                           d_rlen, RescueScratch{DP(B_RBUF, RescueD)}, p, pool,
                            DP(B_MAP, uint8_t), MAP_BIG, DP(B_NCNT1, uint32_t), d_nonrep, DP(B_FLAGS, uint32_t),
                            DP(B_NSRC, uint64_t), dhdr, DP(B_BIGL, uint32_t));
         SCHK(hipGetLastError());
@@ -2188,11 +2372,12 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
                            DP(B_ST, ReadStat), DP(B_NCNT1, uint32_t), d_nonrep, DP(B_NCNT2, uint32_t),
                            DP(B_RBASE, uint64_t), d_resc, b.pool_n, dhdr, DP(B_RLIST, uint32_t));
         hipLaunchKernelGGL(k_rescue_w, dim3(RESCUE_GRID), dim3(64 * FN_WAVES), 0, st, DP(B_QRS, rsa_query_randstrobe),
-                           DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t), d_qbase, p, rescue_cutoff, DP(B_RBUF, RescueD),
+                           DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t), d_qbase, DP(B_ST, ReadStat), D_SEQ, d_roff,
+                           d_rlen, p, rescue_cutoff, DP(B_RBUF, RescueD),
                            pool, DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t), DP(B_RBASE, uint64_t), dhdr,
                            DP(B_RLIST, uint32_t), DP(B_RBIGL, uint32_t));
         hipLaunchKernelGGL(k_rescue_big, dim3(1), dim3(64), 0, st, DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo),
-                           DP(B_QCNT, uint32_t), d_qbase, p, rescue_cutoff, DP(B_RBUF, RescueD), pool,
+                           DP(B_QCNT, uint32_t), d_qbase, DP(B_ST, ReadStat), D_SEQ, d_roff, d_rlen, p, rescue_cutoff, DP(B_RBUF, RescueD), pool,
                            DP(B_MAP, uint8_t), MAP_BIG, DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t),
                            DP(B_RBASE, uint64_t), dhdr, DP(B_RBIGL, uint32_t));
         SCHK(hipGetLastError());
@@ -2270,10 +2455,12 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
                  NAM = sizeof(rsa_nam), HIT = sizeof(HitD);
     c.reads = n; c.read_bases = bases; c.qrs = hh.qrs; c.found = hh.found; c.filtered = hh.found - hh.good;
     c.hits = hh.hits_find; c.nams = total; c.rescued = hh.resc_reads;
-    c.alg_bytes[RSA_K_RANDSTROBES] = (double)bases + QRS * hh.qrs + 24.0 * n;
-    // query randstrobe, bucket bounds, QrsInfo; the found entries; the hits into the slots
-    c.alg_bytes[RSA_K_LOOKUP] = (QRS + 16 + QI) * hh.qrs + 8.0 * hh.found + RS * hh.scan_all + HIT * hh.hits_find +
-                                sizeof(ReadStat) * (double)n;
+    // fused (k_seed_query): the read bases and read table, per query randstrobe its bucket bounds,
+    // the found entries, the hits into the slots, the per-read results; the randstrobes and
+    // QrsInfo stay in registers (the predicted rescue / global-map reads aside: hh.qw_q)
+    c.alg_bytes[RSA_K_RANDSTROBES] = 0;
+    c.alg_bytes[RSA_K_LOOKUP] = (double)bases + 24.0 * n + 16.0 * hh.qrs + 8.0 * hh.found + RS * hh.scan_all +
+                                HIT * hh.hits_find + sizeof(ReadStat) * (double)n + (QRS + QI) * hh.qw_q;
     // the hits from the read's slot (k_lookup wrote them), the NAMs, the per-read results
     c.alg_bytes[RSA_K_FIND_NAMS] = HIT * hh.hits_find + NAM * hh.n1 + (16.0 + sizeof(ReadStat)) * n;
     c.alg_bytes[RSA_K_RESCUE] = (QRS + QI) * hh.resc_q + RS * hh.resc_scan + 2 * HIT * hh.resc_hits + NAM * hh.n2;

@@ -124,6 +124,33 @@ def test_seed_by_score_order(setup):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("qw", ["0", "2"])
+def test_seed_query_write_modes(setup, monkeypatch, qw):
+    """k_seed_query (randstrobes + lookup fused) writes a read's query randstrobes and
+    QrsInfo only when it predicts the global-map or rescue pass will read them; the
+    passes make them themselves (query_lane) for a read it did not.  RSA_SEED_QW=0
+    (never written: every rescued / global-map read goes through query_lane) and 2
+    (always written) must both give the oracle's NAMs.  Reads of 520-840 bases (joined
+    golden reads) take the lane path (k_randstrobes + k_lookup) beside the fused one."""
+    name, idx, ctx, ora = setup
+    reads = _reads(name)
+    joined = [b"".join(reads[i:i + 6])[:520 + 40 * (i % 9)] for i in range(0, min(len(reads), 60), 6)]
+    reads = reads + [r for r in joined if len(r) > 512]
+    monkeypatch.setenv("RSA_SEED_QW", qw)
+    for rescue_level in (2, 1):
+        nams, nonrep, resc = ctx.seed(reads, rescue_level=rescue_level)
+        bad = []
+        for i, r in enumerate(reads):
+            w, wn, wr = ora.seed(r, rescue_level=rescue_level)
+            if not _nam_equal(nams[i], w) or np.float32(nonrep[i]).view(np.uint32) != np.float32(wn).view(np.uint32) \
+                    or bool(resc[i]) != wr:
+                bad.append(i)
+        assert not bad, f"RSA_SEED_QW={qw} rescue_level={rescue_level}: {len(bad)} reads differ, first {bad[:5]}"
+        if rescue_level == 2:
+            assert any(resc), "no rescued read: the fallback did not run"
+
+
+@pytest.mark.gpu
 def test_seed_batch_independent(setup):
     name, idx, ctx, ora = setup
     reads = _reads(name)
