@@ -206,9 +206,10 @@ KERNEL_LIMITER = {
     "ext_band_wide": "latency of the few (~3 a call) 64-lane jobs, one wave each",
     "find_nams": "LDS latency and divergence of the robin_hood map emulation, one wave per read",
     "sites": "latency of random reference windows (one read per NAM)",
-    "lookup": "random HBM lines: one 128-B bucket line per query randstrobe (bounds + up to 7 entries; "
-              "larger buckets add their entries' line)",
-    "randstrobes": "xxh64 and the syncmer window in LDS, one wave per read",
+    "lookup": "k_seed_query (randstrobes + lookup fused, one wave per read): xxh64 and the syncmer window in "
+              "LDS, then random HBM lines: one 128-B bucket line per query randstrobe (bounds + up to 7 "
+              "entries; larger buckets add their entries' line)",
+    "randstrobes": "one lane per read (reads over 512 bp only)",
     "rescue": "latency, rescued reads only",
 }
 

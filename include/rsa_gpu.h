@@ -302,7 +302,9 @@ int rsa_index_download(rsa_ctx* ctx, rsa_ref_randstrobe* randstrobes, uint64_t* 
 /* kernels of the path, in stats arrays */
 enum {
     RSA_K_RANDSTROBES = 0, /* syncmers + randstrobes per read (randstrobes.cpp:57-254) */
-    RSA_K_LOOKUP = 1,      /* bucket lookup, filter probe, min_diff count (nam.cpp:68-85,920-943) */
+    RSA_K_LOOKUP = 1,      /* randstrobes + bucket lookup, filter probe, min_diff count, fused (k_seed_query;
+                            * randstrobes.cpp:57-254, nam.cpp:68-85,920-943); RANDSTROBES then times only
+                            * the lane kernel of reads over 512 bp */
     RSA_K_FIND_NAMS = 2,   /* hits_per_ref + merge_hits_into_nams (nam.cpp:87-245) */
     RSA_K_RESCUE = 3,      /* find_nams_rescue (nam.cpp:946-1010) */
     RSA_K_COMPACT = 4,     /* NAM output compaction */
@@ -331,6 +333,9 @@ typedef struct rsa_kernel_stats {
     /* wall time of the calls ([0] rsa_seed, [1] rsa_extend), ms summed over calls: whole call,
      * waiting for a free stream lane, blocked on the device (event waits); the rest is host work */
     double call_ms[2], lane_wait_ms[2], device_wait_ms[2];
+    /* query randstrobes the seeding call wrote out (the reads k_seed_query predicted the
+     * global-map / rescue passes need), and reads whose randstrobes those passes had to make */
+    uint64_t query_written, query_fixed_reads;
 } rsa_kernel_stats;
 
 int rsa_get_stats(rsa_ctx* ctx, rsa_kernel_stats* out);

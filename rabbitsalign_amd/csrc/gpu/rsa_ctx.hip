@@ -916,6 +916,8 @@ int rsa_seed(rsa_ctx* ctx, const rsa_read_batch* rb, int32_t rescue_level, uint3
     ctx->stats.hits += c.hits;
     ctx->stats.nams += c.nams;
     ctx->stats.rescued_reads += c.rescued;
+    ctx->stats.query_written += c.qw;
+    ctx->stats.query_fixed_reads += c.qfix;
     return RSA_OK;
 }
 

@@ -69,5 +69,6 @@ struct KTimer {
 // per-call counters and algorithmic bytes of the seeding kernels
 struct SeedCounters {
     uint64_t reads = 0, read_bases = 0, qrs = 0, found = 0, filtered = 0, hits = 0, nams = 0, rescued = 0;
+    uint64_t qw = 0, qfix = 0;      // query randstrobes written out; reads query_lane made them for
     double alg_bytes[RSA_K_COUNT] = {0};
 };

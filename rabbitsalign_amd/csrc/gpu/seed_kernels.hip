@@ -75,6 +75,7 @@ struct SeedHdr {
     // statistics (DESIGN.md "Kernels": algorithmic bytes and per-read counts)
     unsigned long long qrs, found, good, hits_find, hits_all, scan_find, scan_all, n1, n2, resc_reads, resc_q,
         resc_scan, resc_hits, qw_q;   // qw_q: query randstrobes written out (reads with ReadStat::qw)
+    unsigned long long qfix;        // reads query_lane made the randstrobes of (k_seed_query's prediction missed)
 };
 
 // The call's pool: per entry one hit, one open NAM, one NAM, one group hit and
@@ -737,7 +738,7 @@ __device__ __noinline__ void query_lane(int r, const char* __restrict__ seq, con
                                         const uint32_t* __restrict__ rlen, const uint64_t* __restrict__ qbase,
                                         const SeedIndexParams& p, SyncD* __restrict__ sm,
                                         rsa_query_randstrobe* __restrict__ qrs, QrsInfo* __restrict__ qi,
-                                        ReadStat* __restrict__ st) {
+                                        ReadStat* __restrict__ st, SeedHdr* __restrict__ hdr) {
     const int len = (int)rlen[r];
     const uint64_t base = qbase[r];
     const int k = p.k;
@@ -763,6 +764,7 @@ __device__ __noinline__ void query_lane(int r, const char* __restrict__ seq, con
         }
     }
     st[r].qw = 1;
+    atomicAdd(&hdr->qfix, 1ull);
 }
 
 // ---------------------------------------------------------------------------
@@ -1432,7 +1434,7 @@ k_find_nams_big(rsa_query_randstrobe* __restrict__ qrs, QrsInfo* __restrict__ qi
         const unsigned long long e = atomicAdd(&hdr->pool_used, (unsigned long long)hf);
         if (e + hf > pool.n) { atomicOr(&hdr->errors, SEED_E_POOL); ncnt[r] = 0; continue; }
         nsrc[r] = pool.arena_base + e;
-        if (!st[r].qw) query_lane(r, seq, roff, rlen, qbase, p, scr.sync(qbase[r]), qrs, qi, st);
+        if (!st[r].qw) query_lane(r, seq, roff, rlen, qbase, p, scr.sync(qbase[r]), qrs, qi, st, hdr);
         find_nams_read(r, qrs, qi, qcnt, qbase, st, p, pool.hits + e, pool.open + e, pool.nams + e,
                        map_scratch + (size_t)lane * map_stride(map_cap), map_cap, ncnt, nonrep, flags);
         if (flags[r] & 2u) atomicOr(&hdr->errors, SEED_E_FIND);
@@ -1560,14 +1562,28 @@ k_rescue_select(int n_reads, int32_t rescue_level, const ReadStat* __restrict__ 
     rlist[atomicAdd(&hdr->rcount, 1u)] = (uint32_t)r;
 }
 
+// The rescued reads whose query randstrobes k_seed_query did not write (a read its
+// prediction missed): query_lane makes them before k_rescue_w reads them.  One
+// block walking the device list; normally it finds nothing to do.  (A separate
+// launch: the call inside k_rescue_w put a stack frame into that kernel.)
+__global__ void __launch_bounds__(64)
+k_query_fix(const uint32_t* __restrict__ rlist, SeedHdr* __restrict__ hdr, const char* __restrict__ seq,
+            const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen, const uint64_t* __restrict__ qbase,
+            SeedIndexParams p, RescueScratch scr, rsa_query_randstrobe* __restrict__ qrs, QrsInfo* __restrict__ qi,
+            ReadStat* __restrict__ st) {
+    const uint32_t nr = hdr->rcount;
+    for (uint32_t t = threadIdx.x; t < nr; t += 64) {
+        const int r = (int)rlist[t];
+        if (!st[r].qw) query_lane(r, seq, roff, rlen, qbase, p, scr.sync(qbase[r]), qrs, qi, st, hdr);
+    }
+}
+
 // find_nams_rescue (nam.cpp:955-1012) of the listed reads: one wave per read,
 // lane 0, maps in LDS; a fixed grid walks the device list
 #define RESCUE_GRID 256
 __global__ void __launch_bounds__(64 * FN_WAVES)
-k_rescue_w(rsa_query_randstrobe* __restrict__ qrs, QrsInfo* __restrict__ qi,
-           const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, ReadStat* __restrict__ st,
-           const char* __restrict__ seq, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
-           SeedIndexParams p,
+k_rescue_w(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi,
+           const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, SeedIndexParams p,
            uint32_t rescue_cutoff, RescueD* __restrict__ rbuf, SeedPool pool, uint32_t* __restrict__ ncnt2,
            uint32_t* __restrict__ flags, const uint64_t* __restrict__ rbase, SeedHdr* __restrict__ hdr,
            const uint32_t* __restrict__ rlist, uint32_t* __restrict__ rbig_list) {
@@ -1577,7 +1593,6 @@ k_rescue_w(rsa_query_randstrobe* __restrict__ qrs, QrsInfo* __restrict__ qi,
     const uint32_t nr = hdr->rcount;
     for (uint32_t t = blockIdx.x * FN_WAVES + w; t < nr; t += gridDim.x * FN_WAVES) {
         const int r = (int)rlist[t];
-        if (!st[r].qw) query_lane(r, seq, roff, rlen, qbase, p, RescueScratch{rbuf}.sync(qbase[r]), qrs, qi, st);
         rescue_read(r, qrs, qi, qcnt, qbase, rbase, p, rescue_cutoff, rbuf, pool.hits, pool.open, pool.nams, pool.grp,
                     pool.added, s_map[w], FN_MAP_CAP, ncnt2, flags);
         if (flags[r] & 4u) rbig_list[atomicAdd(&hdr->rbig_count, 1u)] = (uint32_t)r;
@@ -1587,10 +1602,8 @@ k_rescue_w(rsa_query_randstrobe* __restrict__ qrs, QrsInfo* __restrict__ qi,
 // the rescued reads whose maps outgrow LDS: one lane per read, global map scratch,
 // the read's pool entries again
 __global__ void __launch_bounds__(64)
-k_rescue_big(rsa_query_randstrobe* __restrict__ qrs, QrsInfo* __restrict__ qi,
-             const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, ReadStat* __restrict__ st,
-             const char* __restrict__ seq, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
-             SeedIndexParams p,
+k_rescue_big(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi,
+             const uint32_t* __restrict__ qcnt, const uint64_t* __restrict__ qbase, SeedIndexParams p,
              uint32_t rescue_cutoff, RescueD* __restrict__ rbuf, SeedPool pool, uint8_t* __restrict__ map_scratch,
              uint32_t map_cap, uint32_t* __restrict__ ncnt2, uint32_t* __restrict__ flags,
              const uint64_t* __restrict__ rbase, SeedHdr* __restrict__ hdr, const uint32_t* __restrict__ rbig_list) {
@@ -1599,7 +1612,6 @@ k_rescue_big(rsa_query_randstrobe* __restrict__ qrs, QrsInfo* __restrict__ qi,
     const uint32_t nb = hdr->rbig_count;
     for (uint32_t t = lane; t < nb; t += BIG_LANES) {
         const int r = (int)rbig_list[t];
-        if (!st[r].qw) query_lane(r, seq, roff, rlen, qbase, p, RescueScratch{rbuf}.sync(qbase[r]), qrs, qi, st);
         rescue_read(r, qrs, qi, qcnt, qbase, rbase, p, rescue_cutoff, rbuf, pool.hits, pool.open, pool.nams, pool.grp,
                     pool.added, map_scratch + (size_t)lane * map_stride(map_cap), map_cap, ncnt2, flags);
         if (flags[r] & 4u) atomicOr(&hdr->errors, SEED_E_RESCUE);
@@ -2371,13 +2383,16 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
         hipLaunchKernelGGL(k_rescue_select, dim3((n + 255) / 256), dim3(256), 0, st, (int)n, rescue_level,
                            DP(B_ST, ReadStat), DP(B_NCNT1, uint32_t), d_nonrep, DP(B_NCNT2, uint32_t),
                            DP(B_RBASE, uint64_t), d_resc, b.pool_n, dhdr, DP(B_RLIST, uint32_t));
+        if (wave_ok)
+            hipLaunchKernelGGL(k_query_fix, dim3(1), dim3(64), 0, st, DP(B_RLIST, uint32_t), dhdr, D_SEQ, d_roff,
+                               d_rlen, d_qbase, p, RescueScratch{DP(B_RBUF, RescueD)},
+                               DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo), DP(B_ST, ReadStat));
         hipLaunchKernelGGL(k_rescue_w, dim3(RESCUE_GRID), dim3(64 * FN_WAVES), 0, st, DP(B_QRS, rsa_query_randstrobe),
-                           DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t), d_qbase, DP(B_ST, ReadStat), D_SEQ, d_roff,
-                           d_rlen, p, rescue_cutoff, DP(B_RBUF, RescueD),
+                           DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t), d_qbase, p, rescue_cutoff, DP(B_RBUF, RescueD),
                            pool, DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t), DP(B_RBASE, uint64_t), dhdr,
                            DP(B_RLIST, uint32_t), DP(B_RBIGL, uint32_t));
         hipLaunchKernelGGL(k_rescue_big, dim3(1), dim3(64), 0, st, DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo),
-                           DP(B_QCNT, uint32_t), d_qbase, DP(B_ST, ReadStat), D_SEQ, d_roff, d_rlen, p, rescue_cutoff, DP(B_RBUF, RescueD), pool,
+                           DP(B_QCNT, uint32_t), d_qbase, p, rescue_cutoff, DP(B_RBUF, RescueD), pool,
                            DP(B_MAP, uint8_t), MAP_BIG, DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t),
                            DP(B_RBASE, uint64_t), dhdr, DP(B_RBIGL, uint32_t));
         SCHK(hipGetLastError());
@@ -2454,7 +2469,7 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
     const double QRS = sizeof(rsa_query_randstrobe), QI = sizeof(QrsInfo), RS = sizeof(rsa_ref_randstrobe),
                  NAM = sizeof(rsa_nam), HIT = sizeof(HitD);
     c.reads = n; c.read_bases = bases; c.qrs = hh.qrs; c.found = hh.found; c.filtered = hh.found - hh.good;
-    c.hits = hh.hits_find; c.nams = total; c.rescued = hh.resc_reads;
+    c.hits = hh.hits_find; c.nams = total; c.rescued = hh.resc_reads; c.qw = hh.qw_q; c.qfix = hh.qfix;
     // fused (k_seed_query): the read bases and read table, per query randstrobe its bucket bounds,
     // the found entries, the hits into the slots, the per-read results; the randstrobes and
     // QrsInfo stay in registers (the predicted rescue / global-map reads aside: hh.qw_q)

@@ -34,6 +34,8 @@ void add_stats(rsa_kernel_stats& a, const rsa_kernel_stats& b) {
         a.lane_wait_ms[i] += b.lane_wait_ms[i];
         a.device_wait_ms[i] += b.device_wait_ms[i];
     }
+    a.query_written += b.query_written;
+    a.query_fixed_reads += b.query_fixed_reads;
 }
 
 class MultiEngine final : public Engine {

@@ -88,7 +88,7 @@ KERNELS = ["randstrobes", "lookup", "find_nams", "rescue", "compact", "ext_scan"
            "ext_band_panel", "sites"]
 # the extension scan is k_ext_scan_v unless RSA_SCAN_V=0 selects the two-layout k_ext_scan_g (rsa_ctx.hip)
 SCAN_SYMBOL = "k_ext_scan_g" if os.environ.get("RSA_SCAN_V", "1")[:1] == "0" else "k_ext_scan_v"
-KERNEL_SYMBOLS = {"randstrobes": "k_rs_wave", "lookup": "k_lookup", "find_nams": "k_find_nams_w2",
+KERNEL_SYMBOLS = {"randstrobes": "k_randstrobes", "lookup": "k_seed_query", "find_nams": "k_find_nams_w2",
                   "rescue": "k_rescue_w", "compact": "k_compact", "ext_scan": SCAN_SYMBOL, "ext_band": "k_ext_band16",
                   "ext_band_wide": "k_ext_band64", "ext_band_panel": "k_ext_band_panel",
                   "sites": "k_sites"}
@@ -106,7 +106,8 @@ class KernelStats(C.Structure):
                 ("jobs", C.c_uint64), ("dp_cells", C.c_uint64),
                 ("band_deferred", C.c_uint64), ("band_overflow", C.c_uint64),
                 ("scan_certified", C.c_uint64), ("scan_redo", C.c_uint64),
-                ("call_ms", C.c_double * 2), ("lane_wait_ms", C.c_double * 2), ("device_wait_ms", C.c_double * 2)]
+                ("call_ms", C.c_double * 2), ("lane_wait_ms", C.c_double * 2), ("device_wait_ms", C.c_double * 2),
+                ("query_written", C.c_uint64), ("query_fixed_reads", C.c_uint64)]
 
 
 def stats_dict(ks: "KernelStats") -> dict:

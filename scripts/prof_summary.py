@@ -37,26 +37,37 @@ def busy(db):
         rows = c.execute("select name, start, \"end\" from kernels order by start").fetchall()
     except sqlite3.Error:
         return None
-    seed = [r for r in rows if short(r[0]) == "k_lookup"]
+    seed = [r for r in rows if short(r[0]) in ("k_lookup", "k_seed_query")]
     if not seed:
         return None
     lo, hi = seed[0][1], max(r[2] for r in seed)
     iv = [(max(s, lo), min(e, hi)) for _, s, e in rows if e > lo and s < hi]
-    union, cur_s, cur_e, tot = 0, None, None, 0
-    win = {}
-    for s, e in iv:
-        tot += e - s
-        if cur_e is None or s > cur_e:
-            if cur_e is not None:
-                union += cur_e - cur_s
-            cur_s, cur_e = s, e
-        else:
-            cur_e = max(cur_e, e)
-    if cur_e is not None:
-        union += cur_e - cur_s
+
+    def union_of(ivs):
+        union, cur_s, cur_e, tot = 0, None, None, 0
+        for s, e in sorted(ivs):
+            tot += e - s
+            if cur_e is None or s > cur_e:
+                if cur_e is not None:
+                    union += cur_e - cur_s
+                cur_s, cur_e = s, e
+            else:
+                cur_e = max(cur_e, e)
+        if cur_e is not None:
+            union += cur_e - cur_s
+        return union, tot
+
+    union, tot = union_of(iv)
     span = hi - lo
-    return {"span_ms": span / 1e6, "busy_union_ms": union / 1e6, "busy_frac": union / span if span else None,
-            "kernel_sum_ms": tot / 1e6, "mean_concurrency": tot / union if union else None}
+    out = {"span_ms": span / 1e6, "busy_union_ms": union / 1e6, "busy_frac": union / span if span else None,
+           "kernel_sum_ms": tot / 1e6, "mean_concurrency": tot / union if union else None}
+    # the score scan's launches: their own union (two combined extension calls can overlap)
+    sc = [(max(s, lo), min(e, hi)) for n, s, e in rows if short(n).startswith("void k_ext_scan_v") and e > lo and s < hi]
+    if sc:
+        su, st = union_of(sc)
+        out["scan_v"] = {"launches": len(sc), "sum_ms": st / 1e6, "union_ms": su / 1e6,
+                         "self_concurrency": st / su if su else None}
+    return out
 
 
 def counter(db, cname):
@@ -94,10 +105,14 @@ def main():
                      f"{'' if rd is None else f'{rd:.0f}'} | {'' if wr is None else f'{wr:.0f}'} |")
     b = busy(os.path.join(src, "trace", "run_results.db"))
     if b:
-        lines += ["", f"GPU busy over the mapping span (first to last `k_lookup`, warm-up included): "
+        lines += ["", f"GPU busy over the mapping span (first to last seeding kernel, warm-up included): "
                       f"{b['busy_union_ms']:.1f} ms of {b['span_ms']:.1f} ms = {100 * b['busy_frac']:.1f} % "
                       f"(union of kernel intervals); summed kernel time {b['kernel_sum_ms']:.1f} ms, mean "
                       f"concurrency while busy {b['mean_concurrency']:.2f}."]
+        if b.get("scan_v"):
+            v = b["scan_v"]
+            lines += ["", f"`k_ext_scan_v` launches: {v['launches']}, summed duration {v['sum_ms']:.1f} ms, union "
+                          f"{v['union_ms']:.1f} ms (launches overlapping each other: {v['self_concurrency']:.2f}x)."]
     with open(out + "_rocprof.md", "w") as f:
         f.write("\n".join(lines) + "\n")
     with open(out + "_traffic.json", "w") as f:

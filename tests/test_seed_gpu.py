@@ -138,7 +138,13 @@ def test_seed_query_write_modes(setup, monkeypatch, qw):
     reads = reads + [r for r in joined if len(r) > 512]
     monkeypatch.setenv("RSA_SEED_QW", qw)
     for rescue_level in (2, 1):
+        ctx.reset_stats()
         nams, nonrep, resc = ctx.seed(reads, rescue_level=rescue_level)
+        st = ctx.stats()
+        if rescue_level == 2:
+            # 0: every rescued read's randstrobes were made by query_lane; 2: none were needed
+            assert (st["query_fixed_reads"] > 0) == (qw == "0"), st["query_fixed_reads"]
+            assert (st["query_written"] > 0) == (qw == "2") or qw == "0", st["query_written"]
         bad = []
         for i, r in enumerate(reads):
             w, wn, wr = ora.seed(r, rescue_level=rescue_level)
