@@ -10,6 +10,7 @@
 // We replay the exact single-worker timeline until the estimate is frozen; from
 // then on chunks are independent and run in parallel on the host workers, each
 // calling the GPU engine (seeding + extension) for its own chunk.
+#include <sys/mman.h>
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -645,6 +646,31 @@ void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistributio
 }
 
 }  // namespace
+
+bool huge_buffers_on() {
+    static const bool on = [] {
+        const char* v = getenv("RSA_HUGE_BUFFERS");
+        return !v || atoi(v) != 0;
+    }();
+    return on;
+}
+
+void* huge_buffer_alloc(size_t bytes) {
+    const size_t len = (bytes + kHugeBufferMin - 1) & ~(kHugeBufferMin - 1);
+    // over-map by 2 MB and trim, so the buffer starts on a huge-page boundary
+    void* m = mmap(nullptr, len + kHugeBufferMin, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (m == MAP_FAILED) throw std::bad_alloc();
+    const uintptr_t a = ((uintptr_t)m + kHugeBufferMin - 1) & ~(uintptr_t)(kHugeBufferMin - 1);
+    if (a > (uintptr_t)m) munmap(m, a - (uintptr_t)m);
+    const uintptr_t end = (uintptr_t)m + len + kHugeBufferMin;
+    if (end > a + len) munmap((void*)(a + len), end - (a + len));
+    (void)madvise((void*)a, len, MADV_HUGEPAGE);
+    return (void*)a;
+}
+
+void huge_buffer_free(void* p, size_t bytes) {
+    munmap(p, (bytes + kHugeBufferMin - 1) & ~(kHugeBufferMin - 1));
+}
 
 void tune_malloc() {
     static std::once_flag once;

@@ -543,12 +543,28 @@ std::string sam_header(const References& refs, const std::string& rg_id, const s
 // uninitialised: a record is written into room reserved with resize() (an upper
 // bound of its length) and the unused tail is cut off again, without the
 // zero fill a std::string::resize would spend on every record.
+// Buffers of 2 MB and more (a chunk's SAM text, its reverse complements) are their own
+// anonymous mappings advised for transparent huge pages (RSA_HUGE_BUFFERS=0: the heap):
+// the formatting stores and the writer's copy into the page cache then walk one TLB
+// entry per 2 MB instead of 512.  The chunk buffers are pooled, so the mappings persist.
+bool huge_buffers_on();                          // once per process (RSA_HUGE_BUFFERS, default on)
+void* huge_buffer_alloc(size_t bytes);          // throws std::bad_alloc
+void huge_buffer_free(void* p, size_t bytes);
+constexpr size_t kHugeBufferMin = size_t(2) << 20;
 template <class T> struct NoInitAlloc : std::allocator<T> {
     template <class U> struct rebind { using other = NoInitAlloc<U>; };
     NoInitAlloc() = default;
     template <class U> NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
     template <class U> void construct(U* p) noexcept { ::new ((void*)p) U; }
     template <class U, class... A> void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+    T* allocate(size_t n) {
+        if (n * sizeof(T) >= kHugeBufferMin && huge_buffers_on()) return (T*)huge_buffer_alloc(n * sizeof(T));
+        return std::allocator<T>::allocate(n);
+    }
+    void deallocate(T* p, size_t n) {
+        if (n * sizeof(T) >= kHugeBufferMin && huge_buffers_on()) huge_buffer_free(p, n * sizeof(T));
+        else std::allocator<T>::deallocate(p, n);
+    }
 };
 using SamText = std::vector<char, NoInitAlloc<char>>;
 
