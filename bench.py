@@ -281,6 +281,8 @@ def pick_io_dir(requested: str, need_bytes: int) -> str:
     import tempfile
     if requested:
         return requested
+    # the node's ranks write their files side by side: room for all of them
+    need_bytes *= max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
     for d in (tempfile.gettempdir(), "/dev/shm"):
         try:
             st = os.statvfs(d)
