@@ -365,8 +365,18 @@ __device__ __forceinline__ int qcode7(unsigned char b) {
 // jobs[order[k]] for k < n; results land at out[order[k]].  Every job handed
 // here has 0 < qlen <= 32 * RV and rlen <= WCAP (the host routes the rest to
 // k_ext_scan).
+// waves per SIMD the register allocation is held to (VS_MINW_SHORT for RV <= 5, VS_MINW_LONG
+// above; 0 = the compiler's choice)
+#ifndef VS_MINW_SHORT
+#define VS_MINW_SHORT 0
+#endif
+#ifndef VS_MINW_LONG
+#define VS_MINW_LONG 0
+#endif
+template <int RV> struct VsMinW { static constexpr int value = RV <= 5 ? VS_MINW_SHORT : VS_MINW_LONG; };
+
 template <int RV, int WCAP>
-__global__ void __launch_bounds__(64 * VS_WAVES)
+__global__ void __launch_bounds__(64 * VS_WAVES, VsMinW<RV>::value)
 k_ext_scan_v(const ExtJobDev* __restrict__ jobs, const int* __restrict__ order, int n,
              const char* __restrict__ qbuf, const char* __restrict__ ref, ScanRes* __restrict__ out,
              int match, int mismatch, int gO, int gE, int* __restrict__ err) {

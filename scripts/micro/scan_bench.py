@@ -43,8 +43,10 @@ def main():
     rng = np.random.default_rng(1)
     ref = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, 4_000_000)].copy()
     ctx = native.GpuContext(native.empty_index(ref, np.array([0, len(ref)], np.uint64)))
+    L = int(os.environ.get("SCAN_BENCH_L", "150"))      # query length; window = L + 107 (headline shape)
+    W = int(os.environ.get("SCAN_BENCH_W", str(L + 107)))
     for n in sizes:
-        q, jobs = make(rng, ref, n)
+        q, jobs = make(rng, ref, n, L, W)
         ctx.extend(q, jobs)                       # warm-up (buffers, code)
         ctx.reset_stats()
         reps = max(1, min(20, 200_000 // n))
