@@ -351,7 +351,9 @@ def self_launch(args) -> int:
         return rc or 1
     if not args.no_multi_device:
         log(0, f"multi-device leg: one process, rsam_add_devices over {args.gpus} GPUs, one SAM file")
-        rc2, md = launch.run_child([sys.executable, me, "--multi-device-leg", *argv])
+        # bounded: the rank leg's line is already in hand and must come out whatever this leg does
+        md_timeout = float(os.environ.get("RSA_BENCH_MD_TIMEOUT", "600"))
+        rc2, md = launch.run_child([sys.executable, me, "--multi-device-leg", *argv], timeout=md_timeout)
         line["multi_device"] = (md or {}).get("multi_device") if rc2 == 0 and md else \
             {"error": f"multi-device leg exited with {rc2}"}
     print(json.dumps(line), flush=True)

@@ -178,6 +178,32 @@ static bool ext_priority() {
     return on;
 }
 
+// RSA_SEED_CU_EIGHTHS=k (0..6): the seeding lanes' streams leave k eighths of the CUs to the
+// extension kernels (hipExtStreamCreateWithCUMask).  CU i stays in the mask unless
+// (i % 8 - i / 32) mod 8 < k: that removes k CUs of every 32-CU XCD whether the mask
+// enumerates CUs XCD by XCD or interleaved across the XCDs.  Default 0: no mask.
+static int seed_cu_eighths() {
+    static const int k = [] {
+        const char* v = getenv("RSA_SEED_CU_EIGHTHS");
+        const int x = v ? atoi(v) : 0;
+        return x < 0 ? 0 : (x > 6 ? 6 : x);
+    }();
+    return k;
+}
+
+static hipError_t create_seed_stream(hipStream_t* st) {
+    const int k = seed_cu_eighths();
+    int dev = 0, ncu = 0;
+    if (k > 0 && hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0) {
+        std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+        for (int i = 0; i < ncu; ++i)
+            if ((((i % 8) - (i / 32)) % 8 + 8) % 8 >= k) mask[(size_t)i / 32] |= 1u << (i % 32);
+        return hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size() * 32, mask.data());
+    }
+    return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+}
+
 static Lane* acquire_lane(rsa_ctx* ctx, int kind) {
     if (!ext_priority()) kind = LANE_SEED;
     std::unique_lock<std::mutex> g(ctx->lane_m);
@@ -197,7 +223,7 @@ static Lane* acquire_lane(rsa_ctx* ctx, int kind) {
                 (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
                 e = hipStreamCreateWithPriority(&l->stream, hipStreamNonBlocking, greatest);
             } else {
-                e = hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking);
+                e = create_seed_stream(&l->stream);
             }
             if (e != hipSuccess) { delete l; return nullptr; }
             l->busy = true;

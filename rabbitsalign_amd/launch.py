@@ -44,22 +44,50 @@ def visible_gpus(timeout: float = 300.0) -> int:
         return 0
 
 
-def _relay(cmd: list, env: dict | None) -> tuple[int, dict | None]:
+def _relay(cmd: list, env: dict | None, timeout: float | None = None) -> tuple[int, dict | None]:
     """Run `cmd`; stderr passes through live; stdout lines are relayed to stderr
-    except the last JSON object line, which is returned parsed."""
+    except the last JSON object line, which is returned parsed.  With `timeout`
+    (seconds) the child's process group is killed when it runs longer (exit code
+    124, as timeout(1) reports it)."""
+    import signal
+    import threading
     line = None
-    with subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, bufsize=1) as p:
-        for raw in p.stdout:
-            s = raw.strip()
-            if s.startswith("{") and s.endswith("}"):
+    expired = threading.Event()
+    with subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, bufsize=1,
+                          start_new_session=timeout is not None) as p:
+        def kill():
+            expired.set()
+            print(f"[launch] {cmd[1:3]} still running after {timeout:.0f} s: killed", file=sys.stderr, flush=True)
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+            except OSError:
+                return
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
                 try:
-                    line = json.loads(s)
-                    continue
-                except ValueError:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except OSError:
                     pass
-            print(raw, end="", file=sys.stderr, flush=True)
-        rc = p.wait()
-    return rc, line
+        timer = threading.Timer(timeout, kill) if timeout else None
+        if timer:
+            timer.daemon = True
+            timer.start()
+        try:
+            for raw in p.stdout:
+                s = raw.strip()
+                if s.startswith("{") and s.endswith("}"):
+                    try:
+                        line = json.loads(s)
+                        continue
+                    except ValueError:
+                        pass
+                print(raw, end="", file=sys.stderr, flush=True)
+            rc = p.wait()
+        finally:
+            if timer:
+                timer.cancel()
+    return (124 if expired.is_set() else rc), (None if expired.is_set() else line)
 
 
 def run_ranks(script: str, script_args: list, nproc: int, env: dict | None = None,
@@ -71,6 +99,7 @@ def run_ranks(script: str, script_args: list, nproc: int, env: dict | None = Non
     return _relay(cmd, env)
 
 
-def run_child(cmd: list, env: dict | None = None) -> tuple[int, dict | None]:
-    """One more process (e.g. the product's multi-device leg); (exit code, its JSON line)."""
-    return _relay(cmd, env)
+def run_child(cmd: list, env: dict | None = None, timeout: float | None = None) -> tuple[int, dict | None]:
+    """One more process (e.g. the product's multi-device leg); (exit code, its JSON line).
+    `timeout`: kill it (and report 124) after that many seconds."""
+    return _relay(cmd, env, timeout)

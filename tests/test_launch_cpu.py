@@ -45,3 +45,19 @@ def test_bench_more_gpus_than_visible_fails_cleanly():
     assert p.returncode == 2, p.stderr[-2000:]
     assert "2 GPUs requested, 0 visible" in p.stderr
     assert not any(l.strip().startswith("{") for l in p.stdout.splitlines())
+
+
+def test_run_child_timeout_kills_the_child():
+    """The multi-device leg runs under a time limit (bench.py RSA_BENCH_MD_TIMEOUT): a child
+    that outlives it is killed with its process group, and the caller gets 124 and no line
+    instead of waiting, so the rank leg's result line still comes out."""
+    import sys
+    import time
+    from rabbitsalign_amd import launch
+    t = time.time()
+    rc, line = launch.run_child([sys.executable, "-c", "import time; print('{\"x\": 1}', flush=True); time.sleep(60)"],
+                                timeout=2)
+    assert rc == 124 and line is None
+    assert time.time() - t < 30
+    rc, line = launch.run_child([sys.executable, "-c", "print('{\"x\": 2}')"], timeout=60)
+    assert rc == 0 and line == {"x": 2}
