@@ -819,16 +819,21 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
 }
 
 #define B16_GROUPS 4
-#define B16_DIRCAP 4096
 #define B16_SEGCAP 320
 
+// DIRCAP: direction bytes of one job in the reference's 3-a-cell count (one byte a cell
+// here).  4096 holds the bands of 150-bp reads up to 9 cells wide (deferral 0.04 % on
+// the headline); for 250-bp reads only 5 cells, which sent 15 % of the PE 2x250 jobs to
+// the one-wave kernel.  8192 (chosen for batches with queries over 200 bp) holds 9 cells
+// at 250 bp for 1.6x the LDS a wave (13.5 KB: 11 waves a CU instead of 20).
+template <int DIRCAP>
 __global__ void __launch_bounds__(64)
 k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan, int n_jobs,
              const int* __restrict__ idx, const char* __restrict__ qbuf, const char* __restrict__ ref,
              uint32_t* __restrict__ cig_pool, uint32_t* __restrict__ raw_pool, rsa_aln* __restrict__ out, int match,
              int mismatch, int gO, int gE, int bonus, int* __restrict__ queue, int* __restrict__ qcount,
              int* __restrict__ overflow, int* __restrict__ redo, int* __restrict__ redo_count) {
-    __shared__ __attribute__((aligned(16))) int8_t s_dir[B16_GROUPS][DirCells<B16_DIRCAP>::BYTES];
+    __shared__ __attribute__((aligned(16))) int8_t s_dir[B16_GROUPS][DirCells<DIRCAP>::BYTES];
     __shared__ uint8_t s_qc[B16_GROUPS][B16_SEGCAP];
     __shared__ uint8_t s_rc[B16_GROUPS][B16_SEGCAP];
     const int lane = threadIdx.x & 63, g = lane >> 4, z = lane & 15;
@@ -849,7 +854,7 @@ k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
         }
         return;
     }
-    const bool done = band_group<16, B16_DIRCAP, B16_SEGCAP, B16_SEGCAP>(
+    const bool done = band_group<16, DIRCAP, B16_SEGCAP, B16_SEGCAP>(
         j, z, jb, sr, qbuf, ref, cig_pool, raw_pool, out, match, mismatch, gO, gE, bonus, s_dir[g], s_qc[g], s_rc[g],
         redo, redo_count);
     if (!done && z == 0) {
@@ -1168,12 +1173,17 @@ void launch_ext_scan(int rmax, dim3 grid, dim3 block, hipStream_t st, const ExtJ
 #undef RSA_L
 }
 
-void launch_ext_band16(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n, const int* idx,
-                       const char* q, const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match,
-                       int mismatch, int gO, int gE, int bonus, int* queue, int* qcount, int* overflow, int* redo,
-                       int* redo_count) {
-    hipLaunchKernelGGL(k_ext_band16, grid, dim3(64), 0, st, jobs, scan, n, idx, q, ref, cig, raw, out, match, mismatch,
-                       gO, gE, bonus, queue, qcount, overflow, redo, redo_count);
+void launch_ext_band16(int dircap, dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n,
+                       const int* idx, const char* q, const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out,
+                       int match, int mismatch, int gO, int gE, int bonus, int* queue, int* qcount, int* overflow,
+                       int* redo, int* redo_count) {
+#define RSA_B16(DC)                                                                                                \
+    hipLaunchKernelGGL(k_ext_band16<DC>, grid, dim3(64), 0, st, jobs, scan, n, idx, q, ref, cig, raw, out, match, \
+                       mismatch, gO, gE, bonus, queue, qcount, overflow, redo, redo_count)
+    if (dircap >= 12288) RSA_B16(12288);
+    else if (dircap >= 8192) RSA_B16(8192);
+    else RSA_B16(4096);
+#undef RSA_B16
 }
 
 void launch_ext_band64(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, const char* q,

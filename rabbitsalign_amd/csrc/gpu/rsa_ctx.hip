@@ -34,7 +34,7 @@ __global__ void k_ext_band_panel(const ExtJobDev* jobs, const ScanRes* scan, int
                                  uint8_t* scratch, int64_t scr_stride, int64_t dir_cap, int match, int mismatch,
                                  int gO, int gE, int bonus, int* overflow, int over_code, int* redo,
                                  int* redo_count);
-void launch_ext_band16(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n, const int* idx,
+void launch_ext_band16(int dircap, dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n, const int* idx,
                        const char* q, const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match,
                        int mismatch, int gO, int gE, int bonus, int* queue, int* qcount, int* overflow, int* redo,
                        int* redo_count);
@@ -428,6 +428,15 @@ uint64_t rsa_extend_cigar_bound(const rsa_job_batch* jb) {
 // the raw traceback ops
 static const int64_t BIG_DIR_CAP = 16ll << 20;
 static const int BIG_CHUNK = 32;
+// k_ext_band16's direction capacity for a call whose longest query (windows <= 2 kb) is
+// qmax: 8192 above 200 bp (see k_ext_band16); RSA_BAND16_DIRCAP=4096/8192/12288 fixes it
+static int band16_dircap(uint32_t qmax) {
+    const char* v = getenv("RSA_BAND16_DIRCAP");   // per call: the tests switch it
+    const int forced = v ? atoi(v) : 0;
+    if (forced > 0) return forced;
+    return qmax > 200 ? 8192 : 4096;
+}
+
 // waves draining the band16 deferral queue: k_ext_band64 holds 35 KB of LDS, so a CU
 // keeps 4 of them (one a SIMD) and 1024 cover the chip; a wave past the queue's end exits
 // at once (PE 2x250 defers ~15 % of its jobs: 512 waves left half the SIMDs idle)
@@ -469,6 +478,7 @@ struct rsa_pending {
     uint64_t guess = 0, cells = 0, qr_bytes = 0;
     uint64_t certified = 0;            // jobs k_ext_scan_v took on the word score alone
     int rmax = 1;                      // k_ext_scan's rows-per-lane bound for this call's jobs
+    int band16_dircap = 4096;          // k_ext_band16's direction capacity for this call's queries
     ExtStatus* d_status = nullptr;     // in the lane's staged upload
 };
 
@@ -503,6 +513,7 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
     uint64_t cig_off = 0;
     uint64_t cells = 0, qr_bytes = 0;
     int rmax = 1;
+    uint32_t qmax = 0;
     for (uint32_t i = 0; i < n; ++i) {
         const rsa_job& s = jb->jobs[i];
         if (s.ref_id < 0 || s.ref_id >= (int)ctx->contig_off.size() - 1 || s.query_offset + s.query_len > jb->queries_len) {
@@ -528,6 +539,7 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
         if (s.ref_len <= 2000) {
             cells += (uint64_t)s.query_len * s.ref_len;
             rmax = std::max(rmax, (int)((s.query_len + 63) / 64));
+            qmax = std::max(qmax, s.query_len);
         }
     }
     P.cells = cells;
@@ -614,6 +626,7 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
         for (uint32_t i = 0; i < n; ++i) ord[i] = (int)i;
     }
     P.rmax = rmax;
+    P.band16_dircap = band16_dircap(qmax);
     // jobs, scan order and the zeroed status in one copy
     HIPCHK(hipMemcpyAsync(L->d_jobs.p, L->h_jobs.p, stage_bytes(n), hipMemcpyHostToDevice, st));
     L->kt.arm();
@@ -647,7 +660,7 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
     // the compaction below never reads an unwritten result) and clears every job's
     // overflow flag, which k_ext_band64 sets for the bands it cannot hold
     L->kt.begin(st, RSA_K_EXT_BAND);
-    launch_ext_band16(dim3((n + 3) / 4), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(), (int)n, nullptr,
+    launch_ext_band16(P.band16_dircap, dim3((n + 3) / 4), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(), (int)n, nullptr,
                       L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(),
                       L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open, jb->gap_extend, jb->end_bonus,
                       L->d_queue.as<int>(), &dst->qcount, L->d_over.as<int>(), L->d_redo.as<int>(), &dst->rcount);
@@ -738,7 +751,7 @@ static int ext_finish(rsa_pending& P) {
         L->kt.end(st);
         HIPCHK(hipMemsetAsync(&P.d_status->qcount, 0, 2 * sizeof(int), st));    // qcount, ocount
         L->kt.begin(st, RSA_K_EXT_BAND);
-        launch_ext_band16(dim3((redo + 3) / 4), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(), redo, d_redo,
+        launch_ext_band16(P.band16_dircap, dim3((redo + 3) / 4), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(), redo, d_redo,
                           L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(),
                           L->d_alns.as<rsa_aln>(), P.match, P.mismatch, P.gap_open, P.gap_extend, P.end_bonus,
                           L->d_queue.as<int>(), &P.d_status->qcount, L->d_over.as<int>(), nullptr, nullptr);
