@@ -128,6 +128,8 @@ static bool scan_v_env() {
     return !(v && v[0] == '0');
 }
 
+static const int BAND64_GRID_MAX = 1024;
+
 struct rsa_ctx {
     int device = 0;
     bool scan_v = scan_v_env();
@@ -149,6 +151,7 @@ struct rsa_ctx {
     std::mutex lane_m;
     std::condition_variable lane_cv;
     int n_pending = 0;                 // rsa_extend_async calls not yet waited for
+    std::atomic<int> band64_recent{BAND64_GRID_MAX};   // decaying max of recent calls' band16 deferrals
     // stats
     std::mutex stat_m;
     rsa_kernel_stats stats{};
@@ -440,10 +443,14 @@ static int band16_dircap(uint32_t qmax) {
 // waves draining the band16 deferral queue: k_ext_band64 holds 35 KB of LDS, so a CU
 // keeps 4 of them (one a SIMD) and 1024 cover the chip; a wave past the queue's end exits
 // at once (PE 2x250 defers ~15 % of its jobs: 512 waves left half the SIMDs idle)
-static const int BAND64_GRID_DEFAULT = 1024;
-static int band64_grid() {                          // RSA_BAND64_GRID overrides (A/B)
-    static const int g = getenv("RSA_BAND64_GRID") ? std::max(1, atoi(getenv("RSA_BAND64_GRID"))) : BAND64_GRID_DEFAULT;
-    return g;
+// The grid follows the deferrals of the context's recent calls (twice the decaying
+// maximum, 64..1024 waves): with k_ext_band16's 8 KB class almost nothing is deferred,
+// and 1024 idle waves of 35 KB each cost ~0.15 ms a call while they found CUs.  Extra
+// deferrals only lengthen the grid-stride loop.  RSA_BAND64_GRID fixes the grid (A/B).
+static int band64_grid(const rsa_ctx* ctx) {
+    static const int g = getenv("RSA_BAND64_GRID") ? std::max(1, atoi(getenv("RSA_BAND64_GRID"))) : 0;
+    if (g) return g;
+    return std::min(BAND64_GRID_MAX, std::max(64, 2 * ctx->band64_recent.load(std::memory_order_relaxed)));
 }
 static const uint64_t DENSE_GUESS = 24;    // CIGAR ops per job copied before the total is known
 
@@ -667,7 +674,7 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
     HIPCHK(hipGetLastError());
     L->kt.end(st);
     L->kt.begin(st, RSA_K_EXT_BAND_WIDE);
-    launch_ext_band64(dim3(std::min<uint32_t>(n, (uint32_t)band64_grid())), st, L->d_jobs.as<ExtJobDev>(),
+    launch_ext_band64(dim3(std::min<uint32_t>(n, (uint32_t)band64_grid(ctx))), st, L->d_jobs.as<ExtJobDev>(),
                       L->d_scan.as<ScanRes>(), L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(),
                       L->d_raw.as<uint32_t>(), L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open,
                       jb->gap_extend, jb->end_bonus, L->d_queue.as<int>(), &dst->qcount, L->d_over.as<int>(),
@@ -737,6 +744,10 @@ static int ext_finish(rsa_pending& P) {
         if (int rc = ext_panel(P, hs)) return rc;
     const int redo = hs.rcount;
     uint64_t deferred = (uint64_t)hs.qcount, overflowed = (uint64_t)hs.ocount;
+    {   // the next calls' k_ext_band64 grid (band64_grid)
+        const int prev = ctx->band64_recent.load(std::memory_order_relaxed);
+        ctx->band64_recent.store(std::max(hs.qcount, prev - prev / 4), std::memory_order_relaxed);
+    }
     if (redo > 0) {
         // the listed jobs' path had an insertion next to a deletion (or no path): the
         // byte layout may score them differently, so they take the exact two-layout
@@ -758,7 +769,7 @@ static int ext_finish(rsa_pending& P) {
         HIPCHK(hipGetLastError());
         L->kt.end(st);
         L->kt.begin(st, RSA_K_EXT_BAND_WIDE);
-        launch_ext_band64(dim3(std::min(redo, band64_grid())), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(),
+        launch_ext_band64(dim3(std::min(redo, band64_grid(ctx))), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(),
                           L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(),
                           L->d_alns.as<rsa_aln>(), P.match, P.mismatch, P.gap_open, P.gap_extend, P.end_bonus,
                           L->d_queue.as<int>(), &P.d_status->qcount, L->d_over.as<int>(), &P.d_status->ocount,
