@@ -51,7 +51,7 @@ public:
     Engine* inner = nullptr;
     bool replay = false;
     std::mutex m;
-    std::map<const void*, SeedBatchOut> seeds;
+    std::map<uint64_t, SeedBatchOut> seeds;
     std::map<uint64_t, std::vector<AlignmentInfo>> exts;
     double seed_ms = 0, ext_ms = 0;   // replay: emulated device latency per call (the thread sleeps)
     const char* name() const override { return replay ? "replay" : "record"; }
@@ -62,7 +62,10 @@ public:
         if (ms > 0) std::this_thread::sleep_for(std::chrono::microseconds((long)(ms * 1000)));
     }
     void seed(const std::vector<std::string_view>& reads, int rl, unsigned rc, SeedBatchOut& out) override {
-        const void* key = reads.empty() ? nullptr : (const void*)reads[0];
+        // keyed by content: the pipeline recycles its chunk buffers, so addresses repeat
+        uint64_t key = 1469598103934665603ULL ^ reads.size();
+        for (size_t i = 0; i < reads.size(); i += std::max<size_t>(1, reads.size() / 64))
+            for (char ch : reads[i]) key = (key ^ (unsigned char)ch) * 1099511628211ULL;
         if (replay) {
             nap(seed_ms);
             std::lock_guard<std::mutex> g(m);
