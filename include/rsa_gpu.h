@@ -181,7 +181,19 @@ int rsa_seed(rsa_ctx* ctx, const rsa_read_batch* reads, int32_t rescue_level, ui
 /* ---- extension ---------------------------------------------------------- */
 
 /* One Smith-Waterman job: query bytes (caller buffer) vs a window of the
- * device-resident reference (contig ref_id, [ref_start, ref_start+ref_len)). */
+ * device-resident reference (contig ref_id, [ref_start, ref_start+ref_len)).
+ * query_len holds the length in its low 24 bits.  A mate-rescue job may ask for
+ * rescue_mate_part's pre-check as well (has_shared_substring, src/aln.cpp:1000-1013,
+ * called at 1058): RSA_JOB_SHARED_CHECK | RSA_JOB_K(k) in query_len's high bits, for a
+ * query of up to 1024 bp and a window of up to 4096.  The result then carries
+ * RSA_ALN_NO_SHARED in rsa_aln.flags when no (2k/3)-mer of the query taken every k/3
+ * bases occurs in the window: the caller's rescue is unaligned, and the SW result
+ * (still computed) is not used. */
+#define RSA_JOB_LEN_MASK 0x00FFFFFFu
+#define RSA_JOB_SHARED_CHECK 0x80000000u
+#define RSA_JOB_K(k) ((((uint32_t)(k)) & 0x7Fu) << 24)
+#define RSA_SHARED_QMAX 1024
+#define RSA_SHARED_WMAX 4096
 typedef struct rsa_job {
     uint64_t query_offset;
     uint32_t query_len;
@@ -206,8 +218,9 @@ typedef struct rsa_aln {
     uint32_t query_start, query_end;   /* half-open */
     uint64_t cigar_offset;             /* into cigar_pool */
     uint32_t cigar_len;
-    uint32_t pad_;
+    uint32_t flags;                    /* RSA_ALN_NO_SHARED (jobs with RSA_JOB_SHARED_CHECK) */
 } rsa_aln;
+#define RSA_ALN_NO_SHARED 1u
 
 typedef struct rsa_aln_batch {
     rsa_aln* alns;             /* [n_jobs] */

@@ -80,6 +80,7 @@ public:
         for (size_t i = 0; i < jobs.size(); ++i) {
             const auto& j = jobs[i];
             const char* ref = refs_.concat.data() + refs_.offsets[j.ref_id] + j.ref_start;
+            if (rsa::shared_check_fails(j, std::string_view(ref, j.ref_len))) { out[i].no_shared = true; continue; }
             cig.resize(2 * (j.query.size() + j.ref_len) + 16);
             ora_aln_info info;
             ora_aligner_align(j.query.data(), (int)j.query.size(), ref, (int)j.ref_len, p.match, p.mismatch,

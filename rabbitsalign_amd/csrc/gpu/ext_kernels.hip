@@ -616,7 +616,7 @@ __device__ __forceinline__ int gscan_f(int A, int gE) {
 __device__ __forceinline__ void aln_sentinel(rsa_aln* out, int j, const ExtJobDev& jb, int score) {
     rsa_aln a;
     a.sw_score = score; a.edit_distance = 100000; a.ref_start = a.ref_end = a.query_start = a.query_end = 0;
-    a.cigar_offset = jb.cig_off; a.cigar_len = 0; a.pad_ = 0;
+    a.cigar_offset = jb.cig_off; a.cigar_len = 0; a.flags = 0;
     out[j] = a;
 }
 
@@ -751,7 +751,7 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
     // traceback (ssw.c:748-776), leader lane
     rsa_aln a;
     a.sw_score = 0; a.edit_distance = 0; a.ref_start = a.ref_end = a.query_start = a.query_end = 0;
-    a.cigar_offset = jb.cig_off; a.cigar_len = 0; a.pad_ = 0;
+    a.cigar_offset = jb.cig_off; a.cigar_len = 0; a.flags = 0;
     uint32_t* raw = raw_pool + jb.cig_off;
     int i = read_l - 1, jx = ref_l - 1, ecount = 0, l = 0, temp2 = 2;
     int line = width_d * 3 * (read_l - 1);
@@ -862,7 +862,7 @@ k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
         // every job, including one the 64-lane kernel leaves to the one-lane pass
         rsa_aln a;
         a.sw_score = 0; a.edit_distance = 0; a.ref_start = a.ref_end = a.query_start = a.query_end = 0;
-        a.cigar_offset = jb.cig_off; a.cigar_len = 0; a.pad_ = 0;
+        a.cigar_offset = jb.cig_off; a.cigar_len = 0; a.flags = 0;
         out[j] = a;
         queue[atomicAdd(qcount, 1)] = j;
     }
@@ -1040,7 +1040,7 @@ k_ext_band_panel(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__
     // traceback (ssw.c:748-776)
     rsa_aln a;
     a.sw_score = 0; a.edit_distance = 0; a.ref_start = a.ref_end = a.query_start = a.query_end = 0;
-    a.cigar_offset = jb.cig_off; a.cigar_len = 0; a.pad_ = 0;
+    a.cigar_offset = jb.cig_off; a.cigar_len = 0; a.flags = 0;
     int i = read_l - 1, jx = ref_l - 1, ecount = 0, l = 0, temp2 = 2;
     int64_t line = (int64_t)width_d * 3 * (read_l - 1);
     uint32_t op = 0, prev_op = 0;
@@ -1163,6 +1163,79 @@ void launch_cigar_compact(hipStream_t st, const rsa_aln* alns, rsa_aln* alns_out
     hipLaunchKernelGGL(k_cig_bsum, dim3(nb), dim3(CCP_THREADS), 0, st, alns, n_jobs, bsum);
     hipLaunchKernelGGL(k_cig_bscan, dim3(1), dim3(1024), 0, st, bsum, nb, total);
     hipLaunchKernelGGL(k_cig_copy, dim3(nb), dim3(CCP_THREADS), 0, st, alns, alns_out, n_jobs, bsum, slots, dense);
+}
+
+// ---------------------------------------------------------------------------
+// k_shared_check: rescue_mate_part's pre-check has_shared_substring (aln.cpp:1000-1013)
+// for the jobs that ask for it (RSA_JOB_SHARED_CHECK): is any substring of sub = 2k/3
+// query bytes starting at i = 0, step, 2 step, ... (i + sub < qlen, step = k/3) found
+// in the window (std::string::find: exact bytes, whole match inside the window)?  One
+// wave a job, the window staged in LDS; lane x tries window positions x, x + 64, ...
+// for one substring at a time (8-byte words composed from aligned LDS loads, the last
+// one masked), and the wave stops at the first substring found anywhere.
+// list[2f] = job index, list[2f + 1] = k; res[f] = 1 when nothing is shared.
+// ---------------------------------------------------------------------------
+#define SH_WAVES 4
+__device__ __forceinline__ uint64_t sh_word(const uint8_t* w, int p) {   // bytes w[p .. p+8), first lowest
+    const int a = p & ~7, o = (p & 7) * 8;
+    const uint64_t lo = *(const uint64_t*)(w + a), hi = *(const uint64_t*)(w + a + 8);
+    return o ? (lo >> o) | (hi << (64 - o)) : lo;
+}
+__device__ __forceinline__ uint64_t sh_qword(const char* q, int p, int n) {   // n <= 8 bytes of q at p
+    uint64_t x = 0;
+    for (int b = 0; b < n; ++b) x |= (uint64_t)(uint8_t)q[p + b] << (8 * b);
+    return x;
+}
+
+__global__ void __launch_bounds__(64 * SH_WAVES)
+k_shared_check(const ExtJobDev* __restrict__ jobs, const uint32_t* __restrict__ list, int nl,
+               const char* __restrict__ qbuf, const char* __restrict__ ref, uint8_t* __restrict__ res) {
+    __shared__ __attribute__((aligned(8))) uint8_t s_w[SH_WAVES][RSA_SHARED_WMAX + 32];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int f = blockIdx.x * SH_WAVES + w;
+    if (f >= nl) return;                             // the whole wave
+    const ExtJobDev jb = jobs[list[2 * f]];
+    const int k = (int)list[2 * f + 1];
+    const int qlen = (int)jb.qlen, rlen = (int)jb.rlen;
+    const int sub = 2 * k / 3, step = k / 3;
+    uint8_t* win = s_w[w];
+    const char* r = ref + jb.r_off;
+    for (int x = lane; x < rlen + 32; x += 64) win[x] = x < rlen ? (uint8_t)r[x] : 0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const char* q = qbuf + jb.q_off;
+    const int nw = (sub + 7) / 8;                    // words a substring spans (sub <= 2 * 127 / 3)
+    bool found = false;
+    if (sub > 0 && step > 0 && sub <= 24) {
+        for (int i = 0; i + sub < qlen; i += step) {
+            uint64_t qw[3], mk[3];
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                const int n = t < nw ? min(8, sub - 8 * t) : 0;
+                qw[t] = n ? sh_qword(q, i + 8 * t, n) : 0;
+                mk[t] = n == 8 ? ~0ull : ((1ull << (8 * n)) - 1);
+            }
+            bool hit = false;
+            for (int p = lane; p + sub <= rlen; p += 64) {
+                bool eq = true;
+#pragma unroll
+                for (int t = 0; t < 3; ++t)
+                    if (t < nw) eq = eq && ((sh_word(win, p + 8 * t) & mk[t]) == qw[t]);
+                hit = hit || eq;
+            }
+            if (__builtin_amdgcn_ballot_w64(hit)) { found = true; break; }
+        }
+    } else if (sub > 24) {
+        found = true;                                // outside the kernel's shapes: the host never asks
+    }
+    if (lane == 0) res[f] = found ? 0 : 1;
+}
+
+void launch_shared_check(int nl, hipStream_t st, const ExtJobDev* jobs, const uint32_t* list, const char* q,
+                         const char* ref, uint8_t* res) {
+    if (nl <= 0) return;
+    hipLaunchKernelGGL(k_shared_check, dim3((nl + SH_WAVES - 1) / SH_WAVES), dim3(64 * SH_WAVES), 0, st, jobs, list,
+                       nl, q, ref, res);
 }
 
 // host-side launcher: RMAX from the longest query of the batch

@@ -38,6 +38,8 @@ void launch_ext_band16(int dircap, dim3 grid, hipStream_t st, const ExtJobDev* j
                        const char* q, const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match,
                        int mismatch, int gO, int gE, int bonus, int* queue, int* qcount, int* overflow, int* redo,
                        int* redo_count);
+void launch_shared_check(int nl, hipStream_t st, const ExtJobDev* jobs, const uint32_t* list, const char* q,
+                         const char* ref, uint8_t* res);
 void launch_ext_band64(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, const char* q,
                        const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match, int mismatch, int gO,
                        int gE, int bonus, const int* queue, const int* qcount, int* overflow, int* ocount, int* redo,
@@ -113,8 +115,8 @@ struct Lane {
     // d_alns holds results with CIGAR slot offsets, d_alns_out the copy with packed offsets
     // d_redo: jobs whose certified word result the band path could not confirm (k_ext_scan_v)
     DevBuf d_q, d_jobs, d_scan, d_alns, d_alns_out, d_cig, d_dense, d_raw, d_scratch, d_over, d_queue, d_idx, d_bsum,
-        d_redo;
-    HostBuf h_jobs, h_over, h_status;
+        d_redo, d_shl, d_shres;
+    HostBuf h_jobs, h_over, h_status, h_shl, h_shres;   // h_shl / d_shl: (job, k) pairs of RSA_JOB_SHARED_CHECK
     // seeding
     SeedBufs sb;
 };
@@ -160,6 +162,7 @@ struct rsa_ctx {
 // the message of the calling thread's last failed call: concurrent calls on one
 // context (the host pipeline's workers) never see each other's messages
 static thread_local std::string t_err;
+static thread_local std::vector<uint32_t> t_shl;    // a call's (job, k) shared-check pairs while it is staged
 
 static void set_err(rsa_ctx* ctx, const std::string& s) {
     t_err = s;
@@ -422,7 +425,8 @@ uint64_t rsa_resident_bytes(const rsa_ctx* ctx) { return ctx ? ctx->resident : 0
 
 uint64_t rsa_extend_cigar_bound(const rsa_job_batch* jb) {
     uint64_t t = 0;
-    for (uint32_t i = 0; i < jb->n_jobs; ++i) t += (uint64_t)jb->jobs[i].query_len + jb->jobs[i].ref_len + 8;
+    for (uint32_t i = 0; i < jb->n_jobs; ++i)
+        t += (uint64_t)(jb->jobs[i].query_len & RSA_JOB_LEN_MASK) + jb->jobs[i].ref_len + 8;
     return t;
 }
 
@@ -486,6 +490,7 @@ struct rsa_pending {
     uint64_t certified = 0;            // jobs k_ext_scan_v took on the word score alone
     int rmax = 1;                      // k_ext_scan's rows-per-lane bound for this call's jobs
     int band16_dircap = 4096;          // k_ext_band16's direction capacity for this call's queries
+    uint32_t n_shared = 0;             // jobs with RSA_JOB_SHARED_CHECK (k_shared_check's list)
     ExtStatus* d_status = nullptr;     // in the lane's staged upload
 };
 
@@ -521,8 +526,22 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
     uint64_t cells = 0, qr_bytes = 0;
     int rmax = 1;
     uint32_t qmax = 0;
+    std::vector<uint32_t>& shl = t_shl;
+    shl.clear();
     for (uint32_t i = 0; i < n; ++i) {
-        const rsa_job& s = jb->jobs[i];
+        rsa_job s = jb->jobs[i];
+        if (s.query_len & RSA_JOB_SHARED_CHECK) {
+            const uint32_t k = (s.query_len >> 24) & 0x7Fu;
+            s.query_len &= RSA_JOB_LEN_MASK;
+            if (s.query_len > RSA_SHARED_QMAX || s.ref_len > RSA_SHARED_WMAX || k < 3 || 2 * k / 3 > 24) {
+                set_err(ctx, "rsa_extend: job " + std::to_string(i) + " asks for a shared-substring check outside "
+                             "its limits (query <= 1024, window <= 4096, 3 <= k <= 36)");
+                return RSA_ERR_ARG;
+            }
+            shl.push_back(i);
+            shl.push_back(k);
+        }
+        s.query_len &= RSA_JOB_LEN_MASK;
         if (s.ref_id < 0 || s.ref_id >= (int)ctx->contig_off.size() - 1 || s.query_offset + s.query_len > jb->queries_len) {
             set_err(ctx, "rsa_extend: job " + std::to_string(i) + " out of range");
             return RSA_ERR_ARG;
@@ -634,6 +653,7 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
     }
     P.rmax = rmax;
     P.band16_dircap = band16_dircap(qmax);
+    P.n_shared = (uint32_t)(shl.size() / 2);
     // jobs, scan order and the zeroed status in one copy
     HIPCHK(hipMemcpyAsync(L->d_jobs.p, L->h_jobs.p, stage_bytes(n), hipMemcpyHostToDevice, st));
     L->kt.arm();
@@ -681,6 +701,18 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
                       &dst->ocount, L->d_redo.as<int>(), &dst->rcount);
     HIPCHK(hipGetLastError());
     L->kt.end(st);
+    if (P.n_shared) {   // rescue_mate_part's has_shared_substring for the jobs that asked (aln.cpp:1058)
+        HIPCHK(L->h_shl.ensure(sizeof(uint32_t) * shl.size()));
+        memcpy(L->h_shl.p, shl.data(), sizeof(uint32_t) * shl.size());
+        HIPCHK(L->d_shl.ensure(sizeof(uint32_t) * shl.size()));
+        HIPCHK(L->d_shres.ensure(P.n_shared));
+        HIPCHK(L->h_shres.ensure(P.n_shared));
+        HIPCHK(hipMemcpyAsync(L->d_shl.p, L->h_shl.p, sizeof(uint32_t) * shl.size(), hipMemcpyHostToDevice, st));
+        launch_shared_check((int)P.n_shared, st, L->d_jobs.as<ExtJobDev>(), L->d_shl.as<uint32_t>(), L->d_q.as<char>(),
+                            ctx->d_ref, L->d_shres.as<uint8_t>());
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(L->h_shres.p, L->d_shres.p, P.n_shared, hipMemcpyDeviceToHost, st));
+    }
     P.guess = std::min<uint64_t>(bound, DENSE_GUESS * n);
     return ext_compact_copy(P);
 }
@@ -790,6 +822,8 @@ static int ext_finish(rsa_pending& P) {
         HIPCHK(stream_wait(st, L->sb.done));
     }
     out->cigar_used = hs.total;
+    for (uint32_t f = 0; f < P.n_shared; ++f)          // the stream has drained: the flags are here
+        if (L->h_shres.as<uint8_t>()[f]) out->alns[L->h_shl.as<uint32_t>()[2 * f]].flags |= RSA_ALN_NO_SHARED;
     {
         std::lock_guard<std::mutex> g(ctx->stat_m);
         if (L->kt.on) {

@@ -502,7 +502,7 @@ static bool extend_seed_part(AlignTmpRes& res, const AlignmentParameters& ap, co
 }
 
 // has_shared_substring (aln.cpp:1000-1013)
-static bool has_shared_substring(std::string_view read_seq, std::string_view ref_seq, int k) {
+bool has_shared_substring(std::string_view read_seq, std::string_view ref_seq, int k) {
     int sub_size = 2 * k / 3;
     int step_size = k / 3;
     for (size_t i = 0; i + sub_size < read_seq.size(); i += step_size) {
@@ -526,9 +526,22 @@ static void rescue_window(const Nam& nam, size_t read_len, float mu, float sigma
     ref_end = std::min(ref_len_i, std::max(0, b));
 }
 
+// A rescue whose has_shared_substring test went to the engine with its SW job
+// (SwJob::shared_k): the slot's edit distance until the result is stored
+static constexpr int kSharedDeferred = INT_MIN;
+
+// The engine makes the has_shared_substring test (RSA_SHARED_ON_ENGINE=0: the host
+// always does).  Only once the insert-size estimate is frozen: the test's window is
+// this call's (mu, sigma) and the SW job's is the one at job collection (pc.cpp:333-368),
+// which are the same from then on, and within the device kernel's limits.
+static bool shared_on_engine() {
+    static const bool on = !(getenv("RSA_SHARED_ON_ENGINE") && getenv("RSA_SHARED_ON_ENGINE")[0] == '0');
+    return on;
+}
+
 // rescue_mate_part (aln.cpp:1015-1076)
 static bool rescue_mate_part(AlignTmpRes& res, const Nam& nam, const References& refs, const Read& read, float mu,
-                             float sigma, int k) {
+                             float sigma, int k, bool defer) {
     Alignment alignment;
     const size_t read_len = read.size();
     std::string_view r_tmp = nam.is_rc ? std::string_view(read.seq) : std::string_view(read.rc);
@@ -550,6 +563,12 @@ static bool rescue_mate_part(AlignTmpRes& res, const Nam& nam, const References&
         return true;
     };
     if (ref_end < ref_start + k) return unaligned();
+    if (defer && read_len <= 1024 && ref_end - ref_start <= 4096 && k >= 3 && 2 * k / 3 <= 24) {
+        alignment.edit_distance = kSharedDeferred;      // tested by the engine, stored by store_rescue
+        res.done_align.push_back(false);
+        res.align_res.push_back(alignment);
+        return false;
+    }
     std::string_view segm = sub(refs.seq(nam.ref_id), (size_t)ref_start, (size_t)(ref_end - ref_start));
     if (!has_shared_substring(r_tmp, segm, k)) return unaligned();
     res.done_align.push_back(false);
@@ -559,7 +578,7 @@ static bool rescue_mate_part(AlignTmpRes& res, const Nam& nam, const References&
 
 // rescue_read_part (aln.cpp:1135-1176)
 static void rescue_read_part(int flag, AlignTmpRes& res, const Read& read2, const Read& read1, const MapContext& mc,
-                             NamSpan nams1, Details det[2], int k, float mu, float sigma) {
+                             NamSpan nams1, Details det[2], int k, float mu, float sigma, bool defer) {
     res.type = flag;
     const Nam n_max1 = nams1[0];
     int tries = 0;
@@ -573,7 +592,7 @@ static void rescue_read_part(int flag, AlignTmpRes& res, const Read& read2, cons
         det[0].gapped += gapped;
         det[0].tried_alignment++;
         res.is_read1.push_back(flag != 1);
-        (void)rescue_mate_part(res, nam, mc.refs, read2, mu, sigma, k);
+        (void)rescue_mate_part(res, nam, mc.refs, read2, mu, sigma, k, defer);
         tries++;
     }
 }
@@ -584,13 +603,14 @@ static void align_PE_part(AlignTmpRes& res, const MapContext& mc, NamSpan nams1,
     const float mu = isize.mu, sigma = isize.sigma;
     const float dropoff = mc.mparams.dropoff_threshold;
     const unsigned max_tries = (unsigned)mc.mparams.max_tries;
+    const bool defer = shared_on_engine() && isize.frozen();
     if (nams1.empty() && nams2.empty()) { res.type = 0; return; }
     if (!nams1.empty() && nams2.empty()) {
-        rescue_read_part(1, res, read2, read1, mc, nams1, det, k, mu, sigma);
+        rescue_read_part(1, res, read2, read1, mc, nams1, det, k, mu, sigma, defer);
         return;
     }
     if (nams1.empty() && !nams2.empty()) {
-        rescue_read_part(2, res, read1, read2, mc, nams2, det, k, mu, sigma);   // details unswapped (sic)
+        rescue_read_part(2, res, read1, read2, mc, nams2, det, k, mu, sigma, defer);   // details unswapped (sic)
         return;
     }
     if (top_dropoff(nams1) < dropoff && top_dropoff(nams2) < dropoff && is_proper_nam_pair(nams1[0], nams2[0], mu, sigma)) {
@@ -674,7 +694,7 @@ static void align_PE_part(AlignTmpRes& res, const MapContext& mc, NamSpan nams1,
         } else {
             det[1].nam_inconsistent += !reverse_nam_if_needed(n2, read2, mc.refs, k);
             res.is_read1.push_back(true);
-            (void)rescue_mate_part(res, n2, mc.refs, read1, mu, sigma, k);
+            (void)rescue_mate_part(res, n2, mc.refs, read1, mu, sigma, k, defer);
             det[0].tried_alignment++;
         }
         if (n2.ref_start >= 0) {
@@ -690,7 +710,7 @@ static void align_PE_part(AlignTmpRes& res, const MapContext& mc, NamSpan nams1,
         } else {
             det[0].nam_inconsistent += !reverse_nam_if_needed(n1, read1, mc.refs, k);
             res.is_read1.push_back(false);
-            (void)rescue_mate_part(res, n1, mc.refs, read2, mu, sigma, k);
+            (void)rescue_mate_part(res, n1, mc.refs, read2, mu, sigma, k, defer);
             det[1].tried_alignment++;
         }
         n_high++;
@@ -774,11 +794,15 @@ void rescue_mate_window(const Nam& nam, size_t read_len, float mu, float sigma, 
 }
 
 static void rescue_job(const Nam& nam, const Read& read, const References& refs, float mu, float sigma,
-                       std::vector<SwJob>& jobs) {
+                       std::vector<SwJob>& jobs, int shared_k) {
     std::string_view r_tmp = nam.is_rc ? std::string_view(read.seq) : std::string_view(read.rc);
     uint32_t start, len;
     rescue_mate_window(nam, read.size(), mu, sigma, refs.seq(nam.ref_id).size(), start, len);
-    jobs.push_back(SwJob{r_tmp, nam.ref_id, start, len});
+    jobs.push_back(SwJob{r_tmp, nam.ref_id, start, len, shared_k});
+}
+// the k of a rescue slot whose has_shared_substring test the engine makes, else 0
+static inline int shared_k_of(const AlignTmpRes& res, size_t j, const MapContext& mc) {
+    return res.align_res[j].edit_distance == kSharedDeferred ? mc.iparams.k : 0;
 }
 
 void collect_jobs_pe(AlignTmpRes& res, const RecView&, const RecView&, const Read& read1, const Read& read2,
@@ -788,7 +812,8 @@ void collect_jobs_pe(AlignTmpRes& res, const RecView&, const RecView&, const Rea
     if (res.type == 1 || res.type == 2) {
         for (size_t j = 0; j < n; j += 2) {
             if (!res.done_align[j]) extend_job(res.todo_nams[j], rd(j), mc.refs, jobs);
-            if (!res.done_align[j + 1]) rescue_job(res.todo_nams[j + 1], rd(j + 1), mc.refs, mu, sigma, jobs);
+            if (!res.done_align[j + 1])
+                rescue_job(res.todo_nams[j + 1], rd(j + 1), mc.refs, mu, sigma, jobs, shared_k_of(res, j + 1, mc));
         }
     } else if (res.type == 3) {
         if (!res.done_align[0]) extend_job(res.todo_nams[0], rd(0), mc.refs, jobs);
@@ -797,7 +822,7 @@ void collect_jobs_pe(AlignTmpRes& res, const RecView&, const RecView&, const Rea
         for (size_t j = 0; j < n; ++j) {
             if (res.done_align[j]) continue;
             if (res.is_extend_seed[j]) extend_job(res.todo_nams[j], rd(j), mc.refs, jobs);
-            else rescue_job(res.todo_nams[j], rd(j), mc.refs, mu, sigma, jobs);
+            else rescue_job(res.todo_nams[j], rd(j), mc.refs, mu, sigma, jobs, shared_k_of(res, j, mc));
         }
     }
 }
@@ -846,6 +871,17 @@ void rescue_alignment(const Nam& nam, size_t read_len, float mu, float sigma, si
 static void store_rescue(AlignTmpRes& res, size_t j, const Read& read, const References& refs, float mu, float sigma,
                          AlignmentInfo& info) {
     const Nam& nam = res.todo_nams[j];
+    if (info.no_shared) {                          // rescue_mate_part's unaligned result (aln.cpp:1060-1069)
+        Alignment& a = res.align_res[j];
+        a.cigar = Cigar();
+        a.edit_distance = (int)read.size();
+        a.score = 0;
+        a.ref_start = 0;
+        a.is_rc = nam.is_rc;
+        a.ref_id = nam.ref_id;
+        a.is_unaligned = true;
+        return;
+    }
     rescue_alignment(nam, read.size(), mu, sigma, refs.seq(nam.ref_id).size(), info, res.align_res[j]);
 }
 

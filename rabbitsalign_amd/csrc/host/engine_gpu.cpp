@@ -269,6 +269,8 @@ private:
                     }
                     js[i].query_offset = pos;
                     js[i].query_len = (uint32_t)jobs[t].query.size();
+                    if (jobs[t].shared_k > 0)    // rescue_mate_part's pre-check on the device
+                        js[i].query_len |= RSA_JOB_SHARED_CHECK | RSA_JOB_K(jobs[t].shared_k);
                     js[i].ref_id = jobs[t].ref_id;
                     js[i].ref_start = jobs[t].ref_start;
                     js[i].ref_len = jobs[t].ref_len;
@@ -293,6 +295,7 @@ private:
                     o.edit_distance = a.edit_distance;
                     o.ref_start = a.ref_start; o.ref_end = a.ref_end;
                     o.query_start = a.query_start; o.query_end = a.query_end;
+                    o.no_shared = (a.flags & RSA_ALN_NO_SHARED) != 0;
                     o.cigar.ops.assign(pool + a.cigar_offset, pool + a.cigar_offset + a.cigar_len);
                 }
             }

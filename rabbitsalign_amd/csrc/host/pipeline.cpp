@@ -448,6 +448,14 @@ static inline void prefetch_res(const AlignTmpRes& r) {
 }
 
 // to_uppercase (refs.cpp:10-16, c & ~32) of n bytes into dst
+// rescue jobs whose has_shared_substring test failed in the engine: no aligner call
+// in the reference (rescue_mate_part returns before it)
+static inline uint64_t no_shared_count(const std::vector<AlignmentInfo>& infos) {
+    uint64_t n = 0;
+    for (const AlignmentInfo& i : infos) n += i.no_shared ? 1 : 0;
+    return n;
+}
+
 static inline void upper_into(const char* src, size_t n, char* dst) {
     size_t i = 0;
     for (; i + 8 <= n; i += 8) {
@@ -800,6 +808,7 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
             Unslot u(slots, offl, c.in.index);
             eng.extend(jobs, mc.aparams, infos);
         }
+        c.stats.tot_aligner_calls -= no_shared_count(infos);   // the reference aligns none of those
         c.times.extend += since(te);
         SamText out = os.take();
         SamDigest dg;
@@ -859,7 +868,7 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
                         eng.extend(jobs, mc.aparams, infos);
                     }
                     pre->times.extend += since(te);
-                    pre->stats.tot_aligner_calls += jobs.size();
+                    pre->stats.tot_aligner_calls += jobs.size() - no_shared_count(infos);
                     SamText out = os.take();
                     SamDigest dg;
                     pe_store_last(*pre, mc, isize, infos, 0, opt.rg_id, out, os.digest ? &dg : nullptr);

@@ -121,6 +121,7 @@ struct AlignmentInfo {                          // src/aligner.hpp:20-30
     Cigar cigar;
     unsigned edit_distance = 0, ref_start = 0, ref_end = 0, query_start = 0, query_end = 0;
     int sw_score = 0;
+    bool no_shared = false;                     // a job with SwJob::shared_k: has_shared_substring was false
     int ref_span() const { return (int)(ref_end - ref_start); }
 };
 
@@ -398,7 +399,17 @@ struct SwJob {                                  // query host bytes vs reference
     std::string_view query;                     // into the chunk's read / reverse complement, valid until store
     int ref_id;
     uint32_t ref_start, ref_len;
+    // > 0: a mate rescue whose has_shared_substring(query, window, shared_k) test
+    // (aln.cpp:1058) the engine makes (AlignmentInfo::no_shared); 0: none
+    int shared_k = 0;
 };
+// has_shared_substring (aln.cpp:1000-1013)
+bool has_shared_substring(std::string_view read_seq, std::string_view ref_seq, int k);
+// the engine side of SwJob::shared_k for engines that align on the host: the test, and
+// the SW skipped when it fails
+inline bool shared_check_fails(const SwJob& j, std::string_view window) {
+    return j.shared_k > 0 && !has_shared_substring(j.query, window, j.shared_k);
+}
 
 class Engine {
 public:

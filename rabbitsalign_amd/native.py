@@ -57,7 +57,7 @@ JOB_DTYPE = np.dtype([("query_offset", "<u8"), ("query_len", "<u4"), ("ref_id", 
 
 ALN_DTYPE = np.dtype([("sw_score", "<i4"), ("edit_distance", "<u4"), ("ref_start", "<u4"), ("ref_end", "<u4"),
                       ("query_start", "<u4"), ("query_end", "<u4"), ("cigar_offset", "<u8"),
-                      ("cigar_len", "<u4"), ("pad_", "<u4")])
+                      ("cigar_len", "<u4"), ("flags", "<u4")])
 
 
 class NamBatch(C.Structure):

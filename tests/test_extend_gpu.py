@@ -98,6 +98,63 @@ def test_extend_band16_capacity_classes(ctx, monkeypatch):
     assert deferred["4096"] > deferred["8192"] >= deferred["12288"], deferred
 
 
+def _has_shared_substring(q: bytes, w: bytes, k: int) -> bool:
+    """has_shared_substring (src/aln.cpp:1000-1013) restated: some (2k/3)-mer of the query
+    starting at a multiple of k/3, with i + sub < len(query), occurs in the window."""
+    sub, step = 2 * k // 3, k // 3
+    i = 0
+    while i + sub < len(q):
+        if w.find(q[i:i + sub]) >= 0:
+            return True
+        i += step
+    return False
+
+
+@pytest.mark.gpu
+def test_extend_shared_check(ctx):
+    """RSA_JOB_SHARED_CHECK jobs: k_shared_check's RSA_ALN_NO_SHARED equals the host
+    function on every job (related and unrelated query/window pairs, N bytes, k 3-36,
+    queries up to 1024 bp, windows up to 4096), and unflagged jobs never carry it."""
+    from jobgen import JOB_DTYPE, ACGT, mutate
+    c, ref, offs = ctx
+    rng = np.random.default_rng(21)
+    queries = bytearray()
+    jobs = np.zeros(1500, dtype=JOB_DTYPE)
+    want = []
+    for i in range(len(jobs)):
+        ci = int(rng.integers(0, len(offs) - 1))
+        clen = int(offs[ci + 1] - offs[ci])
+        L = int(rng.choice([20, 100, 150, 250, 1024]))
+        W = int(rng.choice([30, 300, 525, 2000, 2500, 4096]))
+        rs = int(rng.integers(0, clen - W - 1))
+        win = ref[int(offs[ci]) + rs:int(offs[ci]) + rs + W]
+        kind = int(rng.integers(0, 4))
+        if kind == 0 and W > L:                      # the mate inside the window, with errors
+            a = int(rng.integers(0, W - L))
+            q = mutate(rng, win[a:a + L], sub=float(rng.choice([0.01, 0.1, 0.3])), ind=0.01)[:L]
+        elif kind == 1:                              # unrelated
+            q = ACGT[rng.integers(0, 4, L)]
+        else:                                        # unrelated with one planted piece of the window
+            q = ACGT[rng.integers(0, 4, L)].copy()
+            n = int(rng.integers(5, 25))
+            a, b = int(rng.integers(0, max(1, W - n))), int(rng.integers(0, max(1, L - n)))
+            q[b:b + n] = win[a:a + n][:len(q[b:b + n])]
+        if rng.random() < 0.1:
+            q = q.copy(); q[rng.integers(0, len(q), 3)] = ord("N")
+        k = int(rng.choice([3, 10, 15, 20, 24, 32, 36]))
+        flag = i % 5 != 0
+        qb = bytes(q)
+        qlen = len(qb) | ((0x80000000 | (k << 24)) if flag else 0)
+        jobs[i] = (len(queries), qlen, ci, rs, W)
+        queries += qb
+        want.append(flag and not _has_shared_substring(qb, bytes(win), k))
+    alns, _ = c.extend(bytes(queries), jobs)
+    got = [(int(a["flags"]) & 1) == 1 for a in alns]
+    bad = [i for i in range(len(jobs)) if got[i] != want[i]]
+    assert not bad, f"{len(bad)} jobs differ, first {bad[:5]}"
+    assert 50 < sum(want) < len(jobs) - 300, sum(want)
+
+
 def _wide_band_jobs(rng, ref, offs, n):
     """Queries that bridge a long deletion (or carry a long insertion) of the
     window: |ref span - query span| of 65-1200 bp, so banded_sw needs bands far
