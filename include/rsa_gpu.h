@@ -349,6 +349,8 @@ typedef struct rsa_kernel_stats {
     /* query randstrobes the seeding call wrote out (the reads k_seed_query predicted the
      * global-map / rescue passes need), and reads whose randstrobes those passes had to make */
     uint64_t query_written, query_fixed_reads;
+    /* extension jobs that carried RSA_JOB_SHARED_CHECK, and those that came back RSA_ALN_NO_SHARED */
+    uint64_t shared_checks, no_shared;
 } rsa_kernel_stats;
 
 int rsa_get_stats(rsa_ctx* ctx, rsa_kernel_stats* out);

@@ -822,8 +822,12 @@ static int ext_finish(rsa_pending& P) {
         HIPCHK(stream_wait(st, L->sb.done));
     }
     out->cigar_used = hs.total;
+    uint64_t no_shared = 0;
     for (uint32_t f = 0; f < P.n_shared; ++f)          // the stream has drained: the flags are here
-        if (L->h_shres.as<uint8_t>()[f]) out->alns[L->h_shl.as<uint32_t>()[2 * f]].flags |= RSA_ALN_NO_SHARED;
+        if (L->h_shres.as<uint8_t>()[f]) {
+            out->alns[L->h_shl.as<uint32_t>()[2 * f]].flags |= RSA_ALN_NO_SHARED;
+            no_shared++;
+        }
     {
         std::lock_guard<std::mutex> g(ctx->stat_m);
         if (L->kt.on) {
@@ -842,6 +846,8 @@ static int ext_finish(rsa_pending& P) {
         ctx->stats.band_overflow += overflowed;
         ctx->stats.scan_certified += P.certified - (uint64_t)redo;
         ctx->stats.scan_redo += (uint64_t)redo;
+        ctx->stats.shared_checks += P.n_shared;
+        ctx->stats.no_shared += no_shared;
     }
     return RSA_OK;
 }

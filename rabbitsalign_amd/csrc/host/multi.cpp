@@ -36,6 +36,8 @@ void add_stats(rsa_kernel_stats& a, const rsa_kernel_stats& b) {
     }
     a.query_written += b.query_written;
     a.query_fixed_reads += b.query_fixed_reads;
+    a.shared_checks += b.shared_checks;
+    a.no_shared += b.no_shared;
 }
 
 class MultiEngine final : public Engine {

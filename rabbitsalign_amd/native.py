@@ -107,7 +107,8 @@ class KernelStats(C.Structure):
                 ("band_deferred", C.c_uint64), ("band_overflow", C.c_uint64),
                 ("scan_certified", C.c_uint64), ("scan_redo", C.c_uint64),
                 ("call_ms", C.c_double * 2), ("lane_wait_ms", C.c_double * 2), ("device_wait_ms", C.c_double * 2),
-                ("query_written", C.c_uint64), ("query_fixed_reads", C.c_uint64)]
+                ("query_written", C.c_uint64), ("query_fixed_reads", C.c_uint64),
+                ("shared_checks", C.c_uint64), ("no_shared", C.c_uint64)]
 
 
 def stats_dict(ks: "KernelStats") -> dict:
