@@ -56,3 +56,40 @@ def test_thread_count_invariance(data, threads):
     out = str(d / f"t{threads}.sam")
     map_reads(CPU_PORT, fa, reads, out, "-t", threads, "--chunk-size", "200")
     assert sam_body(base) == sam_body(out)
+
+
+def test_shared_substring_on_engine_equals_host(tmp_path):
+    """rescue_mate_part's has_shared_substring: once the insert-size estimate is frozen
+    the engine makes the test with the rescue SW job (SwJob::shared_k; the device kernel in
+    the GPU engine, the host function in these CPU engines) and store_rescue writes the
+    unaligned result.  A third of the second mates are replaced by random sequence, so
+    their rescues find no shared substring; the SAM must equal the all-host test's
+    (RSA_SHARED_ON_ENGINE=0), for both CPU engines."""
+    import random
+    fa, reads = make_dataset(str(tmp_path), pairs=3000, ref_len=200_000, cpu_index=True)
+    rnd = random.Random(5)
+    with open(reads[1]) as f:
+        lines = f.read().split("\n")
+    for r in range(0, len(lines) - 3, 4):
+        if (r // 4) % 3 == 1:
+            lines[r + 1] = "".join(rnd.choice("ACGT") for _ in lines[r + 1])
+    with open(reads[1], "w") as f:
+        f.write("\n".join(lines))
+    outs = {}
+    for binary in (CPU_PORT, CPU_REF):
+        if not os.path.exists(binary):
+            continue
+        for on in ("1", "0"):
+            out = str(tmp_path / f"{os.path.basename(binary)}_{on}.sam")
+            old = os.environ.get("RSA_SHARED_ON_ENGINE")
+            os.environ["RSA_SHARED_ON_ENGINE"] = on
+            try:
+                map_reads(binary, fa, reads, out, "-t", "4", "--chunk-size", "300")
+            finally:
+                if old is None:
+                    del os.environ["RSA_SHARED_ON_ENGINE"]
+                else:
+                    os.environ["RSA_SHARED_ON_ENGINE"] = old
+            outs[(binary, on)] = sam_body(out)
+        assert outs[(binary, "1")] == outs[(binary, "0")], binary
+    assert len(outs) >= 2
