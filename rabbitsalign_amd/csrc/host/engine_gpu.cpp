@@ -191,7 +191,12 @@ public:
         std::unique_lock<std::mutex> l(ext_m_);
         ext_pending_.push_back(&me);
         while (!me.done) {
-            if (ext_active_ < ext_leaders() && !ext_pending_.empty()) {
+            // one more call than ext_leaders() while the queued jobs fill a whole batch: the
+            // calls in flight cannot take the load (PE 2x250 calls run at the batch cap)
+            size_t queued = 0;
+            if (ext_active_ >= ext_leaders() && ext_active_ < ext_leaders() + ext_extra_leaders())
+                for (const ExtReq* r : ext_pending_) queued += r->jobs->size();
+            if ((ext_active_ < ext_leaders() || queued >= ext_batch_jobs()) && !ext_pending_.empty()) {
                 ++ext_active_;
                 std::vector<ExtReq*> batch;
                 size_t n_jobs = 0;
@@ -238,6 +243,11 @@ private:
     // calls rsa_extend for its own chunk); RSA_EXT_BATCH_JOBS: jobs a combined call takes
     static int ext_leaders() {
         static const int n = getenv("RSA_EXT_LEADERS") ? atoi(getenv("RSA_EXT_LEADERS")) : 2;
+        return n;
+    }
+    // RSA_EXT_EXTRA_LEADERS: calls beyond ext_leaders() allowed while a full batch is queued
+    static int ext_extra_leaders() {
+        static const int n = getenv("RSA_EXT_EXTRA_LEADERS") ? std::max(0, atoi(getenv("RSA_EXT_EXTRA_LEADERS"))) : 1;
         return n;
     }
     static size_t ext_batch_jobs() {
