@@ -267,9 +267,12 @@ void rsa_host_free(void* p);
  * index.cpp:28-69, 244-309), the sort by (hash, position) (index.cpp:168),
  * the bucket table with the reference's exact fill rule (index.cpp:174-212)
  * and the filter cutoff (index.cpp:214-238).  The result is byte-identical to
- * the host build (and so to the .sti the reference writes; equal (hash,
- * position) keys in two contigs keep contig order, which pdqsort leaves
- * unspecified). */
+ * the host build and to the .sti the reference writes: entries equal in (hash,
+ * position) (duplicated sequence in two contigs) compare equal under
+ * RefRandstrobe::operator< (randstrobes.hpp:32-35), and their order is the one
+ * pdqsort_branchless's element moves produce; when the device sort finds any
+ * (info.position_ties), the entries in generation order go to the host, where
+ * that sort is replayed (sti_order.hpp), and come back. */
 typedef struct rsa_index_build_params {
     int32_t k, s, t_syncmer;           /* SyncmerParameters */
     int32_t w_min, w_max, max_dist;    /* RandstrobeParameters */
@@ -286,6 +289,8 @@ typedef struct rsa_index_build_info {
     /* HIP-event times (ms): reference upload, syncmers (all passes), randstrobes,
      * sort (both radix passes + gathers), bucket table + counts; wall of the call */
     double ms_upload, ms_syncmers, ms_randstrobes, ms_sort, ms_buckets, ms_total;
+    uint64_t position_ties;            /* entries equal in (hash, position) to their predecessor */
+    double ms_tie_replay;              /* host replay of pdqsort's order (0 without ties), incl. transfers */
 } rsa_index_build_info;
 
 typedef struct rsa_index_build rsa_index_build;

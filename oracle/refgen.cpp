@@ -7,6 +7,8 @@
 //             (src/randstrobes.cpp:207-253, src/nam.cpp:771-1012)
 //   ssw     : ssw_init + ssw_align                  (ext/ssw/ssw.c:789-922)
 //   sam     : Sam::add / add_pair / add_unmapped*   (src/sam.cpp), reverse_complement (revcomp.hpp)
+//   pdqsort : pdqsort_branchless over RefRandstrobe  (src/index.cpp:168, ext/pdqsort/pdqsort.h,
+//             operator< of src/randstrobes.hpp:32-35) on a raw 16-byte entry file
 // Only FASTA parsing (refs.cpp needs the un-vendored zstr) and the SSW base
 // translation table (ssw_cpp.cpp includes a CUDA header) are restated here.
 #include <cinttypes>
@@ -30,6 +32,7 @@
 #include <memory>
 #include <array>
 #include "ssw/ssw.h"
+#include "pdqsort/pdqsort.h"
 
 // refs.cpp:8-58 semantics: name cut at the first ' ', sequence uppercased with c & ~32
 static References read_fasta(const std::string& fn) {
@@ -288,8 +291,26 @@ static int cmd_sam(int argc, char** argv) {
     return 0;
 }
 
+// pdqsort IN OUT: IN holds RefRandstrobe entries (u64 hash, u32 position, u32 packed)
+// back to back; OUT gets them in the order populate()'s sort leaves them
+static int cmd_pdqsort(int argc, char** argv) {
+    if (argc < 4) { fprintf(stderr, "usage: refgen pdqsort IN OUT\n"); return 2; }
+    std::ifstream in(argv[2], std::ios::binary);
+    std::vector<char> raw((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+    static_assert(sizeof(RefRandstrobe) == 16, "the .sti entry layout");
+    std::vector<RefRandstrobe> v(raw.size() / 16);
+    if (!v.empty()) memcpy((void*)v.data(), raw.data(), 16 * v.size());   // the .sti payload layout (index.cpp:91-132)
+    pdqsort_branchless(v.begin(), v.end());
+    FILE* o = fopen(argv[3], "wb");
+    if (!o) return 1;
+    if (!v.empty()) fwrite((const void*)v.data(), 16, v.size(), o);
+    fclose(o);
+    return 0;
+}
+
 int main(int argc, char** argv) {
-    if (argc < 2) { fprintf(stderr, "usage: refgen index|seeds|ssw|sswrand|sam ...\n"); return 2; }
+    if (argc < 2) { fprintf(stderr, "usage: refgen index|seeds|ssw|sswrand|sam|pdqsort ...\n"); return 2; }
+    if (std::string(argv[1]) == "pdqsort") return cmd_pdqsort(argc, argv);
     std::string c = argv[1];
     if (c == "index") return cmd_index(argc, argv);
     if (c == "seeds") return cmd_seeds(argc, argv);

@@ -47,11 +47,13 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "rsa_dev.h"
 #include "../../../include/rsa_gpu.h"
 #include "rsa_seed.h"
+#include "../host/sti_order.hpp"
 
 namespace {
 
@@ -361,16 +363,19 @@ k_fill_u64(uint64_t* __restrict__ p, uint64_t n, uint64_t v) {
 
 // grid-stride over the entries; run starts count the unique hashes and
 // histogram the run length (clamped to 101) of runs longer than one
-// (index.cpp:186-224).  One global atomic per block and bin.
+// (index.cpp:186-224); bin 103 counts entries equal in (hash, position) to their
+// predecessor (the ties whose order is pdqsort's).  One global atomic per block and bin.
 constexpr int RC_BLOCKS = 2048;
+constexpr int RC_BINS = 104;
 __global__ void __launch_bounds__(TPB)
 k_run_counts(const rsa_ref_randstrobe* __restrict__ rs, uint64_t n, unsigned long long* __restrict__ hist) {
-    __shared__ unsigned long long lh[103];
-    for (int j = threadIdx.x; j < 103; j += TPB) lh[j] = 0;
+    __shared__ unsigned long long lh[RC_BINS];
+    for (int j = threadIdx.x; j < RC_BINS; j += TPB) lh[j] = 0;
     __syncthreads();
-    unsigned long long starts = 0;
+    unsigned long long starts = 0, ties = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * TPB) {
         const uint64_t h = rs[i].hash;
+        if (i > 0 && rs[i - 1].hash == h && rs[i - 1].position == rs[i].position) ties++;
         if (i == 0 || rs[i - 1].hash != h) {
             starts++;
             if (i + 1 < n && rs[i + 1].hash == h) {          // a run longer than one
@@ -382,8 +387,9 @@ k_run_counts(const rsa_ref_randstrobe* __restrict__ rs, uint64_t n, unsigned lon
         }
     }
     atomicAdd(&lh[102], starts);
+    if (ties) atomicAdd(&lh[103], ties);
     __syncthreads();
-    for (int j = threadIdx.x; j < 103; j += TPB)
+    for (int j = threadIdx.x; j < RC_BINS; j += TPB)
         if (lh[j]) atomicAdd(&hist[j], lh[j]);
 }
 
@@ -662,14 +668,14 @@ rsa_index_build* rsa_index_build_run(int device, const char* ref_seq, const uint
         BCHK(hipGetLastError());
     }
     BCHK(hipEventRecord(ev[5], st));
-    dfree(d_raw);
+    // d_raw (generation order) stays until the tie count is known: the replay starts from it
 
     // bucket table + run-length histogram
     const uint64_t nb = 1ull << bits;
     BCHK(hipMalloc(&B->d_starts, 8 * (nb + 1)));
     unsigned long long* d_hist = nullptr;
-    BCHK(dalloc((void**)&d_hist, 8 * 103));
-    BCHK(hipMemsetAsync(d_hist, 0, 8 * 103, st));
+    BCHK(dalloc((void**)&d_hist, 8 * RC_BINS));
+    BCHK(hipMemsetAsync(d_hist, 0, 8 * RC_BINS, st));
     BCHK(hipEventRecord(ev[6], st));
     // no hash change at all (n <= 1 or a single run): every bucket gets n (index.cpp:206-208)
     k_fill_u64<<<grid_of(nb + 1), TPB, 0, st>>>(B->d_starts, nb + 1, n);
@@ -683,9 +689,26 @@ rsa_index_build* rsa_index_build_run(int device, const char* ref_seq, const uint
         BCHK(hipGetLastError());
     }
     BCHK(hipEventRecord(ev[7], st));
-    unsigned long long hist[103];
+    unsigned long long hist[RC_BINS];
     BCHK(hipMemcpyAsync(hist, d_hist, sizeof hist, hipMemcpyDeviceToHost, st));
     BCHK(hipStreamSynchronize(st));
+
+    // equal (hash, position) in two contigs: the reference's order of those entries is
+    // what pdqsort_branchless's moves leave (index.cpp:168).  Replay that sort on the
+    // host from generation order and put its result in place of the device sort's; keys
+    // (and so the bucket table and the counts) are the same either way.
+    const uint64_t ties = hist[103];
+    double ms_ties = 0;
+    if (ties) {
+        const auto tr = std::chrono::steady_clock::now();
+        std::vector<rsa_ref_randstrobe> h(n);
+        BCHK(hipMemcpy(h.data(), d_raw, sizeof(rsa_ref_randstrobe) * n, hipMemcpyDeviceToHost));
+        const int threads = (int)std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
+        rsa::sti_order::pdqsort_replay(h.data(), n, threads);
+        BCHK(hipMemcpy(B->d_rs, h.data(), sizeof(rsa_ref_randstrobe) * n, hipMemcpyHostToDevice));
+        ms_ties = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr).count();
+    }
+    dfree(d_raw);
 
     // filter cutoff (index.cpp:214-238) from the clamped histogram: counts sorted
     // descending, the value at rank index_cutoff (or the smallest), clamped to [30, 100]
@@ -718,6 +741,8 @@ rsa_index_build* rsa_index_build_run(int device, const char* ref_seq, const uint
         info->filter_cutoff = filter_cutoff;
         info->n_segments = n_seg;
         info->replayed_segments = n_replayed;
+        info->position_ties = ties;
+        info->ms_tie_replay = ms_ties;
         float t = 0;
         (void)hipEventElapsedTime(&t, ev[0], ev[1]); info->ms_upload = t;
         (void)hipEventElapsedTime(&t, ev[1], ev[2]); info->ms_syncmers = t;

@@ -391,6 +391,7 @@ void build_default_index(StiIndex& idx, const References& refs, const IndexParam
                           info.ms_total};
     std::copy(ms, ms + 6, idx.device_build_ms);
     idx.replayed_segments = info.replayed_segments;
+    idx.position_ties = info.position_ties;
 }
 
 // engine of librsalign.so (capi.cpp)

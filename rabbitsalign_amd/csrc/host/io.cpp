@@ -20,6 +20,7 @@
 #include <thread>
 
 #include "rsa_host.hpp"
+#include "sti_order.hpp"
 
 namespace rsa {
 
@@ -601,9 +602,11 @@ void StiIndex::build(const References& refs, const IndexParameters& p, int bits_
     randstrobes.clear();
     randstrobes.reserve(n);
     for (auto& v : per) { randstrobes.insert(randstrobes.end(), v.begin(), v.end()); std::vector<rsa_ref_randstrobe>().swap(v); }
-    // RefRandstrobe::operator< orders by (hash, position); ties (equal hash and
-    // position in two contigs) are left in contig order here while the
-    // reference's pdqsort_branchless leaves them in an unspecified order.
+    // RefRandstrobe::operator< orders by (hash, position) (randstrobes.hpp:32-35).
+    // A fast parallel sort first; when two contigs hold an entry with equal hash
+    // and position, their order is the one pdqsort_branchless's moves leave
+    // (index.cpp:168), so the array goes back to generation order and the sort is
+    // replayed (sti_order.hpp).
     auto lt = [](const rsa_ref_randstrobe& a, const rsa_ref_randstrobe& b) {
         if (a.hash != b.hash) return a.hash < b.hash;
         return a.position < b.position;
@@ -626,6 +629,11 @@ void StiIndex::build(const References& refs, const IndexParameters& p, int bits_
             }
             for (auto& x : mt) x.join();
         }
+    }
+    position_ties = sti_order::count_ties(randstrobes.data(), n, threads);
+    if (position_ties) {
+        sti_order::to_generation_order(randstrobes.data(), n, threads);
+        sti_order::pdqsort_replay(randstrobes.data(), n, threads);
     }
     // bucket table + filter cutoff (index.cpp:174-238)
     bucket_starts.clear();

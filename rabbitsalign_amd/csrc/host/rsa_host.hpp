@@ -318,6 +318,9 @@ struct StiIndex {                               // .sti contents (src/index.cpp:
     bool built_on_device = false;
     double device_build_ms[6] = {0, 0, 0, 0, 0, 0};
     uint64_t replayed_segments = 0;
+    // entries equal in (hash, position) to their predecessor: their order is pdqsort's
+    // (sti_order.hpp), replayed by both builds when this is not 0
+    uint64_t position_ties = 0;
     // a GPU build kept in HBM (no host copy): the GPU engine adopts it; a host
     // copy is downloaded only when something needs one (.sti write, a CPU engine)
     struct DeviceBuild {

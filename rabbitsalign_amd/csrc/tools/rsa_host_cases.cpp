@@ -9,6 +9,10 @@
 // stores "aln ref_start length edit_distance global_ed score is_rc is_unaligned
 // gapped n_ops op...".  mu / sigma are read as floats (strtof), as the pipeline
 // holds them.  The functions are the product's own (rsa_host.hpp).
+//
+// `rsa_host_cases pdqsort IN OUT THREADS` instead sorts a raw 16-byte entry file
+// (the .sti payload) with the product's replay of pdqsort_branchless
+// (sti_order.hpp), for the comparison with the reference's own sort.
 #include <cstdio>
 #include <cstdlib>
 #include <iostream>
@@ -16,6 +20,7 @@
 #include <string>
 
 #include "../host/rsa_host.hpp"
+#include "../host/sti_order.hpp"
 
 using namespace rsa;
 
@@ -50,7 +55,22 @@ static void print_aln(const Alignment& a) {
     printf("\n");
 }
 
-int main() {
+static int pdqsort_file(const char* in_path, const char* out_path, int threads) {
+    FILE* f = fopen(in_path, "rb");
+    if (!f) return 1;
+    std::vector<rsa_ref_randstrobe> v;
+    rsa_ref_randstrobe e;
+    while (fread(&e, sizeof e, 1, f) == 1) v.push_back(e);
+    fclose(f);
+    sti_order::pdqsort_replay(v.data(), v.size(), threads);
+    FILE* o = fopen(out_path, "wb");
+    if (!o) return 1;
+    if (!v.empty()) fwrite(v.data(), sizeof e, v.size(), o);
+    return fclose(o) == 0 ? 0 : 1;
+}
+
+int main(int argc, char** argv) {
+    if (argc >= 4 && std::string(argv[1]) == "pdqsort") return pdqsort_file(argv[2], argv[3], argc > 4 ? atoi(argv[4]) : 1);
     std::string line;
     while (std::getline(std::cin, line)) {
         std::istringstream in(line);

@@ -277,7 +277,7 @@ class IndexBuildInfo(C.Structure):
                 ("bits", C.c_int32), ("filter_cutoff", C.c_int32), ("n_segments", C.c_uint64),
                 ("replayed_segments", C.c_uint64), ("ms_upload", C.c_double), ("ms_syncmers", C.c_double),
                 ("ms_randstrobes", C.c_double), ("ms_sort", C.c_double), ("ms_buckets", C.c_double),
-                ("ms_total", C.c_double)]
+                ("ms_total", C.c_double), ("position_ties", C.c_uint64), ("ms_tie_replay", C.c_double)]
 
 
 def build_index(ref: np.ndarray, contig_offsets: np.ndarray, k=20, s=16, w_min=2, w_max=12, max_dist=80, q=255,

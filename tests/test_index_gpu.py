@@ -71,36 +71,19 @@ def test_gpu_index_matches_reference_sti(tmp_path):
 @pytest.mark.gpu
 def test_gpu_index_repetitive_reference(tmp_path):
     """rep.fa (140 contigs copied from each other) has thousands of entries with equal
-    (hash, position) in several contigs.  pdqsort_branchless (index.cpp:168) is not
-    stable and leaves them in an unspecified order; the GPU build and the host build
-    keep contig order.  So: GPU == host byte for byte, and GPU == the reference's .sti
-    up to the order inside those tie groups (same multiset per group, same bucket
-    table, same filter cutoff).  The reference's bytes come from oracle/_ref/refgen
-    (the reference's own populate(), built here) when it is present."""
+    (hash, position) in several contigs.  Their order is what pdqsort_branchless's element
+    moves leave (index.cpp:168); the GPU build counts them on the device and replays that
+    sort on the host (sti_order.hpp).  The GPU .sti is the reference's, byte for byte,
+    and so is the host build's."""
     from rabbitsalign_amd import native
     fa = os.path.join(GOLDEN, "rep.fa")
     g = _index(fa, tmp_path / "g.sti", "-r", "150")
+    assert hashlib.sha256(g).hexdigest() == golden_sha("rep")
     c = _index(fa, tmp_path / "c.sti", "-r", "150", "--cpu-index")
     assert g == c
-    refgen = os.path.join(ROOT, "oracle", "_ref", "refgen")
-    if not os.path.exists(refgen):
-        pytest.skip("reference populate() build (oracle/_ref/refgen) absent")
-    subprocess.run([refgen, "index", fa, "150", str(tmp_path / "r.sti"), "4"], check=True, capture_output=True)
-    with open(tmp_path / "r.sti", "rb") as f:
-        assert hashlib.sha256(f.read()).hexdigest() == golden_sha("rep")
-    a, b = native.read_sti(str(tmp_path / "g.sti")), native.read_sti(str(tmp_path / "r.sti"))
-    assert (a["filter_cutoff"], a["bits"]) == (b["filter_cutoff"], b["bits"])
-    assert np.array_equal(a["bucket_starts"], b["bucket_starts"])
-    ra, rb = a["randstrobes"], b["randstrobes"]
-    assert np.array_equal(ra["hash"], rb["hash"]) and np.array_equal(ra["position"], rb["position"])
-    diff = np.nonzero(ra["packed"] != rb["packed"])[0]
-    assert len(diff) > 0                                   # the fixture does exercise ties
-    key = lambda r: np.lexsort((r["packed"], r["position"], r["hash"]))
-    assert np.array_equal(ra[key(ra)], rb[key(rb)])        # same entries ...
-    same = (ra["hash"][diff] == ra["hash"][diff - 1]) & (ra["position"][diff] == ra["position"][diff - 1])
-    same |= (ra["hash"][diff] == ra["hash"][np.minimum(diff + 1, len(ra) - 1)]) & \
-            (ra["position"][diff] == ra["position"][np.minimum(diff + 1, len(ra) - 1)])
-    assert same.all()                                      # ... differing only inside tie groups
+    ra = native.read_sti(str(tmp_path / "g.sti"))["randstrobes"]
+    tie = (ra["hash"][1:] == ra["hash"][:-1]) & (ra["position"][1:] == ra["position"][:-1])
+    assert tie.sum() > 0                                   # the fixture does exercise ties
 
 
 @pytest.mark.gpu
