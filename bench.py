@@ -14,8 +14,13 @@ reported beside it.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload pe150_3g]
 
 N>1: one process per GPU under torch.distributed.run; every rank holds the
-replicated index and maps its own shard of pairs (no data-path collective);
-the wall time is the max over ranks and the read count the sum ("weak").
+replicated index, and all ranks map ONE shared FASTQ pair of N x --pairs pairs per
+step in the product's rank/world mode (rsam_part_* / rsam_map_files_part, DESIGN.md
+§7): each rank counts the newlines of its 1/N of each file, the counts are
+all-gathered (the only exchange before mapping), and each rank maps its contiguous
+chunks into its own SAM part; header + parts in rank order are the one-process SAM
+(checked untimed, `parity.parts_equal_one_process`).  The wall time is the max over
+ranks and the read count the sum ("weak": per-GPU work fixed).
 rank 0 prints one JSON line.  `python3 bench.py --gpus N` without WORLD_SIZE
 starts the N ranks itself (rabbitsalign_amd/launch.py; the launcher never
 touches the GPU), then runs the product's one-process multi-device path
@@ -293,6 +298,54 @@ def pick_io_dir(requested: str, need_bytes: int) -> str:
     return tempfile.gettempdir()
 
 
+def write_shared_fastq(reads, f1, f2, tag, io_dir, rank, world, barrier):
+    """N>1: the ranks' slices of one read set as ONE FASTQ pair.  Each rank formats its slice
+    into part files, the part sizes are all-gathered, rank 0 sizes the shared files, and
+    every rank copies its part to its offset (copy_file_range)."""
+    import torch.distributed as dist
+    mine = [os.path.join(io_dir, f"{tag}_slice_1.fq"), os.path.join(io_dir, f"{tag}_slice_2.fq") if f2 else None]
+    reads.write_fastq(mine[0], mine[1])
+    sizes = [os.path.getsize(p) if p else 0 for p in mine]
+    every = [None] * world
+    dist.all_gather_object(every, sizes)
+    targets = [f1, f2]
+    if rank == 0:
+        for i, t in enumerate(targets):
+            if t:
+                with open(t, "wb") as f:
+                    f.truncate(sum(e[i] for e in every))
+    barrier()
+    for i, (src, dst) in enumerate(zip(mine, targets)):
+        if not src:
+            continue
+        off = sum(e[i] for e in every[:rank])
+        with open(src, "rb") as a, open(dst, "r+b") as b:
+            left, o_in, o_out = sizes[i], 0, off
+            while left:
+                n = os.copy_file_range(a.fileno(), b.fileno(), left, o_in, o_out)
+                if n <= 0:
+                    raise OSError(f"copy_file_range into {dst} stopped")
+                left, o_in, o_out = left - n, o_in + n, o_out + n
+        os.remove(src)
+    barrier()
+
+
+def files_concat_equal(paths, one) -> bool:
+    """The files in `paths` back to back == `one`, byte for byte (streamed)."""
+    if sum(os.path.getsize(p) for p in paths) != os.path.getsize(one):
+        return False
+    with open(one, "rb") as f:
+        for p in paths:
+            with open(p, "rb") as g:
+                while True:
+                    b = g.read(1 << 24)
+                    if not b:
+                        break
+                    if f.read(len(b)) != b:
+                        return False
+    return True
+
+
 def host_cpu() -> dict:
     """CPU model and NUMA layout of the box (cpu_baseline context)."""
     model = None
@@ -536,7 +589,9 @@ def main():
     batches = []
     t = time.time()
     for s in range(n_sets):
-        first = shard.first_pair(rank, s, n_sets, P)
+        # set s holds pairs [s*world*P, (s+1)*world*P) of the synthetic stream; this rank generates
+        # (and, at N>1, writes into the shared files) its slice, which its part maps
+        first = shard.shared_set_first(s, rank, world, P)
         batches.append(m.synthetic_reads(args.read_seed, first, P, wl["read_len"], wl["mu"], wl["sigma"],
                                          wl["paired"]))
     log(rank, f"generated {n_sets} x {P} {'pairs' if wl['paired'] else 'reads'} in {time.time()-t:.1f} s")
@@ -547,23 +602,38 @@ def main():
     # mapper over the same files would find them); every step truncates and rewrites its SAM.
     io_dir = pick_io_dir(args.io_dir, n_sets * P * (2 if wl["paired"] else 1) * (2 * wl["read_len"] + 80)
                          + max(args.steps, args.warmup) * P * (2 if wl["paired"] else 1) * (2 * wl["read_len"] + 120))
-    tag = f"rsa_bench_{os.getpid()}_r{rank}"
+    # one tag for the whole job (the ranks share the FASTQ files): rank 0's pid, broadcast
+    job = [os.getpid()]
+    if world > 1:
+        dist.broadcast_object_list(job, src=0)
+    tag = f"rsa_bench_{job[0]}"
     fqs = []
     t = time.time()
     for s, b in enumerate(batches):
         f1 = os.path.join(io_dir, f"{tag}_s{s}_1.fq")
         f2 = os.path.join(io_dir, f"{tag}_s{s}_2.fq") if wl["paired"] else None
-        b.write_fastq(f1, f2)
+        if world == 1:
+            b.write_fastq(f1, f2)
+        else:
+            write_shared_fastq(b, f1, f2, f"{tag}_r{rank}", io_dir, rank, world, barrier)
         fqs.append((f1, f2))
-    # every step writes a SAM file of its own (a new file, as a mapping run makes one);
-    # the files are removed after the timed region
-    sam_paths = [os.path.join(io_dir, f"{tag}_step{s}.sam") for s in range(total_steps)]
+    # every step writes a SAM file of its own (a new file, as a mapping run makes one; at N>1
+    # the rank's part); the files are removed after the timed region
+    sam_paths = [os.path.join(io_dir, f"{tag}_r{rank}_step{s}.sam") for s in range(total_steps)]
     fq_bytes = sum(os.path.getsize(f) for pair in fqs for f in pair if f)
-    log(rank, f"wrote {n_sets} FASTQ sets ({fq_bytes / 1e9:.2f} GB) to {io_dir} in {time.time()-t:.1f} s")
+    log(rank, f"{'wrote' if world == 1 else 'wrote shared'} {n_sets} FASTQ sets ({fq_bytes / 1e9:.2f} GB) to "
+              f"{io_dir} in {time.time()-t:.1f} s")
 
+    parts = {}
     def map_step(s):
         f1, f2 = fqs[s % n_sets]
-        return m.map_files(f1, f2, threads=threads, chunk_size=args.chunk_size, sam_path=sam_paths[s])
+        if world == 1:
+            return m.map_files(f1, f2, threads=threads, chunk_size=args.chunk_size, sam_path=sam_paths[s])
+        # rank/world mode: the plan (newline counts of this rank's 1/N of each file, all-gathered
+        # over RCCL) is part of the step, then this rank's chunks -> its SAM part
+        part = shard.plan_shared_input(f1, f2, args.chunk_size, threads, device="cpu" if rehearse else "cuda")
+        parts[s % n_sets] = part.as_dict()
+        return m.map_files_part(f1, f2, part, threads=threads, sam_path=sam_paths[s])
 
     def drop_sams(upto, keep=()):
         for f in sam_paths[:upto]:
@@ -621,11 +691,29 @@ def main():
         timed_files_identical = all(fhash(sam_paths[s]) == fhash(set_file[s % n_sets])
                                     for s in checked) if checked else None
         hashes = [set_hash.get(s % n_sets, 0) for s in range(args.warmup, total_steps)]
+        # N>1, untimed: header + every rank's part of read set 0 (its warm-up files) == one
+        # process mapping the whole shared input (rank 0, rsam_map_files)
+        parts_parity = None
+        if world > 1 and 0 in set_file:
+            paths = [None] * world
+            dist.all_gather_object(paths, set_file[0])
+            if rank == 0:
+                one = os.path.join(io_dir, f"{tag}_one.sam")
+                f1, f2 = fqs[0]
+                o = m.map_files(f1, f2, threads=threads, chunk_size=args.chunk_size, sam_path=one)
+                parts_parity = {"parts_equal_one_process": files_concat_equal(paths, one),
+                                "one_process_reads": o.n_reads, "one_process_sam_bytes": os.path.getsize(one),
+                                "read_set": 0, "plan": parts.get(0)}
+                os.remove(one)
+                log(rank, f"parts of set 0 concatenated == one-process SAM: {parts_parity['parts_equal_one_process']}")
+            barrier()
     finally:
-        for pair in fqs:
-            for f in pair:
-                if f and os.path.exists(f):
-                    os.remove(f)
+        barrier()
+        if rank == 0:
+            for pair in fqs:
+                for f in pair:
+                    if f and os.path.exists(f):
+                        os.remove(f)
         drop_sams(total_steps)
     # host CPU time of this rank's timed steps (all threads, user + system): the
     # host-bound part of the path, steadier than wall-time throughput on a shared box
@@ -741,7 +829,11 @@ def main():
                    "sam_file_bytes_per_step": sam_file_bytes,
                    "note": "value = FASTQ files -> SAM file (rsam_map_files: reads streamed by a reader "
                            "thread per file while mapping); FASTQ in the page cache, SAM rewritten each step"},
-            "parity": parity,
+            "parity": parity if world == 1 else parts_parity,
+            **({"shared_input": {"pairs_per_step": P * world, "plan_rank0": parts.get(0),
+                                 "note": "every rank maps its chunks of ONE FASTQ pair (rsam_map_files_part); the "
+                                         "plan's newline counts are all-gathered over RCCL inside the timed step"}}
+               if world > 1 else {}),
             "kernels": kernel_table(ks),
             "device_counters": {k: v for k, v in ks.items() if k != "kernels"},
             "host_cpu": {"cpu_s_per_step": round(host_cpu_s / args.steps, 4),

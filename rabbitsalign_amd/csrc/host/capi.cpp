@@ -362,21 +362,27 @@ static void fill_stats(const PipelineResult& res, rsam_stats* out) {
 
 // the pipeline over `src` with the SAM (header + body) to sam_path, or kept in memory
 // only when sam_path is empty; map_seconds covers opening the output to the last byte
+// `first_chunk` / `header`: a rank's part (rsam_map_files_part)
 static int map_source(rsam* m, ReadSource& src, int threads, int chunk_size, const char* sam_path, rsam_stats* out,
-                      std::chrono::steady_clock::time_point t0) {
+                      std::chrono::steady_clock::time_point t0, size_t first_chunk = 0, bool header = true,
+                      size_t end_chunk = SIZE_MAX) {
     PcSampler sampler;
     SinkState st;
     if (sam_path && *sam_path) {
         st.f = fopen(sam_path, "wb");
         if (!st.f) throw std::runtime_error(std::string("cannot open ") + sam_path);
-        std::string hdr = sam_header(m->refs, "", {}, "rsalign (library)");
-        fwrite(hdr.data(), 1, hdr.size(), st.f);
+        if (header) {
+            std::string hdr = sam_header(m->refs, "", {}, "rsalign (library)");
+            fwrite(hdr.data(), 1, hdr.size(), st.f);
+        }
     }
     MapContext mc{m->refs, m->idx.params, m->ap, m->mp};
     PipelineOptions po;
     po.threads = threads;
     po.chunk_size = chunk_size;
     po.digest = m->digest;
+    po.first_chunk = first_chunk;
+    po.end_chunk = end_chunk;
     SamSink sk = st.f ? sink_fn : nullptr;
     PipelineResult res = src.paired() ? run_pipeline_pe(src, *m->eng, mc, po, sk, &st)
                                       : run_pipeline_se(src, *m->eng, mc, po, sk, &st);
@@ -418,6 +424,89 @@ int rsam_map_files(rsam* m, const char* fq1, const char* fq2, int interleaved, i
         std::unique_ptr<ReadSource> src = open_fastq_source(fq1, fq2 ? fq2 : "", interleaved != 0,
                                                             (size_t)std::max(1, chunk_size));
         return map_source(m, *src, threads, chunk_size, sam_path, out, t0);
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+static void to_c(const PartPlan& p, rsam_part* o) {
+    o->rank = p.rank;
+    o->world = p.world;
+    o->chunk_size = p.chunk_size;
+    o->total_pairs = p.total_records;
+    o->n_chunks = p.n_chunks;
+    o->first_chunk = p.first_chunk;
+    o->end_chunk = p.end_chunk;
+    o->first_pair = p.first_record;
+    o->n_pairs = p.n_records;
+    o->offset1 = p.offset1;
+    o->offset2 = p.offset2;
+}
+
+static PartPlan from_c(const rsam_part& o) {
+    PartPlan p;
+    p.rank = o.rank;
+    p.world = o.world;
+    p.chunk_size = o.chunk_size;
+    p.total_records = o.total_pairs;
+    p.n_chunks = o.n_chunks;
+    p.first_chunk = o.first_chunk;
+    p.end_chunk = o.end_chunk;
+    p.first_record = o.first_pair;
+    p.n_records = o.n_pairs;
+    p.offset1 = o.offset1;
+    p.offset2 = o.offset2;
+    return p;
+}
+
+int rsam_part_count(const char* path, int rank, int world, int threads, uint64_t* counts) {
+    if (!path || !counts) return -1;
+    try {
+        const std::vector<uint64_t> c = count_part_lines(path, rank, world, threads);
+        std::copy(c.begin(), c.end(), counts);
+        return 0;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+int rsam_part_plan(const char* fq1, const char* fq2, int rank, int world, int chunk_size, const uint64_t* counts1,
+                   const uint64_t* counts2, int threads, rsam_part* out) {
+    if (!fq1 || !out) return -1;
+    try {
+        const size_t nb = (size_t)std::max(0, world) * RSAM_PART_BLOCKS;
+        const bool se = !fq2 || !*fq2;
+        std::vector<uint64_t> c1, c2;
+        if (counts1) c1.assign(counts1, counts1 + nb);
+        if (counts2 && !se) c2.assign(counts2, counts2 + nb);
+        to_c(plan_part(fq1, se ? "" : fq2, rank, world, (size_t)std::max(1, chunk_size), c1, c2, threads), out);
+        return 0;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+int rsam_map_files_part(rsam* m, const char* fq1, const char* fq2, const rsam_part* part, int threads,
+                        const char* sam_path, rsam_stats* out) {
+    tune_malloc();
+    if (!m || !fq1 || !part) return -1;
+    try {
+        const auto t0 = std::chrono::steady_clock::now();
+        const PartPlan pl = from_c(*part);
+        if (pl.world < 1 || pl.rank < 0 || pl.rank >= pl.world || pl.first_chunk > pl.end_chunk)
+            throw std::runtime_error("rsam_map_files_part: bad part");
+        const bool header = pl.rank == 0;
+        if (pl.n_records == 0) {              // more ranks than chunks: an empty part
+            rsam_reads empty;
+            auto src = make_vector_source(&empty.r1, (fq2 && *fq2) ? &empty.r2 : nullptr, 1);
+            return map_source(m, *src, threads, (int)pl.chunk_size, sam_path, out, t0, 0, header);
+        }
+        std::unique_ptr<ReadSource> src = open_fastq_part_source(fq1, fq2 ? fq2 : "", pl);
+        return map_source(m, *src, threads, (int)pl.chunk_size, sam_path, out, t0, (size_t)pl.first_chunk, header,
+                          (size_t)pl.end_chunk);
     } catch (const std::exception& e) {
         g_err = e.what();
         return -1;

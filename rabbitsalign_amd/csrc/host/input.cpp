@@ -22,6 +22,7 @@
 #include <emmintrin.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <exception>
@@ -245,6 +246,8 @@ class FileBlocks {
         size_t per_block, ahead;
         MappedFile mf;
         size_t pos = 0;                             // mapped mode: next record's offset
+        uint64_t left = UINT64_MAX;                 // records still to read (a rank's part ends early)
+        bool plain_only = false;                    // a rank's part: no kseq fallback (see PartPlan)
         size_t populated = 0;                       // mapped bytes already in the page table
         std::unique_ptr<FastxReader> seq;           // sequential mode
         std::mutex m;
@@ -301,14 +304,20 @@ class FileBlocks {
         }
         // returns the mapped offset the block ends at (0 in sequential mode)
         size_t read_block(Block& b) {
-            b.recs.reserve(per_block);
+            const size_t cap = (size_t)std::min<uint64_t>(per_block, left);
+            const size_t got = fill_block(b, cap);
+            left -= got;
+            return pos;
+        }
+        size_t fill_block(Block& b, size_t cap) {
+            b.recs.reserve(cap);
             if (!seq) {
                 populate(16u << 20);
                 const char* end = mf.p + mf.n;
                 const char* p = mf.p + pos;
                 NlIter it(p, end);
                 RecView r;
-                while (b.recs.size() < per_block && p < end) {
+                while (b.recs.size() < cap && p < end) {
                     const NlIter save = it;
                     const char* at = p;
                     if (!plain_record(p, end, it, r)) {
@@ -319,11 +328,15 @@ class FileBlocks {
                     b.recs.push_back(r);
                 }
                 pos = (size_t)(p - mf.p);
-                if (b.recs.size() == per_block || p >= end) return pos;
+                if (b.recs.size() == cap || p >= end) return b.recs.size();
+                if (plain_only)
+                    throw std::runtime_error(path + ": the record at byte " + std::to_string(pos) +
+                                             " is not in the plain four-line FASTQ layout, which a rank's part of "
+                                             "the input needs (map the file in one process instead)");
                 // not the plain layout from here on: kseq over the rest of the mapped bytes
                 seq.reset(new FastxReader(p, (size_t)(end - p)));
             }
-            const size_t want = per_block - b.recs.size();
+            const size_t want = cap - b.recs.size();
             b.owned.reserve(want);
             Record r;
             while (b.owned.size() < want && seq->next(r)) {
@@ -331,20 +344,31 @@ class FileBlocks {
                 r = Record();
             }
             for (const Record& x : b.owned) b.recs.push_back(RecView(x));
-            return pos;
+            return b.recs.size();
         }
     };
 
 public:
-    FileBlocks(const std::string& path, size_t per_block, size_t ahead) : st_(std::make_shared<State>()) {
+    // `start` / `max_records` / `plain_only`: a rank's part of a mapped file (PartPlan)
+    FileBlocks(const std::string& path, size_t per_block, size_t ahead, uint64_t start = 0,
+               uint64_t max_records = UINT64_MAX, bool plain_only = false)
+        : st_(std::make_shared<State>()) {
         State& s = *st_;
         s.path = path;
         s.per_block = std::max<size_t>(1, per_block);
         s.ahead = std::max<size_t>(1, ahead);
+        s.left = max_records;
+        s.plain_only = plain_only;
         if (!s.mf.open_map(s.path)) {
             s.mf.reset();
+            if (start || plain_only)
+                throw std::runtime_error(path + ": a rank's part of the input needs a regular, uncompressed file");
             s.seq.reset(new FastxReader(s.path));   // throws when the file cannot be opened
         }
+        if (start > s.mf.n) throw std::runtime_error(path + ": part offset past the end of the file");
+        s.pos = (size_t)start;
+        s.populated = (size_t)start;
+        s.dropped = (size_t)start & ~(size_t)4095;
         std::shared_ptr<State> keep = st_;
         th_ = std::thread([keep] { keep->run(); });
     }
@@ -442,6 +466,44 @@ private:
     std::thread th_;
 };
 
+// block idx of one file (single-end) or of both mate files, as chunk `index`
+bool take_chunk(FileBlocks& f1, FileBlocks* f2, bool interleaved, size_t block, size_t index, InputChunk& out) {
+    out.clear();
+    out.index = index;
+    Block b1, b2;
+    const bool h1 = f1.take(block, b1);
+    if (f2) {
+        const bool h2 = f2->take(block, b2);
+        if (h1 != h2 || b1.recs.size() != b2.recs.size())
+            throw std::runtime_error("read files have different record counts");
+        if (!h1) return false;
+        out.r1 = std::move(b1.recs);
+        out.r2 = std::move(b2.recs);
+        out.owned1 = std::move(b1.owned);   // the vectors' buffers move, the records stay put
+        out.owned2 = std::move(b2.owned);
+        return true;
+    }
+    if (!h1) return false;
+    if (interleaved) {
+        out.singletons = distribute_interleaved(b1.recs.data(), b1.recs.size(), out.r1, out.r2);
+    } else {
+        out.r1 = std::move(b1.recs);
+    }
+    out.owned1 = std::move(b1.owned);
+    return true;
+}
+
+// readlen.cpp:16-29 over InputBuffer::read_records(.., 500) (pc.cpp:74-107): the
+// first 500 records of each file, or the first 1000 records of an interleaved
+// file; 150 when the first file has none
+int estimate_from(FileBlocks& f1, FileBlocks* f2, bool interleaved) {
+    uint64_t tot1 = 0, n1 = 0, tot2 = 0, n2 = 0;
+    f1.peek_lengths(interleaved ? 1000 : 500, tot1, n1);
+    if (n1 == 0) return 150;
+    if (f2) f2->peek_lengths(500, tot2, n2);
+    return (int)((tot1 + tot2) / (n1 + n2));
+}
+
 class FastqSource final : public ReadSource {
 public:
     FastqSource(const std::string& p1, const std::string& p2, bool interleaved, size_t chunk)
@@ -452,57 +514,243 @@ public:
         if (!p2.empty()) f2_.reset(new FileBlocks(p2, per, kAhead));
     }
     bool paired() const override { return f2_ != nullptr || interleaved_; }
-    bool get(size_t idx, InputChunk& out) override {
-        out.clear();
-        out.index = idx;
-        Block b1, b2;
-        const bool h1 = f1_->take(idx, b1);
-        if (f2_) {
-            const bool h2 = f2_->take(idx, b2);
-            if (h1 != h2 || b1.recs.size() != b2.recs.size())
-                throw std::runtime_error("read files have different record counts");
-            if (!h1) return false;
-            out.r1 = std::move(b1.recs);
-            out.r2 = std::move(b2.recs);
-            out.owned1 = std::move(b1.owned);   // the vectors' buffers move, the records stay put
-            out.owned2 = std::move(b2.owned);
-            return true;
-        }
-        if (!h1) return false;
-        if (interleaved_) {
-            out.singletons = distribute_interleaved(b1.recs.data(), b1.recs.size(), out.r1, out.r2);
-        } else {
-            out.r1 = std::move(b1.recs);
-        }
-        out.owned1 = std::move(b1.owned);
-        return true;
-    }
+    bool get(size_t idx, InputChunk& out) override { return take_chunk(*f1_, f2_.get(), interleaved_, idx, idx, out); }
     void release(InputChunk& c) override {
         f1_->done(c.index);
         if (f2_) f2_->done(c.index);
         c.clear();
     }
-    // readlen.cpp:16-29 over InputBuffer::read_records(.., 500) (pc.cpp:74-107): the
-    // first 500 records of each file, or the first 1000 records of an interleaved
-    // file; 150 when the first file has none
     void cancel() override {
         f1_->cancel();
         if (f2_) f2_->cancel();
     }
-    int estimate_read_length() override {
-        uint64_t tot1 = 0, n1 = 0, tot2 = 0, n2 = 0;
-        f1_->peek_lengths(interleaved_ ? 1000 : 500, tot1, n1);
-        if (n1 == 0) return 150;
-        if (f2_) f2_->peek_lengths(500, tot2, n2);
-        return (int)((tot1 + tot2) / (n1 + n2));
-    }
+    int estimate_read_length() override { return estimate_from(*f1_, f2_.get(), interleaved_); }
 
 private:
     bool interleaved_;
     std::unique_ptr<FileBlocks> f1_, f2_;
 };
 
+// ------------------------------------------------------- a rank's part --
+class PartSource final : public ReadSource {
+public:
+    PartSource(const std::string& p1, const std::string& p2, const PartPlan& plan)
+        : p1_(p1), p2_(p2), plan_(plan) {
+        static const size_t kAhead = getenv("RSA_READ_AHEAD") ? (size_t)atol(getenv("RSA_READ_AHEAD")) : 4;
+        const size_t per = (size_t)std::max<uint64_t>(1, plan.chunk_size);
+        // paired: one chunk past the part when there is one (the pipeline's insert-size replay
+        // may part() it, PipelineOptions::end_chunk)
+        const uint64_t tail = p2.empty() ? 0 : std::min<uint64_t>(per, plan.total_records - plan.first_record -
+                                                                            plan.n_records);
+        const uint64_t n = plan.n_records ? plan.n_records + tail : 0;
+        r1_.reset(new FileBlocks(p1, per, kAhead, plan.offset1, n, true));
+        if (!p2.empty()) r2_.reset(new FileBlocks(p2, per, kAhead, plan.offset2, n, true));
+        if (plan.first_chunk > 0 && !p2.empty()) open_prefix();
+    }
+    bool paired() const override { return !p2_.empty(); }
+    bool get(size_t idx, InputChunk& out) override {
+        if (idx < plan_.first_chunk) {
+            if (!f1_) throw std::logic_error("a chunk before the part asked for without the insert-size replay");
+            return take_chunk(*f1_, f2_.get(), false, idx, idx, out);
+        }
+        if (idx > plan_.end_chunk || (idx == plan_.end_chunk && !paired())) {
+            out.clear();
+            out.index = idx;
+            return false;
+        }
+        return take_chunk(*r1_, r2_.get(), false, idx - plan_.first_chunk, idx, out);
+    }
+    void release(InputChunk& c) override {
+        if (c.index < plan_.first_chunk) {
+            if (f1_) f1_->done(c.index);
+            if (f2_) f2_->done(c.index);
+        } else {
+            r1_->done(c.index - plan_.first_chunk);
+            if (r2_) r2_->done(c.index - plan_.first_chunk);
+        }
+        c.clear();
+    }
+    void cancel() override {
+        for (FileBlocks* f : {f1_.get(), f2_.get(), r1_.get(), r2_.get()})
+            if (f) f->cancel();
+    }
+    // from the file start, as one process estimates it (called before mapping starts)
+    int estimate_read_length() override {
+        if (!f1_) open_prefix();
+        return estimate_from(*f1_, f2_.get(), false);
+    }
+
+private:
+    // the files from their start: chunks 0 .. first_chunk - 1, read one block ahead
+    void open_prefix() {
+        const size_t per = (size_t)std::max<uint64_t>(1, plan_.chunk_size);
+        f1_.reset(new FileBlocks(p1_, per, 1));
+        if (!p2_.empty()) f2_.reset(new FileBlocks(p2_, per, 1));
+    }
+    std::string p1_, p2_;
+    PartPlan plan_;
+    std::unique_ptr<FileBlocks> f1_, f2_;          // from the file start (insert-size replay, estimate)
+    std::unique_ptr<FileBlocks> r1_, r2_;          // the part
+};
+
+struct Fd {
+    int fd = -1;
+    explicit Fd(const std::string& path) : fd(::open(path.c_str(), O_RDONLY)) {
+        if (fd < 0) throw std::runtime_error("cannot open " + path);
+    }
+    ~Fd() { if (fd >= 0) close(fd); }
+    uint64_t size() const {
+        struct stat st;
+        if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode))
+            throw std::runtime_error("a rank's part of the input needs regular files");
+        return (uint64_t)st.st_size;
+    }
+};
+
+inline uint64_t block_at(uint64_t size, uint64_t nb, uint64_t b) {
+    return (uint64_t)((unsigned __int128)size * b / nb);
+}
+
+// '\n' bytes of [p, p + n): SSE2 compares, a popcount per 64 bytes
+inline uint64_t count_nl(const char* p, size_t n) {
+    uint64_t c = 0;
+    size_t i = 0;
+    const __m128i nl = _mm_set1_epi8('\n');
+    for (; i + 64 <= n; i += 64) {
+        const uint64_t m0 = (uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128((const __m128i*)(p + i)), nl));
+        const uint64_t m1 = (uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128((const __m128i*)(p + i + 16)), nl));
+        const uint64_t m2 = (uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128((const __m128i*)(p + i + 32)), nl));
+        const uint64_t m3 = (uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128((const __m128i*)(p + i + 48)), nl));
+        c += (uint64_t)__builtin_popcountll(m0 | m1 << 16 | m2 << 32 | m3 << 48);
+    }
+    for (; i < n; ++i) c += p[i] == '\n';
+    return c;
+}
+
+// newline counts of blocks [b0, b0 + nblk) of nb, read with pread (no mapping: the
+// page cache copies straight into a per-thread buffer)
+std::vector<uint64_t> count_blocks(const std::string& path, uint64_t nb, uint64_t b0, uint64_t nblk, int threads) {
+    Fd f(path);
+    const uint64_t size = f.size();
+    std::vector<uint64_t> out(nblk, 0);
+    std::atomic<uint64_t> next{0};
+    std::exception_ptr err;
+    std::mutex em;
+    auto work = [&] {
+        std::vector<char> buf(4u << 20);
+        try {
+            for (uint64_t j; (j = next.fetch_add(1)) < nblk;) {
+                uint64_t a = block_at(size, nb, b0 + j);
+                const uint64_t e = block_at(size, nb, b0 + j + 1);
+                uint64_t c = 0;
+                while (a < e) {
+                    const ssize_t got = pread(f.fd, buf.data(), (size_t)std::min<uint64_t>(buf.size(), e - a), (off_t)a);
+                    if (got <= 0) throw std::runtime_error("read failed: " + path);
+                    c += count_nl(buf.data(), (size_t)got);
+                    a += (uint64_t)got;
+                }
+                out[j] = c;
+            }
+        } catch (...) {
+            std::lock_guard<std::mutex> g(em);
+            if (!err) err = std::current_exception();
+        }
+    };
+    const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max(1, threads), nblk));
+    std::vector<std::thread> ws;
+    for (int t = 1; t < T; ++t) ws.emplace_back(work);
+    work();
+    for (auto& w : ws) w.join();
+    if (err) std::rethrow_exception(err);
+    return out;
+}
+
+// byte offset just past newline number k (1-based) of a file whose nb blocks hold `lines`
+uint64_t after_newline(const std::string& path, const std::vector<uint64_t>& lines, uint64_t k) {
+    Fd f(path);
+    const uint64_t size = f.size(), nb = lines.size();
+    uint64_t before = 0, b = 0;
+    while (b < nb && before + lines[b] < k) before += lines[b++];
+    if (b == nb) throw std::runtime_error(path + ": fewer lines than the part plan needs");
+    uint64_t a = block_at(size, nb, b);
+    const uint64_t e = block_at(size, nb, b + 1);
+    uint64_t want = k - before;
+    std::vector<char> buf(1u << 20);
+    while (a < e) {
+        const ssize_t got = pread(f.fd, buf.data(), (size_t)std::min<uint64_t>(buf.size(), e - a), (off_t)a);
+        if (got <= 0) throw std::runtime_error("read failed: " + path);
+        for (ssize_t i = 0; i < got; ++i)
+            if (buf[(size_t)i] == '\n' && --want == 0) return a + (uint64_t)i + 1;
+        a += (uint64_t)got;
+    }
+    throw std::runtime_error(path + ": newline count changed while planning");
+}
+
+// records of a plain four-line FASTQ from its block counts (a last line without '\n' counts)
+uint64_t records_of(const std::string& path, const std::vector<uint64_t>& lines) {
+    Fd f(path);
+    const uint64_t size = f.size();
+    uint64_t n = 0;
+    for (uint64_t c : lines) n += c;
+    if (size) {
+        char last = 0;
+        if (pread(f.fd, &last, 1, (off_t)(size - 1)) != 1) throw std::runtime_error("read failed: " + path);
+        if (last != '\n') ++n;
+    }
+    if (n % 4) throw std::runtime_error(path + ": " + std::to_string(n) + " lines, not a plain four-line FASTQ (a "
+                                        "rank's part needs one record per four lines; map it in one process)");
+    return n / 4;
+}
+
+void check_record_start(const std::string& path, uint64_t off) {
+    Fd f(path);
+    char c = 0;
+    if (pread(f.fd, &c, 1, (off_t)off) != 1 || c != '@')
+        throw std::runtime_error(path + ": no FASTQ record starts at byte " + std::to_string(off) +
+                                 " (a rank's part needs the plain four-line layout)");
+}
+
 }  // namespace
+
+std::vector<uint64_t> count_part_lines(const std::string& path, int rank, int world, int threads) {
+    if (world < 1 || rank < 0 || rank >= world) throw std::runtime_error("bad rank/world");
+    return count_blocks(path, (uint64_t)world * kPartBlocks, (uint64_t)rank * kPartBlocks, kPartBlocks, threads);
+}
+
+PartPlan plan_part(const std::string& p1, const std::string& p2, int rank, int world, size_t chunk_size,
+                   std::vector<uint64_t> lines1, std::vector<uint64_t> lines2, int threads) {
+    if (world < 1 || rank < 0 || rank >= world) throw std::runtime_error("bad rank/world");
+    const uint64_t nb = (uint64_t)world * kPartBlocks;
+    if (lines1.empty()) lines1 = count_blocks(p1, nb, 0, nb, threads);
+    if (!p2.empty() && lines2.empty()) lines2 = count_blocks(p2, nb, 0, nb, threads);
+    if (lines1.size() != nb || (!p2.empty() && lines2.size() != nb))
+        throw std::runtime_error("part plan: expected world * 64 block counts per file");
+    PartPlan pl;
+    pl.rank = rank;
+    pl.world = world;
+    pl.chunk_size = std::max<size_t>(1, chunk_size);
+    pl.total_records = records_of(p1, lines1);
+    if (!p2.empty() && records_of(p2, lines2) != pl.total_records)
+        throw std::runtime_error("read files have different record counts");
+    pl.n_chunks = (pl.total_records + pl.chunk_size - 1) / pl.chunk_size;
+    pl.first_chunk = pl.n_chunks * (uint64_t)rank / (uint64_t)world;
+    pl.end_chunk = pl.n_chunks * (uint64_t)(rank + 1) / (uint64_t)world;
+    pl.first_record = std::min(pl.total_records, pl.first_chunk * pl.chunk_size);
+    pl.n_records = std::min(pl.total_records, pl.end_chunk * pl.chunk_size) - pl.first_record;
+    if (pl.n_records) {
+        pl.offset1 = pl.first_record ? after_newline(p1, lines1, 4 * pl.first_record) : 0;
+        check_record_start(p1, pl.offset1);
+        if (!p2.empty()) {
+            pl.offset2 = pl.first_record ? after_newline(p2, lines2, 4 * pl.first_record) : 0;
+            check_record_start(p2, pl.offset2);
+        }
+    }
+    return pl;
+}
+
+std::unique_ptr<ReadSource> open_fastq_part_source(const std::string& p1, const std::string& p2, const PartPlan& plan) {
+    return std::unique_ptr<ReadSource>(new PartSource(p1, p2, plan));
+}
 
 std::unique_ptr<ReadSource> make_vector_source(const std::vector<Record>* r1, const std::vector<Record>* r2,
                                                size_t chunk_size) {

@@ -21,6 +21,7 @@ namespace {
 
 struct Opts {
     int threads = 3, chunk_size = 10000, device = 0, max_secondary = 0;
+    int rank = 0, world = 1;           // --rank / --world: this process maps one part of the input
     std::string out_file, rg_id, ref, reads1, reads2, devices;
     std::vector<std::string> rg;
     bool verbose = false, eqx = false, no_unmapped = false, details = false, create_index = false,
@@ -40,6 +41,8 @@ void usage(const char* prog) {
             "  -t INT threads [3]   --chunk-size INT [10000]   -o PATH   --eqx   -U   --details\n"
             "  --rg-id ID  --rg TAG:VALUE   -N INT   -i/--create-index   --use-index   --device INT   --cpu-index\n"
             "  --devices LIST  map on several GPUs of this node (e.g. 0,1,2,3; index replicated per device)\n"
+            "  --rank R --world W  map part R of W of the input (plain FASTQ); the SAM parts of ranks\n"
+            "                      0..W-1 concatenated are the one-process SAM (rank 0's has the header)\n"
             "  seeding: -r -m -k -l -u -s -c -b      alignment: -A -B -O -E -L\n"
             "  search: -f FLOAT -S FLOAT -M INT -R INT\n",
             prog, prog);
@@ -73,6 +76,8 @@ Opts parse(int argc, char** argv, bool& ok) {
         else if (a == "--cpu-index") o.cpu_index = true;
         else if (a == "--device") o.device = atoi(need(i));
         else if (a == "--devices") o.devices = need(i);
+        else if (a == "--rank") o.rank = atoi(need(i));
+        else if (a == "--world") o.world = atoi(need(i));
         else if (a == "-r") { o.r = atoi(need(i)); o.r_set = true; }
         else if (a == "-m") o.m = atoi(need(i));
         else if (a == "-k") o.k = atoi(need(i));
@@ -125,9 +130,21 @@ int cli_main(int argc, char** argv, EngineFactory factory, const char* prog) {
         // interleaved file) is taken from the records it has parsed, which stay queued
         // for mapping -- a pipe or stdin is read once, as the reference's
         // RewindableFile replays what the estimate read (fastq.cpp:1-65)
+        if (o.world < 1 || o.rank < 0 || o.rank >= o.world) throw std::runtime_error("--rank must be in [0, --world)");
+        const bool part = o.world > 1;
+        if (part && o.interleaved) throw std::runtime_error("--rank/--world take two read files or one single-end file");
         std::unique_ptr<ReadSource> src;
-        if (!o.reads1.empty() && !index_cmd)
-            src = open_fastq_source(o.reads1, o.reads2, o.interleaved, (size_t)std::max(1, o.chunk_size));
+        PartPlan plan;
+        if (!o.reads1.empty() && !index_cmd) {
+            if (part) {
+                // no exchange between the ranks here: each counts every block of the files
+                plan = plan_part(o.reads1, o.reads2, o.rank, o.world, (size_t)std::max(1, o.chunk_size), {}, {},
+                                 std::max(1, o.threads));
+                src = open_fastq_part_source(o.reads1, o.reads2, plan);
+            } else {
+                src = open_fastq_source(o.reads1, o.reads2, o.interleaved, (size_t)std::max(1, o.chunk_size));
+            }
+        }
         if (src && !o.r_set) o.r = src->estimate_read_length();
         IndexParameters ip = IndexParameters::from_read_length(o.r, o.k, o.s, o.l, o.u, o.c, o.m);
         auto t0 = std::chrono::steady_clock::now();
@@ -174,10 +191,16 @@ int cli_main(int argc, char** argv, EngineFactory factory, const char* prog) {
         std::string cmd;
         for (int i = 0; i < argc; ++i) { cmd += argv[i]; cmd += ' '; }
         std::string hdr = sam_header(refs, o.rg_id, o.rg, cmd);
-        fwrite(hdr.data(), 1, hdr.size(), out);
+        if (o.rank == 0) fwrite(hdr.data(), 1, hdr.size(), out);
         MapContext mc{refs, idx.params, ap, mp};
         PipelineOptions po;
         po.threads = o.threads; po.chunk_size = o.chunk_size; po.rg_id = o.rg_id;
+        po.first_chunk = part ? (size_t)plan.first_chunk : 0;
+        po.end_chunk = part ? (size_t)plan.end_chunk : SIZE_MAX;
+        if (part && o.verbose)
+            fprintf(stderr, "[%s] rank %d of %d: chunks [%lu, %lu) of %lu, pairs [%lu, %lu)\n", prog, o.rank, o.world,
+                    (unsigned long)plan.first_chunk, (unsigned long)plan.end_chunk, (unsigned long)plan.n_chunks,
+                    (unsigned long)plan.first_record, (unsigned long)(plan.first_record + plan.n_records));
         if (o.verbose) fprintf(stderr, "[%s] mapping %s%s%s%s\n", prog, o.reads1.c_str(), o.reads2.empty() ? "" : " + ",
                                o.reads2.c_str(), o.interleaved ? " (interleaved)" : "");
         PipelineResult res = src->paired() ? run_pipeline_pe(*src, *eng, mc, po, write_sink, out)

@@ -140,7 +140,8 @@ struct OrderedSink {
     SamDigest total;
     bool closing = false;
     std::thread writer;
-    OrderedSink(SamSink s, void* u, bool d) : sink(s), user(u), digest(d) {
+    // `first`: the first chunk index this sink writes (a rank's part starts later)
+    OrderedSink(SamSink s, void* u, bool d, size_t first = 0) : sink(s), user(u), digest(d), next(first) {
         if (sink) writer = std::thread([this] { write_loop(); });
     }
     ~OrderedSink() { close(); }
@@ -536,8 +537,11 @@ void pe_seed(PeChunk& c, Engine& eng, const MapContext& mc, CpuSlots& slots) {
 // on_frozen (sequential phase only) runs once, right after the pair whose
 // sample freezes the insert-size estimate: from there on no later chunk depends
 // on this one's remaining pairs, so the other workers can start.
+// `replay_only`: a chunk before a rank's part (PipelineOptions::first_chunk), parted
+// only for the insert-size estimate: nothing of it is used once the estimate froze.
 template <class OnFrozen>
-void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize, OnFrozen&& on_frozen) {
+void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize, OnFrozen&& on_frozen,
+             bool replay_only = false) {
     bool was_frozen = isize.frozen();
     c.rng.seed((unsigned)c.in.index);
     const size_t n = c.size();
@@ -590,6 +594,7 @@ void pe_part(PeChunk& c, const MapContext& mc, InsertSizeDistribution& isize, On
             was_frozen = true;
             on_frozen(c);
         }
+        if (replay_only && was_frozen) break;
     }
     c.seeds.clear();
     c.times.part += since(t);
@@ -704,7 +709,15 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
     const auto t0 = Clock::now();
     PipelineResult result;
     eng.set_alignment_params(mc.aparams);     // hamming_align with the site checks (GPU engine)
-    OrderedSink os(sink, user, opt.digest);
+    // a rank's part: chunks below `first` are replayed for the insert-size estimate only
+    const size_t first = opt.first_chunk, end = opt.end_chunk;
+    if (first >= end) {                     // an empty part (more ranks than chunks)
+        result.map_seconds = since(t0);
+        return result;
+    }
+    auto rel = [first](size_t i) { return i >= first ? i - first : i; };   // position among the run's own chunks
+    auto mine = [first, end](size_t i) { return i >= first && i < end; };
+    OrderedSink os(sink, user, opt.digest, first);
     const int T = std::max(1, opt.threads);
     const bool offl = eng.offloads();
     const int W = T + wait_workers(eng, T);
@@ -723,8 +736,17 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
         if (i >= claimed.size()) claimed.resize(i + 1, 0);
         claimed[i] = 1;
     };
-    size_t n_chunks = SIZE_MAX;    // chunks of the input, once a claim has run past its end
-    size_t next_seed = 0;          // every chunk below is claimed
+    // the next chunk to prefetch: unclaimed, and never a replay chunk past 0 (those are
+    // loaded by the leader when the estimate needs them)
+    size_t next_seed = 0;          // every chunk below is claimed (or a replay chunk)
+    auto skip_claimed = [&] {
+        for (;;) {
+            if (next_seed > 0 && next_seed < first) next_seed = first;
+            else if (is_claimed(next_seed)) next_seed++;
+            else break;
+        }
+    };
+    size_t n_chunks = end;         // chunks of the input (of the part), once a claim has run past its end
     size_t consumed = 0;           // chunks handed past stage 1
     bool frozen = false, done = false;
     bool early = false;            // the parallel stage opened from inside part() (early_freeze)
@@ -773,11 +795,11 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
         std::unique_lock<std::mutex> g(m);
         if (!is_claimed(idx)) {                 // nobody claimed it yet
             claim(idx);
-            while (is_claimed(next_seed)) next_seed++;
+            skip_claimed();
             g.unlock();
             auto c = stage1(idx);
             g.lock();
-            if (c) consumed++;
+            if (c && idx >= first) consumed++;
             cv.notify_all();
             return c;
         }
@@ -793,7 +815,7 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
         if (failure || !seeded.count(idx)) return nullptr;
         auto c = std::move(seeded[idx]);
         seeded.erase(idx);
-        consumed++;
+        if (idx >= first) consumed++;
         cv.notify_all();
         return c;
     };
@@ -834,7 +856,7 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
                 std::lock_guard<std::mutex> g(m);
                 frozen = true;
                 frozen_isize = isize;
-                next_par = cur_chunk.in.index + 1;
+                next_par = std::max(cur_chunk.in.index + 1, first);
                 early = true;
                 cv.notify_all();
             };
@@ -850,18 +872,24 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
                     cv.notify_all();
                 }
                 if (lost) return;
-                if (pre) pe_part(*pre, mc, isize, early_freeze);
+                if (pre) pe_part(*pre, mc, isize, early_freeze, !mine(pre->in.index));
                 size_t next = 1;
-                while (pre && !isize.frozen()) {
+                while (pre && !isize.frozen() && pre->in.index < end) {
+                    const bool own = mine(pre->in.index);         // else replayed for the estimate only
                     jobs.clear();
-                    pe_get_str(*pre, mc, isize.mu, isize.sigma, jobs);
+                    if (own) pe_get_str(*pre, mc, isize.mu, isize.sigma, jobs);
                     std::unique_ptr<PeChunk> cur = acquire(next);
                     if (!cur) {
                         std::lock_guard<std::mutex> g(m);
                         if (failure) return;
                     }
-                    if (cur) pe_part(*cur, mc, isize, early_freeze);
+                    if (cur) pe_part(*cur, mc, isize, early_freeze, !mine(cur->in.index));
                     next++;
+                    if (!own) {
+                        recycle(std::move(pre));
+                        pre = std::move(cur);
+                        continue;
+                    }
                     const auto te = Clock::now();
                     {
                         Unslot u(slots, offl, pre->in.index);
@@ -879,12 +907,13 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
                     pre = std::move(cur);
                 }
                 lt.sequential = since(t0);
+                if (pre && !mine(pre->in.index)) recycle(std::move(pre));   // replayed only
                 std::lock_guard<std::mutex> g(m);
                 frozen = true;
                 frozen_isize = isize;
                 handed = std::move(pre);                 // may be null: everything was sequential
                 leader_busy = false;
-                if (!early) next_par = next;
+                if (!early) next_par = std::max(next, first);
                 if (next_par >= n_chunks && !handed) done = true;
                 cv.notify_all();
             }
@@ -898,11 +927,12 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
                         if (failure || done) break;
                         if (frozen && handed) { c = std::move(handed); break; }
                         if (frozen && next_par < n_chunks) { idx = next_par++; break; }
-                        if ((lead_seeded || next_seed <= early_seeds) && next_seed < n_chunks &&
-                            next_seed < consumed + window) {
+                        skip_claimed();
+                        if ((lead_seeded || rel(next_seed) <= early_seeds) && next_seed < n_chunks &&
+                            rel(next_seed) < consumed + window) {
                             pf = next_seed;
                             claim(pf);
-                            while (is_claimed(next_seed)) next_seed++;
+                            skip_claimed();
                             break;
                         }
                         if (frozen && next_par >= n_chunks && !leader_busy) { done = true; cv.notify_all(); break; }
@@ -1019,8 +1049,8 @@ PipelineResult run_pipeline_se(ReadSource& src, Engine& eng, const MapContext& m
     auto t0 = std::chrono::steady_clock::now();
     PipelineResult result;
     eng.set_alignment_params(mc.aparams);
-    OrderedSink os(sink, user, opt.digest);
-    std::atomic<size_t> next{0};
+    OrderedSink os(sink, user, opt.digest, opt.first_chunk);
+    std::atomic<size_t> next{opt.first_chunk};      // chunks are independent: a part starts at its own
     std::mutex stat_m;
     const int T = std::max(1, opt.threads);
     const bool offl = eng.offloads();

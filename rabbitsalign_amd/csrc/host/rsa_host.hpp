@@ -686,6 +686,43 @@ std::unique_ptr<ReadSource> make_interleaved_vector_source(const std::vector<Rec
 std::unique_ptr<ReadSource> open_fastq_source(const std::string& path1, const std::string& path2, bool interleaved,
                                               size_t chunk_size);
 
+// ------------------------------------------------------- a rank's part ---
+// rank/world mode: one input pair of plain four-line FASTQ files,
+// mapped by `world` processes (one per GPU).  The records are cut into the same
+// chunks of chunk_size pairs a single process maps, so every chunk keeps its
+// chunk_index (the minstd_rand seed, pc.cpp:1583); rank r maps chunks
+// [r*C/W, (r+1)*C/W) of the C chunks.  Each rank replays the single-worker
+// timeline from chunk 0 until the insert-size estimate freezes (its output
+// discarded), so it reaches the same frozen estimate; if the estimate is still
+// open at the part's end, the next chunk's part() is replayed as well (the last
+// chunk is stored with the estimate after it).  Rank r's SAM part holds
+// exactly its chunks' records (rank 0's part starts with the header): the parts
+// concatenated in rank order are the one-process SAM.
+//
+// Finding a part's first record needs the record count before it.  Each file is
+// cut into world * kPartBlocks equal byte blocks; a rank counts the newlines of its
+// own kPartBlocks blocks, the counts of all ranks are exchanged (an all-gather of
+// world * kPartBlocks integers per file, done by the caller), and the plan follows:
+// record i starts after newline 4i.  With no exchange a rank counts every block.
+constexpr int kPartBlocks = 64;
+struct PartPlan {
+    int rank = 0, world = 1;
+    uint64_t chunk_size = 10000;
+    uint64_t total_records = 0, n_chunks = 0;    // records (pairs) of the input, chunks of the input
+    uint64_t first_chunk = 0, end_chunk = 0;     // this rank's chunks
+    uint64_t first_record = 0, n_records = 0;    // this rank's records
+    uint64_t offset1 = 0, offset2 = 0;           // byte offset of first_record in each file
+};
+// newline counts of rank `rank`'s kPartBlocks blocks of a file cut into world * kPartBlocks
+std::vector<uint64_t> count_part_lines(const std::string& path, int rank, int world, int threads);
+// the plan from all world * kPartBlocks counts of each file (an empty vector: counted here);
+// p2 empty: single-end
+PartPlan plan_part(const std::string& p1, const std::string& p2, int rank, int world, size_t chunk_size,
+                   std::vector<uint64_t> lines1, std::vector<uint64_t> lines2, int threads);
+// the chunks of the plan, streamed (plus chunks 0.. from the file start when the
+// paired pipeline replays the insert-size phase)
+std::unique_ptr<ReadSource> open_fastq_part_source(const std::string& p1, const std::string& p2, const PartPlan& plan);
+
 // ------------------------------------------------------------ pipeline ---
 // called at the start of every pipeline worker thread (profiling hooks; null by default)
 extern void (*g_worker_start_hook)();
@@ -695,6 +732,12 @@ struct PipelineOptions {
     int chunk_size = 10000;
     std::string rg_id;
     bool digest = false;   // compute PipelineResult::sam_digest (in the workers, in parallel)
+    // a rank's part (PartPlan): chunks [first_chunk, end_chunk) are this rank's.  The
+    // paired pipeline still runs the chunks before them through part() until the
+    // insert-size estimate freezes, and -- when it has not frozen by then -- chunk
+    // end_chunk too, whose part() moves the estimate chunk end_chunk - 1 is stored
+    // with (pc.cpp:1739-1798); it writes nothing of those
+    size_t first_chunk = 0, end_chunk = SIZE_MAX;
 };
 
 // --interleaved input (InputBuffer::read_records + distribute_interleaved,

@@ -39,10 +39,24 @@ class _Info(C.Structure):
                 ("index_replayed_segments", C.c_uint64)]
 
 
+class Part(C.Structure):
+    """rsam_part (include/rsalign.h): one rank's chunks of a shared input."""
+    _fields_ = [("rank", C.c_int32), ("world", C.c_int32), ("chunk_size", C.c_uint64), ("total_pairs", C.c_uint64),
+                ("n_chunks", C.c_uint64), ("first_chunk", C.c_uint64), ("end_chunk", C.c_uint64),
+                ("first_pair", C.c_uint64), ("n_pairs", C.c_uint64), ("offset1", C.c_uint64), ("offset2", C.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+PART_BLOCKS = 64     # RSAM_PART_BLOCKS
+
+
 EXPORTED_SYMBOLS = [
     "rsam_open_files", "rsam_open_synthetic", "rsam_open_like", "rsam_close", "rsam_get_info",
     "rsam_reads_load", "rsam_reads_load_interleaved", "rsam_reads_synthetic", "rsam_reads_write_fastq", "rsam_reads_count", "rsam_reads_free", "rsam_map", "rsam_map_files",
     "rsam_set_sam_digest", "rsam_add_devices", "rsam_kernel_stats", "rsam_reset_kernel_stats", "rsam_engine_name", "rsam_last_error",
+    "rsam_part_count", "rsam_part_plan", "rsam_map_files_part",
 ]
 
 _LIBS: dict = {}
@@ -82,8 +96,39 @@ def load(path: str = PRODUCT_LIB) -> C.CDLL:
     lib.rsam_engine_name.restype = cp
     lib.rsam_engine_name.argtypes = [vp]
     lib.rsam_last_error.restype = cp
+    u64p = C.POINTER(C.c_uint64)
+    lib.rsam_part_count.argtypes = [cp, i32, i32, i32, u64p]
+    lib.rsam_part_plan.argtypes = [cp, cp, i32, i32, i32, u64p, u64p, i32, C.POINTER(Part)]
+    lib.rsam_map_files_part.argtypes = [vp, cp, cp, C.POINTER(Part), i32, cp, C.POINTER(_Stats)]
     _LIBS[path] = lib
     return lib
+
+
+def part_count(path, rank: int, world: int, threads: int = 8, lib_path: str = PRODUCT_LIB) -> list:
+    """Newline counts of rank's PART_BLOCKS byte blocks of `path` (rsam_part_count)."""
+    lib = load(lib_path)
+    out = (C.c_uint64 * PART_BLOCKS)()
+    if lib.rsam_part_count(str(path).encode(), rank, world, threads, out) != 0:
+        raise RuntimeError(f"rsam_part_count: {lib.rsam_last_error().decode()}")
+    return list(out)
+
+
+def part_plan(fq1, fq2, rank: int, world: int, chunk_size: int = 10000, counts1=None, counts2=None,
+              threads: int = 8, lib_path: str = PRODUCT_LIB) -> Part:
+    """Rank's part of the input (rsam_part_plan); counts: all world * PART_BLOCKS block counts
+    of each file (rank-major, e.g. all-gathered part_count results) or None to count here."""
+    lib = load(lib_path)
+    def arr(c):
+        if c is None:
+            return None
+        if len(c) != world * PART_BLOCKS:
+            raise ValueError("expected world * PART_BLOCKS counts")
+        return (C.c_uint64 * len(c))(*[int(x) for x in c])
+    part = Part()
+    if lib.rsam_part_plan(str(fq1).encode(), str(fq2).encode() if fq2 else None, rank, world, chunk_size,
+                          arr(counts1), arr(counts2), threads, C.byref(part)) != 0:
+        raise RuntimeError(f"rsam_part_plan: {lib.rsam_last_error().decode()}")
+    return part
 
 
 @dataclass
@@ -201,6 +246,17 @@ class Mapper:
                                       str(sam_path).encode() if sam_path else None, C.byref(st))
         if rc != 0:
             raise RuntimeError(f"rsam_map_files: {self._lib.rsam_last_error().decode()}")
+        return MapStats(**{f: getattr(st, f) for f, _ in _Stats._fields_})
+
+    def map_files_part(self, fq1, fq2, part: Part, threads=8, sam_path=None) -> MapStats:
+        """A rank's part of one input (rsam_map_files_part): its chunks' SAM records to
+        sam_path (rank 0: header first); the parts in rank order are the one-process SAM."""
+        st = _Stats()
+        rc = self._lib.rsam_map_files_part(self._h, str(fq1).encode(), str(fq2).encode() if fq2 else None,
+                                           C.byref(part), threads, str(sam_path).encode() if sam_path else None,
+                                           C.byref(st))
+        if rc != 0:
+            raise RuntimeError(f"rsam_map_files_part: {self._lib.rsam_last_error().decode()}")
         return MapStats(**{f: getattr(st, f) for f, _ in _Stats._fields_})
 
     def set_sam_digest(self, on: bool):

@@ -11,6 +11,37 @@ from __future__ import annotations
 STAT_FIELDS = ("n_reads", "sam_bytes", "sw_calls", "tried", "nam_rescue", "mate_rescue", "inconsistent")
 
 
+def plan_shared_input(fq1, fq2, chunk_size: int, threads: int, device="cpu", lib_path=None):
+    """This rank's part of ONE input pair mapped by every rank (rsam_part_*):
+    each rank counts the newlines of its own 1/world of each file, the counts are
+    all-gathered (world * 64 integers per file, the only exchange before mapping), and
+    the plan follows.  Without a process group: the whole input as one part."""
+    import torch
+    import torch.distributed as dist
+    from . import mapper
+    kw = {"lib_path": lib_path} if lib_path else {}
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return mapper.part_plan(fq1, fq2, 0, 1, chunk_size, None, None, threads, **kw)
+    rank, world = dist.get_rank(), dist.get_world_size()
+    files = [f for f in (fq1, fq2) if f]
+    mine = torch.tensor([c for f in files for c in mapper.part_count(f, rank, world, threads, **kw)],
+                        dtype=torch.int64, device=device)
+    got = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(got, mine)
+    rows = [g.cpu().tolist() for g in got]
+    B = mapper.PART_BLOCKS
+    counts = [[c for r in rows for c in r[i * B:(i + 1) * B]] for i in range(len(files))]
+    return mapper.part_plan(fq1, fq2, rank, world, chunk_size, counts[0], counts[1] if fq2 else None, threads, **kw)
+
+
+def shared_set_first(read_set: int, rank: int, world: int, pairs_per_rank: int) -> int:
+    """First synthetic pair of rank `rank`'s slice of read set `read_set`: set s is pairs
+    [s*world*P, (s+1)*world*P), written as ONE FASTQ pair with the ranks' slices in rank
+    order, so rank r's part (chunks [r*C/W, (r+1)*C/W) when P is a multiple of the chunk
+    size) is exactly its slice."""
+    return (read_set * world + rank) * pairs_per_rank
+
+
 def first_pair(rank: int, step: int, total_steps: int, pairs_per_step: int) -> int:
     """Index of the first synthetic pair rank `rank` maps in step `step`.
     Ranges of different (rank, step) never overlap."""

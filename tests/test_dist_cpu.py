@@ -88,3 +88,66 @@ def test_two_rank_sharding_gloo():
     for r in range(2):
         assert _map_shard(m, r, 1).sam_hash == res[r][0][1]
     m.close()
+
+
+# ---- one shared input over the ranks (rank/world mode, rsam_map_files_part) ------
+PART = dict(pairs=2600, chunk=300)
+
+
+def _part_worker(rank, world, port, fq1, fq2, out_dir, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    from rabbitsalign_amd import mapper, shard
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = mapper.Mapper.synthetic(CFG["seed"], CFG["ref_len"], CFG["contigs"], CFG["L"], threads=2,
+                                    lib_path=REF_CPU_LIB)
+        part = shard.plan_shared_input(fq1, fq2, PART["chunk"], threads=2, lib_path=REF_CPU_LIB)
+        sam = os.path.join(out_dir, f"part{rank}.sam")
+        st = m.map_files_part(fq1, fq2, part, threads=2, sam_path=sam)
+        wall, tot = shard.reduce_run(1.0, {f: getattr(st, f) for f in shard.STAT_FIELDS}, device="cpu")
+        q.put((rank, part.as_dict(), tot))
+        m.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.skipif(not os.path.exists(REF_CPU_LIB), reason="CPU-path library not built")
+def test_two_rank_shared_input_gloo(tmp_path):
+    """Two ranks map ONE FASTQ pair: each counts its half of each file, the counts are
+    all-gathered over gloo, each maps its chunks into its own SAM part.  Header + parts in
+    rank order == the single-process SAM of the same files, byte for byte; the summed
+    statistics == the single process's."""
+    import torch.multiprocessing as mp
+    from rabbitsalign_amd import mapper, shard
+    m = mapper.Mapper.synthetic(CFG["seed"], CFG["ref_len"], CFG["contigs"], CFG["L"], threads=2,
+                                lib_path=REF_CPU_LIB)
+    reads = m.synthetic_reads(7, 0, PART["pairs"], CFG["L"], 300.0, 30.0, True)
+    fq1, fq2 = str(tmp_path / "r1.fq"), str(tmp_path / "r2.fq")
+    reads.write_fastq(fq1, fq2)
+    reads.close()
+    one = str(tmp_path / "one.sam")
+    st1 = m.map_files(fq1, fq2, threads=2, chunk_size=PART["chunk"], sam_path=one)
+    m.close()
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_part_worker, args=(r, 2, port, fq1, fq2, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        rank, part, tot = q.get(timeout=600)
+        res[rank] = (part, tot)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n_chunks = (PART["pairs"] + PART["chunk"] - 1) // PART["chunk"]
+    assert res[0][0]["first_chunk"] == 0 and res[0][0]["end_chunk"] == res[1][0]["first_chunk"]
+    assert res[1][0]["end_chunk"] == n_chunks and res[1][0]["first_chunk"] > 0
+    parts = b"".join(open(tmp_path / f"part{r}.sam", "rb").read() for r in range(2))
+    assert parts == open(one, "rb").read()
+    for r in range(2):
+        assert res[r][1]["n_reads"] == st1.n_reads
+        assert all(res[r][1][f] == getattr(st1, f) for f in shard.STAT_FIELDS)
