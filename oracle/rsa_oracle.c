@@ -847,16 +847,20 @@ static int banded_sw(const int8_t* ref, const int8_t* read, int ref_len, int rea
     return l;
 }
 
-/* ssw_align (ssw.c:818-922) with flag 0x0f, filters 0, filterd 32767 */
-void ora_ssw_align(const int8_t* q, int qlen, const int8_t* r, int rlen, int match, int mismatch,
-                   int gap_open, int gap_extend, ora_ssw_res* res, uint32_t* cigar) {
+/* ssw_align (ssw.c:818-922) with flag 0x0f, filters 0, filterd 32767;
+ * force_word: the word layout whatever the byte pass scores (the scan kernel's
+ * certified path, ora_scan_certificate) */
+static void ssw_align_impl(const int8_t* q, int qlen, const int8_t* r, int rlen, int match, int mismatch,
+                           int gap_open, int gap_extend, ora_ssw_res* res, uint32_t* cigar, int force_word) {
     res->ref_begin1 = -1; res->read_begin1 = -1; res->flag = 0; res->n_cigar = 0;
     /* byte mode first (16 stripes, end_ref starts at -1); a max >= 255-bias
      * (bias = mismatch) overflows and the word kernel (8 stripes, end_ref
      * starts at 0) recomputes everything (ssw.c:838-850) */
     int word = 0;
-    ora_end fwd = sw_scan(r, 0, rlen, q, qlen, match, mismatch, gap_open, gap_extend, 0, -1, (qlen + 15) / 16);
-    if (fwd.score + mismatch >= 255) {
+    ora_end fwd = {0, -1, 0};
+    if (!force_word)
+        fwd = sw_scan(r, 0, rlen, q, qlen, match, mismatch, gap_open, gap_extend, 0, -1, (qlen + 15) / 16);
+    if (force_word || fwd.score + mismatch >= 255) {
         word = 1;
         fwd = sw_scan(r, 0, rlen, q, qlen, match, mismatch, gap_open, gap_extend, 0, 0, (qlen + 7) / 8);
     }
@@ -887,6 +891,41 @@ void ora_ssw_align(const int8_t* q, int qlen, const int8_t* r, int rlen, int mat
     free(rbuf);
     if (n < 0) res->flag = 1;
     else res->n_cigar = n;
+}
+
+void ora_ssw_align(const int8_t* q, int qlen, const int8_t* r, int rlen, int match, int mismatch,
+                   int gap_open, int gap_extend, ora_ssw_res* res, uint32_t* cigar) {
+    ssw_align_impl(q, qlen, r, rlen, match, mismatch, gap_open, gap_extend, res, cigar, 0);
+}
+
+/* The scan kernel's certificate (k_ext_scan_v).  SSW scores a job in
+ * the byte layout and switches to the word layout when the byte max saturates
+ * (score + bias >= 255, bias = mismatch, ssw.c:838-850).  The kernel runs the word
+ * layout first and takes its result without the byte pass when the word score
+ * reaches that bound AND the band path of the word result (banded_sw's traceback,
+ * ssw.c:590-774) has no insertion next to a deletion: the two layouts differ only
+ * where a cross-stripe F would open an E gap (an I directly followed by a D), so
+ * such a path scores at least as high in the byte layout, whose max then saturates.
+ * Returns 0: word score below the bound (not a candidate); 1: the path has an I
+ * next to a D (the kernel re-runs the job exactly); 2: certified, and the byte
+ * layout does saturate; -1: certified but the byte layout does not saturate (a
+ * counterexample to the argument). */
+int ora_scan_certificate(const int8_t* q, int qlen, const int8_t* r, int rlen, int match, int mismatch,
+                         int gap_open, int gap_extend) {
+    ora_end w = sw_scan(r, 0, rlen, q, qlen, match, mismatch, gap_open, gap_extend, 0, 0, (qlen + 7) / 8);
+    if (w.score + mismatch < 255) return 0;
+    uint32_t* cig = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(2 * (qlen + rlen) + 16));
+    ora_ssw_res res;
+    ssw_align_impl(q, qlen, r, rlen, match, mismatch, gap_open, gap_extend, &res, cig, 1);
+    int adjacent = res.flag != 0;              /* a failed band pass is re-run as well */
+    for (int i = 0; !adjacent && i + 1 < res.n_cigar; ++i) {
+        const uint32_t a = cig[i] & 0xf, b = cig[i + 1] & 0xf;
+        adjacent = (a == 1 && b == 2) || (a == 2 && b == 1);
+    }
+    free(cig);
+    if (adjacent) return 1;
+    ora_end b = sw_scan(r, 0, rlen, q, qlen, match, mismatch, gap_open, gap_extend, 0, -1, (qlen + 15) / 16);
+    return b.score + mismatch >= 255 ? 2 : -1;
 }
 
 /* TranslateBase with kBaseTranslation (ssw_cpp.cpp:12-25, 352-363):

@@ -95,6 +95,12 @@ typedef struct ora_ssw_res {    /* s_align (ssw.h) fields used by the C++ wrappe
 void ora_ssw_align(const int8_t* q, int qlen, const int8_t* r, int rlen, int match, int mismatch,
                    int gap_open, int gap_extend, ora_ssw_res* res, uint32_t* cigar);
 
+/* the scan kernel's word-result certificate on one job (rsa_oracle.c): 0 not a
+ * candidate, 1 path with an I next to a D, 2 certified and the byte layout saturates,
+ * -1 certified but it does not (a counterexample) */
+int ora_scan_certificate(const int8_t* q, int qlen, const int8_t* r, int rlen, int match, int mismatch,
+                         int gap_open, int gap_extend);
+
 typedef struct ora_aln_info {   /* AlignmentInfo (aligner.hpp:20-30) */
     uint32_t edit_distance, ref_start, ref_end, query_start, query_end;
     int32_t sw_score;
