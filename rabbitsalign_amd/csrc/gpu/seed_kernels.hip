@@ -1626,40 +1626,78 @@ k_rescue_big(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __rest
 // the tile's scan (a thread walking a private run of reads waited on one
 // dependent load per read: 142 us a call).
 #define SEED_NSTAT 14
-#define SS_TPB 256           // one workgroup of 4 waves: it finds a CU sooner on a busy GPU than 16 waves did
-#define SS_PER 16            // reads a thread takes per tile (tiles of SS_TPB * SS_PER = 4096 reads)
+// Final NAM offsets (exclusive scan of the per-read NAM counts) and the call's 14
+// statistics, in two launches: k_seed_count -- one read a thread, a workgroup of SS_TPB
+// reads -- scans within its workgroup, writes the workgroup's NAM total and adds its
+// statistics to the header (14 atomics a workgroup); k_seed_scan (one workgroup) scans
+// the totals into workgroup offsets; k_compact adds its read's workgroup offset and
+// writes the final offset.  (The single-workgroup scan this replaces walked the batch
+// in serial tiles: 89 us a call of 20000 reads; with the statistics summed in
+// k_seed_scan instead, one serial load chain cost it 21 us.)
+#define SS_TPB 256
 #define SS_WAVES (SS_TPB / 64)
 __global__ void __launch_bounds__(SS_TPB)
-k_seed_scan(int n_reads, const uint8_t* __restrict__ rescued, const uint32_t* __restrict__ ncnt1,
-            const uint32_t* __restrict__ ncnt2, const uint32_t* __restrict__ qcnt, const ReadStat* __restrict__ st,
-            uint64_t* __restrict__ ooff, SeedHdr* __restrict__ hdr) {
-    __shared__ uint64_t s_w[SS_WAVES];
+k_seed_count(int n_reads, const uint8_t* __restrict__ rescued, const uint32_t* __restrict__ ncnt1,
+             const uint32_t* __restrict__ ncnt2, const uint32_t* __restrict__ qcnt, const ReadStat* __restrict__ st,
+             uint32_t* __restrict__ loc, uint64_t* __restrict__ bsum, SeedHdr* __restrict__ hdr) {
+    __shared__ uint32_t s_w[SS_WAVES];
     __shared__ unsigned long long s_stat[SEED_NSTAT];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int r = blockIdx.x * SS_TPB + t;
     if (t < SEED_NSTAT) s_stat[t] = 0;
     uint64_t v[SEED_NSTAT] = {0};    // qrs found good hits_find hits_all scan_find scan_all n1 n2 rr rq rscan rhits qw_q
-    uint64_t carry = 0;
-    for (int base = 0; base < n_reads; base += SS_TPB * SS_PER) {
-        const int r0 = base + t * SS_PER;
-        uint32_t cnt[SS_PER];
-        uint64_t mine = 0;
+    uint32_t cnt = 0;
+    if (r < n_reads) {
+        const bool rs = rescued[r] != 0;
+        const uint32_t c1 = ncnt1[r], c2 = rs ? ncnt2[r] : 0, q = qcnt[r];
+        const ReadStat x = st[r];
+        cnt = rs ? c2 : c1;
+        v[0] = q; v[1] = x.found; v[2] = x.good; v[3] = x.hits_find; v[4] = x.hits_all;
+        v[5] = x.scan_find; v[6] = x.scan_all; v[7] = c1; v[8] = c2;
+        if (rs) { v[9] = 1; v[10] = q; v[11] = x.scan_all; v[12] = x.hits_all; }
+        if (x.qw) v[13] = q;
+    }
+    uint32_t x = cnt;                            // wave inclusive scan
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();                             // s_stat zeroed, s_w written
+    uint32_t wpre = 0, tot = 0;
 #pragma unroll
-        for (int j = 0; j < SS_PER; ++j) {
-            const int r = r0 + j;
-            cnt[j] = 0;
-            if (r < n_reads) {
-                const bool rs = rescued[r] != 0;
-                const uint32_t c1 = ncnt1[r], c2 = rs ? ncnt2[r] : 0, q = qcnt[r];
-                const ReadStat x = st[r];
-                cnt[j] = rs ? c2 : c1;
-                v[0] += q; v[1] += x.found; v[2] += x.good; v[3] += x.hits_find; v[4] += x.hits_all;
-                v[5] += x.scan_find; v[6] += x.scan_all; v[7] += c1; v[8] += c2;
-                if (rs) { v[9] += 1; v[10] += q; v[11] += x.scan_all; v[12] += x.hits_all; }
-                if (x.qw) v[13] += q;
-            }
-            mine += cnt[j];
-        }
-        uint64_t x = mine;                       // wave inclusive scan of the threads' sums
+    for (int j = 0; j < SS_WAVES; ++j) {
+        wpre += j < w ? s_w[j] : 0;
+        tot += s_w[j];
+    }
+    if (r < n_reads) loc[r] = wpre + x - cnt;
+#pragma unroll
+    for (int k = 0; k < SEED_NSTAT; ++k) {       // wave sums, one LDS atomic a wave
+        uint64_t a = v[k];
+        for (int o = 32; o >= 1; o >>= 1) a += __shfl_xor(a, o, 64);
+        if (lane == 0 && a) atomicAdd(&s_stat[k], (unsigned long long)a);
+    }
+    __syncthreads();
+    if (t == 0) bsum[blockIdx.x] = tot;
+    if (t < SEED_NSTAT && s_stat[t]) {
+        // qrs found good hits_find hits_all scan_find scan_all n1 n2 resc_reads resc_q resc_scan resc_hits qw_q
+        unsigned long long* dst[SEED_NSTAT] = {&hdr->qrs, &hdr->found, &hdr->good, &hdr->hits_find, &hdr->hits_all,
+                                               &hdr->scan_find, &hdr->scan_all, &hdr->n1, &hdr->n2, &hdr->resc_reads,
+                                               &hdr->resc_q, &hdr->resc_scan, &hdr->resc_hits, &hdr->qw_q};
+        atomicAdd(dst[t], s_stat[t]);
+    }
+}
+
+__global__ void __launch_bounds__(SS_TPB)
+k_seed_scan(int n_blocks, int n_reads, uint64_t* __restrict__ bsum, uint64_t* __restrict__ ooff,
+            SeedHdr* __restrict__ hdr) {
+    __shared__ uint64_t s_w[SS_WAVES];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint64_t carry = 0;
+    for (int base = 0; base < n_blocks; base += SS_TPB) {   // block totals -> exclusive block offsets, in place
+        const int b = base + t;
+        const uint64_t mine = b < n_blocks ? bsum[b] : 0;
+        uint64_t x = mine;
         for (int o = 1; o < 64; o <<= 1) {
             const uint64_t y = __shfl_up(x, o, 64);
             if (lane >= o) x += y;
@@ -1669,29 +1707,16 @@ k_seed_scan(int n_reads, const uint8_t* __restrict__ rescued, const uint32_t* __
         uint64_t wpre = 0, tot = 0;
 #pragma unroll
         for (int j = 0; j < SS_WAVES; ++j) {
-            const uint64_t sj = s_w[j];
-            wpre += j < w ? sj : 0;
-            tot += sj;
+            wpre += j < w ? s_w[j] : 0;
+            tot += s_w[j];
         }
-        uint64_t off = carry + wpre + x - mine;
-#pragma unroll
-        for (int j = 0; j < SS_PER; ++j) {
-            if (r0 + j < n_reads) ooff[r0 + j] = off;
-            off += cnt[j];
-        }
+        if (b < n_blocks) bsum[b] = carry + wpre + x - mine;
         carry += tot;
-        __syncthreads();                         // s_w is rewritten by the next tile
+        __syncthreads();
     }
-    for (int k = 0; k < SEED_NSTAT; ++k)
-        if (v[k]) atomicAdd(&s_stat[k], (unsigned long long)v[k]);
-    __syncthreads();
     if (t == 0) {
         ooff[n_reads] = carry;
         hdr->total = carry;
-        hdr->qrs = s_stat[0]; hdr->found = s_stat[1]; hdr->good = s_stat[2]; hdr->hits_find = s_stat[3];
-        hdr->hits_all = s_stat[4]; hdr->scan_find = s_stat[5]; hdr->scan_all = s_stat[6]; hdr->n1 = s_stat[7];
-        hdr->n2 = s_stat[8]; hdr->resc_reads = s_stat[9]; hdr->resc_q = s_stat[10]; hdr->resc_scan = s_stat[11];
-        hdr->resc_hits = s_stat[12]; hdr->qw_q = s_stat[13];
     }
 }
 
@@ -1705,48 +1730,6 @@ k_seed_scan(int n_reads, const uint8_t* __restrict__ rescued, const uint32_t* __
 // stable by descending score, so NAM i goes to its rank: the NAMs scoring
 // higher, plus the equal ones before it.  One wave a read, scores by shuffle.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(64)
-k_compact(int n_reads, const uint64_t* __restrict__ nsrc, const uint64_t* __restrict__ rbase,
-          uint64_t arena_base, const uint32_t* __restrict__ ncnt1, const uint32_t* __restrict__ ncnt2,
-          const uint8_t* __restrict__ rescued, const rsa_nam* __restrict__ arena,
-          const uint64_t* __restrict__ ooff, uint64_t cap, rsa_nam* __restrict__ out,
-          uint32_t* __restrict__ nam_read, int by_score) {
-    const int r = blockIdx.x;
-    if (r >= n_reads) return;
-    const bool resc = rescued[r] != 0;
-    const rsa_nam* src = arena + (resc ? arena_base + rbase[r] : nsrc[r]);
-    const uint32_t n = resc ? ncnt2[r] : ncnt1[r];
-    const uint64_t o = ooff[r];
-    if (o + n > cap) return;
-    if (by_score && n >= 2 && n <= 16) {
-        const int i = threadIdx.x;
-        const float si = i < (int)n ? src[i].score : 0.0f;
-        int rank = 0;
-        for (int j = 0; j < (int)n; ++j) {
-            const float sj = __shfl(si, j, 64);
-            rank += (sj > si || (sj == si && j < i)) ? 1 : 0;
-        }
-        if (i < (int)n) {
-            out[o + rank] = src[i];
-            if (nam_read) nam_read[o + rank] = (uint32_t)r;
-        }
-        return;
-    }
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        out[o + i] = src[i];
-        if (nam_read) nam_read[o + i] = (uint32_t)r;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_sites: per-NAM site checks (SURVEY.md §8 f1), 16 lanes per final NAM.
-// reverse_nam_if_needed (src/aln.cpp:60-93): the NAM's first and last k-mers
-// against the reference, as is or with the read reversed; then, for the
-// (reversed) NAM, extend_seed_part's test (aln.cpp:374-431): a read-length
-// projection gets its Hamming distance and, when hd / len < 0.05 (float
-// quotient, double compare), its mismatch positions.  The host then builds
-// hamming_align's result without touching the reference.
-// ---------------------------------------------------------------------------
 // complement of src/revcomp.hpp:10-27 (A/C/G/T/U either case, all else N)
 __device__ __forceinline__ unsigned char rc_base(unsigned char c) {
     switch (c) {
@@ -1758,12 +1741,81 @@ __device__ __forceinline__ unsigned char rc_base(unsigned char c) {
     }
 }
 
+// What k_sites needs of a final NAM besides the NAM: where its read and its contig
+// lie, and the slot of its site check (its read's list start + nam_id).  k_compact
+// writes it with the NAM, so k_sites starts with one round of loads, not three.
+struct SiteDesc {
+    uint64_t read_off;        // the read in the call's sequence buffer
+    uint64_t ref_off;         // the NAM's contig in the resident reference
+    uint64_t slot;            // sites[] index; ~0: nam_id outside its read's list (a broken permutation)
+    uint32_t read_len, ref_len;
+};
+
+__global__ void __launch_bounds__(64)
+k_compact(int n_reads, const uint64_t* __restrict__ nsrc, const uint64_t* __restrict__ rbase,
+          uint64_t arena_base, const uint32_t* __restrict__ ncnt1, const uint32_t* __restrict__ ncnt2,
+          const uint8_t* __restrict__ rescued, const rsa_nam* __restrict__ arena, const uint32_t* __restrict__ loc,
+          const uint64_t* __restrict__ boff, uint64_t* __restrict__ ooff, uint64_t cap, rsa_nam* __restrict__ out,
+          SiteDesc* __restrict__ desc, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
+          const uint64_t* __restrict__ coff, const char* __restrict__ seq, char* __restrict__ seq_rc, int by_score) {
+    const int r = blockIdx.x;
+    if (r >= n_reads) return;
+    const bool resc = rescued[r] != 0;
+    const rsa_nam* src = arena + (resc ? arena_base + rbase[r] : nsrc[r]);
+    const uint32_t n = resc ? ncnt2[r] : ncnt1[r];
+    const uint64_t o = boff[r / SS_TPB] + loc[r];          // k_seed_count + k_seed_scan
+    if (threadIdx.x == 0) ooff[r] = o;
+    if (desc && n) {                                         // the read's reverse complement for k_sites
+        const uint64_t ro = roff[r];
+        const uint32_t len = rlen[r];
+        for (uint32_t i = threadIdx.x; i < len; i += blockDim.x)
+            seq_rc[ro + i] = (char)rc_base((unsigned char)seq[ro + len - 1 - i]);
+    }
+    if (o + n > cap) return;
+    auto put = [&](uint64_t at, const rsa_nam& x) {
+        out[at] = x;
+        if (!desc) return;
+        SiteDesc d;
+        d.read_off = roff[r];
+        d.read_len = rlen[r];
+        const uint64_t c0 = coff[x.ref_id];
+        d.ref_off = c0;
+        d.ref_len = (uint32_t)(coff[x.ref_id + 1] - c0);
+        d.slot = (x.nam_id >= 0 && (uint32_t)x.nam_id < n) ? o + (uint64_t)x.nam_id : ~0ull;
+        desc[at] = d;
+    };
+    if (by_score && n >= 2 && n <= 16) {
+        const int i = threadIdx.x;
+        const float si = i < (int)n ? src[i].score : 0.0f;
+        int rank = 0;
+        for (int j = 0; j < (int)n; ++j) {
+            const float sj = __shfl(si, j, 64);
+            rank += (sj > si || (sj == si && j < i)) ? 1 : 0;
+        }
+        if (i < (int)n) put(o + rank, src[i]);
+        return;
+    }
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) put(o + i, src[i]);
+}
+
+// ---------------------------------------------------------------------------
+// k_sites: per-NAM site checks (SURVEY.md §8 f1), 16 lanes per final NAM.
+// reverse_nam_if_needed (src/aln.cpp:60-93): the NAM's first and last k-mers
+// against the reference, as is or with the read reversed; then, for the
+// (reversed) NAM, extend_seed_part's test (aln.cpp:374-431): a read-length
+// projection gets its Hamming distance and, when hd / len < 0.05 (float
+// quotient, double compare), its mismatch positions.  The host then builds
+// hamming_align's result without touching the reference.
+// ---------------------------------------------------------------------------
+
+// a read and its reverse complement (k_compact writes the latter into the call's rc
+// buffer, at the read's offset)
 struct SiteRead {
     const char* s;
+    int64_t rc_delta;          // rc buffer - read buffer (the same for every read of a call)
     int64_t len;
-    __device__ __forceinline__ unsigned char at(bool rc, int64_t i) const {
-        return rc ? rc_base((unsigned char)s[len - 1 - i]) : (unsigned char)s[i];
-    }
+    __device__ __forceinline__ const char* side(bool rc) const { return s + (rc ? rc_delta : 0); }
+    __device__ __forceinline__ unsigned char at(bool rc, int64_t i) const { return (unsigned char)side(rc)[i]; }
 };
 
 // 16 lanes per NAM, 4 NAMs per wave: a lane compares every 16th byte and the
@@ -1782,50 +1834,38 @@ __device__ bool site_kmer_eq(const char* ref, int64_t rlen, int64_t rpos, const 
     const uint64_t ra = rp > (uint64_t)rlen ? (uint64_t)rlen : rp, qa = qp > (uint64_t)rd.len ? (uint64_t)rd.len : qp;
     const uint64_t rl = min((uint64_t)k, (uint64_t)rlen - ra), ql = min((uint64_t)k, (uint64_t)rd.len - qa);
     bool bad = rl != ql;
-    for (uint64_t j = l16; j < rl && !bad; j += 16)
-        bad = (unsigned char)ref[ra + j] != rd.at(rc, (int64_t)(qa + j));
+    if (!bad)                                  // every byte's load issued before any compare
+        for (uint64_t j = l16; j < rl; j += 16) bad |= (unsigned char)ref[ra + j] != rd.at(rc, (int64_t)(qa + j));
     return grp_ballot(bad) == 0;
 }
 
 // Mismatch mask of one lane's 16 window positions x0 .. x0 + 15 (bit b: x0 + b < n and the
 // reference byte differs from the oriented read byte).  The group's 16 lanes cover 256
-// positions, so a read of <= 256 bp takes one round of loads instead of one per 16
-// positions.  Both sides come by five aligned dword loads: the window lies inside its
-// contig and the reference buffer has 64 bytes of padding past the last one; the read
-// buffer has SEQ_PAD bytes of padding before the first read and after the last.
-__device__ __forceinline__ uint32_t rc_byte4(uint32_t w) {     // rc_base on each byte
-    uint32_t o = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        const uint32_t u = (w >> (8 * b)) & 0xDFu;             // upper case (only letters reach A/C/G/T/U)
-        const uint32_t c = u == 'A' ? 'T' : u == 'C' ? 'G' : u == 'G' ? 'C' : (u == 'T' || u == 'U') ? 'A' : 'N';
-        o |= c << (8 * b);
-    }
-    return o;
-}
+// positions, so a read of <= 256 bp takes one round of loads.  Each side is two aligned
+// 16-byte loads and a byte funnel: the window lies inside its contig and the reference
+// buffer has 64 bytes of padding past the last one; the read buffer has SEQ_PAD bytes
+// of padding before the first read and after the last.
 __device__ __forceinline__ void load16(const char* p, uint32_t out[4]) {   // bytes p[0 .. 16), any alignment
     const uintptr_t a = (uintptr_t)p;
-    const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)(a & 3);
-    uint32_t d[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) d[k] = w[k];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) out[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+    const uint4* q = (const uint4*)(a & ~(uintptr_t)15);
+    const uint4 x = q[0], y = q[1];
+    const bool w2 = (a & 8) != 0, w1 = (a & 4) != 0;
+    const uint32_t sh = (uint32_t)a & 3u;
+    // words (a >> 2) & 3 .. + 4 of the 32 loaded bytes: shift by two words, then by one
+    const uint32_t t0 = w2 ? x.z : x.x, t1 = w2 ? x.w : x.y, t2 = w2 ? y.x : x.z, t3 = w2 ? y.y : x.w,
+                   t4 = w2 ? y.z : y.x, t5 = w2 ? y.w : y.y;
+    const uint32_t u0 = w1 ? t1 : t0, u1 = w1 ? t2 : t1, u2 = w1 ? t3 : t2, u3 = w1 ? t4 : t3, u4 = w1 ? t5 : t4;
+    out[0] = __builtin_amdgcn_alignbyte(u1, u0, sh);
+    out[1] = __builtin_amdgcn_alignbyte(u2, u1, sh);
+    out[2] = __builtin_amdgcn_alignbyte(u3, u2, sh);
+    out[3] = __builtin_amdgcn_alignbyte(u4, u3, sh);
 }
 __device__ __forceinline__ uint32_t window_mask(const char* ref_win, const SiteRead& rd, bool rc, int64_t x0,
                                                 int64_t n) {
     if (x0 >= n) return 0u;
     uint32_t r[4], q[4];
     load16(ref_win + x0, r);
-    if (!rc) {
-        load16(rd.s + x0, q);
-    } else {                                   // q byte b = rc_base(s[n - 1 - (x0 + b)])
-        uint32_t t[4];
-        load16(rd.s + (n - x0 - 16), t);       // s[n - x0 - 16 .. n - x0), reversed below
-#pragma unroll
-        for (int k = 0; k < 4; ++k) q[k] = rc_byte4(__builtin_bswap32(t[3 - k]));
-    }
+    load16(rd.side(rc) + x0, q);
     uint32_t m = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1838,9 +1878,8 @@ __device__ __forceinline__ uint32_t window_mask(const char* ref_win, const SiteR
 }
 
 // reads over 1024 bp: masks past the four kept in registers, out of line
-__device__ __attribute__((noinline)) uint32_t window_mask_far(const char* ref_win, const char* s, int64_t len, bool rc,
-                                                              int64_t x0) {
-    return window_mask(ref_win, SiteRead{s, len}, rc, x0, len);
+__device__ __forceinline__ uint32_t window_mask_far(const char* ref_win, const SiteRead& rd, bool rc, int64_t x0) {
+    return window_mask(ref_win, rd, rc, x0, rd.len);
 }
 
 // sums / exclusive prefix sums over a 16-lane group
@@ -1859,32 +1898,55 @@ __device__ __forceinline__ uint32_t grp_excl_scan(uint32_t v, int l16) {
     return x - v;
 }
 
-__global__ void __launch_bounds__(256)
-k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read, SeedHdr* __restrict__ err_hdr,
-        uint64_t cap, const uint64_t* __restrict__ ooff, const char* __restrict__ seq, const uint64_t* __restrict__ roff,
-        const uint32_t* __restrict__ rlen, SeedIndexParams p, rsa_nam_site* __restrict__ sites,
+// 16 lanes a NAM, SITES_BLOCK NAMs a block, a fixed grid walking the batch's NAMs.  A
+// NAM's loads come in two rounds: the NAM with its descriptor (k_compact), then --
+// together -- the two k-mers of the orientation test and the read-length window of
+// the NAM as it stands (the common outcome, aln.cpp:60-93 finds most NAMs consistent
+// as they are); a reversed NAM loads its window again.  Pool space is taken with one
+// atomic a block: same-address atomics from every wave serialise (one a wave made the
+// kernel 2.7x slower than one a 16-NAM block, profiles/r05/sites_ab).
+#define SITES_BLOCK 16
+// waves a SIMD the register budget is sized for (RSA_SITES_WAVES at build time: 5 = 92
+// VGPRs, what the compiler picks unasked; 6 = 80 with a few spills, 8 = 64 with more)
+#ifndef RSA_SITES_WAVES
+#define RSA_SITES_WAVES 5
+#endif
+__global__ void __launch_bounds__(16 * SITES_BLOCK) __attribute__((amdgpu_waves_per_eu(RSA_SITES_WAVES)))
+k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, SeedHdr* __restrict__ err_hdr,
+        uint64_t cap, const char* __restrict__ seq, const char* __restrict__ seq_rc, SeedIndexParams p,
+        rsa_nam_site* __restrict__ sites,
         uint16_t* __restrict__ pool, uint64_t pool_cap, unsigned long long* __restrict__ pool_used, int ham,
         int h_match, int h_mismatch, int h_bonus) {
-    __shared__ uint32_t s_need[16], s_base[16];
-    __shared__ unsigned long long s_at;
     // a batch whose NAMs overflow the output was not compacted whole (k_compact skips
-    // the reads past `cap`, so their nam_read entries were never written): no site
-    // checks then -- the host reports RSA_ERR_CAPACITY and the caller asks again
+    // the reads past `cap`, so their descriptors were never written): no site checks
+    // then -- the host reports RSA_ERR_CAPACITY and the caller asks again
+    __shared__ uint32_t s_need[SITES_BLOCK], s_base[SITES_BLOCK];
+    __shared__ unsigned long long s_at;
     const uint64_t total = (uint64_t)err_hdr->total <= cap ? (uint64_t)err_hdr->total : 0;
     const int l16 = threadIdx.x & 15, grp = threadIdx.x >> 4;
-    // a fixed grid walks the batch's NAMs, 16 a block per round (the count is known on the device only)
-    for (uint64_t blk = blockIdx.x; blk * 16 < total; blk += gridDim.x) {
-    const uint64_t g0 = blk * 16 + grp;
+    for (uint64_t blk = blockIdx.x; blk * SITES_BLOCK < total; blk += gridDim.x) {
+    const uint64_t g0 = blk * SITES_BLOCK + grp;
     const bool valid = g0 < total;
     const uint64_t g = valid ? g0 : total - 1;             // idle groups shadow the last NAM (ballots stay uniform)
-    const uint32_t r = nam_read[g];
-    const SiteRead rd{seq + roff[r], (int64_t)rlen[r]};
     const rsa_nam nam = nams[g];
-    const char* ref = p.ref + p.coff[nam.ref_id];
-    const int64_t ref_len = (int64_t)(p.coff[nam.ref_id + 1] - p.coff[nam.ref_id]);
+    const SiteDesc d = desc[g];
+    const char* ref = p.ref + d.ref_off;
+    const int64_t ref_len = (int64_t)d.ref_len;
+    const SiteRead rd{seq + d.read_off, seq_rc - seq, (int64_t)d.read_len};
     const int k = p.k;
     bool is_rc = nam.is_rc != 0;
     int64_t qs = nam.query_start, qe = nam.query_end;
+    // projected_ref_start = max(0, ref_start - query_start); projected_ref_end =
+    // min(ref_end + |read| - query_end, |contig|) (size_t arithmetic, aln.cpp:374-431)
+    auto proj = [&](int64_t q_s, int64_t q_e, int64_t& ps) {
+        ps = max((int64_t)0, (int64_t)nam.ref_start - q_s);
+        const uint64_t pe = min((uint64_t)((int64_t)nam.ref_end + rd.len - q_e), (uint64_t)ref_len);
+        return pe - (uint64_t)ps == (uint64_t)rd.len;
+    };
+    int64_t ps = 0;
+    bool hamming = proj(qs, qe, ps);
+    // the window as the NAM stands, issued with the k-mer loads below
+    uint32_t m0 = hamming ? window_mask(ref + ps, rd, is_rc, 16 * l16, rd.len) : 0u;
     uint32_t flags;
     const bool fwd_ok = site_kmer_eq(ref, ref_len, nam.ref_start, rd, is_rc, qs, k, l16) &
                         site_kmer_eq(ref, ref_len, (int64_t)nam.ref_end - k, rd, is_rc, qe - k, k, l16);
@@ -1899,58 +1961,60 @@ k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read,
             is_rc = !is_rc;
             qs = qs2;
             qe = qe2;
+            hamming = proj(qs, qe, ps);
+            m0 = hamming ? window_mask(ref + ps, rd, is_rc, 16 * l16, rd.len) : 0u;
         } else {
             flags = 2;
+            hamming = false;
         }
     }
+    const int n = (int)rd.len;
     uint32_t hd = 0, mm_off = 0;
-    uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;      // this lane's mismatch masks, positions c * 256 + 16 * l16 + b
+    uint32_t m1 = 0, m2 = 0, m3 = 0;             // this lane's masks, positions c * 256 + 16 * l16 + b
     bool want = false;
-    int64_t ps = 0;
     // the mask of chunk c (256 positions): registers for the first four, loads again beyond
-    auto mask_of = [&](int64_t c) -> uint32_t {
+    auto mask_of = [&](int c) -> uint32_t {
         if (c < 4) return c == 0 ? m0 : c == 1 ? m1 : c == 2 ? m2 : m3;
-        return window_mask_far(ref + ps, rd.s, rd.len, is_rc, 256 * c + 16 * l16);
+        return window_mask_far(ref + ps, rd, is_rc, 256 * (int64_t)c + 16 * l16);
     };
-    if (flags != 2) {
-        // projected_ref_start = max(0, ref_start - query_start); projected_ref_end =
-        // min(ref_end + |read| - query_end, |contig|) (size_t arithmetic)
-        ps = max((int64_t)0, (int64_t)nam.ref_start - qs);
-        const uint64_t pe = min((uint64_t)((int64_t)nam.ref_end + rd.len - qe), (uint64_t)ref_len);
-        if (pe - (uint64_t)ps == (uint64_t)rd.len) {
-            flags |= RSA_SITE_HAMMING;
-            // masks of the first 1024 positions stay in registers for the passes below
+    if (hamming) {
+        flags |= RSA_SITE_HAMMING;
+        hd = __popc(m0);
+        // reads over 256 bp: the masks of positions 256 .. 1023 into registers too
 #pragma nounroll
-            for (int64_t c = 0; 256 * c < rd.len; ++c) {
-                const uint32_t mc = window_mask(ref + ps, rd, is_rc, 256 * c + 16 * l16, rd.len);
-                m0 = c == 0 ? mc : m0;
-                m1 = c == 1 ? mc : m1;
-                m2 = c == 2 ? mc : m2;
-                m3 = c == 3 ? mc : m3;
-                hd += __popc(mc);
-            }
-            hd = grp_sum(hd);
-            want = (double)((float)hd / (float)rd.len) < 0.05;
+        for (int c = 1; 256 * c < n; ++c) {
+            const uint32_t mc = window_mask(ref + ps, rd, is_rc, 256 * (int64_t)c + 16 * l16, rd.len);
+            m1 = c == 1 ? mc : m1;
+            m2 = c == 2 ? mc : m2;
+            m3 = c == 3 ? mc : m3;
+            hd += __popc(mc);
         }
+        hd = grp_sum(hd);
+        want = (double)((float)hd / (float)rd.len) < 0.05;
     }
-    // pool space: a block-wide prefix over its 16 NAMs and one atomic per block (positions:
+    // the pool's u16 words hold positions and hamming_align's segment ends: longer reads
+    // leave the accepted window to the host (RSA_SITE_POOL_FULL: it recomputes it)
+    const bool fits = n <= 65535;
+    // pool space: a block-wide prefix over its NAMs and one atomic a block (positions:
     // n_mm words; hamming_align's result: a 6-word header and at most 2 n_mm + 3 ops of 2 words)
-    const uint32_t need = ham ? 12u + 4u * hd : hd;
-    if (l16 == 0) s_need[grp] = (want && valid) ? need : 0;
+    const uint32_t need = (want && valid && fits) ? (ham ? 12u + 4u * hd : hd) : 0u;
+    if (l16 == 0) s_need[grp] = need;
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t acc = 0;
-        for (int j = 0; j < 16; ++j) { s_base[j] = acc; acc += s_need[j]; }
+        for (int j = 0; j < SITES_BLOCK; ++j) { s_base[j] = acc; acc += s_need[j]; }
         s_at = acc ? atomicAdd(pool_used, (unsigned long long)acc) : 0ull;
     }
     __syncthreads();
     if (want) {
         const unsigned long long at = s_at + s_base[grp];
-        if (at + need <= pool_cap && !ham) {
+        if (!fits || at + need > pool_cap) {
+            flags |= RSA_SITE_POOL_FULL;
+        } else if (!ham) {
             flags |= RSA_SITE_POSITIONS;
             mm_off = (uint32_t)at;
             uint32_t m = 0;
-            for (int64_t c = 0; 256 * c < rd.len && m < hd; ++c) {
+            for (int c = 0; 256 * c < n && m < hd; ++c) {
                 uint32_t bits = mask_of(c);
                 const uint32_t cnt = __popc(bits);
                 uint32_t o = m + grp_excl_scan(cnt, l16);
@@ -1962,25 +2026,24 @@ k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read,
                 }
                 m += grp_sum(cnt);
             }
-        } else if (at + need <= pool_cap) {
+        } else {
             // hamming_align (aligner.cpp:219-302) over the window just tested: the group walks
             // the mismatch positions in order (16-base ballots) twice, every lane computing the
             // same values; lane 0 writes the result
             flags |= RSA_SITE_POSITIONS | RSA_SITE_ALIGNED;
             mm_off = (uint32_t)at;
-            const int64_t n = rd.len;
             // 1. highest_scoring_segment (aligner.cpp:219-252), run by run: between mismatches
             //    the score only grows, so each run of matches needs one check at its end
-            int64_t start = 0, best_start = 0, best_end = 0, i = 0;
+            int start = 0, best_start = 0, best_end = 0, i = 0;
             int score = h_bonus, best = 0;
-            for (int64_t i0 = 0; i0 < n; i0 += 16) {
+            for (int i0 = 0; i0 < n; i0 += 16) {
                 // lane (i0 / 16) % 16 of the group holds positions i0 .. i0 + 15
-                uint32_t bits = (uint32_t)__shfl((int)mask_of(i0 >> 8), (int)((i0 >> 4) & 15), 16);
+                uint32_t bits = (uint32_t)__shfl((int)mask_of(i0 >> 8), (i0 >> 4) & 15, 16);
                 while (bits) {
-                    const int64_t m = i0 + __builtin_ctz(bits);
+                    const int m = i0 + __builtin_ctz(bits);
                     bits &= bits - 1;
                     if (m > i) {
-                        score += h_match * (int)(m - i);
+                        score += h_match * (m - i);
                         if (score > best) { best_start = start; best = score; best_end = m; }
                     }
                     score -= h_mismatch;
@@ -1990,7 +2053,7 @@ k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read,
                 }
             }
             if (n > i) {
-                score += h_match * (int)(n - i);
+                score += h_match * (n - i);
                 if (score > best) { best_start = start; best = score; best_end = n; }
             }
             if (score + h_bonus > best) { best = score + h_bonus; best_end = n; best_start = start; }
@@ -2009,15 +2072,15 @@ k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read,
                 have = true;
             };
             if (best_start > 0) push(4, (uint32_t)best_start);
-            int64_t cur = best_start;
-            for (int64_t i0 = best_start & ~(int64_t)15; i0 < best_end; i0 += 16) {
-                uint32_t bits = (uint32_t)__shfl((int)mask_of(i0 >> 8), (int)((i0 >> 4) & 15), 16);
+            int cur = best_start;
+            for (int i0 = best_start & ~15; i0 < best_end; i0 += 16) {
+                uint32_t bits = (uint32_t)__shfl((int)mask_of(i0 >> 8), (i0 >> 4) & 15, 16);
                 // positions in [best_start, best_end) only
-                const int64_t lo = best_start - i0, hi = best_end - i0;
+                const int lo = best_start - i0, hi = best_end - i0;
                 if (lo > 0) bits &= ~((1u << lo) - 1u);
                 if (hi < 16) bits &= (1u << hi) - 1u;
                 while (bits) {
-                    const int64_t m = i0 + __builtin_ctz(bits);
+                    const int m = i0 + __builtin_ctz(bits);
                     bits &= bits - 1;
                     if (m > cur) push(7, (uint32_t)(m - cur));
                     push(8, 1);
@@ -2040,8 +2103,6 @@ k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read,
                 pool[at + 4] = (uint16_t)ed;
                 pool[at + 5] = (uint16_t)n_ops;
             }
-        } else {
-            flags |= RSA_SITE_POOL_FULL;
         }
     }
     if (valid && l16 == 0) {
@@ -2052,10 +2113,9 @@ k_sites(const rsa_nam* __restrict__ nams, const uint32_t* __restrict__ nam_read,
         out.mm_offset = mm_off;
         out.orig_query_start = nam.query_start;
         out.orig_query_end = nam.query_end;
-        // at the NAM's index in its read's list as found (nam_id; the NAMs may come sorted)
+        // at the NAM's index in its read's list as found (nam_id; the NAMs may come sorted);
         // a nam_id outside the list would alias another NAM's slot: no write, the call fails
-        const uint64_t ro = ooff[r], rn = ooff[r + 1] - ro;
-        if (nam.nam_id >= 0 && (uint64_t)nam.nam_id < rn) sites[ro + (uint64_t)nam.nam_id] = out;
+        if (d.slot != ~0ull) sites[d.slot] = out;
         else atomicOr(&err_hdr->errors, SEED_E_SITE);
     }
     __syncthreads();                             // s_need / s_base / s_at are reused next round
@@ -2099,7 +2159,7 @@ hipError_t bucket_lines_build(const uint64_t* starts, const rsa_ref_randstrobe* 
 enum {
     B_SEQ, B_ROFF, B_RLEN, B_QBASE, B_QRS, B_QCNT, B_SYNC, B_QI, B_ST, B_X, B_ARENA, B_PHIT, B_POPEN, B_PGRP, B_PADD,
     B_NCNT1, B_FLAGS, B_MAP, B_NCNT2, B_NSRC, B_RBASE, B_BIGL, B_RBIGL, B_RBUF, B_OUT, B_SLOTS, B_SITES, B_POOL,
-    B_NREAD, B_RSLIST, B_RLIST
+    B_NREAD, B_RSLIST, B_RLIST, B_LOC, B_BSUM, B_SEQRC
 };
 // every host side of a transfer is page-locked: a pageable one would make the copy synchronous
 enum { H_X, H_QBASE, H_RSLIST };
@@ -2145,6 +2205,7 @@ static hipError_t hens(SeedBufs& b, int i, size_t bytes) {
 // windows by aligned dwords that may start or end up to 19 bytes outside a read
 #define SEQ_PAD 64
 #define D_SEQ ((char*)b.p[B_SEQ] + SEQ_PAD)
+#define D_SEQRC ((char*)b.p[B_SEQRC] + SEQ_PAD)     // reverse complements, at the reads' offsets (k_compact)
 #define HP(i, T) ((T*)b.h[i])
 
 static const uint32_t MAP_BIG = 65536 + 512;
@@ -2306,11 +2367,14 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
     SCHK(dens(b, B_BIGL, 4ull * n));
     SCHK(dens(b, B_RBIGL, 4ull * n));
     SCHK(dens(b, B_RLIST, 4ull * n));
+    SCHK(dens(b, B_LOC, 4ull * n));                                        // k_seed_count: offsets in a workgroup
+    SCHK(dens(b, B_BSUM, 8ull * ((n + SS_TPB - 1) / SS_TPB + 1)));          // workgroup totals -> offsets
     SCHK(dens(b, B_RBUF, sizeof(RescueD) * (nq_cap + 1)));
     SCHK(dens(b, B_MAP, (size_t)MAP_BIG * 9 * 4 * MAP_BIG_LANES));
     SCHK(dens(b, B_OUT, sizeof(rsa_nam) * (cap + 1)));
     if (out->sites) {
-        SCHK(dens(b, B_NREAD, 4ull * (cap + 1)));
+        SCHK(dens(b, B_NREAD, sizeof(SiteDesc) * (cap + 1)));       // per-NAM site descriptors
+        SCHK(dens(b, B_SEQRC, total_len + 2 * SEQ_PAD));
         SCHK(dens(b, B_SITES, sizeof(rsa_nam_site) * (cap + 1)));
         SCHK(dens(b, B_POOL, 2 * std::max<uint64_t>(1, out->mm_capacity)));
     }
@@ -2399,22 +2463,27 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
         kt.end(st);
         // 5. final offsets and the NAM lists back to back
         kt.begin(st, RSA_K_COMPACT);
-        hipLaunchKernelGGL(k_seed_scan, dim3(1), dim3(SS_TPB), 0, st, (int)n, d_resc, DP(B_NCNT1, uint32_t),
-                           DP(B_NCNT2, uint32_t), DP(B_QCNT, uint32_t), DP(B_ST, ReadStat), d_ooff, dhdr);
+        const int n_sblk = (int)((n + SS_TPB - 1) / SS_TPB);
+        hipLaunchKernelGGL(k_seed_count, dim3(std::max(1, n_sblk)), dim3(SS_TPB), 0, st, (int)n, d_resc,
+                           DP(B_NCNT1, uint32_t), DP(B_NCNT2, uint32_t), DP(B_QCNT, uint32_t), DP(B_ST, ReadStat),
+                           DP(B_LOC, uint32_t), DP(B_BSUM, uint64_t), dhdr);
+        hipLaunchKernelGGL(k_seed_scan, dim3(1), dim3(SS_TPB), 0, st, n_sblk, (int)n, DP(B_BSUM, uint64_t), d_ooff,
+                           dhdr);
         hipLaunchKernelGGL(k_compact, dim3(n), dim3(64), 0, st, (int)n, DP(B_NSRC, uint64_t), DP(B_RBASE, uint64_t),
-                           slots, DP(B_NCNT1, uint32_t), DP(B_NCNT2, uint32_t), d_resc, DP(B_ARENA, rsa_nam), d_ooff,
-                           cap, DP(B_OUT, rsa_nam), out->sites ? DP(B_NREAD, uint32_t) : nullptr,
-                           out->order == RSA_NAMS_BY_SCORE ? 1 : 0);
+                           slots, DP(B_NCNT1, uint32_t), DP(B_NCNT2, uint32_t), d_resc, DP(B_ARENA, rsa_nam),
+                           DP(B_LOC, uint32_t), DP(B_BSUM, uint64_t), d_ooff,
+                           cap, DP(B_OUT, rsa_nam), out->sites ? DP(B_NREAD, SiteDesc) : nullptr, d_roff, d_rlen,
+                           p.coff, D_SEQ, D_SEQRC, out->order == RSA_NAMS_BY_SCORE ? 1 : 0);
         SCHK(hipGetLastError());
         kt.end(st);
         // 6. site checks (aln.cpp:60-93, 374-431)
         if (out->sites) {
             kt.begin(st, RSA_K_SITES);
-            const uint32_t grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1, (cap + 15) / 16), 4096);
-            hipLaunchKernelGGL(k_sites, dim3(grid), dim3(256), 0, st, DP(B_OUT, rsa_nam), DP(B_NREAD, uint32_t), dhdr,
-                               cap, d_ooff, D_SEQ, d_roff, d_rlen, p, DP(B_SITES, rsa_nam_site), DP(B_POOL, uint16_t),
-                               out->mm_capacity, &dhdr->mm_used, out->hamming_align ? 1 : 0, out->match, out->mismatch,
-                               out->end_bonus);
+            const uint32_t grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1, (cap + SITES_BLOCK - 1) / SITES_BLOCK),
+                                                               4096);
+            hipLaunchKernelGGL(k_sites, dim3(grid), dim3(16 * SITES_BLOCK), 0, st, DP(B_OUT, rsa_nam), DP(B_NREAD, SiteDesc), dhdr,
+                               cap, D_SEQ, D_SEQRC, p, DP(B_SITES, rsa_nam_site), DP(B_POOL, uint16_t), out->mm_capacity,
+                               &dhdr->mm_used, out->hamming_align ? 1 : 0, out->match, out->mismatch, out->end_bonus);
             SCHK(hipGetLastError());
             kt.end(st);
         }

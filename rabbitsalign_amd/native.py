@@ -134,10 +134,12 @@ _lib = None
 
 
 def load(path: str = GPU_LIB):
-    """Load librsa_gpu.so; raises if it is missing (no fallback path exists)."""
+    """Load librsa_gpu.so; raises if it is missing (no fallback path exists).
+    RSA_GPU_LIB names another build of the same library (kernel A/B tooling)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = os.environ.get("RSA_GPU_LIB", path)
     if not os.path.exists(path):
         raise RuntimeError(f"{path} not built: run __graft_entry__.build() (no CPU fallback exists)")
     lib = C.CDLL(path)
