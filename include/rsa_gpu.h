@@ -221,6 +221,8 @@ typedef struct rsa_aln {
     uint32_t flags;                    /* RSA_ALN_NO_SHARED (jobs with RSA_JOB_SHARED_CHECK) */
 } rsa_aln;
 #define RSA_ALN_NO_SHARED 1u
+#define RSA_ALN_WORD_CERT 2u       /* informational: the scan's word-layout result stood on its band-path
+                                      certificate (no byte-layout pass ran) */
 
 typedef struct rsa_aln_batch {
     rsa_aln* alns;             /* [n_jobs] */

@@ -82,6 +82,9 @@ int rsam_map(rsam* m, const rsam_reads* reads, int threads, int chunk_size, cons
  * SAM byte written (the reference's consumer cost, src/main.cpp:446,595). */
 int rsam_map_files(rsam* m, const char* fq1, const char* fq2, int interleaved, int threads, int chunk_size,
                    const char* sam_path, rsam_stats* out);
+/* Note for long-lived hosts: a run that fails while a reader thread is blocked in
+ * read() of a stalled pipe or terminal (not a regular file) returns after 2 s and
+ * leaves that thread detached, holding its descriptor, until the read returns. */
 
 /* ---- a rank's part of one input (rank/world mode) -----------
  * `world` processes (one per GPU, each with its own rsam) map ONE pair of plain

@@ -642,15 +642,18 @@ __device__ __forceinline__ int dir_byte(const int8_t* dirp, int cell, int sub) {
 // ScanRes.word bit 1): the job's banded path must have no insertion next to a
 // deletion, or the job is listed for the exact two-layout scan (rsa_ctx.hip).
 // raw: the path's ops in order (0 M, 1 I, 2 D); ok = false lists the job as is.
-__device__ __forceinline__ void cert_check(const ScanRes& sr, int j, const uint32_t* raw, int nraw, bool ok,
+// Returns true when the job's word result stands on the certificate (its rsa_aln gets
+// RSA_ALN_WORD_CERT, which the context counts as scan_certified).
+__device__ __forceinline__ bool cert_check(const ScanRes& sr, int j, const uint32_t* raw, int nraw, bool ok,
                                            int* redo, int* redo_count) {
-    if (!(sr.word & 2) || !redo) return;
+    if (!(sr.word & 2) || !redo) return false;
     bool bad = !ok;
     for (int k = 1; k < nraw && !bad; ++k) {
         const uint32_t a = raw[k - 1] & 0xf, b = raw[k] & 0xf;
         bad = (a == 1 && b == 2) || (a == 2 && b == 1);
     }
     if (bad) redo[atomicAdd(redo_count, 1)] = j;
+    return !bad;
 }
 
 template <int DIRCAP> struct DirCells { static constexpr int BYTES = ((DIRCAP + 2) / 3 + 15) & ~15; };
@@ -812,8 +815,9 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
     if (op == 0) { ++l; raw[l - 1] = cig((uint32_t)ecount + 1, op); }
     else { l += 2; raw[l - 2] = cig((uint32_t)ecount, op); raw[l - 1] = cig(1, 0); }
     for (int s = 0, t = l - 1; s < t; ++s, --t) { const uint32_t x = raw[s]; raw[s] = raw[t]; raw[t] = x; }
-    cert_check(sr, j, raw, l, true, redo, redo_count);
+    const bool certified = cert_check(sr, j, raw, l, true, redo, redo_count);
     ext_finish(jb, sr, q, r, raw, l, cig_pool + jb.cig_off, a, match, mismatch, bonus, gO, gE, qc, rc);
+    if (certified) a.flags |= RSA_ALN_WORD_CERT;
     out[j] = a;
     return true;
 }
@@ -1068,8 +1072,9 @@ k_ext_band_panel(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__
     if (op == 0) { ++l; raw[l - 1] = cig((uint32_t)ecount + 1, op); }
     else { l += 2; raw[l - 2] = cig((uint32_t)ecount, op); raw[l - 1] = cig(1, 0); }
     for (int s = 0, e = l - 1; s < e; ++s, --e) { const uint32_t x = raw[s]; raw[s] = raw[e]; raw[e] = x; }
-    cert_check(sr, j, raw, l, true, redo, redo_count);
+    const bool certified = cert_check(sr, j, raw, l, true, redo, redo_count);
     ext_finish(jb, sr, q, r, raw, l, cig_pool + jb.cig_off, a, match, mismatch, bonus, gO, gE, s_qc, s_rc);
+    if (certified) a.flags |= RSA_ALN_WORD_CERT;
     out[j] = a;
 }
 

@@ -487,7 +487,6 @@ struct rsa_pending {
     uint32_t n = 0;
     int32_t match = 0, mismatch = 0, gap_open = 0, gap_extend = 0, end_bonus = 0;
     uint64_t guess = 0, cells = 0, qr_bytes = 0;
-    uint64_t certified = 0;            // jobs k_ext_scan_v took on the word score alone
     int rmax = 1;                      // k_ext_scan's rows-per-lane bound for this call's jobs
     int band16_dircap = 4096;          // k_ext_band16's direction capacity for this call's queries
     uint32_t n_shared = 0;             // jobs with RSA_JOB_SHARED_CHECK (k_shared_check's list)
@@ -535,7 +534,7 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
             s.query_len &= RSA_JOB_LEN_MASK;
             if (s.query_len > RSA_SHARED_QMAX || s.ref_len > RSA_SHARED_WMAX || k < 3 || 2 * k / 3 > 24) {
                 set_err(ctx, "rsa_extend: job " + std::to_string(i) + " asks for a shared-substring check outside "
-                             "its limits (query <= 1024, window <= 4096, 3 <= k <= 36)");
+                             "its limits (query <= 1024, window <= 4096, 3 <= k <= 37)");
                 return RSA_ERR_ARG;
             }
             shl.push_back(i);
@@ -642,11 +641,6 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
             if (cls[i] < 0) ord[rest_at++] = (int)i;
             else ord[cnt[(size_t)cls[i] * (maxr + 1) + (maxr - hj[i].rlen)]++] = (int)i;
         }
-        // certified: word results k_ext_scan_v may take on the word score alone (queries that can
-        // reach the byte bound; shorter ones run the byte layout only)
-        if (use_v)
-            for (uint32_t i = 0; i < n; ++i)
-                if (cls[i] >= 0 && (int64_t)jb->match * hj[i].qlen + jb->mismatch >= 255) P.certified++;
     } else {
         rest_n = n;
         for (uint32_t i = 0; i < n; ++i) ord[i] = (int)i;
@@ -822,6 +816,10 @@ static int ext_finish(rsa_pending& P) {
         HIPCHK(stream_wait(st, L->sb.done));
     }
     out->cigar_used = hs.total;
+    // scan_certified: the jobs whose word result stood on the band-path certificate, as the
+    // band kernels flagged them (not a prediction from the query lengths)
+    uint64_t certified = 0;
+    for (uint32_t i = 0; i < n; ++i) certified += (out->alns[i].flags & RSA_ALN_WORD_CERT) ? 1 : 0;
     uint64_t no_shared = 0;
     for (uint32_t f = 0; f < P.n_shared; ++f)          // the stream has drained: the flags are here
         if (L->h_shres.as<uint8_t>()[f]) {
@@ -844,7 +842,7 @@ static int ext_finish(rsa_pending& P) {
         ctx->stats.dp_cells += P.cells;
         ctx->stats.band_deferred += deferred;
         ctx->stats.band_overflow += overflowed;
-        ctx->stats.scan_certified += P.certified - (uint64_t)redo;
+        ctx->stats.scan_certified += certified;
         ctx->stats.scan_redo += (uint64_t)redo;
         ctx->stats.shared_checks += P.n_shared;
         ctx->stats.no_shared += no_shared;

@@ -74,9 +74,12 @@ public:
         idx.bucket_starts.swap(st);
         return true;
     }
+    // a pipeline start sets them while seeding calls of another run on this engine may
+    // read them: every seeding call takes one consistent snapshot under the lock
     void set_alignment_params(const AlignmentParameters& p) override {
+        std::lock_guard<std::mutex> g(ap_m_);
         ap_ = p;
-        ap_set_.store(true, std::memory_order_release);
+        ap_set_ = true;
     }
 
     ~GpuEngine() override {
@@ -140,7 +143,14 @@ public:
         static const bool want_sites = !(getenv("RSA_SITES") && getenv("RSA_SITES")[0] == '0');   // A/B switch
         // hamming_align on the device too (RSA_SITE_ALIGNED, RSA_SITE_ALIGN=0: positions only)
         static const bool align_env = !(getenv("RSA_SITE_ALIGN") && getenv("RSA_SITE_ALIGN")[0] == '0');
-        const bool hamming_on = align_env && ap_set_.load(std::memory_order_acquire);
+        AlignmentParameters hp;
+        bool hp_set;
+        {
+            std::lock_guard<std::mutex> g(ap_m_);
+            hp = ap_;
+            hp_set = ap_set_;
+        }
+        const bool hamming_on = align_env && hp_set;
         size_t cap = std::max<size_t>(1024, 12 * n);
         for (;;) {
             // 12 + 4 n_mm words an accepted site at most (n_mm < 5 % of the read): overflow is
@@ -152,7 +162,7 @@ public:
             // lists of <= 16 NAMs come sorted (RSA_NAMS_BY_SCORE): part() works on them in place
             rsa_nam_batch nb{out.nams.data(), cap, out.offsets.data(), out.nonrep.data(), out.rescued.data(), 0,
                              want_sites ? out.sites.data() : nullptr, out.mm_pool.data(), mm_cap, 0,
-                             RSA_NAMS_BY_SCORE, hamming_on ? 1u : 0u, ap_.match, ap_.mismatch, ap_.end_bonus, 0};
+                             RSA_NAMS_BY_SCORE, hamming_on ? 1u : 0u, hp.match, hp.mismatch, hp.end_bonus, 0};
             int rc = rsa_seed(ctx_, &rb, rescue_level, rescue_cutoff, &nb);
             if (rc == RSA_ERR_CAPACITY) { cap = nb.needed + 16; continue; }
             if (rc != RSA_OK) throw std::runtime_error(std::string("rsa_seed: ") + rsa_last_error(ctx_));
@@ -339,8 +349,9 @@ private:
     rsa_ctx* ctx_ = nullptr;
     std::mutex staging_m_;
     std::vector<std::unique_ptr<Staging>> staging_;
+    std::mutex ap_m_;
     AlignmentParameters ap_;                    // hamming_align's scores (set_alignment_params)
-    std::atomic<bool> ap_set_{false};
+    bool ap_set_ = false;
     std::vector<Staging*> free_;
 };
 

@@ -448,7 +448,6 @@ static inline void prefetch_res(const AlignTmpRes& r) {
     prefetch_vec(r.type4_nams);
 }
 
-// to_uppercase (refs.cpp:10-16, c & ~32) of n bytes into dst
 // rescue jobs whose has_shared_substring test failed in the engine: no aligner call
 // in the reference (rescue_mate_part returns before it)
 static inline uint64_t no_shared_count(const std::vector<AlignmentInfo>& infos) {
@@ -457,6 +456,7 @@ static inline uint64_t no_shared_count(const std::vector<AlignmentInfo>& infos) 
     return n;
 }
 
+// to_uppercase (refs.cpp:10-16, c & ~32) of n bytes into dst
 static inline void upper_into(const char* src, size_t n, char* dst) {
     size_t i = 0;
     for (; i + 8 <= n; i += 8) {
