@@ -358,6 +358,8 @@ typedef struct rsa_kernel_stats {
     uint64_t query_written, query_fixed_reads;
     /* extension jobs that carried RSA_JOB_SHARED_CHECK, and those that came back RSA_ALN_NO_SHARED */
     uint64_t shared_checks, no_shared;
+    /* seeding calls whose first download was short and took a second round trip */
+    uint64_t seed_second_trips;
 } rsa_kernel_stats;
 
 int rsa_get_stats(rsa_ctx* ctx, rsa_kernel_stats* out);

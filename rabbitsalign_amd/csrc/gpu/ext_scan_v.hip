@@ -382,6 +382,7 @@ k_ext_scan_v(const ExtJobDev* __restrict__ jobs, const int* __restrict__ order, 
              int match, int mismatch, int gO, int gE, int* __restrict__ err) {
     __shared__ __attribute__((aligned(4))) uint8_t s_r[VS_JOBS][WCAP + 2 * VS_PAD];
     __shared__ __attribute__((aligned(16))) uint16_t s_prof[VS_JOBS][VProf<RV>::JOB];
+    __shared__ __attribute__((aligned(4))) uint8_t s_q[VS_JOBS][32 * RV];   // query codes (qcode7), 7 past the query
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int slot = wave * (64 / VS_G) + lane / VS_G, gl = lane & (VS_G - 1);
     const int k = blockIdx.x * VS_JOBS + slot;
@@ -393,7 +394,7 @@ k_ext_scan_v(const ExtJobDev* __restrict__ jobs, const int* __restrict__ order, 
     const int qlen = (int)jb.qlen, rlen = (int)jb.rlen;
     uint8_t* rc = s_r[slot] + VS_PAD;
     uint16_t* prof = s_prof[slot];
-    const char* q = qbuf + jb.q_off;
+    uint8_t* qc = s_q[slot];
 
     // stage: the window as SSW codes, code-4 padding before it and from its end to the end
     // of the slot (the wave's steps read up to 32 columns past its longest window), and
@@ -414,8 +415,26 @@ k_ext_scan_v(const ExtJobDev* __restrict__ jobs, const int* __restrict__ order, 
             }
         }
     }
+    {
+        // the query once, by aligned dwords (the forward and the reverse profile both read it
+        // from LDS; the query buffer's allocation covers the dword past its last byte)
+        for (int i = qlen + gl; i < 32 * RV; i += VS_G) qc[i] = 7;
+        const int pre = (int)(jb.q_off & 3);
+        const uint32_t* w = (const uint32_t*)(qbuf + (jb.q_off - (uint64_t)pre));
+        const int nw = (pre + qlen + 3) >> 2;
+        for (int i = gl; i < nw; i += VS_G) {
+            const uint32_t x = w[i];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int pos = 4 * i + b - pre;
+                if (pos >= 0 && pos < qlen) qc[pos] = (uint8_t)qcode7((x >> (8 * b)) & 0xFF);
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     const uint32_t m16 = h_bits16(match), x16 = h_bits16(-mismatch);
-    prof_build<RV>(prof, gl, [&](int p) { return p < qlen ? qcode7((unsigned char)q[p]) : 7; }, m16, x16);
+    prof_build<RV>(prof, gl, [&](int p) { return (int)qc[p]; }, m16, x16);
     __syncthreads();
 
     const int vl_used = (qlen + RV - 1) / RV;
@@ -466,8 +485,7 @@ k_ext_scan_v(const ExtJobDev* __restrict__ jobs, const int* __restrict__ order, 
         __builtin_amdgcn_wave_barrier();
         if (ron)
             for (int i = gl; i < VS_PAD; i += VS_G) rc[ref_end1 + 1 + i] = 4;
-        prof_build<RV>(prof, gl, [&](int p) { return p < nrow ? qcode7((unsigned char)q[read_end1 - p]) : 7; }, m16,
-                       x16);
+        prof_build<RV>(prof, gl, [&](int p) { return p < nrow ? (int)qc[read_end1 - p] : 7; }, m16, x16);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
         const int seg = word ? (nrow + 7) / 8 : (nrow + 15) / 16;

@@ -1006,6 +1006,7 @@ int rsa_seed(rsa_ctx* ctx, const rsa_read_batch* rb, int32_t rescue_level, uint3
     ctx->stats.rescued_reads += c.rescued;
     ctx->stats.query_written += c.qw;
     ctx->stats.query_fixed_reads += c.qfix;
+    ctx->stats.seed_second_trips += c.second_trip;
     return RSA_OK;
 }
 

@@ -43,6 +43,9 @@ struct SeedBufs {
     void* h[SEED_NHBUF] = {nullptr};
     size_t hcap[SEED_NHBUF] = {0};
     uint64_t pool_n = 0;         // entries of the global-map / rescue pool (grows when a call runs out)
+    // NAMs a read and pool words a NAM of the lane's last call: the first download's size
+    // (a guess too small costs a second round trip, e.g. 9.4 NAMs a read on PE 2x250)
+    double nam_rate = 0, mm_rate = 0;
     hipEvent_t done = nullptr;   // blocking-sync event (RSA_WAIT=event)
 };
 

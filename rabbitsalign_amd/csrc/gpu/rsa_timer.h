@@ -70,5 +70,6 @@ struct KTimer {
 struct SeedCounters {
     uint64_t reads = 0, read_bases = 0, qrs = 0, found = 0, filtered = 0, hits = 0, nams = 0, rescued = 0;
     uint64_t qw = 0, qfix = 0;      // query randstrobes written out; reads query_lane made them for
+    uint64_t second_trip = 0;       // the first download was short
     double alg_bytes[RSA_K_COUNT] = {0};
 };

@@ -1578,8 +1578,196 @@ k_query_fix(const uint32_t* __restrict__ rlist, SeedHdr* __restrict__ hdr, const
     }
 }
 
-// find_nams_rescue (nam.cpp:955-1012) of the listed reads: one wave per read,
-// lane 0, maps in LDS; a fixed grid walks the device list
+// ---------------------------------------------------------------------------
+// find_nams_rescue of one read by a whole wave (k_rescue_w).  The same result as
+// rescue_read, with the parallel parts spread over the lanes:
+//  - the read's query randstrobes with a hit, per orientation in order (ballot
+//    compaction), ranked by cmp1 (count, q_start, q_end; unique keys, so any
+//    correct sort is std::sort's) -- at most RW_MAXS a side (reads up to ~330 bp),
+//    else the whole read runs rescue_read on lane 0;
+//  - the taken prefix (nam.cpp:982-988) from the ranks;
+//  - every taken randstrobe's index entries, 64 a round: add_to_hits_per_ref_pre
+//    and add_to_hits_per_ref keep an entry iff its |q span - r span| is <= the
+//    minimum over the entries before it (an entry not kept never lowers the
+//    running min_diff), so a wave prefix-minimum decides, and lane 0 inserts the
+//    kept keys in order into the robin_hood map (nam.cpp:87-107).  Both passes
+//    keep the same entries, and a key's list id is fixed at its insertion, so the
+//    hits of the second pass are recorded in the first (as staged HitD);
+//  - the hits in cmp2 (q_start) order of their randstrobes, then
+//    merge_hits_into_nams_fast per map (merge_fast, lane 0).
+// Before: lane 0 alone walked the entries one dependent load at a time, twice
+// (k_rescue_w averaged 524 us a launch on PE 2x250).
+// ---------------------------------------------------------------------------
+#define RW_MAXS 64                                         // randstrobes a side the wave path ranks (one a lane)
+struct RwStrobe { uint64_t pos; uint32_t count, qs, qe, stage_off, stage_cnt, pad; };
+
+// exclusive prefix minimum over the wave (INT_MAX below lane 0)
+__device__ __forceinline__ int wave_excl_min(int v, int lane, int& all) {
+    int x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x = min(x, y);
+    }
+    all = __shfl(x, 63, 64);
+    const int e = __shfl_up(x, 1, 64);
+    return lane == 0 ? INT_MAX : e;
+}
+
+__device__ void rescue_read_wave(int r, int lane, const rsa_query_randstrobe* __restrict__ qrs,
+                                 const QrsInfo* __restrict__ qi, const uint32_t* __restrict__ qcnt,
+                                 const uint64_t* __restrict__ qbase, const uint64_t* __restrict__ roff,
+                                 const SeedIndexParams& p, uint32_t rescue_cutoff, RescueD* __restrict__ rbuf,
+                                 const SeedPool& pool, uint8_t* ms, RwStrobe* sv, uint32_t* __restrict__ ncnt,
+                                 uint32_t* __restrict__ flags) {
+    const int nq = (int)qcnt[r];
+    const uint64_t base = qbase[r];
+    // 1. the randstrobes with a hit of each side, in order, into sv[side][..]
+    int n_side[2] = {0, 0};
+    for (int i0 = 0; i0 < nq; i0 += 64) {
+        const int i = i0 + lane;
+        bool hit = false, rev = false;
+        RwStrobe x = {};
+        if (i < nq) {
+            const QrsInfo o = qi[base + i];
+            const rsa_query_randstrobe q = qrs[base + i];
+            hit = (o.flags & 1) != 0;
+            rev = q.is_reverse != 0;
+            x.pos = o.pos; x.count = o.count; x.qs = q.start; x.qe = q.end;
+        }
+#pragma unroll
+        for (int o = 0; o < 2; ++o) {
+            const bool take = hit && (rev == (o == 1));
+            const uint64_t bm = __ballot(take);
+            const int at = n_side[o] + __popcll(bm & (lane ? (~0ull >> (64 - lane)) : 0ull));
+            if (take && at < RW_MAXS) sv[o * RW_MAXS + at] = x;
+            n_side[o] += __popcll(bm);
+        }
+    }
+    if (n_side[0] > RW_MAXS || n_side[1] > RW_MAXS) {      // a read this path does not rank: lane 0, as before
+        if (lane == 0)
+            rescue_read(r, qrs, qi, qcnt, qbase, roff, p, rescue_cutoff, rbuf, pool.hits, pool.open, pool.nams,
+                        pool.grp, pool.added, ms, FN_MAP_CAP, ncnt, flags);
+        return;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    DMap m[2];
+    map_bind(m[0], ms, FN_MAP_CAP, 0);
+    map_bind(m[1], ms, FN_MAP_CAP, 1);
+    rh_new_reserved(m[0]);
+    rh_new_reserved(m[1]);
+    HitD* stage = pool.grp + roff[r];                      // kept hits in cmp1 order (room: hits_all)
+    int n_stage = 0, n_lists = 0, taken[2] = {0, 0};
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+        RwStrobe* v = sv + o * RW_MAXS;
+        const int n = n_side[o];
+        // 2. cmp1 ranks (one element a lane), then the taken prefix of the sorted order
+        RwStrobe e0 = {};
+        if (lane < n) e0 = v[lane];
+        int rk0 = 0;
+        for (int j = 0; j < n; ++j) {
+            const RwStrobe y = v[j];
+            rk0 += (y.count != e0.count ? y.count < e0.count : (y.qs != e0.qs ? y.qs < e0.qs : y.qe < e0.qe)) ? 1 : 0;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (lane < n) v[rk0] = e0;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        // taken = the first sorted index a with (count > rescue_cutoff && a >= 5) || count > 1000
+        const bool stop_here = lane < n && ((v[lane].count > rescue_cutoff && lane >= 5) || v[lane].count > 1000);
+        const uint64_t sm = __ballot(stop_here);
+        const int stop = sm ? __builtin_ctzll(sm) : n;
+        taken[o] = stop;
+        // 3. the kept entries of each taken randstrobe: map keys in order (lane 0) and staged hits
+        for (int a = 0; a < stop; ++a) {
+            const RwStrobe x = v[a];
+            const int qspan = (int)x.qe - (int)x.qs;
+            int carry = INT_MAX;
+            const int off = n_stage;
+            for (uint32_t c0 = 0; c0 < x.count; c0 += 64) {
+                const uint32_t i = c0 + lane;
+                int d = INT_MAX, rs = 0, re = 0;
+                uint32_t key = 0;
+                if (i < x.count) {
+                    const rsa_ref_randstrobe ent = p.rs[x.pos + i];
+                    rs = (int)ent.position;
+                    re = rs + (int)(ent.packed & 0xFF) + p.k;
+                    d = qspan - (re - rs);
+                    d = d < 0 ? -d : d;
+                    key = ent.packed >> 8;
+                }
+                int all;
+                const int before = min(carry, wave_excl_min(d, lane, all));
+                carry = min(carry, all);
+                uint64_t km = __ballot(i < x.count && d <= before);
+                while (km) {
+                    const int b = __builtin_ctzll(km);
+                    km &= km - 1;
+                    const uint32_t k_b = (uint32_t)__shfl((int)key, b, 64);
+                    const int rs_b = __shfl(rs, b, 64), re_b = __shfl(re, b, 64);
+                    if (lane == 0) {
+                        bool ins;
+                        const int32_t lid = rh_get_or_insert(m[o], k_b, n_lists, ins);
+                        if (ins) n_lists++;
+                        HitD h;
+                        h.qs = (int)x.qs; h.qe = (int)x.qe; h.rs = rs_b; h.re = re_b; h.list = lid | (o << 30); h.pad = 0;
+                        stage[n_stage] = h;
+                    }
+                    n_stage++;
+                }
+            }
+            if (lane == 0) { v[a].stage_off = (uint32_t)off; v[a].stage_cnt = (uint32_t)(n_stage - off); }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    const int ovf = (lane == 0) ? ((m[0].overflow || m[1].overflow) ? 1 : 0) : 0;
+    if (__shfl(ovf, 0, 64)) {
+        if (lane == 0) { flags[r] |= 4; ncnt[r] = 0; }
+        return;
+    }
+    // 4. the hits: taken randstrobes in q_start order (cmp2, nam.cpp:948-952; q_starts of a side
+    //    are distinct), each one's staged hits in entry order
+    HitD* hits = pool.hits + roff[r];
+    int n_hits = 0;
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+        const RwStrobe* v = sv + o * RW_MAXS;
+        const int n = taken[o];
+        // the hit offset of each taken randstrobe = the staged hits of the taken ones with a smaller q_start
+        RwStrobe e0 = {};
+        if (lane < n) e0 = v[lane];
+        int off0 = 0, tot = 0;
+        for (int j = 0; j < n; ++j) {
+            const RwStrobe y = v[j];
+            off0 += y.qs < e0.qs ? (int)y.stage_cnt : 0;
+            tot += (int)y.stage_cnt;
+        }
+        for (int a = 0; a < n; ++a) {                      // each randstrobe's run, lanes over its hits
+            const int so = __shfl((int)e0.stage_off, a, 64), sc = __shfl((int)e0.stage_cnt, a, 64);
+            const int d0 = __shfl(off0, a, 64);
+            for (int h = lane; h < sc; h += 64) hits[n_hits + d0 + h] = stage[so + h];
+        }
+        n_hits += tot;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");       // lane 0 reads what every lane wrote
+    __builtin_amdgcn_wave_barrier();
+    if (lane != 0) return;
+    rsa_nam* out = pool.nams + roff[r];
+    rsa_nam* open = pool.open + roff[r];
+    HitD* grp = pool.grp + roff[r];
+    uint8_t* added = pool.added + roff[r];
+    int n_out = 0;
+    merge_fast(m[0], 0, hits, n_hits, p.k, open, added, grp, out, n_out);
+    merge_fast(m[1], 1, hits, n_hits, p.k, open, added, grp, out, n_out);
+    ncnt[r] = (uint32_t)n_out;
+    flags[r] = (flags[r] & ~4u) | 8u;   // bit3: rescued result present
+}
+
+// find_nams_rescue (nam.cpp:955-1012) of the listed reads: one wave per read
+// (rescue_read_wave), maps in LDS; a fixed grid walks the device list
 #define RESCUE_GRID 256
 __global__ void __launch_bounds__(64 * FN_WAVES)
 k_rescue_w(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restrict__ qi,
@@ -1588,14 +1776,14 @@ k_rescue_w(const rsa_query_randstrobe* __restrict__ qrs, const QrsInfo* __restri
            uint32_t* __restrict__ flags, const uint64_t* __restrict__ rbase, SeedHdr* __restrict__ hdr,
            const uint32_t* __restrict__ rlist, uint32_t* __restrict__ rbig_list) {
     __shared__ __attribute__((aligned(16))) uint8_t s_map[FN_WAVES][FN_MAP_CAP * 9 * 4];
+    __shared__ __attribute__((aligned(16))) RwStrobe s_sv[FN_WAVES][2 * RW_MAXS];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane != 0) return;
     const uint32_t nr = hdr->rcount;
     for (uint32_t t = blockIdx.x * FN_WAVES + w; t < nr; t += gridDim.x * FN_WAVES) {
         const int r = (int)rlist[t];
-        rescue_read(r, qrs, qi, qcnt, qbase, rbase, p, rescue_cutoff, rbuf, pool.hits, pool.open, pool.nams, pool.grp,
-                    pool.added, s_map[w], FN_MAP_CAP, ncnt2, flags);
-        if (flags[r] & 4u) rbig_list[atomicAdd(&hdr->rbig_count, 1u)] = (uint32_t)r;
+        rescue_read_wave(r, lane, qrs, qi, qcnt, qbase, rbase, p, rescue_cutoff, rbuf, pool, s_map[w], s_sv[w], ncnt2,
+                         flags);
+        if (lane == 0 && (flags[r] & 4u)) rbig_list[atomicAdd(&hdr->rbig_count, 1u)] = (uint32_t)r;
     }
 }
 
@@ -2489,11 +2677,15 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
         }
         // 7. one download of the header + per-read results, and the outputs up to a guessed size
         SCHK(hipMemcpyAsync(hx, dx, X.down, hipMemcpyDeviceToHost, st));
-        const uint64_t guess = std::min<uint64_t>(cap, 8ull * n + 1024);
+        // the first download's size: 8 NAMs a read, or 1.15 x the lane's last call's rate
+        const uint64_t guess =
+            std::min<uint64_t>(cap, (uint64_t)((double)n * std::max(8.0, 1.15 * b.nam_rate)) + 1024);
         SCHK(hipMemcpyAsync(out->nams, b.p[B_OUT], sizeof(rsa_nam) * guess, hipMemcpyDeviceToHost, st));
         // pool words copied before the total is known: ~1 accepted site a read, n_mm words each,
-        // or 12 + 4 n_mm with hamming_align's results
-        const uint64_t mm_guess = out->sites ? std::min<uint64_t>(out->mm_capacity, (out->hamming_align ? 3 : 1) * guess) : 0;
+        // or 12 + 4 n_mm with hamming_align's results (or 1.15 x the last call's words a NAM)
+        const double mm_a_nam = std::max((double)(out->hamming_align ? 3 : 1), 1.15 * b.mm_rate);
+        const uint64_t mm_guess =
+            out->sites ? std::min<uint64_t>(out->mm_capacity, (uint64_t)(mm_a_nam * (double)guess)) : 0;
         if (out->sites) {
             SCHK(hipMemcpyAsync(out->sites, b.p[B_SITES], sizeof(rsa_nam_site) * guess, hipMemcpyDeviceToHost, st));
             if (mm_guess) SCHK(hipMemcpyAsync(out->mm_pool, b.p[B_POOL], 2 * mm_guess, hipMemcpyDeviceToHost, st));
@@ -2518,7 +2710,10 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
         const uint64_t mm_used = out->sites ? std::min<uint64_t>(hh.mm_used, out->mm_capacity) : 0;
         if (out->sites) out->mm_used = mm_used;
         else out->mm_used = 0;
+        if (n) b.nam_rate = (double)total / (double)n;
+        if (total) b.mm_rate = (double)mm_used / (double)total;
         if (total > guess || mm_used > mm_guess) {   // rare: a second round trip for the rest
+            c.second_trip = 1;
             if (total > guess) {
                 SCHK(hipMemcpyAsync(out->nams + guess, DP(B_OUT, rsa_nam) + guess, sizeof(rsa_nam) * (total - guess),
                                     hipMemcpyDeviceToHost, st));

@@ -120,11 +120,12 @@ static int wait_workers(const Engine& eng, int threads) {
 }
 
 // Chunks' SAM text in chunk order (OutputBuffer::output_records, pc.cpp:119-135).
-// One writer thread of its own hands the text to the sink, so no worker ever
-// blocks on the output file and nobody contends for it: the page-cache writes of
-// one file are serialised by the kernel anyway (the inode lock), and parallel
-// pwrite()s only spun on that lock.  Workers wait only when more
-// than kMaxQueued bytes are waiting for the writer.
+// One writer thread of its own hands the text to the sink, so no worker blocks on
+// the output file behind other chunks and nobody contends for it: the page-cache
+// writes of one file are serialised by the kernel anyway (the inode lock), and
+// parallel pwrite()s only spun on that lock.  Workers wait only when
+// more than kMaxQueued bytes are waiting for the writer.
+
 struct OrderedSink {
     SamSink sink;
     void* user;
@@ -140,11 +141,20 @@ struct OrderedSink {
     SamDigest total;
     bool closing = false;
     std::thread writer;
+    // RSA_SINK_TRACE=<file>: one line a write (instrumentation): seconds since the sink opened
+    // at the call and at the return, bytes, bytes still queued, W
+    FILE* trace = nullptr;
+    Clock::time_point t_open = Clock::now();
     // `first`: the first chunk index this sink writes (a rank's part starts later)
     OrderedSink(SamSink s, void* u, bool d, size_t first = 0) : sink(s), user(u), digest(d), next(first) {
+        static const char* trace_path = getenv("RSA_SINK_TRACE");
+        if (sink && trace_path) trace = fopen(trace_path, "a");
         if (sink) writer = std::thread([this] { write_loop(); });
     }
-    ~OrderedSink() { close(); }
+    ~OrderedSink() {
+        close();
+        if (trace) fclose(trace);
+    }
     // every chunk written (the writer drained and stopped)
     void close() {
         {
@@ -206,11 +216,6 @@ struct OrderedSink {
     }
     void write_loop() {
         if (g_worker_start_hook) g_worker_start_hook();
-        // RSA_SINK_TRACE=<file>: one line a write (instrumentation): seconds since the
-        // writer started at the call and at the return, bytes, bytes still queued
-        static const char* trace_path = getenv("RSA_SINK_TRACE");
-        FILE* trace = trace_path ? fopen(trace_path, "a") : nullptr;
-        const auto t0 = Clock::now();
         std::unique_lock<std::mutex> g(m);
         for (;;) {
             cv.wait(g, [&] { return closing || !queue.empty(); });
@@ -219,16 +224,16 @@ struct OrderedSink {
             queue.pop_front();
             const size_t behind = queued_bytes;
             g.unlock();
-            const double ta = since(t0);
+            const double ta = since(t_open);
             sink(user, t.data(), t.size());
-            if (trace) fprintf(trace, "%.4f %.4f %zu %zu\n", ta, since(t0), t.size(), behind);
+            if (trace) fprintf(trace, "%.4f %.4f %zu %zu W\n", ta, since(t_open), t.size(), behind);
             const size_t n = t.size();
             give_back(t);
             g.lock();
             queued_bytes -= n;
             room_cv.notify_all();
         }
-        if (trace) { fprintf(trace, "end %.4f\n", since(t0)); fclose(trace); }
+        if (trace) fprintf(trace, "end %.4f\n", since(t_open));
     }
 };
 

@@ -108,7 +108,7 @@ class KernelStats(C.Structure):
                 ("scan_certified", C.c_uint64), ("scan_redo", C.c_uint64),
                 ("call_ms", C.c_double * 2), ("lane_wait_ms", C.c_double * 2), ("device_wait_ms", C.c_double * 2),
                 ("query_written", C.c_uint64), ("query_fixed_reads", C.c_uint64),
-                ("shared_checks", C.c_uint64), ("no_shared", C.c_uint64)]
+                ("shared_checks", C.c_uint64), ("no_shared", C.c_uint64), ("seed_second_trips", C.c_uint64)]
 
 
 def stats_dict(ks: "KernelStats") -> dict:

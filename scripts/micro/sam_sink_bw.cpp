@@ -4,6 +4,7 @@
 //   mmapT  : ftruncate to the total, MAP_SHARED mapping, T threads each copying
 //            every T-th chunk to its offset (each worker copying its own chunk)
 //   mmapPT : the same with MADV_POPULATE_WRITE of each chunk's range before the copy
+//   mmapFT : fallocate of the whole file first (blocks allocated up front), then as mmapPT
 //   cold   : write() of 200 distinct chunks filled beforehand (source out of cache, as the
 //            writer thread finds the chunks other workers formatted)
 //   coldB  : the same while B background threads copy memory (a busy host)
@@ -51,9 +52,11 @@ static double by_write(const std::string& path, const std::vector<char>& buf) {
     return kTotal / dt / 1e9;
 }
 
-static double by_mmap(const std::string& path, const std::vector<char>& buf, int threads, bool populate) {
+static double by_mmap(const std::string& path, const std::vector<char>& buf, int threads, bool populate,
+                      bool falloc = false) {
     int fd = open(path.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0644);
     const double t = now();
+    if (falloc && fallocate(fd, 0, 0, (off_t)kTotal) != 0) { perror("fallocate"); return 0; }
     if (ftruncate(fd, (off_t)kTotal) != 0) { perror("ftruncate"); return 0; }
     char* m = (char*)mmap(nullptr, kTotal, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
     if (m == MAP_FAILED) { perror("mmap"); return 0; }
@@ -172,6 +175,7 @@ int main(int argc, char** argv) {
             printf("%s (fs magic 0x%lx): write %.2f GB/s", argv[a], (unsigned long)sf.f_type, by_write(p, buf));
             for (int t : {1, 4, 8, 16}) printf(", mmap%d %.2f", t, by_mmap(p, buf, t, false));
             for (int t : {4, 8, 16}) printf(", mmapP%d %.2f", t, by_mmap(p, buf, t, true));
+            for (int t : {4, 8, 16}) printf(", mmapF%d %.2f", t, by_mmap(p, buf, t, true, true));
             printf(" GB/s\n");
             fflush(stdout);
         }

@@ -21,7 +21,7 @@ def calls(path):
             out.append((cur, float(f[1])))
             cur = []
         else:
-            cur.append((float(f[0]), float(f[1]), int(f[2]), int(f[3])))
+            cur.append((float(f[0]), float(f[1]), int(f[2]), int(f[3])) + ((f[4],) if len(f) > 4 else ("W",)))
     return out
 
 
@@ -31,8 +31,13 @@ def main():
         if not cur:
             continue
         gaps = [(cur[i][0] - cur[i - 1][1]) * 1e3 for i in range(1, len(cur))]
-        busy = sum(b - a for a, b, _, _ in cur)
-        nbytes = sum(n for _, _, n, _ in cur)
+        busy = sum(x[1] - x[0] for x in cur)
+        nbytes = sum(x[2] for x in cur)
+        for kind in ("W", "D"):                       # writer thread / direct hand-off (RSA_SINK_DIRECT)
+            k = [x for x in cur if x[4] == kind]
+            if k:
+                kb, kn = sum(x[1] - x[0] for x in k), sum(x[2] for x in k)
+                print(f"    {kind}: {len(k)} writes, {kn / 1e6:.0f} MB, {kn / max(kb, 1e-9) / 1e9:.2f} GB/s")
         big = [(i, round(g, 1)) for i, g in enumerate(gaps, 1) if g > 2.0]
         print(f"  first {cur[0][0] * 1e3:5.1f} ms  idle {sum(g for g in gaps if g > 0):5.1f} ms  busy {busy * 1e3:5.1f} ms "
               f"({nbytes / busy / 1e9:.2f} GB/s)  end {end * 1e3:5.1f} ms  gaps>2ms {big}")
