@@ -21,6 +21,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cstdio>
 #include <climits>
 #include <cstdlib>
 #include <cstring>
@@ -64,6 +66,17 @@ struct HitD {
 #define SEED_E_FIND 2u      // robin_hood emulation overflow in the global-map pass
 #define SEED_E_RESCUE 4u    // the same in the rescue pass
 #define SEED_E_SITE 8u      // k_sites met a NAM whose nam_id is outside its read's list (a broken permutation)
+// RSA_SEED_PROF builds (never the product): per-phase shader cycles of the fused
+// query kernel and k_find_nams_w2, summed over waves, printed by seed_run
+#ifdef RSA_SEED_PROF
+#define SPROF_READS 32768
+__device__ unsigned int g_seed_prof[SPROF_READS][20];    // per read (r < SPROF_READS), plain stores
+#define SPROF_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define SPROF_ADD(i, d) do { if (lane == 0 && r < SPROF_READS) g_seed_prof[r][i] = (unsigned int)(d); } while (0)
+#else
+#define SPROF_T(v)
+#define SPROF_ADD(i, d)
+#endif
 struct SeedHdr {
     unsigned long long pool_used;   // pool entries handed out
     unsigned long long total;       // final NAMs of the batch
@@ -306,7 +319,7 @@ __device__ __forceinline__ uint64_t rw_canon(uint64_t X, int n) {
     return fwd < rc ? fwd : rc;
 }
 
-__device__ __forceinline__ void rs_pick(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sp, int n, int i,
+__device__ __forceinline__ void rs_pick(const uint64_t* __restrict__ sh, const uint16_t* __restrict__ sp, int n, int i,
                                         bool rc, int len, const SeedIndexParams& p, uint64_t& h, uint32_t& a,
                                         uint32_t& b) {
     // syncmer x of the (possibly reversed) list: index n-1-x, position len - pos - k when reversed
@@ -331,7 +344,7 @@ __device__ __forceinline__ void rs_pick(const uint64_t* __restrict__ sh, const u
 // syncmer count n, with their canonical k-mer hashes in hs[0, n) and positions in sp[0, n).
 // s_nw is a wave-private LDS int (the tie walk's count).
 __device__ __forceinline__ int rw_syncmers(const char* __restrict__ sq, int len, const SeedIndexParams& p, int lane,
-                                           uint32_t* cw, uint32_t* nm, uint64_t* hs, uint32_t* sp, int* s_nw) {
+                                           uint32_t* cw, uint32_t* nm, uint64_t* hs, uint16_t* sp, int* s_nw) {
     const int k = p.k, sl = p.s, W = k - sl + 1;
     // 1. codes and N mask
     for (int i = lane; i < RW_MAXLEN / 16 + 4; i += 64) cw[i] = 0;
@@ -369,7 +382,7 @@ __device__ __forceinline__ int rw_syncmers(const char* __restrict__ sq, int len,
             sync = mo == p.t - 1;
         }
         const uint64_t b = __ballot(sync);
-        if (sync) sp[n + __popcll(b & ((1ULL << lane) - 1))] = (uint32_t)(pe - k + 1);
+        if (sync) sp[n + __popcll(b & ((1ULL << lane) - 1))] = (uint16_t)(pe - k + 1);
         n += __popcll(b);
     }
     if (__ballot(tie)) {                                // wave-uniform
@@ -398,7 +411,7 @@ __device__ __forceinline__ int rw_syncmers(const char* __restrict__ sq, int len,
                     min_val = hw[W - 1];
                     min_pos = i - sl + 1;
                 }
-                if (min_pos == i - k + p.t) sp[nn++] = (uint32_t)(i - k + 1);
+                if (min_pos == i - k + p.t) sp[nn++] = (uint16_t)(i - k + 1);
             }
             *s_nw = nn;
         }
@@ -417,7 +430,7 @@ __device__ __forceinline__ int rw_syncmers(const char* __restrict__ sq, int len,
     __shared__ uint32_t s_code[RW_WAVES][RW_MAXLEN / 16 + 4];                                \
     __shared__ uint32_t s_nm[RW_WAVES][RW_MAXLEN / 32 + 4];                                  \
     __shared__ uint64_t s_h[RW_WAVES][RW_MAXLEN];   /* s-mer hash by end, then k-mer hashes */ \
-    __shared__ uint32_t s_sp[RW_WAVES][RW_MAXLEN];  /* syncmer positions */                  \
+    __shared__ uint16_t s_sp[RW_WAVES][RW_MAXLEN];  /* syncmer positions (< RW_MAXLEN) */    \
     __shared__ int s_n[RW_WAVES]
 
 // rsa_randstrobes (the randstrobe API): every query randstrobe written out
@@ -433,7 +446,7 @@ k_rs_wave(const char* __restrict__ seq, const uint64_t* __restrict__ roff, const
     if (len > RW_MAXLEN) return;                        // k_randstrobes takes it
     if (len < p.w_max) { if (lane == 0) qcnt[r] = 0; return; }   // randstrobes.cpp:209
     uint64_t* hs = s_h[w];
-    uint32_t* sp = s_sp[w];
+    uint16_t* sp = s_sp[w];
     const int n = rw_syncmers(seq + roff[r], len, p, lane, s_code[w], s_nm[w], hs, sp, &s_n[w]);
     // 4b. randstrobes, forward then reverse complement
     const int m = n > p.w_min ? n - p.w_min : 0;
@@ -485,6 +498,10 @@ __device__ __forceinline__ int wave_excl_scan_lk(int v, int lane, int& total) {
     return x - v;
 }
 
+__device__ __forceinline__ QrsInfo lookup_hit(const rsa_query_randstrobe& q, const SeedIndexParams& p, bool hit,
+                                              uint64_t a, uint64_t lo, uint64_t ub, const rsa_ref_randstrobe* eb,
+                                              bool one = false);
+
 // One query randstrobe against the index (index.hpp:57-93, nam.cpp:68-85): its
 // QrsInfo, and the run of equal hashes as eb[lo, ub)
 __device__ __forceinline__ QrsInfo lookup_one(const rsa_query_randstrobe& q, const SeedIndexParams& p, uint64_t& lo,
@@ -535,6 +552,17 @@ __device__ __forceinline__ QrsInfo lookup_one(const rsa_query_randstrobe& q, con
             if (hit) ub = upper_bound_hash(eb, lo, b - a, q.hash);
         }
     }
+    return lookup_hit(q, p, hit, a, lo, ub, eb);
+}
+
+// The QrsInfo of a query randstrobe whose run of equal hashes is eb[lo, ub) (hit)
+// in the bucket starting at index entry a
+// (one: the run is a single entry, whose span the caller holds: one hit)
+__device__ __forceinline__ QrsInfo lookup_hit(const rsa_query_randstrobe& q, const SeedIndexParams& p, bool hit,
+                                              uint64_t a, uint64_t lo, uint64_t ub, const rsa_ref_randstrobe* eb,
+                                              bool one) {
+    QrsInfo o;
+    o.pos = END64; o.count = 0; o.hits = 0; o.flags = 0; o.pad = 0;
     if (hit) {
         o.pos = a + lo;
         o.flags = 1;
@@ -543,7 +571,9 @@ __device__ __forceinline__ QrsInfo lookup_one(const rsa_query_randstrobe& q, con
         // ub - lo > filter_cutoff, and the probe's random line is not fetched
         if (ub - lo > (uint64_t)p.filter_cutoff) o.flags |= 2;
         o.count = (uint32_t)min<uint64_t>(ub - lo, 0xFFFFFFFFull);
-        if (o.count <= 1000) {
+        if (one) {
+            o.hits = 1;                                 // the first entry always passes the min_diff filter
+        } else if (o.count <= 1000) {
             // add_to_hits_per_ref min_diff filter (nam.cpp:68-85)
             int min_diff = INT_MAX;
             uint32_t h = 0;
@@ -559,6 +589,93 @@ __device__ __forceinline__ QrsInfo lookup_one(const rsa_query_randstrobe& q, con
         }
     }
     return o;
+}
+
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+    return (uint64_t)hi << 32 | lo;
+}
+
+// lookup_one for a whole wave over the BucketLine table (p.lines set; called by
+// every lane, `valid` marks the lanes with a query randstrobe).  The lines are
+// fetched cooperatively: in instruction j the 8 lanes of group g = lane / 8 load
+// the 16-byte parts of the line of lane 8j + g, so each load instruction touches
+// 8 lines, whole, instead of 64 (a lane walking its own line issues 8 loads to
+// it: 8x the address translations and requests).  Lines and keys go to the
+// groups through the wave's LDS (s_top, s_key: 64 entries), each group compares
+// its line's entries with the owner's key (two ballots), and the bounds come
+// back to the owners through s_ab; buckets over BL_CAP are searched in p.rs by
+// the owner as before.
+__device__ __forceinline__ QrsInfo lookup_coop(const rsa_query_randstrobe& q, bool valid, const SeedIndexParams& p,
+                                               int lane, uint64_t& lo, uint64_t& ub, const rsa_ref_randstrobe*& eb,
+                                               uint64_t* s_top, uint64_t* s_key, uint4* s_ab, uint2* s_ent,
+                                               bool& one, uint2& ent, unsigned long long* prof) {
+    // a lane without a randstrobe fetches line 0 (its results are dropped): the
+    // loads stay unconditional, so all eight are in flight at once
+    const uint64_t top = valid ? q.hash >> (64 - p.bits) : 0;
+    const int g = lane >> 3, part = lane & 7;
+    s_top[lane] = top;
+    s_key[lane] = q.hash;
+    WSYNC_SEED();
+    uint4 w[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j] = ((const uint4*)(p.lines + s_top[8 * j + g]))[part];
+#ifdef RSA_SEED_PROF
+    const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_s_waitcnt(0x0F70);                   // vmcnt(0): the lines are in
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+    prof[0] += c1 - c0;
+#endif
+    uint32_t own_lt = 0, own_le = 0;                      // the owner's group: entries < / <= its key
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint64_t kj = s_key[8 * j + g];
+        const uint64_t x0 = (uint64_t)w[j].x | (uint64_t)w[j].y << 32;    // part 0: start; else: entry hash
+        const uint64_t mlt = __ballot(part >= 1 && x0 < kj), mle = __ballot(part >= 1 && x0 <= kj);
+        if (part == 0) s_ab[8 * j + g] = w[j];            // the bounds of line 8j + g
+        if (part >= 1 && x0 == kj) s_ent[8 * j + g] = make_uint2(w[j].z, w[j].w);   // an equal entry's position, packed
+        if ((lane >> 3) == j) {
+            own_lt = (uint32_t)(mlt >> (8 * (lane & 7))) & 0xFFu;
+            own_le = (uint32_t)(mle >> (8 * (lane & 7))) & 0xFFu;
+        }
+    }
+    WSYNC_SEED();
+    const uint4 ab = s_ab[lane];
+    ent = s_ent[lane];
+    one = false;
+    const uint64_t a = (uint64_t)ab.x | (uint64_t)ab.y << 32, b = (uint64_t)ab.z | (uint64_t)ab.w << 32;
+#ifdef RSA_SEED_PROF
+    const unsigned long long c2 = __builtin_amdgcn_s_memtime();
+    prof[1] += c2 - c1;
+#endif
+    bool hit = false;
+    lo = 0; ub = 0;
+    eb = p.rs;
+    if (valid) {
+        if (b - a <= BL_CAP) {
+            eb = p.lines[top].e;
+            const uint32_t in = ((1u << (uint32_t)(b - a)) - 1u) << 1;   // parts 1 .. c hold the entries
+            lo = (uint32_t)__popc(own_lt & in); ub = (uint32_t)__popc(own_le & in);
+            hit = ub > lo;
+            // a run of one entry, and the only equal part of the line (so s_ent holds it)
+            one = ub == lo + 1 && __popc(own_le ^ own_lt) == 1;
+        } else {
+            eb = p.rs + a;
+            lo = lower_bound_hash(eb, 0, b - a, q.hash);
+            hit = lo < b - a && eb[lo].hash == q.hash;
+            if (hit) ub = upper_bound_hash(eb, lo, b - a, q.hash);
+        }
+    }
+#ifdef RSA_SEED_PROF
+    const unsigned long long c3 = __builtin_amdgcn_s_memtime();
+    prof[2] += c3 - c2;
+    const QrsInfo o = lookup_hit(q, p, hit, a, lo, ub, eb, one);
+    const unsigned long long c4 = __builtin_amdgcn_s_memtime();
+    prof[3] += c4 - c3;
+    return o;
+#else
+    return lookup_hit(q, p, hit, a, lo, ub, eb, one);
+#endif
 }
 
 // a read's lookup statistics (ReadStat fields)
@@ -591,9 +708,19 @@ struct LkStat {
 };
 
 // the hits of one non-filtered randstrobe (add_to_hits_per_ref order) into slot[at, ...)
+// (one: the run is the single entry {position, packed} = ent)
 __device__ __forceinline__ void lk_emit(const rsa_query_randstrobe& q, uint64_t lo, uint64_t ub,
-                                        const rsa_ref_randstrobe* eb, const SeedIndexParams& p, HitD* slot, int at) {
+                                        const rsa_ref_randstrobe* eb, const SeedIndexParams& p, HitD* slot, int at,
+                                        bool one = false, uint2 ent = make_uint2(0u, 0u)) {
     const int qs = (int)q.start, qe = (int)q.end;
+    if (one) {
+        HitD hd;
+        hd.qs = qs; hd.qe = qe; hd.rs = (int)ent.x; hd.re = (int)ent.x + (int)(ent.y & 0xFF) + p.k;
+        hd.list = (int32_t)(ent.y >> 8);
+        hd.pad = q.is_reverse ? 1 : 0;
+        slot[at] = hd;
+        return;
+    }
     int min_diff = INT_MAX, h = at;
     for (uint64_t e = lo; e < ub; ++e) {
         const rsa_ref_randstrobe x = eb[e];
@@ -671,6 +798,9 @@ k_seed_query(const char* __restrict__ seq, const uint64_t* __restrict__ roff, co
              rsa_query_randstrobe* __restrict__ qrs, uint32_t* __restrict__ qcnt, QrsInfo* __restrict__ qi,
              ReadStat* __restrict__ st, HitD* __restrict__ hit_slots) {
     RW_LDS_DECL;
+    __shared__ uint64_t s_top[RW_WAVES][64], s_key[RW_WAVES][64];   // lookup_coop's exchange
+    __shared__ uint4 s_ab[RW_WAVES][64];
+    __shared__ uint2 s_ent[RW_WAVES][64];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int r = blockIdx.x * RW_WAVES + w;
     if (r >= n_reads) return;                           // the whole wave leaves together
@@ -681,34 +811,58 @@ k_seed_query(const char* __restrict__ seq, const uint64_t* __restrict__ roff, co
         return;
     }
     uint64_t* hs = s_h[w];
-    uint32_t* sp = s_sp[w];
+    uint16_t* sp = s_sp[w];
+    SPROF_T(q0);
     const int n = rw_syncmers(seq + roff[r], len, p, lane, s_code[w], s_nm[w], hs, sp, &s_n[w]);
+    SPROF_T(q1);
     const int m = n > p.w_min ? n - p.w_min : 0;
     const int nq = 2 * m;
     HitD* slot = hit_slots + (size_t)r * LK_HCAP;
     LkStat ls;
     int hoff = 0;
+    unsigned long long acc_wait[4] = {0, 0, 0, 0};      // RSA_SEED_PROF: lookup_coop's phases
+#ifdef RSA_SEED_PROF
+    unsigned long long acc_pick = 0, acc_coop = 0, acc_emit = 0;
+#endif
     for (int i0 = 0; i0 < nq; i0 += 64) {
+        SPROF_T(l0);
         const int x = i0 + lane;
         QrsInfo o;
         o.flags = 0; o.hits = 0;
         rsa_query_randstrobe q;
         uint64_t lo = 0, ub = 0;
+        bool one = false;                               // lookup_coop: a single-entry run, held in ent
+        uint2 ent = make_uint2(0u, 0u);
         const rsa_ref_randstrobe* eb = p.rs;
+        q.hash = 0; q.start = 0; q.end = 0; q.is_reverse = 0; q.pad_ = 0;
         if (x < nq) {
             const bool rcx = x >= m;
             uint64_t h; uint32_t a, b;
             rs_pick(hs, sp, n, rcx ? x - m : x, rcx, len, p, h, a, b);
             q.hash = h; q.start = a; q.end = b + (uint32_t)p.k; q.is_reverse = rcx ? 1 : 0; q.pad_ = 0;
-            o = lookup_one(q, p, lo, ub, eb);
-            ls.add(o);
         }
+        SPROF_T(l1);
+        if (p.lines) {                                  // kernel-uniform: the whole wave
+            const QrsInfo oc = lookup_coop(q, x < nq, p, lane, lo, ub, eb, s_top[w], s_key[w], s_ab[w], s_ent[w], one,
+                                           ent, acc_wait);
+            if (x < nq) o = oc;
+        } else if (x < nq) {
+            o = lookup_one(q, p, lo, ub, eb);
+        }
+        if (x < nq) ls.add(o);
+        SPROF_T(l2);
         const bool emit = (o.flags & 1) && !(o.flags & 2) && o.hits > 0;
         int tot;
         const int at = hoff + wave_excl_scan_lk(emit ? (int)o.hits : 0, lane, tot);
-        if (emit && at + (int)o.hits <= LK_HCAP) lk_emit(q, lo, ub, eb, p, slot, at);
+        if (emit && at + (int)o.hits <= LK_HCAP) lk_emit(q, lo, ub, eb, p, slot, at, one, ent);
         hoff += tot;
+#ifdef RSA_SEED_PROF
+        SPROF_T(l3);
+        acc_pick += l1 - l0; acc_coop += l2 - l1; acc_emit += l3 - l2;
+#endif
     }
+    SPROF_ADD(11, acc_pick); SPROF_ADD(12, acc_coop); SPROF_ADD(13, acc_emit); SPROF_ADD(14, acc_wait[0]); SPROF_ADD(15, acc_wait[1]); SPROF_ADD(16, acc_wait[2]); SPROF_ADD(17, acc_wait[3]);
+    SPROF_T(q2);
     ls.wave_sum();                                      // every lane holds the read's totals
     const float nonrep = ls.found > 0 ? (float)ls.good / (float)ls.found : 1.0f;   // nam.cpp:920
     const bool need = qw_mode == 2 ||
@@ -728,6 +882,8 @@ k_seed_query(const char* __restrict__ seq, const uint64_t* __restrict__ roff, co
         }
     }
     if (lane == 0) { qcnt[r] = (uint32_t)nq; st[r] = ls.to_stat(need ? 1u : 0u); }
+    SPROF_T(q3);
+    SPROF_ADD(0, q1 - q0); SPROF_ADD(1, q2 - q1); SPROF_ADD(2, q3 - q2); SPROF_ADD(3, 1);
 }
 
 // The query randstrobes and QrsInfo of read r on one lane, for a read the fused
@@ -1182,13 +1338,12 @@ __device__ void find_nams_read(int r, const rsa_query_randstrobe* __restrict__ q
 //   2. lane 0 inserts the keys into the two robin_hood emulations (LDS) in
 //      hit order; the occupied slots, fwd map then rc map, give the list order
 //      merge_hits_into_nams walks (nam.cpp:370-536)
-//   3. one lane per list runs the merge.  The maps are dead by then and their
-//      LDS holds the NAMs: a list with c hits creates at most c NAMs, so it
-//      owns c entries at its hit offset.  NAMs stay where they were created
-//      and carry the sequence number of their emission (flush of passed
-//      NAMs, then the final sweep), which is their place in the output; the
-//      open set is "created and not yet emitted", in creation order, exactly
-//      the reference's open_nams vector.
+//   3. the lists one after another, the whole wave on each (merge_list_wave):
+//      NAMs in registers, one a lane, in creation order; they carry the
+//      sequence number of their emission (flush of passed NAMs, then the final
+//      sweep), which is their place in the output; the open set is "created
+//      and not yet emitted", in creation order, exactly the reference's
+//      open_nams vector.
 // Reads with more than FN2_HCAP hits or whose maps would rehash past
 // FN_MAP_CAP are flagged (flags = 2) for the global-scratch kernel above.
 // ---------------------------------------------------------------------------
@@ -1196,83 +1351,98 @@ __device__ void find_nams_read(int r, const rsa_query_randstrobe* __restrict__ q
 #define FN2_HCAP 128
 #define FN2_MAPB (2 * FN_MAP_CAP * 9)
 
-struct __attribute__((aligned(16))) SeqNam {   // a NAM under construction (nam.hpp:11-38 fields)
-    int32_t qs, qe, qprev, rs, re, rprev, n_hits, seq;   // seq < 0: open
-};
-static_assert(FN2_HCAP * sizeof(SeqNam) <= FN2_MAPB, "NAM store shares the maps' LDS");
-
-__device__ __forceinline__ int wave_excl_scan(int v, int lane, int& total) {
-    int x = v;
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    total = __shfl(x, 63, 64);
-    return x - v;
-}
 
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 typedef __attribute__((address_space(3))) HitD LHit;
-typedef __attribute__((address_space(3))) SeqNam LSeq;
 typedef __attribute__((address_space(3))) int2 LInt2;
 
-// merge_hits_into_nams for one list (nam.cpp:370-536); returns the NAMs emitted
-__device__ int merge_list_seq(int32_t lid, const LHit* hits, int n_hits, int k, LSeq* a, int& n_created) {
-    int n_out = 0, first_open = 0;
-    n_created = 0;
-    unsigned prev_q_start = 0;
-    for (int hi = 0; hi < n_hits; ++hi) {
-        if (hits[hi].list != lid) continue;
-        const int xqs = hits[hi].qs, xqe = hits[hi].qe, xrs = hits[hi].rs, xre = hits[hi].re;
-        bool added = false;
-        for (int o = first_open; o < n_created; ++o) {
-            LSeq& on = a[o];
-            if (on.seq >= 0) continue;
-            if (on.qprev < xqs && xqs <= on.qe && on.rprev < xrs && xrs <= on.re) {
-                if (xqe > on.qe && xre > on.re) {
-                    on.qe = xqe; on.re = xre; on.qprev = xqs; on.rprev = xrs; on.n_hits++;
-                    added = true; break;
-                } else if (xqe <= on.qe && xre <= on.re) {
-                    on.qprev = xqs; on.rprev = xrs; on.n_hits++;
-                    added = true; break;
-                }
-            }
-        }
-        if (!added) {
-            LSeq& nn = a[n_created++];
-            nn.qs = xqs; nn.qe = xqe; nn.qprev = xqs; nn.rs = xrs; nn.re = xre; nn.rprev = xrs;
-            nn.n_hits = 1; nn.seq = -1;
-        }
-        if ((unsigned)xqs > prev_q_start + (unsigned)k) {      // emit the NAMs the query has passed
-            for (int o = first_open; o < n_created; ++o)
-                if (a[o].seq < 0 && a[o].qe < xqs) a[o].seq = n_out++;
-            while (first_open < n_created && a[first_open].seq >= 0) first_open++;
-            prev_q_start = (unsigned)xqs;
-        }
-    }
-    for (int o = first_open; o < n_created; ++o)
-        if (a[o].seq < 0) a[o].seq = n_out++;
-    return n_out;
+// a hit's fields on its lane (list = -1: no hit)
+struct WaveHit { int qs, qe, rs, re, list; };
+__device__ __forceinline__ WaveHit load_wave_hit(const LHit* hits, int h, int n_hits) {
+    WaveHit x;
+    x.qs = x.qe = x.rs = x.re = 0; x.list = -1;
+    if (h < n_hits) { x.qs = hits[h].qs; x.qe = hits[h].qe; x.rs = hits[h].rs; x.re = hits[h].re; x.list = hits[h].list; }
+    return x;
 }
 
-// inserts the keys of one orientation's hits (operator[], nam.cpp:68-85) and
-// rewrites their list field to the list id | orientation << 30
-__device__ __forceinline__ void map_insert_hits(LMap& m, int orient, LHit* hits, int n_hits) {
-    rh_new_reserved(m);
-    int n_lists = 0;
-    uint32_t last_key = 0;
-    int32_t last_lid = -1;
-    for (int h = 0; h < n_hits; ++h) {
-        if (hits[h].pad != orient) continue;
-        const uint32_t key = (uint32_t)hits[h].list;
-        if (last_lid < 0 || key != last_key) {          // operator[] on a present key changes nothing
-            bool ins;
-            last_lid = rh_get_or_insert(m, key, n_lists, ins);
-            if (ins) n_lists++;
-            last_key = key;
+// a NAM under construction in a lane's registers (nam.hpp:11-38 fields); seq < 0: open
+struct RegNam { int qs, qe, qprev, rs, re, rprev, n_hits, seq; };
+
+// does hit x extend NAM a (the two accepting branches of nam.cpp merge_hits_into_nams)
+__device__ __forceinline__ bool nam_takes(const RegNam& a, int xqs, int xqe, int xrs, int xre) {
+    return a.seq < 0 && a.qprev < xqs && xqs <= a.qe && a.rprev < xrs && xrs <= a.re &&
+           ((xqe > a.qe && xre > a.re) || (xqe <= a.qe && xre <= a.re));
+}
+__device__ __forceinline__ void nam_take(RegNam& a, int xqs, int xqe, int xrs, int xre) {
+    if (xqe > a.qe && xre > a.re) { a.qe = xqe; a.re = xre; }
+    a.qprev = xqs; a.rprev = xrs; a.n_hits++;
+}
+__device__ __forceinline__ void nam_open(RegNam& a, int xqs, int xqe, int xrs, int xre) {
+    a.qs = xqs; a.qe = xqe; a.qprev = xqs; a.rs = xrs; a.re = xre; a.rprev = xrs; a.n_hits = 1; a.seq = -1;
+}
+__device__ __forceinline__ void nam_write(const RegNam& a, int base, int ref_id, int orient, rsa_nam* out) {
+    rsa_nam x;
+    x.nam_id = base + a.seq;                                // position in the read's NAM vector
+    x.query_start = a.qs; x.query_end = a.qe; x.query_prev_hit_startpos = a.qprev;
+    x.ref_start = a.rs; x.ref_end = a.re; x.ref_prev_hit_startpos = a.rprev;
+    x.n_hits = a.n_hits; x.ref_id = ref_id; x.score = 0.0f; x.is_rc = orient;
+    x.score = nam_score(x);
+    out[x.nam_id] = x;
+}
+
+// merge_hits_into_nams for list `lid` on the whole wave; writes its NAMs at
+// out[base + emission order] and returns their number
+__device__ int merge_list_wave(int lid, const WaveHit& h0, const WaveHit& h1, int n_hits, int k, int lane, int ref_id,
+                               rsa_nam* out, int base) {
+    RegNam A, B;                                            // NAM lane (bank 0), lane + 64 (bank 1)
+    nam_open(A, 0, 0, 0, 0); nam_open(B, 0, 0, 0, 0);
+    int n_created = 0, n_out = 0;
+    unsigned prev_q_start = 0;
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (int c = 0; c < 2 && c * 64 < n_hits; ++c) {
+        const WaveHit& hv = c ? h1 : h0;
+        uint64_t mask = __ballot(hv.list == lid);
+        while (mask) {
+            const int h = __builtin_ctzll(mask);
+            mask &= mask - 1;
+            const int xqs = __builtin_amdgcn_readlane(hv.qs, h), xqe = __builtin_amdgcn_readlane(hv.qe, h);
+            const int xrs = __builtin_amdgcn_readlane(hv.rs, h), xre = __builtin_amdgcn_readlane(hv.re, h);
+            const bool inA = lane < n_created, inB = lane + 64 < n_created;
+            const uint64_t mA = __ballot(inA && nam_takes(A, xqs, xqe, xrs, xre));
+            if (mA) {
+                if (lane == __builtin_ctzll(mA)) nam_take(A, xqs, xqe, xrs, xre);
+            } else {
+                const uint64_t mB = n_created > 64 ? __ballot(inB && nam_takes(B, xqs, xqe, xrs, xre)) : 0ull;
+                if (mB) {
+                    if (lane == __builtin_ctzll(mB)) nam_take(B, xqs, xqe, xrs, xre);
+                } else {
+                    if (n_created < 64) { if (lane == n_created) nam_open(A, xqs, xqe, xrs, xre); }
+                    else if (lane + 64 == n_created) nam_open(B, xqs, xqe, xrs, xre);
+                    n_created++;
+                }
+            }
+            if ((unsigned)xqs > prev_q_start + (unsigned)k) {       // emit the NAMs the query has passed
+                const bool eA = lane < n_created && A.seq < 0 && A.qe < xqs;
+                const bool eB = lane + 64 < n_created && B.seq < 0 && B.qe < xqs;
+                const uint64_t bA = __ballot(eA), bB = __ballot(eB);
+                if (eA) A.seq = n_out + __popcll(bA & below);
+                if (eB) B.seq = n_out + __popcll(bA) + __popcll(bB & below);
+                n_out += __popcll(bA) + __popcll(bB);
+                prev_q_start = (unsigned)xqs;
+            }
         }
-        hits[h].list = last_lid | (orient << 30);
     }
+    {                                                       // the final sweep, creation order
+        const bool eA = lane < n_created && A.seq < 0, eB = lane + 64 < n_created && B.seq < 0;
+        const uint64_t bA = __ballot(eA), bB = __ballot(eB);
+        if (eA) A.seq = n_out + __popcll(bA & below);
+        if (eB) B.seq = n_out + __popcll(bA) + __popcll(bB & below);
+        n_out += __popcll(bA) + __popcll(bB);
+    }
+    const int orient = (lid >> 30) & 1;
+    if (lane < n_created) nam_write(A, base, ref_id, orient, out);
+    if (lane + 64 < n_created) nam_write(B, base, ref_id, orient, out);
+    return n_out;
 }
 
 __global__ void __launch_bounds__(64 * FN2_WAVES)
@@ -1297,11 +1467,17 @@ k_find_nams_w2(const ReadStat* __restrict__ st, const HitD* __restrict__ hit_slo
         return;
     }
     LHit* hits = LDS_PTR(HitD, s_hits[w]);
+    SPROF_T(f0);
     // 1. the read's hits, written in add_to_hits_per_ref order by k_lookup
     const int n_hits = (int)rs.hits_find;
     const HitD* slot = hit_slots + (size_t)r * LK_HCAP;
-    for (int h = lane; h < n_hits; h += 64) st_hit(&hits[h], slot[h]);
+    const bool v0 = lane < n_hits, v1 = lane + 64 < n_hits;
+    HitD x0, x1;
+    x0.list = x1.list = 0; x0.pad = x1.pad = 0;
+    if (v0) { x0 = slot[lane]; st_hit(&hits[lane], x0); }
+    if (v1) { x1 = slot[lane + 64]; st_hit(&hits[lane + 64], x1); }
     WSYNC_SEED();
+    SPROF_T(f1);
     // 2. the two robin_hood maps (fwd, rc) in LDS
     LMap m0, m1;
     {
@@ -1315,23 +1491,80 @@ k_find_nams_w2(const ReadStat* __restrict__ st, const HitD* __restrict__ hit_slo
         m0.info2 = m1.info2 = nullptr; m0.keys2 = m1.keys2 = nullptr; m0.vals2 = m1.vals2 = nullptr;  // rehash -> fallback
     }
     if (lane == 0) nonrep[r] = rs.found > 0 ? (float)rs.good / (float)rs.found : 1.0f;   // nam.cpp:920
+    // operator[] on the key just looked up changes nothing (nam.cpp:68-85), so only
+    // the first hit of each run of equal keys, in its orientation's hit order,
+    // touches the map: the runs come from ballots, the map insertions stay in hit
+    // order on one lane per map, and the rest of each run copies its list id
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    uint64_t M[2][2], S[2][2];                         // [orientation][hit chunk]: hits, run starts
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+        M[o][0] = __ballot(v0 && (int)x0.pad == o);
+        M[o][1] = __ballot(v1 && (int)x1.pad == o);
+    }
+    uint32_t last0[2];                                  // key of each orientation's last hit in chunk 0
+#pragma unroll
+    for (int o = 0; o < 2; ++o)
+        last0[o] = M[o][0] ? (uint32_t)__builtin_amdgcn_readlane(x0.list, 63 - __builtin_clzll(M[o][0])) : 0u;
+    bool start0 = false, start1 = false;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const HitD& x = c ? x1 : x0;
+        const bool v = c ? v1 : v0;
+        const int o = (int)x.pad & 1;
+        const uint64_t pm = (o ? M[1][c] : M[0][c]) & below;
+        const uint32_t pk = (uint32_t)__shfl(x.list, pm ? 63 - __builtin_clzll(pm) : lane, 64);
+        bool has_prev = pm != 0;
+        uint32_t prevk = pk;
+        if (c == 1 && !pm && (o ? M[1][0] : M[0][0])) { has_prev = true; prevk = last0[o]; }
+        const bool st_ = v && (!has_prev || prevk != (uint32_t)x.list);
+        S[0][c] = __ballot(st_ && o == 0);
+        S[1][c] = __ballot(st_ && o == 1);
+        if (c) start1 = st_; else start0 = st_;
+    }
     if (lane < 2) {
         // each map sees its own keys in hit order, which fixes its slot layout; list
         // ids only have to be distinct, so each map numbers its lists itself: lane 0
         // fills the fwd map while lane 1 fills the rc map (each writes only its own
-        // orientation's hits).  The map is built by value per lane: picking m0 or m1
-        // by reference would take their addresses (scratch).
+        // orientation's run starts).  The map is built by value per lane: picking m0
+        // or m1 by reference would take their addresses (scratch).
         LMap m;
         uint8_t* bm = s_map[w] + (size_t)lane * FN_MAP_CAP * 9;
         m.cap = FN_MAP_CAP;
         m.keys = LDS_PTR(uint32_t, bm); m.vals = LDS_PTR(int32_t, bm + (size_t)FN_MAP_CAP * 4);
         m.info = LDS_PTR(uint8_t, bm + (size_t)FN_MAP_CAP * 8);
         m.info2 = nullptr; m.keys2 = nullptr; m.vals2 = nullptr;   // rehash -> fallback
-        map_insert_hits(m, lane, hits, n_hits);
+        rh_new_reserved(m);
+        int n_lists = 0;
+        for (int c = 0; c < 2; ++c) {
+            uint64_t mask = lane ? S[1][c] : S[0][c];
+            while (mask) {
+                const int h = 64 * c + (int)__builtin_ctzll(mask);
+                mask &= mask - 1;
+                bool ins;
+                const int32_t lid = rh_get_or_insert(m, (uint32_t)hits[h].list, n_lists, ins);
+                if (ins) n_lists++;
+                hits[h].list = lid | (lane << 30);
+            }
+        }
         s_ctl[w][1 + lane] = (int)m.nwb;
         s_ctl[w][3 - lane * 3] = m.overflow ? 1 : 0;         // lane 0 -> [3], lane 1 -> [0]
     }
     WSYNC_SEED();
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {                       // the rest of each run: its start's list id
+        const HitD& x = c ? x1 : x0;
+        const bool v = c ? v1 : v0;
+        const int o = (int)x.pad & 1;
+        if (v && !(c ? start1 : start0)) {
+            const uint64_t sm = (o ? S[1][c] : S[0][c]) & below;
+            const uint64_t s0 = o ? S[1][0] : S[0][0];
+            const int st_h = sm ? 64 * c + 63 - __builtin_clzll(sm) : 63 - __builtin_clzll(s0);
+            hits[64 * c + lane].list = hits[st_h].list;
+        }
+    }
+    WSYNC_SEED();
+    SPROF_T(f2);
     if (s_ctl[w][0] | s_ctl[w][3]) {
         if (lane == 0) {
             flags[r] = 2; ncnt[r] = 0;
@@ -1373,41 +1606,26 @@ k_find_nams_w2(const ReadStat* __restrict__ st, const HitD* __restrict__ hit_slo
         }
         nl += occ;
     }
-    WSYNC_SEED();                                        // maps dead from here: their LDS holds NAMs
-    LSeq* store = LDS_PTR(SeqNam, s_map[w]);
+    WSYNC_SEED();
+    SPROF_T(f3);
     rsa_nam* out = nam_buf + (size_t)r * FN2_HCAP;          // a read's fixed NAM slot (NAMs <= hits)
-    // 3. one lane per list, 64 lists a round
-    int hbase = 0, obase = 0;
-    for (int l0 = 0; l0 < nl; l0 += 64) {
-        const int l = l0 + lane;
-        int cnt = 0;
-        int2 li = make_int2(0, 0);
-        if (l < nl) {
-            li.x = order[l].x;
-            li.y = order[l].y;
-            for (int h = 0; h < n_hits; ++h) cnt += hits[h].list == li.x;
-        }
-        int tot;
-        const int hb = hbase + wave_excl_scan(cnt, lane, tot);
-        hbase += tot;
-        int n_out = 0, n_created = 0;
-        if (l < nl) n_out = merge_list_seq(li.x, hits, n_hits, p.k, store + hb, n_created);
-        int total;
-        const int ob = obase + wave_excl_scan(n_out, lane, total);
-        obase += total;
-        const int orient = (li.x >> 30) & 1;
-        for (int c = 0; c < n_created; ++c) {
-            const LSeq& s = store[hb + c];
-            rsa_nam x;
-            x.nam_id = ob + s.seq;                        // position in the read's NAM vector
-            x.query_start = s.qs; x.query_end = s.qe; x.query_prev_hit_startpos = s.qprev;
-            x.ref_start = s.rs; x.ref_end = s.re; x.ref_prev_hit_startpos = s.rprev;
-            x.n_hits = s.n_hits; x.ref_id = li.y; x.score = 0.0f; x.is_rc = orient;
-            x.score = nam_score(x);
-            out[x.nam_id] = x;
-        }
+    // 3. merge_hits_into_nams (nam.cpp:370-536), one list after another in list
+    //    order, the whole wave on one list: hit h's fields sit on lane h % 64
+    //    (bank h / 64) and come out by readlane in hit order; NAM o (creation
+    //    order) lives in the registers of lane o % 64, bank o / 64.  "The first
+    //    open NAM the hit extends" is the lowest set bit of a ballot, the flush
+    //    of passed NAMs a ballot ranked by creation order.
+    WaveHit h0 = load_wave_hit(hits, lane, n_hits), h1 = load_wave_hit(hits, lane + 64, n_hits);
+    int obase = 0;
+    for (int l = 0; l < nl; ++l) {
+        const int lid = order[l].x, ref_id = order[l].y;
+        const int n_out = merge_list_wave(lid, h0, h1, n_hits, p.k, lane, ref_id, out, obase);
+        obase += n_out;
     }
     if (lane == 0) { ncnt[r] = (uint32_t)obase; flags[r] = 0; nsrc[r] = (uint64_t)r * FN2_HCAP; }
+    SPROF_T(f4);
+    SPROF_ADD(4, f1 - f0); SPROF_ADD(5, f2 - f1); SPROF_ADD(6, f3 - f2); SPROF_ADD(7, f4 - f3); SPROF_ADD(8, 1);
+    SPROF_ADD(9, n_hits); SPROF_ADD(10, nl);
 }
 
 // ---------------------------------------------------------------------------
@@ -1996,6 +2214,9 @@ k_compact(int n_reads, const uint64_t* __restrict__ nsrc, const uint64_t* __rest
 // hamming_align's result without touching the reference.
 // ---------------------------------------------------------------------------
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4 GU4;   // global loads, not flat ones
+typedef const __attribute__((address_space(1))) unsigned char GU8;
 // a read and its reverse complement (k_compact writes the latter into the call's rc
 // buffer, at the read's offset)
 struct SiteRead {
@@ -2012,6 +2233,31 @@ struct SiteRead {
 __device__ __forceinline__ uint32_t grp_ballot(bool v) {
     const uint64_t b = __ballot(v);
     return (uint32_t)(b >> (threadIdx.x & 48)) & 0xFFFFu;
+}
+
+// site_kmer_eq for k <= 32, in two steps so that every load of a NAM's checks is in
+// flight at once: KmerLoad holds the clamped spans and the lane's two byte pairs
+// (positions l16 and l16 + 16; a position past the span reads its first byte, valid
+// memory, and is not compared)
+struct KmerLoad { uint32_t rl, ql; unsigned char r0, q0, r1, q1; };
+__device__ __forceinline__ KmerLoad kmer_load(const char* ref, int64_t rlen, int64_t rpos, const SiteRead& rd, bool rc,
+                                              int64_t qpos, int k, int l16) {
+    const uint64_t rp = (uint64_t)rpos, qp = (uint64_t)qpos;
+    const uint64_t ra = rp > (uint64_t)rlen ? (uint64_t)rlen : rp, qa = qp > (uint64_t)rd.len ? (uint64_t)rd.len : qp;
+    KmerLoad x;
+    x.rl = (uint32_t)min((uint64_t)k, (uint64_t)rlen - ra);
+    x.ql = (uint32_t)min((uint64_t)k, (uint64_t)rd.len - qa);
+    const uint32_t j0 = (uint32_t)l16 < x.rl ? (uint32_t)l16 : 0u, j1 = (uint32_t)l16 + 16u < x.rl ? (uint32_t)l16 + 16u : 0u;
+    GU8* rb = (GU8*)(ref + ra);
+    GU8* qb = (GU8*)(rd.side(rc) + qa);
+    x.r0 = rb[j0]; x.q0 = qb[j0]; x.r1 = rb[j1]; x.q1 = qb[j1];
+    return x;
+}
+__device__ __forceinline__ bool kmer_test(const KmerLoad& x, int l16) {
+    bool bad = x.rl != x.ql;
+    if ((uint32_t)l16 < x.rl) bad |= x.r0 != x.q0;
+    if ((uint32_t)l16 + 16u < x.rl) bad |= x.r1 != x.q1;
+    return grp_ballot(bad) == 0;
 }
 
 // sub(ref, rpos, k) == sub(read view, qpos, k) with std::string::substr clamping
@@ -2035,8 +2281,8 @@ __device__ bool site_kmer_eq(const char* ref, int64_t rlen, int64_t rpos, const 
 // of padding before the first read and after the last.
 __device__ __forceinline__ void load16(const char* p, uint32_t out[4]) {   // bytes p[0 .. 16), any alignment
     const uintptr_t a = (uintptr_t)p;
-    const uint4* q = (const uint4*)(a & ~(uintptr_t)15);
-    const uint4 x = q[0], y = q[1];
+    GU4* q = (GU4*)(a & ~(uintptr_t)15);
+    const u32x4 x = q[0], y = q[1];
     const bool w2 = (a & 8) != 0, w1 = (a & 4) != 0;
     const uint32_t sh = (uint32_t)a & 3u;
     // words (a >> 2) & 3 .. + 4 of the 32 loaded bytes: shift by two words, then by one
@@ -2050,10 +2296,10 @@ __device__ __forceinline__ void load16(const char* p, uint32_t out[4]) {   // by
 }
 __device__ __forceinline__ uint32_t window_mask(const char* ref_win, const SiteRead& rd, bool rc, int64_t x0,
                                                 int64_t n) {
-    if (x0 >= n) return 0u;
+    const int64_t xl = x0 < n ? x0 : 0;        // past the read: load in range, mask nothing
     uint32_t r[4], q[4];
-    load16(ref_win + x0, r);
-    load16(rd.side(rc) + x0, q);
+    load16(ref_win + xl, r);
+    load16(rd.side(rc) + xl, q);
     uint32_t m = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -2062,7 +2308,7 @@ __device__ __forceinline__ uint32_t window_mask(const char* ref_win, const SiteR
         for (int b = 0; b < 4; ++b) m |= ((x >> (8 * b)) & 0xFFu) ? (1u << (4 * k + b)) : 0u;
     }
     const int64_t left = n - x0;               // positions past the read end do not count
-    return left >= 16 ? m : m & ((1u << left) - 1u);
+    return left >= 16 ? m : left <= 0 ? 0u : m & ((1u << left) - 1u);
 }
 
 // reads over 1024 bp: masks past the four kept in registers, out of line
@@ -2133,17 +2379,35 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
     };
     int64_t ps = 0;
     bool hamming = proj(qs, qe, ps);
-    // the window as the NAM stands, issued with the k-mer loads below
-    uint32_t m0 = hamming ? window_mask(ref + ps, rd, is_rc, 16 * l16, rd.len) : 0u;
+    // the window as the NAM stands and the two k-mers: every load issued before any
+    // test (a window that is not tested is loaded from the contig start and dropped)
+    uint32_t m0 = window_mask(ref + (hamming ? ps : 0), rd, is_rc, 16 * l16, rd.len);
     uint32_t flags;
-    const bool fwd_ok = site_kmer_eq(ref, ref_len, nam.ref_start, rd, is_rc, qs, k, l16) &
-                        site_kmer_eq(ref, ref_len, (int64_t)nam.ref_end - k, rd, is_rc, qe - k, k, l16);
+    bool fwd_ok;
+    if (k <= 32) {
+        const KmerLoad a = kmer_load(ref, ref_len, nam.ref_start, rd, is_rc, qs, k, l16);
+        const KmerLoad b = kmer_load(ref, ref_len, (int64_t)nam.ref_end - k, rd, is_rc, qe - k, k, l16);
+        __builtin_amdgcn_sched_barrier(0);                 // every load above issued before the first test
+        fwd_ok = kmer_test(a, l16) & kmer_test(b, l16);
+    } else {
+        fwd_ok = site_kmer_eq(ref, ref_len, nam.ref_start, rd, is_rc, qs, k, l16) &
+                 site_kmer_eq(ref, ref_len, (int64_t)nam.ref_end - k, rd, is_rc, qe - k, k, l16);
+    }
+    if (!hamming) m0 = 0u;
     if (fwd_ok) {
         flags = 0;
     } else {
         const int64_t qs2 = rd.len - nam.query_end, qe2 = rd.len - nam.query_start;
-        const bool rev_ok = site_kmer_eq(ref, ref_len, nam.ref_start, rd, !is_rc, qs2, k, l16) &
-                            site_kmer_eq(ref, ref_len, (int64_t)nam.ref_end - k, rd, !is_rc, qe2 - k, k, l16);
+        bool rev_ok;
+        if (k <= 32) {
+            const KmerLoad a = kmer_load(ref, ref_len, nam.ref_start, rd, !is_rc, qs2, k, l16);
+            const KmerLoad b = kmer_load(ref, ref_len, (int64_t)nam.ref_end - k, rd, !is_rc, qe2 - k, k, l16);
+            __builtin_amdgcn_sched_barrier(0);
+            rev_ok = kmer_test(a, l16) & kmer_test(b, l16);
+        } else {
+            rev_ok = site_kmer_eq(ref, ref_len, nam.ref_start, rd, !is_rc, qs2, k, l16) &
+                     site_kmer_eq(ref, ref_len, (int64_t)nam.ref_end - k, rd, !is_rc, qe2 - k, k, l16);
+        }
         if (rev_ok) {
             flags = 1;
             is_rc = !is_rc;
@@ -2728,6 +2992,25 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
         }
         break;
     }
+#ifdef RSA_SEED_PROF
+    {
+        static std::atomic<int> calls{0};
+        if (++calls % 20 == 0) {
+            static std::vector<unsigned int> h((size_t)SPROF_READS * 20);
+            unsigned long long v[20] = {};
+            if (hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_seed_prof), 4ull * h.size()) == hipSuccess) {
+                for (size_t i = 0; i < std::min<size_t>(n, SPROF_READS); ++i)
+                    for (int j = 0; j < 20; ++j) v[j] += h[i * 20 + j];
+                const double qw = v[3] ? (double)v[3] : 1.0, fw = v[8] ? (double)v[8] : 1.0;
+                fprintf(stderr, "seedprof query/wave cycles: syncmers %.0f lookups %.0f tail %.0f | find_nams/wave: "
+                        "copy %.0f maps %.0f order %.0f merge %.0f | hits/read %.1f lists/read %.1f | lookup: pick %.0f fetch %.0f "
+                        "emit %.0f (line wait %.0f, ballots %.0f, search %.0f, count %.0f)\n",
+                        v[0] / qw, v[1] / qw, v[2] / qw, v[4] / fw, v[5] / fw, v[6] / fw, v[7] / fw, v[9] / fw, v[10] / fw,
+                        v[11] / qw, v[12] / qw, v[13] / qw, v[14] / qw, v[15] / qw, v[16] / qw, v[17] / qw);
+            }
+        }
+    }
+#endif
     // counters and algorithmic bytes (DESIGN.md "Kernels")
     const uint64_t total = hh.total;
     const double QRS = sizeof(rsa_query_randstrobe), QI = sizeof(QrsInfo), RS = sizeof(rsa_ref_randstrobe),

@@ -79,7 +79,11 @@ def counter(db, cname):
 
 def main():
     src, out = sys.argv[1], sys.argv[2]
-    kt = kernel_times(os.path.join(src, "trace", "run_results.db"))
+    tdb = os.path.join(src, "trace", "run_results.db")
+    if not os.path.exists(tdb):
+        import glob
+        tdb = (glob.glob(os.path.join(src, "t*", "**", "*.db"), recursive=True) or [tdb])[0]
+    kt = kernel_times(tdb)
     fetch = write = {}
     fdb = os.path.join(src, "pmc_fetch", "run_results.db")
     wdb = os.path.join(src, "pmc_write", "run_results.db")
@@ -103,7 +107,7 @@ def main():
         lines.append(f"| {k} | {v['calls']} | {v['total_ms']:.2f} | {100 * v['total_ms'] / total:.1f} | "
                      f"{v['avg_us']:.1f} | {v['min_us']:.1f} | {v['max_us']:.1f} | "
                      f"{'' if rd is None else f'{rd:.0f}'} | {'' if wr is None else f'{wr:.0f}'} |")
-    b = busy(os.path.join(src, "trace", "run_results.db"))
+    b = busy(tdb)
     if b:
         lines += ["", f"GPU busy over the mapping span (first to last seeding kernel, warm-up included): "
                       f"{b['busy_union_ms']:.1f} ms of {b['span_ms']:.1f} ms = {100 * b['busy_frac']:.1f} % "
