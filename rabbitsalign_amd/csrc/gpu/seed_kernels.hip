@@ -71,6 +71,7 @@ struct HitD {
 #ifdef RSA_SEED_PROF
 #define SPROF_READS 32768
 __device__ unsigned int g_seed_prof[SPROF_READS][20];    // per read (r < SPROF_READS), plain stores
+__device__ unsigned int g_sites_prof[4096 * 4][8];       // k_sites: per (block, wave), summed over its NAM rounds
 #define SPROF_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define SPROF_ADD(i, d) do { if (lane == 0 && r < SPROF_READS) g_seed_prof[r][i] = (unsigned int)(d); } while (0)
 #else
@@ -2358,7 +2359,11 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
     __shared__ unsigned long long s_at;
     const uint64_t total = (uint64_t)err_hdr->total <= cap ? (uint64_t)err_hdr->total : 0;
     const int l16 = threadIdx.x & 15, grp = threadIdx.x >> 4;
+#ifdef RSA_SEED_PROF
+    unsigned long long sp_acc[6] = {0, 0, 0, 0, 0, 0};
+#endif
     for (uint64_t blk = blockIdx.x; blk * SITES_BLOCK < total; blk += gridDim.x) {
+    SPROF_T(t0);
     const uint64_t g0 = blk * SITES_BLOCK + grp;
     const bool valid = g0 < total;
     const uint64_t g = valid ? g0 : total - 1;             // idle groups shadow the last NAM (ballots stay uniform)
@@ -2420,6 +2425,7 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
             hamming = false;
         }
     }
+    SPROF_T(t1);
     const int n = (int)rd.len;
     uint32_t hd = 0, mm_off = 0;
     uint32_t m1 = 0, m2 = 0, m3 = 0;             // this lane's masks, positions c * 256 + 16 * l16 + b
@@ -2450,6 +2456,7 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
     // pool space: a block-wide prefix over its NAMs and one atomic a block (positions:
     // n_mm words; hamming_align's result: a 6-word header and at most 2 n_mm + 3 ops of 2 words)
     const uint32_t need = (want && valid && fits) ? (ham ? 12u + 4u * hd : hd) : 0u;
+    SPROF_T(t2);
     if (l16 == 0) s_need[grp] = need;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2458,6 +2465,7 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
         s_at = acc ? atomicAdd(pool_used, (unsigned long long)acc) : 0ull;
     }
     __syncthreads();
+    SPROF_T(t3);
     if (want) {
         const unsigned long long at = s_at + s_base[grp];
         if (!fits || at + need > pool_cap) {
@@ -2486,22 +2494,31 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
             mm_off = (uint32_t)at;
             // 1. highest_scoring_segment (aligner.cpp:219-252), run by run: between mismatches
             //    the score only grows, so each run of matches needs one check at its end
+            //    Only the 16-position blocks holding a mismatch are visited (a group ballot
+            //    of the lanes' masks, in position order): the others change nothing here.
             int start = 0, best_start = 0, best_end = 0, i = 0;
             int score = h_bonus, best = 0;
-            for (int i0 = 0; i0 < n; i0 += 16) {
-                // lane (i0 / 16) % 16 of the group holds positions i0 .. i0 + 15
-                uint32_t bits = (uint32_t)__shfl((int)mask_of(i0 >> 8), (i0 >> 4) & 15, 16);
-                while (bits) {
-                    const int m = i0 + __builtin_ctz(bits);
-                    bits &= bits - 1;
-                    if (m > i) {
-                        score += h_match * (m - i);
-                        if (score > best) { best_start = start; best = score; best_end = m; }
+            for (int c = 0; 256 * c < n; ++c) {
+                const uint32_t mc = mask_of(c);
+                uint32_t nz = grp_ballot(mc != 0u);
+                while (nz) {
+                    // lane li of the group holds positions 256 c + 16 li .. + 15
+                    const int li = __builtin_ctz(nz);
+                    nz &= nz - 1;
+                    const int i0 = 256 * c + 16 * li;
+                    uint32_t bits = (uint32_t)__shfl((int)mc, li, 16);
+                    while (bits) {
+                        const int m = i0 + __builtin_ctz(bits);
+                        bits &= bits - 1;
+                        if (m > i) {
+                            score += h_match * (m - i);
+                            if (score > best) { best_start = start; best = score; best_end = m; }
+                        }
+                        score -= h_mismatch;
+                        if (score < 0) { start = m + 1; score = 0; }
+                        if (score > best) { best_start = start; best = score; best_end = m + 1; }
+                        i = m + 1;
                     }
-                    score -= h_mismatch;
-                    if (score < 0) { start = m + 1; score = 0; }
-                    if (score > best) { best_start = start; best = score; best_end = m + 1; }
-                    i = m + 1;
                 }
             }
             if (n > i) {
@@ -2525,19 +2542,30 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
             };
             if (best_start > 0) push(4, (uint32_t)best_start);
             int cur = best_start;
-            for (int i0 = best_start & ~15; i0 < best_end; i0 += 16) {
-                uint32_t bits = (uint32_t)__shfl((int)mask_of(i0 >> 8), (i0 >> 4) & 15, 16);
-                // positions in [best_start, best_end) only
-                const int lo = best_start - i0, hi = best_end - i0;
-                if (lo > 0) bits &= ~((1u << lo) - 1u);
-                if (hi < 16) bits &= (1u << hi) - 1u;
-                while (bits) {
-                    const int m = i0 + __builtin_ctz(bits);
-                    bits &= bits - 1;
-                    if (m > cur) push(7, (uint32_t)(m - cur));
-                    push(8, 1);
-                    ed++;
-                    cur = m + 1;
+            for (int c = best_start >> 8; 256 * c < best_end; ++c) {
+                // this lane's positions in [best_start, best_end) only, blocks with a mismatch visited
+                const int p0 = 256 * c + 16 * l16;
+                uint32_t mine = mask_of(c);
+                const int lo = best_start - p0, hi = best_end - p0;
+                if (lo >= 16 || hi <= 0) mine = 0u;
+                else {
+                    if (lo > 0) mine &= ~((1u << lo) - 1u);
+                    if (hi < 16) mine &= (1u << hi) - 1u;
+                }
+                uint32_t nz = grp_ballot(mine != 0u);
+                while (nz) {
+                    const int li = __builtin_ctz(nz);
+                    nz &= nz - 1;
+                    const int i0 = 256 * c + 16 * li;
+                    uint32_t bits = (uint32_t)__shfl((int)mine, li, 16);
+                    while (bits) {
+                        const int m = i0 + __builtin_ctz(bits);
+                        bits &= bits - 1;
+                        if (m > cur) push(7, (uint32_t)(m - cur));
+                        push(8, 1);
+                        ed++;
+                        cur = m + 1;
+                    }
                 }
             }
             if (best_end > cur) push(7, (uint32_t)(best_end - cur));
@@ -2557,6 +2585,7 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
             }
         }
     }
+    SPROF_T(t4);
     if (valid && l16 == 0) {
         rsa_nam_site out;
         out.flags = (uint8_t)flags;
@@ -2571,7 +2600,17 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
         else atomicOr(&err_hdr->errors, SEED_E_SITE);
     }
     __syncthreads();                             // s_need / s_base / s_at are reused next round
+#ifdef RSA_SEED_PROF
+    SPROF_T(t5);
+    sp_acc[0] += t1 - t0; sp_acc[1] += t2 - t1; sp_acc[2] += t3 - t2; sp_acc[3] += t4 - t3; sp_acc[4] += t5 - t4;
+    sp_acc[5] += 1;
+#endif
     }
+#ifdef RSA_SEED_PROF
+    const int wv = (int)(threadIdx.x >> 6);
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096)
+        for (int i = 0; i < 6; ++i) g_sites_prof[blockIdx.x * 4 + wv][i] = (unsigned int)sp_acc[i];
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -3007,6 +3046,16 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
                         "emit %.0f (line wait %.0f, ballots %.0f, search %.0f, count %.0f)\n",
                         v[0] / qw, v[1] / qw, v[2] / qw, v[4] / fw, v[5] / fw, v[6] / fw, v[7] / fw, v[9] / fw, v[10] / fw,
                         v[11] / qw, v[12] / qw, v[13] / qw, v[14] / qw, v[15] / qw, v[16] / qw, v[17] / qw);
+                static std::vector<unsigned int> hs((size_t)4096 * 4 * 8);
+                unsigned long long u[8] = {};
+                if (hipMemcpyFromSymbol(hs.data(), HIP_SYMBOL(g_sites_prof), 4ull * hs.size()) == hipSuccess) {
+                    for (size_t i = 0; i < (size_t)4096 * 4; ++i)
+                        for (int j = 0; j < 8; ++j) u[j] += hs[i * 8 + j];
+                    const double rr = u[5] ? (double)u[5] : 1.0;
+                    fprintf(stderr, "seedprof k_sites per wave-round cycles: loads+kmers %.0f window %.0f sync %.0f "
+                            "pool/align %.0f tail %.0f | rounds %.0f\n", u[0] / rr, u[1] / rr, u[2] / rr, u[3] / rr,
+                            u[4] / rr, rr);
+                }
             }
         }
     }
