@@ -46,6 +46,7 @@ struct SeedBufs {
     // NAMs a read and pool words a NAM of the lane's last call: the first download's size
     // (a guess too small costs a second round trip, e.g. 9.4 NAMs a read on PE 2x250)
     double nam_rate = 0, mm_rate = 0;
+    double resc_rate = -1;          // rescued reads a read in the lane's last call (-1: none yet)
     hipEvent_t done = nullptr;   // blocking-sync event (RSA_WAIT=event)
 };
 

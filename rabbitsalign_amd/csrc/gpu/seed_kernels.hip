@@ -24,6 +24,7 @@
 #include <atomic>
 #include <cstdio>
 #include <climits>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -615,14 +616,37 @@ __device__ __forceinline__ QrsInfo lookup_coop(const rsa_query_randstrobe& q, bo
     // loads stay unconditional, so all eight are in flight at once
     const uint64_t top = valid ? q.hash >> (64 - p.bits) : 0;
     const int g = lane >> 3, part = lane & 7;
+#ifdef RSA_SEED_PROF
+    const unsigned long long cs = __builtin_amdgcn_s_memtime();
+#endif
     s_top[lane] = top;
     s_key[lane] = q.hash;
     WSYNC_SEED();
     uint4 w[8];
+#ifdef RSA_SEED_PROF
+    uint64_t tj[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tj[j] = s_top[8 * j + g];
+    __builtin_amdgcn_s_waitcnt(0xC07F & ~0x0F00);           // lgkmcnt(0): the line indices are in
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long ca = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = ((const uint4*)(p.lines + tj[j]))[part];
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long cm = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 4; j < 8; ++j) w[j] = ((const uint4*)(p.lines + tj[j]))[part];
+    __builtin_amdgcn_sched_barrier(0);
+    prof[4] += ca - cs; prof[5] += cm - ca;
+#else
 #pragma unroll
     for (int j = 0; j < 8; ++j) w[j] = ((const uint4*)(p.lines + s_top[8 * j + g]))[part];
+#endif
 #ifdef RSA_SEED_PROF
     const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+    prof[6] += c0 - cm;
     __builtin_amdgcn_s_waitcnt(0x0F70);                   // vmcnt(0): the lines are in
     const unsigned long long c1 = __builtin_amdgcn_s_memtime();
     prof[0] += c1 - c0;
@@ -821,7 +845,7 @@ k_seed_query(const char* __restrict__ seq, const uint64_t* __restrict__ roff, co
     HitD* slot = hit_slots + (size_t)r * LK_HCAP;
     LkStat ls;
     int hoff = 0;
-    unsigned long long acc_wait[4] = {0, 0, 0, 0};      // RSA_SEED_PROF: lookup_coop's phases
+    unsigned long long acc_wait[7] = {0, 0, 0, 0, 0, 0, 0};   // RSA_SEED_PROF: lookup_coop's phases
 #ifdef RSA_SEED_PROF
     unsigned long long acc_pick = 0, acc_coop = 0, acc_emit = 0;
 #endif
@@ -862,7 +886,7 @@ k_seed_query(const char* __restrict__ seq, const uint64_t* __restrict__ roff, co
         acc_pick += l1 - l0; acc_coop += l2 - l1; acc_emit += l3 - l2;
 #endif
     }
-    SPROF_ADD(11, acc_pick); SPROF_ADD(12, acc_coop); SPROF_ADD(13, acc_emit); SPROF_ADD(14, acc_wait[0]); SPROF_ADD(15, acc_wait[1]); SPROF_ADD(16, acc_wait[2]); SPROF_ADD(17, acc_wait[3]);
+    SPROF_ADD(11, acc_pick); SPROF_ADD(12, acc_coop); SPROF_ADD(13, acc_emit); SPROF_ADD(14, acc_wait[0]); SPROF_ADD(15, acc_wait[1]); SPROF_ADD(16, acc_wait[2]); SPROF_ADD(17, acc_wait[3]); SPROF_ADD(18, acc_wait[4]); SPROF_ADD(19, acc_wait[5] + acc_wait[6]);
     SPROF_T(q2);
     ls.wave_sum();                                      // every lane holds the read's totals
     const float nonrep = ls.found > 0 ? (float)ls.good / (float)ls.found : 1.0f;   // nam.cpp:920
@@ -2942,7 +2966,13 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
             hipLaunchKernelGGL(k_query_fix, dim3(1), dim3(64), 0, st, DP(B_RLIST, uint32_t), dhdr, D_SEQ, d_roff,
                                d_rlen, d_qbase, p, RescueScratch{DP(B_RBUF, RescueD)},
                                DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo), DP(B_ST, ReadStat));
-        hipLaunchKernelGGL(k_rescue_w, dim3(RESCUE_GRID), dim3(64 * FN_WAVES), 0, st, DP(B_QRS, rsa_query_randstrobe),
+        // the persistent rescue walk is sized from the lane's last call (rescue is rare on
+        // most inputs, and 256 idle 52-KB-LDS workgroups still queue behind the other
+        // lanes' kernels); the grid-stride loop takes any count
+        const uint32_t resc_grid =
+            b.resc_rate < 0 ? RESCUE_GRID
+                            : (uint32_t)std::min<double>(RESCUE_GRID, std::max(8.0, std::ceil(1.5 * b.resc_rate * n / FN_WAVES)));
+        hipLaunchKernelGGL(k_rescue_w, dim3(resc_grid), dim3(64 * FN_WAVES), 0, st, DP(B_QRS, rsa_query_randstrobe),
                            DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t), d_qbase, p, rescue_cutoff, DP(B_RBUF, RescueD),
                            pool, DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t), DP(B_RBASE, uint64_t), dhdr,
                            DP(B_RLIST, uint32_t), DP(B_RBIGL, uint32_t));
@@ -3014,6 +3044,7 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
         if (out->sites) out->mm_used = mm_used;
         else out->mm_used = 0;
         if (n) b.nam_rate = (double)total / (double)n;
+        if (n) b.resc_rate = (double)hh.resc_reads / (double)n;
         if (total) b.mm_rate = (double)mm_used / (double)total;
         if (total > guess || mm_used > mm_guess) {   // rare: a second round trip for the rest
             c.second_trip = 1;
@@ -3043,9 +3074,10 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
                 const double qw = v[3] ? (double)v[3] : 1.0, fw = v[8] ? (double)v[8] : 1.0;
                 fprintf(stderr, "seedprof query/wave cycles: syncmers %.0f lookups %.0f tail %.0f | find_nams/wave: "
                         "copy %.0f maps %.0f order %.0f merge %.0f | hits/read %.1f lists/read %.1f | lookup: pick %.0f fetch %.0f "
-                        "emit %.0f (line wait %.0f, ballots %.0f, search %.0f, count %.0f)\n",
+                        "emit %.0f (line wait %.0f, ballots %.0f, search %.0f, count %.0f; to indices %.0f, issue %.0f)\n",
                         v[0] / qw, v[1] / qw, v[2] / qw, v[4] / fw, v[5] / fw, v[6] / fw, v[7] / fw, v[9] / fw, v[10] / fw,
-                        v[11] / qw, v[12] / qw, v[13] / qw, v[14] / qw, v[15] / qw, v[16] / qw, v[17] / qw);
+                        v[11] / qw, v[12] / qw, v[13] / qw, v[14] / qw, v[15] / qw, v[16] / qw, v[17] / qw, v[18] / qw,
+                        v[19] / qw);
                 static std::vector<unsigned int> hs((size_t)4096 * 4 * 8);
                 unsigned long long u[8] = {};
                 if (hipMemcpyFromSymbol(hs.data(), HIP_SYMBOL(g_sites_prof), 4ull * hs.size()) == hipSuccess) {
