@@ -79,6 +79,10 @@ __device__ unsigned int g_sites_prof[4096 * 4][8];       // k_sites: per (block,
 #define SPROF_T(v)
 #define SPROF_ADD(i, d)
 #endif
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// one 16-byte part of a bucket line (non-temporal loads measured no better: 146 / 157 µs
+// against 143 / 146, profiles/r05/seed_ab_nt.txt)
+__device__ __forceinline__ uint4 line_part(const BucketLine* L, int part) { return ((const uint4*)L)[part]; }
 struct SeedHdr {
     unsigned long long pool_used;   // pool entries handed out
     unsigned long long total;       // final NAMs of the batch
@@ -632,17 +636,17 @@ __device__ __forceinline__ QrsInfo lookup_coop(const rsa_query_randstrobe& q, bo
     const unsigned long long ca = __builtin_amdgcn_s_memtime();
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) w[j] = ((const uint4*)(p.lines + tj[j]))[part];
+    for (int j = 0; j < 4; ++j) w[j] = line_part(p.lines + tj[j], part);
     __builtin_amdgcn_sched_barrier(0);
     const unsigned long long cm = __builtin_amdgcn_s_memtime();
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int j = 4; j < 8; ++j) w[j] = ((const uint4*)(p.lines + tj[j]))[part];
+    for (int j = 4; j < 8; ++j) w[j] = line_part(p.lines + tj[j], part);
     __builtin_amdgcn_sched_barrier(0);
     prof[4] += ca - cs; prof[5] += cm - ca;
 #else
 #pragma unroll
-    for (int j = 0; j < 8; ++j) w[j] = ((const uint4*)(p.lines + s_top[8 * j + g]))[part];
+    for (int j = 0; j < 8; ++j) w[j] = line_part(p.lines + s_top[8 * j + g], part);
 #endif
 #ifdef RSA_SEED_PROF
     const unsigned long long c0 = __builtin_amdgcn_s_memtime();
@@ -2182,24 +2186,26 @@ struct SiteDesc {
     uint32_t read_len, ref_len;
 };
 
-__global__ void __launch_bounds__(64)
+#define CP_WAVES 4                                         // k_compact: reads (waves) a workgroup
+__global__ void __launch_bounds__(64 * CP_WAVES)
 k_compact(int n_reads, const uint64_t* __restrict__ nsrc, const uint64_t* __restrict__ rbase,
           uint64_t arena_base, const uint32_t* __restrict__ ncnt1, const uint32_t* __restrict__ ncnt2,
           const uint8_t* __restrict__ rescued, const rsa_nam* __restrict__ arena, const uint32_t* __restrict__ loc,
           const uint64_t* __restrict__ boff, uint64_t* __restrict__ ooff, uint64_t cap, rsa_nam* __restrict__ out,
           SiteDesc* __restrict__ desc, const uint64_t* __restrict__ roff, const uint32_t* __restrict__ rlen,
           const uint64_t* __restrict__ coff, const char* __restrict__ seq, char* __restrict__ seq_rc, int by_score) {
-    const int r = blockIdx.x;
-    if (r >= n_reads) return;
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * CP_WAVES + (threadIdx.x >> 6);
+    if (r >= n_reads) return;                                // whole wave
     const bool resc = rescued[r] != 0;
     const rsa_nam* src = arena + (resc ? arena_base + rbase[r] : nsrc[r]);
     const uint32_t n = resc ? ncnt2[r] : ncnt1[r];
     const uint64_t o = boff[r / SS_TPB] + loc[r];          // k_seed_count + k_seed_scan
-    if (threadIdx.x == 0) ooff[r] = o;
+    if (lane == 0) ooff[r] = o;
     if (desc && n) {                                         // the read's reverse complement for k_sites
         const uint64_t ro = roff[r];
         const uint32_t len = rlen[r];
-        for (uint32_t i = threadIdx.x; i < len; i += blockDim.x)
+        for (uint32_t i = lane; i < len; i += 64)
             seq_rc[ro + i] = (char)rc_base((unsigned char)seq[ro + len - 1 - i]);
     }
     if (o + n > cap) return;
@@ -2216,7 +2222,7 @@ k_compact(int n_reads, const uint64_t* __restrict__ nsrc, const uint64_t* __rest
         desc[at] = d;
     };
     if (by_score && n >= 2 && n <= 16) {
-        const int i = threadIdx.x;
+        const int i = lane;
         const float si = i < (int)n ? src[i].score : 0.0f;
         int rank = 0;
         for (int j = 0; j < (int)n; ++j) {
@@ -2226,7 +2232,7 @@ k_compact(int n_reads, const uint64_t* __restrict__ nsrc, const uint64_t* __rest
         if (i < (int)n) put(o + rank, src[i]);
         return;
     }
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) put(o + i, src[i]);
+    for (uint32_t i = lane; i < n; i += 64) put(o + i, src[i]);
 }
 
 // ---------------------------------------------------------------------------
@@ -2239,7 +2245,6 @@ k_compact(int n_reads, const uint64_t* __restrict__ nsrc, const uint64_t* __rest
 // hamming_align's result without touching the reference.
 // ---------------------------------------------------------------------------
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(1))) u32x4 GU4;   // global loads, not flat ones
 typedef const __attribute__((address_space(1))) unsigned char GU8;
 // a read and its reverse complement (k_compact writes the latter into the call's rc
@@ -2967,11 +2972,12 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
                                d_rlen, d_qbase, p, RescueScratch{DP(B_RBUF, RescueD)},
                                DP(B_QRS, rsa_query_randstrobe), DP(B_QI, QrsInfo), DP(B_ST, ReadStat));
         // the persistent rescue walk is sized from the lane's last call (rescue is rare on
-        // most inputs, and 256 idle 52-KB-LDS workgroups still queue behind the other
-        // lanes' kernels); the grid-stride loop takes any count
+        // most inputs -- a few reads a call on the headline -- and 256 idle 52-KB-LDS
+        // workgroups still queue behind the other lanes' kernels); the grid-stride loop
+        // takes any count
         const uint32_t resc_grid =
             b.resc_rate < 0 ? RESCUE_GRID
-                            : (uint32_t)std::min<double>(RESCUE_GRID, std::max(8.0, std::ceil(1.5 * b.resc_rate * n / FN_WAVES)));
+                            : (uint32_t)std::min<double>(RESCUE_GRID, std::max(1.0, std::ceil(1.5 * b.resc_rate * n / FN_WAVES)));
         hipLaunchKernelGGL(k_rescue_w, dim3(resc_grid), dim3(64 * FN_WAVES), 0, st, DP(B_QRS, rsa_query_randstrobe),
                            DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t), d_qbase, p, rescue_cutoff, DP(B_RBUF, RescueD),
                            pool, DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t), DP(B_RBASE, uint64_t), dhdr,
@@ -2990,7 +2996,7 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
                            DP(B_LOC, uint32_t), DP(B_BSUM, uint64_t), dhdr);
         hipLaunchKernelGGL(k_seed_scan, dim3(1), dim3(SS_TPB), 0, st, n_sblk, (int)n, DP(B_BSUM, uint64_t), d_ooff,
                            dhdr);
-        hipLaunchKernelGGL(k_compact, dim3(n), dim3(64), 0, st, (int)n, DP(B_NSRC, uint64_t), DP(B_RBASE, uint64_t),
+        hipLaunchKernelGGL(k_compact, dim3(std::max<uint32_t>(1, (n + CP_WAVES - 1) / CP_WAVES)), dim3(64 * CP_WAVES), 0, st, (int)n, DP(B_NSRC, uint64_t), DP(B_RBASE, uint64_t),
                            slots, DP(B_NCNT1, uint32_t), DP(B_NCNT2, uint32_t), d_resc, DP(B_ARENA, rsa_nam),
                            DP(B_LOC, uint32_t), DP(B_BSUM, uint64_t), d_ooff,
                            cap, DP(B_OUT, rsa_nam), out->sites ? DP(B_NREAD, SiteDesc) : nullptr, d_roff, d_rlen,
