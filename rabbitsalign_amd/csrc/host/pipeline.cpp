@@ -762,14 +762,6 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
     bool lead_seeded = false;      // other prefetch waits until chunk 0 is seeded: it would only queue
                                    // other chunks' seeding ahead of the single-worker timeline
     size_t next_par = 0;           // next chunk for the parallel stage (valid once frozen)
-    // RSA_HEAD_FIRST (default on with a SAM sink): the parallel stage waits until the chunk the
-    // leader hands over has come back from its extension call, and prefetch stays at the early
-    // seeds until then.  The sink must write in chunk order and is the streamed path's bound:
-    // the earlier that chunk's SAM is out, the earlier the writer starts, and its extension
-    // call then runs on a quiet GPU instead of behind every worker's first seeding call.
-    static const bool head_first_env = !getenv("RSA_HEAD_FIRST") || atoi(getenv("RSA_HEAD_FIRST")) != 0;
-    bool gate = head_first_env && sink != nullptr;
-    std::atomic<size_t> gate_chunk{SIZE_MAX};   // the handed chunk, whose extension opens the gate
     std::unique_ptr<PeChunk> handed;                     // part() done in the sequential phase
     InsertSizeDistribution isize, frozen_isize;
     std::exception_ptr failure;
@@ -842,11 +834,6 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
         {
             Unslot u(slots, offl, c.in.index);
             eng.extend(jobs, mc.aparams, infos);
-        }
-        if (c.in.index == gate_chunk) {
-            std::lock_guard<std::mutex> g(m);
-            gate = false;
-            cv.notify_all();
         }
         c.stats.tot_aligner_calls -= no_shared_count(infos);   // the reference aligns none of those
         c.times.extend += since(te);
@@ -930,8 +917,6 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
                 frozen = true;
                 frozen_isize = isize;
                 handed = std::move(pre);                 // may be null: everything was sequential
-                if (handed) gate_chunk = handed->in.index;
-                else gate = false;
                 leader_busy = false;
                 if (!early) next_par = std::max(next, first);
                 if (next_par >= n_chunks && !handed) done = true;
@@ -946,12 +931,9 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
                     for (;;) {
                         if (failure || done) break;
                         if (frozen && handed) { c = std::move(handed); break; }
-                        if (frozen && next_par < n_chunks && !gate) {
-                            idx = next_par++;
-                            break;
-                        }
+                        if (frozen && next_par < n_chunks) { idx = next_par++; break; }
                         skip_claimed();
-                        if (((lead_seeded && !gate) || rel(next_seed) <= early_seeds) && next_seed < n_chunks &&
+                        if ((lead_seeded || rel(next_seed) <= early_seeds) && next_seed < n_chunks &&
                             rel(next_seed) < consumed + window) {
                             pf = next_seed;
                             claim(pf);
