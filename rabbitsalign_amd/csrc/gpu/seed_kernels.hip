@@ -2414,8 +2414,9 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
     int64_t ps = 0;
     bool hamming = proj(qs, qe, ps);
     // the window as the NAM stands and the two k-mers: every load issued before any
-    // test (a window that is not tested is loaded from the contig start and dropped)
-    uint32_t m0 = window_mask(ref + (hamming ? ps : 0), rd, is_rc, 16 * l16, rd.len);
+    // test.  A window that is not tested is loaded from the read itself and dropped (the
+    // read buffer is padded past its last read; a short last contig is not)
+    uint32_t m0 = window_mask(hamming ? ref + ps : rd.s, rd, is_rc, 16 * l16, rd.len);
     uint32_t flags;
     bool fwd_ok;
     if (k <= 32) {
