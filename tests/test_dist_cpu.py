@@ -113,11 +113,13 @@ def _part_worker(rank, world, port, fq1, fq2, out_dir, q):
 
 
 @pytest.mark.skipif(not os.path.exists(REF_CPU_LIB), reason="CPU-path library not built")
-def test_two_rank_shared_input_gloo(tmp_path):
-    """Two ranks map ONE FASTQ pair: each counts its half of each file, the counts are
-    all-gathered over gloo, each maps its chunks into its own SAM part.  Header + parts in
-    rank order == the single-process SAM of the same files, byte for byte; the summed
-    statistics == the single process's."""
+@pytest.mark.parametrize("world", [2, 4])
+def test_shared_input_gloo(tmp_path, world):
+    """`world` ranks map ONE FASTQ pair: each counts its 1/world of each file, the counts
+    are all-gathered over gloo, each maps its chunks into its own SAM part (every rank past
+    the first replays the insert-size estimate from chunk 0).  Header + parts in rank order ==
+    the single-process SAM of the same files, byte for byte; the summed statistics == the
+    single process's."""
     import torch.multiprocessing as mp
     from rabbitsalign_amd import mapper, shard
     m = mapper.Mapper.synthetic(CFG["seed"], CFG["ref_len"], CFG["contigs"], CFG["L"], threads=2,
@@ -133,21 +135,22 @@ def test_two_rank_shared_input_gloo(tmp_path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_part_worker, args=(r, 2, port, fq1, fq2, str(tmp_path), q)) for r in range(2)]
+    procs = [ctx.Process(target=_part_worker, args=(r, world, port, fq1, fq2, str(tmp_path), q)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
-    for _ in range(2):
+    for _ in range(world):
         rank, part, tot = q.get(timeout=600)
         res[rank] = (part, tot)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     n_chunks = (PART["pairs"] + PART["chunk"] - 1) // PART["chunk"]
-    assert res[0][0]["first_chunk"] == 0 and res[0][0]["end_chunk"] == res[1][0]["first_chunk"]
-    assert res[1][0]["end_chunk"] == n_chunks and res[1][0]["first_chunk"] > 0
-    parts = b"".join(open(tmp_path / f"part{r}.sam", "rb").read() for r in range(2))
+    assert res[0][0]["first_chunk"] == 0 and res[world - 1][0]["end_chunk"] == n_chunks
+    for r in range(1, world):
+        assert res[r][0]["first_chunk"] == res[r - 1][0]["end_chunk"] and res[r][0]["first_chunk"] > 0
+    parts = b"".join(open(tmp_path / f"part{r}.sam", "rb").read() for r in range(world))
     assert parts == open(one, "rb").read()
-    for r in range(2):
+    for r in range(world):
         assert res[r][1]["n_reads"] == st1.n_reads
         assert all(res[r][1][f] == getattr(st1, f) for f in shard.STAT_FIELDS)
