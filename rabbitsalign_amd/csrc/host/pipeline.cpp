@@ -110,13 +110,17 @@ struct Unslot {                   // the slot handed back for a blocking section
 // 15.7/15.5, +12 15.8/16.3; r27: +12 17.2/17.6, +16 15.9/16.1, +20 15.9/15.7
 // -- none for an engine computing in-thread)
 
-static int wait_workers(const Engine& eng, int threads) {
+static int wait_workers(const Engine& eng, int threads, bool has_sink) {
     const char* e = getenv("RSA_WAIT_WORKERS");
     if (e) return std::max(0, atoi(e));
-    // 3/4 of the threads (12 of 16).  Round-2 A/B runs disagree from box to box
-    // (profiles/r02/ab_wait_workers*.jsonl): 4 won one box, 12 won three of three
-    // alternating runs on another (19.5/19.0/16.1 vs 17.5/16.6/13.4 Mreads/s)
-    return eng.offloads() ? (3 * threads) / 4 : 0;
+    // 3/4 of the threads (12 of 16) for an in-memory run; 3/8 (6 of 16) when the SAM goes
+    // to a sink, whose writer and readers need the cores the parked workers take when they
+    // wake.  Round 5, alternating runs on two boxes (profiles/r05/wait_workers_ab.txt):
+    // PE 2x150 streamed 21.35/22.00/21.42/21.15 with 6 against 19.77/20.04/21.18/20.10 with
+    // 12, 0.46-0.54 against 0.50-0.59 core-us a read; PE 2x250 streamed 11.74/12.30 against
+    // 11.25/11.80.  In memory 12 stays ahead (24.1 against 23.2 mean).
+    if (!eng.offloads()) return 0;
+    return has_sink ? (3 * threads) / 8 : (3 * threads) / 4;
 }
 
 // Chunks' SAM text in chunk order (OutputBuffer::output_records, pc.cpp:119-135).
@@ -725,7 +729,7 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
     OrderedSink os(sink, user, opt.digest, first);
     const int T = std::max(1, opt.threads);
     const bool offl = eng.offloads();
-    const int W = T + wait_workers(eng, T);
+    const int W = T + wait_workers(eng, T, sink != nullptr);
     CpuSlots slots;
     slots.free = std::max(1, T - io_cores(sink != nullptr, T));
     // prefetch depth (RSA_PREFETCH chunks, default 2W+2; 0 = every worker seeds its own chunk)
@@ -1165,7 +1169,7 @@ PipelineResult run_pipeline_se(ReadSource& src, Engine& eng, const MapContext& m
         std::lock_guard<std::mutex> g(stat_m);
         result.stats.add(local);
     };
-    WorkerPool::get().run(T + wait_workers(eng, T), worker);
+    WorkerPool::get().run(T + wait_workers(eng, T, sink != nullptr), worker);
     os.close();                                  // the last SAM byte is with the sink
     if (failure) std::rethrow_exception(failure);
     result.map_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
