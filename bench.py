@@ -124,6 +124,7 @@ def host_cores(pinned: bool = False) -> int:
 
 
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "latest_traffic.json")
+LINE_PEAK_GLINES = 46.0      # random 128-B lines, 8 lanes a line, 32 GB table (scripts/micro/line_probe.hip)
 EXT_PMC_JSON = os.path.join(ROOT, "profiles", "r04", "ext_pmc.json")
 
 
@@ -200,6 +201,15 @@ def kernel_roofline(name: str, k: dict, ks: dict) -> dict:
                     "frac": round(achieved / HBM_PEAK_GBS, 6)})
         if name in KERNEL_LIMITER:
             out["limiter"] = KERNEL_LIMITER[name]
+        if name == "lookup" and ks.get("query_randstrobes") and ks.get("seed_calls"):
+            # its real currency: one random 128-B bucket line per query randstrobe, against the
+            # measured rate of random line fetches, 8 lanes a line, on a 32 GB table
+            lines = ks["query_randstrobes"] / ks["seed_calls"]
+            got = lines / avg_s / 1e9
+            out["line_fetch"] = {"lines_per_launch": round(lines, 1), "achieved": round(got, 3),
+                                 "peak": LINE_PEAK_GLINES, "unit": "G lines/s",
+                                 "frac": round(got / LINE_PEAK_GLINES, 5),
+                                 "peak_source": "profiles/r05/line_probe.txt (mode 1, 32 GB table)"}
     return out
 
 
@@ -209,11 +219,13 @@ KERNEL_LIMITER = {
     "ext_band": "dependent-issue latency: one 16-lane group walks a job's band row by row (F prefix scan "
                 "over DPP row_shr), 4 jobs a wave, < 2 waves per SIMD at chunk size",
     "ext_band_wide": "latency of the few (~3 a call) 64-lane jobs, one wave each",
-    "find_nams": "LDS latency and divergence of the robin_hood map emulation, one wave per read",
     "sites": "latency of random reference windows (one read per NAM)",
     "lookup": "k_seed_query (randstrobes + lookup fused, one wave per read): xxh64 and the syncmer window in "
-              "LDS, then random HBM lines: one 128-B bucket line per query randstrobe (bounds + up to 7 "
-              "entries; larger buckets add their entries' line)",
+              "LDS, then random HBM lines, 8 lanes a line: one 128-B bucket line per query randstrobe (bounds "
+              "+ up to 7 entries); their issue stalls on address translation (0.87 UTCL1 misses a line, the "
+              "stall grows with the 32 GB table: profiles/r05/seed_table_size.txt)",
+    "find_nams": "one wave per read, the NAM merge wave-parallel (ballots); robin_hood map inserts per run "
+                 "of equal keys on one lane per orientation",
     "randstrobes": "one lane per read (reads over 512 bp only)",
     "rescue": "latency, rescued reads only",
 }
