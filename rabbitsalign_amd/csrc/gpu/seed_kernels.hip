@@ -2186,7 +2186,9 @@ struct SiteDesc {
     uint32_t read_len, ref_len;
 };
 
-#define CP_WAVES 4                                         // k_compact: reads (waves) a workgroup
+// k_compact: reads (waves) a workgroup.  One: four (256-thread workgroups) ran 59 against 44 us
+// a launch under the bench's kernel trace (profiles/r05k_rocprof.md vs r05j)
+#define CP_WAVES 1
 __global__ void __launch_bounds__(64 * CP_WAVES)
 k_compact(int n_reads, const uint64_t* __restrict__ nsrc, const uint64_t* __restrict__ rbase,
           uint64_t arena_base, const uint32_t* __restrict__ ncnt1, const uint32_t* __restrict__ ncnt2,
@@ -2978,7 +2980,7 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
         // takes any count
         const uint32_t resc_grid =
             b.resc_rate < 0 ? RESCUE_GRID
-                            : (uint32_t)std::min<double>(RESCUE_GRID, std::max(1.0, std::ceil(1.5 * b.resc_rate * n / FN_WAVES)));
+                            : (uint32_t)std::min<double>(RESCUE_GRID, std::max(8.0, std::ceil(1.5 * b.resc_rate * n / FN_WAVES)));
         hipLaunchKernelGGL(k_rescue_w, dim3(resc_grid), dim3(64 * FN_WAVES), 0, st, DP(B_QRS, rsa_query_randstrobe),
                            DP(B_QI, QrsInfo), DP(B_QCNT, uint32_t), d_qbase, p, rescue_cutoff, DP(B_RBUF, RescueD),
                            pool, DP(B_NCNT2, uint32_t), DP(B_FLAGS, uint32_t), DP(B_RBASE, uint64_t), dhdr,
