@@ -1360,13 +1360,15 @@ __device__ void find_nams_read(int r, const rsa_query_randstrobe* __restrict__ q
 #define FN_MAP_CAP 256
 
 // ---------------------------------------------------------------------------
-// k_find_nams_w2: one wavefront per read, everything in LDS (≈8.7 KB a read,
+// k_find_nams_w2: one wavefront per read, maps and hits in LDS (≈8.7 KB a read,
 // so a CU keeps ~18 reads in flight).
-//   1. the read's hits, written by k_lookup in add_to_hits_per_ref order
-//      (nam.cpp:68-85, 781-905), are copied to LDS
-//   2. lane 0 inserts the keys into the two robin_hood emulations (LDS) in
-//      hit order; the occupied slots, fwd map then rc map, give the list order
-//      merge_hits_into_nams walks (nam.cpp:370-536)
+//   1. the read's hits, written by k_seed_query in add_to_hits_per_ref order
+//      (nam.cpp:68-85, 781-905), are copied to LDS (and kept in registers, one a lane)
+//   2. lane 0 (fwd) and lane 1 (rc) insert the keys into the two robin_hood
+//      emulations (LDS) in hit order -- only the first hit of each run of equal
+//      keys, found by ballots; the rest of a run copies its list id.  The occupied
+//      slots, fwd map then rc map, give the list order merge_hits_into_nams walks
+//      (nam.cpp:370-536)
 //   3. the lists one after another, the whole wave on each (merge_list_wave):
 //      NAMs in registers, one a lane, in creation order; they carry the
 //      sequence number of their emission (flush of passed NAMs, then the final
