@@ -538,6 +538,16 @@ def main():
     ap.add_argument("--multi-device-leg", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
+    if os.environ.get("RSA_MAPS_OUT"):
+        # diagnostics: the process's mappings as Python exits (before the C-level
+        # destructors run), to attribute addresses in an exit-time native stack trace
+        import atexit
+
+        def _dump_maps(path=os.environ["RSA_MAPS_OUT"]):
+            with open("/proc/self/maps") as src, open(path, "w") as dst:
+                dst.write(src.read())
+        atexit.register(_dump_maps)
+
     if args.multi_device_leg:
         return multi_device_leg(args)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:

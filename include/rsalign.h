@@ -87,8 +87,8 @@ int rsam_map_files(rsam* m, const char* fq1, const char* fq2, int interleaved, i
  * leaves that thread detached, holding its descriptor, until the read returns. */
 
 /* ---- a rank's part of one input (rank/world mode) -----------
- * `world` processes (one per GPU, each with its own rsam) map ONE pair of plain
- * four-line FASTQ files.  The records are cut into the chunks of chunk_size pairs a
+ * `world` processes (one per GPU, each with its own rsam) map ONE pair of FASTQ
+ * files (plain or gzip).  The records are cut into the chunks of chunk_size pairs a
  * single process maps (each keeps its chunk_index, the minstd_rand seed of
  * src/pc.cpp:1583); rank r maps chunks [r*C/W, (r+1)*C/W) of the C chunks, after
  * replaying chunk 0.. until the insert-size estimate freezes (src/aln.cpp, 400
@@ -97,7 +97,7 @@ int rsam_map_files(rsam* m, const char* fq1, const char* fq2, int interleaved, i
  * concatenated in rank order are byte for byte the one-process SAM.  Statistics are
  * per part; the caller sums them over ranks (src/main.cpp:597-600).
  *
- * Planning needs each part's first record.  Each file is cut into world * 64 equal
+ * Planning needs each part's first record.  Each plain file is cut into world * 64 equal
  * byte blocks; rsam_part_count counts the newlines of rank's 64 blocks, the caller
  * all-gathers them (world * 64 integers per file, rank-major), and rsam_part_plan
  * turns them into the part.  NULL counts: the rank counts every block itself. */
@@ -108,14 +108,24 @@ typedef struct rsam_part {
     uint64_t total_pairs, n_chunks;    /* of the whole input */
     uint64_t first_chunk, end_chunk;   /* this rank's chunks */
     uint64_t first_pair, n_pairs;      /* this rank's records (pairs; single-end: reads) */
-    uint64_t offset1, offset2;         /* byte offset of first_pair in each file */
+    uint64_t offset1, offset2;         /* byte offset of first_pair in each file (record index when planned by records) */
+    uint32_t flags;                    /* RSAM_PART_RECORDS1 / _RECORDS2: that file is planned by records */
+    uint32_t reserved;
 } rsam_part;
+/* A file that is not plain four-line FASTQ -- gzip (the reference's usual input,
+ * src/fastq.cpp:1-65), wrapped lines, FASTA -- is planned by records: every rank counts
+ * its records with the kseq parser and streams it from the start, dropping the records
+ * before its part.  rsam_part_count returns zeros for a gzip file (no byte blocks). */
+#define RSAM_PART_RECORDS1 1u
+#define RSAM_PART_RECORDS2 2u
 /* newline counts of rank's RSAM_PART_BLOCKS blocks of `path` (threads: readers) */
 int rsam_part_count(const char* path, int rank, int world, int threads, uint64_t* counts);
 /* the part of `rank` (fq2 NULL or "": single-end); counts1/counts2: world * 64 each or NULL */
 int rsam_part_plan(const char* fq1, const char* fq2, int rank, int world, int chunk_size, const uint64_t* counts1,
                    const uint64_t* counts2, int threads, rsam_part* out);
-/* map a planned part: SAM body of its chunks to sam_path (rank 0: header first) */
+/* map a planned part: SAM body of its chunks to sam_path (rank 0: header first); a part
+ * whose chunk or record bounds do not follow from (rank, world, chunk_size, total_pairs),
+ * or whose byte offsets do not start a record, is refused (-1) */
 int rsam_map_files_part(rsam* m, const char* fq1, const char* fq2, const rsam_part* part, int threads,
                         const char* sam_path, rsam_stats* out);
 

@@ -442,6 +442,8 @@ static void to_c(const PartPlan& p, rsam_part* o) {
     o->n_pairs = p.n_records;
     o->offset1 = p.offset1;
     o->offset2 = p.offset2;
+    o->flags = (p.by_record1 ? RSAM_PART_RECORDS1 : 0u) | (p.by_record2 ? RSAM_PART_RECORDS2 : 0u);
+    o->reserved = 0;
 }
 
 static PartPlan from_c(const rsam_part& o) {
@@ -457,6 +459,8 @@ static PartPlan from_c(const rsam_part& o) {
     p.n_records = o.n_pairs;
     p.offset1 = o.offset1;
     p.offset2 = o.offset2;
+    p.by_record1 = (o.flags & RSAM_PART_RECORDS1) != 0;
+    p.by_record2 = (o.flags & RSAM_PART_RECORDS2) != 0;
     return p;
 }
 
@@ -496,8 +500,7 @@ int rsam_map_files_part(rsam* m, const char* fq1, const char* fq2, const rsam_pa
     try {
         const auto t0 = std::chrono::steady_clock::now();
         const PartPlan pl = from_c(*part);
-        if (pl.world < 1 || pl.rank < 0 || pl.rank >= pl.world || pl.first_chunk > pl.end_chunk)
-            throw std::runtime_error("rsam_map_files_part: bad part");
+        validate_part(fq1, fq2 ? fq2 : "", pl);     // a stale or hand-built part maps nothing
         const bool header = pl.rank == 0;
         if (pl.n_records == 0) {              // more ranks than chunks: an empty part
             rsam_reads empty;

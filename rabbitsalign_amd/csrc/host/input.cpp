@@ -247,6 +247,7 @@ class FileBlocks {
         MappedFile mf;
         size_t pos = 0;                             // mapped mode: next record's offset
         uint64_t left = UINT64_MAX;                 // records still to read (a rank's part ends early)
+        uint64_t skip = 0;                          // records before a part planned by records (PartPlan)
         bool plain_only = false;                    // a rank's part: no kseq fallback (see PartPlan)
         size_t populated = 0;                       // mapped bytes already in the page table
         std::unique_ptr<FastxReader> seq;           // sequential mode
@@ -263,6 +264,17 @@ class FileBlocks {
         void run() {
             if (g_worker_start_hook) g_worker_start_hook();
             try {
+                // a part planned by records: the records before it are parsed and dropped
+                while (skip > 0) {
+                    {
+                        std::lock_guard<std::mutex> g(m);
+                        if (stop) break;
+                    }
+                    Block b;
+                    const size_t got = fill_block(b, (size_t)std::min<uint64_t>(per_block, skip));
+                    if (got == 0) throw std::runtime_error(path + ": fewer records than the part plan skips");
+                    skip -= got;
+                }
                 for (;;) {
                     {
                         std::unique_lock<std::mutex> g(m);
@@ -349,9 +361,10 @@ class FileBlocks {
     };
 
 public:
-    // `start` / `max_records` / `plain_only`: a rank's part of a mapped file (PartPlan)
+    // `start` / `max_records` / `plain_only`: a rank's part of a mapped file (PartPlan);
+    // `skip_records`: a rank's part of a file planned by records (gzip and other layouts)
     FileBlocks(const std::string& path, size_t per_block, size_t ahead, uint64_t start = 0,
-               uint64_t max_records = UINT64_MAX, bool plain_only = false)
+               uint64_t max_records = UINT64_MAX, bool plain_only = false, uint64_t skip_records = 0)
         : st_(std::make_shared<State>()) {
         State& s = *st_;
         s.path = path;
@@ -359,6 +372,7 @@ public:
         s.ahead = std::max<size_t>(1, ahead);
         s.left = max_records;
         s.plain_only = plain_only;
+        s.skip = skip_records;
         if (!s.mf.open_map(s.path)) {
             s.mf.reset();
             if (start || plain_only)
@@ -543,8 +557,17 @@ public:
         const uint64_t tail = p2.empty() ? 0 : std::min<uint64_t>(per, plan.total_records - plan.first_record -
                                                                             plan.n_records);
         const uint64_t n = plan.n_records ? plan.n_records + tail : 0;
-        r1_.reset(new FileBlocks(p1, per, kAhead, plan.offset1, n, true));
-        if (!p2.empty()) r2_.reset(new FileBlocks(p2, per, kAhead, plan.offset2, n, true));
+        // a file planned by bytes starts at its offset and must keep the plain layout; one
+        // planned by records (gzip, other layouts) is parsed from its start, the records
+        // before the part dropped
+        auto open = [&](const std::string& p, bool by_record, uint64_t off) {
+            return by_record ? new FileBlocks(p, per, kAhead, 0, n, false, plan.first_record)
+                             : new FileBlocks(p, per, kAhead, off, n, true);
+        };
+        if (n) {                        // an empty part (an empty input, more ranks than chunks) reads nothing
+            r1_.reset(open(p1, plan.by_record1, plan.offset1));
+            if (!p2.empty()) r2_.reset(open(p2, plan.by_record2, plan.offset2));
+        }
         if (plan.first_chunk > 0 && !p2.empty()) open_prefix();
     }
     bool paired() const override { return !p2_.empty(); }
@@ -553,7 +576,7 @@ public:
             if (!f1_) throw std::logic_error("a chunk before the part asked for without the insert-size replay");
             return take_chunk(*f1_, f2_.get(), false, idx, idx, out);
         }
-        if (idx > plan_.end_chunk || (idx == plan_.end_chunk && !paired())) {
+        if (!r1_ || idx > plan_.end_chunk || (idx == plan_.end_chunk && !paired())) {
             out.clear();
             out.index = idx;
             return false;
@@ -564,7 +587,7 @@ public:
         if (c.index < plan_.first_chunk) {
             if (f1_) f1_->done(c.index);
             if (f2_) f2_->done(c.index);
-        } else {
+        } else if (r1_) {
             r1_->done(c.index - plan_.first_chunk);
             if (r2_) r2_->done(c.index - plan_.first_chunk);
         }
@@ -686,34 +709,65 @@ uint64_t after_newline(const std::string& path, const std::vector<uint64_t>& lin
     throw std::runtime_error(path + ": newline count changed while planning");
 }
 
-// records of a plain four-line FASTQ from its block counts (a last line without '\n' counts)
+// records of a plain four-line FASTQ from its block counts (a last line without '\n'
+// counts; empty lines at the end do not, as kseq skips them); UINT64_MAX when the line
+// count does not fit four lines a record (the file is then planned by records)
 uint64_t records_of(const std::string& path, const std::vector<uint64_t>& lines) {
     Fd f(path);
     const uint64_t size = f.size();
     uint64_t n = 0;
     for (uint64_t c : lines) n += c;
     if (size) {
-        char last = 0;
-        if (pread(f.fd, &last, 1, (off_t)(size - 1)) != 1) throw std::runtime_error("read failed: " + path);
-        if (last != '\n') ++n;
+        char tail[256];
+        const size_t k = (size_t)std::min<uint64_t>(size, sizeof tail);
+        if (pread(f.fd, tail, k, (off_t)(size - k)) != (ssize_t)k) throw std::runtime_error("read failed: " + path);
+        if (tail[k - 1] != '\n') {
+            ++n;
+        } else {
+            size_t j = k - 1;                   // "\n\n...": every '\n' after the first ends an empty line
+            while (j > 0 && (tail[j - 1] == '\n' || tail[j - 1] == '\r') && n > 0) {
+                if (tail[j - 1] == '\n') --n;
+                --j;
+            }
+        }
     }
-    if (n % 4) throw std::runtime_error(path + ": " + std::to_string(n) + " lines, not a plain four-line FASTQ (a "
-                                        "rank's part needs one record per four lines; map it in one process)");
-    return n / 4;
+    return n % 4 ? UINT64_MAX : n / 4;
 }
 
-void check_record_start(const std::string& path, uint64_t off) {
+bool check_record_start(const std::string& path, uint64_t off) {
     Fd f(path);
     char c = 0;
-    if (pread(f.fd, &c, 1, (off_t)off) != 1 || c != '@')
-        throw std::runtime_error(path + ": no FASTQ record starts at byte " + std::to_string(off) +
-                                 " (a rank's part needs the plain four-line layout)");
+    return pread(f.fd, &c, 1, (off_t)off) == 1 && c == '@';
+}
+
+bool is_gzip(const std::string& path) {
+    Fd f(path);
+    unsigned char m[2] = {0, 0};
+    return pread(f.fd, m, 2, 0) == 2 && m[0] == 0x1f && m[1] == 0x8b;
+}
+
+// records of a file as kseq++ reads them (FastxReader): gzip, wrapped lines, FASTA
+uint64_t count_records_kseq(const std::string& path) {
+    FastxReader rd(path);
+    Record r;
+    uint64_t n = 0;
+    while (rd.next(r)) ++n;
+    return n;
+}
+
+void part_bounds(PartPlan& pl) {
+    pl.n_chunks = (pl.total_records + pl.chunk_size - 1) / pl.chunk_size;
+    pl.first_chunk = pl.n_chunks * (uint64_t)pl.rank / (uint64_t)pl.world;
+    pl.end_chunk = pl.n_chunks * (uint64_t)(pl.rank + 1) / (uint64_t)pl.world;
+    pl.first_record = std::min(pl.total_records, pl.first_chunk * pl.chunk_size);
+    pl.n_records = std::min(pl.total_records, pl.end_chunk * pl.chunk_size) - pl.first_record;
 }
 
 }  // namespace
 
 std::vector<uint64_t> count_part_lines(const std::string& path, int rank, int world, int threads) {
     if (world < 1 || rank < 0 || rank >= world) throw std::runtime_error("bad rank/world");
+    if (is_gzip(path)) return std::vector<uint64_t>(kPartBlocks, 0);   // planned by records: not used
     return count_blocks(path, (uint64_t)world * kPartBlocks, (uint64_t)rank * kPartBlocks, kPartBlocks, threads);
 }
 
@@ -721,31 +775,68 @@ PartPlan plan_part(const std::string& p1, const std::string& p2, int rank, int w
                    std::vector<uint64_t> lines1, std::vector<uint64_t> lines2, int threads) {
     if (world < 1 || rank < 0 || rank >= world) throw std::runtime_error("bad rank/world");
     const uint64_t nb = (uint64_t)world * kPartBlocks;
-    if (lines1.empty()) lines1 = count_blocks(p1, nb, 0, nb, threads);
-    if (!p2.empty() && lines2.empty()) lines2 = count_blocks(p2, nb, 0, nb, threads);
-    if (lines1.size() != nb || (!p2.empty() && lines2.size() != nb))
+    const bool gz1 = is_gzip(p1), gz2 = !p2.empty() && is_gzip(p2);
+    if (lines1.empty() && !gz1) lines1 = count_blocks(p1, nb, 0, nb, threads);
+    if (!p2.empty() && lines2.empty() && !gz2) lines2 = count_blocks(p2, nb, 0, nb, threads);
+    if ((!gz1 && lines1.size() != nb) || (!p2.empty() && !gz2 && lines2.size() != nb))
         throw std::runtime_error("part plan: expected world * 64 block counts per file");
     PartPlan pl;
     pl.rank = rank;
     pl.world = world;
     pl.chunk_size = std::max<size_t>(1, chunk_size);
-    pl.total_records = records_of(p1, lines1);
-    if (!p2.empty() && records_of(p2, lines2) != pl.total_records)
-        throw std::runtime_error("read files have different record counts");
-    pl.n_chunks = (pl.total_records + pl.chunk_size - 1) / pl.chunk_size;
-    pl.first_chunk = pl.n_chunks * (uint64_t)rank / (uint64_t)world;
-    pl.end_chunk = pl.n_chunks * (uint64_t)(rank + 1) / (uint64_t)world;
-    pl.first_record = std::min(pl.total_records, pl.first_chunk * pl.chunk_size);
-    pl.n_records = std::min(pl.total_records, pl.end_chunk * pl.chunk_size) - pl.first_record;
+    // the same decision on every rank: it rests on the file's first bytes and on the
+    // all-gathered counts only
+    uint64_t n1 = gz1 ? UINT64_MAX : records_of(p1, lines1);
+    uint64_t n2 = p2.empty() ? 0 : gz2 ? UINT64_MAX : records_of(p2, lines2);
+    pl.by_record1 = n1 == UINT64_MAX;
+    pl.by_record2 = !p2.empty() && n2 == UINT64_MAX;
+    {
+        std::thread t2;
+        std::exception_ptr e2;
+        if (pl.by_record2) t2 = std::thread([&] { try { n2 = count_records_kseq(p2); } catch (...) { e2 = std::current_exception(); } });
+        if (pl.by_record1) n1 = count_records_kseq(p1);
+        if (t2.joinable()) t2.join();
+        if (e2) std::rethrow_exception(e2);
+    }
+    pl.total_records = n1;
+    if (!p2.empty() && n2 != pl.total_records) throw std::runtime_error("read files have different record counts");
+    part_bounds(pl);
     if (pl.n_records) {
-        pl.offset1 = pl.first_record ? after_newline(p1, lines1, 4 * pl.first_record) : 0;
-        check_record_start(p1, pl.offset1);
-        if (!p2.empty()) {
-            pl.offset2 = pl.first_record ? after_newline(p2, lines2, 4 * pl.first_record) : 0;
-            check_record_start(p2, pl.offset2);
-        }
+        auto offset = [&](const std::string& p, bool by_record, const std::vector<uint64_t>& lines) -> uint64_t {
+            if (by_record) return pl.first_record;
+            const uint64_t off = pl.first_record ? after_newline(p, lines, 4 * pl.first_record) : 0;
+            if (!check_record_start(p, off))
+                throw std::runtime_error(p + ": no FASTQ record starts at byte " + std::to_string(off) +
+                                         " (a rank's part of an uncompressed file needs the plain four-line layout)");
+            return off;
+        };
+        pl.offset1 = offset(p1, pl.by_record1, lines1);
+        if (!p2.empty()) pl.offset2 = offset(p2, pl.by_record2, lines2);
     }
     return pl;
+}
+
+void validate_part(const std::string& p1, const std::string& p2, const PartPlan& plan) {
+    auto bad = [](const std::string& why) { throw std::runtime_error("inconsistent part: " + why); };
+    if (plan.world < 1 || plan.rank < 0 || plan.rank >= plan.world) bad("rank/world");
+    if (plan.chunk_size < 1) bad("chunk size");
+    PartPlan want = plan;
+    part_bounds(want);
+    if (want.n_chunks != plan.n_chunks || want.first_chunk != plan.first_chunk || want.end_chunk != plan.end_chunk)
+        bad("chunks [" + std::to_string(plan.first_chunk) + ", " + std::to_string(plan.end_chunk) + ") of " +
+            std::to_string(plan.n_chunks) + " for rank " + std::to_string(plan.rank) + " of " +
+            std::to_string(plan.world) + " over " + std::to_string(plan.total_records) + " records");
+    if (want.first_record != plan.first_record || want.n_records != plan.n_records)
+        bad("records [" + std::to_string(plan.first_record) + ", +" + std::to_string(plan.n_records) +
+            ") for its chunks");
+    if (!plan.n_records) return;
+    auto check = [&](const std::string& p, bool by_record, uint64_t off) {
+        if (by_record ? off != plan.first_record : !check_record_start(p, off))
+            bad(p + ": no record " + std::to_string(plan.first_record) + " at " + (by_record ? "record " : "byte ") +
+                std::to_string(off));
+    };
+    check(p1, plan.by_record1, plan.offset1);
+    if (!p2.empty()) check(p2, plan.by_record2, plan.offset2);
 }
 
 std::unique_ptr<ReadSource> open_fastq_part_source(const std::string& p1, const std::string& p2, const PartPlan& plan) {

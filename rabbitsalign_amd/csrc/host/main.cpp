@@ -41,8 +41,9 @@ void usage(const char* prog) {
             "  -t INT threads [3]   --chunk-size INT [10000]   -o PATH   --eqx   -U   --details\n"
             "  --rg-id ID  --rg TAG:VALUE   -N INT   -i/--create-index   --use-index   --device INT   --cpu-index\n"
             "  --devices LIST  map on several GPUs of this node (e.g. 0,1,2,3; index replicated per device)\n"
-            "  --rank R --world W  map part R of W of the input (plain FASTQ); the SAM parts of ranks\n"
-            "                      0..W-1 concatenated are the one-process SAM (rank 0's has the header)\n"
+            "  --rank R --world W  map part R of W of the input (FASTQ, plain or gzip); the SAM parts of\n"
+            "                      ranks 0..W-1 concatenated are the one-process SAM (rank 0's has the header;\n"
+            "                      its @PG command line is the run's own, e.g. its -o)\n"
             "  seeding: -r -m -k -l -u -s -c -b      alignment: -A -B -O -E -L\n"
             "  search: -f FLOAT -S FLOAT -M INT -R INT\n",
             prog, prog);
@@ -188,8 +189,15 @@ int cli_main(int argc, char** argv, EngineFactory factory, const char* prog) {
         const double t_upload = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
         FILE* out = o.out_file.empty() ? stdout : fopen(o.out_file.c_str(), "wb");
         if (!out) throw std::runtime_error("cannot open " + o.out_file);
+        // the @PG command line leaves --rank/--world out: rank 0's header is the one a
+        // single process given the other arguments writes
         std::string cmd;
-        for (int i = 0; i < argc; ++i) { cmd += argv[i]; cmd += ' '; }
+        for (int i = 0; i < argc; ++i) {
+            const std::string a = argv[i];
+            if ((a == "--rank" || a == "--world") && i + 1 < argc) { ++i; continue; }
+            cmd += a;
+            cmd += ' ';
+        }
         std::string hdr = sam_header(refs, o.rg_id, o.rg, cmd);
         if (o.rank == 0) fwrite(hdr.data(), 1, hdr.size(), out);
         MapContext mc{refs, idx.params, ap, mp};

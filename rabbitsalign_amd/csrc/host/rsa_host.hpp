@@ -687,7 +687,7 @@ std::unique_ptr<ReadSource> open_fastq_source(const std::string& path1, const st
                                               size_t chunk_size);
 
 // ------------------------------------------------------- a rank's part ---
-// rank/world mode: one input pair of plain four-line FASTQ files,
+// rank/world mode: one input pair of FASTQ files (plain or gzip),
 // mapped by `world` processes (one per GPU).  The records are cut into the same
 // chunks of chunk_size pairs a single process maps, so every chunk keeps its
 // chunk_index (the minstd_rand seed, pc.cpp:1583); rank r maps chunks
@@ -704,6 +704,12 @@ std::unique_ptr<ReadSource> open_fastq_source(const std::string& path1, const st
 // own kPartBlocks blocks, the counts of all ranks are exchanged (an all-gather of
 // world * kPartBlocks integers per file, done by the caller), and the plan follows:
 // record i starts after newline 4i.  With no exchange a rank counts every block.
+//
+// A file that is not in that layout -- gzip (the reference's usual input, read with
+// kseq++: src/fastq.cpp:1-65), wrapped lines, FASTA -- is planned by records instead
+// (`by_record`): each rank counts the file's records with the kseq parser and skips
+// the records before its part while it streams the file from its start.  The
+// block counts of such a file are not used (rsam_part_count returns zeros for gzip).
 constexpr int kPartBlocks = 64;
 struct PartPlan {
     int rank = 0, world = 1;
@@ -711,7 +717,8 @@ struct PartPlan {
     uint64_t total_records = 0, n_chunks = 0;    // records (pairs) of the input, chunks of the input
     uint64_t first_chunk = 0, end_chunk = 0;     // this rank's chunks
     uint64_t first_record = 0, n_records = 0;    // this rank's records
-    uint64_t offset1 = 0, offset2 = 0;           // byte offset of first_record in each file
+    uint64_t offset1 = 0, offset2 = 0;           // byte offset of first_record in each file (record index when by_record)
+    bool by_record1 = false, by_record2 = false; // the file is planned by records (see above)
 };
 // newline counts of rank `rank`'s kPartBlocks blocks of a file cut into world * kPartBlocks
 std::vector<uint64_t> count_part_lines(const std::string& path, int rank, int world, int threads);
@@ -719,6 +726,9 @@ std::vector<uint64_t> count_part_lines(const std::string& path, int rank, int wo
 // p2 empty: single-end
 PartPlan plan_part(const std::string& p1, const std::string& p2, int rank, int world, size_t chunk_size,
                    std::vector<uint64_t> lines1, std::vector<uint64_t> lines2, int threads);
+// throws unless `plan` is a consistent part of these files (chunk and record bounds,
+// a record starting at each byte offset)
+void validate_part(const std::string& p1, const std::string& p2, const PartPlan& plan);
 // the chunks of the plan, streamed (plus chunks 0.. from the file start when the
 // paired pipeline replays the insert-size phase)
 std::unique_ptr<ReadSource> open_fastq_part_source(const std::string& p1, const std::string& p2, const PartPlan& plan);

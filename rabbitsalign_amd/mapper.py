@@ -43,7 +43,8 @@ class Part(C.Structure):
     """rsam_part (include/rsalign.h): one rank's chunks of a shared input."""
     _fields_ = [("rank", C.c_int32), ("world", C.c_int32), ("chunk_size", C.c_uint64), ("total_pairs", C.c_uint64),
                 ("n_chunks", C.c_uint64), ("first_chunk", C.c_uint64), ("end_chunk", C.c_uint64),
-                ("first_pair", C.c_uint64), ("n_pairs", C.c_uint64), ("offset1", C.c_uint64), ("offset2", C.c_uint64)]
+                ("first_pair", C.c_uint64), ("n_pairs", C.c_uint64), ("offset1", C.c_uint64), ("offset2", C.c_uint64),
+                ("flags", C.c_uint32), ("reserved", C.c_uint32)]
 
     def as_dict(self) -> dict:
         return {f: getattr(self, f) for f, _ in self._fields_}

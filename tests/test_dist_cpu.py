@@ -113,13 +113,15 @@ def _part_worker(rank, world, port, fq1, fq2, out_dir, q):
 
 
 @pytest.mark.skipif(not os.path.exists(REF_CPU_LIB), reason="CPU-path library not built")
-@pytest.mark.parametrize("world", [2, 4])
-def test_shared_input_gloo(tmp_path, world):
+@pytest.mark.parametrize("world,gz", [(2, False), (4, False), (2, True)], ids=["w2", "w4", "w2_gzip"])
+def test_shared_input_gloo(tmp_path, world, gz):
     """`world` ranks map ONE FASTQ pair: each counts its 1/world of each file, the counts
     are all-gathered over gloo, each maps its chunks into its own SAM part (every rank past
     the first replays the insert-size estimate from chunk 0).  Header + parts in rank order ==
     the single-process SAM of the same files, byte for byte; the summed statistics == the
-    single process's."""
+    single process's.  gzip: the ranks map .fq.gz files (planned by records: each rank
+    counts the records and skips to its part) and must still give the one-process SAM of
+    the plain files."""
     import torch.multiprocessing as mp
     from rabbitsalign_amd import mapper, shard
     m = mapper.Mapper.synthetic(CFG["seed"], CFG["ref_len"], CFG["contigs"], CFG["L"], threads=2,
@@ -131,6 +133,13 @@ def test_shared_input_gloo(tmp_path, world):
     one = str(tmp_path / "one.sam")
     st1 = m.map_files(fq1, fq2, threads=2, chunk_size=PART["chunk"], sam_path=one)
     m.close()
+    if gz:
+        import gzip
+        import shutil
+        for f in (fq1, fq2):
+            with open(f, "rb") as a, gzip.open(f + ".gz", "wb", compresslevel=1) as b:
+                shutil.copyfileobj(a, b)
+        fq1, fq2 = fq1 + ".gz", fq2 + ".gz"
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -147,6 +156,7 @@ def test_shared_input_gloo(tmp_path, world):
         assert p.exitcode == 0
     n_chunks = (PART["pairs"] + PART["chunk"] - 1) // PART["chunk"]
     assert res[0][0]["first_chunk"] == 0 and res[world - 1][0]["end_chunk"] == n_chunks
+    assert all(res[r][0]["flags"] == (3 if gz else 0) for r in range(world))   # RSAM_PART_RECORDS1 | _RECORDS2
     for r in range(1, world):
         assert res[r][0]["first_chunk"] == res[r - 1][0]["end_chunk"] and res[r][0]["first_chunk"] > 0
     parts = b"".join(open(tmp_path / f"part{r}.sam", "rb").read() for r in range(world))
@@ -154,3 +164,27 @@ def test_shared_input_gloo(tmp_path, world):
     for r in range(world):
         assert res[r][1]["n_reads"] == st1.n_reads
         assert all(res[r][1][f] == getattr(st1, f) for f in shard.STAT_FIELDS)
+
+
+@pytest.mark.skipif(not os.path.exists(REF_CPU_LIB), reason="CPU-path library not built")
+def test_part_refuses_inconsistent_plan(tmp_path):
+    """rsam_map_files_part re-checks the part it is handed: chunk bounds that do not follow
+    from rank/world, a record range that does not match the chunks, or a byte offset that
+    does not start a record are refused before anything is mapped."""
+    from rabbitsalign_amd import mapper
+    m = mapper.Mapper.synthetic(CFG["seed"], CFG["ref_len"], CFG["contigs"], CFG["L"], threads=2,
+                                lib_path=REF_CPU_LIB)
+    reads = m.synthetic_reads(7, 0, 900, CFG["L"], 300.0, 30.0, True)
+    fq1, fq2 = str(tmp_path / "r1.fq"), str(tmp_path / "r2.fq")
+    reads.write_fastq(fq1, fq2)
+    reads.close()
+    good = mapper.part_plan(fq1, fq2, 1, 2, 100, None, None, 2, lib_path=REF_CPU_LIB)
+    assert good.first_chunk == 4 and good.first_pair == 400 and good.offset1 > 0
+    st = m.map_files_part(fq1, fq2, good, threads=2, sam_path=str(tmp_path / "ok.sam"))
+    assert st.n_reads == 2 * good.n_pairs
+    for field, delta in (("offset1", 1), ("first_chunk", 1), ("first_pair", 100), ("n_pairs", -1), ("offset2", -3)):
+        bad = mapper.Part.from_buffer_copy(good)
+        setattr(bad, field, getattr(bad, field) + delta)
+        with pytest.raises(RuntimeError, match="inconsistent part"):
+            m.map_files_part(fq1, fq2, bad, threads=2, sam_path=str(tmp_path / "bad.sam"))
+    m.close()
