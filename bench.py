@@ -841,6 +841,8 @@ def main():
             "index_build": {"on": "gpu" if info["index_on_device"] else "host",
                             "seconds": round(info["index_seconds"], 3), "device_ms": info["index_device_ms"],
                             "replayed_segments": info["index_replayed_segments"],
+                            "position_ties": info["index_position_ties"],
+                            "ms_tie_replay": round(info["index_ms_tie_replay"], 1),
                             "note": "StrobemerIndex::populate (index.cpp:141-309) via rsa_index_build_run; the "
                                     "index stays in HBM and the engine adopts it (rsa_open_built)"},
             "roofline": rl,

@@ -281,6 +281,7 @@ typedef struct rsa_index_build_params {
     uint64_t q;
     int32_t bits;                      /* < 0: pick_bits (index.cpp:135-139) */
     float f;                           /* top fraction of repetitive hashes (-f, default 0.0002) */
+    int32_t threads;                   /* host threads for the tie-order replay (<= 0: the machine's, max 64) */
 } rsa_index_build_params;
 
 typedef struct rsa_index_build_info {

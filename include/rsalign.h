@@ -38,7 +38,9 @@ typedef struct rsam_stats {
 /* Open from files: FASTA + optional .sti (NULL: build the index in memory). */
 rsam* rsam_open_files(const char* ref_fa, const char* sti, int read_len, int device, int threads, char* err,
                       size_t err_len);
-/* Open on a synthetic reference (seeded): n_contigs equal contigs. */
+/* Open on a synthetic reference (seeded): n_contigs equal contigs.
+ * RSA_SYNTH_DUP=<bp> (measurement): chr1[1 Mb, 1 Mb + bp) is copied onto chr2 at the same
+ * coordinates, a PAR-like region whose randstrobes tie in (hash, position). */
 rsam* rsam_open_synthetic(uint64_t seed, uint64_t ref_len, int n_contigs, int read_len, int device, int threads,
                           char* err, size_t err_len);
 /* Open on the host-side reference + index of another mapper (no rebuild). */
@@ -55,6 +57,8 @@ typedef struct rsam_info {
     int32_t pad_;
     double index_device_ms[6];         /* GPU build phases: upload, syncmers, randstrobes, sort, buckets, total */
     uint64_t index_replayed_segments;  /* GPU build: segments replayed past their warm-up (tandem repeats) */
+    uint64_t index_position_ties;      /* entries equal in (hash, position) to their predecessor (other contigs) */
+    double index_ms_tie_replay;        /* GPU build: host replay of pdqsort's order of those ties, incl. transfers */
 } rsam_info;
 int rsam_get_info(const rsam* m, rsam_info* out);
 

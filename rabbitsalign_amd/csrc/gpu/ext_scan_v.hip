@@ -187,8 +187,10 @@ __device__ __forceinline__ FwdV fwd_v(const uint16_t* __restrict__ prof, int nro
             E[r] = hmax3(E[r] - GE2, t, zero);
             Fw = hmax3(Fw - GE2, t, zero);
             F = hmax3(F - GE2, t, zero);
-            cm = hmax(cm, h);
         }
+        // the column maximum over row pairs: one three-input max per two rows
+#pragma unroll
+        for (int r = 0; r < RV; r += 2) cm = r + 1 < RV ? hmax3(cm, Hout[r], Hout[r + 1]) : hmax(cm, Hout[r]);
         F_out = h2_bits(F);
         Fw_out = h2_bits(Fw);
         H_last = h2_bits(Hout[RV - 1]);
@@ -307,8 +309,10 @@ __device__ __forceinline__ void rev_v(const uint16_t* __restrict__ prof, int nro
             E[r] = hmax3(E[r] - GE2, t, zero);
             Fw = hmax3(Fw - GE2, t, zero);
             F = hmax3(F - GE2, t, zero);
-            cm = hmax(cm, h);           // padding rows included: cm >= the valid rows' maximum
         }
+        // padding rows included: cm >= the valid rows' maximum
+#pragma unroll
+        for (int r = 0; r < RV; r += 2) cm = r + 1 < RV ? hmax3(cm, Hout[r], Hout[r + 1]) : hmax(cm, Hout[r]);
         F_out = h2_bits(F);
         Fw_out = h2_bits(Fw);
         H_last = h2_bits(Hout[RV - 1]);
@@ -360,9 +364,24 @@ __device__ __forceinline__ int qcode7(unsigned char b) {
     return c < 4 ? c : 7;
 }
 
+// 4 bytes as 4 codes, packed: byte b (at position pos0 + b) -> code(byte) when the
+// position is in [0, len), else `pad`
+template <class CF>
+__device__ __forceinline__ uint32_t codes4(uint32_t x, int pos0, int len, CF code, uint32_t pad) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const int pos = pos0 + b;
+        const uint32_t c = (pos >= 0 && pos < len) ? (uint32_t)code((x >> (8 * b)) & 0xFF) : pad;
+        r |= c << (8 * b);
+    }
+    return r;
+}
+
 }  // namespace
 
-// jobs[order[k]] for k < n; results land at out[order[k]].  Every job handed
+// Job k < n is sjobs[k] (the descriptors in scan order, staged so by the host) and
+// its result lands at out[order[k]].  Every job handed
 // here has 0 < qlen <= 32 * RV and rlen <= WCAP (the host routes the rest to
 // k_ext_scan).
 // waves per SIMD the register allocation is held to (VS_MINW_SHORT for RV <= 5, VS_MINW_LONG
@@ -377,58 +396,63 @@ template <int RV> struct VsMinW { static constexpr int value = RV <= 5 ? VS_MINW
 
 template <int RV, int WCAP>
 __global__ void __launch_bounds__(64 * VS_WAVES, VsMinW<RV>::value)
-k_ext_scan_v(const ExtJobDev* __restrict__ jobs, const int* __restrict__ order, int n,
+k_ext_scan_v(const ExtJobDev* __restrict__ sjobs, const int* __restrict__ order, int n,
              const char* __restrict__ qbuf, const char* __restrict__ ref, ScanRes* __restrict__ out,
              int match, int mismatch, int gO, int gE, int* __restrict__ err) {
-    __shared__ __attribute__((aligned(4))) uint8_t s_r[VS_JOBS][WCAP + 2 * VS_PAD];
+    // a slot: VS_PAD bytes of padding, the window from the dword-aligned base (its first
+    // byte at base + (r_off & 3)), WCAP + VS_PAD bytes after the base in all
+    constexpr int SLOT = WCAP + 2 * VS_PAD + 4;
+    constexpr int QSLOT = 32 * RV + 4;
+    __shared__ __attribute__((aligned(4))) uint8_t s_r[VS_JOBS][SLOT];
     __shared__ __attribute__((aligned(16))) uint16_t s_prof[VS_JOBS][VProf<RV>::JOB];
-    __shared__ __attribute__((aligned(4))) uint8_t s_q[VS_JOBS][32 * RV];   // query codes (qcode7), 7 past the query
+    __shared__ __attribute__((aligned(4))) uint8_t s_q[VS_JOBS][QSLOT];   // query codes (qcode7), 7 past the query
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int slot = wave * (64 / VS_G) + lane / VS_G, gl = lane & (VS_G - 1);
     const int k = blockIdx.x * VS_JOBS + slot;
     const bool on = k < n;
+    // the descriptor and the result index in one round trip (both indexed by k)
     const int j = on ? order[k] : 0;
     ExtJobDev jb;
     jb.q_off = 0; jb.r_off = 0; jb.qlen = 0; jb.rlen = 0; jb.cig_off = 0;
-    if (on) jb = jobs[j];
+    if (on) jb = sjobs[k];
     const int qlen = (int)jb.qlen, rlen = (int)jb.rlen;
-    uint8_t* rc = s_r[slot] + VS_PAD;
+    const int pre = (int)(jb.r_off & 3), preq = (int)(jb.q_off & 3);
+    uint8_t* rcb = s_r[slot] + VS_PAD;
+    uint8_t* rc = rcb + pre;
     uint16_t* prof = s_prof[slot];
-    uint8_t* qc = s_q[slot];
+    uint8_t* qc = s_q[slot] + preq;
 
-    // stage: the window as SSW codes, code-4 padding before it and from its end to the end
-    // of the slot (the wave's steps read up to 32 columns past its longest window), and
-    // the forward profile
-    for (int i = gl; i < VS_PAD; i += VS_G) rc[i - VS_PAD] = 4;
-    for (int i = rlen + gl; i < WCAP + VS_PAD; i += VS_G) rc[i] = 4;
+    // stage the window and the query as SSW codes, a dword (4 codes) at a time.  Every
+    // load of a lane is issued before any is used (indices clamped into the job's own
+    // dwords; the device reference carries 64 bytes of tail padding and the query
+    // buffer a dword past its end), then the codes are written: code-4 padding before
+    // the window and from its end to the end of the slot (the wave's steps read up to
+    // 32 columns past its longest window), query code 7 past the query.
     {
-        // aligned dwords covering the window (the device reference carries 64 bytes of tail padding)
-        const int pre = (int)(jb.r_off & 3);
+        constexpr int WD = ((WCAP + 6) / 4 + VS_G - 1) / VS_G;      // window dwords a lane loads at most
+        constexpr int QD = (32 * RV + 3 + 4 * VS_G - 1) / (4 * VS_G);   // query dwords a lane loads at most
         const uint32_t* w = (const uint32_t*)(ref + (jb.r_off - (uint64_t)pre));
-        const int nw = (pre + rlen + 3) >> 2;
-        for (int i = gl; i < nw; i += VS_G) {
-            const uint32_t x = w[i];
+        const uint32_t* qw = (const uint32_t*)(qbuf + (jb.q_off - (uint64_t)preq));
+        const int nw = (pre + rlen + 3) >> 2, nq = (preq + qlen + 3) >> 2;
+        const int wl = max(nw - 1, 0), ql = max(nq - 1, 0);
+        uint32_t x[WD], y[QD];
 #pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int pos = 4 * i + b - pre;
-                if (pos >= 0 && pos < rlen) rc[pos] = (uint8_t)ssw_code((x >> (8 * b)) & 0xFF);
-            }
+        for (int t = 0; t < WD; ++t) x[t] = w[min(gl + t * VS_G, wl)];
+#pragma unroll
+        for (int t = 0; t < QD; ++t) y[t] = qw[min(gl + t * VS_G, ql)];
+        uint32_t* rcw = (uint32_t*)rcb;
+        for (int i = gl; i < VS_PAD / 4; i += VS_G) rcw[i - VS_PAD / 4] = 0x04040404u;
+#pragma unroll
+        for (int t = 0; t < WD; ++t) {
+            const int i = gl + t * VS_G;
+            if (i < nw) rcw[i] = codes4(x[t], 4 * i - pre, rlen, [](uint32_t b) { return ssw_code((unsigned char)b); }, 4u);
         }
-    }
-    {
-        // the query once, by aligned dwords (the forward and the reverse profile both read it
-        // from LDS; the query buffer's allocation covers the dword past its last byte)
-        for (int i = qlen + gl; i < 32 * RV; i += VS_G) qc[i] = 7;
-        const int pre = (int)(jb.q_off & 3);
-        const uint32_t* w = (const uint32_t*)(qbuf + (jb.q_off - (uint64_t)pre));
-        const int nw = (pre + qlen + 3) >> 2;
-        for (int i = gl; i < nw; i += VS_G) {
-            const uint32_t x = w[i];
+        for (int i = nw + gl; i < (WCAP + VS_PAD + 4) / 4; i += VS_G) rcw[i] = 0x04040404u;
+        uint32_t* qcw = (uint32_t*)s_q[slot];
 #pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int pos = 4 * i + b - pre;
-                if (pos >= 0 && pos < qlen) qc[pos] = (uint8_t)qcode7((x >> (8 * b)) & 0xFF);
-            }
+        for (int t = 0; t < QD; ++t) {
+            const int i = gl + t * VS_G;
+            if (i < QSLOT / 4) qcw[i] = codes4(y[t], 4 * i - preq, qlen, [](uint32_t b) { return qcode7((unsigned char)b); }, 7u);
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -533,13 +557,14 @@ int scan_v_wcap(uint32_t rlen) {
     return 0;
 }
 
-void launch_ext_scan_v(int rv, int wcap, int n, hipStream_t st, const ExtJobDev* jobs, const int* order, const char* q,
+// sjobs: the class's descriptors in scan order; order: their indices (results go to out[order[k]])
+void launch_ext_scan_v(int rv, int wcap, int n, hipStream_t st, const ExtJobDev* sjobs, const int* order, const char* q,
                        const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE, int* err) {
     if (n <= 0) return;
     const dim3 grid((n + VS_JOBS - 1) / VS_JOBS), block(64 * VS_WAVES);
 #define RSA_V(RR, WW)                                                                                             \
     if (rv == RR && wcap == WW) {                                                                                 \
-        hipLaunchKernelGGL((k_ext_scan_v<RR, WW>), grid, block, 0, st, jobs, order, n, q, ref, out, match,        \
+        hipLaunchKernelGGL((k_ext_scan_v<RR, WW>), grid, block, 0, st, sjobs, order, n, q, ref, out, match,       \
                            mismatch, gO, gE, err);                                                                \
         return;                                                                                                   \
     }

@@ -668,15 +668,29 @@ rsa_index_build* rsa_index_build_run(int device, const char* ref_seq, const uint
         BCHK(hipGetLastError());
     }
     BCHK(hipEventRecord(ev[5], st));
-    // d_raw (generation order) stays until the tie count is known: the replay starts from it
+    // d_raw (generation order) stays until the tie count is known: the replay starts from
+    // it.  The counts run first, so without ties it is freed before the bucket table exists
+    // (the peak is then entries + raw entries, not + the table)
 
-    // bucket table + run-length histogram
-    const uint64_t nb = 1ull << bits;
-    BCHK(hipMalloc(&B->d_starts, 8 * (nb + 1)));
+    // run-length histogram (and the tie count, bin 103), then the bucket table
     unsigned long long* d_hist = nullptr;
     BCHK(dalloc((void**)&d_hist, 8 * RC_BINS));
     BCHK(hipMemsetAsync(d_hist, 0, 8 * RC_BINS, st));
     BCHK(hipEventRecord(ev[6], st));
+    if (n) {
+        k_run_counts<<<(unsigned)std::min<uint64_t>(RC_BLOCKS, grid_of(n)), TPB, 0, st>>>(B->d_rs, n, d_hist);
+        BCHK(hipGetLastError());
+    }
+    unsigned long long hist[RC_BINS];
+    BCHK(hipMemcpyAsync(hist, d_hist, sizeof hist, hipMemcpyDeviceToHost, st));
+    BCHK(hipStreamSynchronize(st));
+    const uint64_t ties = hist[103];
+    if (!ties) {
+        dfree(d_raw);
+        d_raw = nullptr;
+    }
+    const uint64_t nb = 1ull << bits;
+    BCHK(hipMalloc(&B->d_starts, 8 * (nb + 1)));
     // no hash change at all (n <= 1 or a single run): every bucket gets n (index.cpp:206-208)
     k_fill_u64<<<grid_of(nb + 1), TPB, 0, st>>>(B->d_starts, nb + 1, n);
     BCHK(hipGetLastError());
@@ -684,31 +698,27 @@ rsa_index_build* rsa_index_build_run(int device, const char* ref_seq, const uint
         k_bucket_table<<<grid_of(n), TPB, 0, st>>>(B->d_rs, n, bits, B->d_starts);
         BCHK(hipGetLastError());
     }
-    if (n) {
-        k_run_counts<<<(unsigned)std::min<uint64_t>(RC_BLOCKS, grid_of(n)), TPB, 0, st>>>(B->d_rs, n, d_hist);
-        BCHK(hipGetLastError());
-    }
     BCHK(hipEventRecord(ev[7], st));
-    unsigned long long hist[RC_BINS];
-    BCHK(hipMemcpyAsync(hist, d_hist, sizeof hist, hipMemcpyDeviceToHost, st));
     BCHK(hipStreamSynchronize(st));
 
     // equal (hash, position) in two contigs: the reference's order of those entries is
     // what pdqsort_branchless's moves leave (index.cpp:168).  Replay that sort on the
     // host from generation order and put its result in place of the device sort's; keys
     // (and so the bucket table and the counts) are the same either way.
-    const uint64_t ties = hist[103];
     double ms_ties = 0;
     if (ties) {
         const auto tr = std::chrono::steady_clock::now();
         std::vector<rsa_ref_randstrobe> h(n);
         BCHK(hipMemcpy(h.data(), d_raw, sizeof(rsa_ref_randstrobe) * n, hipMemcpyDeviceToHost));
-        const int threads = (int)std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
+        dfree(d_raw);
+        d_raw = nullptr;
+        // the caller's thread budget (the machine's, at most 64, when it gives none)
+        const int threads = bp->threads > 0 ? bp->threads
+                                            : (int)std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
         rsa::sti_order::pdqsort_replay(h.data(), n, threads);
         BCHK(hipMemcpy(B->d_rs, h.data(), sizeof(rsa_ref_randstrobe) * n, hipMemcpyHostToDevice));
         ms_ties = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr).count();
     }
-    dfree(d_raw);
 
     // filter cutoff (index.cpp:214-238) from the clamped histogram: counts sorted
     // descending, the value at rank index_cutoff (or the smallest), clamped to [30, 100]

@@ -472,8 +472,10 @@ struct ExtStatus {            // device-side counters of one rsa_extend call
 };
 
 // byte offsets of the scan order and the status in the staged job upload of n jobs
+// one staged upload per call: [ExtJobDev x n | scan order x n | ExtJobDev x n in scan order | ExtStatus]
 static size_t stage_order_off(uint32_t n) { return sizeof(ExtJobDev) * (size_t)n; }
-static size_t stage_status_off(uint32_t n) { return (stage_order_off(n) + sizeof(int) * (size_t)n + 15) & ~(size_t)15; }
+static size_t stage_sorted_off(uint32_t n) { return (stage_order_off(n) + sizeof(int) * (size_t)n + 15) & ~(size_t)15; }
+static size_t stage_status_off(uint32_t n) { return stage_sorted_off(n) + sizeof(ExtJobDev) * (size_t)n; }
 static size_t stage_bytes(uint32_t n) { return stage_status_off(n) + sizeof(ExtStatus); }
 
 }  // extern "C"
@@ -606,6 +608,9 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
     }
     uint32_t cls_n[NCLS_MAX] = {0}, rest_n = 0;
     int* ord = reinterpret_cast<int*>(L->h_jobs.as<char>() + stage_order_off(n));
+    // the descriptors again in scan order: a scan wave reads its jobs' descriptors and
+    // result indices side by side (no dependent load through the order)
+    ExtJobDev* sj = reinterpret_cast<ExtJobDev*>(L->h_jobs.as<char>() + stage_sorted_off(n));
     if (grouped) {
         const uint32_t maxr = 1024;
         std::vector<uint32_t> cnt((size_t)ncls * (maxr + 1), 0);
@@ -638,12 +643,13 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
             }
         uint64_t rest_at = at;
         for (uint32_t i = 0; i < n; ++i) {
-            if (cls[i] < 0) ord[rest_at++] = (int)i;
-            else ord[cnt[(size_t)cls[i] * (maxr + 1) + (maxr - hj[i].rlen)]++] = (int)i;
+            const uint64_t k = cls[i] < 0 ? rest_at++ : cnt[(size_t)cls[i] * (maxr + 1) + (maxr - hj[i].rlen)]++;
+            ord[k] = (int)i;
+            sj[k] = hj[i];
         }
     } else {
         rest_n = n;
-        for (uint32_t i = 0; i < n; ++i) ord[i] = (int)i;
+        for (uint32_t i = 0; i < n; ++i) { ord[i] = (int)i; sj[i] = hj[i]; }
     }
     P.rmax = rmax;
     P.band16_dircap = band16_dircap(qmax);
@@ -654,11 +660,12 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
     L->kt.begin(st, RSA_K_EXT_SCAN);
     {
         const int* d_ord = reinterpret_cast<const int*>(L->d_jobs.as<char>() + stage_order_off(n));
+        const ExtJobDev* d_sj = reinterpret_cast<const ExtJobDev*>(L->d_jobs.as<char>() + stage_sorted_off(n));
         uint32_t off = 0;
         for (int c = 0; c < ncls; ++c) {
             if (!cls_n[c]) continue;
             if (use_v)
-                launch_ext_scan_v(cls_rows[c], cls_wcap[c], (int)cls_n[c], st, L->d_jobs.as<ExtJobDev>(), d_ord + off,
+                launch_ext_scan_v(cls_rows[c], cls_wcap[c], (int)cls_n[c], st, d_sj + off, d_ord + off,
                                   L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(), jb->match, jb->mismatch,
                                   jb->gap_open, jb->gap_extend, &dst->err);
             else

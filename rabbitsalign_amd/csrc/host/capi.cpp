@@ -142,11 +142,23 @@ static void setup_params(rsam* m) {
     m->mp.rescue_cutoff = m->mp.rescue_level < 100 ? m->mp.rescue_level * m->idx.filter_cutoff : 1000;
 }
 
+// Open mappers of the process.  When the last one closes, the pipeline's pooled
+// threads are joined and its pooled (page-locked) buffers freed while that
+// mapper's engine is still open: nothing of the library then runs or stays
+// allocated, so the process can unload it or exit without a destructor touching
+// a torn-down HIP runtime.
+static std::mutex g_open_m;
+static int g_open = 0;
+
 static rsam* open_common(rsam* m, int device, char* err, size_t err_len) {
     try {
         setup_params(m);
         auto t = std::chrono::steady_clock::now();
         m->eng = make_default_engine(m->refs, m->idx, device);
+        {
+            std::lock_guard<std::mutex> g(g_open_m);
+            ++g_open;
+        }
         m->upload_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
         return m;
     } catch (const std::exception& e) {
@@ -191,6 +203,12 @@ rsam* rsam_open_synthetic(uint64_t seed, uint64_t ref_len, int n_contigs, int re
     try {
         m->read_len = read_len;
         m->refs.seqs = synth::reference(seed, ref_len, n_contigs, std::max(1, threads));
+        if (const char* dup = getenv("RSA_SYNTH_DUP")) {
+            // a PAR-like duplicated region (measurement of the index build's tie path)
+            const uint64_t len = strtoull(dup, nullptr, 10), at = 1u << 20;
+            if (len && n_contigs > 1 && m->refs.seqs[0].size() >= at + len && m->refs.seqs[1].size() >= at + len)
+                m->refs.seqs[1].replace(at, len, m->refs.seqs[0], at, len);
+        }
         for (int c = 0; c < n_contigs; ++c) m->refs.names.push_back("chr" + std::to_string(c + 1));
         finish_refs(m->refs);
         auto t = std::chrono::steady_clock::now();
@@ -224,7 +242,16 @@ rsam* rsam_open_like(const rsam* o, int device, int threads, char* err, size_t e
     return open_common(m, device, err, err_len);
 }
 
-void rsam_close(rsam* m) { delete m; }
+void rsam_close(rsam* m) {
+    if (!m) return;
+    bool last = false;
+    {
+        std::lock_guard<std::mutex> g(g_open_m);
+        last = --g_open == 0;
+    }
+    if (last) release_pipeline_resources();
+    delete m;
+}
 
 int rsam_get_info(const rsam* m, rsam_info* out) {
     if (!m || !out) return -1;
@@ -243,6 +270,8 @@ int rsam_get_info(const rsam* m, rsam_info* out) {
     out->pad_ = 0;
     for (int i = 0; i < 6; ++i) out->index_device_ms[i] = m->idx.device_build_ms[i];
     out->index_replayed_segments = m->idx.replayed_segments;
+    out->index_position_ties = m->idx.position_ties;
+    out->index_ms_tie_replay = m->idx.ms_tie_replay;
     return 0;
 }
 

@@ -366,8 +366,8 @@ std::unique_ptr<Engine> make_gpu_engine(const References& refs, const StiIndex& 
 // parameters, a CPU engine opened on the same index)
 void build_default_index(StiIndex& idx, const References& refs, const IndexParameters& p, int bits_override, float f,
                          int threads, int device, bool host_copy) {
-    (void)threads;
     rsa_index_build_params bp{};
+    bp.threads = threads;
     bp.k = p.k; bp.s = p.s; bp.t_syncmer = p.t;
     bp.w_min = (int)p.w_min; bp.w_max = (int)p.w_max; bp.max_dist = p.max_dist;
     bp.q = (uint64_t)p.q;
@@ -403,6 +403,7 @@ void build_default_index(StiIndex& idx, const References& refs, const IndexParam
     std::copy(ms, ms + 6, idx.device_build_ms);
     idx.replayed_segments = info.replayed_segments;
     idx.position_ties = info.position_ties;
+    idx.ms_tie_replay = info.ms_tie_replay;
 }
 
 // engine of librsalign.so (capi.cpp)

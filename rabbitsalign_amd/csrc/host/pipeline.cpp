@@ -137,7 +137,14 @@ struct OrderedSink {
     static constexpr size_t kMaxQueued = 768u << 20;
     std::mutex m;
     std::condition_variable cv, room_cv;
-    std::map<size_t, std::pair<SamText, SamDigest>> pending;
+    // a chunk's text may come in pieces (PeChunk SAM pieces, pe_store_last): the
+    // writer takes the pieces of the next chunk in order as they come, so it can
+    // start on a chunk while the rest of it is still being formatted
+    struct Entry {
+        std::deque<std::pair<SamText, SamDigest>> pieces;
+        bool done = false;                    // its last piece is in
+    };
+    std::map<size_t, Entry> pending;
     std::deque<SamText> queue;                // in chunk order, for the writer
     size_t queued_bytes = 0;
     size_t next = 0;
@@ -179,6 +186,11 @@ struct OrderedSink {
         static Spares* p = new Spares();     // never destroyed: no exit-time teardown
         return *p;
     }
+    static void clear_spares() {
+        std::vector<SamText> v;
+        std::lock_guard<std::mutex> g(spares().m);
+        v.swap(spares().v);
+    }
     SamText take() {
         static const bool off = getenv("RSA_SAM_REUSE") && atoi(getenv("RSA_SAM_REUSE")) == 0;
         Spares& sp = spares();
@@ -196,22 +208,30 @@ struct OrderedSink {
         sp.v.push_back(std::move(s));
     }
     // `made`: the chunk's digest, folded in while its text was written (Sam::digest_into)
-    void put(size_t idx, SamText&& s, const SamDigest* made = nullptr) {
+    void put(size_t idx, SamText&& s, const SamDigest* made = nullptr) { put_piece(idx, std::move(s), made, true); }
+    // the next piece of chunk idx's text (`last`: the chunk is complete with it)
+    void put_piece(size_t idx, SamText&& s, const SamDigest* made, bool last) {
         SamDigest d;
         if (digest) d = made ? *made : SamDigest::of(s.data(), s.size());   // in the calling worker
         std::unique_lock<std::mutex> g(m);
-        pending.emplace(idx, std::make_pair(std::move(s), d));
+        Entry& e = pending[idx];
+        e.pieces.emplace_back(std::move(s), d);
+        e.done = last;
         bool moved = false;
         for (auto it = pending.find(next); it != pending.end(); it = pending.find(next)) {
-            bytes += it->second.first.size();
-            total.append(it->second.second);
-            if (sink) {
-                queued_bytes += it->second.first.size();
-                queue.push_back(std::move(it->second.first));
-                moved = true;
-            } else {
-                give_back(it->second.first);
+            for (auto& pc : it->second.pieces) {
+                bytes += pc.first.size();
+                total.append(pc.second);
+                if (sink) {
+                    queued_bytes += pc.first.size();
+                    queue.push_back(std::move(pc.first));
+                    moved = true;
+                } else {
+                    give_back(pc.first);
+                }
             }
+            it->second.pieces.clear();
+            if (!it->second.done) break;          // more of this chunk to come
             pending.erase(it);
             next++;
         }
@@ -240,6 +260,8 @@ struct OrderedSink {
         if (trace) fprintf(trace, "end %.4f\n", since(t_open));
     }
 };
+
+void release_sam_spares() { OrderedSink::clear_spares(); }
 
 struct PeChunk {
     InputChunk in;                            // the source's records; in.r1/in.r2[i].seq upper-cased by pe_load
@@ -273,6 +295,13 @@ struct ChunkPool {
         auto c = std::move(free.back());
         free.pop_back();
         return c;
+    }
+    void clear() {
+        std::vector<std::unique_ptr<PeChunk>> v;
+        {
+            std::lock_guard<std::mutex> g(m);
+            v.swap(free);
+        }
     }
     void put(std::unique_ptr<PeChunk> c) {
         if (!c) return;
@@ -310,6 +339,11 @@ struct ScratchLease {
         std::lock_guard<std::mutex> g(mu());
         if (pool().size() < 64) pool().push_back(std::move(s));
     }
+    static void clear() {
+        std::vector<std::unique_ptr<WorkerScratch>> v;
+        std::lock_guard<std::mutex> g(mu());
+        v.swap(pool());
+    }
 };
 
 // Worker threads outlive the mapping calls (each bench step is one call, and
@@ -340,13 +374,29 @@ public:
         static WorkerPool* p = new WorkerPool();     // never destroyed: no exit-time teardown
         return *p;
     }
+    // every pool thread ended and joined (no mapping call may be running); the next run()
+    // starts new ones
+    void shutdown() {
+        std::lock_guard<std::mutex> busy(run_m_);
+        std::vector<std::thread> ts;
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+            ts.swap(threads_);
+        }
+        cv_.notify_all();
+        for (auto& t : ts) t.join();
+        std::lock_guard<std::mutex> g(m_);
+        stop_ = false;
+    }
 
 private:
     void loop() {
-        uint64_t seen = 0;
+        uint64_t seen = 0;         // a thread made by run() takes part in that run's generation
         std::unique_lock<std::mutex> g(m_);
         for (;;) {
-            cv_.wait(g, [&] { return generation_ != seen && pending_ > 0; });
+            cv_.wait(g, [&] { return stop_ || (generation_ != seen && pending_ > 0); });
+            if (stop_) return;
             seen = generation_;
             pending_--;
             running_++;
@@ -364,6 +414,7 @@ private:
     const std::function<void()>* job_ = nullptr;
     int pending_ = 0, running_ = 0;
     uint64_t generation_ = 0;
+    bool stop_ = false;
 };
 
 ChunkPool& chunk_pool() {
@@ -626,10 +677,16 @@ void pe_get_str(PeChunk& c, const MapContext& mc, float mu, float sigma, std::ve
     c.times.collect += since(t);
 }
 
-// the chunk's extension results start at infos[pos]
+// pairs per piece of a chunk's SAM text handed to the writer (RSA_SAM_PIECE; 0 = the
+// whole chunk at once): the writer starts on a chunk while its last() runs on
+static size_t sam_piece_pairs() {
+    static const size_t n = getenv("RSA_SAM_PIECE") ? (size_t)atol(getenv("RSA_SAM_PIECE")) : 2000;
+    return n;
+}
+
+// the chunk's extension results start at infos[pos]; its SAM text goes to `os` in pieces
 void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistribution& isize,
-                   std::vector<AlignmentInfo>& infos, size_t pos, const std::string& rg_id, SamText& out,
-                   SamDigest* digest) {
+                   std::vector<AlignmentInfo>& infos, size_t pos, const std::string& rg_id, OrderedSink& os) {
     const auto t = Clock::now();
     const size_t n = c.size();
     const bool pf = prefetch_on();
@@ -640,31 +697,42 @@ void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistributio
         const Read read1(c.in.r1[i].seq, c.rc(i, 0)), read2(c.in.r2[i].seq, c.rc(i, 1));
         pos = store_results_pe(c.res[i], read1, read2, mc, isize.mu, isize.sigma, infos, pos);
     }
-    out.clear();
-    out.reserve(7 * (size_t)mc.mparams.r * n);
-    Sam sam(out, mc.refs, mc.mparams.cigar_eqx, rg_id, mc.mparams.output_unmapped, mc.mparams.details);
-    sam.digest_into(digest);
-    for (size_t i = 0; i < n; ++i) {
-        if (pf && i + 2 * ahead < n) {
-            prefetch_obj(c.res[i + 2 * ahead]);
-            prefetch_obj(c.in.r1[i + 2 * ahead]);
-            prefetch_obj(c.in.r2[i + 2 * ahead]);
+    const size_t piece = sam_piece_pairs() ? sam_piece_pairs() : std::max<size_t>(n, 1);
+    double t_out = 0;
+    for (size_t a = 0; a < n || a == 0; a += piece) {
+        const size_t b = std::min(n, a + piece);
+        SamText out = os.take();
+        out.reserve(7 * (size_t)mc.mparams.r * (b - a));
+        Sam sam(out, mc.refs, mc.mparams.cigar_eqx, rg_id, mc.mparams.output_unmapped, mc.mparams.details);
+        SamDigest dg;
+        if (os.digest) sam.digest_into(&dg);
+        for (size_t i = a; i < b; ++i) {
+            if (pf && i + 2 * ahead < n) {
+                prefetch_obj(c.res[i + 2 * ahead]);
+                prefetch_obj(c.in.r1[i + 2 * ahead]);
+                prefetch_obj(c.in.r2[i + 2 * ahead]);
+            }
+            if (pf && i + ahead < n) {
+                prefetch_record(c.in.r1[i + ahead]);
+                prefetch_record(c.in.r2[i + ahead]);
+                prefetch_res(c.res[i + ahead]);
+                // SEQ comes from the chunk's upper-cased copy or its reverse complement,
+                // both written at load time and long out of cache
+                prefetch_str(c.in.r1[i + ahead].seq);
+                prefetch_str(c.in.r2[i + ahead].seq);
+                prefetch_str(c.rc(i + ahead, 0));
+                prefetch_str(c.rc(i + ahead, 1));
+            }
+            const Read read1(c.in.r1[i].seq, c.rc(i, 0)), read2(c.in.r2[i].seq, c.rc(i, 1));
+            align_PE_read_last(c.res[i], c.in.r1[i], c.in.r2[i], read1, read2, sam, c.stats, isize, mc, c.rng);
         }
-        if (pf && i + ahead < n) {
-            prefetch_record(c.in.r1[i + ahead]);
-            prefetch_record(c.in.r2[i + ahead]);
-            prefetch_res(c.res[i + ahead]);
-            // SEQ comes from the chunk's upper-cased copy or its reverse complement,
-            // both written at load time and long out of cache
-            prefetch_str(c.in.r1[i + ahead].seq);
-            prefetch_str(c.in.r2[i + ahead].seq);
-            prefetch_str(c.rc(i + ahead, 0));
-            prefetch_str(c.rc(i + ahead, 1));
-        }
-        const Read read1(c.in.r1[i].seq, c.rc(i, 0)), read2(c.in.r2[i].seq, c.rc(i, 1));
-        align_PE_read_last(c.res[i], c.in.r1[i], c.in.r2[i], read1, read2, sam, c.stats, isize, mc, c.rng);
+        const auto tp = Clock::now();
+        os.put_piece(c.in.index, std::move(out), os.digest ? &dg : nullptr, b >= n);
+        t_out += since(tp);
+        if (n == 0) break;
     }
-    c.times.last += since(t);
+    c.times.output += t_out;
+    c.times.last += since(t) - t_out;
 }
 
 }  // namespace
@@ -841,12 +909,7 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
         }
         c.stats.tot_aligner_calls -= no_shared_count(infos);   // the reference aligns none of those
         c.times.extend += since(te);
-        SamText out = os.take();
-        SamDigest dg;
-        pe_store_last(c, mc, est, infos, 0, opt.rg_id, out, os.digest ? &dg : nullptr);
-        const auto tp = Clock::now();
-        os.put(c.in.index, std::move(out), os.digest ? &dg : nullptr);
-        c.times.output += since(tp);
+        pe_store_last(c, mc, est, infos, 0, opt.rg_id, os);
     };
 
     auto worker = [&](bool leader) {
@@ -906,10 +969,7 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
                     }
                     pre->times.extend += since(te);
                     pre->stats.tot_aligner_calls += jobs.size() - no_shared_count(infos);
-                    SamText out = os.take();
-                    SamDigest dg;
-                    pe_store_last(*pre, mc, isize, infos, 0, opt.rg_id, out, os.digest ? &dg : nullptr);
-                    os.put(pre->in.index, std::move(out), os.digest ? &dg : nullptr);
+                    pe_store_last(*pre, mc, isize, infos, 0, opt.rg_id, os);
                     local.add(pre->stats);
                     lt.add(pre->times);
                     recycle(std::move(pre));
@@ -1049,7 +1109,26 @@ struct SeScratchPool {
         std::lock_guard<std::mutex> g(m);
         if (v.size() < 64) v.push_back(std::move(x));
     }
+    void clear() {
+        std::vector<std::unique_ptr<SeScratch>> d;
+        std::lock_guard<std::mutex> g(m);
+        d.swap(v);
+    }
 };
+
+// Every thread and pooled buffer the pipeline keeps between mapping calls: the
+// worker pool's threads end (joined), and the recycled chunks, scratch and SAM
+// buffers -- page-locked ones included, which go back through the engine's
+// allocator -- are freed.  The caller guarantees no mapping call is running and
+// that the engine whose allocator made them is still open (rsam_close: before the
+// last engine goes).
+void release_pipeline_resources() {
+    WorkerPool::get().shutdown();
+    chunk_pool().clear();
+    ScratchLease::clear();
+    SeScratchPool::get().clear();
+    release_sam_spares();
+}
 
 // Single-end: perform_task_async_se (pc.cpp:814-1096).  No insert-size state;
 // records are NOT upper-cased on this path; chunks are independent from the start.

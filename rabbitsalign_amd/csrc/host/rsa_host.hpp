@@ -321,6 +321,7 @@ struct StiIndex {                               // .sti contents (src/index.cpp:
     // entries equal in (hash, position) to their predecessor: their order is pdqsort's
     // (sti_order.hpp), replayed by both builds when this is not 0
     uint64_t position_ties = 0;
+    double ms_tie_replay = 0;                   // GPU build: host replay of the tie order, incl. transfers
     // a GPU build kept in HBM (no host copy): the GPU engine adopts it; a host
     // copy is downloaded only when something needs one (.sti write, a CPU engine)
     struct DeviceBuild {
@@ -769,6 +770,9 @@ bool same_name(std::string_view n1, std::string_view n2);
 // defaults that cost 0.93-1.00 core-us a read on the box, with these 0.77-0.87
 // (A/B, profiles/r02/ab_malloc.jsonl).  Only memory retention changes.
 void tune_malloc();
+// ends the pipeline's pooled worker threads and frees its pooled buffers (no mapping
+// call may run; the engine that allocated page-locked buffers must still be open)
+void release_pipeline_resources();
 
 // thread-summed seconds per phase (instrumentation of the host pipeline)
 struct PhaseTimes {

@@ -36,7 +36,8 @@ class _Info(C.Structure):
                 ("canonical_read_length", C.c_int32), ("index_seconds", C.c_double),
                 ("upload_seconds", C.c_double), ("device_resident_bytes", C.c_uint64),
                 ("index_on_device", C.c_int32), ("pad_", C.c_int32), ("index_device_ms", C.c_double * 6),
-                ("index_replayed_segments", C.c_uint64)]
+                ("index_replayed_segments", C.c_uint64), ("index_position_ties", C.c_uint64),
+                ("index_ms_tie_replay", C.c_double)]
 
 
 class Part(C.Structure):
@@ -103,6 +104,15 @@ def load(path: str = PRODUCT_LIB) -> C.CDLL:
     lib.rsam_map_files_part.argtypes = [vp, cp, cp, C.POINTER(Part), i32, cp, C.POINTER(_Stats)]
     _LIBS[path] = lib
     return lib
+
+
+def unload(path: str = PRODUCT_LIB) -> None:
+    """dlclose a library load() opened (every mapper of it closed first: rsam_close of the
+    last one joins the pipeline's threads and frees its pooled buffers)."""
+    lib = _LIBS.pop(path, None)
+    if lib is not None:
+        import _ctypes
+        _ctypes.dlclose(lib._handle)
 
 
 def part_count(path, rank: int, world: int, threads: int = 8, lib_path: str = PRODUCT_LIB) -> list:

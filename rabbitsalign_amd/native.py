@@ -271,7 +271,7 @@ def load_index(fasta: str, sti: str) -> Index:
 class IndexBuildParams(C.Structure):
     _fields_ = [("k", C.c_int32), ("s", C.c_int32), ("t_syncmer", C.c_int32), ("w_min", C.c_int32),
                 ("w_max", C.c_int32), ("max_dist", C.c_int32), ("q", C.c_uint64), ("bits", C.c_int32),
-                ("f", C.c_float)]
+                ("f", C.c_float), ("threads", C.c_int32)]
 
 
 class IndexBuildInfo(C.Structure):
@@ -283,13 +283,13 @@ class IndexBuildInfo(C.Structure):
 
 
 def build_index(ref: np.ndarray, contig_offsets: np.ndarray, k=20, s=16, w_min=2, w_max=12, max_dist=80, q=255,
-                bits=-1, f=0.0002, device=0):
+                bits=-1, f=0.0002, device=0, threads=0):
     """StrobemerIndex::populate on the GPU (rsa_index_build_run): returns
     (randstrobes [RS_DTYPE], bucket_starts [u64], filter_cutoff, info dict)."""
     lib = load()
     ref = np.ascontiguousarray(ref, dtype=np.uint8)
     offs = np.ascontiguousarray(contig_offsets, dtype=np.uint64)
-    p = IndexBuildParams(k, s, (k - s) // 2 + 1, w_min, w_max, max_dist, q, bits, f)
+    p = IndexBuildParams(k, s, (k - s) // 2 + 1, w_min, w_max, max_dist, q, bits, f, threads)
     info = IndexBuildInfo()
     err = C.create_string_buffer(512)
     h = lib.rsa_index_build_run(device, _ptr(ref), _ptr(offs), len(offs) - 1, C.byref(p), C.byref(info), err, 512)

@@ -4,7 +4,7 @@ processes, each writing the SAM of its own chunks.
 - library: two ranks (spawned processes, both on GPU 0, a gloo group for the plan's
   count exchange) plan with rabbitsalign_amd.shard.plan_shared_input and map with
   rsam_map_files_part; header + part 0 + part 1 == one process's SAM, byte for byte,
-  and the summed statistics are the one process's;
+  and the summed statistics are the one process's -- for plain and for gzip input;
 - CLI: `rsalign --rank R --world 3` (each rank plans alone) -- the parts minus @PG
   concatenate to the one-process SAM, on a repetitive reference whose insert-size
   estimate stays open across chunks.
@@ -46,7 +46,8 @@ def _rank(rank, world, port, fq1, fq2, out_dir, q):
 
 
 @pytest.mark.gpu
-def test_two_ranks_on_gpu0_equal_one_process(tmp_path):
+@pytest.mark.parametrize("gz", [False, True], ids=["plain", "gzip"])
+def test_two_ranks_on_gpu0_equal_one_process(tmp_path, gz):
     import torch.multiprocessing as mp
     from rabbitsalign_amd import mapper, shard
     m = mapper.Mapper.synthetic(CFG["seed"], CFG["ref_len"], CFG["contigs"], CFG["L"], device=0, threads=4)
@@ -58,6 +59,13 @@ def test_two_ranks_on_gpu0_equal_one_process(tmp_path):
     one = tmp_path / "one.sam"
     st1 = m.map_files(fq1, fq2, threads=4, chunk_size=CFG["chunk"], sam_path=str(one))
     m.close()
+    if gz:                          # the ranks map .fq.gz (parts planned by records)
+        import gzip
+        import shutil
+        for f in (fq1, fq2):
+            with open(f, "rb") as a, gzip.open(f + ".gz", "wb", compresslevel=1) as b:
+                shutil.copyfileobj(a, b)
+        fq1, fq2 = fq1 + ".gz", fq2 + ".gz"
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
