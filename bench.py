@@ -509,6 +509,85 @@ def multi_device_leg(args) -> int:
     return 0
 
 
+class _NoTorch:
+    """the few torch calls of a 1-GPU run, without torch (RSA_BENCH_NO_TORCH=1)"""
+    class cuda:
+        @staticmethod
+        def is_available():
+            return True          # the mapper's open fails loudly without a GPU
+
+        @staticmethod
+        def set_device(d):
+            pass                 # the device goes to the mapper explicitly
+
+        @staticmethod
+        def synchronize():
+            pass                 # mapping calls return after their device work
+
+    @staticmethod
+    def device(*a):
+        return None
+
+
+def ab_run(args, m, map_step, sam_paths, n_sets, threads) -> int:
+    """--ab: alternate environment settings of the host pipeline over the same read sets
+    (streamed FASTQ -> SAM file, as the headline), --ab-steps steps per setting per round;
+    per setting: every step's Mreads/s, the first chunk's extension bounds and the time the
+    first SAM text reached the writer.  Settings are read per mapping call."""
+    settings = [dict(kv.split("=", 1) for kv in grp.split(",") if kv) for grp in args.ab.split("|")]
+    res = {i: {"env": st, "mreads_s": [], "first_ext_ms": [], "first_out_ms": [], "core_us_per_read": [],
+               "kern": {}}
+           for i, st in enumerate(settings)}
+    kern_names = ("ext_scan", "ext_band", "lookup", "find_nams", "sites")
+    base = {k: os.environ.get(k) for st in settings for k in st}
+    s = args.warmup
+    for r in range(args.ab_rounds):
+        for i, st in enumerate(settings):
+            for k, v in base.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+            os.environ.update(st)
+            m.reset_kernel_stats()
+            for _ in range(args.ab_steps):
+                idx = args.warmup + (s % max(1, args.steps))
+                ru0 = resource.getrusage(resource.RUSAGE_SELF)
+                x = map_step(idx)
+                ru1 = resource.getrusage(resource.RUSAGE_SELF)
+                cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+                res[i]["mreads_s"].append(round(x.n_reads / x.map_seconds / 1e6, 3))
+                res[i]["first_ext_ms"].append([round(1e3 * x.t_first_ext_begin, 1), round(1e3 * x.t_first_ext_end, 1)])
+                res[i]["first_out_ms"].append(round(1e3 * x.t_first_out, 1))
+                res[i]["core_us_per_read"].append(round(1e6 * cpu / max(1, x.n_reads), 3))
+                if os.path.exists(sam_paths[idx]):
+                    os.remove(sam_paths[idx])
+                s += 1
+            ks = m.kernel_stats()
+            for kn in kern_names:
+                k = ks["kernels"].get(kn)
+                if k:
+                    acc = res[i]["kern"].setdefault(kn, {"ms": 0.0, "launches": 0})
+                    acc["ms"] += k["ms"]
+                    acc["launches"] += k["launches"]
+            res[i]["kern"].setdefault("dp_cells", 0)
+            res[i]["kern"]["dp_cells"] += ks.get("dp_cells_timed", 0)
+    for v in res.values():
+        kk = v["kern"]
+        for kn in kern_names:
+            if kn in kk:
+                kk[kn]["us_per_launch"] = round(1e3 * kk[kn]["ms"] / max(1, kk[kn]["launches"]), 1)
+        if "ext_scan" in kk and kk["ext_scan"]["ms"] > 0:
+            kk["scan_gcells_s"] = round(kk["dp_cells"] / (kk["ext_scan"]["ms"] * 1e-3) / 1e9, 1)
+        xs = sorted(v["mreads_s"])
+        v["median"] = xs[len(xs) // 2]
+        v["mean"] = round(sum(xs) / len(xs), 3)
+    print(json.dumps({"ab": list(res.values()), "steps_each": args.ab_steps, "rounds": args.ab_rounds,
+                      "threads": threads}), flush=True)
+    m.close()
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -536,6 +615,12 @@ def main():
                     help="N>1: skip the product's one-process multi-device leg (one SAM file over N GPUs)")
     ap.add_argument("--md-steps", type=int, default=3, help="timed steps of the multi-device leg")
     ap.add_argument("--multi-device-leg", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--ab", default="",
+                    help="measurement mode (1 GPU): 'K=V,K2=V2|K=V3' -- environment settings of the host pipeline "
+                         "run alternately after the warm-up, --ab-steps steps each, --ab-rounds times; prints one "
+                         "{\"ab\": ...} line instead of the headline")
+    ap.add_argument("--ab-rounds", type=int, default=3)
+    ap.add_argument("--ab-steps", type=int, default=4)
     args = ap.parse_args()
 
     if os.environ.get("RSA_MAPS_OUT"):
@@ -571,8 +656,17 @@ def main():
     # torch first: its libamdhip64 (soname libamdhip64.so.7) is then the one
     # runtime of the process and librsa_gpu.so binds to it; loading ours first
     # would put two HIP runtimes in one process (torch needs "libamdhip64.so").
-    import torch
-    import torch.distributed as dist
+    # RSA_BENCH_NO_TORCH=1 (N=1, profiling runs): no torch at all, so the process has
+    # the system ROCm's runtime only -- the one rocprofv3's tool library uses.  With
+    # torch's bundled HSA runtime beside it, the tool's exit-time finalisation under
+    # --memory-copy-trace touches GPU mappings the other runtime's teardown removed
+    # (profiles/r06/exit_abort.txt).  A mapping call returns after its
+    # device work, so torch.cuda.synchronize has nothing to wait for at N=1.
+    if os.environ.get("RSA_BENCH_NO_TORCH") == "1" and world == 1:
+        torch, dist = _NoTorch(), None
+    else:
+        import torch
+        import torch.distributed as dist
     from rabbitsalign_amd import mapper as M
     from rabbitsalign_amd import shard
     M.load()
@@ -677,6 +771,8 @@ def main():
         drop_sams(args.warmup, keep=set(set_file.values()))
         m.reset_kernel_stats()
         m.set_sam_digest(False)
+        if args.ab and world == 1:
+            return ab_run(args, m, map_step, sam_paths, n_sets, threads)
 
         barrier()
         torch.cuda.synchronize()
@@ -697,7 +793,10 @@ def main():
                       f"seed {st.t_seed:.2f} extend {st.t_extend:.2f} part {st.t_part:.2f} "
                       f"collect {st.t_collect:.2f} last {st.t_last:.2f}; sequential phase {st.t_sequential:.3f} s "
                       f"(chunk 0 seeded at {st.t_first_seeded:.3f} s), last chunk: finish {st.t_last_start:.3f} s, "
-                      f"SAM out {st.t_last_put:.3f} s; workers done {st.t_workers_done:.3f} s")
+                      f"SAM out {st.t_last_put:.3f} s; workers done {st.t_workers_done:.3f} s; first chunk "
+                      f"extension {st.t_first_ext_begin * 1e3:.1f}-{st.t_first_ext_end * 1e3:.1f} ms, first SAM "
+                      f"text to the writer {st.t_first_out * 1e3:.1f} ms"
+                      + (f", replayed chunks {st.replayed_chunks}" if st.replayed_chunks else ""))
         torch.cuda.synchronize()
         barrier()
         elapsed = time.perf_counter() - t0

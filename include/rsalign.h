@@ -33,6 +33,10 @@ typedef struct rsam_stats {
     /* s from the call: chunk 0 seeded; the last chunk's extension + store began; the last
      * chunk's SAM text went to the sink; all workers done (map_seconds: the sink closed) */
     double t_first_seeded, t_last_start, t_last_put, t_workers_done;
+    /* s from the call: the first SAM text reached the writer; the first chunk's extension
+     * call began and returned; chunks parted only for the insert-size estimate (rank mode) */
+    double t_first_out, t_first_ext_begin, t_first_ext_end;
+    uint64_t replayed_chunks;
 } rsam_stats;
 
 /* Open from files: FASTA + optional .sti (NULL: build the index in memory). */

@@ -836,7 +836,10 @@ k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
              const int* __restrict__ idx, const char* __restrict__ qbuf, const char* __restrict__ ref,
              uint32_t* __restrict__ cig_pool, uint32_t* __restrict__ raw_pool, rsa_aln* __restrict__ out, int match,
              int mismatch, int gO, int gE, int bonus, int* __restrict__ queue, int* __restrict__ qcount,
-             int* __restrict__ overflow, int* __restrict__ redo, int* __restrict__ redo_count) {
+             int* __restrict__ overflow, int* __restrict__ redo, int* __restrict__ redo_count, int prio) {
+    // the extension finishes chunks the SAM writer waits for: its waves may claim the
+    // SIMDs they share with the seeding kernels first (s_setprio, RSA_EXT_SETPRIO)
+    if (prio) __builtin_amdgcn_s_setprio(2);
     __shared__ __attribute__((aligned(16))) int8_t s_dir[B16_GROUPS][DirCells<DIRCAP>::BYTES];
     __shared__ uint8_t s_qc[B16_GROUPS][B16_SEGCAP];
     __shared__ uint8_t s_rc[B16_GROUPS][B16_SEGCAP];
@@ -1254,10 +1257,10 @@ void launch_ext_scan(int rmax, dim3 grid, dim3 block, hipStream_t st, const ExtJ
 void launch_ext_band16(int dircap, dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n,
                        const int* idx, const char* q, const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out,
                        int match, int mismatch, int gO, int gE, int bonus, int* queue, int* qcount, int* overflow,
-                       int* redo, int* redo_count) {
+                       int* redo, int* redo_count, int prio) {
 #define RSA_B16(DC)                                                                                                \
     hipLaunchKernelGGL(k_ext_band16<DC>, grid, dim3(64), 0, st, jobs, scan, n, idx, q, ref, cig, raw, out, match, \
-                       mismatch, gO, gE, bonus, queue, qcount, overflow, redo, redo_count)
+                       mismatch, gO, gE, bonus, queue, qcount, overflow, redo, redo_count, prio)
     if (dircap >= 12288) RSA_B16(12288);
     else if (dircap >= 8192) RSA_B16(8192);
     else RSA_B16(4096);

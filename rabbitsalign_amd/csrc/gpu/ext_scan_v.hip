@@ -398,7 +398,10 @@ template <int RV, int WCAP>
 __global__ void __launch_bounds__(64 * VS_WAVES, VsMinW<RV>::value)
 k_ext_scan_v(const ExtJobDev* __restrict__ sjobs, const int* __restrict__ order, int n,
              const char* __restrict__ qbuf, const char* __restrict__ ref, ScanRes* __restrict__ out,
-             int match, int mismatch, int gO, int gE, int* __restrict__ err) {
+             int match, int mismatch, int gO, int gE, int* __restrict__ err, int prio) {
+    // the extension finishes chunks the SAM writer waits for: its waves may claim the
+    // SIMDs they share with the seeding kernels first (s_setprio, RSA_EXT_SETPRIO)
+    if (prio) __builtin_amdgcn_s_setprio(2);
     // a slot: VS_PAD bytes of padding, the window from the dword-aligned base (its first
     // byte at base + (r_off & 3)), WCAP + VS_PAD bytes after the base in all
     constexpr int SLOT = WCAP + 2 * VS_PAD + 4;
@@ -559,13 +562,13 @@ int scan_v_wcap(uint32_t rlen) {
 
 // sjobs: the class's descriptors in scan order; order: their indices (results go to out[order[k]])
 void launch_ext_scan_v(int rv, int wcap, int n, hipStream_t st, const ExtJobDev* sjobs, const int* order, const char* q,
-                       const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE, int* err) {
+                       const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE, int* err, int prio) {
     if (n <= 0) return;
     const dim3 grid((n + VS_JOBS - 1) / VS_JOBS), block(64 * VS_WAVES);
 #define RSA_V(RR, WW)                                                                                             \
     if (rv == RR && wcap == WW) {                                                                                 \
         hipLaunchKernelGGL((k_ext_scan_v<RR, WW>), grid, block, 0, st, sjobs, order, n, q, ref, out, match,       \
-                           mismatch, gO, gE, err);                                                                \
+                           mismatch, gO, gE, err, prio);                                                          \
         return;                                                                                                   \
     }
     RSA_V(2, 512) RSA_V(3, 512) RSA_V(4, 512) RSA_V(5, 512) RSA_V(6, 512) RSA_V(7, 512) RSA_V(8, 512)

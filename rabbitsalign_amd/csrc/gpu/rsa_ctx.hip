@@ -37,7 +37,7 @@ __global__ void k_ext_band_panel(const ExtJobDev* jobs, const ScanRes* scan, int
 void launch_ext_band16(int dircap, dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n, const int* idx,
                        const char* q, const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match,
                        int mismatch, int gO, int gE, int bonus, int* queue, int* qcount, int* overflow, int* redo,
-                       int* redo_count);
+                       int* redo_count, int prio);
 void launch_shared_check(int nl, hipStream_t st, const ExtJobDev* jobs, const uint32_t* list, const char* q,
                          const char* ref, uint8_t* res);
 void launch_ext_band64(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, const char* q,
@@ -47,7 +47,7 @@ void launch_ext_band64(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const S
 int scan_v_rows(uint32_t qlen);
 int scan_v_wcap(uint32_t rlen);
 void launch_ext_scan_v(int rv, int wcap, int n, hipStream_t st, const ExtJobDev* jobs, const int* order, const char* q,
-                       const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE, int* err);
+                       const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE, int* err, int prio);
 void launch_cigar_compact(hipStream_t st, const rsa_aln* alns, rsa_aln* alns_out, int n_jobs, const uint32_t* slots,
                           uint32_t* dense, uint64_t* bsum, uint64_t* total);
 
@@ -179,6 +179,13 @@ enum { LANE_SEED = 0, LANE_EXT = 1 };
 // calls mostly run chunks ahead of it, so the command processor dispatches the
 // extension kernels' workgroups first when both wait for compute units
 // (RSA_EXT_PRIORITY=0: one pool at normal priority for both kinds).
+// the extension kernels' waves raise their issue priority on the SIMDs they share with
+// the seeding kernels (RSA_EXT_SETPRIO, read per call; default on)
+static int ext_setprio() {
+    const char* e = getenv("RSA_EXT_SETPRIO");
+    return e && e[0] == '0' ? 0 : 1;
+}
+
 static bool ext_priority() {
     static const bool on = !(getenv("RSA_EXT_PRIORITY") && getenv("RSA_EXT_PRIORITY")[0] == '0');
     return on;
@@ -667,7 +674,7 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
             if (use_v)
                 launch_ext_scan_v(cls_rows[c], cls_wcap[c], (int)cls_n[c], st, d_sj + off, d_ord + off,
                                   L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(), jb->match, jb->mismatch,
-                                  jb->gap_open, jb->gap_extend, &dst->err);
+                                  jb->gap_open, jb->gap_extend, &dst->err, ext_setprio());
             else
                 launch_ext_scan_g(cls_rows[c], (int)cls_n[c], st, L->d_jobs.as<ExtJobDev>(), d_ord + off,
                                   L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(), jb->match, jb->mismatch,
@@ -691,7 +698,8 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
     launch_ext_band16(P.band16_dircap, dim3((n + 3) / 4), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(), (int)n, nullptr,
                       L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(),
                       L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open, jb->gap_extend, jb->end_bonus,
-                      L->d_queue.as<int>(), &dst->qcount, L->d_over.as<int>(), L->d_redo.as<int>(), &dst->rcount);
+                      L->d_queue.as<int>(), &dst->qcount, L->d_over.as<int>(), L->d_redo.as<int>(), &dst->rcount,
+                      ext_setprio());
     HIPCHK(hipGetLastError());
     L->kt.end(st);
     L->kt.begin(st, RSA_K_EXT_BAND_WIDE);
@@ -798,7 +806,8 @@ static int ext_finish(rsa_pending& P) {
         launch_ext_band16(P.band16_dircap, dim3((redo + 3) / 4), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(), redo, d_redo,
                           L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(),
                           L->d_alns.as<rsa_aln>(), P.match, P.mismatch, P.gap_open, P.gap_extend, P.end_bonus,
-                          L->d_queue.as<int>(), &P.d_status->qcount, L->d_over.as<int>(), nullptr, nullptr);
+                          L->d_queue.as<int>(), &P.d_status->qcount, L->d_over.as<int>(), nullptr, nullptr,
+                          ext_setprio());
         HIPCHK(hipGetLastError());
         L->kt.end(st);
         L->kt.begin(st, RSA_K_EXT_BAND_WIDE);

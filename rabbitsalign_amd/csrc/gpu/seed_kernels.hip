@@ -2261,55 +2261,64 @@ struct SiteRead {
     __device__ __forceinline__ unsigned char at(bool rc, int64_t i) const { return (unsigned char)side(rc)[i]; }
 };
 
-// 16 lanes per NAM, 4 NAMs per wave: a lane compares every 16th byte and the
-// group combines its ballot bits (in position order, so mismatch positions come
-// out sorted without a sort)
+// G lanes per NAM (8 by default: 8 NAMs per wave; RSA_SITES_G=16 selects 16 lanes, 4
+// NAMs a wave): a lane compares every G-th byte of a k-mer and 256 / G consecutive
+// window positions of every 256-position chunk, and the group combines its ballot bits
+// (in position order, so mismatch positions come out sorted without a sort)
+template <int G>
 __device__ __forceinline__ uint32_t grp_ballot(bool v) {
     const uint64_t b = __ballot(v);
-    return (uint32_t)(b >> (threadIdx.x & 48)) & 0xFFFFu;
+    return (uint32_t)(b >> (threadIdx.x & (64 - G))) & ((1u << G) - 1u);
 }
 
 // site_kmer_eq for k <= 32, in two steps so that every load of a NAM's checks is in
-// flight at once: KmerLoad holds the clamped spans and the lane's two byte pairs
-// (positions l16 and l16 + 16; a position past the span reads its first byte, valid
-// memory, and is not compared)
-struct KmerLoad { uint32_t rl, ql; unsigned char r0, q0, r1, q1; };
-__device__ __forceinline__ KmerLoad kmer_load(const char* ref, int64_t rlen, int64_t rpos, const SiteRead& rd, bool rc,
-                                              int64_t qpos, int k, int l16) {
+// flight at once: KmerLoad holds the clamped spans and the lane's 32 / G byte pairs
+// (positions lg + G t; a position past the span reads its first byte, valid memory, and
+// is not compared)
+template <int G> struct KmerLoad { uint32_t rl, ql; unsigned char r[32 / G], q[32 / G]; };
+template <int G>
+__device__ __forceinline__ KmerLoad<G> kmer_load(const char* ref, int64_t rlen, int64_t rpos, const SiteRead& rd,
+                                                 bool rc, int64_t qpos, int k, int lg) {
     const uint64_t rp = (uint64_t)rpos, qp = (uint64_t)qpos;
     const uint64_t ra = rp > (uint64_t)rlen ? (uint64_t)rlen : rp, qa = qp > (uint64_t)rd.len ? (uint64_t)rd.len : qp;
-    KmerLoad x;
+    KmerLoad<G> x;
     x.rl = (uint32_t)min((uint64_t)k, (uint64_t)rlen - ra);
     x.ql = (uint32_t)min((uint64_t)k, (uint64_t)rd.len - qa);
-    const uint32_t j0 = (uint32_t)l16 < x.rl ? (uint32_t)l16 : 0u, j1 = (uint32_t)l16 + 16u < x.rl ? (uint32_t)l16 + 16u : 0u;
     GU8* rb = (GU8*)(ref + ra);
     GU8* qb = (GU8*)(rd.side(rc) + qa);
-    x.r0 = rb[j0]; x.q0 = qb[j0]; x.r1 = rb[j1]; x.q1 = qb[j1];
+#pragma unroll
+    for (int t = 0; t < 32 / G; ++t) {
+        const uint32_t j = (uint32_t)(lg + G * t) < x.rl ? (uint32_t)(lg + G * t) : 0u;
+        x.r[t] = rb[j];
+        x.q[t] = qb[j];
+    }
     return x;
 }
-__device__ __forceinline__ bool kmer_test(const KmerLoad& x, int l16) {
+template <int G>
+__device__ __forceinline__ bool kmer_test(const KmerLoad<G>& x, int lg) {
     bool bad = x.rl != x.ql;
-    if ((uint32_t)l16 < x.rl) bad |= x.r0 != x.q0;
-    if ((uint32_t)l16 + 16u < x.rl) bad |= x.r1 != x.q1;
-    return grp_ballot(bad) == 0;
+#pragma unroll
+    for (int t = 0; t < 32 / G; ++t)
+        if ((uint32_t)(lg + G * t) < x.rl) bad |= x.r[t] != x.q[t];
+    return grp_ballot<G>(bad) == 0;
 }
 
 // sub(ref, rpos, k) == sub(read view, qpos, k) with std::string::substr clamping
 // (a position past the end -- negative ints included, as size_t -- gives "")
+template <int G>
 __device__ bool site_kmer_eq(const char* ref, int64_t rlen, int64_t rpos, const SiteRead& rd, bool rc, int64_t qpos,
-                             int k, int l16) {
+                             int k, int lg) {
     const uint64_t rp = (uint64_t)rpos, qp = (uint64_t)qpos;
     const uint64_t ra = rp > (uint64_t)rlen ? (uint64_t)rlen : rp, qa = qp > (uint64_t)rd.len ? (uint64_t)rd.len : qp;
     const uint64_t rl = min((uint64_t)k, (uint64_t)rlen - ra), ql = min((uint64_t)k, (uint64_t)rd.len - qa);
     bool bad = rl != ql;
     if (!bad)                                  // every byte's load issued before any compare
-        for (uint64_t j = l16; j < rl; j += 16) bad |= (unsigned char)ref[ra + j] != rd.at(rc, (int64_t)(qa + j));
-    return grp_ballot(bad) == 0;
+        for (uint64_t j = lg; j < rl; j += G) bad |= (unsigned char)ref[ra + j] != rd.at(rc, (int64_t)(qa + j));
+    return grp_ballot<G>(bad) == 0;
 }
 
-// Mismatch mask of one lane's 16 window positions x0 .. x0 + 15 (bit b: x0 + b < n and the
-// reference byte differs from the oriented read byte).  The group's 16 lanes cover 256
-// positions, so a read of <= 256 bp takes one round of loads.  Each side is two aligned
+// Mismatch mask of 16 window positions x0 .. x0 + 15 (bit b: x0 + b < n and the
+// reference byte differs from the oriented read byte).  Each side is two aligned
 // 16-byte loads and a byte funnel: the window lies inside its contig and the reference
 // buffer has 64 bytes of padding past the last one; the read buffer has SEQ_PAD bytes
 // of padding before the first read and after the last.
@@ -2328,8 +2337,8 @@ __device__ __forceinline__ void load16(const char* p, uint32_t out[4]) {   // by
     out[2] = __builtin_amdgcn_alignbyte(u3, u2, sh);
     out[3] = __builtin_amdgcn_alignbyte(u4, u3, sh);
 }
-__device__ __forceinline__ uint32_t window_mask(const char* ref_win, const SiteRead& rd, bool rc, int64_t x0,
-                                                int64_t n) {
+__device__ __forceinline__ uint32_t window_mask16(const char* ref_win, const SiteRead& rd, bool rc, int64_t x0,
+                                                  int64_t n) {
     const int64_t xl = x0 < n ? x0 : 0;        // past the read: load in range, mask nothing
     uint32_t r[4], q[4];
     load16(ref_win + xl, r);
@@ -2344,60 +2353,80 @@ __device__ __forceinline__ uint32_t window_mask(const char* ref_win, const SiteR
     const int64_t left = n - x0;               // positions past the read end do not count
     return left >= 16 ? m : left <= 0 ? 0u : m & ((1u << left) - 1u);
 }
+// the mask of a lane's 256 / G positions x0 .. (bit b: position x0 + b)
+template <int G>
+__device__ __forceinline__ uint32_t window_mask(const char* ref_win, const SiteRead& rd, bool rc, int64_t x0,
+                                                int64_t n) {
+    if (G == 16) return window_mask16(ref_win, rd, rc, x0, n);
+    const uint32_t lo = window_mask16(ref_win, rd, rc, x0, n);
+    const uint32_t hi = window_mask16(ref_win, rd, rc, x0 + 16, n);
+    return lo | (hi << 16);
+}
 
 // reads over 1024 bp: masks past the four kept in registers, out of line
+template <int G>
 __device__ __forceinline__ uint32_t window_mask_far(const char* ref_win, const SiteRead& rd, bool rc, int64_t x0) {
-    return window_mask(ref_win, rd, rc, x0, rd.len);
+    return window_mask<G>(ref_win, rd, rc, x0, rd.len);
 }
 
-// sums / exclusive prefix sums over a 16-lane group
+// sums / exclusive prefix sums over a G-lane group
+template <int G>
 __device__ __forceinline__ uint32_t grp_sum(uint32_t v) {
 #pragma unroll
-    for (int o = 8; o >= 1; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 16);
+    for (int o = G / 2; o >= 1; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, G);
     return v;
 }
-__device__ __forceinline__ uint32_t grp_excl_scan(uint32_t v, int l16) {
+template <int G>
+__device__ __forceinline__ uint32_t grp_excl_scan(uint32_t v, int lg) {
     uint32_t x = v;
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, o, 16);
-        if (l16 >= o) x += y;
+    for (int o = 1; o < G; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o, G);
+        if (lg >= o) x += y;
     }
     return x - v;
 }
 
-// 16 lanes a NAM, SITES_BLOCK NAMs a block, a fixed grid walking the batch's NAMs.  A
-// NAM's loads come in two rounds: the NAM with its descriptor (k_compact), then --
-// together -- the two k-mers of the orientation test and the read-length window of
-// the NAM as it stands (the common outcome, aln.cpp:60-93 finds most NAMs consistent
-// as they are); a reversed NAM loads its window again.  Pool space is taken with one
+// G lanes a NAM, 256 / G NAMs a block of 256 threads, a fixed grid walking the batch's
+// NAMs.  A NAM's loads come in two rounds: the NAM with its descriptor (k_compact), then
+// -- together -- the two k-mers of the orientation test and the read-length window of
+// the NAM as it stands (the common outcome, aln.cpp:60-93 finds most NAMs consistent as
+// they are); a reversed NAM loads its window again.  The kernel waits on memory most of
+// its cycles, so 8 lanes a NAM (8 NAMs a wave, two 16-position masks a lane) keeps twice
+// the NAMs' loads in flight per wave as 16 lanes did.  Pool space is taken with one
 // atomic a block: same-address atomics from every wave serialise (one a wave made the
 // kernel 2.7x slower than one a 16-NAM block, profiles/r05/sites_ab).
-#define SITES_BLOCK 16
+#define SITES_TPB 256
 // waves a SIMD the register budget is sized for (RSA_SITES_WAVES at build time: 5 = 92
 // VGPRs, what the compiler picks unasked; 6 = 80 with a few spills, 8 = 64 with more)
 #ifndef RSA_SITES_WAVES
 #define RSA_SITES_WAVES 5
 #endif
-__global__ void __launch_bounds__(16 * SITES_BLOCK) __attribute__((amdgpu_waves_per_eu(RSA_SITES_WAVES)))
+// 8 lanes a NAM hold twice the window bytes a lane: 4 waves a SIMD (128 VGPRs) keep it
+// out of scratch (5 spilled 36 registers)
+template <int G> struct SitesWaves { static constexpr int value = G == 8 ? 4 : RSA_SITES_WAVES; };
+template <int G>
+__global__ void __launch_bounds__(SITES_TPB) __attribute__((amdgpu_waves_per_eu(SitesWaves<G>::value)))
 k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, SeedHdr* __restrict__ err_hdr,
         uint64_t cap, const char* __restrict__ seq, const char* __restrict__ seq_rc, SeedIndexParams p,
         rsa_nam_site* __restrict__ sites,
         uint16_t* __restrict__ pool, uint64_t pool_cap, unsigned long long* __restrict__ pool_used, int ham,
         int h_match, int h_mismatch, int h_bonus) {
+    constexpr int NB = SITES_TPB / G;            // NAMs a block
+    constexpr int PL = 256 / G;                  // positions a lane of each 256-position chunk
     // a batch whose NAMs overflow the output was not compacted whole (k_compact skips
     // the reads past `cap`, so their descriptors were never written): no site checks
     // then -- the host reports RSA_ERR_CAPACITY and the caller asks again
-    __shared__ uint32_t s_need[SITES_BLOCK], s_base[SITES_BLOCK];
+    __shared__ uint32_t s_need[NB], s_base[NB];
     __shared__ unsigned long long s_at;
     const uint64_t total = (uint64_t)err_hdr->total <= cap ? (uint64_t)err_hdr->total : 0;
-    const int l16 = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const int lg = threadIdx.x & (G - 1), grp = threadIdx.x / G;
 #ifdef RSA_SEED_PROF
     unsigned long long sp_acc[6] = {0, 0, 0, 0, 0, 0};
 #endif
-    for (uint64_t blk = blockIdx.x; blk * SITES_BLOCK < total; blk += gridDim.x) {
+    for (uint64_t blk = blockIdx.x; blk * NB < total; blk += gridDim.x) {
     SPROF_T(t0);
-    const uint64_t g0 = blk * SITES_BLOCK + grp;
+    const uint64_t g0 = blk * NB + grp;
     const bool valid = g0 < total;
     const uint64_t g = valid ? g0 : total - 1;             // idle groups shadow the last NAM (ballots stay uniform)
     const rsa_nam nam = nams[g];
@@ -2420,17 +2449,17 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
     // the window as the NAM stands and the two k-mers: every load issued before any
     // test.  A window that is not tested is loaded from the read itself and dropped (the
     // read buffer is padded past its last read; a short last contig is not)
-    uint32_t m0 = window_mask(hamming ? ref + ps : rd.s, rd, is_rc, 16 * l16, rd.len);
+    uint32_t m0 = window_mask<G>(hamming ? ref + ps : rd.s, rd, is_rc, PL * lg, rd.len);
     uint32_t flags;
     bool fwd_ok;
     if (k <= 32) {
-        const KmerLoad a = kmer_load(ref, ref_len, nam.ref_start, rd, is_rc, qs, k, l16);
-        const KmerLoad b = kmer_load(ref, ref_len, (int64_t)nam.ref_end - k, rd, is_rc, qe - k, k, l16);
+        const KmerLoad<G> a = kmer_load<G>(ref, ref_len, nam.ref_start, rd, is_rc, qs, k, lg);
+        const KmerLoad<G> b = kmer_load<G>(ref, ref_len, (int64_t)nam.ref_end - k, rd, is_rc, qe - k, k, lg);
         __builtin_amdgcn_sched_barrier(0);                 // every load above issued before the first test
-        fwd_ok = kmer_test(a, l16) & kmer_test(b, l16);
+        fwd_ok = kmer_test<G>(a, lg) & kmer_test<G>(b, lg);
     } else {
-        fwd_ok = site_kmer_eq(ref, ref_len, nam.ref_start, rd, is_rc, qs, k, l16) &
-                 site_kmer_eq(ref, ref_len, (int64_t)nam.ref_end - k, rd, is_rc, qe - k, k, l16);
+        fwd_ok = site_kmer_eq<G>(ref, ref_len, nam.ref_start, rd, is_rc, qs, k, lg) &
+                 site_kmer_eq<G>(ref, ref_len, (int64_t)nam.ref_end - k, rd, is_rc, qe - k, k, lg);
     }
     if (!hamming) m0 = 0u;
     if (fwd_ok) {
@@ -2439,13 +2468,13 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
         const int64_t qs2 = rd.len - nam.query_end, qe2 = rd.len - nam.query_start;
         bool rev_ok;
         if (k <= 32) {
-            const KmerLoad a = kmer_load(ref, ref_len, nam.ref_start, rd, !is_rc, qs2, k, l16);
-            const KmerLoad b = kmer_load(ref, ref_len, (int64_t)nam.ref_end - k, rd, !is_rc, qe2 - k, k, l16);
+            const KmerLoad<G> a = kmer_load<G>(ref, ref_len, nam.ref_start, rd, !is_rc, qs2, k, lg);
+            const KmerLoad<G> b = kmer_load<G>(ref, ref_len, (int64_t)nam.ref_end - k, rd, !is_rc, qe2 - k, k, lg);
             __builtin_amdgcn_sched_barrier(0);
-            rev_ok = kmer_test(a, l16) & kmer_test(b, l16);
+            rev_ok = kmer_test<G>(a, lg) & kmer_test<G>(b, lg);
         } else {
-            rev_ok = site_kmer_eq(ref, ref_len, nam.ref_start, rd, !is_rc, qs2, k, l16) &
-                     site_kmer_eq(ref, ref_len, (int64_t)nam.ref_end - k, rd, !is_rc, qe2 - k, k, l16);
+            rev_ok = site_kmer_eq<G>(ref, ref_len, nam.ref_start, rd, !is_rc, qs2, k, lg) &
+                     site_kmer_eq<G>(ref, ref_len, (int64_t)nam.ref_end - k, rd, !is_rc, qe2 - k, k, lg);
         }
         if (rev_ok) {
             flags = 1;
@@ -2453,7 +2482,7 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
             qs = qs2;
             qe = qe2;
             hamming = proj(qs, qe, ps);
-            m0 = hamming ? window_mask(ref + ps, rd, is_rc, 16 * l16, rd.len) : 0u;
+            m0 = hamming ? window_mask<G>(ref + ps, rd, is_rc, PL * lg, rd.len) : 0u;
         } else {
             flags = 2;
             hamming = false;
@@ -2462,12 +2491,12 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
     SPROF_T(t1);
     const int n = (int)rd.len;
     uint32_t hd = 0, mm_off = 0;
-    uint32_t m1 = 0, m2 = 0, m3 = 0;             // this lane's masks, positions c * 256 + 16 * l16 + b
+    uint32_t m1 = 0, m2 = 0, m3 = 0;             // this lane's masks, positions c * 256 + PL * lg + b
     bool want = false;
     // the mask of chunk c (256 positions): registers for the first four, loads again beyond
     auto mask_of = [&](int c) -> uint32_t {
         if (c < 4) return c == 0 ? m0 : c == 1 ? m1 : c == 2 ? m2 : m3;
-        return window_mask_far(ref + ps, rd, is_rc, 256 * (int64_t)c + 16 * l16);
+        return window_mask_far<G>(ref + ps, rd, is_rc, 256 * (int64_t)c + PL * lg);
     };
     if (hamming) {
         flags |= RSA_SITE_HAMMING;
@@ -2475,13 +2504,13 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
         // reads over 256 bp: the masks of positions 256 .. 1023 into registers too
 #pragma nounroll
         for (int c = 1; 256 * c < n; ++c) {
-            const uint32_t mc = window_mask(ref + ps, rd, is_rc, 256 * (int64_t)c + 16 * l16, rd.len);
+            const uint32_t mc = window_mask<G>(ref + ps, rd, is_rc, 256 * (int64_t)c + PL * lg, rd.len);
             m1 = c == 1 ? mc : m1;
             m2 = c == 2 ? mc : m2;
             m3 = c == 3 ? mc : m3;
             hd += __popc(mc);
         }
-        hd = grp_sum(hd);
+        hd = grp_sum<G>(hd);
         want = (double)((float)hd / (float)rd.len) < 0.05;
     }
     // the pool's u16 words hold positions and hamming_align's segment ends: longer reads
@@ -2491,11 +2520,11 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
     // n_mm words; hamming_align's result: a 6-word header and at most 2 n_mm + 3 ops of 2 words)
     const uint32_t need = (want && valid && fits) ? (ham ? 12u + 4u * hd : hd) : 0u;
     SPROF_T(t2);
-    if (l16 == 0) s_need[grp] = need;
+    if (lg == 0) s_need[grp] = need;
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t acc = 0;
-        for (int j = 0; j < SITES_BLOCK; ++j) { s_base[j] = acc; acc += s_need[j]; }
+        for (int j = 0; j < NB; ++j) { s_base[j] = acc; acc += s_need[j]; }
         s_at = acc ? atomicAdd(pool_used, (unsigned long long)acc) : 0ull;
     }
     __syncthreads();
@@ -2511,36 +2540,36 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
             for (int c = 0; 256 * c < n && m < hd; ++c) {
                 uint32_t bits = mask_of(c);
                 const uint32_t cnt = __popc(bits);
-                uint32_t o = m + grp_excl_scan(cnt, l16);
+                uint32_t o = m + grp_excl_scan<G>(cnt, lg);
                 while (bits) {
                     const int b = __builtin_ctz(bits);
                     bits &= bits - 1;
-                    if (valid) pool[at + o] = (uint16_t)(256 * c + 16 * l16 + b);
+                    if (valid) pool[at + o] = (uint16_t)(256 * c + PL * lg + b);
                     ++o;
                 }
-                m += grp_sum(cnt);
+                m += grp_sum<G>(cnt);
             }
         } else {
             // hamming_align (aligner.cpp:219-302) over the window just tested: the group walks
-            // the mismatch positions in order (16-base ballots) twice, every lane computing the
+            // the mismatch positions in order (per-lane ballots) twice, every lane computing the
             // same values; lane 0 writes the result
             flags |= RSA_SITE_POSITIONS | RSA_SITE_ALIGNED;
             mm_off = (uint32_t)at;
             // 1. highest_scoring_segment (aligner.cpp:219-252), run by run: between mismatches
             //    the score only grows, so each run of matches needs one check at its end
-            //    Only the 16-position blocks holding a mismatch are visited (a group ballot
+            //    Only the lanes' position blocks holding a mismatch are visited (a group ballot
             //    of the lanes' masks, in position order): the others change nothing here.
             int start = 0, best_start = 0, best_end = 0, i = 0;
             int score = h_bonus, best = 0;
             for (int c = 0; 256 * c < n; ++c) {
                 const uint32_t mc = mask_of(c);
-                uint32_t nz = grp_ballot(mc != 0u);
+                uint32_t nz = grp_ballot<G>(mc != 0u);
                 while (nz) {
-                    // lane li of the group holds positions 256 c + 16 li .. + 15
+                    // lane li of the group holds positions 256 c + PL li .. + PL - 1
                     const int li = __builtin_ctz(nz);
                     nz &= nz - 1;
-                    const int i0 = 256 * c + 16 * li;
-                    uint32_t bits = (uint32_t)__shfl((int)mc, li, 16);
+                    const int i0 = 256 * c + PL * li;
+                    uint32_t bits = (uint32_t)__shfl((int)mc, li, G);
                     while (bits) {
                         const int m = i0 + __builtin_ctz(bits);
                         bits &= bits - 1;
@@ -2566,7 +2595,7 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
             bool have = false;
             auto push = [&](uint32_t op, uint32_t len) {
                 if (have && (last & 0xf) == op) { last += len << 4; return; }
-                if (have && l16 == 0 && valid) {
+                if (have && lg == 0 && valid) {
                     pool[at + 6 + 2 * n_ops] = (uint16_t)(last & 0xFFFF);
                     pool[at + 7 + 2 * n_ops] = (uint16_t)(last >> 16);
                 }
@@ -2578,20 +2607,20 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
             int cur = best_start;
             for (int c = best_start >> 8; 256 * c < best_end; ++c) {
                 // this lane's positions in [best_start, best_end) only, blocks with a mismatch visited
-                const int p0 = 256 * c + 16 * l16;
+                const int p0 = 256 * c + PL * lg;
                 uint32_t mine = mask_of(c);
                 const int lo = best_start - p0, hi = best_end - p0;
-                if (lo >= 16 || hi <= 0) mine = 0u;
+                if (lo >= PL || hi <= 0) mine = 0u;
                 else {
                     if (lo > 0) mine &= ~((1u << lo) - 1u);
-                    if (hi < 16) mine &= (1u << hi) - 1u;
+                    if (hi < PL) mine &= (1u << hi) - 1u;
                 }
-                uint32_t nz = grp_ballot(mine != 0u);
+                uint32_t nz = grp_ballot<G>(mine != 0u);
                 while (nz) {
                     const int li = __builtin_ctz(nz);
                     nz &= nz - 1;
-                    const int i0 = 256 * c + 16 * li;
-                    uint32_t bits = (uint32_t)__shfl((int)mine, li, 16);
+                    const int i0 = 256 * c + PL * li;
+                    uint32_t bits = (uint32_t)__shfl((int)mine, li, G);
                     while (bits) {
                         const int m = i0 + __builtin_ctz(bits);
                         bits &= bits - 1;
@@ -2604,12 +2633,12 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
             }
             if (best_end > cur) push(7, (uint32_t)(best_end - cur));
             if (n - best_end > 0) push(4, (uint32_t)(n - best_end));
-            if (have && l16 == 0 && valid) {
+            if (have && lg == 0 && valid) {
                 pool[at + 6 + 2 * n_ops] = (uint16_t)(last & 0xFFFF);
                 pool[at + 7 + 2 * n_ops] = (uint16_t)(last >> 16);
             }
             n_ops += have ? 1 : 0;
-            if (l16 == 0 && valid) {
+            if (lg == 0 && valid) {
                 pool[at + 0] = (uint16_t)((uint32_t)best & 0xFFFF);
                 pool[at + 1] = (uint16_t)((uint32_t)best >> 16);
                 pool[at + 2] = (uint16_t)best_start;
@@ -2620,7 +2649,7 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
         }
     }
     SPROF_T(t4);
-    if (valid && l16 == 0) {
+    if (valid && lg == 0) {
         rsa_nam_site out;
         out.flags = (uint8_t)flags;
         out.orig_is_rc = (uint8_t)(nam.is_rc != 0);
@@ -2645,6 +2674,12 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096)
         for (int i = 0; i < 6; ++i) g_sites_prof[blockIdx.x * 4 + wv][i] = (unsigned int)sp_acc[i];
 #endif
+}
+
+// lanes per NAM of k_sites (RSA_SITES_G: 8 or 16; default 8), read per call
+static int sites_lanes() {
+    const char* e = getenv("RSA_SITES_G");
+    return e && atoi(e) == 16 ? 16 : 8;
 }
 
 // ---------------------------------------------------------------------------
@@ -3011,11 +3046,19 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
         // 6. site checks (aln.cpp:60-93, 374-431)
         if (out->sites) {
             kt.begin(st, RSA_K_SITES);
-            const uint32_t grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1, (cap + SITES_BLOCK - 1) / SITES_BLOCK),
-                                                               4096);
-            hipLaunchKernelGGL(k_sites, dim3(grid), dim3(16 * SITES_BLOCK), 0, st, DP(B_OUT, rsa_nam), DP(B_NREAD, SiteDesc), dhdr,
-                               cap, D_SEQ, D_SEQRC, p, DP(B_SITES, rsa_nam_site), DP(B_POOL, uint16_t), out->mm_capacity,
-                               &dhdr->mm_used, out->hamming_align ? 1 : 0, out->match, out->mismatch, out->end_bonus);
+            const int sg = sites_lanes();
+            const uint64_t nb = SITES_TPB / sg;
+            const uint32_t grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1, (cap + nb - 1) / nb), 4096);
+            if (sg == 16)
+                hipLaunchKernelGGL(k_sites<16>, dim3(grid), dim3(SITES_TPB), 0, st, DP(B_OUT, rsa_nam), DP(B_NREAD, SiteDesc),
+                                   dhdr, cap, D_SEQ, D_SEQRC, p, DP(B_SITES, rsa_nam_site), DP(B_POOL, uint16_t),
+                                   out->mm_capacity, &dhdr->mm_used, out->hamming_align ? 1 : 0, out->match,
+                                   out->mismatch, out->end_bonus);
+            else
+                hipLaunchKernelGGL(k_sites<8>, dim3(grid), dim3(SITES_TPB), 0, st, DP(B_OUT, rsa_nam), DP(B_NREAD, SiteDesc),
+                                   dhdr, cap, D_SEQ, D_SEQRC, p, DP(B_SITES, rsa_nam_site), DP(B_POOL, uint16_t),
+                                   out->mm_capacity, &dhdr->mm_used, out->hamming_align ? 1 : 0, out->match,
+                                   out->mismatch, out->end_bonus);
             SCHK(hipGetLastError());
             kt.end(st);
         }

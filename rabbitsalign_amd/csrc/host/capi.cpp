@@ -387,6 +387,10 @@ static void fill_stats(const PipelineResult& res, rsam_stats* out) {
     out->t_last_start = res.phases.last_start;
     out->t_last_put = res.phases.last_put;
     out->t_workers_done = res.phases.workers_done;
+    out->t_first_out = res.phases.first_out;
+    out->t_first_ext_begin = res.phases.first_ext_begin;
+    out->t_first_ext_end = res.phases.first_ext_end;
+    out->replayed_chunks = res.phases.replayed;
 }
 
 // the pipeline over `src` with the SAM (header + body) to sam_path, or kept in memory

@@ -147,6 +147,7 @@ struct OrderedSink {
     std::map<size_t, Entry> pending;
     std::deque<SamText> queue;                // in chunk order, for the writer
     size_t queued_bytes = 0;
+    double first_out = 0;                     // s after opening: the first text reached the writer
     size_t next = 0;
     uint64_t bytes = 0;
     SamDigest total;
@@ -222,6 +223,7 @@ struct OrderedSink {
             for (auto& pc : it->second.pieces) {
                 bytes += pc.first.size();
                 total.append(pc.second);
+                if (!first_out) first_out = since(t_open);
                 if (sink) {
                     queued_bytes += pc.first.size();
                     queue.push_back(std::move(pc.first));
@@ -678,10 +680,13 @@ void pe_get_str(PeChunk& c, const MapContext& mc, float mu, float sigma, std::ve
 }
 
 // pairs per piece of a chunk's SAM text handed to the writer (RSA_SAM_PIECE; 0 = the
-// whole chunk at once): the writer starts on a chunk while its last() runs on
+// whole chunk at once, the default): with pieces the writer starts on a chunk while its
+// last() runs on.  Measured (profiles/r06/ab_pieces.json, 16 alternating steps each):
+// pieces of 2000 pairs bring the first SAM text to the writer 3 ms earlier a step (10.8
+// against 14.0 ms) but the streamed rate falls from 19.7 to 18.7 Mreads/s
 static size_t sam_piece_pairs() {
-    static const size_t n = getenv("RSA_SAM_PIECE") ? (size_t)atol(getenv("RSA_SAM_PIECE")) : 2000;
-    return n;
+    const char* e = getenv("RSA_SAM_PIECE");        // per chunk (A/B runs change it between calls)
+    return e ? (size_t)atol(e) : 0;
 }
 
 // the chunk's extension results start at infos[pos]; its SAM text goes to `os` in pieces
@@ -803,6 +808,13 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
     // prefetch depth (RSA_PREFETCH chunks, default 2W+2; 0 = every worker seeds its own chunk)
     const char* pf_env = getenv("RSA_PREFETCH");
     const size_t window = pf_env ? (size_t)atol(pf_env) : 2 * (size_t)W + 2;
+    // until the first chunk's extension call has returned, the prefetch stays this many
+    // chunks ahead (RSA_EARLY_WINDOW; 0 = the full window from the start): the first
+    // chunk's extension -- on the path to the first SAM byte -- then shares the GPU with
+    // a few seeding calls, not with the whole window's
+    const char* ew_env = getenv("RSA_EARLY_WINDOW");
+    const size_t early_window = ew_env ? (size_t)atol(ew_env) : 0;
+    bool first_extended = false;
 
     std::mutex m;
     std::condition_variable cv;
@@ -830,10 +842,14 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
     bool leader_busy = true;       // the leader may still hand a chunk over: nobody ends the run before
     // chunks 1..RSA_EARLY_SEEDS (default 2) are seeded alongside chunk 0: the writer needs them
     // right after it, and a few calls do not crowd chunk 0's seeding out of the GPU
-    static const size_t early_seeds = getenv("RSA_EARLY_SEEDS") ? (size_t)atoi(getenv("RSA_EARLY_SEEDS")) : 2;
+    const size_t early_seeds = getenv("RSA_EARLY_SEEDS") ? (size_t)atoi(getenv("RSA_EARLY_SEEDS")) : 2;
     bool lead_seeded = false;      // other prefetch waits until chunk 0 is seeded: it would only queue
                                    // other chunks' seeding ahead of the single-worker timeline
     size_t next_par = 0;           // next chunk for the parallel stage (valid once frozen)
+    // while the leader replays chunks before a rank's part (the estimate still open after
+    // chunk 0), the other workers seed the next kReplayAhead of them ahead of it
+    static constexpr size_t kReplayAhead = 2;
+    size_t lead_next = 0;          // the replay chunk after the leader's (0: no replay prefetch)
     std::unique_ptr<PeChunk> handed;                     // part() done in the sequential phase
     InsertSizeDistribution isize, frozen_isize;
     std::exception_ptr failure;
@@ -903,9 +919,16 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
         pe_get_str(c, mc, est.mu, est.sigma, jobs);
         c.stats.tot_aligner_calls += jobs.size();
         const auto te = Clock::now();
+        if (c.in.index == first) c.times.first_ext_begin = since(t0);
         {
             Unslot u(slots, offl, c.in.index);
             eng.extend(jobs, mc.aparams, infos);
+        }
+        if (c.in.index == first) {
+            c.times.first_ext_end = since(t0);
+            std::lock_guard<std::mutex> g(m);
+            first_extended = true;
+            cv.notify_all();
         }
         c.stats.tot_aligner_calls -= no_shared_count(infos);   // the reference aligns none of those
         c.times.extend += since(te);
@@ -950,6 +973,11 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
                     const bool own = mine(pre->in.index);         // else replayed for the estimate only
                     jobs.clear();
                     if (own) pe_get_str(*pre, mc, isize.mu, isize.sigma, jobs);
+                    if (next < first) {
+                        std::lock_guard<std::mutex> g(m);
+                        lead_next = next + 1;
+                        cv.notify_all();
+                    }
                     std::unique_ptr<PeChunk> cur = acquire(next);
                     if (!cur) {
                         std::lock_guard<std::mutex> g(m);
@@ -958,14 +986,22 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
                     if (cur) pe_part(*cur, mc, isize, early_freeze, !mine(cur->in.index));
                     next++;
                     if (!own) {
+                        lt.replayed++;
                         recycle(std::move(pre));
                         pre = std::move(cur);
                         continue;
                     }
                     const auto te = Clock::now();
+                    if (pre->in.index == first) pre->times.first_ext_begin = since(t0);
                     {
                         Unslot u(slots, offl, pre->in.index);
                         eng.extend(jobs, mc.aparams, infos);
+                    }
+                    if (pre->in.index == first) {
+                        pre->times.first_ext_end = since(t0);
+                        std::lock_guard<std::mutex> g(m);
+                        first_extended = true;
+                        cv.notify_all();
                     }
                     pre->times.extend += since(te);
                     pre->stats.tot_aligner_calls += jobs.size() - no_shared_count(infos);
@@ -976,7 +1012,10 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
                     pre = std::move(cur);
                 }
                 lt.sequential = since(t0);
-                if (pre && !mine(pre->in.index)) recycle(std::move(pre));   // replayed only
+                if (pre && !mine(pre->in.index)) {     // replayed only
+                    lt.replayed++;
+                    recycle(std::move(pre));
+                }
                 std::lock_guard<std::mutex> g(m);
                 frozen = true;
                 frozen_isize = isize;
@@ -996,9 +1035,15 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
                         if (failure || done) break;
                         if (frozen && handed) { c = std::move(handed); break; }
                         if (frozen && next_par < n_chunks) { idx = next_par++; break; }
+                        if (!frozen && lead_next) {       // replay chunks just ahead of the leader
+                            for (size_t r = lead_next; r < std::min(first, lead_next + kReplayAhead); ++r)
+                                if (!is_claimed(r)) { pf = r; claim(r); break; }
+                            if (pf != SIZE_MAX) break;
+                        }
                         skip_claimed();
+                        const size_t win = first_extended || !early_window ? window : std::min(window, early_window);
                         if ((lead_seeded || rel(next_seed) <= early_seeds) && next_seed < n_chunks &&
-                            rel(next_seed) < consumed + window) {
+                            rel(next_seed) < consumed + win) {
                             pf = next_seed;
                             claim(pf);
                             skip_claimed();
@@ -1066,6 +1111,7 @@ PipelineResult run_pipeline_pe(ReadSource& src, Engine& eng, const MapContext& m
     if (failure) std::rethrow_exception(failure);
     result.stats = stats_all;
     result.phases = phases_all;
+    result.phases.first_out = os.first_out;
     result.singletons = singletons.load();
     result.map_seconds = since(t0);
     result.sam_bytes = os.bytes;

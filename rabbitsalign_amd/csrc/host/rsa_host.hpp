@@ -780,7 +780,14 @@ struct PhaseTimes {
     // since the call started: chunk 0 loaded and seeded; the last chunk's finish began
     // ... its SAM text went to the sink; every worker was done (the sink may still be writing)
     double first_seeded = 0, last_start = 0, last_put = 0, workers_done = 0;
+    // the first SAM text reached the writer; the first chunk's extension call began / returned
+    double first_out = 0, first_ext_begin = 0, first_ext_end = 0;
+    uint64_t replayed = 0;                      // chunks parted only for the insert-size estimate
     void add(const PhaseTimes& o) {
+        first_out = std::max(first_out, o.first_out);
+        first_ext_begin = std::max(first_ext_begin, o.first_ext_begin);
+        first_ext_end = std::max(first_ext_end, o.first_ext_end);
+        replayed += o.replayed;
         seed += o.seed; extend += o.extend; part += o.part; collect += o.collect; last += o.last;
         sequential += o.sequential; load += o.load; output += o.output;
         first_seeded = std::max(first_seeded, o.first_seeded);

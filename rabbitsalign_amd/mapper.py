@@ -27,7 +27,8 @@ class _Stats(C.Structure):
                 ("t_seed", C.c_double), ("t_extend", C.c_double), ("t_part", C.c_double),
                 ("t_collect", C.c_double), ("t_last", C.c_double), ("t_sequential", C.c_double),
                 ("t_first_seeded", C.c_double), ("t_last_start", C.c_double), ("t_last_put", C.c_double),
-                ("t_workers_done", C.c_double)]
+                ("t_workers_done", C.c_double), ("t_first_out", C.c_double), ("t_first_ext_begin", C.c_double),
+                ("t_first_ext_end", C.c_double), ("replayed_chunks", C.c_uint64)]
 
 
 class _Info(C.Structure):
@@ -163,6 +164,10 @@ class MapStats:
     t_last_start: float = 0.0
     t_last_put: float = 0.0
     t_workers_done: float = 0.0
+    t_first_out: float = 0.0
+    t_first_ext_begin: float = 0.0
+    t_first_ext_end: float = 0.0
+    replayed_chunks: int = 0
 
 
 class Reads:

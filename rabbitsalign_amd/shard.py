@@ -49,6 +49,9 @@ def first_pair(rank: int, step: int, total_steps: int, pairs_per_step: int) -> i
 
 
 def _reduce(values, op, device):
+    import sys
+    if "torch" not in sys.modules:       # no torch, no process group (a 1-GPU run without torch)
+        return list(values)
     import torch
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
@@ -60,6 +63,9 @@ def _reduce(values, op, device):
 
 def reduce_run(elapsed_s: float, stats: dict, device="cpu") -> tuple[float, dict]:
     """Max wall time over ranks and the sum of every counter in `stats`."""
+    import sys
+    if "torch" not in sys.modules:
+        return elapsed_s, {k: int(round(float(v))) for k, v in stats.items()}
     import torch.distributed as dist
     (wall,) = _reduce([elapsed_s], dist.ReduceOp.MAX, device)
     keys = sorted(stats)
