@@ -88,11 +88,18 @@ __device__ __forceinline__ int grp_min(int v) {
     return v;
 }
 
-// query profile of one job: [code 0..4][row r of a virtual lane][virtual lane 0..31], f16 bits
+// query profile of one job: [code 0..3][row r of a virtual lane][virtual lane 0..31], f16 bits.
+// Reference code 4 (N, and the padding around a window) scores -mismatch against every
+// query row, so its row is one block-wide constant row after the jobs' profiles: a job in
+// slot j stages code 4 as the row offset 4 * (VS_JOBS - j), which lands there.  One row a
+// job fewer in LDS (4 codes, not 5): 6 workgroups a CU instead of 5 at 8 rows a virtual
+// lane (2 x 250 bp), the same address arithmetic a step.
 template <int RV> struct VProf {
     static constexpr int CODE = RV * 32;            // u16 entries per reference code
-    static constexpr int JOB = 5 * CODE;
+    static constexpr int JOB = 4 * CODE;
 };
+// the staged code of reference code 4 for the job in `slot`
+__device__ __forceinline__ uint32_t pad_code(int slot) { return 4u * (uint32_t)(VS_JOBS - slot); }
 
 // The packed scores of a step's rows: low halves against code clo (virtual lane
 // gl), high halves against code chi (virtual lane 16 + gl).  Two 16-bit LDS
@@ -124,7 +131,7 @@ __device__ __forceinline__ void prof_build(uint16_t* __restrict__ prof, int gl, 
         for (int r = 0; r < RV; ++r) {
             const int q = qcode(v * RV + r);
 #pragma unroll
-            for (int code = 0; code < 5; ++code)
+            for (int code = 0; code < 4; ++code)
                 prof[code * VProf<RV>::CODE + r * 32 + v] = (uint16_t)(q == code ? m16 : x16);
         }
     }
@@ -407,7 +414,7 @@ k_ext_scan_v(const ExtJobDev* __restrict__ sjobs, const int* __restrict__ order,
     constexpr int SLOT = WCAP + 2 * VS_PAD + 4;
     constexpr int QSLOT = 32 * RV + 4;
     __shared__ __attribute__((aligned(4))) uint8_t s_r[VS_JOBS][SLOT];
-    __shared__ __attribute__((aligned(16))) uint16_t s_prof[VS_JOBS][VProf<RV>::JOB];
+    __shared__ __attribute__((aligned(16))) uint16_t s_prof[VS_JOBS + 1][VProf<RV>::JOB];   // + the code-4 row
     __shared__ __attribute__((aligned(4))) uint8_t s_q[VS_JOBS][QSLOT];   // query codes (qcode7), 7 past the query
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int slot = wave * (64 / VS_G) + lane / VS_G, gl = lane & (VS_G - 1);
@@ -423,6 +430,7 @@ k_ext_scan_v(const ExtJobDev* __restrict__ sjobs, const int* __restrict__ order,
     uint8_t* rcb = s_r[slot] + VS_PAD;
     uint8_t* rc = rcb + pre;
     uint16_t* prof = s_prof[slot];
+    const uint32_t pc = pad_code(slot), pc4 = pc * 0x01010101u;
     uint8_t* qc = s_q[slot] + preq;
 
     // stage the window and the query as SSW codes, a dword (4 codes) at a time.  Every
@@ -444,13 +452,20 @@ k_ext_scan_v(const ExtJobDev* __restrict__ sjobs, const int* __restrict__ order,
 #pragma unroll
         for (int t = 0; t < QD; ++t) y[t] = qw[min(gl + t * VS_G, ql)];
         uint32_t* rcw = (uint32_t*)rcb;
-        for (int i = gl; i < VS_PAD / 4; i += VS_G) rcw[i - VS_PAD / 4] = 0x04040404u;
+        for (int i = gl; i < VS_PAD / 4; i += VS_G) rcw[i - VS_PAD / 4] = pc4;
 #pragma unroll
         for (int t = 0; t < WD; ++t) {
             const int i = gl + t * VS_G;
-            if (i < nw) rcw[i] = codes4(x[t], 4 * i - pre, rlen, [](uint32_t b) { return ssw_code((unsigned char)b); }, 4u);
+            if (i < nw)
+                rcw[i] = codes4(x[t], 4 * i - pre, rlen, [&](uint32_t b) {
+                    const uint32_t c = (uint32_t)ssw_code((unsigned char)b);
+                    return c < 4 ? c : pc;
+                }, pc);
         }
-        for (int i = nw + gl; i < (WCAP + VS_PAD + 4) / 4; i += VS_G) rcw[i] = 0x04040404u;
+        for (int i = nw + gl; i < (WCAP + VS_PAD + 4) / 4; i += VS_G) rcw[i] = pc4;
+        // the block's code-4 row (every wave writes the same values; the barrier after the
+        // profiles orders them before any read)
+        for (int i = threadIdx.x; i < VProf<RV>::CODE; i += 64 * VS_WAVES) s_prof[VS_JOBS][i] = (uint16_t)h_bits16(-mismatch);
         uint32_t* qcw = (uint32_t*)s_q[slot];
 #pragma unroll
         for (int t = 0; t < QD; ++t) {
@@ -511,7 +526,7 @@ k_ext_scan_v(const ExtJobDev* __restrict__ sjobs, const int* __restrict__ order,
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
         if (ron)
-            for (int i = gl; i < VS_PAD; i += VS_G) rc[ref_end1 + 1 + i] = 4;
+            for (int i = gl; i < VS_PAD; i += VS_G) rc[ref_end1 + 1 + i] = (uint8_t)pc;
         prof_build<RV>(prof, gl, [&](int p) { return p < nrow ? (int)qc[read_end1 - p] : 7; }, m16, x16);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();

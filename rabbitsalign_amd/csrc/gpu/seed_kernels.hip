@@ -2676,10 +2676,14 @@ k_sites(const rsa_nam* __restrict__ nams, const SiteDesc* __restrict__ desc, See
 #endif
 }
 
-// lanes per NAM of k_sites (RSA_SITES_G: 8 or 16; default 8), read per call
-static int sites_lanes() {
+// lanes per NAM of k_sites (RSA_SITES_G=8/16 fixes it; read per call).  By default 8 for
+// reads of <= 192 bp on average, 16 above: in-bench launches (profiles/r06/ab_setprio_sites*.json)
+// 2 x 150 bp 211 -> 179 us with 8, 2 x 250 bp 371 -> 421 us (a wave's 8 groups walk more
+// mismatches each in hamming_align, and the serial walks diverge)
+static int sites_lanes(uint64_t bases, uint32_t n) {
     const char* e = getenv("RSA_SITES_G");
-    return e && atoi(e) == 16 ? 16 : 8;
+    if (e && (atoi(e) == 8 || atoi(e) == 16)) return atoi(e);
+    return bases <= 192ull * n ? 8 : 16;
 }
 
 // ---------------------------------------------------------------------------
@@ -3046,7 +3050,7 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
         // 6. site checks (aln.cpp:60-93, 374-431)
         if (out->sites) {
             kt.begin(st, RSA_K_SITES);
-            const int sg = sites_lanes();
+            const int sg = sites_lanes(bases, n);
             const uint64_t nb = SITES_TPB / sg;
             const uint32_t grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1, (cap + nb - 1) / nb), 4096);
             if (sg == 16)
