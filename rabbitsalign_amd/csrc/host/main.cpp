@@ -165,8 +165,18 @@ int cli_main(int argc, char** argv, EngineFactory factory, const char* prog) {
             build_index(true);
             std::string out = o.out_file.empty() ? sti_path : o.out_file;
             idx.write(out);
-            if (o.verbose) fprintf(stderr, "wrote %s (%zu randstrobes, bits %d, filter cutoff %d)\n", out.c_str(),
-                                   (size_t)idx.size(), idx.bits, idx.filter_cutoff);
+            if (o.verbose) {
+                fprintf(stderr, "wrote %s (%zu randstrobes, bits %d, filter cutoff %d)\n", out.c_str(),
+                        (size_t)idx.size(), idx.bits, idx.filter_cutoff);
+                if (idx.built_on_device)
+                    fprintf(stderr, "GPU build %.1f ms (upload %.1f, syncmers %.1f, randstrobes %.1f, sort %.1f, buckets "
+                                    "%.1f); (hash, position) ties %lu, their order replayed on the host in %.1f ms\n",
+                            idx.device_build_ms[5], idx.device_build_ms[0], idx.device_build_ms[1],
+                            idx.device_build_ms[2], idx.device_build_ms[3], idx.device_build_ms[4],
+                            (unsigned long)idx.position_ties, idx.ms_tie_replay);
+                else
+                    fprintf(stderr, "host build; (hash, position) ties %lu\n", (unsigned long)idx.position_ties);
+            }
             return 0;
         }
         if (o.use_index) {
