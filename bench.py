@@ -125,7 +125,7 @@ def host_cores(pinned: bool = False) -> int:
 
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "latest_traffic.json")
 LINE_PEAK_GLINES = 46.0      # random 128-B lines, 8 lanes a line, 32 GB table (scripts/micro/line_probe.hip)
-EXT_PMC_JSON = os.path.join(ROOT, "profiles", "r04", "ext_pmc.json")
+EXT_PMC_JSON = os.path.join(ROOT, "profiles", "r06", "ext_pmc.json")
 
 
 def scan_pmc(symbol: str):
@@ -194,7 +194,7 @@ def kernel_roofline(name: str, k: dict, ks: dict) -> dict:
                                  "achieved": round(issued / 1e9, 2), "peak": round(ceiling / 1e9, 1),
                                  "unit": "G wave64 VALU instr/s", "frac": round(issued / ceiling, 4),
                                  "cells_ceiling_Gcells": round(ceiling / ipc / 1e9, 1),
-                                 "source": "profiles/r04/ext_pmc.json"}
+                                 "source": "profiles/r06/ext_pmc.json"}
     else:
         achieved = per_launch_bytes / avg_s / 1e9
         out.update({"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",

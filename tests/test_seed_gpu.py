@@ -167,11 +167,15 @@ def test_seed_batch_independent(setup):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lanes", ["8", "16"])
 @pytest.mark.parametrize("mm_capacity", [None, 8])
-def test_sites(setup, mm_capacity):
+def test_sites(setup, mm_capacity, lanes, monkeypatch):
     """k_sites against the oracle's ora_nam_site (reverse_nam_if_needed
     aln.cpp:60-93 + extend_seed_part's Hamming test aln.cpp:374-395), for every NAM of
-    every golden read; a tiny position pool must flag POOL_FULL instead of writing."""
+    every golden read; a tiny position pool must flag POOL_FULL instead of writing.  Both
+    kernel shapes: 8 and 16 lanes a NAM (RSA_SITES_G; the call's default follows the mean
+    read length)."""
+    monkeypatch.setenv("RSA_SITES_G", lanes)
     name, idx, ctx, ora = setup
     reads = _reads(name)
     ref = idx.ref_seq.tobytes()
@@ -199,11 +203,13 @@ def test_sites(setup, mm_capacity):
 
 
 @pytest.mark.gpu
-def test_sites_hamming_align(setup):
+@pytest.mark.parametrize("lanes", ["8", "16"])
+def test_sites_hamming_align(setup, lanes, monkeypatch):
     """k_sites with hamming_align on (rsa_nam_batch.hamming_align, RSA_SITE_ALIGNED): every
     accepted site's score, segment, mismatch count and CIGAR equal the oracle's literal
     restatement of aligner.cpp:219-302 on the same oriented read and projected window;
-    everything else equals the positions mode."""
+    everything else equals the positions mode.  Both kernel shapes (RSA_SITES_G 8 / 16)."""
+    monkeypatch.setenv("RSA_SITES_G", lanes)
     from rabbitsalign_amd.native import GpuContext
     name, idx, ctx, ora = setup
     reads = _reads(name)
