@@ -265,7 +265,11 @@ __device__ PassOut sw_pass_dispatch(const uint8_t* qc, int nrow, const uint8_t* 
 template <int RMAX>
 __global__ void __launch_bounds__(64 * SCAN_WAVES)
 k_ext_scan(const ExtJobDev* __restrict__ jobs, int n_jobs, const int* __restrict__ idx, const char* __restrict__ qbuf,
-           const char* __restrict__ ref, ScanRes* __restrict__ out, int match, int mismatch, int gO, int gE) {
+           const char* __restrict__ ref, ScanRes* __restrict__ out, int match, int mismatch, int gO, int gE,
+           const int* __restrict__ n_dev) {
+    // n_dev: the list's length as the device counted it (the in-stream redo pass); the
+    // grid covers n_jobs at most
+    if (n_dev) n_jobs = min(n_jobs, *n_dev);
     __shared__ uint8_t s_q[SCAN_WAVES][MAXQ_LDS];
     // every packed 16-bit score stays far inside int16
     const bool fused_ok = match >= 0 && match <= 28 && mismatch >= 0 && mismatch < 4000 && gO >= 0 && gO < 4000 &&
@@ -836,10 +840,12 @@ k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
              const int* __restrict__ idx, const char* __restrict__ qbuf, const char* __restrict__ ref,
              uint32_t* __restrict__ cig_pool, uint32_t* __restrict__ raw_pool, rsa_aln* __restrict__ out, int match,
              int mismatch, int gO, int gE, int bonus, int* __restrict__ queue, int* __restrict__ qcount,
-             int* __restrict__ overflow, int* __restrict__ redo, int* __restrict__ redo_count, int prio) {
+             int* __restrict__ overflow, int* __restrict__ redo, int* __restrict__ redo_count, int prio,
+             const int* __restrict__ n_dev) {
     // the extension finishes chunks the SAM writer waits for: its waves may claim the
     // SIMDs they share with the seeding kernels first (s_setprio, RSA_EXT_SETPRIO)
     if (prio) __builtin_amdgcn_s_setprio(2);
+    if (n_dev) n_jobs = min(n_jobs, *n_dev);      // the in-stream redo pass: the device's count
     __shared__ __attribute__((aligned(16))) int8_t s_dir[B16_GROUPS][DirCells<DIRCAP>::BYTES];
     __shared__ uint8_t s_qc[B16_GROUPS][B16_SEGCAP];
     __shared__ uint8_t s_rc[B16_GROUPS][B16_SEGCAP];
@@ -1248,8 +1254,9 @@ void launch_shared_check(int nl, hipStream_t st, const ExtJobDev* jobs, const ui
 
 // host-side launcher: RMAX from the longest query of the batch
 void launch_ext_scan(int rmax, dim3 grid, dim3 block, hipStream_t st, const ExtJobDev* jobs, int n, const int* idx,
-                     const char* q, const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE) {
-#define RSA_L(RM) hipLaunchKernelGGL((k_ext_scan<RM>), grid, block, 0, st, jobs, n, idx, q, ref, out, match, mismatch, gO, gE)
+                     const char* q, const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE,
+                     const int* n_dev) {
+#define RSA_L(RM) hipLaunchKernelGGL((k_ext_scan<RM>), grid, block, 0, st, jobs, n, idx, q, ref, out, match, mismatch, gO, gE, n_dev)
     if (rmax <= 2) RSA_L(2); else if (rmax <= 4) RSA_L(4); else if (rmax <= 8) RSA_L(8); else RSA_L(16);
 #undef RSA_L
 }
@@ -1257,10 +1264,10 @@ void launch_ext_scan(int rmax, dim3 grid, dim3 block, hipStream_t st, const ExtJ
 void launch_ext_band16(int dircap, dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n,
                        const int* idx, const char* q, const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out,
                        int match, int mismatch, int gO, int gE, int bonus, int* queue, int* qcount, int* overflow,
-                       int* redo, int* redo_count, int prio) {
+                       int* redo, int* redo_count, int prio, const int* n_dev) {
 #define RSA_B16(DC)                                                                                                \
     hipLaunchKernelGGL(k_ext_band16<DC>, grid, dim3(64), 0, st, jobs, scan, n, idx, q, ref, cig, raw, out, match, \
-                       mismatch, gO, gE, bonus, queue, qcount, overflow, redo, redo_count, prio)
+                       mismatch, gO, gE, bonus, queue, qcount, overflow, redo, redo_count, prio, n_dev)
     if (dircap >= 12288) RSA_B16(12288);
     else if (dircap >= 8192) RSA_B16(8192);
     else RSA_B16(4096);

@@ -22,7 +22,7 @@
 #include "rsa_timer.h"
 
 void launch_ext_scan(int rmax, dim3 grid, dim3 block, hipStream_t st, const ExtJobDev* jobs, int n, const int* idx,
-                     const char* q, const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE);
+                     const char* q, const char* ref, ScanRes* out, int match, int mismatch, int gO, int gE, const int* n_dev = nullptr);
 int scan_g_rows(uint32_t qlen);
 void scan_g_classes(int* rows5);
 int scan_g_max_ref();
@@ -37,7 +37,7 @@ __global__ void k_ext_band_panel(const ExtJobDev* jobs, const ScanRes* scan, int
 void launch_ext_band16(int dircap, dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, int n, const int* idx,
                        const char* q, const char* ref, uint32_t* cig, uint32_t* raw, rsa_aln* out, int match,
                        int mismatch, int gO, int gE, int bonus, int* queue, int* qcount, int* overflow, int* redo,
-                       int* redo_count, int prio);
+                       int* redo_count, int prio, const int* n_dev = nullptr);
 void launch_shared_check(int nl, hipStream_t st, const ExtJobDev* jobs, const uint32_t* list, const char* q,
                          const char* ref, uint8_t* res);
 void launch_ext_band64(dim3 grid, hipStream_t st, const ExtJobDev* jobs, const ScanRes* scan, const char* q,
@@ -471,12 +471,28 @@ static int64_t band_stride(int64_t dir_cap) {
 }
 
 struct ExtStatus {            // device-side counters of one rsa_extend call
-    int qcount;               // jobs deferred by k_ext_band16
-    int ocount;               // jobs k_ext_band64 could not hold
+    int qcount;               // jobs deferred by k_ext_band16 (of the last band pass)
+    int ocount;               // jobs k_ext_band64 could not hold (every pass)
     uint64_t total;           // dense CIGAR ops (k_cigar_compact)
     int rcount;               // jobs listed in d_redo (certificate not met)
     int err;                  // k_ext_scan_v found an alignment end outside its job (a defect)
+    int qcount1;              // jobs deferred by the first band pass (the in-stream redo pass runs after it)
+    int pad_;
 };
+
+// The jobs whose word result the band kernels could not certify (d_redo) are re-run in the
+// same stream, before the results are compacted and copied (RSA_REDO_DEV, default on): the
+// exact two-layout scan and the band kernels over the device's own list, on a grid for up to
+// REDO_DEV_CAP jobs (an empty list costs three near-empty launches).  About two calls in
+// three list a job (444 of 7.3 M jobs at 2 x 150 bp); without this every such call waited for
+// the first results, launched the pass from the host and copied everything again.  A list
+// longer than the cap takes the host path (ext_finish).  RSA_REDO_DEV=<cap> (tests: 0 = the
+// host path only, 1 = a cap the redo tests exceed).
+static const int REDO_DEV_CAP = 128;
+static int redo_dev_cap() {
+    const char* e = getenv("RSA_REDO_DEV");
+    return e ? std::max(0, atoi(e)) : REDO_DEV_CAP;
+}
 
 // byte offsets of the scan order and the status in the staged job upload of n jobs
 // one staged upload per call: [ExtJobDev x n | scan order x n | ExtJobDev x n in scan order | ExtStatus]
@@ -498,6 +514,7 @@ struct rsa_pending {
     uint64_t guess = 0, cells = 0, qr_bytes = 0;
     int rmax = 1;                      // k_ext_scan's rows-per-lane bound for this call's jobs
     int band16_dircap = 4096;          // k_ext_band16's direction capacity for this call's queries
+    int redo_dev = 0;                  // jobs the in-stream redo pass covers (0: none enqueued)
     uint32_t n_shared = 0;             // jobs with RSA_JOB_SHARED_CHECK (k_shared_check's list)
     ExtStatus* d_status = nullptr;     // in the lane's staged upload
 };
@@ -710,6 +727,29 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
                       &dst->ocount, L->d_redo.as<int>(), &dst->rcount);
     HIPCHK(hipGetLastError());
     L->kt.end(st);
+    P.redo_dev = (int)std::min<uint32_t>(n, (uint32_t)redo_dev_cap());
+    if (P.redo_dev > 0) {
+        const int cap = P.redo_dev;
+        const int* d_redo = L->d_redo.as<int>();
+        HIPCHK(hipMemcpyAsync(&dst->qcount1, &dst->qcount, sizeof(int), hipMemcpyDeviceToDevice, st));
+        HIPCHK(hipMemsetAsync(&dst->qcount, 0, sizeof(int), st));          // k_ext_band64's queue restarts
+        launch_ext_scan(P.rmax, dim3((cap + 3) / 4), dim3(256), st, L->d_jobs.as<ExtJobDev>(), cap, d_redo,
+                        L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(), jb->match, jb->mismatch,
+                        jb->gap_open, jb->gap_extend, &dst->rcount);
+        HIPCHK(hipGetLastError());
+        launch_ext_band16(P.band16_dircap, dim3((cap + 3) / 4), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(),
+                          cap, d_redo, L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(),
+                          L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open, jb->gap_extend,
+                          jb->end_bonus, L->d_queue.as<int>(), &dst->qcount, L->d_over.as<int>(), nullptr, nullptr,
+                          ext_setprio(), &dst->rcount);
+        HIPCHK(hipGetLastError());
+        launch_ext_band64(dim3(std::min(cap, band64_grid(ctx))), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(),
+                          L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(),
+                          L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open, jb->gap_extend,
+                          jb->end_bonus, L->d_queue.as<int>(), &dst->qcount, L->d_over.as<int>(), &dst->ocount,
+                          nullptr, nullptr);
+        HIPCHK(hipGetLastError());
+    }
     if (P.n_shared) {   // rescue_mate_part's has_shared_substring for the jobs that asked (aln.cpp:1058)
         HIPCHK(L->h_shl.ensure(sizeof(uint32_t) * shl.size()));
         memcpy(L->h_shl.p, shl.data(), sizeof(uint32_t) * shl.size());
@@ -783,12 +823,16 @@ static int ext_finish(rsa_pending& P) {
     if (hs.err) { set_err(ctx, "rsa_extend: k_ext_scan_v produced an alignment end outside its job"); return RSA_ERR_INTERNAL; }
     if (hs.ocount > 0)
         if (int rc = ext_panel(P, hs)) return rc;
-    const int redo = hs.rcount;
-    uint64_t deferred = (uint64_t)hs.qcount, overflowed = (uint64_t)hs.ocount;
+    int redo = hs.rcount;
+    // the first band pass's deferrals (before the in-stream redo pass reset the queue)
+    const int q1 = P.redo_dev > 0 ? hs.qcount1 : hs.qcount;
+    uint64_t deferred = (uint64_t)q1 + (P.redo_dev > 0 ? (uint64_t)hs.qcount : 0), overflowed = (uint64_t)hs.ocount;
     {   // the next calls' k_ext_band64 grid (band64_grid)
         const int prev = ctx->band64_recent.load(std::memory_order_relaxed);
-        ctx->band64_recent.store(std::max(hs.qcount, prev - prev / 4), std::memory_order_relaxed);
+        ctx->band64_recent.store(std::max(q1, prev - prev / 4), std::memory_order_relaxed);
     }
+    const int redo_total = redo;
+    if (redo > 0 && redo <= P.redo_dev) redo = 0;     // done in the stream already
     if (redo > 0) {
         // the listed jobs' path had an insertion next to a deletion (or no path): the
         // byte layout may score them differently, so they take the exact two-layout
@@ -859,7 +903,7 @@ static int ext_finish(rsa_pending& P) {
         ctx->stats.band_deferred += deferred;
         ctx->stats.band_overflow += overflowed;
         ctx->stats.scan_certified += certified;
-        ctx->stats.scan_redo += (uint64_t)redo;
+        ctx->stats.scan_redo += (uint64_t)redo_total;
         ctx->stats.shared_checks += P.n_shared;
         ctx->stats.no_shared += no_shared;
     }

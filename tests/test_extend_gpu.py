@@ -320,11 +320,16 @@ def _block_replacement_jobs(rng, ref, offs, n, L=250):
 
 
 @pytest.mark.gpu
-def test_extend_scan_certificate_and_redo(ctx):
+@pytest.mark.parametrize("redo_dev", [None, "0", "1"], ids=["in_stream", "host", "cap_exceeded"])
+def test_extend_scan_certificate_and_redo(ctx, redo_dev, monkeypatch):
     """k_ext_scan_v takes the word layout on the word score alone and the band path
     certifies it; jobs whose path puts an insertion next to a deletion are re-run
     through the two-layout scan.  Both outcomes occur here and every result is
-    Aligner::align's."""
+    Aligner::align's -- with the re-run in the call's stream (default), from the host
+    (RSA_REDO_DEV=0), and from the host after an in-stream pass whose cap the list
+    exceeds (RSA_REDO_DEV=1)."""
+    if redo_dev is not None:
+        monkeypatch.setenv("RSA_REDO_DEV", redo_dev)
     c, ref, offs = ctx
     rng = np.random.default_rng(31)
     queries, jobs, pairs = _block_replacement_jobs(rng, ref, offs, 1500)
@@ -344,7 +349,7 @@ def test_extend_scan_certificate_and_redo(ctx):
             bad.append((i, o, got))
     assert not bad, f"{len(bad)} mismatches, first: {bad[0]}"
     st = c.stats()
-    assert st["scan_certified"] > 1000 and st["scan_redo"] > 0, st
+    assert st["scan_certified"] > 1000 and st["scan_redo"] > 1, st
 
 
 @pytest.mark.gpu
