@@ -228,6 +228,8 @@ KERNEL_LIMITER = {
                  "of equal keys on one lane per orientation",
     "randstrobes": "one lane per read (reads over 512 bp only)",
     "rescue": "latency, rescued reads only",
+    "ext_redo": "latency: the jobs (about one a call) whose word result the band path could not certify, "
+                "re-run through the two-layout scan (one wave a job) and the band kernels in the call's stream",
 }
 
 

@@ -334,7 +334,8 @@ enum {
     RSA_K_EXT_BAND_WIDE = 7, /* the same, 64 lanes/job, for the jobs the 16-lane kernel queues */
     RSA_K_EXT_BAND_PANEL = 8, /* the same, one wave per job sweeping 64-cell panels (bands > 64 cells) */
     RSA_K_SITES = 9,       /* per-NAM orientation + Hamming site checks (aln.cpp:60-93, 374-431) */
-    RSA_K_COUNT = 10
+    RSA_K_EXT_REDO = 10,   /* the re-run of uncertified scan results: two-layout scan + band kernels */
+    RSA_K_COUNT = 11
 };
 
 typedef struct rsa_kernel_stats {

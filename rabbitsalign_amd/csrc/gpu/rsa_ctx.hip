@@ -733,6 +733,7 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
         const int* d_redo = L->d_redo.as<int>();
         HIPCHK(hipMemcpyAsync(&dst->qcount1, &dst->qcount, sizeof(int), hipMemcpyDeviceToDevice, st));
         HIPCHK(hipMemsetAsync(&dst->qcount, 0, sizeof(int), st));          // k_ext_band64's queue restarts
+        L->kt.begin(st, RSA_K_EXT_REDO);
         launch_ext_scan(P.rmax, dim3((cap + 3) / 4), dim3(256), st, L->d_jobs.as<ExtJobDev>(), cap, d_redo,
                         L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(), jb->match, jb->mismatch,
                         jb->gap_open, jb->gap_extend, &dst->rcount);
@@ -749,6 +750,7 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
                           jb->end_bonus, L->d_queue.as<int>(), &dst->qcount, L->d_over.as<int>(), &dst->ocount,
                           nullptr, nullptr);
         HIPCHK(hipGetLastError());
+        L->kt.end(st);
     }
     if (P.n_shared) {   // rescue_mate_part's has_shared_substring for the jobs that asked (aln.cpp:1058)
         HIPCHK(L->h_shl.ensure(sizeof(uint32_t) * shl.size()));
@@ -839,22 +841,18 @@ static int ext_finish(rsa_pending& P) {
         // scan (k_ext_scan: SSW's byte-then-word decision) and the band kernels again
         if (redo > (int)n) { set_err(ctx, "rsa_extend: redo list overflow"); return RSA_ERR_INTERNAL; }
         const int* d_redo = L->d_redo.as<int>();
-        L->kt.begin(st, RSA_K_EXT_SCAN);
+        L->kt.begin(st, RSA_K_EXT_REDO);
         launch_ext_scan(P.rmax, dim3((redo + 3) / 4), dim3(256), st, L->d_jobs.as<ExtJobDev>(), redo, d_redo,
                         L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(), P.match, P.mismatch, P.gap_open,
                         P.gap_extend);
         HIPCHK(hipGetLastError());
-        L->kt.end(st);
         HIPCHK(hipMemsetAsync(&P.d_status->qcount, 0, 2 * sizeof(int), st));    // qcount, ocount
-        L->kt.begin(st, RSA_K_EXT_BAND);
         launch_ext_band16(P.band16_dircap, dim3((redo + 3) / 4), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(), redo, d_redo,
                           L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(),
                           L->d_alns.as<rsa_aln>(), P.match, P.mismatch, P.gap_open, P.gap_extend, P.end_bonus,
                           L->d_queue.as<int>(), &P.d_status->qcount, L->d_over.as<int>(), nullptr, nullptr,
                           ext_setprio());
         HIPCHK(hipGetLastError());
-        L->kt.end(st);
-        L->kt.begin(st, RSA_K_EXT_BAND_WIDE);
         launch_ext_band64(dim3(std::min(redo, band64_grid(ctx))), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(),
                           L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(),
                           L->d_alns.as<rsa_aln>(), P.match, P.mismatch, P.gap_open, P.gap_extend, P.end_bonus,

@@ -85,15 +85,15 @@ class AlnBatch(C.Structure):
 
 
 KERNELS = ["randstrobes", "lookup", "find_nams", "rescue", "compact", "ext_scan", "ext_band", "ext_band_wide",
-           "ext_band_panel", "sites"]
+           "ext_band_panel", "sites", "ext_redo"]
 # the extension scan is k_ext_scan_v unless RSA_SCAN_V=0 selects the two-layout k_ext_scan_g (rsa_ctx.hip)
 SCAN_SYMBOL = "k_ext_scan_g" if os.environ.get("RSA_SCAN_V", "1")[:1] == "0" else "k_ext_scan_v"
 KERNEL_SYMBOLS = {"randstrobes": "k_randstrobes", "lookup": "k_seed_query", "find_nams": "k_find_nams_w2",
                   "rescue": "k_rescue_w", "compact": "k_compact", "ext_scan": SCAN_SYMBOL, "ext_band": "k_ext_band16",
                   "ext_band_wide": "k_ext_band64", "ext_band_panel": "k_ext_band_panel",
-                  "sites": "k_sites"}
+                  "sites": "k_sites", "ext_redo": "k_ext_scan"}
 NK = len(KERNELS)
-EXT_KERNELS = ("ext_scan", "ext_band", "ext_band_wide", "ext_band_panel")   # launched by rsa_extend
+EXT_KERNELS = ("ext_scan", "ext_band", "ext_band_wide", "ext_band_panel", "ext_redo")   # launched by rsa_extend
 
 
 class KernelStats(C.Structure):
