@@ -626,18 +626,23 @@ __device__ __forceinline__ void aln_sentinel(rsa_aln* out, int j, const ExtJobDe
 
 // The direction matrix keeps the reference's byte layout for addressing (cell c of
 // band row i at byte 3 (width_d i + c), bytes [de, df, dh], SET_D in ssw.c), but LDS holds
-// one byte per cell: the band fill always writes a cell's three bytes together, so a
+// one code per cell: the band fill always writes a cell's three bytes together, so a
 // packed cell decodes to exactly the bytes the reference layout would hold there (an
-// unwritten cell, 0, to three zeros).  A third of the LDS lets k_ext_band16 keep three
-// times as many jobs resident.  Packed byte: bit 0 de - 2, bit 1 df - 4, bits 2-3 dh as
-// 1 (1), de (2), df (3).
-__device__ __forceinline__ int8_t dir_pack(int de, int df, int dh) {
+// unwritten cell, 0, to three zeros; a cell a wider band pass left behind to what that
+// pass wrote).  Code: bit 0 de - 2, bit 1 df - 4, bits 2-3 dh as 1 (1), de (2), df (3) --
+// never 0 for a written cell, and 4 bits wide.  NIB = false: one byte a cell (a third
+// of the reference's bytes); NIB = true: a nibble a cell, two cells a byte in the
+// reference's cell order (cell c in byte c / 2, low nibble for even c), a sixth.  The
+// nibbles cost a lane-pair merge per row; k_ext_band16 takes them where LDS sets its
+// occupancy (the 8192 / 16384 classes: 5 instead of 2-3 waves a SIMD at 250 bp).
+__device__ __forceinline__ int dir_pack(int de, int df, int dh) {
     const int dhc = dh == 1 ? 1 : (dh == de ? 2 : 3);
-    return (int8_t)((de - 2) | ((df - 4) << 1) | (dhc << 2));
+    return (de - 2) | ((df - 4) << 1) | (dhc << 2);
 }
 // byte `sub` (0..2) of cell `cell`, i.e. reference byte 3 cell + sub
+template <bool NIB>
 __device__ __forceinline__ int dir_byte(const int8_t* dirp, int cell, int sub) {
-    const int v = (int)(uint8_t)dirp[cell];
+    const int v = NIB ? ((int)(uint8_t)dirp[cell >> 1] >> ((cell & 1) * 4)) & 15 : (int)(uint8_t)dirp[cell];
     if (v == 0) return 0;
     const int de = 2 + (v & 1), df = 4 + ((v >> 1) & 1), dhc = (v >> 2) & 3;
     return sub == 0 ? de : (sub == 1 ? df : (dhc == 1 ? 1 : (dhc == 2 ? de : df)));
@@ -660,15 +665,18 @@ __device__ __forceinline__ bool cert_check(const ScanRes& sr, int j, const uint3
     return !bad;
 }
 
-template <int DIRCAP> struct DirCells { static constexpr int BYTES = ((DIRCAP + 2) / 3 + 15) & ~15; };
+template <int DIRCAP, bool NIB> struct DirCells {
+    static constexpr int CELLS = (DIRCAP + 2) / 3;
+    static constexpr int BYTES = ((NIB ? (CELLS + 1) / 2 : CELLS) + 15) & ~15;
+};
 
 // banded_sw + traceback + ext_finish of job j by a group of G lanes (z = lane in
 // group).  LDS: dir[DIRCAP], qc[QCAP], rc[RCAP].  Returns false when the job does
 // not fit the group (nothing written).  Lane z keeps the reference's h_b[z+1] and
 // e_b[z+1] in registers; its reads of h_b[e], e_b[e] and h_b[e-1] are DPP shifts
 // (index 0 and indices past the group are always 0), so the row loop has no LDS
-// round trip and no barrier.
-template <int G, int DIRCAP, int QCAP, int RCAP>
+// round trip and no barrier.  NIB: the direction cells' packing (dir_byte).
+template <int G, int DIRCAP, int QCAP, int RCAP, bool NIB>
 __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr, const char* __restrict__ qbuf,
                            const char* __restrict__ ref, uint32_t* __restrict__ cig_pool,
                            uint32_t* __restrict__ raw_pool, rsa_aln* __restrict__ out, int match, int mismatch,
@@ -692,7 +700,7 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
         const int gj = ref_begin + x;
         rc[x] = (uint8_t)((gj >= 0 && gj < rlen) ? ssw_code((unsigned char)r[gj]) : 4);
     }
-    for (int x = z * 16; x < DirCells<DIRCAP>::BYTES; x += G * 16) *(int4*)(dir + x) = make_int4(0, 0, 0, 0);
+    for (int x = z * 16; x < DirCells<DIRCAP, NIB>::BYTES; x += G * 16) *(int4*)(dir + x) = make_int4(0, 0, 0, 0);
     WSYNC();
 
     const int len = ref_l > read_l ? ref_l : read_l;
@@ -712,6 +720,16 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
             const int edge = end + 1 < width - 1 ? end + 1 : width - 1;
             const int jj = beg + z;
             const bool on = jj <= end;
+            // Row i's cells are one run of nibbles from cell width_d i; lane pairs (even
+            // cell, odd cell) of the row write whole bytes.  The row's first byte when its
+            // cell is odd, and its last when its cell is even, hold a nibble of another row
+            // or of a cell this pass leaves alone: those two lanes merge into the byte in
+            // LDS, read here, well before the store, so the wait is hidden by the row's work.
+            const int cell = width_d * i + z;
+            const bool odd = NIB && (cell & 1);
+            const bool merge = NIB && on && (odd ? z == 0 : jj == end);
+            int held = 0;
+            if (merge) held = (int)(uint8_t)dir[cell >> 1];
             const int sh = i - bw >= 1 ? 1 : 0;
             const bool clr = z == edge - 1;
             HB = clr ? 0 : HB;
@@ -739,8 +757,16 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
             const int m = e1 > f1 ? e1 : f1;
             const int H = m > diag ? m : diag;
             const int dh = m <= diag ? 1 : (e1 > f1 ? de : df);
-            if (on) {
-                dir[width_d * i + z] = dir_pack(de, df, dh);
+            const int code = on ? dir_pack(de, df, dh) : 0;
+            if constexpr (NIB) {
+                const int code_up = gshl1z<G>(code);    // the odd cell after an even one
+                if (on && (!odd || z == 0)) {
+                    const int b = odd ? ((held & 0x0f) | (code << 4))
+                                      : (merge ? ((held & 0xf0) | code) : (code | (code_up << 4)));
+                    dir[cell >> 1] = (int8_t)b;
+                }
+            } else if (on) {
+                dir[cell] = (int8_t)code;
             }
             lmax = (on && H > lmax) ? H : lmax;
             EB = on ? E : EB;                            // h_b[1..u] = h_c[1..u]
@@ -792,7 +818,7 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
                 const int ik = i - k, jk = jx - k;
                 const int ck = lineC - k * width_d + (jk - max(ik - bw, 0));
                 const int atk = 3 * ck + 2;
-                dvs[k] = (ik >= 0 && jk > 0 && atk >= 0 && atk < s2) ? dir_byte(dir, ck, 2) : 0;
+                dvs[k] = (ik >= 0 && jk > 0 && atk >= 0 && atk < s2) ? dir_byte<NIB>(dir, ck, 2) : 0;
             }
             bool more = true;
 #pragma unroll
@@ -809,7 +835,7 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
         const int cell = lineC + (jx - max(i - bw, 0));
         const int at = 3 * cell + temp2;                   // = line + (jx - max(i - bw, 0)) * 3 + temp2
         if (at < 0 || at >= s2) { fail = true; break; }
-        if (!step(dir_byte(dir, cell, temp2))) { fail = true; break; }
+        if (!step(dir_byte<NIB>(dir, cell, temp2))) { fail = true; break; }
     }
     if (fail) {                                     // banded_sw failed -> flag 1 sentinel
         aln_sentinel(out, j, jb, -100000);
@@ -829,11 +855,14 @@ __device__ bool band_group(int j, int z, const ExtJobDev& jb, const ScanRes& sr,
 #define B16_GROUPS 4
 #define B16_SEGCAP 320
 
-// DIRCAP: direction bytes of one job in the reference's 3-a-cell count (one byte a cell
-// here).  4096 holds the bands of 150-bp reads up to 9 cells wide (deferral 0.04 % on
-// the headline); for 250-bp reads only 5 cells, which sent 15 % of the PE 2x250 jobs to
-// the one-wave kernel.  8192 (chosen for batches with queries over 200 bp) holds 9 cells
-// at 250 bp for 1.6x the LDS a wave (13.5 KB: 11 waves a CU instead of 20).
+// DIRCAP: direction bytes of one job in the reference's 3-a-cell count.  4096 holds the
+// bands of 150-bp reads up to 9 cells wide (deferral 0.04 % on the headline) in a byte a
+// cell (8 KB of LDS a wave, 5 waves a SIMD); for 250-bp reads only 5 cells, which sent
+// 15 % of the PE 2x250 jobs to the one-wave kernel.  8192 (chosen for batches with
+// queries over 200 bp) holds 9 cells at 250 bp; with a byte a cell it took 13.5 KB a wave
+// (2-3 waves a SIMD), with a nibble a cell 7.9 KB (5 waves).  16384 holds every band a
+// 16-lane group can (15 cells at 250 bp) in 13.2 KB.
+#define B16_NIB (DIRCAP > 4096)
 template <int DIRCAP>
 __global__ void __launch_bounds__(64)
 k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ scan, int n_jobs,
@@ -846,7 +875,7 @@ k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
     // SIMDs they share with the seeding kernels first (s_setprio, RSA_EXT_SETPRIO)
     if (prio) __builtin_amdgcn_s_setprio(2);
     if (n_dev) n_jobs = min(n_jobs, *n_dev);      // the in-stream redo pass: the device's count
-    __shared__ __attribute__((aligned(16))) int8_t s_dir[B16_GROUPS][DirCells<DIRCAP>::BYTES];
+    __shared__ __attribute__((aligned(16))) int8_t s_dir[B16_GROUPS][DirCells<DIRCAP, B16_NIB>::BYTES];
     __shared__ uint8_t s_qc[B16_GROUPS][B16_SEGCAP];
     __shared__ uint8_t s_rc[B16_GROUPS][B16_SEGCAP];
     const int lane = threadIdx.x & 63, g = lane >> 4, z = lane & 15;
@@ -867,7 +896,7 @@ k_ext_band16(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
         }
         return;
     }
-    const bool done = band_group<16, DIRCAP, B16_SEGCAP, B16_SEGCAP>(
+    const bool done = band_group<16, DIRCAP, B16_SEGCAP, B16_SEGCAP, B16_NIB>(
         j, z, jb, sr, qbuf, ref, cig_pool, raw_pool, out, match, mismatch, gO, gE, bonus, s_dir[g], s_qc[g], s_rc[g],
         redo, redo_count);
     if (!done && z == 0) {
@@ -891,7 +920,7 @@ k_ext_band64(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
              rsa_aln* __restrict__ out, int match, int mismatch, int gO, int gE, int bonus,
              const int* __restrict__ queue, const int* __restrict__ qcount, int* __restrict__ overflow,
              int* __restrict__ ocount, int* __restrict__ redo, int* __restrict__ redo_count) {
-    __shared__ __attribute__((aligned(16))) int8_t s_dir[DirCells<B64_DIRCAP>::BYTES];
+    __shared__ __attribute__((aligned(16))) int8_t s_dir[DirCells<B64_DIRCAP, false>::BYTES];
     __shared__ uint8_t s_qc[B64_QCAP];
     __shared__ uint8_t s_rc[B64_RCAP];
     const int z = threadIdx.x & 63;
@@ -900,7 +929,7 @@ k_ext_band64(const ExtJobDev* __restrict__ jobs, const ScanRes* __restrict__ sca
         const int j = queue[t];
         const ExtJobDev jb = jobs[j];
         const ScanRes sr = scan[j];
-        const bool done = band_group<64, B64_DIRCAP, B64_QCAP, B64_RCAP>(
+        const bool done = band_group<64, B64_DIRCAP, B64_QCAP, B64_RCAP, false>(
             j, z, jb, sr, qbuf, ref, cig_pool, raw_pool, out, match, mismatch, gO, gE, bonus, s_dir, s_qc, s_rc,
             redo, redo_count);
         if (!done && z == 0) { overflow[j] = 1; atomicAdd(ocount, 1); }
@@ -1268,7 +1297,7 @@ void launch_ext_band16(int dircap, dim3 grid, hipStream_t st, const ExtJobDev* j
 #define RSA_B16(DC)                                                                                                \
     hipLaunchKernelGGL(k_ext_band16<DC>, grid, dim3(64), 0, st, jobs, scan, n, idx, q, ref, cig, raw, out, match, \
                        mismatch, gO, gE, bonus, queue, qcount, overflow, redo, redo_count, prio, n_dev)
-    if (dircap >= 12288) RSA_B16(12288);
+    if (dircap >= 16384) RSA_B16(16384);
     else if (dircap >= 8192) RSA_B16(8192);
     else RSA_B16(4096);
 #undef RSA_B16

@@ -443,7 +443,7 @@ uint64_t rsa_extend_cigar_bound(const rsa_job_batch* jb) {
 static const int64_t BIG_DIR_CAP = 16ll << 20;
 static const int BIG_CHUNK = 32;
 // k_ext_band16's direction capacity for a call whose longest query (windows <= 2 kb) is
-// qmax: 8192 above 200 bp (see k_ext_band16); RSA_BAND16_DIRCAP=4096/8192/12288 fixes it
+// qmax: 8192 above 200 bp (see k_ext_band16); RSA_BAND16_DIRCAP=4096/8192/16384 fixes it
 static int band16_dircap(uint32_t qmax) {
     const char* v = getenv("RSA_BAND16_DIRCAP");   // per call: the tests switch it
     const int forced = v ? atoi(v) : 0;

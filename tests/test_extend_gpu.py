@@ -83,19 +83,19 @@ def test_extend_band_paths_exercised(ctx):
 
 @pytest.mark.gpu
 def test_extend_band16_capacity_classes(ctx, monkeypatch):
-    """k_ext_band16 comes in three direction capacities (4096 / 8192 / 12288; a call
+    """k_ext_band16 comes in three direction capacities (4096 / 8192 / 16384; a call
     with queries over 200 bp takes 8192).  250-bp jobs with indels (bands of 3-15 cells)
     give the oracle's results in each, and a larger capacity defers fewer jobs to the
     one-wave kernel."""
     c, ref, offs = ctx
     deferred = {}
-    for cap in ("4096", "8192", "12288"):
+    for cap in ("4096", "8192", "16384"):
         monkeypatch.setenv("RSA_BAND16_DIRCAP", cap)
         c.reset_stats()
         bad = _compare(c, ref, offs, 11, 2500, qlens=(250, 240, 300))
         assert not bad, f"RSA_BAND16_DIRCAP={cap}: {len(bad)} mismatches, first: {bad[0]}"
         deferred[cap] = c.stats()["band_deferred"]
-    assert deferred["4096"] > deferred["8192"] >= deferred["12288"], deferred
+    assert deferred["4096"] > deferred["8192"] >= deferred["16384"], deferred
 
 
 def _has_shared_substring(q: bytes, w: bytes, k: int) -> bool:
