@@ -26,7 +26,11 @@ def symbolise(maps, pcs):
             bylib["?"].append((pc, pc))
     sym = {}
     for name, v in bylib.items():
-        lib = name.replace("/tmp/code/RabbitBio__RabbitSAlign/repo", os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        lib = name
+        for part in ("/rabbitsalign_amd/", "/oracle/"):     # the box's copy of this tree -> here
+            if part in name and not os.path.exists(name):
+                lib = root + part + name.split(part, 1)[1]
         if not os.path.exists(lib):
             for pc, _ in v:
                 sym[pc] = f"[{os.path.basename(name)}]"
