@@ -823,6 +823,9 @@ static int ext_finish(rsa_pending& P) {
     HIPCHK(stream_wait(st, L->sb.done));
     ExtStatus hs = *L->h_status.as<ExtStatus>();
     if (hs.err) { set_err(ctx, "rsa_extend: k_ext_scan_v produced an alignment end outside its job"); return RSA_ERR_INTERNAL; }
+    // the jobs listed before the panel pass: the in-stream redo pass covered them when
+    // there were at most P.redo_dev; the panel pass below may list more, which it did not
+    const int listed_in_stream = hs.rcount;
     if (hs.ocount > 0)
         if (int rc = ext_panel(P, hs)) return rc;
     int redo = hs.rcount;
@@ -834,7 +837,7 @@ static int ext_finish(rsa_pending& P) {
         ctx->band64_recent.store(std::max(q1, prev - prev / 4), std::memory_order_relaxed);
     }
     const int redo_total = redo;
-    if (redo > 0 && redo <= P.redo_dev) redo = 0;     // done in the stream already
+    if (redo > 0 && redo == listed_in_stream && redo <= P.redo_dev) redo = 0;     // done in the stream already
     if (redo > 0) {
         // the listed jobs' path had an insertion next to a deletion (or no path): the
         // byte layout may score them differently, so they take the exact two-layout

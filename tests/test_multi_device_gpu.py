@@ -10,18 +10,32 @@ from helpers import ROOT
 REF_LIB = os.path.join(ROOT, "oracle", "_ref", "librsalign_ref.so")
 
 
+def _first_diffs(d, k=4):
+    """the first k differing SAM body lines of one.sam / multi.sam (the failure message)"""
+    with open(d / "one.sam", "rb") as f1, open(d / "multi.sam", "rb") as f2:
+        x = [ln for ln in f1 if not ln.startswith(b"@")]
+        y = [ln for ln in f2 if not ln.startswith(b"@")]
+    out = [f"{len(x)} / {len(y)} lines"]
+    for i, (p, q) in enumerate(zip(x, y)):
+        if p != q:
+            out.append(f"line {i}:\n one   {p[:300]!r}\n multi {q[:300]!r}")
+            if len(out) > k:
+                break
+    return "\n".join(out)
+
+
 @pytest.mark.gpu
-def test_add_devices_same_sam():
+def test_add_devices_same_sam(tmp_path):
     import torch  # noqa: F401
     from rabbitsalign_amd import mapper as M
     m = M.Mapper.synthetic(3, 20_000_000, 4, 150, device=0, threads=8)
     try:
         reads = m.synthetic_reads(9, 0, 40_000, 150, 300.0, 30.0, True)
-        a = m.map(reads, threads=8)
+        a = m.map(reads, threads=8, sam_path=tmp_path / "one.sam")
         m.add_devices([0])
         m.reset_kernel_stats()
-        b = m.map(reads, threads=8)
-        assert (a.sam_hash, a.sam_bytes) == (b.sam_hash, b.sam_bytes)
+        b = m.map(reads, threads=8, sam_path=tmp_path / "multi.sam")
+        assert (a.sam_hash, a.sam_bytes) == (b.sam_hash, b.sam_bytes), _first_diffs(tmp_path)
         assert m.engine.endswith("x2")
         assert m.kernel_stats()["kernels"]["ext_scan"]["launches"] > 0
         if os.path.exists(REF_LIB):
