@@ -149,6 +149,7 @@ struct OrderedSink {
     size_t queued_bytes = 0;
     double first_out = 0;                     // s after opening: the first text reached the writer
     size_t next = 0;
+    const size_t first;                       // the first chunk this sink writes
     uint64_t bytes = 0;
     SamDigest total;
     bool closing = false;
@@ -158,7 +159,8 @@ struct OrderedSink {
     FILE* trace = nullptr;
     Clock::time_point t_open = Clock::now();
     // `first`: the first chunk index this sink writes (a rank's part starts later)
-    OrderedSink(SamSink s, void* u, bool d, size_t first = 0) : sink(s), user(u), digest(d), next(first) {
+    OrderedSink(SamSink s, void* u, bool d, size_t first_ = 0)
+        : sink(s), user(u), digest(d), next(first_), first(first_) {
         static const char* trace_path = getenv("RSA_SINK_TRACE");
         if (sink && trace_path) trace = fopen(trace_path, "a");
         if (sink) writer = std::thread([this] { write_loop(); });
@@ -684,9 +686,12 @@ void pe_get_str(PeChunk& c, const MapContext& mc, float mu, float sigma, std::ve
 // last() runs on.  Measured (profiles/r06/ab_pieces.json, 16 alternating steps each):
 // pieces of 2000 pairs bring the first SAM text to the writer 3 ms earlier a step (10.8
 // against 14.0 ms) but the streamed rate falls from 19.7 to 18.7 Mreads/s
-static size_t sam_piece_pairs() {
+// RSA_SAM_PIECE_FIRST: the same for the run's first chunk only (the writer's first bytes wait
+// for it; the other chunks stay whole)
+static size_t sam_piece_pairs(bool first_chunk) {
     const char* e = getenv("RSA_SAM_PIECE");        // per chunk (A/B runs change it between calls)
-    return e ? (size_t)atol(e) : 0;
+    const char* f = first_chunk ? getenv("RSA_SAM_PIECE_FIRST") : nullptr;
+    return f ? (size_t)atol(f) : e ? (size_t)atol(e) : 0;
 }
 
 // the chunk's extension results start at infos[pos]; its SAM text goes to `os` in pieces
@@ -702,7 +707,8 @@ void pe_store_last(PeChunk& c, const MapContext& mc, const InsertSizeDistributio
         const Read read1(c.in.r1[i].seq, c.rc(i, 0)), read2(c.in.r2[i].seq, c.rc(i, 1));
         pos = store_results_pe(c.res[i], read1, read2, mc, isize.mu, isize.sigma, infos, pos);
     }
-    const size_t piece = sam_piece_pairs() ? sam_piece_pairs() : std::max<size_t>(n, 1);
+    const size_t pp = sam_piece_pairs(c.in.index == os.first);
+    const size_t piece = pp ? pp : std::max<size_t>(n, 1);
     double t_out = 0;
     for (size_t a = 0; a < n || a == 0; a += piece) {
         const size_t b = std::min(n, a + piece);
