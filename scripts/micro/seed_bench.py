@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--calls", type=int, default=30)
     ap.add_argument("--read-len", type=int, default=150)
     ap.add_argument("--out", default="")
+    ap.add_argument("--ab", default="", help="'VAR=a|VAR=b': settings alternated (--rounds times), per-setting means")
+    ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime: torch's)
     from rabbitsalign_amd import native
@@ -61,6 +63,24 @@ def main():
     batches = [batch(100 + i) for i in range(4)]
     for bt in batches[:2]:                                        # warm-up
         ctx.seed(bt, sites=True, order=native.NAMS_BY_SCORE, hamming=(2, 8, 10))
+    if a.ab:
+        sets = [dict(kv.split("=", 1) for kv in x.split(",")) for x in a.ab.split("|")]
+        acc = [dict() for _ in sets]
+        for _ in range(a.rounds):
+            for i, env in enumerate(sets):
+                os.environ.update(env)
+                ctx.reset_stats()
+                for c in range(a.calls):
+                    ctx.seed(batches[c % len(batches)], sites=True, order=native.NAMS_BY_SCORE, hamming=(2, 8, 10))
+                for k, v in ctx.stats()["kernels"].items():
+                    if v["launches"]:
+                        x = acc[i].setdefault(k, [0.0, 0])
+                        x[0] += v["ms"]; x[1] += v["launches"]
+        for env, kv in zip(sets, acc):
+            print(json.dumps({"env": env, "read_len": L, "us_per_launch":
+                              {k: round(1e3 * ms / n, 1) for k, (ms, n) in kv.items()}}), flush=True)
+        ctx.close()
+        return
     ctx.reset_stats()
     t = time.time()
     for c in range(a.calls):

@@ -37,7 +37,8 @@ def busy(db):
         rows = c.execute("select name, start, \"end\" from kernels order by start").fetchall()
     except sqlite3.Error:
         return None
-    seed = [r for r in rows if short(r[0]) in ("k_lookup", "k_seed_query")]
+    base = lambda n: short(n).split("<")[0].split()[-1]      # "void k_seed_query<256, 6>" -> k_seed_query
+    seed = [r for r in rows if base(r[0]) in ("k_lookup", "k_seed_query")]
     if not seed:
         return None
     lo, hi = seed[0][1], max(r[2] for r in seed)
