@@ -62,6 +62,22 @@ int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, 
 int seed_randstrobes_run(SeedBufs& b, hipStream_t st, const SeedIndexParams& p, const rsa_read_batch* rb,
                          rsa_randstrobe_batch* out, std::string& err);
 
+// RSA_SYNC_DEBUG=1 (debugging): wait for every extension launch and name the one that failed
+static bool sync_debug() {
+    static const bool on = getenv("RSA_SYNC_DEBUG") && getenv("RSA_SYNC_DEBUG")[0] == '1';
+    return on;
+}
+#define LAUNCHCHK(name, stream)                                                               \
+    do {                                                                                      \
+        HIPCHK(hipGetLastError());                                                            \
+        if (sync_debug()) {                                                                   \
+            const hipError_t s_ = hipStreamSynchronize(stream);                               \
+            if (s_ != hipSuccess) {                                                           \
+                set_err(ctx, std::string("after ") + (name) + ": " + hipGetErrorString(s_));  \
+                return RSA_ERR_HIP;                                                           \
+            }                                                                                 \
+        }                                                                                     \
+    } while (0)
 #define HIPCHK(x)                                                                   \
     do {                                                                            \
         hipError_t e_ = (x);                                                        \
@@ -527,7 +543,7 @@ static int ext_compact_copy(rsa_pending& P) {
     hipStream_t st = L->stream;
     launch_cigar_compact(st, L->d_alns.as<rsa_aln>(), L->d_alns_out.as<rsa_aln>(), (int)P.n, L->d_cig.as<uint32_t>(),
                          L->d_dense.as<uint32_t>(), L->d_bsum.as<uint64_t>(), &P.d_status->total);
-    HIPCHK(hipGetLastError());
+    LAUNCHCHK("compaction", st);
     HIPCHK(hipMemcpyAsync(L->h_status.p, P.d_status, sizeof(ExtStatus), hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(P.out->alns, L->d_alns_out.p, sizeof(rsa_aln) * P.n, hipMemcpyDeviceToHost, st));
     if (P.guess)
@@ -544,6 +560,11 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
     P.n = n;
     P.match = jb->match; P.mismatch = jb->mismatch; P.gap_open = jb->gap_open; P.gap_extend = jb->gap_extend;
     P.end_bonus = jb->end_bonus;
+    if (rsa_poison_every())                        // tests: nothing an earlier call wrote survives
+        for (DevBuf* b : {&L->d_q, &L->d_jobs, &L->d_scan, &L->d_alns, &L->d_alns_out, &L->d_cig, &L->d_dense, &L->d_raw,
+                          &L->d_scratch, &L->d_over, &L->d_queue, &L->d_idx, &L->d_bsum, &L->d_redo, &L->d_shl,
+                          &L->d_shres})
+            if (b->p) HIPCHK(hipMemsetAsync(b->p, 0xA5, b->cap, L->stream));
     // host job descriptors
     HIPCHK(L->h_jobs.ensure(stage_bytes(n)));
     ExtJobDev* hj = L->h_jobs.as<ExtJobDev>();
@@ -696,14 +717,14 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
                 launch_ext_scan_g(cls_rows[c], (int)cls_n[c], st, L->d_jobs.as<ExtJobDev>(), d_ord + off,
                                   L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(), jb->match, jb->mismatch,
                                   jb->gap_open, jb->gap_extend);
-            HIPCHK(hipGetLastError());
+            LAUNCHCHK("scan class", st);
             off += cls_n[c];
         }
         if (rest_n) {
             launch_ext_scan(rmax, dim3((rest_n + 3) / 4), dim3(256), st, L->d_jobs.as<ExtJobDev>(),
                             (int)rest_n, d_ord + off, L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(),
                             jb->match, jb->mismatch, jb->gap_open, jb->gap_extend);
-            HIPCHK(hipGetLastError());
+            LAUNCHCHK("scan rest", st);
         }
     }
     L->kt.end(st);
@@ -717,7 +738,7 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
                       L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open, jb->gap_extend, jb->end_bonus,
                       L->d_queue.as<int>(), &dst->qcount, L->d_over.as<int>(), L->d_redo.as<int>(), &dst->rcount,
                       ext_setprio());
-    HIPCHK(hipGetLastError());
+    LAUNCHCHK("band16", st);
     L->kt.end(st);
     L->kt.begin(st, RSA_K_EXT_BAND_WIDE);
     launch_ext_band64(dim3(std::min<uint32_t>(n, (uint32_t)band64_grid(ctx))), st, L->d_jobs.as<ExtJobDev>(),
@@ -725,7 +746,7 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
                       L->d_raw.as<uint32_t>(), L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open,
                       jb->gap_extend, jb->end_bonus, L->d_queue.as<int>(), &dst->qcount, L->d_over.as<int>(),
                       &dst->ocount, L->d_redo.as<int>(), &dst->rcount);
-    HIPCHK(hipGetLastError());
+    LAUNCHCHK("band64", st);
     L->kt.end(st);
     P.redo_dev = (int)std::min<uint32_t>(n, (uint32_t)redo_dev_cap());
     if (P.redo_dev > 0) {
@@ -737,19 +758,19 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
         launch_ext_scan(P.rmax, dim3((cap + 3) / 4), dim3(256), st, L->d_jobs.as<ExtJobDev>(), cap, d_redo,
                         L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(), jb->match, jb->mismatch,
                         jb->gap_open, jb->gap_extend, &dst->rcount);
-        HIPCHK(hipGetLastError());
+        LAUNCHCHK("redo scan", st);
         launch_ext_band16(P.band16_dircap, dim3((cap + 3) / 4), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(),
                           cap, d_redo, L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(),
                           L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open, jb->gap_extend,
                           jb->end_bonus, L->d_queue.as<int>(), &dst->qcount, L->d_over.as<int>(), nullptr, nullptr,
                           ext_setprio(), &dst->rcount);
-        HIPCHK(hipGetLastError());
+        LAUNCHCHK("redo band16", st);
         launch_ext_band64(dim3(std::min(cap, band64_grid(ctx))), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(),
                           L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(),
                           L->d_alns.as<rsa_aln>(), jb->match, jb->mismatch, jb->gap_open, jb->gap_extend,
                           jb->end_bonus, L->d_queue.as<int>(), &dst->qcount, L->d_over.as<int>(), &dst->ocount,
                           nullptr, nullptr);
-        HIPCHK(hipGetLastError());
+        LAUNCHCHK("redo band64", st);
         L->kt.end(st);
     }
     if (P.n_shared) {   // rescue_mate_part's has_shared_substring for the jobs that asked (aln.cpp:1058)
@@ -761,7 +782,7 @@ static int ext_enqueue(rsa_ctx* ctx, const rsa_job_batch* jb, rsa_aln_batch* out
         HIPCHK(hipMemcpyAsync(L->d_shl.p, L->h_shl.p, sizeof(uint32_t) * shl.size(), hipMemcpyHostToDevice, st));
         launch_shared_check((int)P.n_shared, st, L->d_jobs.as<ExtJobDev>(), L->d_shl.as<uint32_t>(), L->d_q.as<char>(),
                             ctx->d_ref, L->d_shres.as<uint8_t>());
-        HIPCHK(hipGetLastError());
+        LAUNCHCHK("shared check", st);
         HIPCHK(hipMemcpyAsync(L->h_shres.p, L->d_shres.p, P.n_shared, hipMemcpyDeviceToHost, st));
     }
     P.guess = std::min<uint64_t>(bound, DENSE_GUESS * n);
@@ -797,7 +818,7 @@ static int ext_panel(rsa_pending& P, ExtStatus& hs) {
                            L->d_cig.as<uint32_t>(), L->d_alns.as<rsa_aln>(), L->d_scratch.as<uint8_t>(), bstride,
                            BIG_DIR_CAP, P.match, P.mismatch, P.gap_open, P.gap_extend, P.end_bonus,
                            L->d_over.as<int>(), 2, L->d_redo.as<int>(), &P.d_status->rcount);
-        HIPCHK(hipGetLastError());
+        LAUNCHCHK("panel", st);
         L->kt.end(st);
     }
     HIPCHK(hipMemcpyAsync(L->h_over.p, L->d_over.p, sizeof(int) * n, hipMemcpyDeviceToHost, st));
@@ -848,20 +869,20 @@ static int ext_finish(rsa_pending& P) {
         launch_ext_scan(P.rmax, dim3((redo + 3) / 4), dim3(256), st, L->d_jobs.as<ExtJobDev>(), redo, d_redo,
                         L->d_q.as<char>(), ctx->d_ref, L->d_scan.as<ScanRes>(), P.match, P.mismatch, P.gap_open,
                         P.gap_extend);
-        HIPCHK(hipGetLastError());
+        LAUNCHCHK("host redo scan", st);
         HIPCHK(hipMemsetAsync(&P.d_status->qcount, 0, 2 * sizeof(int), st));    // qcount, ocount
         launch_ext_band16(P.band16_dircap, dim3((redo + 3) / 4), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(), redo, d_redo,
                           L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(),
                           L->d_alns.as<rsa_aln>(), P.match, P.mismatch, P.gap_open, P.gap_extend, P.end_bonus,
                           L->d_queue.as<int>(), &P.d_status->qcount, L->d_over.as<int>(), nullptr, nullptr,
                           ext_setprio());
-        HIPCHK(hipGetLastError());
+        LAUNCHCHK("host redo band16", st);
         launch_ext_band64(dim3(std::min(redo, band64_grid(ctx))), st, L->d_jobs.as<ExtJobDev>(), L->d_scan.as<ScanRes>(),
                           L->d_q.as<char>(), ctx->d_ref, L->d_cig.as<uint32_t>(), L->d_raw.as<uint32_t>(),
                           L->d_alns.as<rsa_aln>(), P.match, P.mismatch, P.gap_open, P.gap_extend, P.end_bonus,
                           L->d_queue.as<int>(), &P.d_status->qcount, L->d_over.as<int>(), &P.d_status->ocount,
                           nullptr, nullptr);
-        HIPCHK(hipGetLastError());
+        LAUNCHCHK("host redo band64", st);
         L->kt.end(st);
         if (int rc = ext_compact_copy(P)) return rc;
         HIPCHK(stream_wait(st, L->sb.done));

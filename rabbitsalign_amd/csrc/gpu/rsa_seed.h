@@ -125,7 +125,17 @@ void seed_bufs_release(SeedBufs& b);
 // that reads memory nothing wrote sees the same garbage in every run instead of
 // whatever a freed allocation left (fresh pages happen to be zero).  Results never
 // depend on it; an uninitialised read then fails every time, not now and then.
+// RSA_POISON=2 (tests): also refill every buffer of a lane at the start of each call, in the
+// call's stream, so a kernel that reads what an earlier call left behind fails too.
+inline bool rsa_poison_every() {
+    static const bool on = getenv("RSA_POISON") && getenv("RSA_POISON")[0] == '2';
+    return on;
+}
 inline hipError_t rsa_poison(void* p, size_t n) {
-    static const bool on = getenv("RSA_POISON") && getenv("RSA_POISON")[0] == '1';
-    return on ? hipMemset(p, 0xA5, n) : hipSuccess;
+    static const bool on = getenv("RSA_POISON") && (getenv("RSA_POISON")[0] == '1' || getenv("RSA_POISON")[0] == '2');
+    if (!on) return hipSuccess;
+    // hipMemset runs on the null stream, which the lanes' non-blocking streams do not wait
+    // for: finish it before the caller queues the buffer's first upload
+    const hipError_t e = hipMemset(p, 0xA5, n);
+    return e == hipSuccess ? hipDeviceSynchronize() : e;
 }

@@ -2885,6 +2885,9 @@ static const uint32_t MAP_BIG_LANES = BIG_LANES;
 int seed_run(SeedBufs& b, hipStream_t st, KTimer& kt, const SeedIndexParams& p, const rsa_read_batch* rb,
              int32_t rescue_level, uint32_t rescue_cutoff, rsa_nam_batch* out, std::string& err, SeedCounters& c) {
     const uint32_t n = rb->n_reads;
+    if (rsa_poison_every())                       // tests: nothing an earlier call wrote survives
+        for (int i = 0; i < SEED_NBUF; ++i)
+            if (b.p[i]) SCHK(hipMemsetAsync(b.p[i], 0xA5, b.cap[i], st));
     // reads longer than RW_MAXLEN (and parameters k_rs_wave cannot take) go one lane per read
     const bool wave_ok = p.k <= 32 && p.s <= 32 && p.s >= 1 && p.k - p.s + 1 <= RW_WMAX && p.k - p.s + 1 >= 1;
     uint32_t n_long = 0;
