@@ -529,6 +529,7 @@ rsa_index_build* rsa_index_build_run(int device, const char* ref_seq, const uint
     BCHK(hipEventRecord(ev[0], st));
     BCHK(hipMalloc(&B->d_ref, total + 64));
     if (total) BCHK(hipMemcpyAsync(B->d_ref, ref_seq, total, hipMemcpyHostToDevice, st));
+    BCHK(hipMemsetAsync(B->d_ref + total, 0, 64, st));        // the tail padding: zeros (rsa_open does the same)
     BCHK(hipEventRecord(ev[1], st));
 
     uint32_t *d_seg_c = nullptr, *d_count = nullptr;
@@ -663,6 +664,8 @@ rsa_index_build* rsa_index_build_run(int device, const char* ref_seq, const uint
     dfree(d_h1);
     dfree(d_tmp);
     BCHK(hipMalloc(&B->d_rs, sizeof(rsa_ref_randstrobe) * (n + 1)));
+    // the entry past the last: all ones (a hash above every key), as in rsa_open
+    BCHK(hipMemsetAsync(B->d_rs + n, 0xFF, sizeof(rsa_ref_randstrobe), st));
     if (n) {
         k_gather_entries<<<grid_of(n), TPB, 0, st>>>(d_raw, idx_final, n, B->d_rs);
         BCHK(hipGetLastError());

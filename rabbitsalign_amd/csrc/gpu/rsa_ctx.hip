@@ -338,9 +338,14 @@ rsa_ctx* rsa_open(int device, const rsa_index_view* v, char* errbuf, size_t err_
     const size_t n_starts = ((size_t)1 << v->bits) + 1;
     hipError_t e = hipMalloc(&ctx->d_ref, ctx->ref_bytes + 64);
     if (e == hipSuccess) e = hipMemcpy(ctx->d_ref, v->ref_seq, ctx->ref_bytes, hipMemcpyHostToDevice);
+    // the tail padding the kernels' wide loads may touch (masked) holds zeros, not whatever
+    // the allocation held: no context differs from another in any byte a kernel reads
+    if (e == hipSuccess) e = hipMemset(ctx->d_ref + ctx->ref_bytes, 0, 64);
     if (e == hipSuccess && v->randstrobes && ctx->n_rs) {
         e = hipMalloc(&ctx->d_rs, sizeof(rsa_ref_randstrobe) * (ctx->n_rs + 1));
         if (e == hipSuccess) e = hipMemcpy(ctx->d_rs, v->randstrobes, sizeof(rsa_ref_randstrobe) * ctx->n_rs, hipMemcpyHostToDevice);
+        // the entry past the last: all ones (a hash above every key), not whatever the allocation held
+        if (e == hipSuccess) e = hipMemset(ctx->d_rs + ctx->n_rs, 0xFF, sizeof(rsa_ref_randstrobe));
     }
     if (e == hipSuccess) e = hipMalloc(&ctx->d_coff, sizeof(uint64_t) * ctx->contig_off.size());
     if (e == hipSuccess)
@@ -349,6 +354,7 @@ rsa_ctx* rsa_open(int device, const rsa_index_view* v, char* errbuf, size_t err_
         e = hipMalloc(&ctx->d_starts, sizeof(uint64_t) * n_starts);
         if (e == hipSuccess) e = hipMemcpy(ctx->d_starts, v->bucket_starts, sizeof(uint64_t) * n_starts, hipMemcpyHostToDevice);
     }
+    if (e == hipSuccess) e = hipDeviceSynchronize();    // the fills above ran on the null stream
     if (e != hipSuccess) {
         std::string s = std::string("rsa_open upload: ") + hipGetErrorString(e);
         rsa_close(ctx);
